@@ -1,0 +1,107 @@
+"""ctypes binding of ``libcrispr_nw.so`` (C ABI declared in ``include/crispr_nw.h``).
+
+This is the in-process replacement of the ``needle`` subprocess boundary of
+CRISPResso (``CRISPResso/CRISPRessoCORE.py:1788-1806``).  The library is built
+in-tree by ``__graft_entry__.build()`` (``crispresso_amd/csrc/Makefile``).  There
+is deliberately no CPU fallback: if the library or a GPU is missing every entry
+point raises :class:`NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libcrispr_nw.so")
+
+NW_OK = 0
+NW_E_INVALID = -1
+NW_E_INEXACT = -2
+NW_E_UNSUPPORTED = -3
+NW_E_HIP = -4
+NW_E_NOMEM = -5
+NW_E_STATE = -6
+NW_TIE_EMBOSS = 0
+NW_FLAG_EMPTY = 1
+
+# Field order of nw_stat (include/crispr_nw.h).
+STAT_FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j", "flags")
+STAT_DTYPE = np.dtype([(f, "<i4") for f in STAT_FIELDS])
+
+# Every symbol include/crispr_nw.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "nw_create", "nw_destroy", "nw_last_error", "nw_set_params", "nw_score_scale",
+    "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload",
+    "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
+    "nw_batch_cells", "nw_batch_geometry", "nw_format_srspair",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP library is missing, failed to load, or a call failed."""
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load and type the shared library once; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as exc:  # pragma: no cover - depends on the ROCm install
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {exc}") from exc
+    ctx_p = c_void_p
+    sig = {
+        "nw_create": (c_int, [c_int, POINTER(c_void_p)]),
+        "nw_destroy": (None, [ctx_p]),
+        "nw_last_error": (c_char_p, [ctx_p]),
+        "nw_set_params": (c_int, [ctx_p, c_float, c_float, c_int, c_float, c_float, c_char_p, c_int]),
+        "nw_score_scale": (c_int, [ctx_p]),
+        "nw_set_reference": (c_int, [ctx_p, c_char_p, c_int32]),
+        "nw_required_stride": (c_int64, [ctx_p, c_int32]),
+        "nw_align_batch": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
+        "nw_batch_upload": (c_int, [ctx_p, c_void_p, c_void_p, c_int64]),
+        "nw_batch_run_async": (c_int, [ctx_p]),
+        "nw_batch_sync": (c_int, [ctx_p, POINTER(c_float)]),
+        "nw_batch_download": (c_int, [ctx_p, c_void_p, c_int64, c_void_p]),
+        "nw_batch_algo_bytes": (c_int64, [ctx_p]),
+        "nw_batch_cells": (c_int64, [ctx_p]),
+        "nw_batch_geometry": (c_int, [ctx_p] + [POINTER(c_int32)] * 5),
+        "nw_format_srspair": (
+            c_int64,
+            [c_void_p, c_int64, c_char_p, c_char_p, c_float, c_float, c_int32, c_int32, c_void_p, c_int64,
+             c_void_p, c_int64],
+        ),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> dict:
+    """Map of each declared symbol to whether the loaded library exports it."""
+    lib = load()
+    out = {}
+    for name in EXPORTS:
+        try:
+            getattr(lib, name)
+            out[name] = True
+        except AttributeError:
+            out[name] = False
+    return out
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None else 0

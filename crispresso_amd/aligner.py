@@ -1,0 +1,209 @@
+"""GPU aligner: the object that stands where one ``needle`` process stood.
+
+Each ``needle`` invocation in the reference (``CRISPRessoCORE.py:1797-1801``
+forward, ``1818-1822`` HDR, ``1913-1917`` RC, ``1926-1930`` RC-HDR) aligns a stream
+of reads against ONE amplicon with the options of ``--needle_options_string``.
+:class:`GpuAligner` is that, in-process: set the amplicon once, align batches.
+Results come back as an :class:`AlignmentBatch` whose fields are exactly what
+``parse_needle_output`` (``CRISPRessoCORE.py:1707-1786``) extracts from the
+srspair text, plus the text itself when a file is wanted.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .needle_options import NeedleOptions
+
+
+class NeedleError(RuntimeError):
+    """Raised where the reference raises NeedleException (CRISPRessoCORE.py:381)."""
+
+
+def pack_reads(reads: Sequence) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate reads (str or bytes) into one uint8 buffer + int64 offsets."""
+    enc = [r.encode("ascii") if isinstance(r, str) else bytes(r) for r in reads]
+    lens = np.fromiter((len(r) for r in enc), dtype=np.int64, count=len(enc))
+    offsets = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    buf = np.frombuffer(b"".join(enc), dtype=np.uint8) if enc else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(buf), offsets
+
+
+_ident_cache: dict = {}
+
+
+def printed_percent(num: int, den: int) -> float:
+    """Value parse_needle_output reads back: eval of the "%4.1f" identity token."""
+    key = (int(num), int(den))
+    v = _ident_cache.get(key)
+    if v is None:
+        v = float("%.1f" % (100.0 * num / den)) if den else 0.0
+        _ident_cache[key] = v
+    return v
+
+
+@dataclass
+class AlignmentBatch:
+    """Alignments of one batch against one amplicon (host copies)."""
+
+    stats: np.ndarray        # structured, _lib.STAT_DTYPE
+    aln: np.ndarray          # uint8 [n, 3, stride]: aligned amplicon, markup, aligned read
+    read_lens: np.ndarray    # int64 [n]
+    scale: int
+    awidth: int = 5000
+
+    def __len__(self) -> int:
+        return len(self.stats)
+
+    def _cols(self, i: int) -> int:
+        return int(min(self.stats["aln_len"][i], self.awidth))
+
+    def ref_seq(self, i: int) -> str:
+        return self.aln[i, 0, : self._cols(i)].tobytes().decode("ascii")
+
+    def align_str(self, i: int) -> str:
+        return self.aln[i, 1, : self._cols(i)].tobytes().decode("ascii")
+
+    def align_seq(self, i: int) -> str:
+        return self.aln[i, 2, : self._cols(i)].tobytes().decode("ascii")
+
+    def identity(self, i: int) -> float:
+        s = self.stats[i]
+        return printed_percent(s["n_ident"], s["aln_len"])
+
+    def score(self, i: int) -> float:
+        return float(self.stats["score"][i]) / self.scale
+
+    def read_end(self, i: int) -> str:
+        """``split()[3]`` of the read line: last read coordinate on the first line."""
+        seg = self.aln[i, 2, : self._cols(i)]
+        return str(int(np.count_nonzero(seg != ord("-"))))
+
+    def empty(self, i: int) -> bool:
+        return bool(self.stats["flags"][i] & _lib.NW_FLAG_EMPTY)
+
+
+class GpuAligner:
+    """One GPU context aligning reads to one amplicon at a time."""
+
+    def __init__(self, device: int = 0, options: Optional[NeedleOptions] = None):
+        self.lib = _lib.load()
+        self.options = options or NeedleOptions()
+        h = ctypes.c_void_p()
+        rc = self.lib.nw_create(int(device), ctypes.byref(h))
+        if rc != _lib.NW_OK:
+            raise _lib.NativeLibraryError(f"nw_create(device={device}) failed with code {rc} (no usable GPU?)")
+        self._h = h
+        self.device = device
+        o = self.options
+        self._check(
+            self.lib.nw_set_params(
+                self._h, o.gap_open, o.gap_extend, int(o.end_weight), o.end_open, o.end_extend,
+                o.matrix.encode(), _lib.NW_TIE_EMBOSS,
+            ),
+            "nw_set_params",
+        )
+        self.scale = int(self.lib.nw_score_scale(self._h))
+        self.reference: Optional[str] = None
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != _lib.NW_OK:
+            msg = self.lib.nw_last_error(self._h).decode(errors="replace")
+            raise NeedleError(f"{what}: {msg} (code {rc})")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.nw_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_reference(self, seq: str) -> None:
+        b = seq.encode("ascii")
+        self._check(self.lib.nw_set_reference(self._h, b, len(b)), "nw_set_reference")
+        self.reference = seq
+
+    # -- device-resident path (bench) ------------------------------------
+    def upload(self, buf: np.ndarray, offsets: np.ndarray) -> None:
+        self._buf, self._off = buf, offsets
+        self._check(self.lib.nw_batch_upload(self._h, _lib.ptr(buf), _lib.ptr(offsets), len(offsets) - 1),
+                    "nw_batch_upload")
+
+    def run_async(self) -> None:
+        self._check(self.lib.nw_batch_run_async(self._h), "nw_batch_run_async")
+
+    def sync(self) -> float:
+        ms = ctypes.c_float(0.0)
+        self._check(self.lib.nw_batch_sync(self._h, ctypes.byref(ms)), "nw_batch_sync")
+        return float(ms.value)
+
+    def algo_bytes(self) -> int:
+        return int(self.lib.nw_batch_algo_bytes(self._h))
+
+    def cells(self) -> int:
+        return int(self.lib.nw_batch_cells(self._h))
+
+    def geometry(self) -> dict:
+        vals = [ctypes.c_int32() for _ in range(5)]
+        self._check(self.lib.nw_batch_geometry(self._h, *[ctypes.byref(v) for v in vals]), "nw_batch_geometry")
+        return dict(zip(("rows_per_lane", "waves_per_block", "grid", "lds_bytes", "tb_in_lds"),
+                        (v.value for v in vals)))
+
+    def download(self, n: int, max_len: int) -> AlignmentBatch:
+        stride = int(self.lib.nw_required_stride(self._h, max(int(max_len), 1)))
+        stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+        aln = np.zeros((n, 3, stride), dtype=np.uint8)
+        self._check(self.lib.nw_batch_download(self._h, _lib.ptr(aln), stride, _lib.ptr(stats)),
+                    "nw_batch_download")
+        lens = np.diff(self._off)
+        return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
+
+    # -- synchronous path ----------------------------------------------------
+    def align_packed(self, buf: np.ndarray, offsets: np.ndarray) -> AlignmentBatch:
+        if self.reference is None:
+            raise NeedleError("no amplicon set")
+        n = len(offsets) - 1
+        lens = np.diff(offsets)
+        max_len = int(lens.max()) if n else 1
+        stride = int(self.lib.nw_required_stride(self._h, max(max_len, 1)))
+        stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+        aln = np.zeros((n, 3, stride), dtype=np.uint8)
+        self._check(
+            self.lib.nw_align_batch(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(aln), stride,
+                                    _lib.ptr(stats)),
+            "nw_align_batch",
+        )
+        return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
+
+    def align(self, reads: Sequence) -> AlignmentBatch:
+        buf, offsets = pack_reads(reads)
+        return self.align_packed(buf, offsets)
+
+
+def format_srspair(batch: AlignmentBatch, aname: str, bnames: Sequence[str], options: NeedleOptions) -> str:
+    """srspair blocks of a batch (needle's default -aformat), via the C++ writer."""
+    lib = _lib.load()
+    names = b"".join(n.encode() + b"\0" for n in bnames)
+    stride = batch.aln.shape[2]
+    args = (aname.encode(), names, options.gap_open, options.gap_extend, batch.scale, options.awidth,
+            _lib.ptr(batch.aln), stride, _lib.ptr(batch.stats), len(batch))
+    need = lib.nw_format_srspair(None, 0, *args)
+    buf = ctypes.create_string_buffer(int(need) + 1)
+    got = lib.nw_format_srspair(buf, int(need) + 1, *args)
+    assert got == need
+    return buf.raw[:need].decode("ascii")

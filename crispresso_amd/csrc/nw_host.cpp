@@ -1,0 +1,395 @@
+// nw_host.cpp -- C ABI (include/crispr_nw.h) over the gfx950 alignment kernel.
+//
+// Owns one HIP stream and the device buffers of one GPU.  Everything the
+// reference did by spawning `needle` (CRISPRessoCORE.py:1788-1936) happens here
+// in-process: the amplicon becomes a substitution profile in HBM, reads are
+// copied once, one kernel aligns the whole batch, results come back as the
+// three alignment strings plus per-read statistics.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/crispr_nw.h"
+#include "nw_device.h"
+
+namespace {
+
+// EDNAFULL (NCBI NUC.4.4), order A T G C S W R Y K M B V H D N U.
+const signed char kEdna[16][16] = {
+    {5, -4, -4, -4, -4, 1, 1, -4, -4, 1, -4, -1, -1, -1, -2, -4},
+    {-4, 5, -4, -4, -4, 1, -4, 1, 1, -4, -1, -4, -1, -1, -2, 5},
+    {-4, -4, 5, -4, 1, -4, 1, -4, 1, -4, -1, -1, -4, -1, -2, -4},
+    {-4, -4, -4, 5, 1, -4, -4, 1, -4, 1, -1, -1, -1, -4, -2, -4},
+    {-4, -4, 1, 1, -1, -4, -2, -2, -2, -2, -1, -1, -3, -3, -1, -4},
+    {1, 1, -4, -4, -4, -1, -2, -2, -2, -2, -3, -3, -1, -1, -1, 1},
+    {1, -4, 1, -4, -2, -2, -1, -4, -2, -2, -3, -1, -3, -1, -1, -4},
+    {-4, 1, -4, 1, -2, -2, -4, -1, -2, -2, -1, -3, -1, -3, -1, 1},
+    {-4, 1, 1, -4, -2, -2, -2, -2, -1, -4, -1, -3, -3, -1, -1, 1},
+    {1, -4, -4, 1, -2, -2, -2, -2, -4, -1, -3, -1, -1, -3, -1, -4},
+    {-4, -1, -1, -1, -1, -3, -3, -1, -1, -3, -1, -2, -2, -2, -1, -1},
+    {-1, -4, -1, -1, -1, -3, -1, -3, -3, -1, -2, -1, -2, -2, -1, -4},
+    {-1, -1, -4, -1, -3, -1, -3, -1, -3, -1, -2, -2, -1, -2, -1, -1},
+    {-1, -1, -1, -4, -3, -1, -1, -3, -1, -3, -2, -2, -2, -1, -1, -1},
+    {-2, -2, -2, -2, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -2},
+    {-4, 5, -4, -4, -4, 1, -4, 1, 1, -4, -1, -4, -1, -1, -2, 5},
+};
+const char kAlphabet[] = "ATGCSWRYKMBVHDNU";
+
+uint8_t code_of(unsigned char c) {
+    const char* p = std::strchr(kAlphabet, std::toupper(c));
+    return (c && p) ? (uint8_t)(p - kAlphabet) : (uint8_t)nw::NCODE_PAD;
+}
+
+constexpr int kMaxRef = 1024;
+constexpr int kMaxLds = 160 * 1024;
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;  // elements
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct nw_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // params
+    float gap_open_f = 10.0f, gap_extend_f = 0.5f;
+    int scale = 2, gap_open = 20, gap_extend = 1;
+    // reference
+    std::string ref;
+    int R = 0;
+    DevBuf<int8_t> d_prof;
+    DevBuf<uint8_t> d_lut, d_amp;
+    // batch
+    int64_t n = 0;
+    int32_t lb_max = 0;
+    int64_t stride = 0;
+    int64_t cells = 0;
+    std::vector<int32_t> read_lens;
+    DevBuf<uint8_t> d_reads;
+    DevBuf<int64_t> d_offsets;
+    DevBuf<uint8_t> d_out;
+    DevBuf<nw::Stat> d_stats;
+    DevBuf<uint8_t> d_tb;
+    nw::LaunchCfg cfg{};
+    bool ran = false;
+};
+
+namespace {
+
+int fail(nw_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIP_OR_FAIL(ctx, expr)                                                        \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? NW_E_NOMEM : NW_E_HIP,       \
+                        "%s failed: %s", #expr, hipGetErrorString(e_));               \
+    } while (0)
+
+int build_profile(nw_ctx* c) {
+    const int La = (int)c->ref.size();
+    const int R = nw::rows_per_lane_for(La);
+    if (R < 0) return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", La, kMaxRef);
+    const int RP = nw::profile_rp(R);
+    std::vector<int8_t> prof((size_t)nw::NCODE * 64 * RP, 0);
+    for (int ai = 0; ai < La; ++ai) {
+        const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+        for (int code = 0; code < nw::NCODE; ++code) {
+            int s = (ca < 16 && code < 16) ? kEdna[ca][code] * c->scale : 0;
+            prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
+        }
+    }
+    uint8_t lut[256];
+    for (int q = 0; q < 256; ++q) lut[q] = code_of((unsigned char)q);
+    HIP_OR_FAIL(c, c->d_prof.reserve(prof.size()));
+    HIP_OR_FAIL(c, c->d_lut.reserve(256));
+    HIP_OR_FAIL(c, c->d_amp.reserve((size_t)La + 16));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof.p, prof.data(), prof.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut.p, lut, 256, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_amp.p, c->ref.data(), La, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->R = R;
+    return NW_OK;
+}
+
+int64_t stride_for(int La, int32_t lb_max) { return ((int64_t)La + lb_max + 15) & ~(int64_t)15; }
+
+int configure(nw_ctx* c) {
+    const int La = (int)c->ref.size();
+    const int R = c->R;
+    nw::LaunchCfg cfg{};
+    cfg.R = R;
+    cfg.tb_in_lds = false;
+    cfg.wpb = 4;
+    for (int wpb : {4, 2, 1}) {
+        int b = nw::lds_bytes_for(R, La, c->lb_max, true, wpb);
+        if (b > 0 && b <= kMaxLds) {
+            cfg.tb_in_lds = true;
+            cfg.wpb = wpb;
+            cfg.lds_bytes = b;
+            break;
+        }
+    }
+    if (!cfg.tb_in_lds) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, false, cfg.wpb);
+    if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
+        return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel", c->lb_max);
+    const int per_cu = std::max(1, std::min(8, kMaxLds / cfg.lds_bytes));
+    const int64_t want = (c->n + cfg.wpb - 1) / cfg.wpb;
+    cfg.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
+    if (!cfg.tb_in_lds) {
+        const int64_t per_wave = nw::tb_bytes_per_wave(R, c->lb_max);
+        HIP_OR_FAIL(c, c->d_tb.reserve((size_t)per_wave * cfg.grid * cfg.wpb));
+    }
+    c->cfg = cfg;
+    return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_create(int device, nw_ctx** out) {
+    if (!out) return NW_E_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NW_E_HIP;
+    if (device < 0 || device >= count) return NW_E_INVALID;
+    nw_ctx* c = new nw_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return NW_E_HIP;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cus = prop.multiProcessorCount;
+    *out = c;
+    return NW_OK;
+}
+
+void nw_destroy(nw_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->d_prof.release(); c->d_lut.release(); c->d_amp.release();
+    c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
+    c->d_stats.release(); c->d_tb.release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* nw_last_error(const nw_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int nw_set_params(nw_ctx* c, float gap_open, float gap_extend, int end_weight, float end_open,
+                  float end_extend, const char* matrix, int tie_policy) {
+    (void)end_open; (void)end_extend;
+    if (!c) return NW_E_INVALID;
+    if (matrix && *matrix) {
+        std::string m(matrix);
+        for (auto& ch : m) ch = (char)std::toupper((unsigned char)ch);
+        if (m != "EDNAFULL") return fail(c, NW_E_UNSUPPORTED, "matrix %s not supported (EDNAFULL only)", matrix);
+    }
+    if (end_weight) return fail(c, NW_E_UNSUPPORTED, "-endweight is not supported (needle default is off)");
+    if (tie_policy != NW_TIE_EMBOSS) return fail(c, NW_E_UNSUPPORTED, "tie policy %d not supported", tie_policy);
+    if (!(gap_open >= 0.0f) || !(gap_extend >= 0.0f) || gap_open > 1000.0f || gap_extend > 1000.0f)
+        return fail(c, NW_E_INVALID, "gap penalties out of range: %g %g", gap_open, gap_extend);
+    int scale = 0;
+    for (int s = 1; s <= 16; s *= 2) {
+        double o = (double)gap_open * s, e = (double)gap_extend * s;
+        if (o == std::floor(o) && e == std::floor(e)) { scale = s; break; }
+    }
+    if (!scale) return fail(c, NW_E_INEXACT, "gap penalties %g/%g are not multiples of 1/16", gap_open, gap_extend);
+    c->gap_open_f = gap_open;
+    c->gap_extend_f = gap_extend;
+    c->scale = scale;
+    c->gap_open = (int)std::lround((double)gap_open * scale);
+    c->gap_extend = (int)std::lround((double)gap_extend * scale);
+    if (!c->ref.empty()) {
+        (void)hipSetDevice(c->device);
+        return build_profile(c);
+    }
+    return NW_OK;
+}
+
+int nw_score_scale(const nw_ctx* c) { return c ? c->scale : 0; }
+
+int nw_set_reference(nw_ctx* c, const char* ref, int32_t ref_len) {
+    if (!c || !ref || ref_len <= 0) return fail(c, NW_E_INVALID, "empty amplicon");
+    if (ref_len > kMaxRef) return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", ref_len, kMaxRef);
+    (void)hipSetDevice(c->device);
+    c->ref.assign(ref, ref + ref_len);
+    c->ran = false;
+    return build_profile(c);
+}
+
+int64_t nw_required_stride(const nw_ctx* c, int32_t max_read_len) {
+    if (!c || c->ref.empty()) return 0;
+    return stride_for((int)c->ref.size(), std::max(max_read_len, 1));
+}
+
+int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
+    if (n < 0 || (n > 0 && (!offsets || !reads))) return fail(c, NW_E_INVALID, "bad batch");
+    (void)hipSetDevice(c->device);
+    const int La = (int)c->ref.size();
+    int32_t lb_max = 1;
+    int64_t cells = 0;
+    c->read_lens.resize((size_t)n);
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t len = offsets[r + 1] - offsets[r];
+        if (len < 0 || len > (1 << 20)) return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
+        c->read_lens[(size_t)r] = (int32_t)len;
+        lb_max = std::max<int32_t>(lb_max, (int32_t)len);
+        cells += (int64_t)La * len;
+    }
+    const int64_t base = n ? offsets[0] : 0;
+    const int64_t nbytes = n ? offsets[n] - base : 0;
+    std::vector<int64_t> rel((size_t)n + 1);
+    for (int64_t r = 0; r <= n; ++r) rel[(size_t)r] = n ? offsets[r] - base : 0;
+    c->n = n;
+    c->lb_max = lb_max;
+    c->cells = cells;
+    c->stride = stride_for(La, lb_max);
+    HIP_OR_FAIL(c, c->d_reads.reserve((size_t)nbytes + 64));
+    HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
+    HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
+    HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
+    if (nbytes) HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, reads + base, (size_t)nbytes, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, rel.data(), sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    int rc = configure(c);
+    if (rc) return rc;
+    c->ran = false;
+    return NW_OK;
+}
+
+int nw_batch_run_async(nw_ctx* c) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty() || !c->d_offsets.p) return fail(c, NW_E_STATE, "no batch uploaded");
+    (void)hipSetDevice(c->device);
+    nw::KernelArgs a{};
+    a.reads = c->d_reads.p;
+    a.offsets = c->d_offsets.p;
+    a.n = c->n;
+    a.prof = c->d_prof.p;
+    a.lut = c->d_lut.p;
+    a.amp = c->d_amp.p;
+    a.La = (int32_t)c->ref.size();
+    a.gap_open = c->gap_open;
+    a.gap_extend = c->gap_extend;
+    a.Lb_max = c->lb_max;
+    a.out = c->d_out.p;
+    a.stride = c->stride;
+    a.stats = c->d_stats.p;
+    a.tb_global = c->d_tb.p;
+    a.tb_wave_bytes = c->cfg.tb_in_lds ? 0 : nw::tb_bytes_per_wave(c->R, c->lb_max);
+    HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
+    if (c->n > 0) HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+    HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
+    c->ran = true;
+    return NW_OK;
+}
+
+int nw_batch_sync(nw_ctx* c, float* kernel_ms) {
+    if (!c) return NW_E_INVALID;
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    if (kernel_ms) {
+        *kernel_ms = 0.0f;
+        if (c->ran) HIP_OR_FAIL(c, hipEventElapsedTime(kernel_ms, c->ev0, c->ev1));
+    }
+    return NW_OK;
+}
+
+int nw_batch_download(nw_ctx* c, char* aln_out, int64_t stride, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (!c->ran) return fail(c, NW_E_STATE, "nothing has run");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    if (c->n == 0) return NW_OK;
+    if (stats)
+        HIP_OR_FAIL(c, hipMemcpy(stats, c->d_stats.p, sizeof(nw::Stat) * (size_t)c->n, hipMemcpyDeviceToHost));
+    if (aln_out) {
+        if (stride < c->stride) return fail(c, NW_E_INVALID, "stride %lld < required %lld", (long long)stride, (long long)c->stride);
+        if (stride == c->stride) {
+            HIP_OR_FAIL(c, hipMemcpy(aln_out, c->d_out.p, (size_t)c->n * 3 * c->stride, hipMemcpyDeviceToHost));
+        } else {
+            HIP_OR_FAIL(c, hipMemcpy2D(aln_out, (size_t)stride, c->d_out.p, (size_t)c->stride, (size_t)c->stride,
+                                       (size_t)c->n * 3, hipMemcpyDeviceToHost));
+        }
+    }
+    return NW_OK;
+}
+
+int64_t nw_batch_algo_bytes(nw_ctx* c) {
+    if (!c || !c->ran) return -1;
+    std::vector<nw::Stat> st((size_t)c->n);
+    if (c->n && nw_batch_download(c, nullptr, 0, (nw_stat*)st.data()) != NW_OK) return -1;
+    int64_t total = 0;
+    for (int64_t r = 0; r < c->n; ++r)
+        if (!(st[(size_t)r].flags & NW_FLAG_EMPTY)) total += c->read_lens[(size_t)r] + 3ll * st[(size_t)r].aln_len + 16;
+    return total;
+}
+
+int64_t nw_batch_cells(const nw_ctx* c) { return c ? c->cells : -1; }
+
+int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
+                      int32_t* lds_bytes, int32_t* tb_in_lds) {
+    if (!c) return NW_E_INVALID;
+    if (rows_per_lane) *rows_per_lane = c->cfg.R;
+    if (waves_per_block) *waves_per_block = c->cfg.wpb;
+    if (grid) *grid = c->cfg.grid;
+    if (lds_bytes) *lds_bytes = c->cfg.lds_bytes;
+    if (tb_in_lds) *tb_in_lds = c->cfg.tb_in_lds ? 1 : 0;
+    return NW_OK;
+}
+
+int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, char* aln_out,
+                   int64_t stride, nw_stat* stats) {
+    int rc = nw_batch_upload(c, reads, offsets, n);
+    if (rc) return rc;
+    if ((rc = nw_batch_run_async(c))) return rc;
+    if ((rc = nw_batch_sync(c, nullptr))) return rc;
+    return nw_batch_download(c, aln_out, stride, stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,473 @@
+// nw_kernel.hip -- batched EMBOSS-needle-compatible global alignment for gfx950.
+//
+// Replaces the per-read DP inside the `needle` process that CRISPResso spawns
+// (CRISPResso/CRISPRessoCORE.py:1791-1806 forward, 1812-1828 HDR, 1910-1936 RC).
+// Semantics are the ones DESIGN.md "EMBOSS semantics" states (affine Gotoh,
+// EDNAFULL, free end gaps, EMBOSS tie rules); the CPU restatement in oracle/ is
+// the parity checker.
+//
+// Mapping (one alignment per 64-lane wavefront):
+//   * rows = amplicon (a), columns = read (b).  Lane l owns rows [l*R, l*R+R).
+//   * the wave walks columns; at step t lane l works on column t-l (a skewed
+//     anti-diagonal wavefront).  The bottom row of lane l (Mo, Y, H) moves to
+//     lane l+1 with one DPP wave_shr:1 per value per step -- no LDS round trip.
+//   * substitution scores come from a per-amplicon profile in LDS laid out
+//     [code][lane][RP] int8, so one ds_read_b32/b64 yields a lane's R scores.
+//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend) kept
+//     in LDS (or a global slab when LDS is too small), walked afterwards by the
+//     whole wave in runs: 64 lanes test 64 cells of the current diagonal/row/
+//     column at once and a ballot finds where the run ends.
+//   * the three alignment strings are written straight to HBM.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nw_device.h"
+
+namespace nw {
+
+constexpr int NEG = -(1 << 28);
+
+template <int R> struct Geo {
+    static constexpr int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);      // profile bytes per lane
+    static constexpr int ES = R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8));  // tb bytes per (column, lane)
+    static constexpr int NW = (R + 7) / 8;                         // 32-bit bit-accumulators
+};
+
+__device__ __forceinline__ int shr1(int v, int fill) {
+    // DPP wave_shr:1 -- lane l receives lane l-1's value, lane 0 keeps `fill`.
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ unsigned push_sign(unsigned acc, int d) {
+    // (acc << 1) | (d < 0)
+    return __builtin_amdgcn_alignbit(acc, (unsigned)d, 31);
+}
+
+__device__ __forceinline__ void lds_fence() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Orders this wave's traceback stores before other lanes' loads of them.
+template <bool TB_LDS>
+__device__ __forceinline__ void tb_fence() {
+    if constexpr (TB_LDS) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ unsigned char upcase(unsigned char c) {
+    return (c >= 'a' && c <= 'z') ? (unsigned char)(c - 32) : c;
+}
+
+// Per-wave LDS layout (offsets in bytes from the wave's base), all 16-aligned.
+struct WaveLds {
+    int raw, coff, lastrow, runs, red, bits, total;
+};
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+template <int R>
+__host__ __device__ inline WaveLds wave_lds_layout(int La, int Lb_max, bool tb_in_lds) {
+    WaveLds w;
+    int o = 0;
+    w.raw = o;     o += align16(Lb_max + 4);
+    w.coff = o;    o += align16(2 * (Lb_max + 4));
+    w.lastrow = o; o += align16(4 * (Lb_max + 1));
+    w.runs = o;    o += align16(4 * (La + Lb_max + 8));
+    w.red = o;     o += 64;
+    w.bits = o;
+    if (tb_in_lds) o += align16(Lb_max * 64 * Geo<R>::ES);
+    w.total = align16(o);
+    return w;
+}
+
+__host__ __device__ inline int shared_lds_bytes(int R, int La) {
+    int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);
+    return align16(NCODE * 64 * RP) + 256 + align16(La + 4);
+}
+
+template <int R>
+__device__ __forceinline__ unsigned load_nibble(const unsigned char* bits, int ai, int bj) {
+    constexpr int ES = Geo<R>::ES;
+    const int lane = ai / R, k = ai - lane * R;
+    const unsigned char* p = bits + ((size_t)bj * 64 + lane) * ES;
+    unsigned w;
+    int nr, kk;
+    if constexpr (ES == 1) { w = *p; nr = R; kk = k; }
+    else if constexpr (ES == 2) { w = *(const unsigned short*)p; nr = R; kk = k; }
+    else if constexpr (ES == 4) { w = *(const unsigned*)p; nr = R; kk = k; }
+    else {
+        const int wi = k >> 3;
+        w = ((const unsigned*)p)[wi];
+        nr = (R - 8 * wi) < 8 ? (R - 8 * wi) : 8;
+        kk = k & 7;
+    }
+    return (w >> (4 * (nr - 1 - kk))) & 0xFu;
+}
+
+template <int R>
+__device__ __forceinline__ void store_bits(unsigned char* bits, int bj, int lane, const unsigned (&acc)[Geo<R>::NW]) {
+    constexpr int ES = Geo<R>::ES;
+    unsigned char* p = bits + ((size_t)bj * 64 + lane) * ES;
+    if constexpr (ES == 1) *p = (unsigned char)acc[0];
+    else if constexpr (ES == 2) *(unsigned short*)p = (unsigned short)acc[0];
+    else if constexpr (ES == 4) *(unsigned*)p = acc[0];
+    else { ((unsigned*)p)[0] = acc[0]; ((unsigned*)p)[1] = acc[1]; }
+}
+
+template <int R>
+__device__ __forceinline__ void load_prof(const unsigned char* prof_lds, int off, int (&sc)[Geo<R>::RP / 4]) {
+    constexpr int RP = Geo<R>::RP;
+    if constexpr (RP == 4) {
+        sc[0] = *(const int*)(prof_lds + off);
+    } else if constexpr (RP == 8) {
+        int2 v = *(const int2*)(prof_lds + off);
+        sc[0] = v.x; sc[1] = v.y;
+    } else {
+        int4 v = *(const int4*)(prof_lds + off);
+        sc[0] = v.x; sc[1] = v.y; sc[2] = v.z; sc[3] = v.w;
+    }
+}
+
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        long long u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Run codes stored in LDS: type << 28 | length.
+enum { RUN_M = 0, RUN_X = 1, RUN_Y = 2 };
+
+template <int R, bool TB_LDS>
+__global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
+    constexpr int RP = Geo<R>::RP;
+    constexpr int NWD = Geo<R>::NW;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int La = args.La;
+    const int O = args.gap_open, E = args.gap_extend;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wpb = blockDim.x >> 6;
+
+    // ---- shared per-block state: profile, ascii->code LUT, amplicon bytes ----
+    unsigned char* prof_lds = smem;
+    const int prof_bytes = NCODE * 64 * RP;
+    unsigned char* lut_lds = smem + align16(prof_bytes);
+    unsigned char* amp_lds = lut_lds + 256;
+    for (int q = tid; q < prof_bytes / 16; q += blockDim.x)
+        ((int4*)prof_lds)[q] = ((const int4*)args.prof)[q];
+    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
+    for (int q = tid; q < La; q += blockDim.x) amp_lds[q] = args.amp[q];
+    __syncthreads();
+
+    const WaveLds L = wave_lds_layout<R>(La, args.Lb_max, TB_LDS);
+    unsigned char* wbase = smem + shared_lds_bytes(R, La) + wave * L.total;
+    unsigned char* raw = wbase + L.raw;
+    unsigned short* coff = (unsigned short*)(wbase + L.coff);
+    int* lastrow = (int*)(wbase + L.lastrow);
+    unsigned* runs = (unsigned*)(wbase + L.runs);
+    const long long gw = (long long)blockIdx.x * wpb + wave;
+    const long long nwaves = (long long)gridDim.x * wpb;
+    unsigned char* bits;
+    if constexpr (TB_LDS) bits = wbase + L.bits;
+    else bits = args.tb_global + gw * args.tb_wave_bytes;
+
+    const int nl = (La + R - 1) / R;        // lanes holding real rows
+    const int ai0 = lane * R;
+    const int lr = (La - 1) / R;            // lane holding the last row
+    const int klast = (La - 1) - lr * R;
+    const int prof_lane = lane * RP;
+    const int pad_coff = NCODE_PAD * 64 * RP;   // offset of the all-zero pad code
+
+    for (long long rd = gw; rd < args.n; rd += nwaves) {
+        const long long off = args.offsets[rd];
+        const int Lb = (int)(args.offsets[rd + 1] - off);
+        Stat* st = args.stats + rd;
+        if (Lb <= 0) {
+            if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; *st = z; }
+            continue;
+        }
+        // ---- stage the read: raw bytes + profile offsets of each column ----
+        const unsigned char* rp = args.reads + off;
+        for (int q = lane; q < Lb + 4; q += 64) {
+            unsigned char c = q < Lb ? rp[q] : (unsigned char)'N';
+            raw[q] = c;
+            coff[q] = (unsigned short)(q < Lb ? lut_lds[c] * 64 * RP : pad_coff);
+        }
+        lds_fence();
+
+        // ---- DP fill ----
+        int Mol[R], Xl[R], Hold[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) { Mol[k] = -O; Xl[k] = NEG; Hold[k] = 0; }
+        int sMo = -O, sY = NEG, sH = 0;    // what this lane's bottom row sends down
+        int Htop = 0;                       // H[row above][column-1]
+        const int nsteps = Lb + nl - 1;
+        // prefetch pipeline: coff for bj+1 loaded one step ahead, scores for bj loaded one step ahead
+        int bj0 = -lane;
+        int c_next = coff[min(max(bj0 + 1, 0), Lb + 3)];
+        int sc[RP / 4];
+        load_prof<R>(prof_lds, coff[min(max(bj0, 0), Lb + 3)] + prof_lane, sc);
+        for (int t = 0; t < nsteps; ++t) {
+            const int bj = t - lane;
+            const int rMo = shr1(sMo, -O);
+            const int rY = shr1(sY, NEG);
+            const int rH = shr1(sH, 0);
+            // issue next loads before the compute that hides their latency
+            int sc_n[RP / 4];
+            load_prof<R>(prof_lds, c_next + prof_lane, sc_n);
+            const int c_nn = coff[min(max(bj + 2, 0), Lb + 3)];
+            if (bj >= 0 && bj < Lb && lane < nl) {
+                unsigned acc[NWD];
+#pragma unroll
+                for (int w = 0; w < NWD; ++w) acc[w] = 0;
+                int Hd = Htop, Mou = rMo, Yu = rY;
+                int mlast = 0;
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const int s = __builtin_amdgcn_sbfe(sc[k >> 2], 8 * (k & 3), 8);
+                    const int M = Hd + s;
+                    const int Xe = Xl[k] - E;
+                    const int X = max(Mol[k], Xe);
+                    const int Ye = Yu - E;
+                    const int Y = max(Mou, Ye);
+                    const int mxy = max(X, Y);
+                    const int H = max(M, mxy);
+                    unsigned a = acc[k >> 3];
+                    a = push_sign(a, Mou - Ye);       // Y extend
+                    a = push_sign(a, Mol[k] - Xe);    // X extend
+                    a = push_sign(a, Y - X);          // X > Y
+                    a = push_sign(a, mxy - M);        // M > max(X, Y)
+                    acc[k >> 3] = a;
+                    mlast = (k == klast) ? M : mlast;
+                    Hd = Hold[k];
+                    Hold[k] = H;
+                    Mol[k] = M - O;
+                    Xl[k] = X;
+                    Mou = M - O;
+                    Yu = Y;
+                }
+                sMo = Mou; sY = Yu; sH = Hold[R - 1];
+                store_bits<R>(bits, bj, lane, acc);
+                if (lane == lr) lastrow[bj] = mlast;
+            }
+            Htop = rH;
+#pragma unroll
+            for (int w = 0; w < RP / 4; ++w) sc[w] = sc_n[w];
+            c_next = c_nn;
+        }
+        // Mol[k] + O is M of the last column for this lane's rows.
+        // ---- start cell: corner, then last column bottom->top, then last row right->left ----
+        long long key = -0x7fffffffffffffffll - 1;
+        if (lane < nl) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int ai = ai0 + k;
+                if (ai < La) {
+                    const long long prio = (ai == La - 1) ? (3ll << 24) : ((2ll << 24) | ai);
+                    const long long kk = ((long long)(Mol[k] + O) << 32) | prio;
+                    key = kk > key ? kk : key;
+                }
+            }
+        }
+        tb_fence<TB_LDS>();
+        for (int q = lane; q < Lb - 1; q += 64) {
+            const long long kk = ((long long)lastrow[q] << 32) | ((1ll << 24) | q);
+            key = kk > key ? kk : key;
+        }
+        key = wave_max_i64(key);
+        const int score = (int)(key >> 32);
+        const int prio = (int)(key & 0xffffffff);
+        int ei, ej;   // 1-based start cell
+        if ((prio >> 24) == 3) { ei = La; ej = Lb; }
+        else if ((prio >> 24) == 2) { ei = (prio & 0xffffff) + 1; ej = Lb; }
+        else { ei = La; ej = (prio & 0xffffff) + 1; }
+
+        // ---- traceback in runs ----
+        int nruns = 0, last_type = -1;
+        auto push = [&](int type, int n) {
+            if (n <= 0) return;
+            if (type == last_type) {
+                if (lane == 0) runs[nruns - 1] += (unsigned)n;
+            } else {
+                if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
+                ++nruns;
+                last_type = type;
+            }
+        };
+        if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
+        else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
+        int i = ei, j = ej, state = RUN_M;
+        while (i > 0 && j > 0) {
+            if (state == RUN_M) {
+                const int ci = i - 1 - lane, cj = j - 1 - lane;
+                const bool valid = ci >= 1 && cj >= 1;
+                unsigned nib = valid ? load_nibble<R>(bits, ci - 1, cj - 1) : 0u;
+                const int best = (nib & 1u) ? RUN_M : ((nib & 2u) ? RUN_X : RUN_Y);
+                const unsigned long long m = __ballot(!valid || best != RUN_M);
+                if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
+                const int k0 = __builtin_ctzll(m);
+                const int nb = __shfl(best, k0, 64);
+                push(RUN_M, k0 + 1);
+                i -= k0 + 1; j -= k0 + 1;
+                state = nb;
+            } else if (state == RUN_X) {
+                const int cj = j - lane;
+                const bool valid = cj >= 1;
+                unsigned nib = valid ? load_nibble<R>(bits, i - 1, cj - 1) : 0u;
+                const unsigned long long m = __ballot(!valid || !(nib & 4u));
+                if (m == 0) { push(RUN_X, 64); j -= 64; continue; }
+                const int k0 = __builtin_ctzll(m);
+                push(RUN_X, k0 + 1);
+                j -= k0 + 1;
+                state = RUN_M;
+            } else {
+                const int ci = i - lane;
+                const bool valid = ci >= 1;
+                unsigned nib = valid ? load_nibble<R>(bits, ci - 1, j - 1) : 0u;
+                const unsigned long long m = __ballot(!valid || !(nib & 8u));
+                if (m == 0) { push(RUN_Y, 64); i -= 64; continue; }
+                const int k0 = __builtin_ctzll(m);
+                push(RUN_Y, k0 + 1);
+                i -= k0 + 1;
+                state = RUN_M;
+            }
+        }
+        if (i > 0) push(RUN_Y, i);
+        if (j > 0) push(RUN_X, j);
+        lds_fence();
+
+        // ---- emit strings, forward order ----
+        unsigned char* o_ref = args.out + rd * 3 * args.stride;
+        unsigned char* o_mk = o_ref + args.stride;
+        unsigned char* o_rd = o_mk + args.stride;
+        int col = 0, ia = 0, jb = 0;
+        int n_id = 0, n_sim = 0, n_gap = 0;
+        for (int q = nruns - 1; q >= 0; --q) {
+            const unsigned rc = runs[q];
+            const int type = (int)(rc >> 28);
+            const int n = (int)(rc & 0x0fffffffu);
+            for (int p = lane; p < n; p += 64) {
+                unsigned char ca = '-', cb = '-', mk = ' ';
+                if (type != RUN_X) ca = amp_lds[ia + p];
+                if (type != RUN_Y) cb = raw[jb + p];
+                // a '-' already in the input (RC-pass reads, CRISPRessoCORE.py:1846) prints
+                // like a gap, so it counts as one, as for an alignment gap
+                const bool gapcol = ca == '-' || cb == '-';
+                n_gap += gapcol;
+                if (type == RUN_M && !gapcol) {
+                    const int ai = ia + p;
+                    const bool id = upcase(ca) == upcase(cb);
+                    const int code = lut_lds[cb];
+                    const signed char s = (signed char)prof_lds[code * 64 * RP + (ai / R) * RP + (ai % R)];
+                    const bool sim = id || s > 0;
+                    mk = id ? '|' : (sim ? ':' : '.');
+                    n_id += id;
+                    n_sim += sim;
+                }
+                o_ref[col + p] = ca;
+                o_mk[col + p] = mk;
+                o_rd[col + p] = cb;
+            }
+            col += n;
+            if (type != RUN_X) ia += n;
+            if (type != RUN_Y) jb += n;
+        }
+        n_id = wave_sum(n_id);
+        n_sim = wave_sum(n_sim);
+        n_gap = wave_sum(n_gap);
+        if (lane == 0) {
+            Stat s;
+            s.aln_len = col;
+            s.n_ident = n_id;
+            s.n_sim = n_sim;
+            s.n_gaps = n_gap;
+            s.score = score;
+            s.end_i = ei;
+            s.end_j = ej;
+            s.flags = 0;
+            *st = s;
+        }
+        lds_fence();
+    }
+}
+
+}  // namespace nw
+
+// ---------------------------------------------------------------- launcher
+
+namespace nw {
+
+template <int R>
+static hipError_t launch_r(const KernelArgs& a, const LaunchCfg& c, hipStream_t s) {
+    if (c.tb_in_lds)
+        hipLaunchKernelGGL((nw_align_kernel<R, true>), dim3(c.grid), dim3(64 * c.wpb), c.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL((nw_align_kernel<R, false>), dim3(c.grid), dim3(64 * c.wpb), c.lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+int lds_bytes_for(int R, int La, int Lb_max, bool tb_in_lds, int wpb) {
+    int per = 0;
+    switch (R) {
+#define NW_CASE(r) case r: per = wave_lds_layout<r>(La, Lb_max, tb_in_lds).total; break;
+        NW_CASE(1) NW_CASE(2) NW_CASE(3) NW_CASE(4) NW_CASE(5) NW_CASE(6) NW_CASE(7) NW_CASE(8)
+        NW_CASE(10) NW_CASE(12) NW_CASE(14) NW_CASE(16)
+#undef NW_CASE
+        default: return -1;
+    }
+    return shared_lds_bytes(R, La) + wpb * per;
+}
+
+int rows_per_lane_for(int La) {
+    int r = (La + 63) / 64;
+    if (r <= 8) return r;
+    if (r <= 10) return 10;
+    if (r <= 12) return 12;
+    if (r <= 14) return 14;
+    if (r <= 16) return 16;
+    return -1;
+}
+
+int tb_bytes_per_wave(int R, int Lb_max) {
+    int es = R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8));
+    return align16(Lb_max * 64 * es);
+}
+
+int profile_rp(int R) { return R <= 4 ? 4 : (R <= 8 ? 8 : 16); }
+
+hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s) {
+    switch (c.R) {
+        case 1: return launch_r<1>(a, c, s);
+        case 2: return launch_r<2>(a, c, s);
+        case 3: return launch_r<3>(a, c, s);
+        case 4: return launch_r<4>(a, c, s);
+        case 5: return launch_r<5>(a, c, s);
+        case 6: return launch_r<6>(a, c, s);
+        case 7: return launch_r<7>(a, c, s);
+        case 8: return launch_r<8>(a, c, s);
+        case 10: return launch_r<10>(a, c, s);
+        case 12: return launch_r<12>(a, c, s);
+        case 14: return launch_r<14>(a, c, s);
+        case 16: return launch_r<16>(a, c, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace nw

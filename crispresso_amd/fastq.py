@@ -1,0 +1,107 @@
+"""FASTQ(.gz) -> the FASTA stream ``needle`` would have read.
+
+Restates the shell stage of the reference pipeline
+(``CRISPRessoCORE.py:1791-1797``, HDR re-stream ``1812-1818``)::
+
+    cat F | gunzip | awk 'NR % 4 == 1 {print ">" $0} NR % 4 == 2 {print $0}' | sed 's/:/_/g'
+
+and what EMBOSS's FASTA reader then keeps: the sequence name is the first
+whitespace-delimited word of the header (here ``@`` + read id with every ``:``
+turned into ``_``), and the sequence keeps letters and the characters
+``*.~?#+-``.  Reads come back packed (one uint8 buffer + int64 offsets) so they
+can go to the GPU without a per-read Python object on the hot path.
+"""
+from __future__ import annotations
+
+import gzip
+import io
+import re
+from typing import List, Tuple
+
+import numpy as np
+
+_KEEP = np.zeros(256, dtype=bool)
+for _c in range(256):
+    ch = chr(_c)
+    _KEEP[_c] = ch.isascii() and (ch.isalpha() or ch in "*.~?#+-")
+
+
+def _open(path: str):
+    with open(path, "rb") as f:
+        magic = f.read(2)
+    if magic == b"\x1f\x8b":
+        return gzip.open(path, "rb")
+    return open(path, "rb")
+
+
+def fasta_name(header_line: bytes) -> str:
+    """Name EMBOSS gives the record awk/sed made of a FASTQ header line."""
+    h = header_line.rstrip(b"\r\n").replace(b":", b"_")
+    tok = h.split()
+    return tok[0].decode("ascii", "replace") if tok else ""
+
+
+def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
+    """-> (fasta names, packed sequences, offsets) in file order."""
+    with _open(path) as f:
+        data = f.read()
+    return fastq_bytes_as_fasta(data)
+
+
+def fastq_bytes_as_fasta(data: bytes) -> Tuple[List[str], np.ndarray, np.ndarray]:
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    headers = lines[0::4]
+    seqs = lines[1::4][: len(headers)]
+    if len(seqs) < len(headers):  # awk prints a header even without a sequence line
+        seqs += [b""] * (len(headers) - len(seqs))
+    names = [fasta_name(h) for h in headers]
+    return (names,) + pack_filtered(seqs)
+
+
+def pack_filtered(seqs: List[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate, dropping bytes EMBOSS's reader would drop (sed ':' -> '_' first)."""
+    joined = b"".join(s.replace(b":", b"_") for s in seqs)
+    raw = np.frombuffer(joined, dtype=np.uint8)
+    lens = np.fromiter((len(s) for s in seqs), dtype=np.int64, count=len(seqs))
+    keep = _KEEP[raw]
+    if keep.all():
+        buf = raw.copy()
+        kept_lens = lens
+    else:
+        seg = np.repeat(np.arange(len(seqs)), lens)
+        kept_lens = np.bincount(seg[keep], minlength=len(seqs)).astype(np.int64)
+        buf = raw[keep].copy()
+    offsets = np.zeros(len(seqs) + 1, dtype=np.int64)
+    np.cumsum(kept_lens, out=offsets[1:])
+    return buf, offsets
+
+
+def parse_fasta_text(text: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
+    """FASTA text (e.g. not_aligned_amplicon_forward.fa) after ``sed 's/:/_/g'``."""
+    names: List[str] = []
+    seqs: List[bytes] = []
+    cur: List[bytes] = []
+    for line in io.BytesIO(text.encode()):
+        line = line.rstrip(b"\r\n")
+        if line.startswith(b">"):
+            if names:
+                seqs.append(b"".join(cur))
+            names.append(fasta_name(line[1:]))
+            cur = []
+        elif names:
+            cur.append(line)
+    if names:
+        seqs.append(b"".join(cur))
+    return (names,) + pack_filtered(seqs)
+
+
+_ws = re.compile(r"\s+")
+
+
+def count_reads(path: str) -> int:
+    """``zcat | wc -l`` / 4, as get_n_reads_fastq (CRISPRessoCORE.py:331-346)."""
+    with _open(path) as f:
+        n = sum(1 for _ in f)
+    return n // 4

@@ -1,0 +1,279 @@
+"""The alignment step of ``run_crispresso``, with the GPU aligner in place of ``needle``.
+
+Mirrors, name for name, what ``CRISPResso/CRISPRessoCORE.py`` does around its
+``needle`` calls so that code written against the reference reads the same:
+
+* :func:`reverse_complement`, :func:`find_wrong_nt` -- ``CORE:129-159``
+* :class:`NeedleException` -- ``CORE:381``; raised with the reference's messages
+* :func:`parse_needle_output` -- restatement of the closure at ``CORE:1707-1786``
+  (reads srspair text back into the DataFrame the quantification consumes)
+* :func:`needle_pass` -- one ``needle`` invocation (``CORE:1791-1806``): FASTQ or
+  FASTA in, DataFrame out, optional ``needle_output_*.txt.gz`` file
+* :func:`align_reads` -- the whole block ``CORE:1788-2000``: forward pass, HDR
+  pass, join, ``min_identity_score`` filter, reverse-complement retry, RC
+  transform and ``_RC`` suffix, concatenation.
+
+Reference quirks reproduced on purpose:
+  1. retry inputs are ``align_seq.replace("_", "")``, so ``-`` gaps stay in them
+     (``CORE:1846``, ``1867``);
+  2. with an HDR amplicon the retry set tests ``score_ref`` twice (``CORE:1844-1845``);
+  3. identities exactly equal to ``min_identity_score`` are neither kept nor
+     retried (strict ``<`` / ``>``, ``CORE:1844-1851``, ``1866-1871``);
+  4. the RC-HDR pass passes the literal text ``args.needle_options_string`` to
+     needle (``CORE:1928``), which makes that needle call fail: by default we
+     raise the same ``NeedleException`` (``rc_hdr_quirk="raise"``);
+     ``rc_hdr_quirk="align"`` runs the pass the author evidently meant.
+  5. read ids lose real underscores (``sed 's/:/_/g'`` then ``_`` -> ``:``,
+     ``CORE:1797``, ``1725``).
+"""
+from __future__ import annotations
+
+import gzip
+import os
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import fastq
+from .aligner import AlignmentBatch, GpuAligner, NeedleError, format_srspair, printed_percent
+from .needle_options import DEFAULT_NEEDLE_OPTIONS, NeedleOptions, UnsupportedNeedleOption
+
+
+class NeedleException(Exception):
+    """CRISPRessoCORE.py:381 -- mapped to exit code 6 by the reference CLI."""
+
+
+_NT_COMPLEMENT = {"A": "T", "C": "G", "G": "C", "T": "A", "N": "N", "_": "_", "-": "-"}
+
+
+def reverse_complement(sequence: str) -> str:
+    """CRISPRessoCORE.py:129-144 (KeyError on characters outside ACGTN_-, as there)."""
+    return "".join([_NT_COMPLEMENT[c] for c in sequence.upper()[-1::-1]])
+
+
+def find_wrong_nt(sequence: str) -> List[str]:
+    """CRISPRessoCORE.py:147-159."""
+    return list(set(sequence.upper()).difference(set(["A", "T", "C", "G", "N"])))
+
+
+# ----------------------------------------------------------------- parsing
+
+def parse_needle_output(needle_filename: str, name: str = "seq", just_score: bool = False) -> pd.DataFrame:
+    """Restatement of the reference parser (CRISPRessoCORE.py:1707-1786).
+
+    Reads srspair text (gzip or plain) line by line exactly as the reference
+    does: find ``# Aligned_sequences``, skip 1, id = last token of the next line
+    with ``_`` -> ``:``, skip 5, identity = last token of the next line stripped
+    of ``%()``, then (unless ``just_score``) skip 7 and take ``split()[2]`` of
+    the first alignment line, ``[21:]`` of the markup line, ``split()[2]`` and
+    ``split()[3]`` of the read line.
+    """
+    needle_data = []
+    try:
+        opener = gzip.open if _is_gzip(needle_filename) else open
+        with opener(needle_filename, mode="rb") as fh:
+            rd = lambda: fh.readline().decode("UTF-8")  # noqa: E731
+            line = rd()
+            while line:
+                while line and ("# Aligned_sequences" not in line):
+                    line = rd()
+                if line:
+                    rd()
+                    line = rd()
+                    id_seq = line.split()[-1].replace("_", ":")
+                    for _ in range(5):
+                        rd()
+                    line = rd()
+                    identity_seq = float(line.strip().split(" ")[-1].replace("%", "").replace(")", "").replace("(", ""))
+                    if just_score:
+                        needle_data.append([id_seq, identity_seq])
+                    else:
+                        for _ in range(7):
+                            rd()
+                        line = rd()
+                        aln_ref_seq = line.split()[2]
+                        aln_str = rd()[21:].rstrip("\n")
+                        line = rd()
+                        aln_query_seq = line.split()[2]
+                        aln_query_len = line.split()[3]
+                        needle_data.append([id_seq, identity_seq, aln_query_len, aln_ref_seq, aln_str, aln_query_seq])
+                    line = rd()
+    except Exception as exc:
+        raise NeedleException("Failed to parse the output of needle!") from exc
+    if just_score:
+        return pd.DataFrame(needle_data, columns=["ID", "score_" + name]).set_index("ID")
+    return pd.DataFrame(
+        needle_data, columns=["ID", "score_" + name, "length", "ref_seq", "align_str", "align_seq"]
+    ).set_index("ID")
+
+
+def _is_gzip(path: str) -> bool:
+    with open(path, "rb") as f:
+        return f.read(2) == b"\x1f\x8b"
+
+
+def batch_to_dataframe(batch: AlignmentBatch, names: Sequence[str], name: str = "seq",
+                       just_score: bool = False) -> pd.DataFrame:
+    """The DataFrame parse_needle_output would build from this batch's srspair text.
+
+    Fast path (no text, no gzip): identical columns, dtypes and values.  Reads
+    needle skips (empty sequences) are absent, as they are from needle's output.
+    """
+    keep = [i for i in range(len(batch)) if not batch.empty(i)]
+    ids = [names[i].split()[-1].replace("_", ":") if names[i].split() else "" for i in keep]
+    st = batch.stats
+    ident = [printed_percent(st["n_ident"][i], st["aln_len"][i]) for i in keep]
+    if just_score:
+        return pd.DataFrame({"ID": ids, "score_" + name: ident}).set_index("ID")
+    data = {
+        "ID": ids,
+        "score_" + name: ident,
+        "length": [batch.read_end(i) for i in keep],
+        "ref_seq": [batch.ref_seq(i) for i in keep],
+        "align_str": [batch.align_str(i) for i in keep],
+        "align_seq": [batch.align_seq(i) for i in keep],
+    }
+    return pd.DataFrame(data, columns=["ID", "score_" + name, "length", "ref_seq", "align_str", "align_seq"]
+                        ).set_index("ID")
+
+
+# ----------------------------------------------------------------- passes
+
+SRSPAIR_HEADER = (
+    "########################################\n# Program: needle\n# Rundate: (crispresso_amd)\n"
+    "# Commandline: needle\n#    -asequence {a}\n#    -bsequence /dev/stdin\n#    -outfile /dev/stdout\n"
+    "# Align_format: srspair\n# Report_file: /dev/stdout\n########################################\n\n"
+)
+SRSPAIR_TRAILER = "#---------------------------------------\n#---------------------------------------\n"
+
+
+@dataclass
+class PassResult:
+    names: List[str]
+    batch: AlignmentBatch
+
+    def dataframe(self, name: str = "ref", just_score: bool = False) -> pd.DataFrame:
+        return batch_to_dataframe(self.batch, self.names, name, just_score)
+
+
+def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: np.ndarray,
+                offsets: np.ndarray, amplicon_id: str = "AMPL", outfile: Optional[str] = None) -> PassResult:
+    """One ``needle -asequence=AMPL -bsequence=/dev/stdin`` run (CRISPRessoCORE.py:1797-1806).
+
+    ``outfile`` (``needle_output_*.txt.gz``) is written only when given, as the
+    reference keeps it only with --keep_intermediate/--dump (CRISPRessoCORE.py:3694-3697).
+    """
+    try:
+        if aligner.reference != amplicon:
+            aligner.set_reference(amplicon)
+        batch = aligner.align_packed(buf, offsets)
+    except (NeedleError, UnsupportedNeedleOption) as exc:
+        raise NeedleException("Needle failed to run, please check the log file.") from exc
+    res = PassResult(list(names), batch)
+    if outfile:
+        text = format_srspair(batch, amplicon_id, res.names, aligner.options)
+        with gzip.open(outfile, "wt") as fh:
+            fh.write(SRSPAIR_HEADER.format(a=amplicon_id))
+            fh.write(text)
+            fh.write(SRSPAIR_TRAILER)
+    return res
+
+
+@dataclass
+class AlignArgs:
+    """The fields of run_crispresso's argparse namespace the alignment step reads."""
+
+    amplicon_seq: str
+    expected_hdr_amplicon_seq: str = ""
+    min_identity_score: float = 60.0
+    needle_options_string: str = DEFAULT_NEEDLE_OPTIONS
+    keep_intermediate: bool = False
+    dump: bool = False
+
+
+def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Optional[GpuAligner] = None,
+                output_dir: Optional[str] = None, database_id: str = "AMPL",
+                rc_hdr_quirk: str = "raise") -> pd.DataFrame:
+    """CRISPRessoCORE.py:1788-2000 on the GPU: returns ``df_needle_alignment``.
+
+    The result has the reference's columns (``score_ref, length, ref_seq,
+    align_str, align_seq`` and, with an HDR amplicon, ``score_repaired,
+    score_diff``) and index (read ids, ``_RC`` suffix for reverse-complement hits).
+    """
+    opts = NeedleOptions.parse(args.needle_options_string)
+    own = aligner is None
+    if own:
+        aligner = GpuAligner(0, opts)
+    keep_files = bool(output_dir) and (args.keep_intermediate or args.dump)
+    _jp = (lambda f: os.path.join(output_dir, f)) if output_dir else (lambda f: f)
+    try:
+        names, buf, offsets = fastq.read_fastq_as_fasta(processed_output_filename)
+        fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
+                          _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None)
+        if args.expected_hdr_amplicon_seq:
+            rep = needle_pass(aligner, args.expected_hdr_amplicon_seq, names, buf, offsets, database_id,
+                              _jp(f"needle_output_repair_{database_id}.txt.gz") if keep_files else None)
+            df_database = fwd.dataframe("ref")
+            df_database_repair = rep.dataframe("repaired", just_score=True)
+            df_database_and_repair = df_database.join(df_database_repair)
+            sr_not_aligned = df_database_and_repair.loc[
+                (df_database_and_repair.score_ref < args.min_identity_score)
+                & (df_database_and_repair.score_ref < args.min_identity_score)
+            ].align_seq.apply(lambda x: x.replace("_", ""))
+            df_database_and_repair = df_database_and_repair.loc[
+                (df_database_and_repair.score_ref > args.min_identity_score)
+                | (df_database_and_repair.score_repaired > args.min_identity_score)
+            ].copy()
+            df_database_and_repair["score_diff"] = (
+                df_database_and_repair.score_ref - df_database_and_repair.score_repaired
+            )
+            df_needle_alignment = df_database_and_repair
+        else:
+            df_needle_alignment = fwd.dataframe("ref")
+            sr_not_aligned = df_needle_alignment.loc[
+                (df_needle_alignment.score_ref < args.min_identity_score)
+            ].align_seq.apply(lambda x: x.replace("_", ""))
+            df_needle_alignment = df_needle_alignment.loc[df_needle_alignment.score_ref > args.min_identity_score]
+
+        if sr_not_aligned.count():
+            fasta_text = "".join(f">{x0}\n{x1}\n" for x0, x1 in sr_not_aligned.items())
+            if keep_files:
+                with gzip.open(_jp("not_aligned_amplicon_forward.fa.gz"), "wt") as fh:
+                    fh.write(fasta_text)
+            rc_names, rc_buf, rc_off = fastq.parse_fasta_text(fasta_text)
+            rc_amp = reverse_complement(args.amplicon_seq)
+            rc = needle_pass(aligner, rc_amp, rc_names, rc_buf, rc_off, database_id,
+                             _jp(f"needle_output_rc_{database_id}.txt.gz") if keep_files else None)
+            if args.expected_hdr_amplicon_seq:
+                if rc_hdr_quirk == "raise":
+                    # CRISPRessoCORE.py:1924-1936 hands needle the literal text
+                    # "args.needle_options_string"; needle fails and the reference raises.
+                    raise NeedleException("Needle failed to run, please check the log file.")
+                rc_rep = needle_pass(aligner, reverse_complement(args.expected_hdr_amplicon_seq), rc_names,
+                                     rc_buf, rc_off, database_id,
+                                     _jp(f"needle_output_repair_rc_{database_id}.txt.gz") if keep_files else None)
+                df_database_and_repair_rc = rc.dataframe("ref").join(rc_rep.dataframe("repaired", just_score=True))
+                df_database_and_repair_rc = df_database_and_repair_rc.loc[
+                    (df_database_and_repair_rc.score_ref > args.min_identity_score)
+                    | (df_database_and_repair_rc.score_repaired > args.min_identity_score)
+                ].copy()
+                df_database_and_repair_rc["score_diff"] = (
+                    df_database_and_repair_rc.score_ref - df_database_and_repair_rc.score_repaired
+                )
+                df_needle_alignment_rc = df_database_and_repair_rc
+            else:
+                df_needle_alignment_rc = rc.dataframe("ref")
+                df_needle_alignment_rc = df_needle_alignment_rc.loc[
+                    df_needle_alignment_rc.score_ref > args.min_identity_score
+                ].copy()
+            df_needle_alignment_rc["ref_seq"] = df_needle_alignment_rc["ref_seq"].apply(reverse_complement)
+            df_needle_alignment_rc["align_seq"] = df_needle_alignment_rc["align_seq"].apply(reverse_complement)
+            df_needle_alignment_rc["align_str"] = df_needle_alignment_rc["align_str"].apply(lambda x: x[::-1])
+            df_needle_alignment_rc.index = map(lambda x: "_".join([x, "RC"]), df_needle_alignment_rc.index)
+            df_needle_alignment = pd.concat([df_needle_alignment, df_needle_alignment_rc])
+        return df_needle_alignment
+    finally:
+        if own:
+            aligner.close()

@@ -1,0 +1,122 @@
+/*
+ * crispr_nw.h -- C ABI of the MI355X batched global aligner (libcrispr_nw.so).
+ *
+ * Drop-in for the EMBOSS `needle` process boundary of CRISPResso's single-amplicon
+ * pipeline.  Today's contract is a shell pipeline
+ *     cat R.fastq.gz | gunzip | awk | sed 's/:/_/g' |
+ *         needle -asequence=AMPL.fa -bsequence=/dev/stdin -outfile=/dev/stdout
+ *                <needle_options_string> | gzip > needle_output_*.txt.gz
+ * (CRISPResso/CRISPRessoCORE.py:1788-1806 forward pass, 1808-1828 HDR pass,
+ *  1910-1936 reverse-complement passes), parsed back by parse_needle_output
+ * (CRISPRessoCORE.py:1707-1786).  The reference has no FFI of its own; the
+ * entry points below are what a ctypes binding of that boundary needs
+ * (SURVEY.md 8b).  Plain C types only; no torch types.
+ *
+ * Threading: one nw_ctx per GPU; a context is NOT thread-safe.  Calls are
+ * synchronous unless named *_async.  Every function returns NW_OK (0) or a
+ * negative NW_E_* code; nw_last_error() holds the message.  Errors map to the
+ * reference's NeedleException ("Needle failed to run", CRISPRessoCORE.py:381,
+ * 1805-1806) in the Python host.
+ */
+#ifndef CRISPR_NW_H
+#define CRISPR_NW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NW_OK 0
+#define NW_E_INVALID (-1)      /* bad argument (null pointer, empty amplicon, ...) */
+#define NW_E_INEXACT (-2)      /* penalties not exactly representable in integer units */
+#define NW_E_UNSUPPORTED (-3)  /* option the GPU path does not implement (matrix, endweight, size) */
+#define NW_E_HIP (-4)          /* HIP runtime error or no device */
+#define NW_E_NOMEM (-5)        /* device or host allocation failed */
+#define NW_E_STATE (-6)        /* call out of order (e.g. run before upload) */
+
+/* Traceback tie policy.  NW_TIE_EMBOSS: EMBOSS needle's strict rules
+ * (M wins only when strictly greater than X and Y, X beats Y only when strictly
+ * greater, gap open wins ties with extend; start cell = corner, then last column
+ * bottom->top, then last row right->left).  DESIGN.md "EMBOSS semantics". */
+#define NW_TIE_EMBOSS 0
+
+/* nw_stat.flags */
+#define NW_FLAG_EMPTY 1        /* zero-length read: no alignment (needle skips it) */
+
+typedef struct nw_ctx nw_ctx;
+
+/* One record per read, written by the GPU. */
+typedef struct {
+    int32_t aln_len;   /* alignment columns incl. end gaps  == srspair "# Length:" */
+    int32_t n_ident;   /* == "# Identity:" numerator   */
+    int32_t n_sim;     /* == "# Similarity:" numerator */
+    int32_t n_gaps;    /* == "# Gaps:" numerator       */
+    int32_t score;     /* "# Score:" x nw_score_scale() */
+    int32_t end_i;     /* 1-based amplicon row where the traceback started */
+    int32_t end_j;     /* 1-based read column where the traceback started  */
+    int32_t flags;     /* NW_FLAG_* */
+} nw_stat;
+
+/* Context lifetime.  device = HIP ordinal.  Replaces launching one `needle`
+ * process per pass (CRISPRessoCORE.py:1804, 1824, 1919, 1932). */
+int nw_create(int device, nw_ctx** out);
+void nw_destroy(nw_ctx* ctx);
+const char* nw_last_error(const nw_ctx* ctx);
+
+/* needle qualifiers (CRISPRessoCORE.py:4226-4231 default
+ * "-gapopen=10 -gapextend=0.5 -awidth3=5000").  matrix must be "EDNAFULL";
+ * end_weight must be 0 (needle's default, which CRISPResso never changes).
+ * Returns NW_E_INEXACT when gap_open/gap_extend are not multiples of 1/16. */
+int nw_set_params(nw_ctx* ctx, float gap_open, float gap_extend, int end_weight,
+                  float end_open, float end_extend, const char* matrix, int tie_policy);
+/* Integer multiplier applied to every score (2 for the defaults). */
+int nw_score_scale(const nw_ctx* ctx);
+
+/* The amplicon (needle -asequence; CRISPRessoCORE.py:1695-1696 / 1704-1705 /
+ * 1885-1907).  Uploads the substitution profile.  1 <= ref_len <= 1024. */
+int nw_set_reference(nw_ctx* ctx, const char* ref, int32_t ref_len);
+
+/* Bytes per string slot a caller must provide for reads up to max_read_len. */
+int64_t nw_required_stride(const nw_ctx* ctx, int32_t max_read_len);
+
+/* Align n reads (needle -bsequence stream) against the current reference.
+ * reads: concatenated bytes; offsets: n+1 byte offsets (read r is
+ * reads[offsets[r] .. offsets[r+1])).  Outputs (caller-owned, host memory):
+ * aln_out: n * 3 * stride bytes; for read r, at r*3*stride: the aligned
+ * amplicon, then (+stride) the markup line, then (+2*stride) the aligned read,
+ * each stats[r].aln_len bytes long, not NUL-terminated.  Synchronous. */
+int nw_align_batch(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n,
+                   char* aln_out, int64_t stride, nw_stat* stats);
+
+/* Same three steps split for device-resident benchmarking: upload keeps the
+ * batch in HBM, run launches the kernel on the context stream (async), sync
+ * waits and returns the kernel time of the last run measured with HIP events
+ * on that stream, download copies results to the host. */
+int nw_batch_upload(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n);
+int nw_batch_run_async(nw_ctx* ctx);
+int nw_batch_sync(nw_ctx* ctx, float* kernel_ms);
+int nw_batch_download(nw_ctx* ctx, char* aln_out, int64_t stride, nw_stat* stats);
+/* Sum over the uploaded batch of (read_len + 3*aln_len + 16): the algorithmic
+ * bytes of the last run.  Valid after nw_batch_download or
+ * nw_batch_algo_bytes computes it on device-side stats copied back. */
+int64_t nw_batch_algo_bytes(nw_ctx* ctx);
+/* Cells (sum of ref_len * read_len) of the uploaded batch. */
+int64_t nw_batch_cells(const nw_ctx* ctx);
+/* Launch geometry of the last run: rows per lane, waves per block, grid, LDS. */
+int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
+                      int32_t* grid, int32_t* lds_bytes, int32_t* tb_in_lds);
+
+/* srspair text of n alignments (the blocks parse_needle_output consumes,
+ * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated
+ * read ids, concatenated.  Writes at most cap bytes; returns the number of
+ * bytes the full text needs (call again with a bigger buffer if > cap).
+ * awidth = needle -awidth3 (alignment columns per line). */
+int64_t nw_format_srspair(char* buf, int64_t cap, const char* aname, const char* bnames,
+                          float gap_open, float gap_extend, int32_t scale, int32_t awidth,
+                          const char* aln, int64_t stride, const nw_stat* stats, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,112 @@
+"""GPU parity: the HIP kernel (through the C ABI) vs the CPU oracle, bit for bit.
+
+Compared per read: the three alignment strings (aligned amplicon, markup,
+aligned read), alignment length, identity/similarity/gap counts, score and the
+traceback start cell.  Integer/byte work, so the bar is exact equality.
+"""
+import numpy as np
+import pytest
+
+from crispresso_amd import synth
+from crispresso_amd.aligner import pack_reads
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j")
+
+
+def assert_same(oracle, amplicon, buf, offsets, batch, label=""):
+    res, aln = oracle.align_batch(amplicon, buf, offsets, nthreads=8)
+    n = len(offsets) - 1
+    assert len(batch) == n
+    lens = np.diff(offsets)
+    bad = []
+    for f in FIELDS:
+        g = batch.stats[f].astype(np.int64)
+        o = res[f].astype(np.int64)
+        mism = np.flatnonzero((g != o) & (lens > 0))
+        if mism.size:
+            bad.append((f, mism[:5].tolist(), g[mism[:5]].tolist(), o[mism[:5]].tolist()))
+    assert not bad, f"{label} stat mismatches: {bad}"
+    for i in range(n):
+        if lens[i] == 0:
+            assert batch.empty(i)
+            continue
+        L = int(res["aln_len"][i])
+        for k in range(3):
+            g = batch.aln[i, k, :L].tobytes()
+            o = aln[i, k, :L].tobytes()
+            assert g == o, f"{label} read {i} string {k}:\n gpu {g!r}\n cpu {o!r}"
+
+
+def test_hand_cases(gpu_aligner_factory, oracle):
+    amp = "ACGTACGTTTGACCA"
+    reads = ["ACGTACGTGACCA", "ACGTACGTTTGACCAGG", "TTGACC", "A", "ACGTACGTTTGACCA", "", "acgtNNNNtttgacca",
+             "GGGGGGGGGGGGGGGGGGGGGGGGGGGGGG", "T-C-A", "ACGTRYKMSWBDHVNU"]
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    buf, off = pack_reads(reads)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "hand")
+
+
+def test_c2_mix(gpu_aligner_factory, oracle):
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 3000, 2)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "c2")
+
+
+def test_parity_mix(gpu_aligner_factory, oracle):
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 3000, 3, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "parity")
+
+
+@pytest.mark.parametrize("La", [1, 2, 7, 63, 64, 65, 128, 129, 192, 250, 257, 320, 384, 448, 512, 513, 640, 768,
+                                 896, 1024])
+def test_amplicon_lengths(gpu_aligner_factory, oracle, La):
+    amp = synth.random_amplicon(La, 100 + La)
+    rng = np.random.Generator(np.random.PCG64(La))
+    reads = []
+    for L in [1, 2, 5, max(1, La - 3), La, La + 7, 60, 130, 300]:
+        if rng.random() < 0.5 and L <= La:
+            s = rng.integers(0, La - L + 1)
+            reads.append(amp[s:s + L])
+        else:
+            reads.append(synth.random_amplicon(L, int(rng.integers(1 << 30))))
+    sub, soff = synth.reads_from(amp, 40, La + 7)
+    reads += synth.unpack(sub, soff)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"La={La}")
+
+
+def test_global_traceback_slab(gpu_aligner_factory, oracle):
+    """Reads long enough that the traceback bits leave LDS for a global slab."""
+    amp = synth.random_amplicon(250, 1)
+    rng = np.random.Generator(np.random.PCG64(9))
+    reads = [synth.random_amplicon(1400, 11), amp[:100] + synth.random_amplicon(1250, 12) + amp[100:]]
+    reads += [amp] * 3 + [amp[5:200]]
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_in_lds"] == 0
+    assert_same(oracle, amp, buf, off, batch, "global-tb")
+
+
+def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle):
+    amp = synth.random_amplicon(180, 21)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    for seed in (1, 2, 3):
+        buf, off = synth.reads_from(amp, 500 + 100 * seed, seed)
+        assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"rep{seed}")
+    amp2 = synth.random_amplicon(300, 22)
+    a.set_reference(amp2)
+    buf, off = synth.reads_from(amp2, 700, 5)
+    assert_same(oracle, amp2, buf, off, a.align_packed(buf, off), "switch-ref")

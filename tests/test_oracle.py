@@ -1,0 +1,196 @@
+"""Pins for the CPU oracle (oracle/nw_oracle.c) -- CPU only.
+
+EMBOSS itself is not available, so the oracle is pinned by:
+  * exhaustive enumeration on tiny inputs: the DP optimum equals the best score
+    over every column sequence of the free-end-gap model;
+  * self-consistency: the traceback's strings re-score to the reported score and
+    reproduce both input sequences; stats match the strings;
+  * known answers for the EMBOSS tie rules (DESIGN.md "EMBOSS semantics");
+  * the srspair text round-trips through the parse_needle_output restatement.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+from crispresso_amd import synth
+
+EDNA = "ATGCSWRYKMBVHDNU"
+
+
+def sub(oracle, x, y):
+    return oracle.load().oracle_sub(oracle.load().oracle_code(ord(x)), oracle.load().oracle_code(ord(y)))
+
+
+def model_score(oracle, ra, rb, O=20, E=1, S=2):
+    """Score of an alignment under the model: one leading and one trailing
+    single-type gap run are free, every other gap run costs O + (k-1)E."""
+    cols = []
+    for x, y in zip(ra, rb):
+        cols.append("P" if (x != "-" and y != "-") else ("A" if y == "-" else "B"))
+    lo, hi = 0, len(cols)
+    if cols and cols[0] != "P":
+        t = cols[0]
+        while lo < hi and cols[lo] == t:
+            lo += 1
+    if hi > lo and cols[hi - 1] != "P":
+        t = cols[hi - 1]
+        while hi > lo and cols[hi - 1] == t:
+            hi -= 1
+    s, q = 0, lo
+    while q < hi:
+        if cols[q] == "P":
+            s += S * sub(oracle, ra[q], rb[q])
+            q += 1
+        else:
+            t, k = cols[q], 0
+            while q < hi and cols[q] == t:
+                k += 1
+                q += 1
+            s -= O + (k - 1) * E
+    return s
+
+
+def all_alignments(a, b):
+    if not a and not b:
+        yield "", ""
+        return
+    if a and b:
+        for x, y in all_alignments(a[1:], b[1:]):
+            yield a[0] + x, b[0] + y
+    if a:
+        for x, y in all_alignments(a[1:], b):
+            yield a[0] + x, "-" + y
+    if b:
+        for x, y in all_alignments(a, b[1:]):
+            yield "-" + x, b[0] + y
+
+
+def brute_best(oracle, a, b):
+    best = None
+    for ra, rb in all_alignments(a, b):
+        # the DP's end cell is an aligned pair in the last row/column, so the
+        # core (between the free end runs) must end with a pair
+        cols = ["P" if (x != "-" and y != "-") else "G" for x, y in zip(ra, rb)]
+        if "P" not in cols:
+            continue
+        s = model_score(oracle, ra, rb)
+        best = s if best is None or s > best else best
+    return best
+
+
+def test_brute_force_optimum(oracle):
+    rng = np.random.Generator(np.random.PCG64(7))
+    for _ in range(300):
+        la, lb = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        alpha = "ACGTN" if rng.random() < 0.3 else "ACGT"
+        a = "".join(rng.choice(list(alpha), la))
+        b = "".join(rng.choice(list(alpha), lb))
+        assert oracle.score(a, b) == brute_best(oracle, a, b), (a, b)
+
+
+def check_alignment(oracle, amp, read, res, ra, mk, rb):
+    assert ra.replace("-", "") == amp
+    assert rb.replace("-", "") == read
+    assert len(ra) == len(rb) == len(mk) == res["aln_len"]
+    assert model_score(oracle, ra, rb) == res["score"], (amp, read, ra, rb)
+    ident = sum(1 for x, y in zip(ra, rb) if x != "-" and y != "-" and x.upper() == y.upper())
+    gaps = sum(1 for x, y in zip(ra, rb) if x == "-" or y == "-")
+    assert res["n_ident"] == ident and res["n_gaps"] == gaps
+    for x, y, m in zip(ra, rb, mk):
+        if x == "-" or y == "-":
+            assert m == " "
+        elif x.upper() == y.upper():
+            assert m == "|"
+        else:
+            assert m == (":" if sub(oracle, x, y) > 0 else ".")
+
+
+def test_traceback_is_optimal_and_consistent(oracle):
+    amp = synth.random_amplicon(120, 3)
+    buf, off = synth.reads_from(amp, 300, 4, synth.PARITY_MIX)
+    for read in synth.unpack(buf, off):
+        res, ra, mk, rb = oracle.align(amp, read)
+        check_alignment(oracle, amp, read, res, ra, mk, rb)
+        assert res["score"] == oracle.score(amp, read)
+
+
+def test_random_pairs_consistent(oracle):
+    rng = np.random.Generator(np.random.PCG64(11))
+    for _ in range(200):
+        la, lb = int(rng.integers(1, 40)), int(rng.integers(1, 40))
+        a = "".join(rng.choice(list(EDNA), la))
+        b = "".join(rng.choice(list(EDNA + "acgt"), lb))
+        res, ra, mk, rb = oracle.align(a, b)
+        check_alignment(oracle, a, b, res, ra, mk, rb)
+
+
+def test_tie_rules_known_answers(oracle):
+    # TT deletion inside TTT: an M/Y tie at (10, 8) goes to the gap (strict M
+    # rule), so the gap sits at the right end of the homopolymer.
+    res, ra, mk, rb = oracle.align("ACGTACGTTTGACCA", "ACGTACGTGACCA")
+    assert (ra, rb) == ("ACGTACGTTTGACCA", "ACGTACGT--GACCA")
+    assert res["score"] == 2 * (13 * 5) - 20 - 1
+    # a read that is a prefix: trailing amplicon overhang is free and printed
+    res, ra, mk, rb = oracle.align("ACGTACGTTTGACCA", "ACGTAC")
+    assert (ra, rb, mk) == ("ACGTACGTTTGACCA", "ACGTAC---------", "||||||         ")
+    assert res["aln_len"] == 15 and res["n_ident"] == 6 and res["n_gaps"] == 9
+    # read longer on both ends: leading and trailing read overhang
+    res, ra, mk, rb = oracle.align("TTGACC", "AAATTGACCGGG")
+    assert (ra, rb) == ("---TTGACC---", "AAATTGACCGGG")
+    # insertion of an A next to an A run: X/M tie -> gap placed right-most
+    res, ra, mk, rb = oracle.align("CCGAATTCG", "CCGAAATTCG")
+    assert (ra, rb) == ("CCGAA-TTCG", "CCGAAATTCG")
+
+
+def test_identity_formatting_boundaries():
+    """Where float32 and double evaluation of 100*i/L print differently with %.1f
+    (SURVEY Appendix A-7).  The oracle and the product both use double; this
+    keeps the exposure visible."""
+    diffs = []
+    for L in range(1, 1201):
+        for i in range(0, L + 1):
+            d = "%.1f" % (100.0 * i / L)
+            f = "%.1f" % float(np.float32(100.0) * np.float32(i) / np.float32(L))
+            if d != f:
+                diffs.append((i, L))
+    assert len(diffs) < 2000
+    assert (0, 1) not in diffs
+
+
+def test_srspair_roundtrip(oracle, tmp_path):
+    from crispresso_amd.needle import parse_needle_output
+
+    amp = synth.random_amplicon(90, 5)
+    buf, off = synth.reads_from(amp, 50, 6, synth.PARITY_MIX)
+    reads = synth.unpack(buf, off)
+    text = []
+    expect = []
+    for k, r in enumerate(reads):
+        res, ra, mk, rb = oracle.align(amp, r)
+        text.append(oracle.srspair("AMPL", f"@M1_2_{k}", res, ra, mk, rb))
+        expect.append((f"@M1:2:{k}", float("%.1f" % (100.0 * res["n_ident"] / res["aln_len"])), str(len(r)), ra, mk, rb))
+    p = tmp_path / "needle.txt"
+    p.write_text("# header\n\n" + "".join(text) + "#-----\n")
+    df = parse_needle_output(str(p), "ref")
+    assert list(df.index) == [e[0] for e in expect]
+    for (idx, row), e in zip(df.iterrows(), expect):
+        assert (row.score_ref, row.length, row.ref_seq, row.align_str, row.align_seq) == e[1:]
+    ds = parse_needle_output(str(p), "repaired", just_score=True)
+    assert list(ds.columns) == ["score_repaired"]
+
+
+def test_cli_matches_library(oracle, tmp_path):
+    import subprocess
+
+    amp = synth.random_amplicon(60, 8)
+    buf, off = synth.reads_from(amp, 20, 9, synth.PARITY_MIX)
+    reads = synth.unpack(buf, off)
+    (tmp_path / "a.fa").write_text(f">AMPL\n{amp}\n")
+    fasta = "".join(f">r{k}\n{r}\n" for k, r in enumerate(reads))
+    out = subprocess.run([oracle.CLI, f"-asequence={tmp_path / 'a.fa'}", "-bsequence=/dev/stdin",
+                          "-outfile=/dev/stdout", "-gapopen=10", "-gapextend=0.5", "-awidth3=5000"],
+                         input=fasta, capture_output=True, text=True, check=True).stdout
+    for k, r in enumerate(reads):
+        res, ra, mk, rb = oracle.align(amp, r)
+        assert oracle.srspair("AMPL", f"r{k}", res, ra, mk, rb) in out
