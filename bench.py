@@ -132,6 +132,7 @@ def main():
     algo_bytes = al.algo_bytes()       # per launch, from this batch's own results
     cells = al.cells()
     geo = al.geometry()
+    geo["fallback_reads"] = al.fallbacks()
     avg_ms = float(np.mean(kernel_ms))
     achieved_gbs = algo_bytes / (avg_ms * 1e-3) / 1e9
     gcups = cells / (avg_ms * 1e-3) / 1e9
@@ -171,7 +172,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": f"nw_align_kernel<{geo['rows_per_lane']},{bool(geo['tb_in_lds'])}>",
+                "kernel": f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>",
                 "kernel_ms_avg": avg_ms,
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",

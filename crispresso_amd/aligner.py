@@ -161,8 +161,13 @@ class GpuAligner:
     def geometry(self) -> dict:
         vals = [ctypes.c_int32() for _ in range(5)]
         self._check(self.lib.nw_batch_geometry(self._h, *[ctypes.byref(v) for v in vals]), "nw_batch_geometry")
-        return dict(zip(("rows_per_lane", "waves_per_block", "grid", "lds_bytes", "tb_in_lds"),
-                        (v.value for v in vals)))
+        g = dict(zip(("rows_per_lane", "waves_per_block", "grid", "lds_bytes", "tb_mode"), (v.value for v in vals)))
+        g["tb_mode"] = _lib.TB_MODES.get(g["tb_mode"], g["tb_mode"])
+        return g
+
+    def fallbacks(self) -> int:
+        """Reads of the last run re-aligned with full traceback storage."""
+        return int(self.lib.nw_batch_fallbacks(self._h))
 
     def download(self, n: int, max_len: int) -> AlignmentBatch:
         stride = int(self.lib.nw_required_stride(self._h, max(int(max_len), 1)))

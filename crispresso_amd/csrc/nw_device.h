@@ -32,19 +32,31 @@ struct KernelArgs {
     Stat* stats;               // [n]
     uint8_t* tb_global;        // traceback slabs when they do not fit LDS
     int64_t tb_wave_bytes;
+    int32_t debug_mode;        // 0 = normal; diagnostic builds of the phases: 1 = stop after
+                               // the start-cell search, 2 = stop after the traceback walk
+    // banded traceback storage (TB_BAND kernels)
+    int32_t band_slots;        // columns of traceback kept per lane
+    int64_t* fallback_list;    // reads whose traceback left the band are appended here
+    int32_t* fallback_count;
+    // work list (full-storage kernel re-running the fallbacks); null = all reads
+    const int64_t* work_list;
+    const int32_t* work_count;
 };
+
+// Traceback storage of a kernel instantiation.
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
     int wpb;         // waves per block
     int grid;        // blocks
     int lds_bytes;   // dynamic LDS per block
-    bool tb_in_lds;
+    int tb_mode;     // TbMode
 };
 
 int rows_per_lane_for(int La);
 int profile_rp(int R);
-int lds_bytes_for(int R, int La, int Lb_max, bool tb_in_lds, int wpb);
+int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb);
 int tb_bytes_per_wave(int R, int Lb_max);
 hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -97,7 +98,12 @@ struct nw_ctx {
     DevBuf<uint8_t> d_out;
     DevBuf<nw::Stat> d_stats;
     DevBuf<uint8_t> d_tb;
-    nw::LaunchCfg cfg{};
+    DevBuf<int64_t> d_fallback;       // reads re-run with full traceback storage
+    DevBuf<int32_t> d_fallback_count;
+    int band_slots = 64;              // 0 disables the banded kernel
+    bool use_band = false;
+    nw::LaunchCfg cfg{};              // full-storage kernel
+    nw::LaunchCfg band_cfg{};         // banded kernel
     bool ran = false;
 };
 
@@ -152,30 +158,48 @@ int64_t stride_for(int La, int32_t lb_max) { return ((int64_t)La + lb_max + 15) 
 int configure(nw_ctx* c) {
     const int La = (int)c->ref.size();
     const int R = c->R;
+    // full-storage kernel: every alignment (band disabled) or only the fallbacks
     nw::LaunchCfg cfg{};
     cfg.R = R;
-    cfg.tb_in_lds = false;
+    cfg.tb_mode = nw::TB_GLOBAL_FULL;
     cfg.wpb = 4;
     for (int wpb : {4, 2, 1}) {
-        int b = nw::lds_bytes_for(R, La, c->lb_max, true, wpb);
+        int b = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_LDS_FULL, 0, wpb);
         if (b > 0 && b <= kMaxLds) {
-            cfg.tb_in_lds = true;
+            cfg.tb_mode = nw::TB_LDS_FULL;
             cfg.wpb = wpb;
             cfg.lds_bytes = b;
             break;
         }
     }
-    if (!cfg.tb_in_lds) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, false, cfg.wpb);
+    if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, 0, cfg.wpb);
     if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
         return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel", c->lb_max);
-    const int per_cu = std::max(1, std::min(8, kMaxLds / cfg.lds_bytes));
-    const int64_t want = (c->n + cfg.wpb - 1) / cfg.wpb;
-    cfg.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
-    if (!cfg.tb_in_lds) {
+    int per_cu = std::max(1, std::min(8, kMaxLds / cfg.lds_bytes));
+    cfg.grid = c->num_cus * per_cu;
+    if (cfg.tb_mode == nw::TB_GLOBAL_FULL) {
         const int64_t per_wave = nw::tb_bytes_per_wave(R, c->lb_max);
         HIP_OR_FAIL(c, c->d_tb.reserve((size_t)per_wave * cfg.grid * cfg.wpb));
     }
     c->cfg = cfg;
+    // banded kernel
+    c->use_band = false;
+    if (c->band_slots > 0) {
+        nw::LaunchCfg b{};
+        b.R = R;
+        b.tb_mode = nw::TB_BAND;
+        b.wpb = 4;
+        b.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_BAND, c->band_slots, b.wpb);
+        if (b.lds_bytes > 0 && b.lds_bytes <= kMaxLds) {
+            per_cu = std::max(1, std::min(8, kMaxLds / b.lds_bytes));
+            const int64_t want = (c->n + b.wpb - 1) / b.wpb;
+            b.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
+            c->band_cfg = b;
+            c->use_band = true;
+        }
+    }
+    HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
+    HIP_OR_FAIL(c, c->d_fallback_count.reserve(4));
     return NW_OK;
 }
 
@@ -269,6 +293,7 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     if (!c) return NW_E_INVALID;
     if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || !reads))) return fail(c, NW_E_INVALID, "bad batch");
+    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS")) c->band_slots = std::max(0, std::atoi(bs));
     (void)hipSetDevice(c->device);
     const int La = (int)c->ref.size();
     int32_t lb_max = 1;
@@ -321,9 +346,21 @@ int nw_batch_run_async(nw_ctx* c) {
     a.stride = c->stride;
     a.stats = c->d_stats.p;
     a.tb_global = c->d_tb.p;
-    a.tb_wave_bytes = c->cfg.tb_in_lds ? 0 : nw::tb_bytes_per_wave(c->R, c->lb_max);
+    a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->R, c->lb_max) : 0;
+    a.band_slots = c->band_slots;
+    a.fallback_list = c->d_fallback.p;
+    a.fallback_count = c->d_fallback_count.p;
+    if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
-    if (c->n > 0) HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, sizeof(int32_t), c->stream));
+    if (c->n > 0) {
+        if (c->use_band) {
+            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
+            a.work_list = c->d_fallback.p;      // re-run what left the band
+            a.work_count = c->d_fallback_count.p;
+        }
+        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+    }
     HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
     c->ran = true;
     return NW_OK;
@@ -373,14 +410,24 @@ int64_t nw_batch_algo_bytes(nw_ctx* c) {
 int64_t nw_batch_cells(const nw_ctx* c) { return c ? c->cells : -1; }
 
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
-                      int32_t* lds_bytes, int32_t* tb_in_lds) {
+                      int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
-    if (rows_per_lane) *rows_per_lane = c->cfg.R;
-    if (waves_per_block) *waves_per_block = c->cfg.wpb;
-    if (grid) *grid = c->cfg.grid;
-    if (lds_bytes) *lds_bytes = c->cfg.lds_bytes;
-    if (tb_in_lds) *tb_in_lds = c->cfg.tb_in_lds ? 1 : 0;
+    const nw::LaunchCfg& k = c->use_band ? c->band_cfg : c->cfg;
+    if (rows_per_lane) *rows_per_lane = k.R;
+    if (waves_per_block) *waves_per_block = k.wpb;
+    if (grid) *grid = k.grid;
+    if (lds_bytes) *lds_bytes = k.lds_bytes;
+    if (tb_mode) *tb_mode = k.tb_mode;
     return NW_OK;
+}
+
+int64_t nw_batch_fallbacks(nw_ctx* c) {
+    if (!c || !c->ran) return -1;
+    (void)hipSetDevice(c->device);
+    int32_t v = 0;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    if (hipMemcpy(&v, c->d_fallback_count.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return c->use_band ? v : 0;
 }
 
 int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, char* aln_out,

@@ -13,10 +13,14 @@
 //     lane l+1 with one DPP wave_shr:1 per value per step -- no LDS round trip.
 //   * substitution scores come from a per-amplicon profile in LDS laid out
 //     [code][lane][RP] int8, so one ds_read_b32/b64 yields a lane's R scores.
-//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend) kept
-//     in LDS (or a global slab when LDS is too small), walked afterwards by the
-//     whole wave in runs: 64 lanes test 64 cells of the current diagonal/row/
-//     column at once and a ballot finds where the run ends.
+//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend).
+//     TB_BAND keeps them only for a diagonal band (a few KB of LDS per read, so
+//     many waves fit a CU); a read whose walk leaves the band is queued on the
+//     device and re-run by the TB_LDS_FULL / TB_GLOBAL_FULL instantiation, which
+//     stores every cell.  Bits inside the band come from the full DP, so the
+//     banded result is exact whenever the walk stays inside.
+//   * the walk is done by the whole wave in runs: 64 lanes test 64 cells of the
+//     current diagonal/row/column at once and a ballot finds where the run ends.
 //   * the three alignment strings are written straight to HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -49,9 +53,9 @@ __device__ __forceinline__ void lds_fence() {
 }
 
 // Orders this wave's traceback stores before other lanes' loads of them.
-template <bool TB_LDS>
+template <int MODE>
 __device__ __forceinline__ void tb_fence() {
-    if constexpr (TB_LDS) {
+    if constexpr (MODE != TB_GLOBAL_FULL) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -66,22 +70,23 @@ __device__ __forceinline__ unsigned char upcase(unsigned char c) {
 
 // Per-wave LDS layout (offsets in bytes from the wave's base), all 16-aligned.
 struct WaveLds {
-    int raw, coff, lastrow, runs, red, bits, total;
+    int raw, coff, lastrow, runs, bits, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
-template <int R>
-__host__ __device__ inline WaveLds wave_lds_layout(int La, int Lb_max, bool tb_in_lds) {
+__host__ __device__ inline int es_of(int R) { return R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8)); }
+
+__host__ __device__ inline WaveLds wave_lds_layout(int R, int La, int Lb_max, int mode, int band_slots) {
     WaveLds w;
     int o = 0;
     w.raw = o;     o += align16(Lb_max + 4);
     w.coff = o;    o += align16(2 * (Lb_max + 4));
     w.lastrow = o; o += align16(4 * (Lb_max + 1));
     w.runs = o;    o += align16(4 * (La + Lb_max + 8));
-    w.red = o;     o += 64;
     w.bits = o;
-    if (tb_in_lds) o += align16(Lb_max * 64 * Geo<R>::ES);
+    if (mode == TB_LDS_FULL) o += align16(Lb_max * 64 * es_of(R));
+    else if (mode == TB_BAND) o += align16(band_slots * 64 * es_of(R));
     w.total = align16(o);
     return w;
 }
@@ -91,29 +96,50 @@ __host__ __device__ inline int shared_lds_bytes(int R, int La) {
     return align16(NCODE * 64 * RP) + 256 + align16(La + 4);
 }
 
-template <int R>
-__device__ __forceinline__ unsigned load_nibble(const unsigned char* bits, int ai, int bj) {
-    constexpr int ES = Geo<R>::ES;
-    const int lane = ai / R, k = ai - lane * R;
-    const unsigned char* p = bits + ((size_t)bj * 64 + lane) * ES;
-    unsigned w;
-    int nr, kk;
-    if constexpr (ES == 1) { w = *p; nr = R; kk = k; }
-    else if constexpr (ES == 2) { w = *(const unsigned short*)p; nr = R; kk = k; }
-    else if constexpr (ES == 4) { w = *(const unsigned*)p; nr = R; kk = k; }
-    else {
-        const int wi = k >> 3;
-        w = ((const unsigned*)p)[wi];
-        nr = (R - 8 * wi) < 8 ? (R - 8 * wi) : 8;
-        kk = k & 7;
+// Where the traceback bits of cell (ai, bj) live.  Full modes: column bj.
+// Banded: lane l keeps columns [l*R + dlo, l*R + dlo + slots).
+template <int R, int MODE>
+struct TbStore {
+    unsigned char* base;
+    int dlo;
+    int slots;
+    __device__ __forceinline__ int slot(int lane, int bj) const {
+        if constexpr (MODE == TB_BAND) return bj - lane * R - dlo;
+        else return bj;
     }
-    return (w >> (4 * (nr - 1 - kk))) & 0xFu;
-}
+    __device__ __forceinline__ bool inside(int s) const {
+        if constexpr (MODE == TB_BAND) return (unsigned)s < (unsigned)slots;
+        else return true;
+    }
+    __device__ __forceinline__ unsigned char* at(int s, int lane) const {
+        return base + ((size_t)s * 64 + lane) * Geo<R>::ES;
+    }
+    // nibble of cell (ai, bj); *oob set when the cell is outside the band.
+    __device__ __forceinline__ unsigned nibble(int ai, int bj, bool* oob) const {
+        constexpr int ES = Geo<R>::ES;
+        const int lane = ai / R, k = ai - lane * R;
+        const int s = slot(lane, bj);
+        if (!inside(s)) { *oob = true; return 0u; }
+        *oob = false;
+        const unsigned char* p = at(s, lane);
+        unsigned w;
+        int nr, kk;
+        if constexpr (ES == 1) { w = *p; nr = R; kk = k; }
+        else if constexpr (ES == 2) { w = *(const unsigned short*)p; nr = R; kk = k; }
+        else if constexpr (ES == 4) { w = *(const unsigned*)p; nr = R; kk = k; }
+        else {
+            const int wi = k >> 3;
+            w = ((const unsigned*)p)[wi];
+            nr = (R - 8 * wi) < 8 ? (R - 8 * wi) : 8;
+            kk = k & 7;
+        }
+        return (w >> (4 * (nr - 1 - kk))) & 0xFu;
+    }
+};
 
 template <int R>
-__device__ __forceinline__ void store_bits(unsigned char* bits, int bj, int lane, const unsigned (&acc)[Geo<R>::NW]) {
+__device__ __forceinline__ void store_bits(unsigned char* p, const unsigned (&acc)[Geo<R>::NW]) {
     constexpr int ES = Geo<R>::ES;
-    unsigned char* p = bits + ((size_t)bj * 64 + lane) * ES;
     if constexpr (ES == 1) *p = (unsigned char)acc[0];
     else if constexpr (ES == 2) *(unsigned short*)p = (unsigned short)acc[0];
     else if constexpr (ES == 4) *(unsigned*)p = acc[0];
@@ -152,7 +178,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // Run codes stored in LDS: type << 28 | length.
 enum { RUN_M = 0, RUN_X = 1, RUN_Y = 2 };
 
-template <int R, bool TB_LDS>
+template <int R, int MODE>
 __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     constexpr int RP = Geo<R>::RP;
     constexpr int NWD = Geo<R>::NW;
@@ -176,7 +202,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     for (int q = tid; q < La; q += blockDim.x) amp_lds[q] = args.amp[q];
     __syncthreads();
 
-    const WaveLds L = wave_lds_layout<R>(La, args.Lb_max, TB_LDS);
+    const WaveLds L = wave_lds_layout(R, La, args.Lb_max, MODE, args.band_slots);
     unsigned char* wbase = smem + shared_lds_bytes(R, La) + wave * L.total;
     unsigned char* raw = wbase + L.raw;
     unsigned short* coff = (unsigned short*)(wbase + L.coff);
@@ -184,9 +210,11 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     unsigned* runs = (unsigned*)(wbase + L.runs);
     const long long gw = (long long)blockIdx.x * wpb + wave;
     const long long nwaves = (long long)gridDim.x * wpb;
-    unsigned char* bits;
-    if constexpr (TB_LDS) bits = wbase + L.bits;
-    else bits = args.tb_global + gw * args.tb_wave_bytes;
+    TbStore<R, MODE> tb;
+    if constexpr (MODE == TB_GLOBAL_FULL) tb.base = args.tb_global + gw * args.tb_wave_bytes;
+    else tb.base = wbase + L.bits;
+    tb.slots = args.band_slots;
+    tb.dlo = 0;
 
     const int nl = (La + R - 1) / R;        // lanes holding real rows
     const int ai0 = lane * R;
@@ -195,13 +223,26 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int prof_lane = lane * RP;
     const int pad_coff = NCODE_PAD * 64 * RP;   // offset of the all-zero pad code
 
-    for (long long rd = gw; rd < args.n; rd += nwaves) {
+    const long long nwork = args.work_list ? (long long)*args.work_count : args.n;
+    for (long long wi = gw; wi < nwork; wi += nwaves) {
+        const long long rd = args.work_list ? args.work_list[wi] : wi;
         const long long off = args.offsets[rd];
         const int Lb = (int)(args.offsets[rd + 1] - off);
         Stat* st = args.stats + rd;
         if (Lb <= 0) {
             if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; *st = z; }
             continue;
+        }
+        if constexpr (MODE == TB_BAND) {
+            // diagonal band [min(0, Lb-La) - m, max(0, Lb-La) + m] widened to the slots we have
+            const int dl = Lb - La;
+            const int span = (dl < 0 ? -dl : dl) + R;
+            const int m = (args.band_slots - span) / 2;
+            if (m < 0) {
+                if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+                continue;
+            }
+            tb.dlo = (dl < 0 ? dl : 0) - m;
         }
         // ---- stage the read: raw bytes + profile offsets of each column ----
         const unsigned char* rp = args.reads + off;
@@ -224,7 +265,8 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         int c_next = coff[min(max(bj0 + 1, 0), Lb + 3)];
         int sc[RP / 4];
         load_prof<R>(prof_lds, coff[min(max(bj0, 0), Lb + 3)] + prof_lane, sc);
-        for (int t = 0; t < nsteps; ++t) {
+        int slot = tb.slot(lane, bj0);
+        for (int t = 0; t < nsteps; ++t, ++slot) {
             const int bj = t - lane;
             const int rMo = shr1(sMo, -O);
             const int rY = shr1(sY, NEG);
@@ -264,7 +306,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     Yu = Y;
                 }
                 sMo = Mou; sY = Yu; sH = Hold[R - 1];
-                store_bits<R>(bits, bj, lane, acc);
+                if (tb.inside(slot)) store_bits<R>(tb.at(slot, lane), acc);
                 if (lane == lr) lastrow[bj] = mlast;
             }
             Htop = rH;
@@ -286,7 +328,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                 }
             }
         }
-        tb_fence<TB_LDS>();
+        tb_fence<MODE>();
         for (int q = lane; q < Lb - 1; q += 64) {
             const long long kk = ((long long)lastrow[q] << 32) | ((1ll << 24) | q);
             key = kk > key ? kk : key;
@@ -299,6 +341,10 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         else if ((prio >> 24) == 2) { ei = (prio & 0xffffff) + 1; ej = Lb; }
         else { ei = La; ej = (prio & 0xffffff) + 1; }
 
+        if (args.debug_mode == 1) {
+            if (lane == 0) { Stat z = {}; z.score = score; z.end_i = ei; z.end_j = ej; *st = z; }
+            continue;
+        }
         // ---- traceback in runs ----
         int nruns = 0, last_type = -1;
         auto push = [&](int type, int n) {
@@ -314,44 +360,53 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
         else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
         int i = ei, j = ej, state = RUN_M;
+        bool left_band = false;
         while (i > 0 && j > 0) {
+            bool oob = false;
+            unsigned long long m;
+            int nb = RUN_M;
             if (state == RUN_M) {
                 const int ci = i - 1 - lane, cj = j - 1 - lane;
                 const bool valid = ci >= 1 && cj >= 1;
-                unsigned nib = valid ? load_nibble<R>(bits, ci - 1, cj - 1) : 0u;
+                const unsigned nib = valid ? tb.nibble(ci - 1, cj - 1, &oob) : 0u;
+                oob = valid && oob;
                 const int best = (nib & 1u) ? RUN_M : ((nib & 2u) ? RUN_X : RUN_Y);
-                const unsigned long long m = __ballot(!valid || best != RUN_M);
+                m = __ballot(!valid || oob || best != RUN_M);
                 if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
-                const int k0 = __builtin_ctzll(m);
-                const int nb = __shfl(best, k0, 64);
-                push(RUN_M, k0 + 1);
-                i -= k0 + 1; j -= k0 + 1;
-                state = nb;
+                nb = __shfl(best, (int)__builtin_ctzll(m), 64);
             } else if (state == RUN_X) {
                 const int cj = j - lane;
                 const bool valid = cj >= 1;
-                unsigned nib = valid ? load_nibble<R>(bits, i - 1, cj - 1) : 0u;
-                const unsigned long long m = __ballot(!valid || !(nib & 4u));
+                const unsigned nib = valid ? tb.nibble(i - 1, cj - 1, &oob) : 0u;
+                oob = valid && oob;
+                m = __ballot(!valid || oob || !(nib & 4u));
                 if (m == 0) { push(RUN_X, 64); j -= 64; continue; }
-                const int k0 = __builtin_ctzll(m);
-                push(RUN_X, k0 + 1);
-                j -= k0 + 1;
-                state = RUN_M;
             } else {
                 const int ci = i - lane;
                 const bool valid = ci >= 1;
-                unsigned nib = valid ? load_nibble<R>(bits, ci - 1, j - 1) : 0u;
-                const unsigned long long m = __ballot(!valid || !(nib & 8u));
+                const unsigned nib = valid ? tb.nibble(ci - 1, j - 1, &oob) : 0u;
+                oob = valid && oob;
+                m = __ballot(!valid || oob || !(nib & 8u));
                 if (m == 0) { push(RUN_Y, 64); i -= 64; continue; }
-                const int k0 = __builtin_ctzll(m);
-                push(RUN_Y, k0 + 1);
-                i -= k0 + 1;
-                state = RUN_M;
             }
+            const int k0 = (int)__builtin_ctzll(m);
+            if (__ballot(oob) & (1ull << k0)) { left_band = true; break; }
+            push(state, k0 + 1);
+            if (state != RUN_Y) j -= k0 + 1;
+            if (state != RUN_X) i -= k0 + 1;
+            state = (state == RUN_M) ? nb : RUN_M;
+        }
+        if (left_band) {
+            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+            continue;
         }
         if (i > 0) push(RUN_Y, i);
         if (j > 0) push(RUN_X, j);
         lds_fence();
+        if (args.debug_mode == 2) {
+            if (lane == 0) { Stat z = {}; z.score = score; z.aln_len = nruns; *st = z; }
+            continue;
+        }
 
         // ---- emit strings, forward order ----
         unsigned char* o_ref = args.out + rd * 3 * args.stride;
@@ -416,23 +471,18 @@ namespace nw {
 
 template <int R>
 static hipError_t launch_r(const KernelArgs& a, const LaunchCfg& c, hipStream_t s) {
-    if (c.tb_in_lds)
-        hipLaunchKernelGGL((nw_align_kernel<R, true>), dim3(c.grid), dim3(64 * c.wpb), c.lds_bytes, s, a);
-    else
-        hipLaunchKernelGGL((nw_align_kernel<R, false>), dim3(c.grid), dim3(64 * c.wpb), c.lds_bytes, s, a);
+    const dim3 grid(c.grid), block(64 * c.wpb);
+    switch (c.tb_mode) {
+        case TB_LDS_FULL: hipLaunchKernelGGL((nw_align_kernel<R, TB_LDS_FULL>), grid, block, c.lds_bytes, s, a); break;
+        case TB_GLOBAL_FULL: hipLaunchKernelGGL((nw_align_kernel<R, TB_GLOBAL_FULL>), grid, block, c.lds_bytes, s, a); break;
+        default: hipLaunchKernelGGL((nw_align_kernel<R, TB_BAND>), grid, block, c.lds_bytes, s, a); break;
+    }
     return hipGetLastError();
 }
 
-int lds_bytes_for(int R, int La, int Lb_max, bool tb_in_lds, int wpb) {
-    int per = 0;
-    switch (R) {
-#define NW_CASE(r) case r: per = wave_lds_layout<r>(La, Lb_max, tb_in_lds).total; break;
-        NW_CASE(1) NW_CASE(2) NW_CASE(3) NW_CASE(4) NW_CASE(5) NW_CASE(6) NW_CASE(7) NW_CASE(8)
-        NW_CASE(10) NW_CASE(12) NW_CASE(14) NW_CASE(16)
-#undef NW_CASE
-        default: return -1;
-    }
-    return shared_lds_bytes(R, La) + wpb * per;
+int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb) {
+    if (rows_per_lane_for(R * 64) != R) return -1;
+    return shared_lds_bytes(R, La) + wpb * wave_lds_layout(R, La, Lb_max, tb_mode, band_slots).total;
 }
 
 int rows_per_lane_for(int La) {
@@ -445,10 +495,7 @@ int rows_per_lane_for(int La) {
     return -1;
 }
 
-int tb_bytes_per_wave(int R, int Lb_max) {
-    int es = R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8));
-    return align16(Lb_max * 64 * es);
-}
+int tb_bytes_per_wave(int R, int Lb_max) { return align16(Lb_max * 64 * es_of(R)); }
 
 int profile_rp(int R) { return R <= 4 ? 4 : (R <= 8 ? 8 : 16); }
 

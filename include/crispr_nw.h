@@ -103,9 +103,14 @@ int nw_batch_download(nw_ctx* ctx, char* aln_out, int64_t stride, nw_stat* stats
 int64_t nw_batch_algo_bytes(nw_ctx* ctx);
 /* Cells (sum of ref_len * read_len) of the uploaded batch. */
 int64_t nw_batch_cells(const nw_ctx* ctx);
-/* Launch geometry of the last run: rows per lane, waves per block, grid, LDS. */
+/* Launch geometry of the kernel that aligns the bulk of the batch: rows per
+ * lane, waves per block, grid, LDS bytes per block, traceback storage
+ * (0 = full in LDS, 1 = full in a global slab, 2 = diagonal band in LDS). */
 int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
-                      int32_t* grid, int32_t* lds_bytes, int32_t* tb_in_lds);
+                      int32_t* grid, int32_t* lds_bytes, int32_t* tb_mode);
+/* Reads of the last run whose traceback left the diagonal band and were
+ * re-aligned with full traceback storage (synchronises). */
+int64_t nw_batch_fallbacks(nw_ctx* ctx);
 
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated

@@ -95,7 +95,7 @@ def test_global_traceback_slab(gpu_aligner_factory, oracle):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_in_lds"] == 0
+    assert a.fallbacks() >= 2
     assert_same(oracle, amp, buf, off, batch, "global-tb")
 
 
@@ -110,3 +110,39 @@ def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle):
     a.set_reference(amp2)
     buf, off = synth.reads_from(amp2, 700, 5)
     assert_same(oracle, amp2, buf, off, a.align_packed(buf, off), "switch-ref")
+
+
+def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch):
+    """Reads whose traceback leaves the diagonal band (large indels, shifted
+    reads) are re-run with full storage; results stay bit-identical."""
+    amp = synth.random_amplicon(250, 1)
+    rng = np.random.Generator(np.random.PCG64(33))
+    reads = []
+    for d in (40, 60, 100, 150):
+        p = int(rng.integers(20, 250 - d - 20))
+        reads.append(amp[:p] + amp[p + d:])                                 # big deletion
+    for k in (40, 80):
+        reads.append(amp[:125] + synth.random_amplicon(k, 50 + k) + amp[125:])  # big insertion
+    reads += [amp[100:], amp[:90], amp[60:200], synth.random_amplicon(250, 77)]  # shifted / unrelated
+    buf0, off0 = synth.reads_from(amp, 400, 8, synth.PARITY_MIX)
+    reads += synth.unpack(buf0, off0)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "band-lds"
+    assert a.fallbacks() >= 6
+    assert_same(oracle, amp, buf, off, batch, "band-fallback")
+
+
+@pytest.mark.parametrize("slots", ["0", "8", "24"])
+def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
+    """Same answers with the band off (full storage only) or very narrow (mostly fallbacks)."""
+    monkeypatch.setenv("CRISPR_NW_BAND_SLOTS", slots)
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 600, 12, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "band-lds")
+    assert_same(oracle, amp, buf, off, batch, f"slots={slots}")
