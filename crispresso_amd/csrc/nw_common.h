@@ -1,0 +1,180 @@
+// nw_common.h -- device helpers shared by the aligner kernels: lane moves,
+// fences, the run-based traceback walk and the string emitter.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nw_device.h"
+
+namespace nw {
+
+constexpr int NEG = -(1 << 28);
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+__device__ __forceinline__ int shr1(int v, int fill) {
+    // DPP wave_shr:1 -- lane l receives lane l-1's value, lane 0 keeps `fill`.
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ void lds_fence() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ unsigned char upcase(unsigned char c) {
+    return (c >= 'a' && c <= 'z') ? (unsigned char)(c - 32) : c;
+}
+
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        long long u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Candidate key for the traceback start cell.  Scan order of the reference
+// walk start (corner, then last column bottom->top, then last row right->left,
+// first strict maximum) becomes "largest (score, priority)".
+__device__ __forceinline__ long long end_key(int score, int cls, int pos) {
+    return ((long long)score << 32) | (((long long)cls << 24) | pos);
+}
+__device__ __forceinline__ void decode_end(long long key, int La, int Lb, int* score, int* ei, int* ej) {
+    *score = (int)(key >> 32);
+    const int prio = (int)(key & 0xffffffff);
+    if ((prio >> 24) == 3) { *ei = La; *ej = Lb; }
+    else if ((prio >> 24) == 2) { *ei = (prio & 0xffffff) + 1; *ej = Lb; }
+    else { *ei = La; *ej = (prio & 0xffffff) + 1; }
+}
+
+// Run codes stored in LDS: type << 28 | length.
+enum { RUN_M = 0, RUN_X = 1, RUN_Y = 2 };
+
+// Traceback walk in runs.  `nib(ai, bj, &oob)` returns the 4-bit cell code
+// (bit0: M > max(X,Y), bit1: X > Y, bit2: X extends, bit3: Y extends) of the
+// 0-based cell, setting oob when the cell is not stored.  Writes runs in
+// end->start order to `runs` (lane 0, at most `cap`), returns the count, or -1
+// when the walk needs a cell outside the stored band or more than `cap` runs.
+template <class Nib>
+__device__ int walk_runs(const Nib& nib, int La, int Lb, int ei, int ej, unsigned* runs, int cap, int lane) {
+    int nruns = 0, last_type = -1;
+    bool full = false;
+    auto push = [&](int type, int n) {
+        if (n <= 0) return;
+        if (type == last_type) {
+            if (lane == 0) runs[nruns - 1] += (unsigned)n;
+        } else if (nruns < cap) {
+            if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
+            ++nruns;
+            last_type = type;
+        } else {
+            full = true;
+        }
+    };
+    if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
+    else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
+    int i = ei, j = ej, state = RUN_M;
+    while (i > 0 && j > 0) {
+        bool oob = false;
+        unsigned long long m;
+        int nb = RUN_M;
+        if (state == RUN_M) {
+            const int ci = i - 1 - lane, cj = j - 1 - lane;
+            const bool valid = ci >= 1 && cj >= 1;
+            const unsigned c = valid ? nib(ci - 1, cj - 1, &oob) : 0u;
+            oob = valid && oob;
+            const int best = (c & 1u) ? RUN_M : ((c & 2u) ? RUN_X : RUN_Y);
+            m = __ballot(!valid || oob || best != RUN_M);
+            if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
+            nb = __shfl(best, (int)__builtin_ctzll(m), 64);
+        } else if (state == RUN_X) {
+            const int cj = j - lane;
+            const bool valid = cj >= 1;
+            const unsigned c = valid ? nib(i - 1, cj - 1, &oob) : 0u;
+            oob = valid && oob;
+            m = __ballot(!valid || oob || !(c & 4u));
+            if (m == 0) { push(RUN_X, 64); j -= 64; continue; }
+        } else {
+            const int ci = i - lane;
+            const bool valid = ci >= 1;
+            const unsigned c = valid ? nib(ci - 1, j - 1, &oob) : 0u;
+            oob = valid && oob;
+            m = __ballot(!valid || oob || !(c & 8u));
+            if (m == 0) { push(RUN_Y, 64); i -= 64; continue; }
+        }
+        const int k0 = (int)__builtin_ctzll(m);
+        if ((__ballot(oob) & (1ull << k0)) || full) return -1;
+        push(state, k0 + 1);
+        if (state != RUN_Y) j -= k0 + 1;
+        if (state != RUN_X) i -= k0 + 1;
+        state = (state == RUN_M) ? nb : RUN_M;
+    }
+    if (i > 0) push(RUN_Y, i);
+    if (j > 0) push(RUN_X, j);
+    return full ? -1 : nruns;
+}
+
+// Writes the aligned amplicon / markup / aligned read for the runs (forward
+// order) and the per-read record.  `sim_score(ai, code)` is the substitution
+// score of amplicon row ai against residue code (only its sign matters).
+template <class Score>
+__device__ void emit_alignment(const unsigned* runs, int nruns, const unsigned char* amp, const unsigned char* raw,
+                               const unsigned char* lut, const Score& sim_score, unsigned char* o_ref,
+                               int64_t stride, int score, int ei, int ej, Stat* st, int lane) {
+    unsigned char* o_mk = o_ref + stride;
+    unsigned char* o_rd = o_mk + stride;
+    int col = 0, ia = 0, jb = 0;
+    int n_id = 0, n_sim = 0, n_gap = 0;
+    for (int q = nruns - 1; q >= 0; --q) {
+        const unsigned rc = runs[q];
+        const int type = (int)(rc >> 28);
+        const int n = (int)(rc & 0x0fffffffu);
+        for (int p = lane; p < n; p += 64) {
+            unsigned char ca = '-', cb = '-', mk = ' ';
+            if (type != RUN_X) ca = amp[ia + p];
+            if (type != RUN_Y) cb = raw[jb + p];
+            // a '-' already in the input (RC-pass reads, CRISPRessoCORE.py:1846) prints
+            // like a gap, so it counts as one, as for an alignment gap
+            const bool gapcol = ca == '-' || cb == '-';
+            n_gap += gapcol;
+            if (type == RUN_M && !gapcol) {
+                const bool id = upcase(ca) == upcase(cb);
+                const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
+                mk = id ? '|' : (sim ? ':' : '.');
+                n_id += id;
+                n_sim += sim;
+            }
+            o_ref[col + p] = ca;
+            o_mk[col + p] = mk;
+            o_rd[col + p] = cb;
+        }
+        col += n;
+        if (type != RUN_X) ia += n;
+        if (type != RUN_Y) jb += n;
+    }
+    n_id = wave_sum(n_id);
+    n_sim = wave_sum(n_sim);
+    n_gap = wave_sum(n_gap);
+    if (lane == 0) {
+        Stat s;
+        s.aln_len = col;
+        s.n_ident = n_id;
+        s.n_sim = n_sim;
+        s.n_gaps = n_gap;
+        s.score = score;
+        s.end_i = ei;
+        s.end_j = ej;
+        s.flags = 0;
+        *st = s;
+    }
+}
+
+}  // namespace nw

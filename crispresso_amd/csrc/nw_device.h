@@ -41,10 +41,11 @@ struct KernelArgs {
     // work list (full-storage kernel re-running the fallbacks); null = all reads
     const int64_t* work_list;
     const int32_t* work_count;
+    int32_t* work_counter;     // dynamic chunk queue of the pair kernel (zeroed per run)
 };
 
 // Traceback storage of a kernel instantiation.
-enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2 };
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
@@ -59,5 +60,12 @@ int profile_rp(int R);
 int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb);
 int tb_bytes_per_wave(int R, int Lb_max);
 hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
+
+// two-reads-per-wave packed int16 kernel (nw_pair.hip); band storage only.
+// Blocks may hold up to kPairMaxThreads threads (its __launch_bounds__).
+constexpr int kPairMaxThreads = 512;
+int pair_lds_bytes_for(int R, int La, int Lb_max, int band_slots, int wpb);
+int pair_profile_bytes_per_lane(int R);
+hipError_t launch_pair(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
 }  // namespace nw

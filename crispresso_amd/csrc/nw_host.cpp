@@ -86,6 +86,7 @@ struct nw_ctx {
     std::string ref;
     int R = 0;
     DevBuf<int8_t> d_prof;
+    DevBuf<int16_t> d_prof16;         // pair kernel: int16, rows padded on top
     DevBuf<uint8_t> d_lut, d_amp;
     // batch
     int64_t n = 0;
@@ -99,9 +100,12 @@ struct nw_ctx {
     DevBuf<nw::Stat> d_stats;
     DevBuf<uint8_t> d_tb;
     DevBuf<int64_t> d_fallback;       // reads re-run with full traceback storage
-    DevBuf<int32_t> d_fallback_count;
-    int band_slots = 64;              // 0 disables the banded kernel
+    DevBuf<int32_t> d_fallback_count; // [0] fallback count, [1] pair-kernel work counter
+    int band_slots = 64;              // 0 disables the banded kernels
+    int pair_slots = 56;
     bool use_band = false;
+    bool use_pair = false;
+    nw::LaunchCfg pair_cfg{};         // packed int16 two-reads-per-wave kernel
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
     bool ran = false;
@@ -140,6 +144,21 @@ int build_profile(nw_ctx* c) {
             prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
         }
     }
+    // int16 profile of the pair kernel: rows padded on top so that the last
+    // amplicon row is the bottom row of the last lane
+    const int R4 = (R + 3) & ~3;
+    const int nl = (La + R - 1) / R, F = nl * R - La;
+    std::vector<int16_t> prof16((size_t)nw::NCODE * 64 * R4, 0);
+    for (int ai = 0; ai < La; ++ai) {
+        const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+        const int g = ai + F;
+        for (int code = 0; code < nw::NCODE; ++code) {
+            int s = (ca < 16 && code < 16) ? kEdna[ca][code] * c->scale : 0;
+            prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
+        }
+    }
+    HIP_OR_FAIL(c, c->d_prof16.reserve(prof16.size()));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16.p, prof16.data(), prof16.size() * 2, hipMemcpyHostToDevice, c->stream));
     uint8_t lut[256];
     for (int q = 0; q < 256; ++q) lut[q] = code_of((unsigned char)q);
     HIP_OR_FAIL(c, c->d_prof.reserve(prof.size()));
@@ -198,6 +217,34 @@ int configure(nw_ctx* c) {
             c->use_band = true;
         }
     }
+    // packed int16 pair kernel: scores must fit int16 with room for differences
+    c->use_pair = false;
+    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "pair" | "band" | "full" (tests/diagnostics)
+    const bool want_pair = !kern || std::strcmp(kern, "pair") == 0;
+    const int64_t hi = 5ll * c->scale * La;
+    const bool fits16 = hi + c->gap_extend < 16000 && 9ll * c->scale * La + c->gap_open + c->gap_extend < 32000;
+    if (want_pair && fits16 && c->pair_slots > 0) {
+        nw::LaunchCfg p{};
+        p.R = R;
+        p.tb_mode = nw::TB_PAIR_BAND;
+        // waves per block that maximise resident waves per CU (LDS-limited; the
+        // kernel's registers allow 3 waves per SIMD = 12 per CU at R <= 4)
+        int best_waves = 0;
+        for (int wpb = 1; wpb <= nw::kPairMaxThreads / 64; ++wpb) {
+            const int b = nw::pair_lds_bytes_for(R, La, c->lb_max, c->pair_slots, wpb);
+            if (b <= 0 || b > kMaxLds) break;
+            const int waves = std::min(wpb * (kMaxLds / b), 12);
+            if (waves > best_waves) { best_waves = waves; p.wpb = wpb; p.lds_bytes = b; }
+        }
+        if (best_waves > 0) {
+            per_cu = std::max(1, best_waves / p.wpb);
+            const int64_t want = ((c->n + 1) / 2 + p.wpb - 1) / p.wpb;
+            p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
+            c->pair_cfg = p;
+            c->use_pair = true;
+        }
+    }
+    if (kern && std::strcmp(kern, "full") == 0) c->use_band = false;
     HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
     HIP_OR_FAIL(c, c->d_fallback_count.reserve(4));
     return NW_OK;
@@ -293,7 +340,7 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     if (!c) return NW_E_INVALID;
     if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || !reads))) return fail(c, NW_E_INVALID, "bad batch");
-    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS")) c->band_slots = std::max(0, std::atoi(bs));
+    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS")) c->band_slots = c->pair_slots = std::max(0, std::atoi(bs));
     (void)hipSetDevice(c->device);
     const int La = (int)c->ref.size();
     int32_t lb_max = 1;
@@ -352,11 +399,19 @@ int nw_batch_run_async(nw_ctx* c) {
     a.fallback_count = c->d_fallback_count.p;
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
-    HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, sizeof(int32_t), c->stream));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
+    a.work_counter = c->d_fallback_count.p + 1;
     if (c->n > 0) {
-        if (c->use_band) {
-            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
+        if (c->use_pair) {
+            nw::KernelArgs ap = a;
+            ap.prof = (const int8_t*)c->d_prof16.p;
+            ap.band_slots = c->pair_slots;
+            HIP_OR_FAIL(c, nw::launch_pair(ap, c->pair_cfg, c->stream));
             a.work_list = c->d_fallback.p;      // re-run what left the band
+            a.work_count = c->d_fallback_count.p;
+        } else if (c->use_band) {
+            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
+            a.work_list = c->d_fallback.p;
             a.work_count = c->d_fallback_count.p;
         }
         HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
@@ -412,7 +467,7 @@ int64_t nw_batch_cells(const nw_ctx* c) { return c ? c->cells : -1; }
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
-    const nw::LaunchCfg& k = c->use_band ? c->band_cfg : c->cfg;
+    const nw::LaunchCfg& k = c->use_pair ? c->pair_cfg : (c->use_band ? c->band_cfg : c->cfg);
     if (rows_per_lane) *rows_per_lane = k.R;
     if (waves_per_block) *waves_per_block = k.wpb;
     if (grid) *grid = k.grid;
@@ -427,7 +482,7 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
     int32_t v = 0;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
     if (hipMemcpy(&v, c->d_fallback_count.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return c->use_band ? v : 0;
+    return (c->use_band || c->use_pair) ? v : 0;
 }
 
 int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, char* aln_out,

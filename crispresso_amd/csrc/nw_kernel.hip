@@ -25,11 +25,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "nw_device.h"
+#include "nw_common.h"
 
 namespace nw {
-
-constexpr int NEG = -(1 << 28);
 
 template <int R> struct Geo {
     static constexpr int RP = R <= 4 ? 4 : (R <= 8 ? 8 : 16);      // profile bytes per lane
@@ -37,20 +35,12 @@ template <int R> struct Geo {
     static constexpr int NW = (R + 7) / 8;                         // 32-bit bit-accumulators
 };
 
-__device__ __forceinline__ int shr1(int v, int fill) {
-    // DPP wave_shr:1 -- lane l receives lane l-1's value, lane 0 keeps `fill`.
-    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
-}
 
 __device__ __forceinline__ unsigned push_sign(unsigned acc, int d) {
     // (acc << 1) | (d < 0)
     return __builtin_amdgcn_alignbit(acc, (unsigned)d, 31);
 }
 
-__device__ __forceinline__ void lds_fence() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Orders this wave's traceback stores before other lanes' loads of them.
 template <int MODE>
@@ -64,16 +54,12 @@ __device__ __forceinline__ void tb_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ unsigned char upcase(unsigned char c) {
-    return (c >= 'a' && c <= 'z') ? (unsigned char)(c - 32) : c;
-}
 
 // Per-wave LDS layout (offsets in bytes from the wave's base), all 16-aligned.
 struct WaveLds {
     int raw, coff, lastrow, runs, bits, total;
 };
 
-__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 __host__ __device__ inline int es_of(int R) { return R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8)); }
 
@@ -160,23 +146,8 @@ __device__ __forceinline__ void load_prof(const unsigned char* prof_lds, int off
     }
 }
 
-__device__ __forceinline__ long long wave_max_i64(long long v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        long long u = __shfl_xor(v, o, 64);
-        v = u > v ? u : v;
-    }
-    return v;
-}
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
-// Run codes stored in LDS: type << 28 | length.
-enum { RUN_M = 0, RUN_X = 1, RUN_Y = 2 };
 
 template <int R, int MODE>
 __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
@@ -334,131 +305,31 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
             key = kk > key ? kk : key;
         }
         key = wave_max_i64(key);
-        const int score = (int)(key >> 32);
-        const int prio = (int)(key & 0xffffffff);
-        int ei, ej;   // 1-based start cell
-        if ((prio >> 24) == 3) { ei = La; ej = Lb; }
-        else if ((prio >> 24) == 2) { ei = (prio & 0xffffff) + 1; ej = Lb; }
-        else { ei = La; ej = (prio & 0xffffff) + 1; }
+        int score, ei, ej;   // 1-based start cell
+        decode_end(key, La, Lb, &score, &ei, &ej);
 
         if (args.debug_mode == 1) {
             if (lane == 0) { Stat z = {}; z.score = score; z.end_i = ei; z.end_j = ej; *st = z; }
             continue;
         }
         // ---- traceback in runs ----
-        int nruns = 0, last_type = -1;
-        auto push = [&](int type, int n) {
-            if (n <= 0) return;
-            if (type == last_type) {
-                if (lane == 0) runs[nruns - 1] += (unsigned)n;
-            } else {
-                if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
-                ++nruns;
-                last_type = type;
-            }
-        };
-        if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
-        else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
-        int i = ei, j = ej, state = RUN_M;
-        bool left_band = false;
-        while (i > 0 && j > 0) {
-            bool oob = false;
-            unsigned long long m;
-            int nb = RUN_M;
-            if (state == RUN_M) {
-                const int ci = i - 1 - lane, cj = j - 1 - lane;
-                const bool valid = ci >= 1 && cj >= 1;
-                const unsigned nib = valid ? tb.nibble(ci - 1, cj - 1, &oob) : 0u;
-                oob = valid && oob;
-                const int best = (nib & 1u) ? RUN_M : ((nib & 2u) ? RUN_X : RUN_Y);
-                m = __ballot(!valid || oob || best != RUN_M);
-                if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
-                nb = __shfl(best, (int)__builtin_ctzll(m), 64);
-            } else if (state == RUN_X) {
-                const int cj = j - lane;
-                const bool valid = cj >= 1;
-                const unsigned nib = valid ? tb.nibble(i - 1, cj - 1, &oob) : 0u;
-                oob = valid && oob;
-                m = __ballot(!valid || oob || !(nib & 4u));
-                if (m == 0) { push(RUN_X, 64); j -= 64; continue; }
-            } else {
-                const int ci = i - lane;
-                const bool valid = ci >= 1;
-                const unsigned nib = valid ? tb.nibble(ci - 1, j - 1, &oob) : 0u;
-                oob = valid && oob;
-                m = __ballot(!valid || oob || !(nib & 8u));
-                if (m == 0) { push(RUN_Y, 64); i -= 64; continue; }
-            }
-            const int k0 = (int)__builtin_ctzll(m);
-            if (__ballot(oob) & (1ull << k0)) { left_band = true; break; }
-            push(state, k0 + 1);
-            if (state != RUN_Y) j -= k0 + 1;
-            if (state != RUN_X) i -= k0 + 1;
-            state = (state == RUN_M) ? nb : RUN_M;
-        }
-        if (left_band) {
+        auto nib = [&](int ai, int bj, bool* oob) { return tb.nibble(ai, bj, oob); };
+        const int nruns = walk_runs(nib, La, Lb, ei, ej, runs, La + Lb + 8, lane);
+        if (nruns < 0) {
             if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
             continue;
         }
-        if (i > 0) push(RUN_Y, i);
-        if (j > 0) push(RUN_X, j);
         lds_fence();
         if (args.debug_mode == 2) {
             if (lane == 0) { Stat z = {}; z.score = score; z.aln_len = nruns; *st = z; }
             continue;
         }
-
         // ---- emit strings, forward order ----
-        unsigned char* o_ref = args.out + rd * 3 * args.stride;
-        unsigned char* o_mk = o_ref + args.stride;
-        unsigned char* o_rd = o_mk + args.stride;
-        int col = 0, ia = 0, jb = 0;
-        int n_id = 0, n_sim = 0, n_gap = 0;
-        for (int q = nruns - 1; q >= 0; --q) {
-            const unsigned rc = runs[q];
-            const int type = (int)(rc >> 28);
-            const int n = (int)(rc & 0x0fffffffu);
-            for (int p = lane; p < n; p += 64) {
-                unsigned char ca = '-', cb = '-', mk = ' ';
-                if (type != RUN_X) ca = amp_lds[ia + p];
-                if (type != RUN_Y) cb = raw[jb + p];
-                // a '-' already in the input (RC-pass reads, CRISPRessoCORE.py:1846) prints
-                // like a gap, so it counts as one, as for an alignment gap
-                const bool gapcol = ca == '-' || cb == '-';
-                n_gap += gapcol;
-                if (type == RUN_M && !gapcol) {
-                    const int ai = ia + p;
-                    const bool id = upcase(ca) == upcase(cb);
-                    const int code = lut_lds[cb];
-                    const signed char s = (signed char)prof_lds[code * 64 * RP + (ai / R) * RP + (ai % R)];
-                    const bool sim = id || s > 0;
-                    mk = id ? '|' : (sim ? ':' : '.');
-                    n_id += id;
-                    n_sim += sim;
-                }
-                o_ref[col + p] = ca;
-                o_mk[col + p] = mk;
-                o_rd[col + p] = cb;
-            }
-            col += n;
-            if (type != RUN_X) ia += n;
-            if (type != RUN_Y) jb += n;
-        }
-        n_id = wave_sum(n_id);
-        n_sim = wave_sum(n_sim);
-        n_gap = wave_sum(n_gap);
-        if (lane == 0) {
-            Stat s;
-            s.aln_len = col;
-            s.n_ident = n_id;
-            s.n_sim = n_sim;
-            s.n_gaps = n_gap;
-            s.score = score;
-            s.end_i = ei;
-            s.end_j = ej;
-            s.flags = 0;
-            *st = s;
-        }
+        auto sim = [&](int ai, int code) {
+            return (int)(signed char)prof_lds[code * 64 * RP + (ai / R) * RP + (ai % R)];
+        };
+        emit_alignment(runs, nruns, amp_lds, raw, lut_lds, sim, args.out + rd * 3 * args.stride, args.stride,
+                       score, ei, ej, st, lane);
         lds_fence();
     }
 }

@@ -105,7 +105,8 @@ int64_t nw_batch_algo_bytes(nw_ctx* ctx);
 int64_t nw_batch_cells(const nw_ctx* ctx);
 /* Launch geometry of the kernel that aligns the bulk of the batch: rows per
  * lane, waves per block, grid, LDS bytes per block, traceback storage
- * (0 = full in LDS, 1 = full in a global slab, 2 = diagonal band in LDS). */
+ * (0 = full in LDS, 1 = full in a global slab, 2 = diagonal band in LDS,
+ * 3 = diagonal band in LDS, two reads per wavefront in packed int16). */
 int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
                       int32_t* grid, int32_t* lds_bytes, int32_t* tb_mode);
 /* Reads of the last run whose traceback left the diagonal band and were

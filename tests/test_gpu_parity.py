@@ -12,6 +12,15 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
+KERNELS = ["pair", "band", "full"]
+
+
+@pytest.fixture(params=KERNELS)
+def kernel(request, monkeypatch):
+    """Run a test once per kernel family (CRISPR_NW_KERNEL selects it)."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", request.param)
+    return request.param
+
 FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j")
 
 
@@ -39,7 +48,7 @@ def assert_same(oracle, amplicon, buf, offsets, batch, label=""):
             assert g == o, f"{label} read {i} string {k}:\n gpu {g!r}\n cpu {o!r}"
 
 
-def test_hand_cases(gpu_aligner_factory, oracle):
+def test_hand_cases(gpu_aligner_factory, oracle, kernel):
     amp = "ACGTACGTTTGACCA"
     reads = ["ACGTACGTGACCA", "ACGTACGTTTGACCAGG", "TTGACC", "A", "ACGTACGTTTGACCA", "", "acgtNNNNtttgacca",
              "GGGGGGGGGGGGGGGGGGGGGGGGGGGGGG", "T-C-A", "ACGTRYKMSWBDHVNU"]
@@ -49,7 +58,7 @@ def test_hand_cases(gpu_aligner_factory, oracle):
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "hand")
 
 
-def test_c2_mix(gpu_aligner_factory, oracle):
+def test_c2_mix(gpu_aligner_factory, oracle, kernel):
     amp = synth.random_amplicon(250, 1)
     buf, off = synth.reads_from(amp, 3000, 2)
     a = gpu_aligner_factory()
@@ -57,7 +66,7 @@ def test_c2_mix(gpu_aligner_factory, oracle):
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "c2")
 
 
-def test_parity_mix(gpu_aligner_factory, oracle):
+def test_parity_mix(gpu_aligner_factory, oracle, kernel):
     amp = synth.random_amplicon(250, 1)
     buf, off = synth.reads_from(amp, 3000, 3, synth.PARITY_MIX)
     a = gpu_aligner_factory()
@@ -67,7 +76,7 @@ def test_parity_mix(gpu_aligner_factory, oracle):
 
 @pytest.mark.parametrize("La", [1, 2, 7, 63, 64, 65, 128, 129, 192, 250, 257, 320, 384, 448, 512, 513, 640, 768,
                                  896, 1024])
-def test_amplicon_lengths(gpu_aligner_factory, oracle, La):
+def test_amplicon_lengths(gpu_aligner_factory, oracle, kernel, La):
     amp = synth.random_amplicon(La, 100 + La)
     rng = np.random.Generator(np.random.PCG64(La))
     reads = []
@@ -99,7 +108,7 @@ def test_global_traceback_slab(gpu_aligner_factory, oracle):
     assert_same(oracle, amp, buf, off, batch, "global-tb")
 
 
-def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle):
+def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle, kernel):
     amp = synth.random_amplicon(180, 21)
     a = gpu_aligner_factory()
     a.set_reference(amp)
@@ -130,7 +139,7 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == "band-lds"
+    assert a.geometry()["tb_mode"] == "pair-band-int16"
     assert a.fallbacks() >= 6
     assert_same(oracle, amp, buf, off, batch, "band-fallback")
 
@@ -144,5 +153,23 @@ def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "band-lds")
+    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "pair-band-int16")
     assert_same(oracle, amp, buf, off, batch, f"slots={slots}")
+
+
+def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle):
+    """Pair kernel: partners of different lengths, empty partners, odd batch size."""
+    amp = synth.random_amplicon(230, 41)
+    rng = np.random.Generator(np.random.PCG64(41))
+    reads = []
+    for k in range(301):
+        L = int(rng.integers(0, 260)) if k % 7 else 0
+        s = int(rng.integers(0, max(1, 230 - L)))
+        r = amp[s:s + L] if rng.random() < 0.7 else synth.random_amplicon(max(L, 1), k)[:L]
+        reads.append(r)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "pair-band-int16"
+    assert_same(oracle, amp, buf, off, batch, "pairs")
