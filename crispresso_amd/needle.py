@@ -20,9 +20,14 @@ Reference quirks reproduced on purpose:
   3. identities exactly equal to ``min_identity_score`` are neither kept nor
      retried (strict ``<`` / ``>``, ``CORE:1844-1851``, ``1866-1871``);
   4. the RC-HDR pass passes the literal text ``args.needle_options_string`` to
-     needle (``CORE:1928``), which makes that needle call fail: by default we
-     raise the same ``NeedleException`` (``rc_hdr_quirk="raise"``);
-     ``rc_hdr_quirk="align"`` runs the pass the author evidently meant.
+     needle (``CORE:1928``), so that needle run produces no alignments; the
+     failure goes unnoticed because ``sb.call`` sees the exit status of the
+     pipeline's last command, ``gzip`` (``CORE:1932-1934``).  The reference
+     therefore joins an EMPTY repair table: RC rows get ``score_repaired`` and
+     ``score_diff`` = NaN.  ``rc_hdr_quirk="reference"`` (default) reproduces
+     that (pinned by tests/golden/syn_hdr_rcfail); ``"align"`` runs the pass the
+     author evidently meant.  (The same exit-status rule means a failing needle
+     never raises NeedleException in the reference; ours raises on real errors.)
   5. read ids lose real underscores (``sed 's/:/_/g'`` then ``_`` -> ``:``,
      ``CORE:1797``, ``1725``).
 """
@@ -195,13 +200,17 @@ class AlignArgs:
 
 def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Optional[GpuAligner] = None,
                 output_dir: Optional[str] = None, database_id: str = "AMPL",
-                rc_hdr_quirk: str = "raise") -> pd.DataFrame:
+                rc_hdr_quirk: str = "reference") -> pd.DataFrame:
     """CRISPRessoCORE.py:1788-2000 on the GPU: returns ``df_needle_alignment``.
 
     The result has the reference's columns (``score_ref, length, ref_seq,
     align_str, align_seq`` and, with an HDR amplicon, ``score_repaired,
     score_diff``) and index (read ids, ``_RC`` suffix for reverse-complement hits).
     """
+    # CRISPRessoCORE.py:1283 and 1350 normalise the amplicons before anything else
+    args.amplicon_seq = args.amplicon_seq.upper().strip().rstrip("\n")
+    if args.expected_hdr_amplicon_seq:
+        args.expected_hdr_amplicon_seq = args.expected_hdr_amplicon_seq.strip().upper()
     opts = NeedleOptions.parse(args.needle_options_string)
     own = aligner is None
     if own:
@@ -247,14 +256,21 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             rc = needle_pass(aligner, rc_amp, rc_names, rc_buf, rc_off, database_id,
                              _jp(f"needle_output_rc_{database_id}.txt.gz") if keep_files else None)
             if args.expected_hdr_amplicon_seq:
-                if rc_hdr_quirk == "raise":
-                    # CRISPRessoCORE.py:1924-1936 hands needle the literal text
-                    # "args.needle_options_string"; needle fails and the reference raises.
-                    raise NeedleException("Needle failed to run, please check the log file.")
-                rc_rep = needle_pass(aligner, reverse_complement(args.expected_hdr_amplicon_seq), rc_names,
-                                     rc_buf, rc_off, database_id,
-                                     _jp(f"needle_output_repair_rc_{database_id}.txt.gz") if keep_files else None)
-                df_database_and_repair_rc = rc.dataframe("ref").join(rc_rep.dataframe("repaired", just_score=True))
+                if rc_hdr_quirk == "reference":
+                    # CRISPRessoCORE.py:1924-1936: needle gets the literal text
+                    # "args.needle_options_string" and aligns nothing; the empty output
+                    # parses to an empty table (CORE:1776-1777)
+                    df_repair_rc = pd.DataFrame([], columns=["ID", "score_repaired"]).set_index("ID")
+                    if keep_files:
+                        with gzip.open(_jp(f"needle_output_repair_rc_{database_id}.txt.gz"), "wt"):
+                            pass
+                else:
+                    rc_rep = needle_pass(aligner, reverse_complement(args.expected_hdr_amplicon_seq), rc_names,
+                                         rc_buf, rc_off, database_id,
+                                         _jp(f"needle_output_repair_rc_{database_id}.txt.gz") if keep_files
+                                         else None)
+                    df_repair_rc = rc_rep.dataframe("repaired", just_score=True)
+                df_database_and_repair_rc = rc.dataframe("ref").join(df_repair_rc)
                 df_database_and_repair_rc = df_database_and_repair_rc.loc[
                     (df_database_and_repair_rc.score_ref > args.min_identity_score)
                     | (df_database_and_repair_rc.score_repaired > args.min_identity_score)

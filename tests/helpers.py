@@ -1,0 +1,48 @@
+"""Test doubles: an aligner with GpuAligner's interface backed by the CPU oracle.
+
+Used only in CPU tests (no GPU in the build container) to exercise the host
+logic around the aligner; the GPU path itself is covered by the -m gpu tests.
+"""
+import numpy as np
+
+from crispresso_amd import _lib
+from crispresso_amd.aligner import AlignmentBatch, pack_reads
+from crispresso_amd.needle_options import NeedleOptions
+from oracle import oracle_py
+
+
+def oracle_batch(amplicon, buf, offsets, awidth=5000, gap_open=10.0, gap_extend=0.5):
+    p = oracle_py.params(gap_open, gap_extend)
+    res, aln = oracle_py.align_batch(amplicon, buf, offsets, p, nthreads=4)
+    n = len(offsets) - 1
+    stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+    for f in ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j"):
+        stats[f] = res[f]
+    lens = np.diff(offsets)
+    stats["flags"] = np.where(lens == 0, _lib.NW_FLAG_EMPTY, 0)
+    stride = ((aln.shape[2] + 15) // 16) * 16
+    out = np.zeros((n, 3, stride), dtype=np.uint8)
+    out[:, :, : aln.shape[2]] = aln
+    return AlignmentBatch(stats, out, lens, p.scale, awidth)
+
+
+class OracleAligner:
+    """Stand-in for GpuAligner (same methods the host code calls)."""
+
+    def __init__(self, device=0, options=None):
+        self.options = options or NeedleOptions()
+        self.scale = oracle_py.params(self.options.gap_open, self.options.gap_extend).scale
+        self.reference = None
+
+    def set_reference(self, seq):
+        self.reference = seq
+
+    def align_packed(self, buf, offsets):
+        return oracle_batch(self.reference, buf, offsets, self.options.awidth, self.options.gap_open,
+                            self.options.gap_extend)
+
+    def align(self, reads):
+        return self.align_packed(*pack_reads(reads))
+
+    def close(self):
+        pass

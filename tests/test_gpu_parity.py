@@ -173,3 +173,23 @@ def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle):
     batch = a.align_packed(buf, off)
     assert a.geometry()["tb_mode"] == "pair-band-int16"
     assert_same(oracle, amp, buf, off, batch, "pairs")
+
+
+def test_needle_cli_matches_oracle_cli(tmp_path, oracle):
+    """The GPU `needle` shim and the oracle CLI print the same srspair blocks."""
+    import subprocess
+    import sys
+
+    amp = synth.random_amplicon(180, 61)
+    buf, off = synth.reads_from(amp, 200, 62, synth.PARITY_MIX)
+    reads = synth.unpack(buf, off)
+    (tmp_path / "a.fa").write_text(f">AMPL\n{amp}\n")
+    fasta = "".join(f">@M0_1_{k} 1_N\n{r}\n" for k, r in enumerate(reads))
+    args = [f"-asequence={tmp_path / 'a.fa'}", "-bsequence=/dev/stdin", "-outfile=/dev/stdout",
+            "-gapopen=10", "-gapextend=0.5", "-awidth3=5000"]
+    import os
+    shim = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "crispresso_amd", "bin", "needle")
+    gpu = subprocess.run([sys.executable, shim] + args, input=fasta, capture_output=True, text=True, check=True).stdout
+    cpu = subprocess.run([oracle.CLI] + args, input=fasta, capture_output=True, text=True, check=True).stdout
+    strip = lambda t: t[t.index("#=="): t.rindex("#---------------------------------------\n#---")]  # noqa: E731
+    assert strip(gpu) == strip(cpu)

@@ -1,0 +1,126 @@
+"""Host-side logic around the aligner (CPU only): needle options, the
+FASTQ->FASTA semantics of the reference pipeline, the srspair writer, the
+DataFrame fast path vs the restated parser, and the reference helpers."""
+import gzip
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from crispresso_amd import fastq, synth
+from crispresso_amd.aligner import format_srspair, pack_reads, printed_percent
+from crispresso_amd.needle import batch_to_dataframe, find_wrong_nt, parse_needle_output, reverse_complement
+from crispresso_amd.needle_options import DEFAULT_NEEDLE_OPTIONS, NeedleOptions, UnsupportedNeedleOption
+from tests.helpers import oracle_batch
+
+
+def test_default_needle_options():
+    o = NeedleOptions.parse(DEFAULT_NEEDLE_OPTIONS)
+    assert (o.gap_open, o.gap_extend, o.awidth, o.end_weight, o.matrix) == (10.0, 0.5, 5000, False, "EDNAFULL")
+
+
+@pytest.mark.parametrize("text,expect", [
+    ("-gapopen 12 -gapextend=1", (12.0, 1.0)),
+    ("-gapopen=5.5 -gapextend 0.25 -noendweight", (5.5, 0.25)),
+    ("-auto -gapopen=10 -gapextend=0.5 -awidth3=60 -aformat3 srspair", (10.0, 0.5)),
+])
+def test_needle_option_forms(text, expect):
+    o = NeedleOptions.parse(text)
+    assert (o.gap_open, o.gap_extend) == expect
+
+
+@pytest.mark.parametrize("text", ["-endweight", "-endweight=Y", "-datafile=EBLOSUM62", "-bogus 3", "stray"])
+def test_unsupported_needle_options_raise(text):
+    with pytest.raises(UnsupportedNeedleOption):
+        NeedleOptions.parse(text)
+
+
+def test_reference_helpers():
+    # tests/crispresso_tests.py:99-101 of the reference
+    assert reverse_complement("ACTGGT") == "ACCAGT"
+    assert reverse_complement("ac-gN_") == "_NC-GT"
+    with pytest.raises(KeyError):
+        reverse_complement("ACR")
+    # the reference test at :93-96 compares None == None; this is the intended check
+    assert sorted(find_wrong_nt("ACBTGCNGRCCACTGFNNC")) == ["B", "F", "R"]
+
+
+def test_fastq_to_fasta_semantics():
+    data = (b"@M1:2:AB-C:1 1:N:0:1\nACGTN\n+\nIIIII\n"
+            b"@r_2 desc\nac.gt-*x1\n+\nIIIIIIIII\n"
+            b"@empty\n\n+\n\n")
+    names, buf, off = fastq.fastq_bytes_as_fasta(data)
+    # awk keeps '@' and the whole header; sed turns every ':' into '_'; EMBOSS keeps the first word
+    assert names == ["@M1_2_AB-C_1", "@r_2", "@empty"]
+    seqs = synth.unpack(buf, off)
+    # EMBOSS keeps letters and *.~?#+- ; digits are dropped
+    assert seqs == ["ACGTN", "ac.gt-*x", ""]
+    # parse_needle_output turns '_' back into ':' (real underscores too)
+    assert names[1].split()[-1].replace("_", ":") == "@r:2"
+
+
+def test_fastq_file_counts(tmp_path):
+    p = tmp_path / "r.fastq.gz"
+    recs = b"".join(b"@id%d\nACGT\n+\nIIII\n" % i for i in range(25))
+    p.write_bytes(gzip.compress(recs))
+    names, buf, off = fastq.read_fastq_as_fasta(str(p))
+    assert len(names) == 25 == fastq.count_reads(str(p))
+
+
+def _batch(amp, reads, awidth=5000):
+    buf, off = pack_reads(reads)
+    return oracle_batch(amp, buf, off, awidth)
+
+
+def test_cpp_writer_matches_oracle_writer(oracle):
+    amp = synth.random_amplicon(120, 9)
+    buf, off = synth.reads_from(amp, 60, 10, synth.PARITY_MIX)
+    reads = synth.unpack(buf, off)
+    batch = oracle_batch(amp, buf, off)
+    names = [f"@M1_2_{k}" for k in range(len(reads))]
+    text = format_srspair(batch, "AMPL", names, NeedleOptions())
+    expect = ""
+    for k, r in enumerate(reads):
+        res, ra, mk, rb = oracle.align(amp, r)
+        expect += oracle.srspair("AMPL", names[k], res, ra, mk, rb)
+    assert text == expect
+
+
+@pytest.mark.parametrize("awidth", [5000, 60])
+def test_dataframe_fast_path_equals_text_parse(tmp_path, awidth):
+    amp = synth.random_amplicon(150, 11)
+    buf, off = synth.reads_from(amp, 200, 12, synth.PARITY_MIX)
+    reads = synth.unpack(buf, off) + ["", "ACGT-ACGT"]
+    buf, off = pack_reads(reads)
+    batch = oracle_batch(amp, buf, off, awidth)
+    names = [f"@M0_1_{k}" for k in range(len(reads))]
+    o = NeedleOptions(awidth=awidth)
+    p = tmp_path / "needle.txt.gz"
+    with gzip.open(p, "wt") as fh:
+        fh.write("# header\n\n" + format_srspair(batch, "AMPL", names, o) + "#---\n")
+    for name, js in (("ref", False), ("repaired", True)):
+        parsed = parse_needle_output(str(p), name, just_score=js)
+        fast = batch_to_dataframe(batch, names, name, just_score=js)
+        pd.testing.assert_frame_equal(parsed, fast)
+    assert len(parsed) == len(reads) - 1        # needle skips the empty read
+
+
+def test_printed_percent_is_printf_rounding():
+    for num, den in [(151, 280), (1, 8), (1, 400), (3, 400), (100, 100), (0, 7)]:
+        assert printed_percent(num, den) == float("%.1f" % (100.0 * num / den))
+
+
+def test_needle_cli_argument_split():
+    from crispresso_amd.needle_cli import split_args
+
+    a, b, out, rest = split_args(["-asequence=A.fa", "-bsequence", "/dev/stdin", "-outfile=/dev/stdout",
+                                  "-gapopen=10", "-gapextend=0.5", "-awidth3=5000"])
+    assert (a, b, out) == ("A.fa", "/dev/stdin", "/dev/stdout")
+    assert NeedleOptions.parse(rest).awidth == 5000
+
+
+def test_needle_cli_rejects_bad_options(capsys):
+    from crispresso_amd.needle_cli import main
+
+    assert main(["-asequence=a", "-bsequence=b", "-endweight"]) == 1
+    assert "endweight" in capsys.readouterr().err
