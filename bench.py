@@ -155,7 +155,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "int16x2" if geo["tb_mode"].startswith("pair") else "int32",
             "data": "synthetic (SURVEY 8d C2 mix: 60% exact, 20% 1-3 subs, 10% del, 5% ins, 5% 1% noise)",
             "config": {
                 "workload": f"C2: {args.reads} synthetic ~250 bp reads x 250 bp amplicon per GPU, "
