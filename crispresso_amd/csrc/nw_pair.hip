@@ -6,8 +6,8 @@
 //   * every VGPR holds read A in its low half and read B in its high half, so
 //     each v_pk_add/sub/max_i16 advances two DP cells;
 //   * the 4 traceback sign bits of both cells are gathered with two v_perm_b32
-//     per row (sign bytes) and shifted into byte-planes: one dword per lane,
-//     column and 4-row group holds both reads' bits;
+//     per row (sign-select bytes) and masked into byte-planes with v_and_or: one
+//     dword per lane, column and 4-row group holds both reads' bits;
 //   * the amplicon's rows are padded at the TOP with zero-score rows: such rows
 //     reproduce the DP boundary (M = 0, H = 0, Y/X never chosen), so the last
 //     amplicon row is always the bottom row of the last lane, and columns before
@@ -208,9 +208,9 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
             rH = dpp_shr1(rH, sH);
             load_prof16<R>(prof_lds + cA[t + 1] + prof_lane, pn_a);
             load_prof16<R>(prof_lds + cB[t + 1] + prof_lane, pn_b);
-            unsigned accT[NG], accU[NG];
+            unsigned acc[NG];
 #pragma unroll
-            for (int g = 0; g < NG; ++g) { accT[g] = 0u; accU[g] = 0u; }
+            for (int g = 0; g < NG; ++g) acc[g] = 0u;
             s16x2 Hd = as_v(Htop), Mou = as_v(rMo), Yu = as_v(rY);
 #pragma unroll
             for (int k = 0; k < R; ++k) {
@@ -227,10 +227,13 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
                 const unsigned d2 = as_u(as_v(Mol[k]) - Xe); // sign: X extends
                 const unsigned d3 = as_u(Y - X);             // sign: X > Y
                 const unsigned d4 = as_u(mxy - M);           // sign: M > max(X, Y)
-                const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x07050301u);
-                const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x07050301u);
-                accT[k >> 2] = (accT[k >> 2] >> 1) | (tt & 0x80808080u);
-                accU[k >> 2] = (accU[k >> 2] >> 1) | (uu & 0x80808080u);
+                // v_perm selectors 8..11 give 0x00/0xff from bit 15/31 of a source: one byte
+                // per (difference, read) -> [yA yB xA xB] and [bXA bXB bMA bMB]; row k of its
+                // 4-row group lands in bit k (first word) and bit 4+k (second word) of each byte
+                const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
+                const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
+                acc[k >> 2] = (tt & (0x01010101u << (k & 3))) | acc[k >> 2];
+                acc[k >> 2] = (uu & (0x10101010u << (k & 3))) | acc[k >> 2];
                 const s16x2 Mo = M - as_v(O2);
                 Hd = as_v(Hold[k]);
                 Hold[k] = as_u(H);
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
             if ((unsigned)slot < (unsigned)slots) {
                 unsigned* p = bits_lane + (size_t)slot * 64 * NG;
 #pragma unroll
-                for (int g = 0; g < NG; ++g) p[g] = accT[g] | (accU[g] >> 4);
+                for (int g = 0; g < NG; ++g) p[g] = acc[g];
             }
             if (lane == lr) lastrow_t[t] = sMo;     // Mo of the last amplicon row
             if (t == tA) {
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
                 const int grp = k >> 2, kk = k & 3;
                 const int gR = (R - 4 * grp) < 4 ? (R - 4 * grp) : 4;
                 const unsigned w = bits[((size_t)s * 64 + ln) * NG + grp];
-                const int hb = 8 * h + 8 - gR + kk, lb = 8 * h + 4 - gR + kk;
+                const int hb = 8 * h + kk, lb = 8 * h + 4 + kk;
                 const unsigned yext = (w >> hb) & 1u, bX = (w >> lb) & 1u;
                 const unsigned xext = (w >> (16 + hb)) & 1u, bM = (w >> (16 + lb)) & 1u;
                 return bM | (bX << 1) | (xext << 2) | (yext << 3);
