@@ -25,7 +25,7 @@ NW_E_NOMEM = -5
 NW_E_STATE = -6
 NW_TIE_EMBOSS = 0
 NW_FLAG_EMPTY = 1
-TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 3: "pair-band-int16"}
+TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 3: "pair-band-int16", 4: "stream-int16"}
 
 # Field order of nw_stat (include/crispr_nw.h).
 STAT_FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j", "flags")
@@ -36,7 +36,8 @@ EXPORTS = (
     "nw_create", "nw_destroy", "nw_last_error", "nw_set_params", "nw_score_scale",
     "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload",
     "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
-    "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_format_srspair",
+    "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
+    "nw_format_srspair",
 )
 
 
@@ -78,6 +79,7 @@ def load() -> ctypes.CDLL:
         "nw_batch_cells": (c_int64, [ctx_p]),
         "nw_batch_geometry": (c_int, [ctx_p] + [POINTER(c_int32)] * 5),
         "nw_batch_fallbacks": (c_int64, [ctx_p]),
+        "nw_batch_kernel_times": (c_int, [ctx_p] + [POINTER(c_float)] * 3),
         "nw_format_srspair": (
             c_int64,
             [c_void_p, c_int64, c_char_p, c_char_p, c_float, c_float, c_int32, c_int32, c_void_p, c_int64,

@@ -169,6 +169,13 @@ class GpuAligner:
         """Reads of the last run re-aligned with full traceback storage."""
         return int(self.lib.nw_batch_fallbacks(self._h))
 
+    def kernel_times(self) -> dict:
+        """Device ms of the last run: DP fill, traceback/emit kernel, the rest."""
+        vals = [ctypes.c_float() for _ in range(3)]
+        self._check(self.lib.nw_batch_kernel_times(self._h, *[ctypes.byref(v) for v in vals]),
+                    "nw_batch_kernel_times")
+        return dict(zip(("fill_ms", "walk_ms", "rest_ms"), (float(v.value) for v in vals)))
+
     def download(self, n: int, max_len: int) -> AlignmentBatch:
         stride = int(self.lib.nw_required_stride(self._h, max(int(max_len), 1)))
         stats = np.zeros(n, dtype=_lib.STAT_DTYPE)

@@ -41,11 +41,13 @@ struct KernelArgs {
     // work list (full-storage kernel re-running the fallbacks); null = all reads
     const int64_t* work_list;
     const int32_t* work_count;
-    int32_t* work_counter;     // dynamic chunk queue of the pair kernel (zeroed per run)
+    int32_t* work_counter;     // dynamic chunk queue of the pair/stream kernels (zeroed per run)
+    // streaming kernels: per-pair traceback regions in HBM (StreamRegion layout)
+    uint8_t* region;
 };
 
 // Traceback storage of a kernel instantiation.
-enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3 };
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3, TB_STREAM = 4 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
@@ -67,5 +69,22 @@ constexpr int kPairMaxThreads = 512;
 int pair_lds_bytes_for(int R, int La, int Lb_max, int band_slots, int wpb);
 int pair_profile_bytes_per_lane(int R);
 hipError_t launch_pair(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
+
+// streaming fill + walk kernels (nw_stream.hip).  Pair p's region starts at
+// region + p * stride: traceback band [slots][64 lanes][NG] words, captures
+// (last-column Mo) [64 lanes][R], last amplicon row Mo [span] (both reads packed).
+constexpr int kStreamMinSpan = 16;   // stream columns per pair at least (bounds live descriptors)
+constexpr int kStreamRunsCap = 512;  // traceback runs per read kept in LDS
+struct StreamRegion {
+    int64_t bits, caps, last, stride;
+};
+__host__ __device__ inline int stream_walk_shared_bytes(int La) { return ((256 + La + 16) + 15) & ~15; }
+int stream_fill_lds_bytes(int R, int wpb);
+int stream_walk_lds_bytes(int La, int wpb);
+StreamRegion stream_region_for(int R, int band_slots, int Lb_max);
+// `after_fill` (may be null) is recorded between the two kernels.
+hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+                         hipEvent_t after_fill);
+hipError_t stream_occupancy(int R, int wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks);
 
 }  // namespace nw

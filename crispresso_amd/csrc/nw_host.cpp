@@ -78,6 +78,7 @@ struct nw_ctx {
     int num_cus = 256;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_fill = nullptr, ev_walk = nullptr;   // after the fill / walk kernels
     std::string err;
     // params
     float gap_open_f = 10.0f, gap_extend_f = 0.5f;
@@ -105,6 +106,12 @@ struct nw_ctx {
     int pair_slots = 56;
     bool use_band = false;
     bool use_pair = false;
+    bool use_stream = false;
+    int stream_slots = 56;
+    int64_t pass_reads = 0;            // reads per fill+walk pass (region memory bound)
+    nw::StreamRegion region{};
+    DevBuf<uint8_t> d_region;          // per-pair traceback regions of the streaming kernels
+    nw::LaunchCfg stream_fill{}, stream_walk{};
     nw::LaunchCfg pair_cfg{};         // packed int16 two-reads-per-wave kernel
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
@@ -220,7 +227,7 @@ int configure(nw_ctx* c) {
     // packed int16 pair kernel: scores must fit int16 with room for differences
     c->use_pair = false;
     const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "pair" | "band" | "full" (tests/diagnostics)
-    const bool want_pair = !kern || std::strcmp(kern, "pair") == 0;
+    const bool want_pair = kern && std::strcmp(kern, "pair") == 0;
     const int64_t hi = 5ll * c->scale * La;
     const bool fits16 = hi + c->gap_extend < 16000 && 9ll * c->scale * La + c->gap_open + c->gap_extend < 32000;
     if (want_pair && fits16 && c->pair_slots > 0) {
@@ -244,9 +251,40 @@ int configure(nw_ctx* c) {
             c->use_pair = true;
         }
     }
+    // streaming fill + walk kernels (default when the scores fit int16)
+    c->use_stream = false;
+    const bool want_stream = !kern || std::strcmp(kern, "stream") == 0;
+    if (want_stream && fits16 && c->stream_slots > 0) {
+        nw::LaunchCfg f{}, w{};
+        f.R = w.R = R;
+        f.tb_mode = w.tb_mode = nw::TB_STREAM;
+        f.wpb = w.wpb = 4;
+        f.lds_bytes = nw::stream_fill_lds_bytes(R, f.wpb);
+        w.lds_bytes = nw::stream_walk_lds_bytes(La, w.wpb);
+        int fb = 0, wb = 0;
+        HIP_OR_FAIL(c, nw::stream_occupancy(R, f.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb));
+        if (fb > 0 && wb > 0) {
+            const int64_t pairs = (c->n + 1) / 2;
+            f.grid = (int)std::max<int64_t>(1, std::min<int64_t>((pairs + f.wpb - 1) / f.wpb, (int64_t)c->num_cus * fb));
+            w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + w.wpb - 1) / w.wpb, (int64_t)c->num_cus * wb));
+            if (const char* g = std::getenv("CRISPR_NW_STREAM_GRID"))   // tests: few long streams
+                f.grid = std::max(1, std::min(f.grid, std::atoi(g)));
+            c->region = nw::stream_region_for(R, c->stream_slots, c->lb_max);
+            int64_t cap_bytes = 16ll << 30;
+            if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
+            int64_t pass_pairs = std::max<int64_t>(1, std::min<int64_t>(pairs, cap_bytes / c->region.stride));
+            c->pass_reads = 2 * pass_pairs;
+            HIP_OR_FAIL(c, c->d_region.reserve((size_t)(pass_pairs * c->region.stride + 64 * 1024)));
+            c->stream_fill = f;
+            c->stream_walk = w;
+            c->use_stream = true;
+            c->use_pair = false;
+        }
+    }
     if (kern && std::strcmp(kern, "full") == 0) c->use_band = false;
     HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    HIP_OR_FAIL(c, c->d_fallback_count.reserve(4));
+    const int64_t passes = c->use_stream ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
+    HIP_OR_FAIL(c, c->d_fallback_count.reserve((size_t)(4 * passes)));
     return NW_OK;
 }
 
@@ -263,7 +301,8 @@ int nw_create(int device, nw_ctx** out) {
     nw_ctx* c = new nw_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess) {
         delete c;
         return NW_E_HIP;
     }
@@ -280,7 +319,10 @@ void nw_destroy(nw_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->d_prof.release(); c->d_lut.release(); c->d_amp.release();
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
-    c->d_stats.release(); c->d_tb.release();
+    c->d_stats.release(); c->d_tb.release(); c->d_region.release();
+    c->d_prof16.release(); c->d_fallback.release(); c->d_fallback_count.release();
+    if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
+    if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -340,7 +382,8 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     if (!c) return NW_E_INVALID;
     if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || !reads))) return fail(c, NW_E_INVALID, "bad batch");
-    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS")) c->band_slots = c->pair_slots = std::max(0, std::atoi(bs));
+    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))
+        c->band_slots = c->pair_slots = c->stream_slots = std::max(0, std::atoi(bs));
     (void)hipSetDevice(c->device);
     const int La = (int)c->ref.size();
     int32_t lb_max = 1;
@@ -398,6 +441,39 @@ int nw_batch_run_async(nw_ctx* c) {
     a.fallback_list = c->d_fallback.p;
     a.fallback_count = c->d_fallback_count.p;
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
+    HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
+    if (c->use_stream) {
+        // passes of at most pass_reads reads (the per-pair regions of one pass stay resident)
+        const int64_t passes = std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads);
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * passes * sizeof(int32_t), c->stream));
+        for (int64_t q = 0; q < passes && c->n > 0; ++q) {
+            const int64_t lo = q * c->pass_reads, hi = std::min(c->n, lo + c->pass_reads);
+            nw::KernelArgs ap = a;
+            ap.offsets = c->d_offsets.p + lo;
+            ap.n = hi - lo;
+            ap.out = c->d_out.p + lo * 3 * c->stride;
+            ap.stats = c->d_stats.p + lo;
+            ap.prof = (const int8_t*)c->d_prof16.p;
+            ap.band_slots = c->stream_slots;
+            ap.region = c->d_region.p;
+            ap.fallback_list = c->d_fallback.p + lo;
+            ap.fallback_count = c->d_fallback_count.p + 4 * q;
+            ap.work_counter = ap.fallback_count + 1;
+            HIP_OR_FAIL(c, nw::launch_stream(ap, c->stream_fill, c->stream_walk, c->stream, q == 0 ? c->ev_fill : nullptr));
+            if (q == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+            nw::KernelArgs af = a;
+            af.offsets = ap.offsets;
+            af.n = ap.n;
+            af.out = ap.out;
+            af.stats = ap.stats;
+            af.work_list = ap.fallback_list;    // exact int32 kernel on what left the band
+            af.work_count = ap.fallback_count;
+            HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->stream));
+        }
+        HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
+        c->ran = true;
+        return NW_OK;
+    }
     HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
     a.work_counter = c->d_fallback_count.p + 1;
@@ -464,10 +540,30 @@ int64_t nw_batch_algo_bytes(nw_ctx* c) {
 
 int64_t nw_batch_cells(const nw_ctx* c) { return c ? c->cells : -1; }
 
+int nw_batch_kernel_times(nw_ctx* c, float* fill_ms, float* walk_ms, float* rest_ms) {
+    if (!c) return NW_E_INVALID;
+    if (!c->ran) return fail(c, NW_E_STATE, "nothing has run");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    float total = 0.0f, f = 0.0f, w = 0.0f;
+    HIP_OR_FAIL(c, hipEventElapsedTime(&total, c->ev0, c->ev1));
+    if (c->use_stream && c->n > 0) {
+        HIP_OR_FAIL(c, hipEventElapsedTime(&f, c->ev0, c->ev_fill));
+        HIP_OR_FAIL(c, hipEventElapsedTime(&w, c->ev_fill, c->ev_walk));
+    } else {
+        f = total;
+    }
+    if (fill_ms) *fill_ms = f;
+    if (walk_ms) *walk_ms = w;
+    if (rest_ms) *rest_ms = total - f - w;
+    return NW_OK;
+}
+
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
-    const nw::LaunchCfg& k = c->use_pair ? c->pair_cfg : (c->use_band ? c->band_cfg : c->cfg);
+    const nw::LaunchCfg& k = c->use_stream ? c->stream_fill
+                             : (c->use_pair ? c->pair_cfg : (c->use_band ? c->band_cfg : c->cfg));
     if (rows_per_lane) *rows_per_lane = k.R;
     if (waves_per_block) *waves_per_block = k.wpb;
     if (grid) *grid = k.grid;
@@ -479,10 +575,15 @@ int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_pe
 int64_t nw_batch_fallbacks(nw_ctx* c) {
     if (!c || !c->ran) return -1;
     (void)hipSetDevice(c->device);
-    int32_t v = 0;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
-    if (hipMemcpy(&v, c->d_fallback_count.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return (c->use_band || c->use_pair) ? v : 0;
+    if (!(c->use_band || c->use_pair || c->use_stream)) return 0;
+    const int64_t passes = c->use_stream ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
+    std::vector<int32_t> v((size_t)(4 * passes));
+    if (hipMemcpy(v.data(), c->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    int64_t total = 0;
+    for (int64_t q = 0; q < passes; ++q) total += v[(size_t)(4 * q)];
+    return total;
 }
 
 int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, char* aln_out,

@@ -1,0 +1,542 @@
+// nw_stream.hip -- streaming wavefront fill + separate traceback kernel.
+//
+// Same recurrence, tie rules and output as nw_kernel.hip / nw_pair.hip.  The
+// pair kernel pays a 63-column ramp-up/ramp-down per pair of reads (lane l
+// starts l columns after lane 0), ~20 % of its DP steps at 250 bp.  Here the
+// pairs of one wavefront follow each other in a single stream of columns:
+//
+//   * pair q occupies stream columns [S_q, S_q + span_q); both reads are
+//     right-aligned in it (read h starts at column pad_h = span_q - Lb_h), so the
+//     columns before a shorter read are neutral pad columns (see nw_pair.hip:
+//     they leave a lane in the boundary state) and both reads end on the pair's
+//     last column;
+//   * lane l works on stream column T - l at step T; when that column is the
+//     first of its next pair, the lane stores its last-column scores of the
+//     finished pair (the "captures"), resets to the boundary state and loads the
+//     next pair's band geometry -- one event per lane and pair, no ramp;
+//   * the traceback band, the captures and the last amplicon row go to a
+//     per-pair region in HBM (7-16 KB per pair; 288 GB leave room for millions
+//     of pairs), so the fill kernel holds no traceback in LDS and its occupancy
+//     is register-limited;
+//   * nw_stream_walk (one wavefront per read, latency-bound, high occupancy)
+//     finds the start cell, walks the band and writes the strings.  Reads whose
+//     walk leaves the band go to the fallback list of the exact int32 kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nw_common.h"
+
+namespace nw {
+
+namespace {
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_v(unsigned u) { return __builtin_bit_cast(s16x2, u); }
+__device__ __forceinline__ unsigned as_u(s16x2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ unsigned pk(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
+__device__ __forceinline__ int half(unsigned w, int h) { return (int)(short)(w >> (16 * h)); }
+
+__device__ __forceinline__ unsigned dpp_shr1(unsigned old, unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+// d = (a & m) | c as one VOP3 (the compiler prefers and+and+or3 = 3 ops for two terms)
+__device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
+    unsigned d;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(m), "v"(c));
+    return d;
+}
+
+constexpr int kRing = 256;         // staged columns per read (power of two)
+constexpr int kRingAlloc = kRing + 2;
+constexpr int kDescQ = 32;         // pair descriptors per wave (ring)
+constexpr int kStage = 64;         // steps between two staging points
+constexpr int kChunk = 2;          // pairs per dequeue
+
+}  // namespace
+
+// ---- per-pair region in HBM --------------------------------------------------
+__host__ __device__ inline StreamRegion stream_region(int R, int band_slots, int Lb_max) {
+    const int NG = ((R + 3) & ~3) / 4;
+    StreamRegion g;
+    g.bits = 0;
+    g.caps = (int64_t)band_slots * 64 * NG * 4;
+    g.last = g.caps + (int64_t)64 * R * 4;
+    const int64_t span_cap = (Lb_max > kStreamMinSpan ? Lb_max : kStreamMinSpan) + 4;
+    g.stride = (g.last + 4 * span_cap + 255) & ~(int64_t)255;
+    return g;
+}
+
+// Band of a pair in the stream (pair-relative column c, padded row g = ai + F):
+// slot = c - lane * R - dlo.  Returns false when the pair has no read or the
+// band cannot hold both reads' start and end diagonals.
+__host__ __device__ inline bool stream_pair_band(int La, int R, int F, int slots, int LbA, int LbB, int* span,
+                                                 int* dlo) {
+    const int Lmax = LbA > LbB ? LbA : LbB;
+    *span = 0;
+    *dlo = 0;
+    if (Lmax <= 0) return false;
+    const int sp = Lmax > kStreamMinSpan ? Lmax : kStreamMinSpan;
+    int lo = 1 << 30, hi = -(1 << 30);
+    const int Lb[2] = {LbA, LbB};
+    for (int h = 0; h < 2; ++h) {
+        if (Lb[h] <= 0) continue;
+        const int pad = sp - Lb[h];
+        const int a = (Lb[h] - La < 0 ? Lb[h] - La : 0) + pad;
+        const int b = (Lb[h] - La > 0 ? Lb[h] - La : 0) + pad;
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    *span = sp;
+    const int room = slots - (hi - lo) - R;
+    if (room < 0) return false;
+    *dlo = lo - room / 2 - F;
+    return true;
+}
+
+template <int R> struct SGeo {
+    static constexpr int R4 = (R + 3) & ~3;
+    static constexpr int PB = 2 * R4;
+    static constexpr int NG = R4 / 4;
+};
+
+__host__ __device__ inline int stream_shared_bytes(int R) {
+    const int PB = 2 * ((R + 3) & ~3);
+    return align16(NCODE * 64 * PB) + 256;
+}
+__host__ __device__ inline int stream_wave_bytes() {
+    return align16(2 * 2 * kRingAlloc) + kDescQ * 48;
+}
+
+template <class T, int N>
+struct SArr { T v[N]; };
+
+template <int R>
+__device__ __forceinline__ void sload_prof(const unsigned char* p, SArr<unsigned, SGeo<R>::R4 / 2>& out) {
+#pragma unroll
+    for (int q = 0; q < SGeo<R>::R4 / 4; ++q) {
+        const uint2 v = ((const uint2*)p)[q];
+        out.v[2 * q] = v.x;
+        out.v[2 * q + 1] = v.y;
+    }
+}
+
+// ============================================================================
+// Fill: one continuous stream of read pairs per wavefront.
+// ============================================================================
+template <int R>
+__global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
+    constexpr int R4 = SGeo<R>::R4;
+    constexpr int PB = SGeo<R>::PB;
+    constexpr int NG = SGeo<R>::NG;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int La = args.La;
+    const int O = args.gap_open, E = args.gap_extend;
+    const unsigned O2 = pk(O, O), E2 = pk(E, E);
+    const unsigned NEG2 = pk(-16384, -16384);
+    const unsigned MO0 = pk(-O, -O);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+
+    unsigned char* prof_lds = smem;
+    const int prof_bytes = NCODE * 64 * PB;
+    unsigned char* lut_lds = smem + align16(prof_bytes);
+    for (int q = tid; q < prof_bytes / 16; q += blockDim.x) ((int4*)prof_lds)[q] = ((const int4*)args.prof)[q];
+    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
+    __syncthreads();
+
+    unsigned char* wbase = smem + stream_shared_bytes(R) + wave * stream_wave_bytes();
+    unsigned short* ringA = (unsigned short*)wbase;
+    unsigned short* ringB = ringA + kRingAlloc;
+    int4* desc = (int4*)(wbase + align16(2 * 2 * kRingAlloc));   // [kDescQ][3]
+
+    const int slots = args.band_slots;
+    const int nl = (La + R - 1) / R;
+    const int F = nl * R - La;
+    const int lr = nl - 1;
+    const int prof_lane = lane * PB;
+    const unsigned short pad_coff = (unsigned short)(NCODE_PAD * 64 * PB);
+    const long long npairs = (args.n + 1) / 2;
+    const StreamRegion reg = stream_region(R, slots, args.Lb_max);
+    constexpr int BIG = 1 << 29;
+
+    // ---- wave-uniform stream state ----
+    int q_count = 0;           // pairs appended so far
+    int S_tail = 0;            // first stream column after the appended pairs
+    bool exhausted = false;
+    long long cur = 0, cur_end = 0;   // dequeued pair range being appended
+    long long next_chunk = 0;
+    if (lane == 0) next_chunk = atomicAdd(args.work_counter, 1);
+    next_chunk = __shfl(next_chunk, 0, 64);
+
+    // Appends pairs (skipping empty / band-less ones, which the walk kernel
+    // handles) until the stream covers column `need` or the queue is empty.
+    auto append = [&](int need) {
+        while (!exhausted && S_tail <= need) {
+            if (cur >= cur_end) {
+                const long long c0 = next_chunk * kChunk;
+                if (c0 >= npairs) { exhausted = true; break; }
+                cur = c0;
+                cur_end = min(npairs, c0 + kChunk);
+                long long nc = 0;
+                if (lane == 0) nc = atomicAdd(args.work_counter, 1);
+                next_chunk = __shfl(nc, 0, 64);
+            }
+            const long long p = cur++;
+            const long long ra = 2 * p, rb = 2 * p + 1;
+            const long long offA = args.offsets[ra];
+            const int LbA = (int)(args.offsets[ra + 1] - offA);
+            long long offB = 0;
+            int LbB = 0;
+            if (rb < args.n) { offB = args.offsets[rb]; LbB = (int)(args.offsets[rb + 1] - offB); }
+            int span, dlo;
+            if (!stream_pair_band(La, R, F, slots, LbA, LbB, &span, &dlo)) continue;
+            if (lane == 0) {
+                int4* d = desc + (q_count & (kDescQ - 1)) * 3;
+                d[0] = make_int4(S_tail, span, dlo, (int)p);
+                d[1] = make_int4(span - LbA, span - LbB, LbA, LbB);
+                d[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
+            }
+            S_tail += span;
+            ++q_count;
+        }
+        lds_fence();
+    };
+
+    // ---- column staging: read bytes -> profile offsets in the ring ----
+    int sq = 0;                 // pair of this lane's staged column (monotone)
+    unsigned ldA = 0, ldB = 0;  // bytes loaded for the next block
+    auto stage_load = [&](int c0) {
+        const int c = c0 + lane;
+        unsigned vA = 0, vB = 0;
+        if (c < S_tail) {
+            while (sq + 1 < q_count && c >= desc[((sq + 1) & (kDescQ - 1)) * 3].x) ++sq;
+            const int4* d = desc + (sq & (kDescQ - 1)) * 3;
+            const int4 d0 = d[0], d1 = d[1], d2 = d[2];
+            const int jj = c - d0.x;
+            const int jA = jj - d1.x, jB = jj - d1.y;
+            const long long oA = (long long)(((unsigned long long)(unsigned)d2.y << 32) | (unsigned)d2.x);
+            const long long oB = (long long)(((unsigned long long)(unsigned)d2.w << 32) | (unsigned)d2.z);
+            if ((unsigned)jA < (unsigned)d1.z) vA = args.reads[oA + jA];
+            if ((unsigned)jB < (unsigned)d1.w) vB = args.reads[oB + jB];
+        }
+        ldA = vA;
+        ldB = vB;
+    };
+    auto stage_write = [&](int c0) {
+        const int idx = (c0 + lane) & (kRing - 1);
+        const unsigned short oA = (unsigned short)(lut_lds[ldA] * 64 * PB);
+        const unsigned short oB = (unsigned short)(lut_lds[ldB] * 64 * PB);
+        ringA[idx] = oA;
+        ringB[idx] = oB;
+        if (idx < kRingAlloc - kRing) { ringA[kRing + idx] = oA; ringB[kRing + idx] = oB; }
+    };
+
+    // ---- prologue ----
+    for (int q = lane; q < kRingAlloc; q += 64) { ringA[q] = pad_coff; ringB[q] = pad_coff; }
+    append(3 * kStage - 1);
+    if (q_count == 0) return;
+    stage_load(0);
+    stage_write(0);
+    stage_load(kStage);
+    stage_write(kStage);
+    stage_load(2 * kStage);
+    lds_fence();
+
+    // ---- per-lane DP state ----
+    unsigned Mol[R], Xl[R], Hold[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
+    unsigned sMo = MO0, sY = NEG2, sH = 0u;
+    unsigned rMo = MO0, rY = NEG2, rH = 0u;
+    unsigned Htop = 0u;
+    int qi = -1;                   // this lane's pair (count index), -1 before the first
+    int evT = lane;                // step of the next event: first column of the next pair
+    int slot = -BIG;
+    unsigned* bitp = nullptr;      // this lane's (slot 0) traceback word in the pair region
+    // last-row word of the current column (lane lr); before its first pair the
+    // lane writes into the scratch words after the last region
+    unsigned* const lr_dummy = (unsigned*)(args.region + npairs * reg.stride);
+    unsigned* lrp = lr_dummy;
+    unsigned* capp = nullptr;      // this lane's captures in the pair region
+    unsigned char* region = args.region;
+
+    SArr<unsigned, R4 / 2> pa0, pb0, pa1, pb1;
+    sload_prof<R>(prof_lds + ringA[(-lane) & (kRing - 1)] + prof_lane, pa0);
+    sload_prof<R>(prof_lds + ringB[(-lane) & (kRing - 1)] + prof_lane, pb0);
+
+    // byte-plane masks of the sign bits, forced into SGPRs so that each row's
+    // merge is two v_and_or_b32 (VOP3 takes no literal on gfx9)
+    unsigned mT[4], mU[4];
+    asm volatile("s_mov_b32 %0, 0x01010101" : "=s"(mT[0]));
+    asm volatile("s_mov_b32 %0, 0x02020202" : "=s"(mT[1]));
+    asm volatile("s_mov_b32 %0, 0x04040404" : "=s"(mT[2]));
+    asm volatile("s_mov_b32 %0, 0x08080808" : "=s"(mT[3]));
+    asm volatile("s_mov_b32 %0, 0x10101010" : "=s"(mU[0]));
+    asm volatile("s_mov_b32 %0, 0x20202020" : "=s"(mU[1]));
+    asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
+    asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
+
+    auto step = [&](int T, int ridx, const SArr<unsigned, R4 / 2>& pa, const SArr<unsigned, R4 / 2>& pb,
+                    SArr<unsigned, R4 / 2>& pn_a, SArr<unsigned, R4 / 2>& pn_b) {
+        if (T == evT) {
+            // this lane's column is the first of its next pair
+            if (qi >= 0) {
+#pragma unroll
+                for (int k = 0; k < R; ++k) capp[k] = Mol[k];
+            }
+            ++qi;
+            // (every variable assigned on both outcomes: keeps them in registers)
+            const bool more = qi < q_count;
+            const int4 d0 = desc[(qi & (kDescQ - 1)) * 3];
+            unsigned char* base = region + (long long)d0.w * reg.stride;
+            evT = more ? d0.x + d0.y + lane : -1;
+            slot = (more && lane < nl) ? -lane * R - d0.z : -BIG;
+            // word of the current column's slot (dereferenced only while 0 <= slot < slots)
+            bitp = (unsigned*)(base + reg.bits) + lane * NG + (long long)slot * (64 * NG);
+            capp = (unsigned*)(base + reg.caps) + lane * R;
+            lrp = more ? (unsigned*)(base + reg.last) : lr_dummy;
+#pragma unroll
+            for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
+            Htop = 0u;
+        }
+        rMo = dpp_shr1(rMo, sMo);
+        rY = dpp_shr1(rY, sY);
+        rH = dpp_shr1(rH, sH);
+        sload_prof<R>(prof_lds + ringA[ridx] + prof_lane, pn_a);
+        sload_prof<R>(prof_lds + ringB[ridx] + prof_lane, pn_b);
+        unsigned acc[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[g] = 0u;
+        s16x2 Hd = as_v(Htop), Mou = as_v(rMo), Yu = as_v(rY);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
+            const s16x2 sc = as_v(__builtin_amdgcn_perm(pb.v[k >> 1], pa.v[k >> 1], sel));
+            const s16x2 M = Hd + sc;
+            const s16x2 Xe = as_v(Xl[k]) - as_v(E2);
+            const s16x2 X = __builtin_elementwise_max(as_v(Mol[k]), Xe);
+            const s16x2 Ye = Yu - as_v(E2);
+            const s16x2 Y = __builtin_elementwise_max(Mou, Ye);
+            const s16x2 mxy = __builtin_elementwise_max(X, Y);
+            const s16x2 H = __builtin_elementwise_max(M, mxy);
+            const unsigned d1 = as_u(Mou - Ye);
+            const unsigned d2 = as_u(as_v(Mol[k]) - Xe);
+            const unsigned d3 = as_u(Y - X);
+            const unsigned d4 = as_u(mxy - M);
+            const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
+            const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
+            acc[k >> 2] = and_or(tt, mT[k & 3], acc[k >> 2]);
+            acc[k >> 2] = and_or(uu, mU[k & 3], acc[k >> 2]);
+            const s16x2 Mo = M - as_v(O2);
+            Hd = as_v(Hold[k]);
+            Hold[k] = as_u(H);
+            Mol[k] = as_u(Mo);
+            Xl[k] = as_u(X);
+            Mou = Mo;
+            Yu = Y;
+        }
+        sMo = as_u(Mou);
+        sY = as_u(Yu);
+        sH = Hold[R - 1];
+        if ((unsigned)slot < (unsigned)slots) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) bitp[g] = acc[g];
+        }
+        ++slot;
+        bitp += 64 * NG;
+        if (lane == lr) { *lrp = sMo; ++lrp; }
+        Htop = rH;
+    };
+
+    int T = 0;
+    for (;;) {
+        if (T > 0) {
+            append(T + 3 * kStage - 1);
+            stage_write(T + kStage);
+            stage_load(T + 2 * kStage);
+        }
+        const int Tend = exhausted ? S_tail + lr : (1 << 30);
+        const int nb = min(kStage, Tend - T + 1);
+        int u = 0;
+        for (; u + 1 < nb; u += 2) {
+            const int ridx = (T + u + 1 - lane) & (kRing - 1);
+            step(T + u, ridx, pa0, pb0, pa1, pb1);
+            step(T + u + 1, ridx + 1, pa1, pb1, pa0, pb0);
+        }
+        if (u < nb) {
+            step(T + u, (T + u + 1 - lane) & (kRing - 1), pa0, pb0, pa1, pb1);
+            break;   // nb odd only at the end of the stream
+        }
+        T += kStage;
+        if (T > Tend) break;
+    }
+}
+
+// ============================================================================
+// Walk + emit: one wavefront per read.
+// ============================================================================
+template <int R>
+__global__ __launch_bounds__(256) void nw_stream_walk(const KernelArgs args) {
+    constexpr int R4 = SGeo<R>::R4;
+    constexpr int NG = SGeo<R>::NG;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int La = args.La;
+    const int O = args.gap_open;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wpb = blockDim.x >> 6;
+    unsigned char* lut_lds = smem;
+    unsigned char* amp_lds = smem + 256;
+    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
+    for (int q = tid; q < La; q += blockDim.x) amp_lds[q] = args.amp[q];
+    __syncthreads();
+    unsigned* runs = (unsigned*)(smem + stream_walk_shared_bytes(La) + wave * kStreamRunsCap * 4);
+
+    const int slots = args.band_slots;
+    const int nl = (La + R - 1) / R;
+    const int F = nl * R - La;
+    const StreamRegion reg = stream_region(R, slots, args.Lb_max);
+    const short* prof16 = (const short*)args.prof;
+
+    for (long long rd = (long long)blockIdx.x * wpb + wave; rd < args.n; rd += (long long)gridDim.x * wpb) {
+        const long long p = rd >> 1;
+        const int h = (int)(rd & 1);
+        const long long ra = 2 * p, rb = 2 * p + 1;
+        const int LbA = (int)(args.offsets[ra + 1] - args.offsets[ra]);
+        const int LbB = rb < args.n ? (int)(args.offsets[rb + 1] - args.offsets[rb]) : 0;
+        const int Lb = h ? LbB : LbA;
+        if (Lb <= 0) {
+            if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; args.stats[rd] = z; }
+            continue;
+        }
+        int span, dlo;
+        if (!stream_pair_band(La, R, F, slots, LbA, LbB, &span, &dlo)) {
+            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+            continue;
+        }
+        const int pad = span - Lb;
+        const unsigned char* base = args.region + p * reg.stride;
+        const unsigned* bits = (const unsigned*)(base + reg.bits);
+        const unsigned* caps = (const unsigned*)(base + reg.caps);
+        const unsigned* last = (const unsigned*)(base + reg.last);
+
+        // ---- start cell ----
+        long long key = -0x7fffffffffffffffll - 1;
+        if (lane < nl) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int ai = lane * R + k - F;
+                if (ai >= 0) {
+                    const int v = half(caps[lane * R + k], h) + O;
+                    const long long kk = (ai == La - 1) ? end_key(v, 3, 0) : end_key(v, 2, ai);
+                    key = kk > key ? kk : key;
+                }
+            }
+        }
+        for (int q = lane; q < Lb - 1; q += 64) {
+            const long long kk = end_key(half(last[pad + q], h) + O, 1, q);
+            key = kk > key ? kk : key;
+        }
+        key = wave_max_i64(key);
+        int score, ei, ej;
+        decode_end(key, La, Lb, &score, &ei, &ej);
+        if (args.debug_mode == 1) {
+            if (lane == 0) { Stat z = {}; z.score = score; z.end_i = ei; z.end_j = ej; args.stats[rd] = z; }
+            continue;
+        }
+
+        // ---- walk ----
+        auto nib = [&](int ai, int bjj, bool* oob) -> unsigned {
+            const int g = ai + F;
+            const int ln = g / R, k = g - ln * R;
+            const int s = bjj + pad - ln * R - dlo;
+            if ((unsigned)s >= (unsigned)slots) { *oob = true; return 0u; }
+            *oob = false;
+            const unsigned w = bits[((size_t)s * 64 + ln) * NG + (k >> 2)];
+            const int kk = k & 3;
+            const int hb = 8 * h + kk, lb = 8 * h + 4 + kk;
+            const unsigned yext = (w >> hb) & 1u, bX = (w >> lb) & 1u;
+            const unsigned xext = (w >> (16 + hb)) & 1u, bM = (w >> (16 + lb)) & 1u;
+            return bM | (bX << 1) | (xext << 2) | (yext << 3);
+        };
+        const int nruns = walk_runs(nib, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        if (nruns < 0) {
+            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+            continue;
+        }
+        lds_fence();
+        if (args.debug_mode == 2) {
+            if (lane == 0) { Stat z = {}; z.score = score; z.aln_len = nruns; args.stats[rd] = z; }
+            continue;
+        }
+        auto sim = [&](int ai, int code) {
+            const int g = ai + F;
+            return (int)prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R];
+        };
+        const long long off = args.offsets[rd];
+        emit_alignment(runs, nruns, amp_lds, args.reads + off, lut_lds, sim, args.out + rd * 3 * args.stride,
+                       args.stride, score, ei, ej, args.stats + rd, lane);
+        lds_fence();
+    }
+}
+
+// ---- host-side helpers ----
+
+int stream_fill_lds_bytes(int R, int wpb) { return stream_shared_bytes(R) + wpb * stream_wave_bytes(); }
+int stream_walk_lds_bytes(int La, int wpb) { return stream_walk_shared_bytes(La) + wpb * kStreamRunsCap * 4; }
+StreamRegion stream_region_for(int R, int band_slots, int Lb_max) { return stream_region(R, band_slots, Lb_max); }
+
+template <int R>
+static hipError_t launch_stream_r(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+                                  hipEvent_t after_fill) {
+    hipLaunchKernelGGL((nw_stream_fill<R>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL((nw_stream_walk<R>), dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+template <int R>
+static hipError_t occupancy_r(int* fill_blocks, int* walk_blocks, int fill_lds, int walk_lds, int wpb) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(fill_blocks, nw_stream_fill<R>, 64 * wpb, fill_lds);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_stream_walk<R>, 64 * wpb, walk_lds);
+}
+
+#define NW_STREAM_DISPATCH(R_, CALL) \
+    switch (R_) {                    \
+        case 1: return CALL(1);      \
+        case 2: return CALL(2);      \
+        case 3: return CALL(3);      \
+        case 4: return CALL(4);      \
+        case 5: return CALL(5);      \
+        case 6: return CALL(6);      \
+        case 7: return CALL(7);      \
+        case 8: return CALL(8);      \
+        case 10: return CALL(10);    \
+        case 12: return CALL(12);    \
+        case 14: return CALL(14);    \
+        case 16: return CALL(16);    \
+        default: return hipErrorInvalidValue; \
+    }
+
+hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+                         hipEvent_t after_fill) {
+#define CALL_(r) launch_stream_r<r>(a, fill, walk, s, after_fill)
+    NW_STREAM_DISPATCH(fill.R, CALL_)
+#undef CALL_
+}
+
+hipError_t stream_occupancy(int R, int wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks) {
+#define CALL_(r) occupancy_r<r>(fill_blocks, walk_blocks, fill_lds, walk_lds, wpb)
+    NW_STREAM_DISPATCH(R, CALL_)
+#undef CALL_
+}
+
+}  // namespace nw

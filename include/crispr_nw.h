@@ -106,12 +106,19 @@ int64_t nw_batch_cells(const nw_ctx* ctx);
 /* Launch geometry of the kernel that aligns the bulk of the batch: rows per
  * lane, waves per block, grid, LDS bytes per block, traceback storage
  * (0 = full in LDS, 1 = full in a global slab, 2 = diagonal band in LDS,
- * 3 = diagonal band in LDS, two reads per wavefront in packed int16). */
+ * 3 = diagonal band in LDS, two reads per wavefront in packed int16,
+ * 4 = streaming fill, two reads per wavefront in packed int16, diagonal band
+ * in HBM + a separate traceback kernel). */
 int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
                       int32_t* grid, int32_t* lds_bytes, int32_t* tb_mode);
 /* Reads of the last run whose traceback left the diagonal band and were
  * re-aligned with full traceback storage (synchronises). */
 int64_t nw_batch_fallbacks(nw_ctx* ctx);
+/* Device time of the last run split by kernel (synchronises): the DP fill,
+ * the traceback/emit kernel and the rest (fallback kernel, memsets).  With the
+ * non-streaming kernels everything is reported as fill.  For batches split
+ * into several passes the first two cover the first pass only. */
+int nw_batch_kernel_times(nw_ctx* ctx, float* fill_ms, float* walk_ms, float* rest_ms);
 
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated

@@ -12,7 +12,8 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["pair", "band", "full"]
+KERNELS = ["stream", "pair", "band", "full"]
+BANDED = {"stream": "stream-int16", "pair": "pair-band-int16"}
 
 
 @pytest.fixture(params=KERNELS)
@@ -121,9 +122,11 @@ def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle, kernel):
     assert_same(oracle, amp2, buf, off, a.align_packed(buf, off), "switch-ref")
 
 
-def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch):
+@pytest.mark.parametrize("family", sorted(BANDED))
+def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
     """Reads whose traceback leaves the diagonal band (large indels, shifted
     reads) are re-run with full storage; results stay bit-identical."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", family)
     amp = synth.random_amplicon(250, 1)
     rng = np.random.Generator(np.random.PCG64(33))
     reads = []
@@ -139,7 +142,7 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == "pair-band-int16"
+    assert a.geometry()["tb_mode"] == BANDED[family]
     assert a.fallbacks() >= 6
     assert_same(oracle, amp, buf, off, batch, "band-fallback")
 
@@ -153,12 +156,14 @@ def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "pair-band-int16")
+    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "stream-int16")
     assert_same(oracle, amp, buf, off, batch, f"slots={slots}")
 
 
-def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle):
-    """Pair kernel: partners of different lengths, empty partners, odd batch size."""
+@pytest.mark.parametrize("family", sorted(BANDED))
+def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle, monkeypatch, family):
+    """Packed kernels: partners of different lengths, empty partners, odd batch size."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", family)
     amp = synth.random_amplicon(230, 41)
     rng = np.random.Generator(np.random.PCG64(41))
     reads = []
@@ -171,8 +176,75 @@ def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == "pair-band-int16"
+    assert a.geometry()["tb_mode"] == BANDED[family]
     assert_same(oracle, amp, buf, off, batch, "pairs")
+
+
+def _mixed_lengths(amp, n, seed):
+    """Reads of every length class: tiny (< the stream's minimum pair span),
+    short, full, longer than the amplicon, empty; exact copies and variants."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    La = len(amp)
+    reads = []
+    for k in range(n):
+        u = rng.random()
+        if u < 0.15:
+            L = int(rng.integers(1, 16))
+        elif u < 0.25:
+            L = 0
+        elif u < 0.6:
+            L = int(rng.integers(16, La))
+        else:
+            L = int(rng.integers(La - 5, La + 40))
+        s = int(rng.integers(0, max(1, La - L)))
+        r = amp[s:s + L] if rng.random() < 0.6 else synth.random_amplicon(max(L, 1), seed * 7919 + k)[:L]
+        reads.append(r)
+    return reads
+
+
+@pytest.mark.parametrize("grid", ["1", "3"])
+def test_stream_long_streams(gpu_aligner_factory, oracle, monkeypatch, grid):
+    """Stream kernel with a tiny grid: every wavefront streams hundreds of pairs
+    back to back (descriptor ring wrap, column ring wrap, chunk refills, pairs
+    of every length class including those shorter than the minimum span)."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
+    monkeypatch.setenv("CRISPR_NW_STREAM_GRID", grid)
+    amp = synth.random_amplicon(250, 5)
+    reads = _mixed_lengths(amp, 1500, 5)
+    sub, soff = synth.reads_from(amp, 1500, 6, synth.PARITY_MIX)
+    reads += synth.unpack(sub, soff)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "stream-int16"
+    assert_same(oracle, amp, buf, off, batch, f"stream grid={grid}")
+
+
+@pytest.mark.parametrize("La", [31, 100, 250, 500])
+def test_stream_mixed_lengths(gpu_aligner_factory, oracle, monkeypatch, La):
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
+    monkeypatch.setenv("CRISPR_NW_STREAM_GRID", "2")
+    amp = synth.random_amplicon(La, 300 + La)
+    reads = _mixed_lengths(amp, 400, La)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"stream La={La}")
+
+
+def test_stream_multiple_passes(gpu_aligner_factory, oracle, monkeypatch):
+    """A region budget smaller than the batch splits it into several fill+walk passes."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
+    monkeypatch.setenv("CRISPR_NW_REGION_MB", "2")      # ~120 pairs per pass at 250 bp
+    amp = synth.random_amplicon(250, 8)
+    buf, off = synth.reads_from(amp, 1001, 9, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert_same(oracle, amp, buf, off, batch, "passes")
+    t = a.kernel_times()
+    assert t["fill_ms"] > 0 and t["walk_ms"] > 0 and t["rest_ms"] >= 0
 
 
 def test_needle_cli_matches_oracle_cli(tmp_path, oracle):
