@@ -73,7 +73,8 @@ hipError_t launch_pair(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 // streaming fill + walk kernels (nw_stream.hip).  Pair p's region starts at
 // region + p * stride: traceback band [slots][64 lanes][NG] words, captures
 // (last-column Mo) [64 lanes][R], last amplicon row Mo [span] (both reads packed).
-constexpr int kStreamMinSpan = 16;   // stream columns per pair at least (bounds live descriptors)
+constexpr int kStreamMinSpan = 64;   // stream columns per pair at least: at most one pair change per
+                                     // lane per 64-step block, few live descriptors
 constexpr int kStreamRunsCap = 512;  // traceback runs per read kept in LDS
 struct StreamRegion {
     int64_t bits, caps, last, stride;

@@ -50,7 +50,7 @@ __device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
 
 constexpr int kRing = 256;         // staged columns per read (power of two)
 constexpr int kRingAlloc = kRing + 2;
-constexpr int kDescQ = 32;         // pair descriptors per wave (ring)
+constexpr int kDescQ = 16;         // pair descriptors per wave (ring)
 constexpr int kStage = 64;         // steps between two staging points
 constexpr int kChunk = 2;          // pairs per dequeue
 
@@ -253,16 +253,38 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
     unsigned sMo = MO0, sY = NEG2, sH = 0u;
     unsigned rMo = MO0, rY = NEG2, rH = 0u;
     unsigned Htop = 0u;
-    int qi = -1;                   // this lane's pair (count index), -1 before the first
-    int evT = lane;                // step of the next event: first column of the next pair
-    int slot = -BIG;
-    unsigned* bitp = nullptr;      // this lane's (slot 0) traceback word in the pair region
-    // last-row word of the current column (lane lr); before its first pair the
-    // lane writes into the scratch words after the last region
-    unsigned* const lr_dummy = (unsigned*)(args.region + npairs * reg.stride);
-    unsigned* lrp = lr_dummy;
-    unsigned* capp = nullptr;      // this lane's captures in the pair region
+    // Pair changes.  evT = step at which this lane's column is the first of its
+    // next pair.  The next pair's pointers (n_*) are prepared for all lanes at
+    // once at the staging point before that step (one change per lane and
+    // 64-step block, span >= 64), so the change itself is a capture store,
+    // register moves and the reset.  Before the first pair and after the last
+    // one the captures / last row go to scratch words after the last region.
     unsigned char* region = args.region;
+    unsigned* const lr_dummy = (unsigned*)(args.region + npairs * reg.stride);
+    unsigned* const caps_dummy = lr_dummy + 256;
+    int qi = -1;                   // this lane's latest prepared pair (count index)
+    int evT = lane;
+    int slot = -BIG;
+    unsigned* bitp = nullptr;      // band word of the current column (used while 0 <= slot < slots)
+    unsigned* lrp = lr_dummy;      // last-row word of the current column (lane lr)
+    unsigned* capp = caps_dummy;   // this lane's captures
+    int n_evT = -1, n_slot = -BIG;
+    unsigned *n_bitp = nullptr, *n_lrp = lr_dummy, *n_capp = caps_dummy;
+    auto prep_events = [&](int T0) {
+        if (evT >= T0 && evT < T0 + kStage) {
+            const int q = qi + 1;
+            const bool more = q < q_count;
+            const int4 d0 = desc[(q & (kDescQ - 1)) * 3];
+            unsigned char* base = region + (long long)d0.w * reg.stride;
+            n_evT = more ? d0.x + d0.y + lane : -1;
+            n_slot = (more && lane < nl) ? -lane * R - d0.z : -BIG;
+            n_bitp = (unsigned*)(base + reg.bits) + lane * NG + (long long)n_slot * (64 * NG);
+            n_capp = more ? (unsigned*)(base + reg.caps) + lane * R : caps_dummy;
+            n_lrp = more ? (unsigned*)(base + reg.last) : lr_dummy;
+            qi = q;
+        }
+    };
+    prep_events(0);
 
     SArr<unsigned, R4 / 2> pa0, pb0, pa1, pb1;
     sload_prof<R>(prof_lds + ringA[(-lane) & (kRing - 1)] + prof_lane, pa0);
@@ -284,21 +306,13 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
                     SArr<unsigned, R4 / 2>& pn_a, SArr<unsigned, R4 / 2>& pn_b) {
         if (T == evT) {
             // this lane's column is the first of its next pair
-            if (qi >= 0) {
 #pragma unroll
-                for (int k = 0; k < R; ++k) capp[k] = Mol[k];
-            }
-            ++qi;
-            // (every variable assigned on both outcomes: keeps them in registers)
-            const bool more = qi < q_count;
-            const int4 d0 = desc[(qi & (kDescQ - 1)) * 3];
-            unsigned char* base = region + (long long)d0.w * reg.stride;
-            evT = more ? d0.x + d0.y + lane : -1;
-            slot = (more && lane < nl) ? -lane * R - d0.z : -BIG;
-            // word of the current column's slot (dereferenced only while 0 <= slot < slots)
-            bitp = (unsigned*)(base + reg.bits) + lane * NG + (long long)slot * (64 * NG);
-            capp = (unsigned*)(base + reg.caps) + lane * R;
-            lrp = more ? (unsigned*)(base + reg.last) : lr_dummy;
+            for (int k = 0; k < R; ++k) capp[k] = Mol[k];
+            evT = n_evT;
+            slot = n_slot;
+            bitp = n_bitp;
+            capp = n_capp;
+            lrp = n_lrp;
 #pragma unroll
             for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
             Htop = 0u;
@@ -358,6 +372,7 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
             append(T + 3 * kStage - 1);
             stage_write(T + kStage);
             stage_load(T + 2 * kStage);
+            prep_events(T);
         }
         const int Tend = exhausted ? S_tail + lr : (1 << 30);
         const int nb = min(kStage, Tend - T + 1);
