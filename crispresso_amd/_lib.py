@@ -14,7 +14,8 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_void_p
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libcrispr_nw.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                        os.environ.get("CRISPR_NW_LIB", "libcrispr_nw.so"))   # variant builds (experiments)
 
 NW_OK = 0
 NW_E_INVALID = -1

@@ -44,6 +44,11 @@ struct KernelArgs {
     int32_t* work_counter;     // dynamic chunk queue of the pair/stream kernels (zeroed per run)
     // streaming kernels: per-pair traceback regions in HBM (StreamRegion layout)
     uint8_t* region;
+    // pair-code score table (R <= 4): [36 code pairs][64 lanes][4 rows] packed
+    // int16x2 (read A's score low, read B's high) over the codes A T G C N and
+    // pad/unknown; null = per-read profile (any alphabet)
+    const uint32_t* ptab;
+    const uint8_t* lut6;       // [256] ascii -> 0..5 in that order, 6 = not in the table
 };
 
 // Traceback storage of a kernel instantiation.
@@ -77,15 +82,18 @@ constexpr int kStreamMinSpan = 64;   // stream columns per pair at least: at mos
                                      // lane per 64-step block, few live descriptors
 constexpr int kStreamRunsCap = 512;  // traceback runs per read kept in LDS
 struct StreamRegion {
-    int64_t bits, caps, last, stride;
+    int64_t bits, caps, last, flags, stride;
 };
+constexpr int kPairCodes = 6;        // pair-table alphabet: A T G C N pad
+enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // read has a code outside the pair table
 __host__ __device__ inline int stream_walk_shared_bytes(int La) { return ((256 + La + 16) + 15) & ~15; }
-int stream_fill_lds_bytes(int R, int wpb);
+int stream_fill_lds_bytes(int R, bool pair_table, int wpb);
 int stream_walk_lds_bytes(int La, int wpb);
 StreamRegion stream_region_for(int R, int band_slots, int Lb_max);
 // `after_fill` (may be null) is recorded between the two kernels.
 hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                          hipEvent_t after_fill);
-hipError_t stream_occupancy(int R, int wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks);
+hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds,
+                            int* fill_blocks, int* walk_blocks);
 
 }  // namespace nw

@@ -88,6 +88,9 @@ struct nw_ctx {
     int R = 0;
     DevBuf<int8_t> d_prof;
     DevBuf<int16_t> d_prof16;         // pair kernel: int16, rows padded on top
+    DevBuf<uint32_t> d_ptab;          // stream kernel: pair-code score table (R <= 4)
+    DevBuf<uint8_t> d_lut6;
+    bool have_ptab = false;
     DevBuf<uint8_t> d_lut, d_amp;
     // batch
     int64_t n = 0;
@@ -163,6 +166,36 @@ int build_profile(nw_ctx* c) {
             int s = (ca < 16 && code < 16) ? kEdna[ca][code] * c->scale : 0;
             prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
         }
+    }
+    // pair-code table of the stream kernel: for every (code of read A, code of
+    // read B) over A T G C N pad, each lane's 4 rows as packed int16x2
+    c->have_ptab = false;
+    if (R4 == 4) {
+        const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+        std::vector<uint32_t> ptab((size_t)nw::kPairCodes * nw::kPairCodes * 64 * 4, 0u);
+        for (int ia = 0; ia < nw::kPairCodes; ++ia)
+            for (int ib = 0; ib < nw::kPairCodes; ++ib)
+                for (int ln = 0; ln < 64; ++ln)
+                    for (int k = 0; k < 4; ++k) {
+                        const size_t src = (size_t)ln * R4 + k;
+                        const uint16_t sa = (uint16_t)prof16[(size_t)codes[ia] * 64 * R4 + src];
+                        const uint16_t sb = (uint16_t)prof16[(size_t)codes[ib] * 64 * R4 + src];
+                        ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
+                    }
+        uint8_t lut6[256];
+        for (int q = 0; q < 256; ++q) {
+            const int code = code_of((unsigned char)q);
+            int r = nw::kPairCodes;   // not in the table
+            for (int i = 0; i < nw::kPairCodes; ++i)
+                if (codes[i] == code) r = i;
+            lut6[q] = (uint8_t)r;
+        }
+        HIP_OR_FAIL(c, c->d_ptab.reserve(ptab.size()));
+        HIP_OR_FAIL(c, c->d_lut6.reserve(256));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_ptab.p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut6.p, lut6, 256, hipMemcpyHostToDevice, c->stream));
+        const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
+        c->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
     }
     HIP_OR_FAIL(c, c->d_prof16.reserve(prof16.size()));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16.p, prof16.data(), prof16.size() * 2, hipMemcpyHostToDevice, c->stream));
@@ -258,11 +291,17 @@ int configure(nw_ctx* c) {
         nw::LaunchCfg f{}, w{};
         f.R = w.R = R;
         f.tb_mode = w.tb_mode = nw::TB_STREAM;
-        f.wpb = w.wpb = 4;
-        f.lds_bytes = nw::stream_fill_lds_bytes(R, f.wpb);
+        // fill: waves per block that maximise resident waves (the pair table is
+        // 36 KB of LDS per block, so bigger blocks share it among more waves)
+        w.wpb = 4;
         w.lds_bytes = nw::stream_walk_lds_bytes(La, w.wpb);
-        int fb = 0, wb = 0;
-        HIP_OR_FAIL(c, nw::stream_occupancy(R, f.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb));
+        int fb = 0, wb = 0, best = -1;
+        for (int wpb : {4, 8, 10}) {
+            const int lds = nw::stream_fill_lds_bytes(R, c->have_ptab, wpb);
+            int b = 0, wb2 = 0;
+            HIP_OR_FAIL(c, nw::stream_occupancy(R, c->have_ptab, wpb, w.wpb, lds, w.lds_bytes, &b, &wb2));
+            if (b * wpb > best) { best = b * wpb; fb = b; wb = wb2; f.wpb = wpb; f.lds_bytes = lds; }
+        }
         if (fb > 0 && wb > 0) {
             const int64_t pairs = (c->n + 1) / 2;
             f.grid = (int)std::max<int64_t>(1, std::min<int64_t>((pairs + f.wpb - 1) / f.wpb, (int64_t)c->num_cus * fb));
@@ -321,6 +360,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
     c->d_prof16.release(); c->d_fallback.release(); c->d_fallback_count.release();
+    c->d_ptab.release(); c->d_lut6.release();
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -426,6 +466,8 @@ int nw_batch_run_async(nw_ctx* c) {
     a.offsets = c->d_offsets.p;
     a.n = c->n;
     a.prof = c->d_prof.p;
+    a.ptab = nullptr;
+    a.lut6 = nullptr;
     a.lut = c->d_lut.p;
     a.amp = c->d_amp.p;
     a.La = (int32_t)c->ref.size();
@@ -456,6 +498,8 @@ int nw_batch_run_async(nw_ctx* c) {
             ap.prof = (const int8_t*)c->d_prof16.p;
             ap.band_slots = c->stream_slots;
             ap.region = c->d_region.p;
+            ap.ptab = c->have_ptab ? c->d_ptab.p : nullptr;
+            ap.lut6 = c->d_lut6.p;
             ap.fallback_list = c->d_fallback.p + lo;
             ap.fallback_count = c->d_fallback_count.p + 4 * q;
             ap.work_counter = ap.fallback_count + 1;

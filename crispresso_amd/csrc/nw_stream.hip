@@ -26,6 +26,10 @@
 
 #include "nw_common.h"
 
+#ifndef NW_FILL_WAVES_PER_SIMD
+#define NW_FILL_WAVES_PER_SIMD 5   // register budget of the fill kernel (occupancy)
+#endif
+
 namespace nw {
 
 namespace {
@@ -64,7 +68,8 @@ __host__ __device__ inline StreamRegion stream_region(int R, int band_slots, int
     g.caps = (int64_t)band_slots * 64 * NG * 4;
     g.last = g.caps + (int64_t)64 * R * 4;
     const int64_t span_cap = (Lb_max > kStreamMinSpan ? Lb_max : kStreamMinSpan) + 4;
-    g.stride = (g.last + 4 * span_cap + 255) & ~(int64_t)255;
+    g.flags = g.last + 4 * span_cap;
+    g.stride = (g.flags + 4 + 255) & ~(int64_t)255;
     return g;
 }
 
@@ -101,9 +106,9 @@ template <int R> struct SGeo {
     static constexpr int NG = R4 / 4;
 };
 
-__host__ __device__ inline int stream_shared_bytes(int R) {
+__host__ __device__ inline int stream_shared_bytes(int R, bool PT) {
     const int PB = 2 * ((R + 3) & ~3);
-    return align16(NCODE * 64 * PB) + 256;
+    return PT ? kPairCodes * kPairCodes * 64 * 16 + 256 : align16(NCODE * 64 * PB) + 256;
 }
 __host__ __device__ inline int stream_wave_bytes() {
     return align16(2 * 2 * kRingAlloc) + kDescQ * 48;
@@ -125,11 +130,16 @@ __device__ __forceinline__ void sload_prof(const unsigned char* p, SArr<unsigned
 // ============================================================================
 // Fill: one continuous stream of read pairs per wavefront.
 // ============================================================================
-template <int R>
-__global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
+// PT: scores from the pair-code table (one ds_read_b128 per column gives the
+// packed scores of both reads for the lane's 4 rows) instead of two per-read
+// profile rows merged with v_perm.
+template <int R, bool PT>
+__global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(const KernelArgs args) {
+    static_assert(!PT || R <= 4, "pair table holds 4 rows per lane");
     constexpr int R4 = SGeo<R>::R4;
     constexpr int PB = SGeo<R>::PB;
     constexpr int NG = SGeo<R>::NG;
+    constexpr int LB = PT ? 16 : PB;    // score bytes per lane and column code
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int La = args.La;
@@ -142,13 +152,14 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
     const int wave = tid >> 6;
 
     unsigned char* prof_lds = smem;
-    const int prof_bytes = NCODE * 64 * PB;
+    const int prof_bytes = PT ? kPairCodes * kPairCodes * 64 * 16 : NCODE * 64 * PB;
     unsigned char* lut_lds = smem + align16(prof_bytes);
-    for (int q = tid; q < prof_bytes / 16; q += blockDim.x) ((int4*)prof_lds)[q] = ((const int4*)args.prof)[q];
-    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
+    const int4* prof_src = PT ? (const int4*)args.ptab : (const int4*)args.prof;
+    for (int q = tid; q < prof_bytes / 16; q += blockDim.x) ((int4*)prof_lds)[q] = prof_src[q];
+    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = PT ? args.lut6[q] : args.lut[q];
     __syncthreads();
 
-    unsigned char* wbase = smem + stream_shared_bytes(R) + wave * stream_wave_bytes();
+    unsigned char* wbase = smem + stream_shared_bytes(R, PT) + wave * stream_wave_bytes();
     unsigned short* ringA = (unsigned short*)wbase;
     unsigned short* ringB = ringA + kRingAlloc;
     int4* desc = (int4*)(wbase + align16(2 * 2 * kRingAlloc));   // [kDescQ][3]
@@ -157,8 +168,9 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
     const int nl = (La + R - 1) / R;
     const int F = nl * R - La;
     const int lr = nl - 1;
-    const int prof_lane = lane * PB;
-    const unsigned short pad_coff = (unsigned short)(NCODE_PAD * 64 * PB);
+    const int prof_lane = lane * LB;
+    const unsigned short pad_coff = (unsigned short)(PT ? (kPairCodes * kPairCodes - 1) * 64 * 16
+                                                         : NCODE_PAD * 64 * PB);
     const long long npairs = (args.n + 1) / 2;
     const StreamRegion reg = stream_region(R, slots, args.Lb_max);
     constexpr int BIG = 1 << 29;
@@ -194,6 +206,7 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
             if (rb < args.n) { offB = args.offsets[rb]; LbB = (int)(args.offsets[rb + 1] - offB); }
             int span, dlo;
             if (!stream_pair_band(La, R, F, slots, LbA, LbB, &span, &dlo)) continue;
+            if (PT && lane == 0) *(int*)(args.region + p * reg.stride + reg.flags) = 0;
             if (lane == 0) {
                 int4* d = desc + (q_count & (kDescQ - 1)) * 3;
                 d[0] = make_int4(S_tail, span, dlo, (int)p);
@@ -203,15 +216,21 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
             S_tail += span;
             ++q_count;
         }
+        // the stream state is wave-uniform: keep it in SGPRs
+        S_tail = __builtin_amdgcn_readfirstlane(S_tail);
+        q_count = __builtin_amdgcn_readfirstlane(q_count);
+        exhausted = __builtin_amdgcn_readfirstlane((int)exhausted) != 0;
         lds_fence();
     };
 
     // ---- column staging: read bytes -> profile offsets in the ring ----
     int sq = 0;                 // pair of this lane's staged column (monotone)
     unsigned ldA = 0, ldB = 0;  // bytes loaded for the next block
+    int ldP = -1;               // their pair (PT: flagged when a byte is outside the table)
     auto stage_load = [&](int c0) {
         const int c = c0 + lane;
         unsigned vA = 0, vB = 0;
+        ldP = -1;
         if (c < S_tail) {
             while (sq + 1 < q_count && c >= desc[((sq + 1) & (kDescQ - 1)) * 3].x) ++sq;
             const int4* d = desc + (sq & (kDescQ - 1)) * 3;
@@ -222,17 +241,32 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
             const long long oB = (long long)(((unsigned long long)(unsigned)d2.w << 32) | (unsigned)d2.z);
             if ((unsigned)jA < (unsigned)d1.z) vA = args.reads[oA + jA];
             if ((unsigned)jB < (unsigned)d1.w) vB = args.reads[oB + jB];
+            ldP = d0.w;
         }
         ldA = vA;
         ldB = vB;
     };
     auto stage_write = [&](int c0) {
         const int idx = (c0 + lane) & (kRing - 1);
-        const unsigned short oA = (unsigned short)(lut_lds[ldA] * 64 * PB);
-        const unsigned short oB = (unsigned short)(lut_lds[ldB] * 64 * PB);
-        ringA[idx] = oA;
-        ringB[idx] = oB;
-        if (idx < kRingAlloc - kRing) { ringA[kRing + idx] = oA; ringB[kRing + idx] = oB; }
+        if constexpr (PT) {
+            int ca = lut_lds[ldA], cb = lut_lds[ldB];
+            if (ca >= kPairCodes || cb >= kPairCodes) {
+                // a code the table does not hold: the read goes to the exact fallback
+                atomicOr((int*)(args.region + (long long)ldP * reg.stride + reg.flags),
+                         (ca >= kPairCodes ? REGION_BAD_A : 0) | (cb >= kPairCodes ? REGION_BAD_B : 0));
+                ca = ca >= kPairCodes ? kPairCodes - 1 : ca;
+                cb = cb >= kPairCodes ? kPairCodes - 1 : cb;
+            }
+            const unsigned short o = (unsigned short)((ca * kPairCodes + cb) * 64 * 16);
+            ringA[idx] = o;
+            if (idx < kRingAlloc - kRing) ringA[kRing + idx] = o;
+        } else {
+            const unsigned short oA = (unsigned short)(lut_lds[ldA] * 64 * PB);
+            const unsigned short oB = (unsigned short)(lut_lds[ldB] * 64 * PB);
+            ringA[idx] = oA;
+            ringB[idx] = oB;
+            if (idx < kRingAlloc - kRing) { ringA[kRing + idx] = oA; ringB[kRing + idx] = oB; }
+        }
     };
 
     // ---- prologue ----
@@ -286,9 +320,21 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
     };
     prep_events(0);
 
-    SArr<unsigned, R4 / 2> pa0, pb0, pa1, pb1;
-    sload_prof<R>(prof_lds + ringA[(-lane) & (kRing - 1)] + prof_lane, pa0);
-    sload_prof<R>(prof_lds + ringB[(-lane) & (kRing - 1)] + prof_lane, pb0);
+    // scores of the next column: PT -> 4 packed dwords in pa; else each read's
+    // R4 int16 profile scores in pa / pb
+    constexpr int SN = PT ? R4 : R4 / 2;
+    using Buf = SArr<unsigned, SN>;
+    auto load_scores = [&](int ridx, Buf& oa, Buf& ob) {
+        if constexpr (PT) {
+            const uint4 v = *(const uint4*)(prof_lds + ringA[ridx] + prof_lane);
+            oa.v[0] = v.x; oa.v[1] = v.y; oa.v[2] = v.z; oa.v[3] = v.w;
+        } else {
+            sload_prof<R>(prof_lds + ringA[ridx] + prof_lane, *(SArr<unsigned, R4 / 2>*)&oa);
+            sload_prof<R>(prof_lds + ringB[ridx] + prof_lane, *(SArr<unsigned, R4 / 2>*)&ob);
+        }
+    };
+    Buf pa0, pb0, pa1, pb1;
+    load_scores((-lane) & (kRing - 1), pa0, pb0);
 
     // byte-plane masks of the sign bits, forced into SGPRs so that each row's
     // merge is two v_and_or_b32 (VOP3 takes no literal on gfx9)
@@ -302,8 +348,7 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    auto step = [&](int T, int ridx, const SArr<unsigned, R4 / 2>& pa, const SArr<unsigned, R4 / 2>& pb,
-                    SArr<unsigned, R4 / 2>& pn_a, SArr<unsigned, R4 / 2>& pn_b) {
+    auto step = [&](int T, int ridx, const Buf& pa, const Buf& pb, Buf& pn_a, Buf& pn_b) {
         if (T == evT) {
             // this lane's column is the first of its next pair
 #pragma unroll
@@ -320,16 +365,20 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
         rMo = dpp_shr1(rMo, sMo);
         rY = dpp_shr1(rY, sY);
         rH = dpp_shr1(rH, sH);
-        sload_prof<R>(prof_lds + ringA[ridx] + prof_lane, pn_a);
-        sload_prof<R>(prof_lds + ringB[ridx] + prof_lane, pn_b);
+        load_scores(ridx, pn_a, pn_b);
         unsigned acc[NG];
 #pragma unroll
         for (int g = 0; g < NG; ++g) acc[g] = 0u;
         s16x2 Hd = as_v(Htop), Mou = as_v(rMo), Yu = as_v(rY);
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-            const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
-            const s16x2 sc = as_v(__builtin_amdgcn_perm(pb.v[k >> 1], pa.v[k >> 1], sel));
+            s16x2 sc;
+            if constexpr (PT) {
+                sc = as_v(pa.v[k]);
+            } else {
+                const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                sc = as_v(__builtin_amdgcn_perm(pb.v[k >> 1], pa.v[k >> 1], sel));
+            }
             const s16x2 M = Hd + sc;
             const s16x2 Xe = as_v(Xl[k]) - as_v(E2);
             const s16x2 X = __builtin_elementwise_max(as_v(Mol[k]), Xe);
@@ -374,8 +423,8 @@ __global__ __launch_bounds__(256) void nw_stream_fill(const KernelArgs args) {
             stage_load(T + 2 * kStage);
             prep_events(T);
         }
-        const int Tend = exhausted ? S_tail + lr : (1 << 30);
-        const int nb = min(kStage, Tend - T + 1);
+        const int Tend = __builtin_amdgcn_readfirstlane(exhausted ? S_tail + lr : (1 << 30));
+        const int nb = __builtin_amdgcn_readfirstlane(min(kStage, Tend - T + 1));
         int u = 0;
         for (; u + 1 < nb; u += 2) {
             const int ridx = (T + u + 1 - lane) & (kRing - 1);
@@ -436,6 +485,10 @@ __global__ __launch_bounds__(256) void nw_stream_walk(const KernelArgs args) {
         }
         const int pad = span - Lb;
         const unsigned char* base = args.region + p * reg.stride;
+        if (args.ptab && (*(const int*)(base + reg.flags) & (h ? REGION_BAD_B : REGION_BAD_A))) {
+            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+            continue;
+        }
         const unsigned* bits = (const unsigned*)(base + reg.bits);
         const unsigned* caps = (const unsigned*)(base + reg.caps);
         const unsigned* last = (const unsigned*)(base + reg.last);
@@ -502,14 +555,35 @@ __global__ __launch_bounds__(256) void nw_stream_walk(const KernelArgs args) {
 
 // ---- host-side helpers ----
 
-int stream_fill_lds_bytes(int R, int wpb) { return stream_shared_bytes(R) + wpb * stream_wave_bytes(); }
+int stream_fill_lds_bytes(int R, bool pair_table, int wpb) {
+    return stream_shared_bytes(R, pair_table) + wpb * stream_wave_bytes();
+}
 int stream_walk_lds_bytes(int La, int wpb) { return stream_walk_shared_bytes(La) + wpb * kStreamRunsCap * 4; }
 StreamRegion stream_region_for(int R, int band_slots, int Lb_max) { return stream_region(R, band_slots, Lb_max); }
+
+template <int R, bool PT>
+static const void* fill_fn() { return (const void*)nw_stream_fill<R, PT>; }
+
+template <int R>
+static const void* pick_fill(bool pair_table) {
+    if constexpr (R <= 4) {
+        if (pair_table) return fill_fn<R, true>();
+    }
+    return fill_fn<R, false>();
+}
 
 template <int R>
 static hipError_t launch_stream_r(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                                   hipEvent_t after_fill) {
-    hipLaunchKernelGGL((nw_stream_fill<R>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    if constexpr (R <= 4) {
+        if (a.ptab)
+            hipLaunchKernelGGL((nw_stream_fill<R, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        else
+            hipLaunchKernelGGL((nw_stream_fill<R, false>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    } else {
+        if (a.ptab) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((nw_stream_fill<R, false>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
@@ -518,10 +592,13 @@ static hipError_t launch_stream_r(const KernelArgs& a, const LaunchCfg& fill, co
 }
 
 template <int R>
-static hipError_t occupancy_r(int* fill_blocks, int* walk_blocks, int fill_lds, int walk_lds, int wpb) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(fill_blocks, nw_stream_fill<R>, 64 * wpb, fill_lds);
+static hipError_t occupancy_r(bool pair_table, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
+                              int* walk_blocks) {
+    if (pair_table && R > 4) return hipErrorInvalidValue;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(fill_blocks, pick_fill<R>(pair_table), 64 * fill_wpb,
+                                                               fill_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_stream_walk<R>, 64 * wpb, walk_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_stream_walk<R>, 64 * walk_wpb, walk_lds);
 }
 
 #define NW_STREAM_DISPATCH(R_, CALL) \
@@ -548,8 +625,9 @@ hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const Launc
 #undef CALL_
 }
 
-hipError_t stream_occupancy(int R, int wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks) {
-#define CALL_(r) occupancy_r<r>(fill_blocks, walk_blocks, fill_lds, walk_lds, wpb)
+hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds,
+                            int* fill_blocks, int* walk_blocks) {
+#define CALL_(r) occupancy_r<r>(pair_table, fill_wpb, walk_wpb, fill_lds, walk_lds, fill_blocks, walk_blocks)
     NW_STREAM_DISPATCH(R, CALL_)
 #undef CALL_
 }

@@ -12,14 +12,17 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["stream", "pair", "band", "full"]
+KERNELS = ["stream", "stream-profile", "pair", "band", "full"]
 BANDED = {"stream": "stream-int16", "pair": "pair-band-int16"}
 
 
 @pytest.fixture(params=KERNELS)
 def kernel(request, monkeypatch):
-    """Run a test once per kernel family (CRISPR_NW_KERNEL selects it)."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", request.param)
+    """Run a test once per kernel family (CRISPR_NW_KERNEL selects it;
+    stream-profile = the stream kernel without the pair-code score table)."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", request.param.split("-")[0])
+    if request.param == "stream-profile":
+        monkeypatch.setenv("CRISPR_NW_PAIR_TABLE", "0")
     return request.param
 
 FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j")
@@ -231,6 +234,31 @@ def test_stream_mixed_lengths(gpu_aligner_factory, oracle, monkeypatch, La):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"stream La={La}")
+
+
+def test_stream_pair_table_rare_codes(gpu_aligner_factory, oracle, monkeypatch):
+    """Reads with IUPAC codes outside the pair table (A T G C N, pad) are flagged
+    in the fill kernel and re-aligned by the exact fallback; their partners are not."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
+    amp = synth.random_amplicon(240, 17)
+    buf0, off0 = synth.reads_from(amp, 600, 18, synth.PARITY_MIX)
+    reads = synth.unpack(buf0, off0)
+    rng = np.random.Generator(np.random.PCG64(19))
+    rare = "RYKMSWBDHVU"
+    bad = set()
+    for k in rng.choice(len(reads), 25, replace=False):
+        r = list(reads[int(k)])
+        if not r:
+            continue
+        r[int(rng.integers(0, len(r)))] = rare[int(rng.integers(0, len(rare)))]
+        reads[int(k)] = "".join(r)
+        bad.add(int(k))
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.fallbacks() >= len(bad)
+    assert_same(oracle, amp, buf, off, batch, "rare-codes")
 
 
 def test_stream_multiple_passes(gpu_aligner_factory, oracle, monkeypatch):
