@@ -29,6 +29,9 @@
 #ifndef NW_FILL_WAVES_PER_SIMD
 #define NW_FILL_WAVES_PER_SIMD 5   // register budget of the fill kernel (occupancy)
 #endif
+#ifndef NW_WALK_WAVES_PER_SIMD
+#define NW_WALK_WAVES_PER_SIMD 8   // the walk is latency-bound: as many waves as fit
+#endif
 
 namespace nw {
 
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
 // Walk + emit: one wavefront per read.
 // ============================================================================
 template <int R>
-__global__ __launch_bounds__(256) void nw_stream_walk(const KernelArgs args) {
+__global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(const KernelArgs args) {
     constexpr int R4 = SGeo<R>::R4;
     constexpr int NG = SGeo<R>::NG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
