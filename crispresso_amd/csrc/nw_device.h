@@ -76,7 +76,7 @@ int pair_profile_bytes_per_lane(int R);
 hipError_t launch_pair(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
 // streaming fill + walk kernels (nw_stream.hip).  Pair p's region starts at
-// region + p * stride: traceback band [64 lanes][slots][NG] words, captures
+// region + p * stride: traceback band [8 lane groups][slots][8 lanes][NG] words, captures
 // (last-column Mo) [64 lanes][R], last amplicon row Mo [span] (both reads packed).
 constexpr int kStreamMinSpan = 64;   // stream columns per pair at least: at most one pair change per
                                      // lane per 64-step block, few live descriptors

@@ -77,7 +77,7 @@ __host__ __device__ inline StreamRegion stream_region(int R, int band_slots, int
 }
 
 // Band of a pair in the stream (pair-relative column c, padded row g = ai + F):
-// slot = c - lane * R - dlo; stored lane-major, word (lane * slots + slot) * NG.  Returns false when the pair has no read or the
+// slot = c - lane * R - dlo; stored at word (((lane / 8) * slots + slot) * 8 + lane % 8) * NG.  Returns false when the pair has no read or the
 // band cannot hold both reads' start and end diagonals.
 __host__ __device__ inline bool stream_pair_band(int La, int R, int F, int slots, int LbA, int LbB, int* span,
                                                  int* dlo) {
@@ -315,9 +315,10 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             unsigned char* base = region + (long long)d0.w * reg.stride;
             n_evT = more ? d0.x + d0.y + lane : -1;
             n_slot = (more && lane < nl) ? -lane * R - d0.z : -BIG;
-            // lane-major band: each lane's words are consecutive in slot order, so
-            // its one-per-step stores fill whole 128-B lines while they sit in L2
-            n_bitp = (unsigned*)(base + reg.bits) + ((long long)lane * slots + n_slot) * NG;
+            // band words grouped by 8 lanes: [lane / 8][slot][lane % 8] -- a 128-B
+            // line (4 slots x 8 lanes) is written within ~38 steps, so it is
+            // complete while still in L2, and a diagonal of the walk reads ~8 lines
+            n_bitp = (unsigned*)(base + reg.bits) + (((long long)(lane >> 3) * slots + n_slot) * 8 + (lane & 7)) * NG;
             n_capp = more ? (unsigned*)(base + reg.caps) + lane * R : caps_dummy;
             n_lrp = more ? (unsigned*)(base + reg.last) : lr_dummy;
             qi = q;
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             for (int g = 0; g < NG; ++g) bitp[g] = acc[g];
         }
         ++slot;
-        bitp += NG;
+        bitp += 8 * NG;
         if (lane == lr) { *lrp = sMo; ++lrp; }
         Htop = rH;
     };
@@ -530,7 +531,7 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
             const int s = bjj + pad - ln * R - dlo;
             if ((unsigned)s >= (unsigned)slots) { *oob = true; return 0u; }
             *oob = false;
-            const unsigned w = bits[((size_t)ln * slots + s) * NG + (k >> 2)];
+            const unsigned w = bits[((((size_t)(ln >> 3) * slots + s) << 3) + (ln & 7)) * NG + (k >> 2)];
             const int kk = k & 3;
             const int hb = 8 * h + kk, lb = 8 * h + 4 + kk;
             const unsigned yext = (w >> hb) & 1u, bX = (w >> lb) & 1u;
