@@ -35,17 +35,50 @@ __device__ __forceinline__ long long wave_max_i64(long long v) {
     return v;
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Wave reductions on DPP (row_shr within 16-lane rows, then row_bcast:15/31):
+// six VALU ops with no LDS round trip; the result is read from lane 63.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_max_step(unsigned v) {
+    const unsigned o = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+    return v > o ? v : o;
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_add_step(unsigned v) {
+    return v + (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = dpp_max_step<0x111, 0xf>(v);
+    v = dpp_max_step<0x112, 0xf>(v);
+    v = dpp_max_step<0x114, 0xf>(v);
+    v = dpp_max_step<0x118, 0xf>(v);
+    v = dpp_max_step<0x142, 0xa>(v);
+    v = dpp_max_step<0x143, 0xc>(v);
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
+    v = dpp_add_step<0x111, 0xf>(v);
+    v = dpp_add_step<0x112, 0xf>(v);
+    v = dpp_add_step<0x114, 0xf>(v);
+    v = dpp_add_step<0x118, 0xf>(v);
+    v = dpp_add_step<0x142, 0xa>(v);
+    v = dpp_add_step<0x143, 0xc>(v);
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ int wave_sum(int v) { return (int)wave_sum_u32((unsigned)v); }
 
 // Candidate key for the traceback start cell.  Scan order of the reference
 // walk start (corner, then last column bottom->top, then last row right->left,
 // first strict maximum) becomes "largest (score, priority)".
 __device__ __forceinline__ long long end_key(int score, int cls, int pos) {
     return ((long long)score << 32) | (((long long)cls << 24) | pos);
+}
+// The same order in 32 bits when |score| < 2^15 and pos < 2^14 (int16 kernels).
+__device__ __forceinline__ unsigned end_key32(int score, int cls, int pos) {
+    return ((unsigned)(score + 32768) << 16) | ((unsigned)cls << 14) | (unsigned)pos;
+}
+__device__ __forceinline__ long long end_key_widen(unsigned k) {
+    return end_key((int)(k >> 16) - 32768, (int)((k >> 14) & 3), (int)(k & 0x3fff));
 }
 __device__ __forceinline__ void decode_end(long long key, int La, int Lb, int* score, int* ei, int* ej) {
     *score = (int)(key >> 32);
@@ -94,7 +127,7 @@ __device__ int walk_runs(const Nib& nib, int La, int Lb, int ei, int ej, unsigne
             const int best = (c & 1u) ? RUN_M : ((c & 2u) ? RUN_X : RUN_Y);
             m = __ballot(!valid || oob || best != RUN_M);
             if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
-            nb = __shfl(best, (int)__builtin_ctzll(m), 64);
+            nb = __builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
         } else if (state == RUN_X) {
             const int cj = j - lane;
             const bool valid = cj >= 1;
@@ -112,6 +145,84 @@ __device__ int walk_runs(const Nib& nib, int La, int Lb, int ei, int ej, unsigne
         }
         const int k0 = (int)__builtin_ctzll(m);
         if ((__ballot(oob) & (1ull << k0)) || full) return -1;
+        push(state, k0 + 1);
+        if (state != RUN_Y) j -= k0 + 1;
+        if (state != RUN_X) i -= k0 + 1;
+        state = (state == RUN_M) ? nb : RUN_M;
+    }
+    if (i > 0) push(RUN_Y, i);
+    if (j > 0) push(RUN_X, j);
+    return full ? -1 : nruns;
+}
+
+// walk_runs with CPL consecutive run cells per lane: one ballot tests 64*CPL
+// cells (lane k holds run offsets k*CPL .. k*CPL+CPL-1), so a 250-cell match run
+// costs one round trip to the band instead of four.  Same results as walk_runs.
+template <int CPL, class Nib>
+__device__ int walk_runs_wide(const Nib& nib, int La, int Lb, int ei, int ej, unsigned* runs, int cap, int lane) {
+    int nruns = 0, last_type = -1;
+    bool full = false;
+    auto push = [&](int type, int n) {
+        if (n <= 0) return;
+        if (type == last_type) {
+            if (lane == 0) runs[nruns - 1] += (unsigned)n;
+        } else if (nruns < cap) {
+            if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
+            ++nruns;
+            last_type = type;
+        } else {
+            full = true;
+        }
+    };
+    if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
+    else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
+    constexpr int W = 64 * CPL;
+    int i = ei, j = ej, state = RUN_M;
+    while (i > 0 && j > 0) {
+        int first = CPL, first_best = RUN_M;
+        bool first_oob = false;
+        unsigned c[CPL];
+        bool valid[CPL], oob[CPL];
+        // all CPL lookups first (independent loads in flight together), then the tests
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int kk = lane * CPL + u;
+            oob[u] = false;
+            if (state == RUN_M) {
+                const int ci = i - 1 - kk, cj = j - 1 - kk;
+                valid[u] = ci >= 1 && cj >= 1;
+                c[u] = valid[u] ? nib(ci - 1, cj - 1, &oob[u]) : 0u;
+            } else if (state == RUN_X) {
+                const int cj = j - kk;
+                valid[u] = cj >= 1;
+                c[u] = valid[u] ? nib(i - 1, cj - 1, &oob[u]) : 0u;
+            } else {
+                const int ci = i - kk;
+                valid[u] = ci >= 1;
+                c[u] = valid[u] ? nib(ci - 1, j - 1, &oob[u]) : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = CPL - 1; u >= 0; --u) {
+            const int best = (c[u] & 1u) ? RUN_M : ((c[u] & 2u) ? RUN_X : RUN_Y);
+            const bool go = state == RUN_M ? best == RUN_M : (c[u] & (state == RUN_X ? 4u : 8u)) != 0;
+            if (!valid[u] || oob[u] || !go) {
+                first = u;
+                first_oob = valid[u] && oob[u];
+                first_best = best;
+            }
+        }
+        const unsigned long long m = __ballot(first < CPL);
+        if (m == 0) {
+            push(state, W);
+            if (state != RUN_Y) j -= W;
+            if (state != RUN_X) i -= W;
+            continue;
+        }
+        const int L = (int)__builtin_ctzll(m);
+        const int k0 = L * CPL + __builtin_amdgcn_readlane(first, L);
+        const int nb = __builtin_amdgcn_readlane(first_best, L);
+        if (__builtin_amdgcn_readlane((int)first_oob, L) || full) return -1;
         push(state, k0 + 1);
         if (state != RUN_Y) j -= k0 + 1;
         if (state != RUN_X) i -= k0 + 1;
@@ -160,9 +271,16 @@ __device__ void emit_alignment(const unsigned* runs, int nruns, const unsigned c
         if (type != RUN_X) ia += n;
         if (type != RUN_Y) jb += n;
     }
-    n_id = wave_sum(n_id);
-    n_sim = wave_sum(n_sim);
-    n_gap = wave_sum(n_gap);
+    if (col < 1024) {   // uniform: the three per-lane counts fit 10 bits each -> one reduction
+        const unsigned t = wave_sum_u32((unsigned)n_id | ((unsigned)n_sim << 10) | ((unsigned)n_gap << 20));
+        n_id = (int)(t & 1023u);
+        n_sim = (int)((t >> 10) & 1023u);
+        n_gap = (int)(t >> 20);
+    } else {
+        n_id = wave_sum(n_id);
+        n_sim = wave_sum(n_sim);
+        n_gap = wave_sum(n_gap);
+    }
     if (lane == 0) {
         Stat s;
         s.aln_len = col;

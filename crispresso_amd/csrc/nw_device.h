@@ -86,7 +86,6 @@ struct StreamRegion {
 };
 constexpr int kPairCodes = 6;        // pair-table alphabet: A T G C N pad
 enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // read has a code outside the pair table
-__host__ __device__ inline int stream_walk_shared_bytes(int La) { return ((256 + La + 16) + 15) & ~15; }
 int stream_fill_lds_bytes(int R, bool pair_table, int wpb);
 int stream_walk_lds_bytes(int La, int wpb);
 StreamRegion stream_region_for(int R, int band_slots, int Lb_max);

@@ -293,7 +293,7 @@ int configure(nw_ctx* c) {
         f.tb_mode = w.tb_mode = nw::TB_STREAM;
         // fill: waves per block that maximise resident waves (the pair table is
         // 36 KB of LDS per block, so bigger blocks share it among more waves)
-        w.wpb = 4;
+        w.wpb = 8;
         w.lds_bytes = nw::stream_walk_lds_bytes(La, w.wpb);
         int fb = 0, wb = 0, best = -1;
         for (int wpb : {4, 8, 10}) {
@@ -444,7 +444,7 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     c->lb_max = lb_max;
     c->cells = cells;
     c->stride = stride_for(La, lb_max);
-    HIP_OR_FAIL(c, c->d_reads.reserve((size_t)nbytes + 64));
+    HIP_OR_FAIL(c, c->d_reads.reserve((size_t)nbytes + 512));   // the walk DMAs whole 256-B chunks
     HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
     HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));

@@ -96,7 +96,6 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wpb = blockDim.x >> 6;
 
     // ---- shared per-block state: int16 profile, ascii->code LUT, amplicon bytes ----
     unsigned char* prof_lds = smem;
@@ -316,7 +315,6 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
                 if ((unsigned)s >= (unsigned)slots) { *oob = true; return 0u; }
                 *oob = false;
                 const int grp = k >> 2, kk = k & 3;
-                const int gR = (R - 4 * grp) < 4 ? (R - 4 * grp) : 4;
                 const unsigned w = bits[((size_t)s * 64 + ln) * NG + grp];
                 const int hb = 8 * h + kk, lb = 8 * h + 4 + kk;
                 const unsigned yext = (w >> hb) & 1u, bX = (w >> lb) & 1u;

@@ -29,6 +29,9 @@
 #ifndef NW_FILL_WAVES_PER_SIMD
 #define NW_FILL_WAVES_PER_SIMD 5   // register budget of the fill kernel (occupancy)
 #endif
+#ifndef NW_WALK_CPL
+#define NW_WALK_CPL 2              // walk cells tested per lane per ballot
+#endif
 #ifndef NW_WALK_WAVES_PER_SIMD
 #define NW_WALK_WAVES_PER_SIMD 8   // the walk is latency-bound: as many waves as fit
 #endif
@@ -447,10 +450,18 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
 }
 
 // ============================================================================
-// Walk + emit: one wavefront per read.
+// Walk + emit: one wavefront per read, latency-bound.  Per read the dependent
+// global round trips are: record offsets; {flags, captures, last row, the read's
+// bytes DMA'd into LDS} together; ~1-3 walk ballots over the band (256 cells
+// each); then the strings are built from LDS only.
 // ============================================================================
+constexpr int kWalkReadCap = 1024;   // reads up to this length are staged in LDS for the emit
+
+__host__ __device__ inline int walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
+__host__ __device__ inline int walk_wave_bytes() { return kStreamRunsCap * 4 + kWalkReadCap + 256; }
+
 template <int R>
-__global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(const KernelArgs args) {
+__global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(const KernelArgs args) {
     constexpr int R4 = SGeo<R>::R4;
     constexpr int NG = SGeo<R>::NG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -460,25 +471,40 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wpb = blockDim.x >> 6;
-    unsigned char* lut_lds = smem;
-    unsigned char* amp_lds = smem + 256;
-    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
-    for (int q = tid; q < La; q += blockDim.x) amp_lds[q] = args.amp[q];
-    __syncthreads();
-    unsigned* runs = (unsigned*)(smem + stream_walk_shared_bytes(La) + wave * kStreamRunsCap * 4);
-
-    const int slots = args.band_slots;
     const int nl = (La + R - 1) / R;
     const int F = nl * R - La;
-    const StreamRegion reg = stream_region(R, slots, args.Lb_max);
     const short* prof16 = (const short*)args.prof;
+
+    // block-shared: ascii->code, amplicon bytes, per amplicon row the codes it scores > 0 against
+    unsigned char* lut_lds = smem;
+    unsigned char* amp_lds = smem + 256;
+    unsigned* rowpos = (unsigned*)(smem + 256 + align16(La + 16));
+    for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = args.lut[q];
+    for (int q = tid; q < La; q += blockDim.x) {
+        amp_lds[q] = args.amp[q];
+        const int g = q + F;
+        unsigned m = 0;
+        for (int code = 0; code < NCODE; ++code)
+            m |= (prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] > 0 ? 1u : 0u) << code;
+        rowpos[q] = m;
+    }
+    __syncthreads();
+    unsigned char* wb = smem + walk_shared_bytes(La) + wave * walk_wave_bytes();
+    unsigned* runs = (unsigned*)wb;
+    unsigned char* rbuf = wb + kStreamRunsCap * 4;
+
+    const int slots = args.band_slots;
+    const StreamRegion reg = stream_region(R, slots, args.Lb_max);
+    // int16 scores; positions (row or column) below 2^14 -> 32-bit start-cell keys
+    const bool small_keys = La < 16384 && args.Lb_max < 16384;
 
     for (long long rd = (long long)blockIdx.x * wpb + wave; rd < args.n; rd += (long long)gridDim.x * wpb) {
         const long long p = rd >> 1;
         const int h = (int)(rd & 1);
         const long long ra = 2 * p, rb = 2 * p + 1;
-        const int LbA = (int)(args.offsets[ra + 1] - args.offsets[ra]);
-        const int LbB = rb < args.n ? (int)(args.offsets[rb + 1] - args.offsets[rb]) : 0;
+        const long long offA = args.offsets[ra], offB1 = args.offsets[ra + 1];
+        const int LbA = (int)(offB1 - offA);
+        const int LbB = rb < args.n ? (int)(args.offsets[rb + 1] - offB1) : 0;
         const int Lb = h ? LbB : LbA;
         if (Lb <= 0) {
             if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; args.stats[rd] = z; }
@@ -491,36 +517,74 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
         }
         const int pad = span - Lb;
         const unsigned char* base = args.region + p * reg.stride;
-        if (args.ptab && (*(const int*)(base + reg.flags) & (h ? REGION_BAD_B : REGION_BAD_A))) {
-            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
-            continue;
-        }
         const unsigned* bits = (const unsigned*)(base + reg.bits);
         const unsigned* caps = (const unsigned*)(base + reg.caps);
         const unsigned* last = (const unsigned*)(base + reg.last);
+        const unsigned char* raw = args.reads + (h ? offB1 : offA);
 
-        // ---- start cell ----
-        long long key = -0x7fffffffffffffffll - 1;
-        if (lane < nl) {
+        // ---- one round of loads: read bytes -> LDS, flags, captures, last row ----
+        // LDS-DMA writes one dword per lane: copy from the 4-byte-aligned address
+        // below the read (the reads buffer is padded) and index by the misalignment
+        const bool cached = Lb <= kWalkReadCap;
+        const int mis = (int)((uintptr_t)raw & 3);
+        if (cached) {
+            const unsigned char* src = raw - mis;
+            for (int m = 0; m < Lb + mis; m += 256)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + m + 4 * lane),
+                                                 (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
+        }
+        const int flags = args.ptab ? *(const int*)(base + reg.flags) : 0;
+        long long key;
+        if (small_keys) {
+            // 32-bit keys, DPP max: score (int16) | class | position
+            unsigned k32 = 0;
+            if (lane < nl) {
 #pragma unroll
-            for (int k = 0; k < R; ++k) {
-                const int ai = lane * R + k - F;
-                if (ai >= 0) {
-                    const int v = half(caps[lane * R + k], h) + O;
-                    const long long kk = (ai == La - 1) ? end_key(v, 3, 0) : end_key(v, 2, ai);
-                    key = kk > key ? kk : key;
+                for (int k = 0; k < R; ++k) {
+                    const int ai = lane * R + k - F;
+                    if (ai >= 0) {
+                        const int v = half(caps[lane * R + k], h) + O;
+                        const unsigned kk = (ai == La - 1) ? end_key32(v, 3, 0) : end_key32(v, 2, ai);
+                        k32 = kk > k32 ? kk : k32;
+                    }
                 }
             }
+#pragma unroll 4
+            for (int q = lane; q < Lb - 1; q += 64) {
+                const unsigned kk = end_key32(half(last[pad + q], h) + O, 1, q);
+                k32 = kk > k32 ? kk : k32;
+            }
+            key = end_key_widen(wave_max_u32(k32));
+        } else {
+            key = -0x7fffffffffffffffll - 1;
+            if (lane < nl) {
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const int ai = lane * R + k - F;
+                    if (ai >= 0) {
+                        const int v = half(caps[lane * R + k], h) + O;
+                        const long long kk = (ai == La - 1) ? end_key(v, 3, 0) : end_key(v, 2, ai);
+                        key = kk > key ? kk : key;
+                    }
+                }
+            }
+            for (int q = lane; q < Lb - 1; q += 64) {
+                const long long kk = end_key(half(last[pad + q], h) + O, 1, q);
+                key = kk > key ? kk : key;
+            }
+            key = wave_max_i64(key);
         }
-        for (int q = lane; q < Lb - 1; q += 64) {
-            const long long kk = end_key(half(last[pad + q], h) + O, 1, q);
-            key = kk > key ? kk : key;
-        }
-        key = wave_max_i64(key);
         int score, ei, ej;
         decode_end(key, La, Lb, &score, &ei, &ej);
+        if (flags & (h ? REGION_BAD_B : REGION_BAD_A)) {
+            // a code outside the pair table: the fill's scores are not this read's
+            if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            continue;
+        }
         if (args.debug_mode == 1) {
             if (lane == 0) { Stat z = {}; z.score = score; z.end_i = ei; z.end_j = ej; args.stats[rd] = z; }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             continue;
         }
 
@@ -538,7 +602,8 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
             const unsigned xext = (w >> (16 + hb)) & 1u, bM = (w >> (16 + lb)) & 1u;
             return bM | (bX << 1) | (xext << 2) | (yext << 3);
         };
-        const int nruns = walk_runs(nib, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        const int nruns = walk_runs_wide<NW_WALK_CPL>(nib, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
             if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
             continue;
@@ -548,12 +613,8 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
             if (lane == 0) { Stat z = {}; z.score = score; z.aln_len = nruns; args.stats[rd] = z; }
             continue;
         }
-        auto sim = [&](int ai, int code) {
-            const int g = ai + F;
-            return (int)prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R];
-        };
-        const long long off = args.offsets[rd];
-        emit_alignment(runs, nruns, amp_lds, args.reads + off, lut_lds, sim, args.out + rd * 3 * args.stride,
+        auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
+        emit_alignment(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, args.out + rd * 3 * args.stride,
                        args.stride, score, ei, ej, args.stats + rd, lane);
         lds_fence();
     }
@@ -564,7 +625,7 @@ __global__ __launch_bounds__(256, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
 int stream_fill_lds_bytes(int R, bool pair_table, int wpb) {
     return stream_shared_bytes(R, pair_table) + wpb * stream_wave_bytes();
 }
-int stream_walk_lds_bytes(int La, int wpb) { return stream_walk_shared_bytes(La) + wpb * kStreamRunsCap * 4; }
+int stream_walk_lds_bytes(int La, int wpb) { return walk_shared_bytes(La) + wpb * walk_wave_bytes(); }
 StreamRegion stream_region_for(int R, int band_slots, int Lb_max) { return stream_region(R, band_slots, Lb_max); }
 
 template <int R, bool PT>
