@@ -59,7 +59,7 @@ __device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
 }
 
 constexpr int kRing = 256;         // staged columns per read (power of two)
-constexpr int kRingAlloc = kRing + 2;
+constexpr int kRingAlloc = kRing + 4;   // + mirror of the first entries (4-step unroll)
 constexpr int kDescQ = 16;         // pair descriptors per wave (ring)
 constexpr int kStage = 64;         // steps between two staging points
 constexpr int kChunk = 2;          // pairs per dequeue
@@ -73,7 +73,7 @@ __host__ __device__ inline StreamRegion stream_region(int R, int band_slots, int
     g.bits = 0;
     g.caps = (int64_t)band_slots * 64 * NG * 4;
     g.last = g.caps + (int64_t)64 * R * 4;
-    const int64_t span_cap = (Lb_max > kStreamMinSpan ? Lb_max : kStreamMinSpan) + 4;
+    const int64_t span_cap = (Lb_max > kStreamMinSpan ? Lb_max : kStreamMinSpan) + 8;
     g.flags = g.last + 4 * span_cap;
     g.stride = (g.flags + 4 + 255) & ~(int64_t)255;
     return g;
@@ -88,7 +88,8 @@ __host__ __device__ inline bool stream_pair_band(int La, int R, int F, int slots
     *span = 0;
     *dlo = 0;
     if (Lmax <= 0) return false;
-    const int sp = Lmax > kStreamMinSpan ? Lmax : kStreamMinSpan;
+    // spans are multiples of 4: every pair starts at the same column phase (mod 4)
+    const int sp = ((Lmax > kStreamMinSpan ? Lmax : kStreamMinSpan) + 3) & ~3;
     int lo = 1 << 30, hi = -(1 << 30);
     const int Lb[2] = {LbA, LbB};
     for (int h = 0; h < 2; ++h) {
@@ -183,7 +184,11 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
 
     // ---- wave-uniform stream state ----
     int q_count = 0;           // pairs appended so far
-    int S_tail = 0;            // first stream column after the appended pairs
+    // The stream starts at column S0 = -lr mod 4: pair starts are then = -lr
+    // (mod 4), so lane lr (the last amplicon row) changes pairs only on the first
+    // of every 4 steps and stores its last-row words 4 at a time.
+    const int S0 = (4 - (lr & 3)) & 3;
+    int S_tail = S0;           // first stream column after the appended pairs
     bool exhausted = false;
     long long cur = 0, cur_end = 0;   // dequeued pair range being appended
     long long next_chunk = 0;
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
     unsigned* const lr_dummy = (unsigned*)(args.region + npairs * reg.stride);
     unsigned* const caps_dummy = lr_dummy + 256;
     int qi = -1;                   // this lane's latest prepared pair (count index)
-    int evT = lane;
+    int evT = S0 + lane;
     int slot = -BIG;
     unsigned* bitp = nullptr;      // band word of the current column (used while 0 <= slot < slots)
     unsigned* lrp = lr_dummy;      // last-row word of the current column (lane lr)
@@ -357,7 +362,8 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    auto step = [&](int T, int ridx, const Buf& pa, const Buf& pb, Buf& pn_a, Buf& pn_b) {
+    unsigned lrv[3] = {0u, 0u, 0u};   // last-row words of sub-steps 0..2 (lane lr)
+    auto step = [&](int T, int ridx, int sub, const Buf& pa, const Buf& pb, Buf& pn_a, Buf& pn_b) {
         if (T == evT) {
             // this lane's column is the first of its next pair
 #pragma unroll
@@ -420,7 +426,12 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
         }
         ++slot;
         bitp += 8 * NG;
-        if (lane == lr) { *lrp = sMo; ++lrp; }
+        if (sub < 3) {
+            lrv[sub] = sMo;
+        } else if (lane == lr) {
+            *(uint4*)lrp = make_uint4(lrv[0], lrv[1], lrv[2], sMo);
+            lrp += 4;
+        }
         Htop = rH;
     };
 
@@ -435,14 +446,18 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
         const int Tend = __builtin_amdgcn_readfirstlane(exhausted ? S_tail + lr : (1 << 30));
         const int nb = __builtin_amdgcn_readfirstlane(min(kStage, Tend - T + 1));
         int u = 0;
-        for (; u + 1 < nb; u += 2) {
+        for (; u + 3 < nb; u += 4) {
             const int ridx = (T + u + 1 - lane) & (kRing - 1);
-            step(T + u, ridx, pa0, pb0, pa1, pb1);
-            step(T + u + 1, ridx + 1, pa1, pb1, pa0, pb0);
+            step(T + u, ridx, 0, pa0, pb0, pa1, pb1);
+            step(T + u + 1, ridx + 1, 1, pa1, pb1, pa0, pb0);
+            step(T + u + 2, ridx + 2, 2, pa0, pb0, pa1, pb1);
+            step(T + u + 3, ridx + 3, 3, pa1, pb1, pa0, pb0);
         }
         if (u < nb) {
-            step(T + u, (T + u + 1 - lane) & (kRing - 1), pa0, pb0, pa1, pb1);
-            break;   // nb odd only at the end of the stream
+            // only at the end of the stream: nb = Tend - T + 1 = 1 (mod 4), the last
+            // step is lane lr's final pair change
+            step(T + u, (T + u + 1 - lane) & (kRing - 1), 0, pa0, pb0, pa1, pb1);
+            break;
         }
         T += kStage;
         if (T > Tend) break;
