@@ -297,7 +297,6 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
     for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
     unsigned sMo = MO0, sY = NEG2, sH = 0u;
     unsigned rMo = MO0, rY = NEG2, rH = 0u;
-    unsigned Htop = 0u;
     // Pair changes.  evT = step at which this lane's column is the first of its
     // next pair.  The next pair's pointers (n_*) are prepared for all lanes at
     // once at the staging point before that step (one change per lane and
@@ -375,16 +374,16 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             lrp = n_lrp;
 #pragma unroll
             for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
-            Htop = 0u;
+            rH = 0u;   // diagonal of row 0 at the pair's first column: the boundary
         }
         rMo = dpp_shr1(rMo, sMo);
         rY = dpp_shr1(rY, sY);
-        rH = dpp_shr1(rH, sH);
         load_scores(ridx, pn_a, pn_b);
         unsigned acc[NG];
 #pragma unroll
         for (int g = 0; g < NG; ++g) acc[g] = 0u;
-        s16x2 Hd = as_v(Htop), Mou = as_v(rMo), Yu = as_v(rY);
+        // rH = H of the row above at the previous column (the diagonal of row 0)
+        s16x2 Hd = as_v(rH), Mou = as_v(rMo), Yu = as_v(rY);
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             s16x2 sc;
@@ -419,6 +418,9 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
         }
         sMo = as_u(Mou);
         sY = as_u(Yu);
+        // the row above's H at this column, for the next step (reads the previous
+        // step's sH; done after its use as the diagonal, so rH needs no copy)
+        rH = dpp_shr1(rH, sH);
         sH = Hold[R - 1];
         if ((unsigned)slot < (unsigned)slots) {
 #pragma unroll
@@ -432,7 +434,6 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             *(uint4*)lrp = make_uint4(lrv[0], lrv[1], lrv[2], sMo);
             lrp += 4;
         }
-        Htop = rH;
     };
 
     int T = 0;
