@@ -38,7 +38,7 @@ EXPORTS = (
     "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload",
     "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
-    "nw_format_srspair",
+    "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair",
 )
 
 
@@ -81,6 +81,9 @@ def load() -> ctypes.CDLL:
         "nw_batch_geometry": (c_int, [ctx_p] + [POINTER(c_int32)] * 5),
         "nw_batch_fallbacks": (c_int64, [ctx_p]),
         "nw_batch_kernel_times": (c_int, [ctx_p] + [POINTER(c_float)] * 3),
+        "nw_align_multi": (c_int, [ctx_p, c_char_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
+                                   c_void_p, c_int64, c_void_p]),
+        "nw_required_stride_multi": (c_int64, [c_void_p, c_int32, c_int32]),
         "nw_format_srspair": (
             c_int64,
             [c_void_p, c_int64, c_char_p, c_char_p, c_float, c_float, c_int32, c_int32, c_void_p, c_int64,

@@ -206,6 +206,36 @@ class GpuAligner:
         buf, offsets = pack_reads(reads)
         return self.align_packed(buf, offsets)
 
+    def align_multi(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
+                    amplicon_of_read: np.ndarray) -> AlignmentBatch:
+        """Pooled batch: read r against amplicons[amplicon_of_read[r]] (nw_align_multi).
+
+        Results in read order; rows are as wide as the longest amplicon needs.
+        Leaves no amplicon set on this aligner (call set_reference before
+        align_packed again).
+        """
+        amps = [a.strip().upper() for a in amplicons]
+        refs = "".join(amps).encode()
+        roff = np.zeros(len(amps) + 1, dtype=np.int64)
+        roff[1:] = np.cumsum([len(a) for a in amps])
+        idx = np.ascontiguousarray(amplicon_of_read, dtype=np.int32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(offsets) - 1
+        if len(idx) != n:
+            raise NeedleError(f"{len(idx)} amplicon indices for {n} reads")
+        lens = np.diff(offsets)
+        max_len = int(lens.max()) if n else 1
+        stride = int(self.lib.nw_required_stride_multi(_lib.ptr(roff), len(amps), max(max_len, 1)))
+        stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+        aln = np.zeros((n, 3, stride), dtype=np.uint8)
+        self._check(
+            self.lib.nw_align_multi(self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf), _lib.ptr(offsets),
+                                    _lib.ptr(idx), n, _lib.ptr(aln), stride, _lib.ptr(stats)),
+            "nw_align_multi",
+        )
+        self.reference = None
+        return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
+
 
 def format_srspair(batch: AlignmentBatch, aname: str, bnames: Sequence[str], options: NeedleOptions) -> str:
     """srspair blocks of a batch (needle's default -aformat), via the C++ writer."""

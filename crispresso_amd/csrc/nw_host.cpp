@@ -457,13 +457,17 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     return NW_OK;
 }
 
-int nw_batch_run_async(nw_ctx* c) {
-    if (!c) return NW_E_INVALID;
-    if (c->ref.empty() || !c->d_offsets.p) return fail(c, NW_E_STATE, "no batch uploaded");
-    (void)hipSetDevice(c->device);
+}  // extern "C"
+
+namespace {
+
+// Launches the kernels for the c->n reads that start at read `base` of the
+// uploaded arrays (outputs, records and fallback queue at the same index).
+// Everything is queued on c->stream; nothing synchronises.
+int launch_range(nw_ctx* c, int64_t base) {
     nw::KernelArgs a{};
     a.reads = c->d_reads.p;
-    a.offsets = c->d_offsets.p;
+    a.offsets = c->d_offsets.p + base;
     a.n = c->n;
     a.prof = c->d_prof.p;
     a.ptab = nullptr;
@@ -474,16 +478,15 @@ int nw_batch_run_async(nw_ctx* c) {
     a.gap_open = c->gap_open;
     a.gap_extend = c->gap_extend;
     a.Lb_max = c->lb_max;
-    a.out = c->d_out.p;
+    a.out = c->d_out.p + base * 3 * c->stride;
     a.stride = c->stride;
-    a.stats = c->d_stats.p;
+    a.stats = c->d_stats.p + base;
     a.tb_global = c->d_tb.p;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->R, c->lb_max) : 0;
     a.band_slots = c->band_slots;
-    a.fallback_list = c->d_fallback.p;
+    a.fallback_list = c->d_fallback.p + base;
     a.fallback_count = c->d_fallback_count.p;
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
-    HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
     if (c->use_stream) {
         // passes of at most pass_reads reads (the per-pair regions of one pass stay resident)
         const int64_t passes = std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads);
@@ -491,16 +494,16 @@ int nw_batch_run_async(nw_ctx* c) {
         for (int64_t q = 0; q < passes && c->n > 0; ++q) {
             const int64_t lo = q * c->pass_reads, hi = std::min(c->n, lo + c->pass_reads);
             nw::KernelArgs ap = a;
-            ap.offsets = c->d_offsets.p + lo;
+            ap.offsets = a.offsets + lo;
             ap.n = hi - lo;
-            ap.out = c->d_out.p + lo * 3 * c->stride;
-            ap.stats = c->d_stats.p + lo;
+            ap.out = a.out + lo * 3 * c->stride;
+            ap.stats = a.stats + lo;
             ap.prof = (const int8_t*)c->d_prof16.p;
             ap.band_slots = c->stream_slots;
             ap.region = c->d_region.p;
             ap.ptab = c->have_ptab ? c->d_ptab.p : nullptr;
             ap.lut6 = c->d_lut6.p;
-            ap.fallback_list = c->d_fallback.p + lo;
+            ap.fallback_list = a.fallback_list + lo;
             ap.fallback_count = c->d_fallback_count.p + 4 * q;
             ap.work_counter = ap.fallback_count + 1;
             HIP_OR_FAIL(c, nw::launch_stream(ap, c->stream_fill, c->stream_walk, c->stream, q == 0 ? c->ev_fill : nullptr));
@@ -514,11 +517,8 @@ int nw_batch_run_async(nw_ctx* c) {
             af.work_count = ap.fallback_count;
             HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->stream));
         }
-        HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
-        c->ran = true;
         return NW_OK;
     }
-    HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
     a.work_counter = c->d_fallback_count.p + 1;
     if (c->n > 0) {
@@ -527,15 +527,29 @@ int nw_batch_run_async(nw_ctx* c) {
             ap.prof = (const int8_t*)c->d_prof16.p;
             ap.band_slots = c->pair_slots;
             HIP_OR_FAIL(c, nw::launch_pair(ap, c->pair_cfg, c->stream));
-            a.work_list = c->d_fallback.p;      // re-run what left the band
+            a.work_list = a.fallback_list;      // re-run what left the band
             a.work_count = c->d_fallback_count.p;
         } else if (c->use_band) {
             HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
-            a.work_list = c->d_fallback.p;
+            a.work_list = a.fallback_list;
             a.work_count = c->d_fallback_count.p;
         }
         HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
     }
+    return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_batch_run_async(nw_ctx* c) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty() || !c->d_offsets.p) return fail(c, NW_E_STATE, "no batch uploaded");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
+    int rc = launch_range(c, 0);
+    if (rc) return rc;
     HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
     c->ran = true;
     return NW_OK;
@@ -637,6 +651,112 @@ int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t
     if ((rc = nw_batch_run_async(c))) return rc;
     if ((rc = nw_batch_sync(c, nullptr))) return rc;
     return nw_batch_download(c, aln_out, stride, stats);
+}
+
+// Pooled batches (CRISPRessoPooled.py:882-908 runs one CRISPResso
+// process -- and one needle -- per amplicon): every read carries the index of
+// its amplicon.  Reads are grouped by amplicon and uploaded once; each group's
+// kernels are queued back to back on the context's stream (the profile upload
+// of the next amplicon is ordered after them); one sync; outputs come back
+// group by group and are scattered to the callers' read order.
+int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
+                   const int64_t* offsets, const int32_t* ref_of_read, int64_t n, char* aln_out, int64_t stride,
+                   nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (n_refs <= 0 || !refs || !ref_offsets) return fail(c, NW_E_INVALID, "no amplicons");
+    if (n < 0 || (n > 0 && (!reads || !offsets || !ref_of_read))) return fail(c, NW_E_INVALID, "bad batch");
+    for (int32_t g = 0; g < n_refs; ++g) {
+        const int64_t L = ref_offsets[g + 1] - ref_offsets[g];
+        if (L <= 0 || L > kMaxRef) return fail(c, NW_E_UNSUPPORTED, "amplicon %d has length %lld", g, (long long)L);
+    }
+    (void)hipSetDevice(c->device);
+    // group reads by amplicon (stable)
+    std::vector<int64_t> first((size_t)n_refs + 1, 0);
+    int32_t lb_all = 1;
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t g = ref_of_read[r];
+        const int64_t len = offsets[r + 1] - offsets[r];
+        if (g < 0 || g >= n_refs) return fail(c, NW_E_INVALID, "read %lld has amplicon index %d", (long long)r, g);
+        if (len < 0 || len > (1 << 20)) return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
+        ++first[(size_t)g + 1];
+        lb_all = std::max<int32_t>(lb_all, (int32_t)len);
+    }
+    for (int32_t g = 0; g < n_refs; ++g) first[(size_t)g + 1] += first[(size_t)g];
+    std::vector<int64_t> order((size_t)n), fill(first.begin(), first.end() - 1);
+    for (int64_t r = 0; r < n; ++r) order[(size_t)fill[(size_t)ref_of_read[r]]++] = r;
+    int64_t stride_all = 16;
+    for (int32_t g = 0; g < n_refs; ++g)
+        if (first[(size_t)g + 1] > first[(size_t)g])
+            stride_all = std::max(stride_all, stride_for((int)(ref_offsets[g + 1] - ref_offsets[g]), lb_all));
+    if (aln_out && stride < stride_all)
+        return fail(c, NW_E_INVALID, "stride %lld < required %lld", (long long)stride, (long long)stride_all);
+    // packed reads in group order
+    std::vector<int64_t> soff((size_t)n + 1, 0);
+    for (int64_t s = 0; s < n; ++s) soff[(size_t)s + 1] = soff[(size_t)s] + (offsets[order[(size_t)s] + 1] - offsets[order[(size_t)s]]);
+    std::vector<char> sreads((size_t)soff[(size_t)n]);
+    for (int64_t s = 0; s < n; ++s) {
+        const int64_t r = order[(size_t)s];
+        std::memcpy(sreads.data() + soff[(size_t)s], reads + offsets[r], (size_t)(offsets[r + 1] - offsets[r]));
+    }
+    HIP_OR_FAIL(c, c->d_reads.reserve(sreads.size() + 512));
+    HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
+    HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * stride_all));
+    HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
+    HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)));
+    if (!sreads.empty())
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, sreads.data(), sreads.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, soff.data(), sizeof(int64_t) * soff.size(), hipMemcpyHostToDevice, c->stream));
+    // one group per amplicon: profile (ordered after the previous group's kernels), geometry, kernels
+    for (int32_t g = 0; g < n_refs; ++g) {
+        const int64_t lo = first[(size_t)g], hi = first[(size_t)g + 1];
+        if (hi == lo) continue;
+        c->ref.assign(refs + ref_offsets[g], refs + ref_offsets[g + 1]);
+        int rc = build_profile(c);
+        if (rc) return rc;
+        int32_t lb = 1;
+        int64_t cells = 0;
+        for (int64_t s = lo; s < hi; ++s) {
+            const int64_t len = soff[(size_t)s + 1] - soff[(size_t)s];
+            lb = std::max<int32_t>(lb, (int32_t)len);
+            cells += (int64_t)c->ref.size() * len;
+        }
+        c->n = hi - lo;
+        c->lb_max = lb;
+        c->cells = cells;
+        c->stride = stride_all;
+        if ((rc = configure(c))) return rc;
+        if ((rc = launch_range(c, lo))) return rc;
+    }
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    // back to the callers' order
+    std::vector<nw::Stat> st((size_t)n);
+    if (n) HIP_OR_FAIL(c, hipMemcpy(st.data(), c->d_stats.p, sizeof(nw::Stat) * (size_t)n, hipMemcpyDeviceToHost));
+    if (stats)
+        for (int64_t s = 0; s < n; ++s) std::memcpy(&stats[order[(size_t)s]], &st[(size_t)s], sizeof(nw::Stat));
+    if (aln_out) {
+        std::vector<char> rows;
+        for (int32_t g = 0; g < n_refs; ++g) {
+            const int64_t lo = first[(size_t)g], hi = first[(size_t)g + 1];
+            if (hi == lo) continue;
+            rows.resize((size_t)(hi - lo) * 3 * stride_all);
+            HIP_OR_FAIL(c, hipMemcpy(rows.data(), c->d_out.p + lo * 3 * stride_all, rows.size(), hipMemcpyDeviceToHost));
+            for (int64_t s = lo; s < hi; ++s)
+                for (int k = 0; k < 3; ++k)
+                    std::memcpy(aln_out + (order[(size_t)s] * 3 + k) * stride, rows.data() + ((s - lo) * 3 + k) * stride_all,
+                                (size_t)stride_all);
+        }
+    }
+    c->n = 0;          // the per-batch getters describe nw_batch_upload batches only
+    c->ran = false;
+    return NW_OK;
+}
+
+int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int32_t max_read_len) {
+    if (!ref_offsets || n_refs <= 0) return 0;
+    int64_t st = 16;
+    for (int32_t g = 0; g < n_refs; ++g)
+        st = std::max(st, stride_for((int)(ref_offsets[g + 1] - ref_offsets[g]), std::max(max_read_len, 1)));
+    return st;
 }
 
 }  // extern "C"

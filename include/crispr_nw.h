@@ -120,6 +120,17 @@ int64_t nw_batch_fallbacks(nw_ctx* ctx);
  * into several passes the first two cover the first pass only. */
 int nw_batch_kernel_times(nw_ctx* ctx, float* fill_ms, float* walk_ms, float* rest_ms);
 
+/* Pooled batch (replaces one CRISPResso + needle process per amplicon,
+ * CRISPRessoPooled.py:882-908): n_refs amplicons packed in `refs` with
+ * ref_offsets[n_refs + 1]; read r is aligned against amplicon ref_of_read[r].
+ * Outputs as nw_align_batch, in the callers' read order; `stride` at least
+ * nw_required_stride_multi(ref_offsets, n_refs, longest read).  Synchronous.
+ * Leaves the context without an uploaded batch (the nw_batch_* getters). */
+int nw_align_multi(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
+                   const char* reads, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
+                   char* aln_out, int64_t stride, nw_stat* stats);
+int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int32_t max_read_len);
+
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated
  * read ids, concatenated.  Writes at most cap bytes; returns the number of

@@ -44,5 +44,25 @@ class OracleAligner:
     def align(self, reads):
         return self.align_packed(*pack_reads(reads))
 
+    def align_multi(self, amplicons, buf, offsets, amplicon_of_read):
+        """Per-amplicon oracle runs, reassembled in read order (reference for nw_align_multi)."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        n = len(offsets) - 1
+        lens = np.diff(offsets)
+        stride = max(((len(a) + int(lens.max() if n else 1) + 15) // 16) * 16 for a in amplicons)
+        stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+        aln = np.zeros((n, 3, stride), dtype=np.uint8)
+        for g, amp in enumerate(amplicons):
+            sel = np.flatnonzero(np.asarray(amplicon_of_read) == g)
+            if not len(sel):
+                continue
+            sub = [bytes(buf[offsets[r]:offsets[r + 1]]) for r in sel]
+            part = self.__class__(options=self.options)
+            part.set_reference(amp)
+            b = part.align_packed(*pack_reads([x.decode() for x in sub]))
+            stats[sel] = b.stats
+            aln[sel, :, : b.aln.shape[2]] = b.aln
+        return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
+
     def close(self):
         pass

@@ -293,3 +293,33 @@ def test_needle_cli_matches_oracle_cli(tmp_path, oracle):
     cpu = subprocess.run([oracle.CLI] + args, input=fasta, capture_output=True, text=True, check=True).stdout
     strip = lambda t: t[t.index("#=="): t.rindex("#---------------------------------------\n#---")]  # noqa: E731
     assert strip(gpu) == strip(cpu)
+
+
+def test_pooled_multi_amplicon(gpu_aligner_factory, oracle):
+    """nw_align_multi: many amplicons in one call (pair-table, profile and int32
+    kernel paths by amplicon length), empty and one-read groups, read order kept;
+    the context aligns single-amplicon batches correctly afterwards."""
+    from crispresso_amd.pooled import align_pooled
+    from tests.helpers import OracleAligner
+
+    rng = np.random.Generator(np.random.PCG64(77))
+    lengths = [150, 180, 64, 231, 256, 257, 300, 420, 199]
+    amps = [synth.random_amplicon(L, 900 + g) for g, L in enumerate(lengths)]
+    reads = []
+    for g, a in enumerate(amps):
+        k = [120, 0, 1, 333, 64, 91, 150, 40, 257][g]
+        reads.append(synth.reads_from(a, k, 950 + g, synth.PARITY_MIX) if k else [])
+    al = gpu_aligner_factory()
+    got = align_pooled(amps, reads, al)
+    want = align_pooled(amps, reads, OracleAligner())
+    for g in range(len(amps)):
+        assert len(got[g]) == len(want[g])
+        for f in FIELDS:
+            assert np.array_equal(got[g].stats[f], want[g].stats[f]), (g, f)
+        for i in range(len(want[g])):
+            L = int(want[g].stats["aln_len"][i])
+            assert np.array_equal(got[g].aln[i, :, :L], want[g].aln[i, :, :L]), (g, i)
+    amp = amps[3]
+    buf, off = synth.reads_from(amp, 500, 999, synth.PARITY_MIX)
+    al.set_reference(amp)
+    assert_same(oracle, amp, buf, off, al.align_packed(buf, off), "after-multi")
