@@ -38,8 +38,27 @@ EXPORTS = (
     "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload",
     "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
-    "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair",
+    "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
 )
+
+# Every symbol include/crispr_quant.h declares.
+QUANT_EXPORTS = (
+    "nwq_create", "nwq_destroy", "nwq_last_error", "nwq_set_params", "nwq_totals_words", "nwq_run",
+    "nwq_run_device",
+)
+
+
+class NwqParams(ctypes.Structure):
+    """nwq_params (include/crispr_quant.h)."""
+    _fields_ = [("len_amplicon", c_int32), ("include_mask", c_void_p), ("exon_mask", c_void_p),
+                ("splicing_mask", c_void_p), ("ignore_substitutions", c_int32), ("ignore_insertions", c_int32),
+                ("ignore_deletions", c_int32), ("window_around_sgrna", c_int32),
+                ("hide_mutations_outside_window_nhej", c_int32), ("amplicon_has_n", c_int32)]
+
+
+NWQ_PRE_UNMODIFIED, NWQ_PRE_HDR, NWQ_PRE_MIXED = 1, 2, 4
+NWQ_NVEC, NWQ_NCOUNTERS = 15, 4
+NWQ_READ_DTYPE = np.dtype([(f, "<i4") for f in ("cls", "n_mutated", "n_inserted", "n_deleted")])
 
 
 class NativeLibraryError(RuntimeError):
@@ -84,6 +103,16 @@ def load() -> ctypes.CDLL:
         "nw_align_multi": (c_int, [ctx_p, c_char_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
                                    c_void_p, c_int64, c_void_p]),
         "nw_required_stride_multi": (c_int64, [c_void_p, c_int32, c_int32]),
+        "nw_batch_device_output": (c_int, [ctx_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)]),
+        "nwq_create": (c_int, [c_int, POINTER(c_void_p)]),
+        "nwq_destroy": (None, [ctx_p]),
+        "nwq_last_error": (c_char_p, [ctx_p]),
+        "nwq_set_params": (c_int, [ctx_p, POINTER(NwqParams)]),
+        "nwq_totals_words": (c_int64, [ctx_p, c_int64]),
+        "nwq_run": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                            POINTER(c_float)]),
+        "nwq_run_device": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                   c_void_p, POINTER(c_float)]),
         "nw_format_srspair": (
             c_int64,
             [c_void_p, c_int64, c_char_p, c_char_p, c_float, c_float, c_int32, c_int32, c_void_p, c_int64,
@@ -102,7 +131,7 @@ def exported_symbols() -> dict:
     """Map of each declared symbol to whether the loaded library exports it."""
     lib = load()
     out = {}
-    for name in EXPORTS:
+    for name in EXPORTS + QUANT_EXPORTS:
         try:
             getattr(lib, name)
             out[name] = True

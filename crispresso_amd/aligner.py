@@ -176,6 +176,14 @@ class GpuAligner:
                     "nw_batch_kernel_times")
         return dict(zip(("fill_ms", "walk_ms", "rest_ms"), (float(v.value) for v in vals)))
 
+    def device_output(self):
+        """(d_aln, stride, d_stats) device pointers of the last run's resident output
+        (nw_batch_device_output); valid until the next upload / align."""
+        d_aln, d_stats, stride = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        self._check(self.lib.nw_batch_device_output(self._h, ctypes.byref(d_aln), ctypes.byref(stride),
+                                                    ctypes.byref(d_stats)), "nw_batch_device_output")
+        return int(d_aln.value), int(stride.value), int(d_stats.value)
+
     def download(self, n: int, max_len: int) -> AlignmentBatch:
         stride = int(self.lib.nw_required_stride(self._h, max(int(max_len), 1)))
         stats = np.zeros(n, dtype=_lib.STAT_DTYPE)

@@ -617,6 +617,17 @@ int nw_batch_kernel_times(nw_ctx* c, float* fill_ms, float* walk_ms, float* rest
     return NW_OK;
 }
 
+int nw_batch_device_output(nw_ctx* c, void** d_aln, int64_t* stride, void** d_stats) {
+    if (!c) return NW_E_INVALID;
+    if (!c->ran || c->n <= 0) return fail(c, NW_E_STATE, "no resident batch (run nw_batch_run_async first)");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    if (d_aln) *d_aln = c->d_out.p;
+    if (stride) *stride = c->stride;
+    if (d_stats) *d_stats = c->d_stats.p;
+    return NW_OK;
+}
+
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;

@@ -1,0 +1,628 @@
+// nw_quant.hip -- indel / substitution quantification of aligned reads on gfx950,
+// and its C ABI (include/crispr_quant.h).
+//
+// Replaces process_df_chunk (CRISPRessoCORE.py:428-753), which walks a DataFrame
+// row by row in Python: regex runs of '.' / '-' over the three alignment strings,
+// ref_positions lookups (CORE:2055-2067), set intersections with INCLUDE_IDXS /
+// EXON_POSITIONS / SPLICING_POSITIONS and numpy fancy-index increments of fifteen
+// per-position vectors.
+//
+// One wave per read, 256 alignment columns per step (4 per lane, dword loads of
+// the three rows).  Per step: base-count prefix (amplicon index of every column)
+// and run boundaries from ballots + mbcnt; substitution positions and deletion
+// run ids are written into a per-wave position array in LDS, run records
+// (deletion: first position, size, window/exon/splice hits from prefix counts;
+// insertion: the two flank positions of CORE:520-526) into per-wave run lists.
+// A run pass classifies the read (HDR / MIXED / NHEJ / UNMODIFIED, CORE:530-575),
+// applies the NHEJ window filter with the reference's quirks (CORE:611-641) and
+// the frameshift analysis (CORE:653-725); a position pass then adds the read's
+// contributions to the block's LDS copy of the vectors -- once per distinct
+// position, which is what numpy's buffered `vec[idx] += 1` does -- and clears the
+// position array for the next read.  Blocks write their vectors to a partial
+// slab; a second kernel sums the slabs into int64 totals.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/crispr_nw.h"
+#include "../../include/crispr_quant.h"
+#include "nw_common.h"
+
+namespace nwq {
+
+enum : int { V_INS, V_DEL, V_MUT, V_ANY, V_INS_MIX, V_DEL_MIX, V_MUT_MIX, V_INS_HDR, V_DEL_HDR, V_MUT_HDR,
+             V_INS_NC, V_DEL_NC, V_MUT_NC, V_AVG_DEL, V_AVG_INS, NV };
+enum : int { C_FS, C_NONFS, C_NONMOD, C_SPLICE };
+enum : unsigned { F_IGN_SUB = 1, F_IGN_INS = 2, F_IGN_DEL = 4, F_HIDE = 8, F_FRAMESHIFT = 16, F_NFIX = 32 };
+enum : unsigned { T_INC = 1, T_EXON = 2, T_SPL = 4 };                 // position table bits
+enum : unsigned { P_SUB = 1, P_INS = 2 };                              // position marks; bits 16+: del run + 1
+enum : int { R_INC = 1, R_EXON = 2, R_SPL = 4, R_KEPT = 8, R_POST = 16 };   // run flags
+
+typedef short run4 __attribute__((ext_vector_type(4)));   // deletion {pos, size, flags, exon count}
+                                                          // insertion {flank a, flank b, size, flags}
+struct QArgs {
+    uint8_t* aln;
+    int64_t stride;
+    const int32_t* len;
+    int64_t len_stride;
+    const uint8_t* pre;
+    int64_t n;
+    int4* out;
+    uint32_t* partial;       // [gridDim.x][nwords]
+    const int32_t* prefix;   // [3][LEN + 1] prefix counts of INC / EXON / SPL, then [LEN] table bytes
+    int32_t LEN, H, run_cap, window, nwords, wave_words, base_words;
+    uint32_t flags;
+};
+
+__device__ __forceinline__ unsigned mbcnt(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+
+// exclusive prefix over lanes of a per-lane count < 2^BITS, and the wave total
+template <int BITS>
+__device__ __forceinline__ int lane_prefix(unsigned v, int* total) {
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const unsigned long long m = ballot((v >> b) & 1u);
+        pre += (int)mbcnt(m) << b;
+        tot += __popcll(m) << b;
+    }
+    *total = tot;
+    return pre;
+}
+
+__device__ __forceinline__ bool wave_any(bool p) { return ballot(p) != 0ull; }
+
+__device__ __forceinline__ void vadd(uint32_t* h, int v, int LEN, unsigned x) {
+    if (x) atomicAdd(h + v * LEN, x);
+}
+
+__global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
+    extern __shared__ uint32_t smem[];
+    const int LEN = a.LEN;
+    uint32_t* blk = smem;                                // vectors, counters, histograms
+    int32_t* incp = (int32_t*)(blk + a.nwords);
+    int32_t* exop = incp + (LEN + 1);
+    int32_t* splp = exop + (LEN + 1);
+    uint8_t* tbl = (uint8_t*)(splp + (LEN + 1));
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wpb = blockDim.x >> 6;
+    uint32_t* posw = smem + a.base_words + wave * a.wave_words;
+    run4* druns = (run4*)(posw + ((LEN + 1) & ~1));
+    run4* iruns = druns + a.run_cap;
+
+    for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) blk[i] = 0;
+    const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
+    for (int i = threadIdx.x; i < pref_words; i += blockDim.x) incp[i] = a.prefix[i];
+    for (int i = threadIdx.x; i < wpb * a.wave_words; i += blockDim.x) smem[a.base_words + i] = 0;
+    __syncthreads();
+
+    const unsigned flags = a.flags;
+    const bool nfix = flags & F_NFIX;
+    const unsigned ign_sub = (flags & F_IGN_SUB) ? 0u : 0xfu;
+    const unsigned ign_ins = (flags & F_IGN_INS) ? 0u : 0xfu;
+    const unsigned ign_del = (flags & F_IGN_DEL) ? 0u : 0xfu;
+    uint32_t* ctr = blk + NV * LEN;
+    uint32_t* hin = ctr + 4;
+    uint32_t* hfs = hin + a.H;
+
+    const int64_t tw = (int64_t)gridDim.x * wpb;
+    for (int64_t r = (int64_t)blockIdx.x * wpb + wave; r < a.n; r += tw) {
+        const unsigned pre = a.pre[r];
+        const int L = a.len[r * a.len_stride];
+        const bool unmod_in = pre & NWQ_PRE_UNMODIFIED;
+        if ((unmod_in && !nfix) || L <= 0 || L > a.stride) {
+            if (lane == 0) a.out[r] = make_int4((unmod_in && !nfix) ? 0 : -1, 0, 0, 0);
+            continue;
+        }
+        uint8_t* Rrow = a.aln + r * 3 * a.stride;
+        uint8_t* Mrow = Rrow + a.stride;
+        const uint8_t* Srow = Mrow + a.stride;
+        const unsigned f0 = (nfix && Rrow[0] == 'N') ? (unsigned)'|' : (unsigned)Mrow[0];
+
+        int Bc = 0, nds = 0, nde = 0, nis = 0, nie = 0;
+        int prev_state = 0;
+        unsigned nsub = 0, nsub_inc = 0, subbits = 0;   // subbits: 1 exon, 2 splice, 4 exon&inc, 8 splice&inc
+        bool neq = false, oob = false;
+        for (int cb = 0; cb <= L; cb += 256) {
+            const int c0 = cb + 4 * lane;
+            uint32_t dr = 0, dm = 0, ds = 0;
+            if (c0 < L) {
+                dr = *(const uint32_t*)(Rrow + c0);
+                dm = *(const uint32_t*)(Mrow + c0);
+                ds = *(const uint32_t*)(Srow + c0);
+            }
+            unsigned isb = 0, gR = 0, gS = 0, dot = 0;
+            uint32_t dmf = dm;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (c0 + k >= L) break;
+                const unsigned rc = (dr >> (8 * k)) & 255u, sc = (ds >> (8 * k)) & 255u;
+                unsigned mc = (dm >> (8 * k)) & 255u;
+                const bool base = rc == 'A' || rc == 'C' || rc == 'G' || rc == 'T' || rc == 'N';
+                isb |= (unsigned)base << k;
+                gR |= (unsigned)(rc == '-') << k;
+                gS |= (unsigned)(sc == '-') << k;
+                if (nfix && rc == 'N') {
+                    mc = '|';
+                    dmf = (dmf & ~(255u << (8 * k))) | ((unsigned)'|' << (8 * k));
+                }
+                dot |= (unsigned)(mc == '.') << k;
+                neq |= mc != f0;
+            }
+            if (nfix && dmf != dm) *(uint32_t*)(Mrow + c0) = dmf;
+            gR &= ign_ins;
+            gS &= ign_del;
+            dot &= ign_sub;
+            // state of the column before this lane's first one
+            const int st = (int)(((gS >> 3) & 1u) | (((gR >> 3) & 1u) << 1));
+            const int pl = nw::shr1(st, prev_state);
+            const unsigned pS = ((gS << 1) | (unsigned)(pl & 1)) & 0xfu;
+            const unsigned pR = ((gR << 1) | (unsigned)((pl >> 1) & 1)) & 0xfu;
+            const unsigned dstart = gS & ~pS, dend = ~gS & pS & 0xfu;
+            const unsigned istart = gR & ~pR, iend = ~gR & pR & 0xfu;
+
+            int tb, tds, tde, tis, tie;
+            const int Bl = Bc + lane_prefix<3>(__popc(isb), &tb);
+            const int dsp = nds + lane_prefix<2>(__popc(dstart), &tds);
+            const int dep = nde + lane_prefix<2>(__popc(dend), &tde);
+            const int isp = nis + lane_prefix<2>(__popc(istart), &tis);
+            const int iep = nie + lane_prefix<2>(__popc(iend), &tie);
+
+            // starts, deletion marks, substitutions
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned lt = (1u << k) - 1u, bit = 1u << k;
+                const int Bk = Bl + __popc(isb & lt);
+                if (dstart & bit) druns[dsp + __popc(dstart & lt)].x = (short)Bk;
+                if (gS & bit) {
+                    const int jr = dsp + __popc(dstart & (lt | bit)) - 1;
+                    if (Bk < LEN) posw[Bk] = (uint32_t)(jr + 1) << 16;
+                    else oob = true;
+                }
+                if (istart & bit) iruns[isp + __popc(istart & lt)].x = (short)(c0 + k);
+                if (dot & bit) {
+                    if (Bk < LEN) {
+                        posw[Bk] = P_SUB;
+                        const unsigned t = tbl[Bk];
+                        ++nsub;
+                        nsub_inc += t & T_INC;
+                        subbits |= ((t & T_EXON) ? 1u : 0u) | ((t & T_SPL) ? 2u : 0u);
+                        if (t & T_INC) subbits |= ((t & T_EXON) ? 4u : 0u) | ((t & T_SPL) ? 8u : 0u);
+                    } else {
+                        oob = true;
+                    }
+                }
+            }
+            // ends (their starts are in LDS by now: one wave, in-order LDS queue)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned lt = (1u << k) - 1u, bit = 1u << k;
+                const int Bk = Bl + __popc(isb & lt);
+                if ((dend & bit) && Bk <= LEN) {
+                    const int j = dep + __popc(dend & lt);
+                    const int ps = druns[j].x;
+                    const int f = (incp[Bk] - incp[ps] > 0 ? R_INC : 0) | (splp[Bk] - splp[ps] > 0 ? R_SPL : 0);
+                    druns[j] = run4{(short)ps, (short)(Bk - ps), (short)f, (short)(exop[Bk] - exop[ps])};
+                }
+                if ((iend & bit) && Bk <= LEN) {
+                    const int j = iep + __popc(iend & lt);
+                    const int c = c0 + k;
+                    const int s0 = iruns[j].x;
+                    const int fa = s0 > 0 ? Bk - 1 : -1;
+                    const int fb = c < L ? Bk : (Bk > 0 ? -Bk : -1);
+                    int f = 0;
+                    if (fa >= 0 && fa < LEN) f |= tbl[fa];
+                    if (fb >= 0 && fb < LEN) f |= tbl[fb];
+                    // T_* and R_INC/R_EXON/R_SPL share bit positions
+                    iruns[j] = run4{(short)fa, (short)fb, (short)(c - s0), (short)f};
+                }
+            }
+            Bc += tb;
+            nds += tds;
+            nde += tde;
+            nis += tis;
+            nie += tie;
+            prev_state = __builtin_amdgcn_readlane(st, 63);
+        }
+
+        const bool bad = Bc != LEN || wave_any(oob);
+        const bool unmod = unmod_in || (nfix && !wave_any(neq));
+        const bool counting = !bad && !unmod;
+        int cls = 0, n_mut = 0, n_ins = 0, n_del = 0;
+        bool windowed = false, noncoding = false;
+        if (counting) {
+            const int nsub_t = (int)nw::wave_sum_u32(nsub), nsubi_t = (int)nw::wave_sum_u32(nsub_inc);
+            bool hit_l = false;
+            for (int j = lane; j < nds; j += 64) hit_l |= (druns[j].z & R_INC) != 0;
+            for (int j = lane; j < nis; j += 64) hit_l |= (iruns[j].w & R_INC) != 0;
+            const bool hit = nsubi_t > 0 || wave_any(hit_l);
+            cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
+            windowed = cls == 1 && a.window != 0;
+
+            bool kept_l = false;
+            for (int j = lane; j < nds; j += 64) kept_l |= !windowed || (druns[j].z & R_INC);
+            const bool post_sel = windowed && wave_any(kept_l);
+            int ndel_l = 0, exdel_l = 0;
+            bool spldel_l = false;
+            for (int j = lane; j < nds; j += 64) {
+                run4 d = druns[j];
+                const bool kept = !windowed || (d.z & R_INC);
+                const bool post = post_sel ? kept : true;
+                d.z |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
+                druns[j] = d;
+                ndel_l += kept ? d.y : 0;
+                exdel_l += post ? d.w : 0;
+                spldel_l |= post && (d.z & R_SPL);
+            }
+            int nins_l = 0, insex_len_l = 0;
+            bool insex_l = false, insspl_l = false;
+            for (int j = lane; j < nis; j += 64) {
+                const run4 e = iruns[j];
+                const bool kept = !windowed || (e.w & R_INC);
+                const int wa = e.x < 0 ? e.x + LEN : e.x, wb = e.y < 0 ? e.y + LEN : e.y;
+                atomicOr(posw + wa, P_INS);
+                atomicOr(posw + wb, P_INS);
+                insspl_l |= (e.w & R_SPL) != 0;
+                if (kept) {
+                    nins_l += e.z;
+                    if (e.w & R_EXON) { insex_l = true; insex_len_l += e.z; }
+                    if (cls != 0) {
+                        atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)e.z);
+                        if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)e.z);
+                    }
+                }
+            }
+            n_mut = windowed ? nsubi_t : nsub_t;
+            n_ins = nw::wave_sum(nins_l);
+            n_del = nw::wave_sum(ndel_l);
+            if ((flags & F_FRAMESHIFT) && cls != 0) {
+                const unsigned sb = (wave_any(subbits & 1u) ? 1u : 0u) | (wave_any(subbits & 2u) ? 2u : 0u) |
+                                    (wave_any(subbits & 4u) ? 4u : 0u) | (wave_any(subbits & 8u) ? 8u : 0u);
+                const bool sub_exon = windowed ? (sb & 4u) : (sb & 1u);
+                const bool sub_spl = windowed ? (sb & 8u) : (sb & 2u);
+                const int exdel = nw::wave_sum(exdel_l);
+                const bool insex = wave_any(insex_l);
+                const int eff = nw::wave_sum(insex_len_l) - exdel;
+                const bool exon_mod = insex || exdel > 0 || sub_exon;
+                const bool has_lens = insex || exdel > 0;
+                const bool spliced = sub_spl || wave_any(spldel_l) || wave_any(insspl_l);
+                if (lane == 0) {
+                    if (spliced) atomicAdd(ctr + C_SPLICE, 1u);
+                    if (exon_mod) {
+                        if (!has_lens) {
+                            atomicAdd(ctr + C_NONFS, 1u);
+                            atomicAdd(hin + LEN, 1u);
+                        } else if (eff % 3 == 0) {
+                            atomicAdd(ctr + C_NONFS, 1u);
+                            atomicAdd(hin + LEN + eff, 1u);
+                        } else {
+                            atomicAdd(ctr + C_FS, 1u);
+                            atomicAdd(hfs + LEN + eff, 1u);
+                        }
+                    } else {
+                        atomicAdd(ctr + C_NONMOD, 1u);
+                    }
+                }
+                noncoding = !exon_mod;
+            }
+        }
+
+        // position pass: the read's per-position vector increments; clears the marks
+        const bool hide = flags & F_HIDE;
+        for (int p = lane; p < LEN; p += 64) {
+            const uint32_t w = posw[p];
+            if (!w) continue;
+            posw[p] = 0;
+            if (!counting) continue;
+            const unsigned sub = w & P_SUB, ins = (w >> 1) & 1u;
+            const int dj = (int)(w >> 16);
+            int rf = 0, dsz = 0;
+            if (dj) {
+                const run4 d = druns[dj - 1];
+                rf = d.z;
+                dsz = d.y;
+            }
+            const unsigned del = dj ? 1u : 0u;
+            const unsigned sub_post = (sub && (!windowed || (tbl[p] & T_INC))) ? 1u : 0u;
+            const unsigned del_post = (del && (rf & R_POST)) ? 1u : 0u;
+            uint32_t* h = blk + p;
+            if (cls == 3) {
+                vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
+            } else if (cls == 2) {
+                vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
+            } else if (cls == 1) {
+                vadd(h, V_MUT, LEN, hide ? sub_post : sub);
+                vadd(h, V_DEL, LEN, hide ? del_post : del);
+                vadd(h, V_INS, LEN, ins);
+            }
+            vadd(h, V_ANY, LEN, (sub | del | ins) ? 1u : 0u);
+            if (noncoding) {
+                vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
+            }
+            if (cls != 0 && del && (rf & R_KEPT)) vadd(h, V_AVG_DEL, LEN, (unsigned)dsz);
+        }
+        // counts are written only for rows left modified (CORE:651-660)
+        if (lane == 0) a.out[r] = cls ? make_int4(cls, n_mut, n_ins, n_del) : make_int4(bad ? -1 : 0, 0, 0, 0);
+    }
+
+    __syncthreads();
+    uint32_t* dst = a.partial + (int64_t)blockIdx.x * a.nwords;
+    for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) dst[i] = blk[i];
+}
+
+__global__ void quant_reduce(const uint32_t* __restrict__ partial, int nblocks, int nwords, int64_t* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nwords) return;
+    int64_t s = 0;
+    for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * nwords + i];
+    out[i] = s;
+}
+
+}  // namespace nwq
+
+// ------------------------------------------------------------------ host side
+
+namespace {
+
+template <class T>
+struct QBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+constexpr int kMaxLds = 160 * 1024;
+
+}  // namespace
+
+struct nwq_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    bool have_params = false;
+    int32_t LEN = 0;
+    uint32_t flags = 0;
+    int32_t window = 0;
+    std::vector<int32_t> prefix;     // host copy of QArgs::prefix
+    QBuf<int32_t> d_prefix;
+    QBuf<uint32_t> d_partial;
+    QBuf<int64_t> d_totals;
+    QBuf<uint8_t> d_aln, d_pre;
+    QBuf<int32_t> d_len;
+    QBuf<nwq_read> d_out;
+};
+
+namespace {
+
+int qfail(nwq_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define QHIP(c, expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) return qfail((c), NW_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int64_t hist_size(int32_t LEN, int64_t stride) { return (int64_t)LEN + stride + 1; }
+int64_t words_for(int32_t LEN, int64_t stride) { return (int64_t)nwq::NV * LEN + 4 + 2 * hist_size(LEN, stride); }
+
+struct QGeom {
+    int wpb, grid, lds, run_cap, wave_words, base_words, nwords;
+};
+
+int geometry(nwq_ctx* c, int64_t stride, int64_t n, QGeom* g) {
+    const int LEN = c->LEN;
+    g->nwords = (int)words_for(LEN, stride);
+    g->run_cap = (int)((stride + 1) / 2 + 1);
+    const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
+    g->base_words = (g->nwords + pref_words + 1) & ~1;
+    g->wave_words = ((LEN + 1) & ~1) + 4 * g->run_cap;
+    g->wpb = 0;
+    for (int w : {8, 4, 2, 1}) {
+        const int lds = 4 * (g->base_words + w * g->wave_words);
+        // at least two blocks per CU unless even a one-wave block needs more
+        if (lds <= kMaxLds / 2 || (w == 1 && lds <= kMaxLds)) {
+            g->wpb = w;
+            g->lds = lds;
+            break;
+        }
+    }
+    if (!g->wpb)
+        return qfail(c, NW_E_UNSUPPORTED, "quantification state for amplicon length %d / stride %lld exceeds LDS",
+                     LEN, (long long)stride);
+    int per_cu = 0;
+    QHIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwq::quant_kernel, 64 * g->wpb, g->lds));
+    per_cu = std::max(per_cu, 1);
+    const int64_t need = (n + g->wpb - 1) / g->wpb;
+    g->grid = (int)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)c->num_cus * per_cu));
+    return NW_OK;
+}
+
+int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, int64_t len_stride,
+             const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms) {
+    if (!c->have_params) return qfail(c, NW_E_STATE, "nwq_set_params not called");
+    if (stride <= 0 || (stride & 3) || stride >= 32768)
+        return qfail(c, NW_E_INVALID, "stride %lld must be a positive multiple of 4 below 32768", (long long)stride);
+    if (n < 0) return qfail(c, NW_E_INVALID, "negative read count");
+    QGeom g;
+    int rc = geometry(c, stride, n, &g);
+    if (rc) return rc;
+    QHIP(c, c->d_partial.reserve((size_t)g.grid * g.nwords));
+    QHIP(c, c->d_totals.reserve((size_t)g.nwords));
+    nwq::QArgs a;
+    a.aln = d_aln;
+    a.stride = stride;
+    a.len = d_len;
+    a.len_stride = len_stride;
+    a.pre = d_pre;
+    a.n = n;
+    a.out = reinterpret_cast<int4*>(d_out);
+    a.partial = c->d_partial.p;
+    a.prefix = c->d_prefix.p;
+    a.LEN = c->LEN;
+    a.H = (int)hist_size(c->LEN, stride);
+    a.run_cap = g.run_cap;
+    a.window = c->window;
+    a.nwords = g.nwords;
+    a.wave_words = g.wave_words;
+    a.base_words = g.base_words;
+    a.flags = c->flags;
+    QHIP(c, hipEventRecord(c->ev0, c->stream));
+    hipLaunchKernelGGL(nwq::quant_kernel, dim3(g.grid), dim3(64 * g.wpb), g.lds, c->stream, a);
+    QHIP(c, hipGetLastError());
+    hipLaunchKernelGGL(nwq::quant_reduce, dim3((g.nwords + 255) / 256), dim3(256), 0, c->stream, c->d_partial.p,
+                       g.grid, g.nwords, c->d_totals.p);
+    QHIP(c, hipGetLastError());
+    QHIP(c, hipEventRecord(c->ev1, c->stream));
+    QHIP(c, hipMemcpyAsync(totals, c->d_totals.p, sizeof(int64_t) * (size_t)g.nwords, hipMemcpyDeviceToHost,
+                           c->stream));
+    QHIP(c, hipStreamSynchronize(c->stream));
+    if (kernel_ms) QHIP(c, hipEventElapsedTime(kernel_ms, c->ev0, c->ev1));
+    return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nwq_create(int device, nwq_ctx** out) {
+    if (!out) return NW_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NW_E_HIP;
+    nwq_ctx* c = new nwq_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        nwq_destroy(c);
+        return NW_E_HIP;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    *out = c;
+    return NW_OK;
+}
+
+void nwq_destroy(nwq_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    c->d_prefix.release();
+    c->d_partial.release();
+    c->d_totals.release();
+    c->d_aln.release();
+    c->d_pre.release();
+    c->d_len.release();
+    c->d_out.release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* nwq_last_error(const nwq_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int nwq_set_params(nwq_ctx* c, const nwq_params* p) {
+    if (!c || !p) return NW_E_INVALID;
+    const int LEN = p->len_amplicon;
+    if (LEN <= 0 || LEN >= 32768) return qfail(c, NW_E_INVALID, "len_amplicon %d out of range (1..32767)", LEN);
+    if (!p->include_mask) return qfail(c, NW_E_INVALID, "include_mask is required");
+    if (hipSetDevice(c->device) != hipSuccess) return qfail(c, NW_E_HIP, "hipSetDevice failed");
+    const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
+    c->prefix.assign((size_t)pref_words, 0);
+    int32_t* inc = c->prefix.data();
+    int32_t* exo = inc + (LEN + 1);
+    int32_t* spl = exo + (LEN + 1);
+    uint8_t* tbl = reinterpret_cast<uint8_t*>(spl + (LEN + 1));
+    for (int i = 0; i < LEN; ++i) {
+        const bool bi = p->include_mask[i] != 0;
+        const bool be = p->exon_mask && p->exon_mask[i];
+        const bool bs = p->exon_mask && p->splicing_mask && p->splicing_mask[i];
+        tbl[i] = (uint8_t)((bi ? nwq::T_INC : 0) | (be ? nwq::T_EXON : 0) | (bs ? nwq::T_SPL : 0));
+        inc[i + 1] = inc[i] + bi;
+        exo[i + 1] = exo[i] + be;
+        spl[i + 1] = spl[i] + bs;
+    }
+    QHIP(c, c->d_prefix.reserve((size_t)pref_words));
+    QHIP(c, hipMemcpy(c->d_prefix.p, c->prefix.data(), sizeof(int32_t) * (size_t)pref_words, hipMemcpyHostToDevice));
+    c->LEN = LEN;
+    c->window = p->window_around_sgrna;
+    c->flags = (p->ignore_substitutions ? nwq::F_IGN_SUB : 0) | (p->ignore_insertions ? nwq::F_IGN_INS : 0) |
+               (p->ignore_deletions ? nwq::F_IGN_DEL : 0) | (p->hide_mutations_outside_window_nhej ? nwq::F_HIDE : 0) |
+               (p->exon_mask ? nwq::F_FRAMESHIFT : 0) | (p->amplicon_has_n ? nwq::F_NFIX : 0);
+    c->have_params = true;
+    return NW_OK;
+}
+
+int64_t nwq_totals_words(const nwq_ctx* c, int64_t stride) {
+    return (c && c->have_params) ? words_for(c->LEN, stride) : 0;
+}
+
+int nwq_run(nwq_ctx* c, uint8_t* aln, int64_t stride, const int32_t* aln_len, const uint8_t* pre, int64_t n,
+            nwq_read* out, int64_t* totals, float* kernel_ms) {
+    if (!c) return NW_E_INVALID;
+    if (n > 0 && (!aln || !aln_len || !pre || !out)) return qfail(c, NW_E_INVALID, "null buffer");
+    if (!totals) return qfail(c, NW_E_INVALID, "null totals");
+    QHIP(c, hipSetDevice(c->device));
+    const size_t nn = (size_t)std::max<int64_t>(n, 1);
+    QHIP(c, c->d_aln.reserve(nn * 3 * (size_t)stride));
+    QHIP(c, c->d_len.reserve(nn));
+    QHIP(c, c->d_pre.reserve(nn));
+    QHIP(c, c->d_out.reserve(nn));
+    if (n > 0) {
+        QHIP(c, hipMemcpyAsync(c->d_aln.p, aln, (size_t)n * 3 * stride, hipMemcpyHostToDevice, c->stream));
+        QHIP(c, hipMemcpyAsync(c->d_len.p, aln_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+        QHIP(c, hipMemcpyAsync(c->d_pre.p, pre, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    }
+    int rc = run_impl(c, c->d_aln.p, stride, c->d_len.p, 1, c->d_pre.p, n, c->d_out.p, totals, kernel_ms);
+    if (rc) return rc;
+    if (n > 0) {
+        QHIP(c, hipMemcpy(out, c->d_out.p, sizeof(nwq_read) * (size_t)n, hipMemcpyDeviceToHost));
+        if (c->flags & nwq::F_NFIX)
+            QHIP(c, hipMemcpy2D(aln + stride, (size_t)(3 * stride), c->d_aln.p + stride, (size_t)(3 * stride),
+                                (size_t)stride, (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return NW_OK;
+}
+
+int nwq_run_device(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_aln_len, int64_t len_stride,
+                   const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms) {
+    if (!c) return NW_E_INVALID;
+    if (n > 0 && (!d_aln || !d_aln_len || !d_pre || !d_out)) return qfail(c, NW_E_INVALID, "null buffer");
+    if (!totals) return qfail(c, NW_E_INVALID, "null totals");
+    if (len_stride <= 0) return qfail(c, NW_E_INVALID, "len_stride must be positive");
+    QHIP(c, hipSetDevice(c->device));
+    return run_impl(c, d_aln, stride, d_aln_len, len_stride, d_pre, n, d_out, totals, kernel_ms);
+}
+
+}  // extern "C"

@@ -1,0 +1,355 @@
+"""Indel / substitution quantification on the GPU (``process_df_chunk`` and the
+row preparation before it), behind the C ABI of ``include/crispr_quant.h``.
+
+Mirrors, name for name, what ``CRISPResso/CRISPRessoCORE.py`` does after the
+alignment block:
+
+* :func:`compute_cut_points`                -- guides -> cut points, CORE:1290-1341
+* :func:`compute_include_idxs`              -- ``INCLUDE_IDXS``, CORE:2740-2762
+* :func:`compute_exon_positions`            -- ``EXON_POSITIONS`` / ``SPLICING_POSITIONS``, CORE:1414-1455
+* :func:`set_globals` / :func:`globals_from_args` -- the module globals
+  ``run_crispresso`` assigns (CORE:1261-1264) and ``process_df_chunk`` reads
+* :func:`process_df_chunk`                  -- CORE:428-753, same argument
+  (``[df, args]``) and the same 22-element return tuple; the per-row loop runs
+  as one HIP kernel (crispresso_amd/csrc/nw_quant.hip)
+* :func:`quantify_alignments`               -- CORE:2014-2067 + process_df_chunk in
+  one kernel pass: ``UNMODIFIED = score_ref == 100``, ``ignore_n_in_alignment``
+  for amplicons with N (align_str rewritten, as the reference does), then the
+  chunk; also accepts the aligner's device-resident output (no host round trip).
+
+There is no CPU fallback: without the HIP library or a GPU every entry point
+raises :class:`~crispresso_amd._lib.NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+from ._lib import NativeLibraryError
+
+VECTOR_NAMES = (
+    "effect_vector_insertion", "effect_vector_deletion", "effect_vector_mutation", "effect_vector_any",
+    "effect_vector_insertion_mixed", "effect_vector_deletion_mixed", "effect_vector_mutation_mixed",
+    "effect_vector_insertion_hdr", "effect_vector_deletion_hdr", "effect_vector_mutation_hdr",
+    "effect_vector_insertion_noncoding", "effect_vector_deletion_noncoding", "effect_vector_mutation_noncoding",
+    "avg_vector_del_all", "avg_vector_ins_all",
+)
+COUNTER_NAMES = ("modified_frameshift", "modified_non_frameshift", "non_modified_non_frameshift",
+                 "splicing_sites_modified")
+CLASS_NAMES = ("UNMODIFIED", "NHEJ", "HDR", "MIXED")
+
+
+class QuantificationError(RuntimeError):
+    """Rows that are not alignments of the amplicon, or a failed kernel call."""
+
+
+# ------------------------------------------------------------ run_crispresso state
+
+_NT_RC = str.maketrans("ATCGN", "TAGCN")
+
+
+def compute_cut_points(amplicon_seq: str, guide_seq: Optional[str], cleavage_offset: int = -3) -> List[int]:
+    """CORE:1290-1341: forward matches cut at start + offset + len - 1, reverse
+    complement matches at start - offset - 1 (re.finditer, non-overlapping)."""
+    if not guide_seq:
+        return []
+    cuts: List[int] = []
+    for g in guide_seq.strip().upper().split(","):
+        rc = g[::-1].translate(_NT_RC)
+        cuts += [m.start() + cleavage_offset + len(g) - 1 for m in re.finditer(g, amplicon_seq)]
+        cuts += [m.start() - cleavage_offset - 1 for m in re.finditer(rc, amplicon_seq)]
+    return cuts
+
+
+def compute_include_idxs(len_amplicon: int, cut_points: Sequence[int], window_around_sgrna: int,
+                         exclude_bp_from_left: int, exclude_bp_from_right: int) -> set:
+    """CORE:2740-2762 (windows of ``max(1, w // 2)`` around each cut point, or the
+    whole amplicon; minus the excluded ends)."""
+    if cut_points and window_around_sgrna > 0:
+        half = max(1, window_around_sgrna // 2)
+        inc = set()
+        for c in cut_points:
+            inc.update(range(max(0, c - half + 1), min(len_amplicon - 1, c + half + 1)))
+    else:
+        inc = set(range(len_amplicon))
+    if exclude_bp_from_left:
+        inc.difference_update(range(exclude_bp_from_left))
+    if exclude_bp_from_right:
+        inc.difference_update(range(len_amplicon)[-exclude_bp_from_right:])
+    return inc
+
+
+def compute_exon_positions(amplicon_seq: str, coding_seq: Optional[str]):
+    """CORE:1414-1455 -> (EXON_POSITIONS sorted list, SPLICING_POSITIONS set), or (None, None)."""
+    if not coding_seq:
+        return None, None
+    L = len(amplicon_seq)
+    exon, splice = set(), []
+    for e in coding_seq.strip().upper().split(","):
+        st = amplicon_seq.find(e)
+        if st < 0:
+            raise ValueError(f"The coding subsequence/s provided:{e} is(are) not contained in the amplicon sequence.")
+        en = st + len(e)
+        exon.update(range(st, en))
+        splice += [max(0, st - 2), max(0, st - 1), min(L - 1, en), min(L - 1, en + 1)]
+    return sorted(exon), set(splice).difference(exon)
+
+
+@dataclass
+class QuantGlobals:
+    LEN_AMPLICON: int
+    INCLUDE_IDXS: set
+    EXON_POSITIONS: Optional[list] = None
+    SPLICING_POSITIONS: Optional[set] = None
+
+
+_GLOBALS: Optional[QuantGlobals] = None
+
+
+def set_globals(LEN_AMPLICON: int, INCLUDE_IDXS, EXON_POSITIONS=None, SPLICING_POSITIONS=None) -> QuantGlobals:
+    """The ``global`` assignments of run_crispresso (CORE:1261-1264)."""
+    global _GLOBALS
+    _GLOBALS = QuantGlobals(int(LEN_AMPLICON), set(int(x) for x in INCLUDE_IDXS),
+                            None if EXON_POSITIONS is None else sorted(int(x) for x in EXON_POSITIONS),
+                            None if SPLICING_POSITIONS is None else set(int(x) for x in SPLICING_POSITIONS))
+    return _GLOBALS
+
+
+def globals_from_args(args) -> QuantGlobals:
+    """Compute and install the globals from CRISPResso args (amplicon_seq, guide_seq,
+    cleavage_offset, window_around_sgrna, exclude_bp_from_left/right, coding_seq)."""
+    amp = args.amplicon_seq.upper().strip()
+    cuts = compute_cut_points(amp, getattr(args, "guide_seq", None), getattr(args, "cleavage_offset", -3))
+    inc = compute_include_idxs(len(amp), cuts, getattr(args, "window_around_sgrna", 1),
+                               getattr(args, "exclude_bp_from_left", 15), getattr(args, "exclude_bp_from_right", 15))
+    exon, spl = compute_exon_positions(amp, getattr(args, "coding_seq", None))
+    return set_globals(len(amp), inc, exon, spl)
+
+
+# ------------------------------------------------------------------ GPU context
+
+class GpuQuantifier:
+    """One ``nwq_ctx`` (one GPU).  Not thread-safe, like the aligner context."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        ctx = ctypes.c_void_p()
+        rc = self._lib.nwq_create(int(device), ctypes.byref(ctx))
+        if rc != 0:
+            raise NativeLibraryError(f"nwq_create(device={device}) failed with code {rc} (no GPU?)")
+        self._ctx = ctx
+        self.device = device
+        self._len = 0
+        self.last_kernel_ms = 0.0
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.nwq_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self._lib.nwq_last_error(self._ctx).decode(errors="replace")
+            raise QuantificationError(f"{what} failed ({rc}): {msg}")
+
+    def set_params(self, g: QuantGlobals, args, amplicon_has_n: bool = False) -> None:
+        L = g.LEN_AMPLICON
+        inc = np.zeros(L, np.uint8)
+        inc[[p for p in g.INCLUDE_IDXS if 0 <= p < L]] = 1
+        keep = [inc]
+        exon_p = spl_p = None
+        if getattr(args, "coding_seq", None):
+            if g.EXON_POSITIONS is None:
+                raise QuantificationError("coding_seq given but EXON_POSITIONS not set")
+            exon = np.zeros(L, np.uint8)
+            exon[[p for p in g.EXON_POSITIONS if 0 <= p < L]] = 1
+            spl = np.zeros(L, np.uint8)
+            spl[[p for p in (g.SPLICING_POSITIONS or ()) if 0 <= p < L]] = 1
+            keep += [exon, spl]
+            exon_p, spl_p = exon.ctypes.data, spl.ctypes.data
+        p = _lib.NwqParams(
+            len_amplicon=L, include_mask=inc.ctypes.data, exon_mask=exon_p, splicing_mask=spl_p,
+            ignore_substitutions=int(bool(getattr(args, "ignore_substitutions", False))),
+            ignore_insertions=int(bool(getattr(args, "ignore_insertions", False))),
+            ignore_deletions=int(bool(getattr(args, "ignore_deletions", False))),
+            window_around_sgrna=int(getattr(args, "window_around_sgrna", 1) or 0),
+            hide_mutations_outside_window_nhej=int(bool(getattr(args, "hide_mutations_outside_window_NHEJ", False))),
+            amplicon_has_n=int(bool(amplicon_has_n)))
+        self._check(self._lib.nwq_set_params(self._ctx, ctypes.byref(p)), "nwq_set_params")
+        self._len = L
+
+    def run(self, aln: np.ndarray, aln_len: np.ndarray, pre: np.ndarray):
+        """aln uint8 [n, 3, stride] (C-contiguous; markup rewritten in place under the
+        N rule) -> (nwq_read structured array [n], totals int64)."""
+        n, three, stride = aln.shape
+        assert three == 3 and aln.dtype == np.uint8 and aln.flags.c_contiguous
+        aln_len = np.ascontiguousarray(aln_len, dtype=np.int32)
+        pre = np.ascontiguousarray(pre, dtype=np.uint8)
+        out = np.zeros(n, dtype=_lib.NWQ_READ_DTYPE)
+        totals = np.zeros(int(self._lib.nwq_totals_words(self._ctx, stride)), dtype=np.int64)
+        ms = ctypes.c_float()
+        self._check(self._lib.nwq_run(self._ctx, aln.ctypes.data, stride, aln_len.ctypes.data, pre.ctypes.data, n,
+                                      out.ctypes.data, totals.ctypes.data, ctypes.byref(ms)), "nwq_run")
+        self.last_kernel_ms = ms.value
+        return out, totals
+
+    def run_device(self, d_aln: int, stride: int, d_len: int, len_stride: int, d_pre: int, n: int, d_out: int):
+        """Device pointers (ints) on this GPU -> totals int64 (host)."""
+        totals = np.zeros(int(self._lib.nwq_totals_words(self._ctx, stride)), dtype=np.int64)
+        ms = ctypes.c_float()
+        self._check(self._lib.nwq_run_device(self._ctx, d_aln, stride, d_len, len_stride, d_pre, n, d_out,
+                                             totals.ctypes.data, ctypes.byref(ms)), "nwq_run_device")
+        self.last_kernel_ms = ms.value
+        return totals
+
+    def unpack_totals(self, totals: np.ndarray, stride: int) -> Dict:
+        L = self._len
+        nv = _lib.NWQ_NVEC * L
+        vec = totals[:nv].reshape(_lib.NWQ_NVEC, L)
+        ctr = totals[nv:nv + 4]
+        H = L + stride + 1
+        hin = totals[nv + 4:nv + 4 + H]
+        hfs = totals[nv + 4 + H:nv + 4 + 2 * H]
+        return {"vectors": {k: vec[i] for i, k in enumerate(VECTOR_NAMES)},
+                "counters": {k: int(ctr[i]) for i, k in enumerate(COUNTER_NAMES)},
+                "hist_inframe": {int(e) - L: int(hin[e]) for e in np.flatnonzero(hin)},
+                "hist_frameshift": {int(e) - L: int(hfs[e]) for e in np.flatnonzero(hfs)}}
+
+
+_DEFAULT: Dict[int, GpuQuantifier] = {}
+
+
+def default_quantifier(device: int = 0) -> GpuQuantifier:
+    q = _DEFAULT.get(device)
+    if q is None:
+        q = _DEFAULT[device] = GpuQuantifier(device)
+    return q
+
+
+# ------------------------------------------------------------------ DataFrame glue
+
+def pack_rows(ref_seq: Sequence[str], align_str: Sequence[str], align_seq: Sequence[str]):
+    """Three string columns -> (uint8 [n, 3, stride], int32 lengths); stride % 16 == 0."""
+    n = len(ref_seq)
+    lens = np.fromiter((len(s) for s in ref_seq), dtype=np.int32, count=n)
+    stride = max(16, (int(lens.max()) + 15) & ~15) if n else 16
+    aln = np.zeros((n, 3, stride), dtype=np.uint8)
+    for k, col in enumerate((ref_seq, align_str, align_seq)):
+        joined = "".join(s.ljust(stride, "\0") for s in col).encode("ascii")
+        aln[:, k, :] = np.frombuffer(joined, dtype=np.uint8).reshape(n, stride)
+    return aln, lens
+
+
+def pre_flags(unmodified, score_diff=None, score_repaired=None, threshold: float = 98.0) -> np.ndarray:
+    """Per-row input flags: UNMODIFIED, and the HDR / MIXED tests of CORE:536-548
+    (NaN compares false, as in the reference)."""
+    pre = np.asarray(unmodified, dtype=bool).astype(np.uint8) * _lib.NWQ_PRE_UNMODIFIED
+    if score_diff is not None:
+        sd = np.asarray(score_diff, dtype=np.float64)
+        sr = np.asarray(score_repaired, dtype=np.float64)
+        with np.errstate(invalid="ignore"):
+            neg = sd < 0
+            pre |= (neg & (sr >= threshold)).astype(np.uint8) * _lib.NWQ_PRE_HDR
+            pre |= (neg & (sr < threshold)).astype(np.uint8) * _lib.NWQ_PRE_MIXED
+    return pre
+
+
+def _result_tuple(df: pd.DataFrame, reads: np.ndarray, tot: Dict, perform_frameshift: bool):
+    if (reads["cls"] < 0).any():
+        bad = df.index[np.flatnonzero(reads["cls"] < 0)[:5]].tolist()
+        raise QuantificationError(f"rows are not alignments of the amplicon (LEN_AMPLICON bases): {bad}")
+    cls = reads["cls"]
+    um_in = df["UNMODIFIED"].to_numpy(dtype=bool)
+    df["UNMODIFIED"] = um_in | (cls == 0)
+    df["NHEJ"] = cls == 1
+    df["HDR"] = cls == 2
+    df["MIXED"] = cls == 3
+    df["n_mutated"] = reads["n_mutated"].astype(np.int64)
+    df["n_inserted"] = reads["n_inserted"].astype(np.int64)
+    df["n_deleted"] = reads["n_deleted"].astype(np.int64)
+    v = {k: a.astype(np.float64) for k, a in tot["vectors"].items()}
+    c = tot["counters"]
+    return (df, v["effect_vector_insertion"], v["effect_vector_deletion"], v["effect_vector_mutation"],
+            v["effect_vector_any"], v["effect_vector_insertion_mixed"], v["effect_vector_deletion_mixed"],
+            v["effect_vector_mutation_mixed"], v["effect_vector_insertion_hdr"], v["effect_vector_deletion_hdr"],
+            v["effect_vector_mutation_hdr"], v["effect_vector_insertion_noncoding"],
+            v["effect_vector_deletion_noncoding"], v["effect_vector_mutation_noncoding"],
+            dict(tot["hist_inframe"]), dict(tot["hist_frameshift"]), v["avg_vector_del_all"],
+            v["avg_vector_ins_all"], c["modified_frameshift"], c["modified_non_frameshift"],
+            c["non_modified_non_frameshift"], c["splicing_sites_modified"])
+
+
+def _run_df(df: pd.DataFrame, args, g: QuantGlobals, quantifier: Optional[GpuQuantifier], n_rule: bool):
+    q = quantifier or default_quantifier()
+    q.set_params(g, args, amplicon_has_n=n_rule)
+    aln, lens = pack_rows(df["ref_seq"].tolist(), df["align_str"].tolist(), df["align_seq"].tolist())
+    hdr = bool(getattr(args, "expected_hdr_amplicon_seq", None))
+    pre = pre_flags(df["UNMODIFIED"].to_numpy(dtype=bool),
+                    df["score_diff"].to_numpy() if hdr else None,
+                    df["score_repaired"].to_numpy() if hdr else None,
+                    float(getattr(args, "hdr_perfect_alignment_threshold", 98.0)))
+    reads, totals = q.run(aln, lens, pre)
+    if n_rule:
+        mk = aln[:, 1, :]
+        df["align_str"] = [mk[i, :lens[i]].tobytes().decode("ascii") for i in range(len(df))]
+    return reads, q.unpack_totals(totals, aln.shape[2])
+
+
+def process_df_chunk(chunk_input, quantifier: Optional[GpuQuantifier] = None, globals_: Optional[QuantGlobals] = None):
+    """CRISPRessoCORE.py:428-753 on the GPU.
+
+    ``chunk_input = [df, args]`` as in the reference: df holds ``ref_seq``,
+    ``align_str``, ``align_seq``, ``UNMODIFIED`` (and ``score_diff`` /
+    ``score_repaired`` when ``args.expected_hdr_amplicon_seq``); the globals come
+    from :func:`set_globals` / :func:`globals_from_args` unless passed.  Returns the
+    reference's 22-tuple: the DataFrame with UNMODIFIED / NHEJ / HDR / MIXED /
+    n_mutated / n_inserted / n_deleted filled in, the thirteen effect vectors
+    (float64, as the reference's np.zeros), hist_inframe, hist_frameshift, the two
+    avg vectors (sums, divided later by the caller, CORE:2962-2973) and the four
+    frameshift counters.
+    """
+    df, args = chunk_input[0], chunk_input[1]
+    g = globals_ or _GLOBALS
+    if g is None:
+        raise QuantificationError("LEN_AMPLICON / INCLUDE_IDXS not set: call set_globals or globals_from_args")
+    reads, tot = _run_df(df, args, g, quantifier, n_rule=False)
+    return _result_tuple(df, reads, tot, bool(getattr(args, "coding_seq", None)))
+
+
+def quantify_alignments(df_needle_alignment: pd.DataFrame, args, quantifier: Optional[GpuQuantifier] = None,
+                        globals_: Optional[QuantGlobals] = None):
+    """CORE:2014-2067 followed by process_df_chunk: UNMODIFIED from score_ref,
+    NHEJ/HDR/MIXED/n_* initialised, ignore_n_in_alignment when the amplicon holds an
+    N (align_str rewritten), then the quantification.  Returns process_df_chunk's
+    tuple (the DataFrame gets the reference's columns except ``ref_positions``)."""
+    df = df_needle_alignment
+    if df.shape[0] == 0:
+        raise QuantificationError("Zero sequences aligned, please check your amplicon sequence")
+    df["UNMODIFIED"] = df.score_ref == 100
+    df["MIXED"] = False
+    df["HDR"] = False
+    df["NHEJ"] = False
+    df["n_mutated"] = 0
+    df["n_inserted"] = 0
+    df["n_deleted"] = 0
+    g = globals_ or _GLOBALS or globals_from_args(args)
+    reads, tot = _run_df(df, args, g, quantifier, n_rule="N" in args.amplicon_seq.upper())
+    return _result_tuple(df, reads, tot, bool(getattr(args, "coding_seq", None)))

@@ -119,6 +119,12 @@ int64_t nw_batch_fallbacks(nw_ctx* ctx);
  * non-streaming kernels everything is reported as fill.  For batches split
  * into several passes the first two cover the first pass only. */
 int nw_batch_kernel_times(nw_ctx* ctx, float* fill_ms, float* walk_ms, float* rest_ms);
+/* Device-resident output of the last nw_batch_run_async (synchronises): the
+ * [n][3][stride] alignment rows and the nw_stat array, valid until the next
+ * upload / align call.  Lets the quantification (include/crispr_quant.h,
+ * nwq_run_device with aln_len = &stats->aln_len, len_stride = 8) consume the
+ * alignments without a round trip through host memory. */
+int nw_batch_device_output(nw_ctx* ctx, void** d_aln, int64_t* stride, void** d_stats);
 
 /* Pooled batch (replaces one CRISPResso + needle process per amplicon,
  * CRISPRessoPooled.py:882-908): n_refs amplicons packed in `refs` with
