@@ -91,6 +91,73 @@ def cpu_baseline(amplicon, buf, offsets, n_sample, threads):
     }
 
 
+def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cpu_sample, no_cpu):
+    """Downstream quantification (process_df_chunk, CORE:428-753) of this rank's
+    aligned reads, straight from the aligner's HBM output (nwq_run_device).
+    Settings: one guide cutting mid-amplicon, CRISPResso defaults otherwise
+    (window_around_sgrna 1, exclude 15 bp each side)."""
+    from crispresso_amd import quantify
+    from crispresso_amd.devmem import DeviceBuffer
+
+    d_aln, stride, d_stats = al.device_output()
+    batch = al.download(n_reads, AMPLICON_LEN + 64)
+    lens = batch.stats["aln_len"].astype(np.int64)
+    ident = batch.stats["n_ident"].astype(np.int64)
+    um = ident == lens
+    args = argparse.Namespace(amplicon_seq=amplicon, guide_seq=amplicon[105:125], cleavage_offset=-3,
+                              window_around_sgrna=1, exclude_bp_from_left=15, exclude_bp_from_right=15,
+                              coding_seq=None, expected_hdr_amplicon_seq=None)
+    g = quantify.globals_from_args(args)
+    q = quantify.GpuQuantifier(local)
+    q.set_params(g, args)
+    pre = quantify.pre_flags(um)
+    d_pre = DeviceBuffer.from_array(pre, local)
+    d_out = DeviceBuffer(16 * n_reads, local)
+    for _ in range(warmup):
+        q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
+    barrier(dist, local)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
+        kms.append(q.last_kernel_ms)
+    barrier(dist, local)
+    elapsed = max_over_ranks(dist, local, time.perf_counter() - t0)
+    algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
+    kavg = float(np.mean(kms))
+    out = {
+        "metric": "quantified reads/s (process_df_chunk on the aligned C2 batch, device-resident)",
+        "value": n_reads * world * steps / elapsed,
+        "unit": "reads/s",
+        "ms_per_step": elapsed / steps * 1e3,
+        "kernel": "nwq::quant_kernel + nwq::quant_reduce",
+        "kernel_ms_avg": kavg,
+        "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "algo_bytes_per_launch": algo,
+                     "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 16 (result); + 3*aln_len for rows not "
+                                       "UNMODIFIED on input (the three alignment rows)"},
+        "settings": "guide mid-amplicon, window_around_sgrna 1, exclude 15/15",
+    }
+    if rank == 0 and world == 1 and not no_cpu:
+        from oracle import quant_oracle as qo
+
+        k = min(cpu_sample, n_reads)
+        rows = [(batch.ref_seq(i), batch.align_str(i), batch.align_seq(i)) for i in range(k)]
+        prm = qo.QuantParams(len_amplicon=g.LEN_AMPLICON, include_idxs=frozenset(g.INCLUDE_IDXS),
+                             window_around_sgrna=1)
+        t1 = time.perf_counter()
+        qo.process_rows([r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows], um[:k], None, None, prm)
+        dt = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": k / dt, "unit": "reads/s", "cores": 1, "kind": "port",
+                               "sample": f"first {k} aligned reads, oracle/quant_oracle.py (pure-Python restatement "
+                                         f"of process_df_chunk), 1 thread, {dt:.2f} s"}
+    d_pre.free()
+    d_out.free()
+    q.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,6 +167,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=100_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-quant", action="store_true", help="skip the downstream quantification leg")
+    ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
     args = ap.parse_args()
 
     rank, local, world, dist = dist_setup(args.gpus)
@@ -143,6 +212,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(amplicon, buf, offsets, min(args.cpu_sample, args.reads), args.cpu_threads)
+
+    quant = None
+    if not args.no_quant:
+        quant = quant_leg(al, amplicon, args.reads, args.steps, args.warmup, dist, local, rank, world,
+                          args.quant_cpu_sample, args.no_cpu)
 
     total_reads = args.reads * world * args.steps
     value = total_reads / elapsed
@@ -191,6 +265,7 @@ def main():
                 },
             },
             "cpu_baseline": cpu,
+            "downstream_quantification": quant,
         }
         print(json.dumps(line), flush=True)
     al.close()

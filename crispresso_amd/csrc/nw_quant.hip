@@ -59,30 +59,38 @@ struct QArgs {
     uint32_t flags;
 };
 
-__device__ __forceinline__ unsigned mbcnt(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
+
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
-
-// exclusive prefix over lanes of a per-lane count < 2^BITS, and the wave total
-template <int BITS>
-__device__ __forceinline__ int lane_prefix(unsigned v, int* total) {
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int b = 0; b < BITS; ++b) {
-        const unsigned long long m = ballot((v >> b) & 1u);
-        pre += (int)mbcnt(m) << b;
-        tot += __popcll(m) << b;
-    }
-    *total = tot;
-    return pre;
-}
-
 __device__ __forceinline__ bool wave_any(bool p) { return ballot(p) != 0ull; }
+
+// Inclusive prefix sum over the 64 lanes on DPP (row_shr 1/2/3 of the input,
+// row_shr 4/8 within rows, row_bcast 15/31 across rows): 7 adds, no LDS.
+template <int CTRL, int ROWS, int BANKS>
+__device__ __forceinline__ unsigned dpp_mov(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, BANKS, false);
+}
+__device__ __forceinline__ unsigned wave_scan_incl(unsigned v) {
+    unsigned s = v + dpp_mov<0x111, 0xf, 0xf>(v);
+    s += dpp_mov<0x112, 0xf, 0xf>(v);
+    s += dpp_mov<0x113, 0xf, 0xf>(v);
+    s += dpp_mov<0x114, 0xf, 0xe>(s);
+    s += dpp_mov<0x118, 0xf, 0xc>(s);
+    s += dpp_mov<0x142, 0xa, 0xf>(s);
+    s += dpp_mov<0x143, 0xc, 0xf>(s);
+    return s;
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) { return ~nw::wave_max_u32(~v); }
 
 __device__ __forceinline__ void vadd(uint32_t* h, int v, int LEN, unsigned x) {
     if (x) atomicAdd(h + v * LEN, x);
 }
+
+// Column step state carried between 256-column steps of one read.
+struct Carry {
+    int B;                  // amplicon bases before the step
+    int ds, de, is, ie;     // deletion / insertion run starts / ends so far
+    int prev;               // gap state of the column before the step (bit0 read gap, bit1 amplicon gap)
+};
 
 __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
     extern __shared__ uint32_t smem[];
@@ -107,251 +115,300 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
 
     const unsigned flags = a.flags;
     const bool nfix = flags & F_NFIX;
+    const bool hide = flags & F_HIDE;
     const unsigned ign_sub = (flags & F_IGN_SUB) ? 0u : 0xfu;
     const unsigned ign_ins = (flags & F_IGN_INS) ? 0u : 0xfu;
     const unsigned ign_del = (flags & F_IGN_DEL) ? 0u : 0xfu;
     uint32_t* ctr = blk + NV * LEN;
     uint32_t* hin = ctr + 4;
     uint32_t* hfs = hin + a.H;
+    const int64_t stride = a.stride;
 
+    // Reads go to waves in groups of 64: one coalesced load of the flags and
+    // lengths, one coalesced store of the results; rows of the next read to
+    // process are loaded while the current one is worked on.
+    const int64_t ngroups = (a.n + 63) >> 6;
     const int64_t tw = (int64_t)gridDim.x * wpb;
-    for (int64_t r = (int64_t)blockIdx.x * wpb + wave; r < a.n; r += tw) {
-        const unsigned pre = a.pre[r];
-        const int L = a.len[r * a.len_stride];
-        const bool unmod_in = pre & NWQ_PRE_UNMODIFIED;
-        if ((unmod_in && !nfix) || L <= 0 || L > a.stride) {
-            if (lane == 0) a.out[r] = make_int4((unmod_in && !nfix) ? 0 : -1, 0, 0, 0);
-            continue;
-        }
-        uint8_t* Rrow = a.aln + r * 3 * a.stride;
-        uint8_t* Mrow = Rrow + a.stride;
-        const uint8_t* Srow = Mrow + a.stride;
-        const unsigned f0 = (nfix && Rrow[0] == 'N') ? (unsigned)'|' : (unsigned)Mrow[0];
+    for (int64_t grp = (int64_t)blockIdx.x * wpb + wave; grp < ngroups; grp += tw) {
+        const int64_t idx = (grp << 6) + lane;
+        const bool valid = idx < a.n;
+        const unsigned mypre = valid ? (unsigned)a.pre[idx] : (unsigned)NWQ_PRE_UNMODIFIED;
+        const int mylen = valid ? a.len[idx * a.len_stride] : 1;
+        const bool skip = (mypre & NWQ_PRE_UNMODIFIED) && !nfix;
+        const bool badlen = mylen <= 0 || mylen > stride;
+        int4 myout = make_int4((!skip && badlen) ? -1 : 0, 0, 0, 0);
+        unsigned long long todo = ballot(!skip && !badlen);
 
-        int Bc = 0, nds = 0, nde = 0, nis = 0, nie = 0;
-        int prev_state = 0;
-        unsigned nsub = 0, nsub_inc = 0, subbits = 0;   // subbits: 1 exon, 2 splice, 4 exon&inc, 8 splice&inc
-        bool neq = false, oob = false;
-        for (int cb = 0; cb <= L; cb += 256) {
-            const int c0 = cb + 4 * lane;
-            uint32_t dr = 0, dm = 0, ds = 0;
+        auto row_ptr = [&](int k) { return a.aln + ((grp << 6) + k) * 3 * stride; };
+        auto load3 = [&](int k, int L, int c0, uint32_t& dr, uint32_t& dm, uint32_t& ds) {
+            dr = dm = ds = 0;
             if (c0 < L) {
-                dr = *(const uint32_t*)(Rrow + c0);
-                dm = *(const uint32_t*)(Mrow + c0);
-                ds = *(const uint32_t*)(Srow + c0);
+                const uint8_t* p = row_ptr(k) + c0;
+                dr = *(const uint32_t*)p;
+                dm = *(const uint32_t*)(p + stride);
+                ds = *(const uint32_t*)(p + 2 * stride);
             }
-            unsigned isb = 0, gR = 0, gS = 0, dot = 0;
-            uint32_t dmf = dm;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (c0 + k >= L) break;
-                const unsigned rc = (dr >> (8 * k)) & 255u, sc = (ds >> (8 * k)) & 255u;
-                unsigned mc = (dm >> (8 * k)) & 255u;
-                const bool base = rc == 'A' || rc == 'C' || rc == 'G' || rc == 'T' || rc == 'N';
-                isb |= (unsigned)base << k;
-                gR |= (unsigned)(rc == '-') << k;
-                gS |= (unsigned)(sc == '-') << k;
-                if (nfix && rc == 'N') {
-                    mc = '|';
-                    dmf = (dmf & ~(255u << (8 * k))) | ((unsigned)'|' << (8 * k));
-                }
-                dot |= (unsigned)(mc == '.') << k;
-                neq |= mc != f0;
-            }
-            if (nfix && dmf != dm) *(uint32_t*)(Mrow + c0) = dmf;
-            gR &= ign_ins;
-            gS &= ign_del;
-            dot &= ign_sub;
-            // state of the column before this lane's first one
-            const int st = (int)(((gS >> 3) & 1u) | (((gR >> 3) & 1u) << 1));
-            const int pl = nw::shr1(st, prev_state);
-            const unsigned pS = ((gS << 1) | (unsigned)(pl & 1)) & 0xfu;
-            const unsigned pR = ((gR << 1) | (unsigned)((pl >> 1) & 1)) & 0xfu;
-            const unsigned dstart = gS & ~pS, dend = ~gS & pS & 0xfu;
-            const unsigned istart = gR & ~pR, iend = ~gR & pR & 0xfu;
-
-            int tb, tds, tde, tis, tie;
-            const int Bl = Bc + lane_prefix<3>(__popc(isb), &tb);
-            const int dsp = nds + lane_prefix<2>(__popc(dstart), &tds);
-            const int dep = nde + lane_prefix<2>(__popc(dend), &tde);
-            const int isp = nis + lane_prefix<2>(__popc(istart), &tis);
-            const int iep = nie + lane_prefix<2>(__popc(iend), &tie);
-
-            // starts, deletion marks, substitutions
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const unsigned lt = (1u << k) - 1u, bit = 1u << k;
-                const int Bk = Bl + __popc(isb & lt);
-                if (dstart & bit) druns[dsp + __popc(dstart & lt)].x = (short)Bk;
-                if (gS & bit) {
-                    const int jr = dsp + __popc(dstart & (lt | bit)) - 1;
-                    if (Bk < LEN) posw[Bk] = (uint32_t)(jr + 1) << 16;
-                    else oob = true;
-                }
-                if (istart & bit) iruns[isp + __popc(istart & lt)].x = (short)(c0 + k);
-                if (dot & bit) {
-                    if (Bk < LEN) {
-                        posw[Bk] = P_SUB;
-                        const unsigned t = tbl[Bk];
-                        ++nsub;
-                        nsub_inc += t & T_INC;
-                        subbits |= ((t & T_EXON) ? 1u : 0u) | ((t & T_SPL) ? 2u : 0u);
-                        if (t & T_INC) subbits |= ((t & T_EXON) ? 4u : 0u) | ((t & T_SPL) ? 8u : 0u);
-                    } else {
-                        oob = true;
-                    }
-                }
-            }
-            // ends (their starts are in LDS by now: one wave, in-order LDS queue)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const unsigned lt = (1u << k) - 1u, bit = 1u << k;
-                const int Bk = Bl + __popc(isb & lt);
-                if ((dend & bit) && Bk <= LEN) {
-                    const int j = dep + __popc(dend & lt);
-                    const int ps = druns[j].x;
-                    const int f = (incp[Bk] - incp[ps] > 0 ? R_INC : 0) | (splp[Bk] - splp[ps] > 0 ? R_SPL : 0);
-                    druns[j] = run4{(short)ps, (short)(Bk - ps), (short)f, (short)(exop[Bk] - exop[ps])};
-                }
-                if ((iend & bit) && Bk <= LEN) {
-                    const int j = iep + __popc(iend & lt);
-                    const int c = c0 + k;
-                    const int s0 = iruns[j].x;
-                    const int fa = s0 > 0 ? Bk - 1 : -1;
-                    const int fb = c < L ? Bk : (Bk > 0 ? -Bk : -1);
-                    int f = 0;
-                    if (fa >= 0 && fa < LEN) f |= tbl[fa];
-                    if (fb >= 0 && fb < LEN) f |= tbl[fb];
-                    // T_* and R_INC/R_EXON/R_SPL share bit positions
-                    iruns[j] = run4{(short)fa, (short)fb, (short)(c - s0), (short)f};
-                }
-            }
-            Bc += tb;
-            nds += tds;
-            nde += tde;
-            nis += tis;
-            nie += tie;
-            prev_state = __builtin_amdgcn_readlane(st, 63);
+        };
+        uint32_t nr = 0, nm = 0, ns = 0;
+        if (todo) {
+            const int k = __builtin_ctzll(todo);
+            load3(k, __builtin_amdgcn_readlane(mylen, k), 4 * lane, nr, nm, ns);
         }
-
-        const bool bad = Bc != LEN || wave_any(oob);
-        const bool unmod = unmod_in || (nfix && !wave_any(neq));
-        const bool counting = !bad && !unmod;
-        int cls = 0, n_mut = 0, n_ins = 0, n_del = 0;
-        bool windowed = false, noncoding = false;
-        if (counting) {
-            const int nsub_t = (int)nw::wave_sum_u32(nsub), nsubi_t = (int)nw::wave_sum_u32(nsub_inc);
-            bool hit_l = false;
-            for (int j = lane; j < nds; j += 64) hit_l |= (druns[j].z & R_INC) != 0;
-            for (int j = lane; j < nis; j += 64) hit_l |= (iruns[j].w & R_INC) != 0;
-            const bool hit = nsubi_t > 0 || wave_any(hit_l);
-            cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
-            windowed = cls == 1 && a.window != 0;
-
-            bool kept_l = false;
-            for (int j = lane; j < nds; j += 64) kept_l |= !windowed || (druns[j].z & R_INC);
-            const bool post_sel = windowed && wave_any(kept_l);
-            int ndel_l = 0, exdel_l = 0;
-            bool spldel_l = false;
-            for (int j = lane; j < nds; j += 64) {
-                run4 d = druns[j];
-                const bool kept = !windowed || (d.z & R_INC);
-                const bool post = post_sel ? kept : true;
-                d.z |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
-                druns[j] = d;
-                ndel_l += kept ? d.y : 0;
-                exdel_l += post ? d.w : 0;
-                spldel_l |= post && (d.z & R_SPL);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const unsigned pre = (unsigned)__builtin_amdgcn_readlane((int)mypre, k);
+            const int L = __builtin_amdgcn_readlane(mylen, k);
+            uint32_t dr = nr, dm = nm, ds = ns;
+            if (todo) {
+                const int k2 = __builtin_ctzll(todo);
+                load3(k2, __builtin_amdgcn_readlane(mylen, k2), 4 * lane, nr, nm, ns);
             }
-            int nins_l = 0, insex_len_l = 0;
-            bool insex_l = false, insspl_l = false;
-            for (int j = lane; j < nis; j += 64) {
-                const run4 e = iruns[j];
-                const bool kept = !windowed || (e.w & R_INC);
-                const int wa = e.x < 0 ? e.x + LEN : e.x, wb = e.y < 0 ? e.y + LEN : e.y;
-                atomicOr(posw + wa, P_INS);
-                atomicOr(posw + wb, P_INS);
-                insspl_l |= (e.w & R_SPL) != 0;
-                if (kept) {
-                    nins_l += e.z;
-                    if (e.w & R_EXON) { insex_l = true; insex_len_l += e.z; }
-                    if (cls != 0) {
-                        atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)e.z);
-                        if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)e.z);
+            uint8_t* Mrow = row_ptr(k) + stride;
+            const unsigned f0 = (nfix && (__builtin_amdgcn_readlane((int)dr, 0) & 255) == 'N')
+                                    ? (unsigned)'|' : (unsigned)(__builtin_amdgcn_readlane((int)dm, 0) & 255);
+            Carry cy{0, 0, 0, 0, 0, 0};
+            unsigned nsub = 0, nsub_inc = 0, subbits = 0;   // subbits: 1 exon, 2 splice, 4 exon&inc, 8 splice&inc
+            int pmin = LEN, pmax = -1;                       // range of positions marked in posw
+            bool neq = false, oob = false;
+            for (int cb = 0; cb <= L; cb += 256) {
+                const int c0 = cb + 4 * lane;
+                if (cb) load3(k, L, c0, dr, dm, ds);
+                unsigned isb = 0, gR = 0, gS = 0, dot = 0;
+                uint32_t dmf = dm;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (c0 + q >= L) break;
+                    const unsigned rc = (dr >> (8 * q)) & 255u, sc = (ds >> (8 * q)) & 255u;
+                    unsigned mc = (dm >> (8 * q)) & 255u;
+                    const bool base = rc == 'A' || rc == 'C' || rc == 'G' || rc == 'T' || rc == 'N';
+                    isb |= (unsigned)base << q;
+                    gR |= (unsigned)(rc == '-') << q;
+                    gS |= (unsigned)(sc == '-') << q;
+                    if (nfix && rc == 'N') {
+                        mc = '|';
+                        dmf = (dmf & ~(255u << (8 * q))) | ((unsigned)'|' << (8 * q));
                     }
+                    dot |= (unsigned)(mc == '.') << q;
+                    neq |= mc != f0;
                 }
-            }
-            n_mut = windowed ? nsubi_t : nsub_t;
-            n_ins = nw::wave_sum(nins_l);
-            n_del = nw::wave_sum(ndel_l);
-            if ((flags & F_FRAMESHIFT) && cls != 0) {
-                const unsigned sb = (wave_any(subbits & 1u) ? 1u : 0u) | (wave_any(subbits & 2u) ? 2u : 0u) |
-                                    (wave_any(subbits & 4u) ? 4u : 0u) | (wave_any(subbits & 8u) ? 8u : 0u);
-                const bool sub_exon = windowed ? (sb & 4u) : (sb & 1u);
-                const bool sub_spl = windowed ? (sb & 8u) : (sb & 2u);
-                const int exdel = nw::wave_sum(exdel_l);
-                const bool insex = wave_any(insex_l);
-                const int eff = nw::wave_sum(insex_len_l) - exdel;
-                const bool exon_mod = insex || exdel > 0 || sub_exon;
-                const bool has_lens = insex || exdel > 0;
-                const bool spliced = sub_spl || wave_any(spldel_l) || wave_any(insspl_l);
-                if (lane == 0) {
-                    if (spliced) atomicAdd(ctr + C_SPLICE, 1u);
-                    if (exon_mod) {
-                        if (!has_lens) {
-                            atomicAdd(ctr + C_NONFS, 1u);
-                            atomicAdd(hin + LEN, 1u);
-                        } else if (eff % 3 == 0) {
-                            atomicAdd(ctr + C_NONFS, 1u);
-                            atomicAdd(hin + LEN + eff, 1u);
+                if (nfix && dmf != dm) *(uint32_t*)(Mrow + c0) = dmf;
+                gR &= ign_ins;
+                gS &= ign_del;
+                dot &= ign_sub;
+                // gap state of the column before this lane's first one
+                const int st = (int)(((gS >> 3) & 1u) | (((gR >> 3) & 1u) << 1));
+                const int pl = nw::shr1(st, cy.prev);
+                const unsigned pS = ((gS << 1) | (unsigned)(pl & 1)) & 0xfu;
+                const unsigned pR = ((gR << 1) | (unsigned)((pl >> 1) & 1)) & 0xfu;
+                const unsigned dstart = gS & ~pS, dend = ~gS & pS & 0xfu;
+                const unsigned istart = gR & ~pR, iend = ~gR & pR & 0xfu;
+
+                // lane prefixes of (bases, del starts, del ends) and (ins starts, ins ends), packed
+                const unsigned va = (unsigned)__popc(isb) | ((unsigned)__popc(dstart) << 9) |
+                                    ((unsigned)__popc(dend) << 17);
+                const unsigned vb = (unsigned)__popc(istart) | ((unsigned)__popc(iend) << 8);
+                const unsigned sa = wave_scan_incl(va), sb = wave_scan_incl(vb);
+                const unsigned ea = sa - va, eb = sb - vb;
+                const int Bl = cy.B + (int)(ea & 511u);
+                const int dsp = cy.ds + (int)((ea >> 9) & 255u);
+                const int dep = cy.de + (int)((ea >> 17) & 255u);
+                const int isp = cy.is + (int)(eb & 255u);
+                const int iep = cy.ie + (int)((eb >> 8) & 255u);
+
+                // starts, deletion marks, substitutions
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned lt = (1u << q) - 1u, bit = 1u << q;
+                    const int Bk = Bl + __popc(isb & lt);
+                    if (dstart & bit) druns[dsp + __popc(dstart & lt)].x = (short)Bk;
+                    if (gS & bit) {
+                        const int jr = dsp + __popc(dstart & (lt | bit)) - 1;
+                        if (Bk < LEN) {
+                            posw[Bk] = (uint32_t)(jr + 1) << 16;
+                            pmin = min(pmin, Bk);
+                            pmax = max(pmax, Bk);
                         } else {
-                            atomicAdd(ctr + C_FS, 1u);
-                            atomicAdd(hfs + LEN + eff, 1u);
+                            oob = true;
                         }
-                    } else {
-                        atomicAdd(ctr + C_NONMOD, 1u);
+                    }
+                    if (istart & bit) iruns[isp + __popc(istart & lt)].x = (short)(c0 + q);
+                    if (dot & bit) {
+                        if (Bk < LEN) {
+                            posw[Bk] = P_SUB;
+                            pmin = min(pmin, Bk);
+                            pmax = max(pmax, Bk);
+                            const unsigned t = tbl[Bk];
+                            ++nsub;
+                            nsub_inc += t & T_INC;
+                            subbits |= ((t & T_EXON) ? 1u : 0u) | ((t & T_SPL) ? 2u : 0u);
+                            if (t & T_INC) subbits |= ((t & T_EXON) ? 4u : 0u) | ((t & T_SPL) ? 8u : 0u);
+                        } else {
+                            oob = true;
+                        }
                     }
                 }
-                noncoding = !exon_mod;
+                // ends (their starts are in LDS by now: one wave, in-order LDS queue)
+                if (dend | iend) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const unsigned lt = (1u << q) - 1u, bit = 1u << q;
+                        const int Bk = Bl + __popc(isb & lt);
+                        if ((dend & bit) && Bk <= LEN) {
+                            const int j = dep + __popc(dend & lt);
+                            const int ps = druns[j].x;
+                            const int f = (incp[Bk] - incp[ps] > 0 ? R_INC : 0) |
+                                          (splp[Bk] - splp[ps] > 0 ? R_SPL : 0);
+                            druns[j] = run4{(short)ps, (short)(Bk - ps), (short)f, (short)(exop[Bk] - exop[ps])};
+                        }
+                        if ((iend & bit) && Bk <= LEN) {
+                            const int j = iep + __popc(iend & lt);
+                            const int c = c0 + q;
+                            const int s0 = iruns[j].x;
+                            const int fa = s0 > 0 ? Bk - 1 : -1;
+                            const int fb = c < L ? Bk : (Bk > 0 ? -Bk : -1);
+                            int f = 0;     // T_* and R_INC / R_EXON / R_SPL share bit positions
+                            if (fa >= 0 && fa < LEN) f |= tbl[fa];
+                            if (fb >= 0 && fb < LEN) f |= tbl[fb];
+                            iruns[j] = run4{(short)fa, (short)fb, (short)(c - s0), (short)f};
+                        }
+                    }
+                }
+                const unsigned ta = (unsigned)__builtin_amdgcn_readlane((int)sa, 63);
+                const unsigned tb = (unsigned)__builtin_amdgcn_readlane((int)sb, 63);
+                cy.B += (int)(ta & 511u);
+                cy.ds += (int)((ta >> 9) & 255u);
+                cy.de += (int)((ta >> 17) & 255u);
+                cy.is += (int)(tb & 255u);
+                cy.ie += (int)((tb >> 8) & 255u);
+                cy.prev = __builtin_amdgcn_readlane(st, 63);
             }
-        }
+            const int nds = cy.ds, nis = cy.is;
 
-        // position pass: the read's per-position vector increments; clears the marks
-        const bool hide = flags & F_HIDE;
-        for (int p = lane; p < LEN; p += 64) {
-            const uint32_t w = posw[p];
-            if (!w) continue;
-            posw[p] = 0;
-            if (!counting) continue;
-            const unsigned sub = w & P_SUB, ins = (w >> 1) & 1u;
-            const int dj = (int)(w >> 16);
-            int rf = 0, dsz = 0;
-            if (dj) {
-                const run4 d = druns[dj - 1];
-                rf = d.z;
-                dsz = d.y;
+            const bool bad = cy.B != LEN || wave_any(oob);
+            const bool unmod = (pre & NWQ_PRE_UNMODIFIED) || (nfix && !wave_any(neq));
+            const bool counting = !bad && !unmod;
+            int cls = 0, n_mut = 0, n_ins = 0, n_del = 0;
+            bool windowed = false, noncoding = false;
+            if (counting) {
+                const int nsub_t = (int)nw::wave_sum_u32(nsub), nsubi_t = (int)nw::wave_sum_u32(nsub_inc);
+                bool hit_l = false;
+                for (int j = lane; j < nds; j += 64) hit_l |= (druns[j].z & R_INC) != 0;
+                for (int j = lane; j < nis; j += 64) hit_l |= (iruns[j].w & R_INC) != 0;
+                const bool hit = nsubi_t > 0 || wave_any(hit_l);
+                cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
+                windowed = cls == 1 && a.window != 0;
+
+                bool kept_l = false;
+                for (int j = lane; j < nds; j += 64) kept_l |= !windowed || (druns[j].z & R_INC);
+                const bool post_sel = windowed && wave_any(kept_l);
+                int ndel_l = 0, exdel_l = 0;
+                bool spldel_l = false;
+                for (int j = lane; j < nds; j += 64) {
+                    run4 d = druns[j];
+                    const bool kept = !windowed || (d.z & R_INC);
+                    const bool post = post_sel ? kept : true;
+                    d.z |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
+                    druns[j] = d;
+                    ndel_l += kept ? d.y : 0;
+                    exdel_l += post ? d.w : 0;
+                    spldel_l |= post && (d.z & R_SPL);
+                }
+                int nins_l = 0, insex_len_l = 0;
+                bool insex_l = false, insspl_l = false;
+                for (int j = lane; j < nis; j += 64) {
+                    const run4 e = iruns[j];
+                    const bool kept = !windowed || (e.w & R_INC);
+                    const int wa = e.x < 0 ? e.x + LEN : e.x, wb = e.y < 0 ? e.y + LEN : e.y;
+                    atomicOr(posw + wa, P_INS);
+                    atomicOr(posw + wb, P_INS);
+                    pmin = min(pmin, min(wa, wb));
+                    pmax = max(pmax, max(wa, wb));
+                    insspl_l |= (e.w & R_SPL) != 0;
+                    if (kept) {
+                        nins_l += e.z;
+                        if (e.w & R_EXON) { insex_l = true; insex_len_l += e.z; }
+                        if (cls != 0) {
+                            atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)e.z);
+                            if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)e.z);
+                        }
+                    }
+                }
+                n_mut = windowed ? nsubi_t : nsub_t;
+                n_ins = nw::wave_sum(nins_l);
+                n_del = nw::wave_sum(ndel_l);
+                if ((flags & F_FRAMESHIFT) && cls != 0) {
+                    const unsigned sb = (wave_any(subbits & 1u) ? 1u : 0u) | (wave_any(subbits & 2u) ? 2u : 0u) |
+                                        (wave_any(subbits & 4u) ? 4u : 0u) | (wave_any(subbits & 8u) ? 8u : 0u);
+                    const bool sub_exon = windowed ? (sb & 4u) : (sb & 1u);
+                    const bool sub_spl = windowed ? (sb & 8u) : (sb & 2u);
+                    const int exdel = nw::wave_sum(exdel_l);
+                    const bool insex = wave_any(insex_l);
+                    const int eff = nw::wave_sum(insex_len_l) - exdel;
+                    const bool exon_mod = insex || exdel > 0 || sub_exon;
+                    const bool has_lens = insex || exdel > 0;
+                    const bool spliced = sub_spl || wave_any(spldel_l) || wave_any(insspl_l);
+                    if (lane == 0) {
+                        if (spliced) atomicAdd(ctr + C_SPLICE, 1u);
+                        if (exon_mod) {
+                            if (!has_lens) {
+                                atomicAdd(ctr + C_NONFS, 1u);
+                                atomicAdd(hin + LEN, 1u);
+                            } else if (eff % 3 == 0) {
+                                atomicAdd(ctr + C_NONFS, 1u);
+                                atomicAdd(hin + LEN + eff, 1u);
+                            } else {
+                                atomicAdd(ctr + C_FS, 1u);
+                                atomicAdd(hfs + LEN + eff, 1u);
+                            }
+                        } else {
+                            atomicAdd(ctr + C_NONMOD, 1u);
+                        }
+                    }
+                    noncoding = !exon_mod;
+                }
             }
-            const unsigned del = dj ? 1u : 0u;
-            const unsigned sub_post = (sub && (!windowed || (tbl[p] & T_INC))) ? 1u : 0u;
-            const unsigned del_post = (del && (rf & R_POST)) ? 1u : 0u;
-            uint32_t* h = blk + p;
-            if (cls == 3) {
-                vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
-            } else if (cls == 2) {
-                vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
-            } else if (cls == 1) {
-                vadd(h, V_MUT, LEN, hide ? sub_post : sub);
-                vadd(h, V_DEL, LEN, hide ? del_post : del);
-                vadd(h, V_INS, LEN, ins);
+
+            // position pass over the marked range: the read's per-position vector
+            // increments (once per distinct position); clears the marks
+            const int lo = (int)wave_min_u32((unsigned)pmin);
+            const int hi = (int)nw::wave_max_u32((unsigned)(pmax + 1)) - 1;
+            for (int p = lo + lane; p <= hi; p += 64) {
+                const uint32_t w = posw[p];
+                if (!w) continue;
+                posw[p] = 0;
+                if (!counting) continue;
+                const unsigned sub = w & P_SUB, ins = (w >> 1) & 1u;
+                const int dj = (int)(w >> 16);
+                int rf = 0, dsz = 0;
+                if (dj) {
+                    const run4 d = druns[dj - 1];
+                    rf = d.z;
+                    dsz = d.y;
+                }
+                const unsigned del = dj ? 1u : 0u;
+                const unsigned sub_post = (sub && (!windowed || (tbl[p] & T_INC))) ? 1u : 0u;
+                const unsigned del_post = (del && (rf & R_POST)) ? 1u : 0u;
+                uint32_t* h = blk + p;
+                if (cls == 3) {
+                    vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
+                } else if (cls == 2) {
+                    vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
+                } else if (cls == 1) {
+                    vadd(h, V_MUT, LEN, hide ? sub_post : sub);
+                    vadd(h, V_DEL, LEN, hide ? del_post : del);
+                    vadd(h, V_INS, LEN, ins);
+                }
+                vadd(h, V_ANY, LEN, 1u);
+                if (noncoding) {
+                    vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
+                }
+                if (cls != 0 && del && (rf & R_KEPT)) vadd(h, V_AVG_DEL, LEN, (unsigned)dsz);
             }
-            vadd(h, V_ANY, LEN, (sub | del | ins) ? 1u : 0u);
-            if (noncoding) {
-                vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
-            }
-            if (cls != 0 && del && (rf & R_KEPT)) vadd(h, V_AVG_DEL, LEN, (unsigned)dsz);
+            // counts are written only for rows left modified (CORE:651-660)
+            if (lane == k) myout = cls ? make_int4(cls, n_mut, n_ins, n_del) : make_int4(bad ? -1 : 0, 0, 0, 0);
         }
-        // counts are written only for rows left modified (CORE:651-660)
-        if (lane == 0) a.out[r] = cls ? make_int4(cls, n_mut, n_ins, n_del) : make_int4(bad ? -1 : 0, 0, 0, 0);
+        if (valid) a.out[idx] = myout;
     }
 
     __syncthreads();
@@ -359,13 +416,18 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
     for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) dst[i] = blk[i];
 }
 
-__global__ void quant_reduce(const uint32_t* __restrict__ partial, int nblocks, int nwords, int64_t* out) {
+// Sum of the per-block slabs: blockIdx.y takes a contiguous slice of the slabs,
+// adds into the (zeroed) int64 totals.
+__global__ void quant_reduce(const uint32_t* __restrict__ partial, int nblocks, int nwords, int slice,
+                             unsigned long long* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nwords) return;
-    int64_t s = 0;
-    for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * nwords + i];
-    out[i] = s;
+    const int b0 = blockIdx.y * slice, b1 = min(nblocks, b0 + slice);
+    unsigned long long s = 0;
+    for (int b = b0; b < b1; ++b) s += partial[(int64_t)b * nwords + i];
+    if (s) atomicAdd(out + i, s);
 }
+
 
 }  // namespace nwq
 
@@ -501,8 +563,10 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
     QHIP(c, hipEventRecord(c->ev0, c->stream));
     hipLaunchKernelGGL(nwq::quant_kernel, dim3(g.grid), dim3(64 * g.wpb), g.lds, c->stream, a);
     QHIP(c, hipGetLastError());
-    hipLaunchKernelGGL(nwq::quant_reduce, dim3((g.nwords + 255) / 256), dim3(256), 0, c->stream, c->d_partial.p,
-                       g.grid, g.nwords, c->d_totals.p);
+    const int slices = std::min(g.grid, 32), slice = (g.grid + slices - 1) / slices;
+    QHIP(c, hipMemsetAsync(c->d_totals.p, 0, sizeof(int64_t) * (size_t)g.nwords, c->stream));
+    hipLaunchKernelGGL(nwq::quant_reduce, dim3((g.nwords + 255) / 256, slices), dim3(256), 0, c->stream,
+                       c->d_partial.p, g.grid, g.nwords, slice, reinterpret_cast<unsigned long long*>(c->d_totals.p));
     QHIP(c, hipGetLastError());
     QHIP(c, hipEventRecord(c->ev1, c->stream));
     QHIP(c, hipMemcpyAsync(totals, c->d_totals.p, sizeof(int64_t) * (size_t)g.nwords, hipMemcpyDeviceToHost,

@@ -4,7 +4,6 @@ CPU oracle (oracle/quant_oracle.py) on seeded synthetic alignments.  Bit-exact:
 every per-row class and count, every vector entry, histogram and counter."""
 from __future__ import annotations
 
-import ctypes
 import functools
 import math
 
@@ -13,6 +12,7 @@ import pandas as pd
 import pytest
 
 from crispresso_amd import _lib, quantify, synth
+from crispresso_amd.devmem import DeviceBuffer
 from oracle import oracle_py
 from oracle import quant_oracle as qo
 from tests.test_quant_oracle import QUANT_SETS, case_inputs, golden_cases, load, params_from
@@ -269,30 +269,6 @@ def test_e2e_capture_quantify_alignments(gq):
             assert out[1 + i].tolist() == q[k], (name, k)
 
 
-class _Hip:
-    """hipMalloc / hipMemcpy through the HIP runtime libcrispr_nw.so already loaded.
-    (torch bundles a second HIP runtime, which sees no GPU once this one owns it.)"""
-
-    def __init__(self):
-        self.lib = ctypes.CDLL("libamdhip64.so.7")
-        self.lib.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-        self.lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        self.lib.hipFree.argtypes = [ctypes.c_void_p]
-
-    def to_device(self, a: np.ndarray) -> int:
-        p = ctypes.c_void_p()
-        assert self.lib.hipMalloc(ctypes.byref(p), max(a.nbytes, 1)) == 0
-        assert self.lib.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0     # host -> device
-        return int(p.value)
-
-    def to_host(self, d: int, a: np.ndarray) -> np.ndarray:
-        assert self.lib.hipMemcpy(a.ctypes.data, d, a.nbytes, 2) == 0     # device -> host
-        return a
-
-    def free(self, d: int) -> None:
-        self.lib.hipFree(d)
-
-
 def test_device_resident_after_aligner(gpu_aligner_factory, gq):
     """Aligner output consumed in HBM (nw_batch_device_output -> nwq_run_device)
     gives what the oracle gives on the downloaded strings."""
@@ -311,15 +287,9 @@ def test_device_resident_after_aligner(gpu_aligner_factory, gq):
     um = score == 100
     prm = make_params(amp, {"guide": True, "window": 10})
     gq.set_params(globals_for(prm), args_for(prm, False))
-    hip = _Hip()
-    d_pre = hip.to_device(quantify.pre_flags(um))
-    d_out = hip.to_device(np.zeros((n, 4), np.int32))
-    try:
-        tot_dev = gq.unpack_totals(gq.run_device(d_aln, stride, d_stats, 8, d_pre, n, d_out), stride)
-        reads_dev = hip.to_host(d_out, np.zeros((n, 4), np.int32))
-    finally:
-        hip.free(d_pre)
-        hip.free(d_out)
+    with DeviceBuffer.from_array(quantify.pre_flags(um)) as d_pre, DeviceBuffer(16 * n) as d_out:
+        tot_dev = gq.unpack_totals(gq.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n, d_out.ptr), stride)
+        reads_dev = d_out.download(np.zeros((n, 4), np.int32))
     R = [batch.aln[i, 0, :lens[i]].tobytes().decode() for i in range(n)]
     M = [batch.aln[i, 1, :lens[i]].tobytes().decode() for i in range(n)]
     S = [batch.aln[i, 2, :lens[i]].tobytes().decode() for i in range(n)]
