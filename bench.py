@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s (x1e12)
 READS_PER_GPU = 1_000_000
+# rocprofv3 --pmc summary of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
+# 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_quant", "pmc_summary.json")
 AMPLICON_LEN = 250
 
 
@@ -71,6 +74,18 @@ def max_over_ranks(dist, local, value):
     t = torch.tensor([value], dtype=torch.float64, device=f"cuda:{local}")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def pmc_traffic(*prefixes):
+    """HBM bytes per launch of the kernels whose names start with `prefixes`, from PMC_SUMMARY."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None
+    vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
+            if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
+    return float(sum(vals)) if vals else None
 
 
 def cpu_baseline(amplicon, buf, offsets, n_sample, threads):
@@ -133,7 +148,9 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
         "kernel": "nwq::quant_kernel + nwq::quant_reduce",
         "kernel_ms_avg": kavg,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce"),
+                     "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT),
                      "algo_bytes_per_launch": algo,
                      "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 16 (result); + 3*aln_len for rows not "
                                        "UNMODIFIED on input (the three alignment rows)"},
@@ -248,7 +265,10 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk",
+                                       "void nw::nw_align_kernel") if geo["tb_mode"].startswith("stream") else None,
+                "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                  "passes of the same bench command, per launch of fill + walk + fallback)",
                 "kernel": (f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
                            if geo["tb_mode"].startswith("stream")
                            else f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>"),
