@@ -181,7 +181,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--reads", type=int, default=READS_PER_GPU)
-    ap.add_argument("--cpu-sample", type=int, default=100_000)
+    ap.add_argument("--cpu-sample", type=int, default=300_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-quant", action="store_true", help="skip the downstream quantification leg")
