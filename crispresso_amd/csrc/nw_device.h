@@ -49,6 +49,9 @@ struct KernelArgs {
     // pad/unknown; null = per-read profile (any alphabet)
     const uint32_t* ptab;
     const uint8_t* lut6;       // [256] ascii -> 0..5 in that order, 6 = not in the table
+    // stream fill, per-read profile path: prof (int16) + 2 * gap_extend, the
+    // diagonal step of the (r + c) * extend biased recurrence (nw_stream.hip)
+    const int16_t* prof_fill;
 };
 
 // Traceback storage of a kernel instantiation.

@@ -88,6 +88,7 @@ struct nw_ctx {
     int R = 0;
     DevBuf<int8_t> d_prof;
     DevBuf<int16_t> d_prof16;         // pair kernel: int16, rows padded on top
+    DevBuf<int16_t> d_prof16f;        // stream fill: d_prof16 + 2 * extend (biased recurrence)
     DevBuf<uint32_t> d_ptab;          // stream kernel: pair-code score table (R <= 4)
     DevBuf<uint8_t> d_lut6;
     bool have_ptab = false;
@@ -167,8 +168,14 @@ int build_profile(nw_ctx* c) {
             prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
         }
     }
+    // The stream fill runs the recurrence on values biased by (r + c) * extend
+    // (nw_stream.hip): the diagonal step then gains 2 * extend, folded into its
+    // scores here.  prof16 itself stays unbiased (walk, pair kernel).
+    const int bias2 = 2 * c->gap_extend;
+    std::vector<int16_t> prof16f(prof16.size());
+    for (size_t q = 0; q < prof16.size(); ++q) prof16f[q] = (int16_t)(prof16[q] + bias2);
     // pair-code table of the stream kernel: for every (code of read A, code of
-    // read B) over A T G C N pad, each lane's 4 rows as packed int16x2
+    // read B) over A T G C N pad, each lane's 4 rows as packed int16x2 (biased)
     c->have_ptab = false;
     if (R4 == 4) {
         const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
@@ -178,8 +185,8 @@ int build_profile(nw_ctx* c) {
                 for (int ln = 0; ln < 64; ++ln)
                     for (int k = 0; k < 4; ++k) {
                         const size_t src = (size_t)ln * R4 + k;
-                        const uint16_t sa = (uint16_t)prof16[(size_t)codes[ia] * 64 * R4 + src];
-                        const uint16_t sb = (uint16_t)prof16[(size_t)codes[ib] * 64 * R4 + src];
+                        const uint16_t sa = (uint16_t)prof16f[(size_t)codes[ia] * 64 * R4 + src];
+                        const uint16_t sb = (uint16_t)prof16f[(size_t)codes[ib] * 64 * R4 + src];
                         ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
                     }
         uint8_t lut6[256];
@@ -199,6 +206,8 @@ int build_profile(nw_ctx* c) {
     }
     HIP_OR_FAIL(c, c->d_prof16.reserve(prof16.size()));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16.p, prof16.data(), prof16.size() * 2, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, c->d_prof16f.reserve(prof16f.size()));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16f.p, prof16f.data(), prof16f.size() * 2, hipMemcpyHostToDevice, c->stream));
     uint8_t lut[256];
     for (int q = 0; q < 256; ++q) lut[q] = code_of((unsigned char)q);
     HIP_OR_FAIL(c, c->d_prof.reserve(prof.size()));
@@ -287,7 +296,11 @@ int configure(nw_ctx* c) {
     // streaming fill + walk kernels (default when the scores fit int16)
     c->use_stream = false;
     const bool want_stream = !kern || std::strcmp(kern, "stream") == 0;
-    if (want_stream && fits16 && c->stream_slots > 0) {
+    // the stream fill's values carry a bias of up to (rows + span) * extend
+    const int64_t nl_rows = (int64_t)((La + R - 1) / R) * R;
+    const int64_t bias_max = (nl_rows + std::max<int64_t>(c->lb_max, 64) + 8) * c->gap_extend;
+    const bool fits16s = fits16 && hi + bias_max + c->gap_open < 16000;
+    if (want_stream && fits16s && c->stream_slots > 0) {
         nw::LaunchCfg f{}, w{};
         f.R = w.R = R;
         f.tb_mode = w.tb_mode = nw::TB_STREAM;
@@ -359,7 +372,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_prof.release(); c->d_lut.release(); c->d_amp.release();
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
-    c->d_prof16.release(); c->d_fallback.release(); c->d_fallback_count.release();
+    c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
@@ -499,6 +512,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             ap.out = a.out + lo * 3 * c->stride;
             ap.stats = a.stats + lo;
             ap.prof = (const int8_t*)c->d_prof16.p;
+            ap.prof_fill = c->d_prof16f.p;
             ap.band_slots = c->stream_slots;
             ap.region = c->d_region.p;
             ap.ptab = c->have_ptab ? c->d_ptab.p : nullptr;

@@ -151,9 +151,17 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
 
     const int La = args.La;
     const int O = args.gap_open, E = args.gap_extend;
-    const unsigned O2 = pk(O, O), E2 = pk(E, E);
+    const unsigned E2 = pk(E, E);
     const unsigned NEG2 = pk(-16384, -16384);
-    const unsigned MO0 = pk(-O, -O);
+    // Biased recurrence: every value of cell (r, c) (r = padded row + 1, c = pair
+    // column + 1; 0 = the DP boundary) carries + (r + c) * E.  A horizontal or
+    // vertical step then adds E, so X = max(Mo_left, X_left) and Y = max(Mo_up,
+    // Y_up) need no "- extend"; the diagonal step's + 2E is in the score table
+    // (prof_fill / ptab), and Mo = M - (O - E).  Traceback differences are
+    // unchanged (both operands carry the same bias); the walk removes the bias
+    // from captures and last row.  Boundary: H(r, 0) = r E, H(0, c) = c E.
+    const unsigned OE2 = pk(O - E, O - E);
+    const unsigned EmO2 = pk(E - O, E - O);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
     unsigned char* prof_lds = smem;
     const int prof_bytes = PT ? kPairCodes * kPairCodes * 64 * 16 : NCODE * 64 * PB;
     unsigned char* lut_lds = smem + align16(prof_bytes);
-    const int4* prof_src = PT ? (const int4*)args.ptab : (const int4*)args.prof;
+    const int4* prof_src = PT ? (const int4*)args.ptab : (const int4*)args.prof_fill;
     for (int q = tid; q < prof_bytes / 16; q += blockDim.x) ((int4*)prof_lds)[q] = prof_src[q];
     for (int q = tid; q < 256; q += blockDim.x) lut_lds[q] = PT ? args.lut6[q] : args.lut[q];
     __syncthreads();
@@ -292,11 +300,23 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
     lds_fence();
 
     // ---- per-lane DP state ----
+    // boundary column of this lane's rows: H(r, 0) = r E for r = lane R + k + 1;
+    // laneH = H(lane R, 0), the diagonal of the lane's top row at its first column
+    const unsigned laneH = pk(lane * R * E, lane * R * E);
+    unsigned kH[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) kH[k] = pk((k + 1) * E, (k + 1) * E);
     unsigned Mol[R], Xl[R], Hold[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
-    unsigned sMo = MO0, sY = NEG2, sH = 0u;
-    unsigned rMo = MO0, rY = NEG2, rH = 0u;
+    for (int k = 0; k < R; ++k) {
+        Hold[k] = as_u(as_v(laneH) + as_v(kH[k]));
+        Mol[k] = as_u(as_v(Hold[k]) + as_v(EmO2));
+        Xl[k] = NEG2;
+    }
+    unsigned sMo = EmO2, sY = NEG2, sH = 0u;
+    // lane 0's DPP "old" operands carry the top boundary row: rMo + E = Mo(0, c)
+    // and rH = H(0, c - 1) at its current column c, advanced by E every step
+    unsigned rMo = EmO2, rY = NEG2, rH = laneH;
     // Pair changes.  evT = step at which this lane's column is the first of its
     // next pair.  The next pair's pointers (n_*) are prepared for all lanes at
     // once at the staging point before that step (one change per lane and
@@ -373,10 +393,15 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             capp = n_capp;
             lrp = n_lrp;
 #pragma unroll
-            for (int k = 0; k < R; ++k) { Mol[k] = MO0; Xl[k] = NEG2; Hold[k] = 0u; }
-            rH = 0u;   // diagonal of row 0 at the pair's first column: the boundary
+            for (int k = 0; k < R; ++k) {
+                Hold[k] = as_u(as_v(laneH) + as_v(kH[k]));
+                Mol[k] = as_u(as_v(Hold[k]) + as_v(EmO2));
+                Xl[k] = NEG2;
+            }
+            rH = laneH;   // diagonal of the top row at the pair's first column: the boundary
+            rMo = EmO2;   // lane 0: Mo(0, 1) - E
         }
-        rMo = dpp_shr1(rMo, sMo);
+        rMo = dpp_shr1(as_u(as_v(rMo) + as_v(E2)), sMo);
         rY = dpp_shr1(rY, sY);
         load_scores(ridx, pn_a, pn_b);
         unsigned acc[NG];
@@ -394,21 +419,19 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
                 sc = as_v(__builtin_amdgcn_perm(pb.v[k >> 1], pa.v[k >> 1], sel));
             }
             const s16x2 M = Hd + sc;
-            const s16x2 Xe = as_v(Xl[k]) - as_v(E2);
-            const s16x2 X = __builtin_elementwise_max(as_v(Mol[k]), Xe);
-            const s16x2 Ye = Yu - as_v(E2);
-            const s16x2 Y = __builtin_elementwise_max(Mou, Ye);
+            const s16x2 X = __builtin_elementwise_max(as_v(Mol[k]), as_v(Xl[k]));
+            const s16x2 Y = __builtin_elementwise_max(Mou, Yu);
             const s16x2 mxy = __builtin_elementwise_max(X, Y);
             const s16x2 H = __builtin_elementwise_max(M, mxy);
-            const unsigned d1 = as_u(Mou - Ye);
-            const unsigned d2 = as_u(as_v(Mol[k]) - Xe);
+            const unsigned d1 = as_u(Mou - Yu);
+            const unsigned d2 = as_u(as_v(Mol[k]) - as_v(Xl[k]));
             const unsigned d3 = as_u(Y - X);
             const unsigned d4 = as_u(mxy - M);
             const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
             const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
             acc[k >> 2] = and_or(tt, mT[k & 3], acc[k >> 2]);
             acc[k >> 2] = and_or(uu, mU[k & 3], acc[k >> 2]);
-            const s16x2 Mo = M - as_v(O2);
+            const s16x2 Mo = M - as_v(OE2);
             Hd = as_v(Hold[k]);
             Hold[k] = as_u(H);
             Mol[k] = as_u(Mo);
@@ -420,7 +443,7 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
         sY = as_u(Yu);
         // the row above's H at this column, for the next step (reads the previous
         // step's sH; done after its use as the diagonal, so rH needs no copy)
-        rH = dpp_shr1(rH, sH);
+        rH = dpp_shr1(as_u(as_v(rH) + as_v(E2)), sH);
         sH = Hold[R - 1];
         if ((unsigned)slot < (unsigned)slots) {
 #pragma unroll
@@ -482,7 +505,7 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
     constexpr int NG = SGeo<R>::NG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int La = args.La;
-    const int O = args.gap_open;
+    const int O = args.gap_open, E = args.gap_extend;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -550,6 +573,11 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
                                                  (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
         }
         const int flags = args.ptab ? *(const int*)(base + reg.flags) : 0;
+        // the fill's Mo of cell (r, c) is M - O + E + (r + c) E (biased recurrence):
+        // captures are column c = span, row r = g + 1; the last row is r = nl R,
+        // column c = pad + q + 1
+        const int capb = O - E - (1 + span) * E;
+        const int lastb = O - E - (nl * R + pad + 1) * E;
         long long key;
         if (small_keys) {
             // 32-bit keys, DPP max: score (int16) | class | position
@@ -559,7 +587,7 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
                 for (int k = 0; k < R; ++k) {
                     const int ai = lane * R + k - F;
                     if (ai >= 0) {
-                        const int v = half(caps[lane * R + k], h) + O;
+                        const int v = half(caps[lane * R + k], h) + capb - (lane * R + k) * E;
                         const unsigned kk = (ai == La - 1) ? end_key32(v, 3, 0) : end_key32(v, 2, ai);
                         k32 = kk > k32 ? kk : k32;
                     }
@@ -567,7 +595,7 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
             }
 #pragma unroll 4
             for (int q = lane; q < Lb - 1; q += 64) {
-                const unsigned kk = end_key32(half(last[pad + q], h) + O, 1, q);
+                const unsigned kk = end_key32(half(last[pad + q], h) + lastb - q * E, 1, q);
                 k32 = kk > k32 ? kk : k32;
             }
             key = end_key_widen(wave_max_u32(k32));
@@ -578,14 +606,14 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
                 for (int k = 0; k < R; ++k) {
                     const int ai = lane * R + k - F;
                     if (ai >= 0) {
-                        const int v = half(caps[lane * R + k], h) + O;
+                        const int v = half(caps[lane * R + k], h) + capb - (lane * R + k) * E;
                         const long long kk = (ai == La - 1) ? end_key(v, 3, 0) : end_key(v, 2, ai);
                         key = kk > key ? kk : key;
                     }
                 }
             }
             for (int q = lane; q < Lb - 1; q += 64) {
-                const long long kk = end_key(half(last[pad + q], h) + O, 1, q);
+                const long long kk = end_key(half(last[pad + q], h) + lastb - q * E, 1, q);
                 key = kk > key ? kk : key;
             }
             key = wave_max_i64(key);
