@@ -35,7 +35,9 @@ VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane
 READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summary of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_quant", "pmc_summary.json")
+# (newest first: the aligner kernels' latest summary, then the one that also holds the quantification kernels)
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_bias_pmc", "pmc_summary.json"),
+                 os.path.join(ROOT, "profiles", "r01_quant", "pmc_summary.json")]
 AMPLICON_LEN = 250
 
 
@@ -77,15 +79,19 @@ def max_over_ranks(dist, local, value):
 
 
 def pmc_traffic(*prefixes):
-    """HBM bytes per launch of the kernels whose names start with `prefixes`, from PMC_SUMMARY."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            summ = json.load(f)
-    except (OSError, ValueError):
-        return None
-    vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
-            if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
-    return float(sum(vals)) if vals else None
+    """(HBM bytes per launch of the kernels whose names start with `prefixes`, source file), from the
+    first summary in PMC_SUMMARIES that holds them."""
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
+                if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
+        if vals:
+            return float(sum(vals)), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(amplicon, buf, offsets, n_sample, threads):
@@ -140,6 +146,7 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
     elapsed = max_over_ranks(dist, local, time.perf_counter() - t0)
     algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
     kavg = float(np.mean(kms))
+    q_traffic, q_src = pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce")
     out = {
         "metric": "quantified reads/s (process_df_chunk on the aligned C2 batch, device-resident)",
         "value": n_reads * world * steps / elapsed,
@@ -149,8 +156,8 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
         "kernel_ms_avg": kavg,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce"),
-                     "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT),
+                     "traffic": q_traffic,
+                     "traffic_source": q_src,
                      "algo_bytes_per_launch": algo,
                      "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 16 (result); + 3*aln_len for rows not "
                                        "UNMODIFIED on input (the three alignment rows)"},
@@ -235,6 +242,8 @@ def main():
         quant = quant_leg(al, amplicon, args.reads, args.steps, args.warmup, dist, local, rank, world,
                           args.quant_cpu_sample, args.no_cpu)
 
+    traffic, traffic_src = (pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk", "void nw::nw_align_kernel")
+                            if geo["tb_mode"].startswith("stream") else (None, None))
     total_reads = args.reads * world * args.steps
     value = total_reads / elapsed
     if rank == 0:
@@ -265,10 +274,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk",
-                                       "void nw::nw_align_kernel") if geo["tb_mode"].startswith("stream") else None,
-                "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                  "passes of the same bench command, per launch of fill + walk + fallback)",
+                "traffic": traffic,
+                "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench "
+                                  "command, per launch of fill + walk + fallback)",
                 "kernel": (f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
                            if geo["tb_mode"].startswith("stream")
                            else f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>"),

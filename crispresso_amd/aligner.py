@@ -194,7 +194,9 @@ class GpuAligner:
         return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
 
     # -- synchronous path ----------------------------------------------------
-    def align_packed(self, buf: np.ndarray, offsets: np.ndarray) -> AlignmentBatch:
+    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True) -> AlignmentBatch:
+        """Align a packed batch.  ``strings=False`` copies back only the per-read
+        records (identity, score, ...): what a ``just_score`` pass (CORE:1740-1741) reads."""
         if self.reference is None:
             raise NeedleError("no amplicon set")
         n = len(offsets) - 1
@@ -202,10 +204,10 @@ class GpuAligner:
         max_len = int(lens.max()) if n else 1
         stride = int(self.lib.nw_required_stride(self._h, max(max_len, 1)))
         stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
-        aln = np.zeros((n, 3, stride), dtype=np.uint8)
+        aln = np.empty((n, 3, stride if strings else 0), dtype=np.uint8)
         self._check(
-            self.lib.nw_align_batch(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(aln), stride,
-                                    _lib.ptr(stats)),
+            self.lib.nw_align_batch(self._h, _lib.ptr(buf), _lib.ptr(offsets), n,
+                                    _lib.ptr(aln) if strings else None, stride, _lib.ptr(stats)),
             "nw_align_batch",
         )
         return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)

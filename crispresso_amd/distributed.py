@@ -68,14 +68,14 @@ class MultiGpuAligner:
             a.set_reference(seq)
         self.reference = seq
 
-    def align_packed(self, buf: np.ndarray, offsets: np.ndarray) -> AlignmentBatch:
+    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True) -> AlignmentBatch:
         n = len(offsets) - 1
         world = len(self.aligners)
         jobs = []
         for rank, al in enumerate(self.aligners):
             lo, hi = shard_range(n, world, rank)
             b, o = slice_batch(buf, offsets, lo, hi)
-            jobs.append(self._pool.submit(al.align_packed, b, o))
+            jobs.append(self._pool.submit(al.align_packed, b, o, strings))
         return concat_batches([j.result() for j in jobs])
 
     def close(self) -> None:

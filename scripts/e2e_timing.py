@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Host-inclusive timings of the aligner path: what a CRISPResso
+run sees, as opposed to bench.py's device-resident `value`.
+
+Stages for N synthetic C2 reads (and the C3 HDR variant), one MI355X:
+  fastq      FASTQ text -> names + packed reads (crispresso_amd.fastq)
+  upload     nw_batch_upload (H2D of reads + offsets)
+  kernels    nw_batch_run_async + sync (device time, HIP events)
+  download   nw_batch_download (D2H of the three strings + records)
+  dataframe  batch_to_dataframe (the DataFrame parse_needle_output would give)
+  align_reads  CRISPRessoCORE.py:1788-2000 end to end (fastq .. filtered DataFrame)
+Usage: e2e_timing.py [n_reads] [out.json]
+"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from crispresso_amd import fastq, synth  # noqa: E402
+from crispresso_amd.aligner import GpuAligner  # noqa: E402
+from crispresso_amd.needle import AlignArgs, align_reads, batch_to_dataframe  # noqa: E402
+
+
+def write_fastq(path, buf, offsets):
+    n = len(offsets) - 1
+    with open(path, "wb") as f:
+        for lo in range(0, n, 100_000):
+            hi = min(n, lo + 100_000)
+            parts = []
+            for i in range(lo, hi):
+                s = bytes(buf[offsets[i]:offsets[i + 1]])
+                parts.append(b"@SYN:1:FC:1:%d:%d 1:N:0:1\n%s\n+\n%s\n" % (i // 1000, i % 1000, s, b"I" * len(s)))
+            f.write(b"".join(parts))
+
+
+def timed(fn, *a, **k):
+    t = time.perf_counter()
+    r = fn(*a, **k)
+    return r, time.perf_counter() - t
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "e2e.json")
+    amp, hdr, buf, off = synth.c3_workload(n)
+    res = {"n_reads": n, "amplicon_len": len(amp)}
+    with tempfile.TemporaryDirectory() as td:
+        fq = os.path.join(td, "reads.fastq")
+        _, res["write_fastq_s"] = timed(write_fastq, fq, buf, off)
+        (names, b2, o2), res["fastq_s"] = timed(fastq.read_fastq_as_fasta, fq)
+        with GpuAligner(0) as al:
+            al.set_reference(amp)
+            al.align_packed(b2[: o2[min(n, 1000)]], o2[: min(n, 1000) + 1])   # warm-up
+            _, res["upload_s"] = timed(al.upload, b2, o2)
+            al.run_async()
+            res["kernels_ms"] = al.sync()
+            maxlen = int(np.diff(o2).max())
+            batch, res["download_s"] = timed(al.download, n, maxlen)
+            _, res["dataframe_s"] = timed(batch_to_dataframe, batch, names, "ref")
+            _, res["align_packed_s"] = timed(al.align_packed, b2, o2)
+            _, res["align_packed_scores_only_s"] = timed(al.align_packed, b2, o2, False)
+            df, res["align_reads_c2_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp), fq, al)
+            res["align_reads_c2_rows"] = int(len(df))
+            df, res["align_reads_c3_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp,
+                                                                       expected_hdr_amplicon_seq=hdr), fq, al)
+            res["align_reads_c3_rows"] = int(len(df))
+    res["pcie_inclusive_reads_per_s"] = n / (res["upload_s"] + res["kernels_ms"] * 1e-3 + res["download_s"])
+    res["align_reads_c2_reads_per_s"] = n / res["align_reads_c2_s"]
+    res["align_reads_c3_reads_per_s"] = n / res["align_reads_c3_s"]
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -37,7 +37,7 @@ class OracleAligner:
     def set_reference(self, seq):
         self.reference = seq
 
-    def align_packed(self, buf, offsets):
+    def align_packed(self, buf, offsets, strings=True):
         return oracle_batch(self.reference, buf, offsets, self.options.awidth, self.options.gap_open,
                             self.options.gap_extend)
 
