@@ -263,10 +263,10 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     const int mxy = max(X, Y);
                     const int H = max(M, mxy);
                     unsigned a = acc[k >> 3];
-                    a = push_sign(a, Mou - Ye);       // Y extend
-                    a = push_sign(a, Mol[k] - Xe);    // X extend
+                    a = push_sign(a, Ye - Mou);       // Y opens (open > extend)
+                    a = push_sign(a, Xe - Mol[k]);    // X opens
                     a = push_sign(a, Y - X);          // X > Y
-                    a = push_sign(a, mxy - M);        // M > max(X, Y)
+                    a = push_sign(a, M - mxy);        // M < max(X, Y)
                     acc[k >> 3] = a;
                     mlast = (k == klast) ? M : mlast;
                     Hd = Hold[k];

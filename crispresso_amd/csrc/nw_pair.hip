@@ -222,10 +222,10 @@ __global__ __launch_bounds__(kPairMaxThreads) void nw_pair_kernel(const KernelAr
                 const s16x2 Y = __builtin_elementwise_max(Mou, Ye);
                 const s16x2 mxy = __builtin_elementwise_max(X, Y);
                 const s16x2 H = __builtin_elementwise_max(M, mxy);
-                const unsigned d1 = as_u(Mou - Ye);          // sign: Y extends
-                const unsigned d2 = as_u(as_v(Mol[k]) - Xe); // sign: X extends
+                const unsigned d1 = as_u(Ye - Mou);          // sign: Y opens (open > extend)
+                const unsigned d2 = as_u(Xe - as_v(Mol[k])); // sign: X opens
                 const unsigned d3 = as_u(Y - X);             // sign: X > Y
-                const unsigned d4 = as_u(mxy - M);           // sign: M > max(X, Y)
+                const unsigned d4 = as_u(M - mxy);           // sign: M < max(X, Y)
                 // v_perm selectors 8..11 give 0x00/0xff from bit 15/31 of a source: one byte
                 // per (difference, read) -> [yA yB xA xB] and [bXA bXB bMA bMB]; row k of its
                 // 4-row group lands in bit k (first word) and bit 4+k (second word) of each byte

@@ -423,10 +423,12 @@ __global__ __launch_bounds__(640, NW_FILL_WAVES_PER_SIMD) void nw_stream_fill(co
             const s16x2 Y = __builtin_elementwise_max(Mou, Yu);
             const s16x2 mxy = __builtin_elementwise_max(X, Y);
             const s16x2 H = __builtin_elementwise_max(M, mxy);
-            const unsigned d1 = as_u(Mou - Yu);
-            const unsigned d2 = as_u(as_v(Mol[k]) - as_v(Xl[k]));
+            // sign bits (nw_common.h walk_runs): Y opens (open > extend), X opens,
+            // X > Y, M < max(X, Y) -- ties extend gaps and stay on the diagonal
+            const unsigned d1 = as_u(Yu - Mou);
+            const unsigned d2 = as_u(as_v(Xl[k]) - as_v(Mol[k]));
             const unsigned d3 = as_u(Y - X);
-            const unsigned d4 = as_u(mxy - M);
+            const unsigned d4 = as_u(M - mxy);
             const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
             const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
             acc[k >> 2] = and_or(tt, mT[k & 3], acc[k >> 2]);

@@ -353,3 +353,59 @@ def quantify_alignments(df_needle_alignment: pd.DataFrame, args, quantifier: Opt
     g = globals_ or _GLOBALS or globals_from_args(args)
     reads, tot = _run_df(df, args, g, quantifier, n_rule="N" in args.amplicon_seq.upper())
     return _result_tuple(df, reads, tot, bool(getattr(args, "coding_seq", None)))
+
+
+# ------------------------------------------------------------------ run summary
+
+def run_summary(df: pd.DataFrame, len_amplicon: int, cut_points: Sequence[int]) -> Dict:
+    """The per-run aggregates ``run_crispresso`` returns after the quantification
+    (the values tests/crispresso_tests.py:181-195 asserts), from the quantified
+    DataFrame (UNMODIFIED / NHEJ / HDR / MIXED / n_* columns):
+
+    * n_total, n_modified, n_unmodified, n_mixed_hdr_nhej, n_repaired   CORE:2025, 2866-2869
+    * nhej_/hdr_/mixed_ inserted / deleted / mutated (rows with n_* > 0)  CORE:3751-3803
+    * df_indels: histogram of ``effective_len - LEN_AMPLICON`` over
+      ``arange(-min_cut, LEN - max_cut)`` (``LEN // 2`` each side without guides)
+                                                                         CORE:2903-2905, 2960-2973, 3886-3888
+    * df_insertion / df_deletion / df_substitution: histograms of n_inserted /
+      n_deleted / n_mutated over ``range(0, max(15, round(p99 of the non-zero
+      values)))``                                                        CORE:2345-2365, 3891-3904
+    * df_alleles: group-by of (align_seq, ref_seq, NHEJ, UNMODIFIED, HDR,
+      n_deleted, n_inserted, n_mutated) sizes, sorted by ``#Reads`` descending
+                                                                         CORE:2923-2946
+    """
+    L = int(len_amplicon)
+    out: Dict = {"n_total": int(df.shape[0])}
+    for key, col in (("n_modified", "NHEJ"), ("n_unmodified", "UNMODIFIED"), ("n_mixed_hdr_nhej", "MIXED"),
+                     ("n_repaired", "HDR")):
+        out[key] = int(df[col].sum())
+    for cls, tag in (("NHEJ", "nhej"), ("HDR", "hdr"), ("MIXED", "mixed")):
+        sel = df[df[cls] == True]  # noqa: E712  (the reference's own test, CORE:3752)
+        for what, col in (("inserted", "n_inserted"), ("deleted", "n_deleted"), ("mutated", "n_mutated")):
+            out[f"{tag}_{what}"] = int(np.sum(sel[col] > 0))
+    eff = L + df["n_inserted"].to_numpy(dtype=np.int64) - df["n_deleted"].to_numpy(dtype=np.int64)
+    if len(cut_points):
+        xmin, xmax = -min(cut_points), L - max(cut_points)
+    else:
+        xmin, xmax = -(L // 2), L // 2
+    hdensity, hlengths = np.histogram(eff - L, np.arange(xmin, xmax))
+    out["df_indels"] = pd.DataFrame(np.vstack([hlengths[:-1], hdensity]).T, columns=["indel_size", "fq"])
+
+    def calculate_range(col):
+        nz = df.loc[df[col] > 0, col]
+        try:
+            return max(15, int(np.round(np.percentile(nz, 99))))
+        except Exception:   # empty selection, as the reference's bare except (CORE:2349)
+            return 15
+
+    for name, col, size_col, sign in (("df_insertion", "n_inserted", "ins_size", 1),
+                                      ("df_deletion", "n_deleted", "del_size", -1),
+                                      ("df_substitution", "n_mutated", "sub_size", 1)):
+        y, x = np.histogram(df[col], bins=range(0, calculate_range(col)))
+        out[name] = pd.DataFrame(np.vstack([sign * x[:-1], y]).T, columns=[size_col, "fq"])
+    alleles = df.groupby(["align_seq", "ref_seq", "NHEJ", "UNMODIFIED", "HDR", "n_deleted", "n_inserted",
+                          "n_mutated"]).size().reset_index()
+    alleles = alleles.rename(columns={0: "#Reads", "align_seq": "Aligned_Sequence", "ref_seq": "Reference_Sequence"})
+    alleles["%Reads"] = alleles["#Reads"] / alleles["#Reads"].sum() * 100.0
+    out["df_alleles"] = alleles.sort_values(by="#Reads", ascending=False)
+    return out

@@ -1,7 +1,9 @@
 /*
  * nw_oracle.c -- scalar CPU restatement of EMBOSS needle 6.6.0 (endweight off).
  *
- * TEST INFRASTRUCTURE ONLY (see nw_oracle.h).  Parity vs EMBOSS: unpinned.
+ * TEST INFRASTRUCTURE ONLY (see nw_oracle.h).  Parity vs EMBOSS: pinned end to end
+ * by the reference's own e2e test values (see the tie rules below); no EMBOSS binary
+ * or source exists offline, so per-alignment golden files are not available.
  *
  * Model (DESIGN.md "EMBOSS semantics"):
  *  - a = amplicon = rows (needle -asequence, CRISPRessoCORE.py:1798),
@@ -10,8 +12,15 @@
  *      M[i][j] = best(M,X,Y)[i-1][j-1] + s(a_i, b_j)
  *      X[i][j] = max(M[i][j-1] - open, X[i][j-1] - extend)   (gap in a, consumes b_j)
  *      Y[i][j] = max(M[i-1][j] - open, Y[i-1][j] - extend)   (gap in b, consumes a_i)
- *    best(): M if M > X and M > Y, else X if X > Y, else Y (strict; ties leave M,
- *    and an X==Y tie picks Y).  Gap choice: open when open >= extend.
+ *    The values need no tie rule; the traceback's choices do:
+ *    predecessor of an M cell: M if M >= X and M >= Y (ties stay on the diagonal),
+ *    else X if X > Y, else Y; a gap run ends (was opened) only when open > extend
+ *    (ties extend the gap).  These two rules are PINNED against real EMBOSS
+ *    through the reference's own end-to-end assertions
+ *    (tests/crispresso_tests.py:181-195, tests/golden/make_e2e_golden.py): the
+ *    previous choice (strict M, open on ties) misses 10 of the 14 asserted values,
+ *    this one reproduces all 14.  The X/Y tie and the start-cell scan order are
+ *    not exercised by that data (unpinned).
  *  - Free end gaps (needle -endweight defaults to false; CRISPResso never sets it):
  *    row 0 / column 0 hold M = 0, X = Y = -inf.  This reproduces EMBOSS's first
  *    row/column initialisation (m = match, ix/iy = -gapopen).
@@ -91,7 +100,7 @@ int oracle_params_init(oracle_params* p, float gap_open, float gap_extend) {
 enum { ST_M = 0, ST_X = 1, ST_Y = 2 };
 
 static inline int best_state(int m, int x, int y) {
-    if (m > x && m > y) return ST_M;
+    if (m >= x && m >= y) return ST_M;
     if (x > y) return ST_X;
     return ST_Y;
 }
@@ -204,11 +213,11 @@ static int align_with(const char* a, int32_t la, const int* ca, const char* b,
             i--; j--;
         } else if (st == ST_X) {
             --k; ra[k] = '-'; rb[k] = b[j - 1];
-            st = (d->M[c - 1] - O >= d->X[c - 1] - E) ? ST_M : ST_X;
+            st = (d->M[c - 1] - O > d->X[c - 1] - E) ? ST_M : ST_X;
             j--;
         } else {
             --k; ra[k] = a[i - 1]; rb[k] = '-';
-            st = (d->M[c - W] - O >= d->Y[c - W] - E) ? ST_M : ST_Y;
+            st = (d->M[c - W] - O > d->Y[c - W] - E) ? ST_M : ST_Y;
             i--;
         }
     }
