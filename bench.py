@@ -36,7 +36,8 @@ READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summary of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic
 # (newest first: the aligner kernels' latest summary, then the one that also holds the quantification kernels)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_bias_pmc", "pmc_summary.json"),
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_diag_pmc", "pmc_summary.json"),
+                 os.path.join(ROOT, "profiles", "r01_bias_pmc", "pmc_summary.json"),
                  os.path.join(ROOT, "profiles", "r01_quant", "pmc_summary.json")]
 AMPLICON_LEN = 250
 
@@ -78,14 +79,16 @@ def max_over_ranks(dist, local, value):
     return float(t.item())
 
 
-def pmc_traffic(*prefixes):
+def pmc_traffic(*prefixes, required=None):
     """(HBM bytes per launch of the kernels whose names start with `prefixes`, source file), from the
-    first summary in PMC_SUMMARIES that holds them."""
+    first summary in PMC_SUMMARIES that holds them (and a kernel starting with `required`)."""
     for path in PMC_SUMMARIES:
         try:
             with open(path) as f:
                 summ = json.load(f)
         except (OSError, ValueError):
+            continue
+        if required and not any(k.startswith(required) for k in summ):
             continue
         vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
                 if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
@@ -242,8 +245,15 @@ def main():
         quant = quant_leg(al, amplicon, args.reads, args.steps, args.warmup, dist, local, rank, world,
                           args.quant_cpu_sample, args.no_cpu)
 
-    traffic, traffic_src = (pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk", "void nw::nw_align_kernel")
-                            if geo["tb_mode"].startswith("stream") else (None, None))
+    diag = geo["tb_mode"].startswith("diag")
+    if diag:
+        traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
+                                           required="nw::nw_band_fill")
+    elif geo["tb_mode"].startswith("stream"):
+        traffic, traffic_src = pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk", "void nw::nw_align_kernel",
+                                           required="void nw::nw_stream_fill")
+    else:
+        traffic, traffic_src = None, None
     total_reads = args.reads * world * args.steps
     value = total_reads / elapsed
     if rank == 0:
@@ -258,7 +268,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int16x2" if geo["tb_mode"].startswith(("pair", "stream")) else "int32",
+            "dtype": "int16x2" if geo["tb_mode"].startswith(("pair", "stream", "diag")) else "int32",
             "data": "synthetic (SURVEY 8d C2 mix: 60% exact, 20% 1-3 subs, 10% del, 5% ins, 5% 1% noise)",
             "config": {
                 "workload": f"C2: {args.reads} synthetic ~250 bp reads x 250 bp amplicon per GPU, "
@@ -277,7 +287,9 @@ def main():
                 "traffic": traffic,
                 "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench "
                                   "command, per launch of fill + walk + fallback)",
-                "kernel": (f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
+                "kernel": ("nw_band_hist/scan/scatter (length sort) + nw_band_fill + nw_band_walk "
+                           "(certified 32-diagonal band) + nw_align_kernel on the uncertified reads" if diag
+                           else f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
                            if geo["tb_mode"].startswith("stream")
                            else f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>"),
                 "kernel_ms_avg": avg_ms,
@@ -289,7 +301,10 @@ def main():
                 "valu": {
                     "gcups": gcups,
                     "cells_per_launch": cells,
-                    "note": "the DP is a dependent integer recurrence: VALU-bound, HBM frac is small by construction",
+                    "note": ("gcups counts the full La x Lb matrix of every read (the work the reference's needle "
+                             "does); the certified band computes 32 diagonals per read and proves the rest cannot "
+                             "change the result (DESIGN.md §4)" if diag else
+                             "the DP is a dependent integer recurrence: VALU-bound, HBM frac is small by construction"),
                 },
             },
             "cpu_baseline": cpu,

@@ -26,7 +26,7 @@ NW_E_NOMEM = -5
 NW_E_STATE = -6
 NW_TIE_EMBOSS = 0
 NW_FLAG_EMPTY = 1
-TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 3: "pair-band-int16", 4: "stream-int16"}
+TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 3: "pair-band-int16", 4: "stream-int16", 5: "diag-int16"}
 
 # Field order of nw_stat (include/crispr_nw.h).
 STAT_FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j", "flags")

@@ -1,0 +1,539 @@
+// nw_band.hip -- certified diagonal-band DP: the default aligner path.
+//
+// The stream kernels (nw_stream.hip) fill every cell of the La x Lb matrix.  A
+// CRISPResso read is a near-copy of its amplicon, so its optimal alignments stay
+// within a few diagonals of the main one.  These kernels fill only a band of
+// kBD = 32 diagonals [dlo, dlo + 31] around [min(0, Lb - La), max(0, Lb - La)]
+// and then PROVE that the result is the full DP's result:
+//
+//   A path that visits a cell on diagonal d = j - i has left |d| residues of one
+//   sequence unpaired on the way there, so it pairs at most
+//       min(Lb - d, La)  (d > 0)   or   min(Lb, La + d)  (d < 0)
+//   residues, and every pair scores at most the matrix maximum (EDNAFULL: 5) while
+//   gaps cost >= 0.  Hence every alignment touching a diagonal outside the band
+//   scores at most UB = maxsub * max(min(Lb - dhi - 1, La), min(Lb, La + dlo - 1)).
+//   If the best in-band score S > UB, every optimal alignment -- and every
+//   alignment tied with one -- lies inside the band.  All values the traceback
+//   compares (the predecessor states of an optimal path, the start cells of the
+//   last row/column with score S, the open/extend choices along the path) are
+//   then values of in-band paths, which the banded DP computes exactly; values it
+//   under-estimates are strictly below S and below the compared optimum.  So the
+//   banded traceback, with the same tie rules, is the full DP's
+//   traceback, bit for bit.
+//
+// Reads that fail the certificate (S <= UB: chimeras, off-target, large indels),
+// whose length differs from the amplicon's by more than 31, or that hold IUPAC
+// codes other than N go to the exact int32 kernel's fallback list.
+//
+// Layout / schedule:
+//   * reads are sorted by length on the device (counting sort, nw_band_hist /
+//     _scan / _scatter); sorted positions (2g, 2g+1) form pair g, both reads of a
+//     pair have the same length (unequal pairs fall back), so they share one
+//     geometry and run packed in int16x2 (read A low, B high);
+//   * one read pair per 16-lane DPP row, 4 pairs per wavefront; lane q owns
+//     diagonals d0 = dlo + 2q and d0 + 1; the wave sweeps anti-diagonals t = i + j
+//     and at each step every lane computes one cell (the diagonal whose parity
+//     matches t).  Predecessors: diag = own lane two steps back, up / left = own
+//     lane or its row neighbour one step back (DPP row_shr:1 / row_shl:1; the row
+//     edge reads -inf = outside the band).  Groups run at tau = t - dlo + kBK, so
+//     the step parity is wave-uniform;
+//   * biased recurrence as in nw_stream.hip: values carry + t * E, so X = max(Mo,
+//     X_left), Y = max(Mo, Y_up) with no "- extend"; the diagonal's + 2E is in
+//     the score table; Mo = M - (O - E);
+//   * 4 traceback bits per cell and read, 4 steps per dword: the same byte-plane
+//     packing as the stream kernels; per pair region: header, the M of each
+//     diagonal's last cell (= the last row / last column cells), bits
+//     [words][16 lanes];
+//   * nw_band_walk: one wavefront per read: start cell from the 32 captures,
+//     certificate, the run-based walk of nw_common.h over the band, strings.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "nw_common.h"
+
+#ifndef NW_BAND_WALK_CPL
+#define NW_BAND_WALK_CPL 2
+#endif
+
+namespace nw {
+
+namespace {
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_v(unsigned u) { return __builtin_bit_cast(s16x2, u); }
+__device__ __forceinline__ unsigned as_u(s16x2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ unsigned pk(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
+__device__ __forceinline__ int half(unsigned w, int h) { return (int)(short)(w >> (16 * h)); }
+__device__ __forceinline__ unsigned max2(unsigned a, unsigned b) {
+    return as_u(__builtin_elementwise_max(as_v(a), as_v(b)));
+}
+__device__ __forceinline__ unsigned add2(unsigned a, unsigned b) { return as_u(as_v(a) + as_v(b)); }
+__device__ __forceinline__ unsigned sub2(unsigned a, unsigned b) { return as_u(as_v(a) - as_v(b)); }
+// DPP within 16-lane rows; lanes without a source keep `old` (-inf: outside the band)
+__device__ __forceinline__ unsigned row_shr1(unsigned old, unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ unsigned row_shl1(unsigned old, unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x101, 0xf, 0xf, false);
+}
+__device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
+    unsigned d;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(m), "v"(c));
+    return d;
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) { return ~wave_max_u32(~v); }
+
+}  // namespace
+
+// ---- geometry shared by fill, walk and host --------------------------------------
+__host__ __device__ inline bool band_geometry(int La, int Lb, int* dlo) {
+    const int D = Lb - La;
+    const int lo0 = D < 0 ? D : 0, hi0 = D > 0 ? D : 0;
+    const int extra = kBandDiags - (hi0 - lo0 + 1);
+    *dlo = 0;
+    if (Lb <= 0 || extra < 0) return false;
+    *dlo = lo0 - extra / 2;
+    return true;
+}
+
+namespace {
+
+constexpr int kBL = kBandDiags / 2;   // lanes per read pair (one DPP row)
+constexpr int kBPW = 64 / kBL;        // read pairs per wavefront
+constexpr int kBK = 64;               // tau = t - dlo + kBK: >= 0 and even
+constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [-17, La + 48]
+constexpr int kJPad = 96;             // pair codes: index j + kJPad, j in [-79, La + 79]
+constexpr int kPadCode = 5;           // lut6: A T G C N pad
+constexpr int kTabBytes = 896;        // [6][36] packed scores (864 B)
+constexpr int kHdrBytes = 16;         // tau_base, dlo, flags, -
+constexpr int kCapBytes = kBandDiags * 4;
+
+__host__ __device__ inline int band_acd_elems(int La) { return La + kAPad + 64; }
+__host__ __device__ inline int band_pcs(int La) { return align16(La + kJPad + 96); }
+
+}  // namespace
+
+__host__ __device__ inline int band_words(int La, int Lb_max) {
+    const int Lbm = Lb_max < La + kBandDiags - 1 ? Lb_max : La + kBandDiags - 1;
+    return (La + Lbm + 80) / 4 + 2;
+}
+__host__ __device__ inline int64_t band_region_stride(int La, int Lb_max) {
+    return ((int64_t)kHdrBytes + kCapBytes + (int64_t)band_words(La, Lb_max) * kBL * 4 + 255) & ~(int64_t)255;
+}
+
+// ============================================================================
+// Counting sort of the reads by length (bucket cap + 1 holds longer reads).
+// Wave-aggregated atomics: one atomic per distinct length per wavefront.
+// ============================================================================
+__device__ __forceinline__ int len_bucket(const int64_t* offsets, long long r, int cap) {
+    const long long L = offsets[r + 1] - offsets[r];
+    return L <= cap ? (int)L : cap + 1;
+}
+
+__global__ __launch_bounds__(256) void nw_band_hist(const KernelArgs a) {
+    const int lane = threadIdx.x & 63;
+    for (long long base = (long long)blockIdx.x * blockDim.x; base < a.n; base += (long long)gridDim.x * blockDim.x) {
+        const long long r = base + threadIdx.x;
+        bool pending = r < a.n;
+        const int b = pending ? len_bucket(a.offsets, r, a.band_lb_cap) : 0;
+        for (;;) {
+            const unsigned long long act = __ballot(pending);
+            if (!act) break;
+            const int leader = (int)__builtin_ctzll(act);
+            const int key = __builtin_amdgcn_readlane(b, leader);
+            const bool mine = pending && b == key;
+            const unsigned long long m = __ballot(mine);
+            if (lane == leader) atomicAdd(&a.sort_hist[key], (int)__popcll(m));
+            if (mine) pending = false;
+        }
+    }
+}
+
+// exclusive scan of sort_hist[0 .. cap + 1] in place (one block of 1024 threads)
+__global__ __launch_bounds__(1024) void nw_band_scan(const KernelArgs a) {
+    __shared__ int part[1024];
+    const int nb = a.band_lb_cap + 2;
+    const int per = (nb + 1023) / 1024;
+    const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+    int s = 0;
+    for (int k = lo; k < hi; ++k) s += a.sort_hist[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = part[threadIdx.x] - s;
+    for (int k = lo; k < hi; ++k) {
+        const int c = a.sort_hist[k];
+        a.sort_hist[k] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void nw_band_scatter(const KernelArgs a) {
+    const int lane = threadIdx.x & 63;
+    int32_t* order = const_cast<int32_t*>(a.band_order);
+    for (long long base = (long long)blockIdx.x * blockDim.x; base < a.n; base += (long long)gridDim.x * blockDim.x) {
+        const long long r = base + threadIdx.x;
+        bool pending = r < a.n;
+        const int b = pending ? len_bucket(a.offsets, r, a.band_lb_cap) : 0;
+        for (;;) {
+            const unsigned long long act = __ballot(pending);
+            if (!act) break;
+            const int leader = (int)__builtin_ctzll(act);
+            const int key = __builtin_amdgcn_readlane(b, leader);
+            const bool mine = pending && b == key;
+            const unsigned long long m = __ballot(mine);
+            int pos = 0;
+            if (lane == leader) pos = atomicAdd(&a.sort_hist[key], (int)__popcll(m));
+            pos = __builtin_amdgcn_readlane(pos, leader);
+            if (mine) {
+                order[pos + (int)__popcll(m & ((1ull << lane) - 1ull))] = (int32_t)r;
+                pending = false;
+            }
+        }
+    }
+}
+
+// ============================================================================
+// Fill
+// ============================================================================
+__global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int La = a.La;
+    const int O = a.gap_open, E = a.gap_extend;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
+    const int q = lane & (kBL - 1), grp = lane / kBL;
+    const unsigned NEG2 = pk(-16384, -16384);
+    const unsigned OE2 = pk(O - E, O - E);
+
+    uint32_t* tab = (uint32_t*)smem;
+    uint16_t* acd = (uint16_t*)(smem + kTabBytes);
+    const int PCS = band_pcs(La);
+    unsigned char* pcd = smem + kTabBytes + align16(2 * band_acd_elems(La)) + (wave * kBPW + grp) * PCS;
+    for (int k = tid; k < 216; k += blockDim.x) tab[k] = a.band_tab[k];
+    for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
+        const int i = k - kAPad;   // row i = amplicon residue i - 1
+        const int c = (i >= 1 && i <= La) ? a.lut6[a.amp[i - 1]] : kPadCode;   // host: amplicon codes <= 5
+        acd[k] = (uint16_t)(c * 36 * 4);
+    }
+    __syncthreads();
+
+    // byte-plane masks of the sign bits (SGPRs: v_and_or_b32 takes no literal)
+    unsigned mT[4], mU[4];
+    asm volatile("s_mov_b32 %0, 0x01010101" : "=s"(mT[0]));
+    asm volatile("s_mov_b32 %0, 0x02020202" : "=s"(mT[1]));
+    asm volatile("s_mov_b32 %0, 0x04040404" : "=s"(mT[2]));
+    asm volatile("s_mov_b32 %0, 0x08080808" : "=s"(mT[3]));
+    asm volatile("s_mov_b32 %0, 0x10101010" : "=s"(mU[0]));
+    asm volatile("s_mov_b32 %0, 0x20202020" : "=s"(mU[1]));
+    asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
+    asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
+
+    const long long npairs = a.band_pair_hi - a.band_pair_lo;
+    const long long nwork = (npairs + kBPW - 1) / kBPW;
+    const int NW = a.band_words;
+    for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nwork; wv += (long long)gridDim.x * wpb) {
+        const long long g = a.band_pair_lo + wv * kBPW + grp;
+        int Lb = La, dlo = 0;
+        bool act = false;
+        long long offA = 0, offB = 0;
+        if (g < a.band_pair_hi) {
+            const long long ra = a.band_order[2 * g];
+            const long long rb = (2 * g + 1 < a.n) ? a.band_order[2 * g + 1] : ra;
+            offA = a.offsets[ra];
+            offB = a.offsets[rb];
+            const int LbA = (int)(a.offsets[ra + 1] - offA);
+            const int LbB = (int)(a.offsets[rb + 1] - offB);
+            act = LbA == LbB && LbA <= a.band_lb_cap && band_geometry(La, LbA, &dlo);
+            if (act) Lb = LbA;
+        }
+        if (!act) band_geometry(La, La, &dlo);   // neutral geometry, nothing stored
+
+        // pair codes of the group's columns (j = 1..Lb real, the rest pad)
+        bool badA = false, badB = false;
+        for (int k = q; k < PCS; k += kBL) {
+            const int j = k - kJPad;
+            int cA = kPadCode, cB = kPadCode;
+            if (act && j >= 1 && j <= Lb) {
+                cA = a.lut6[a.reads[offA + j - 1]];
+                cB = a.lut6[a.reads[offB + j - 1]];
+                // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
+                if (cA > kPadCode) { badA = true; cA = kPadCode; }
+                if (cB > kPadCode) { badB = true; cB = kPadCode; }
+            }
+            pcd[k] = (unsigned char)((cA * 6 + cB) * 4);
+        }
+        const unsigned long long bA = __ballot(badA), bB = __ballot(badB);
+        const int flags = (((bA >> (grp * kBL)) & 0xffffull) ? REGION_BAD_A : 0) |
+                          (((bB >> (grp * kBL)) & 0xffffull) ? REGION_BAD_B : 0);
+
+        // wave-uniform tau range; per lane: boundary and capture steps
+        const unsigned tlo = act ? (unsigned)(kBK - dlo) : 0xffffffffu;
+        const unsigned thi = act ? (unsigned)(kBK - dlo + La + Lb) : 0u;
+        const unsigned dmax = (unsigned)(-dlo > dlo + kBandDiags - 1 ? -dlo : dlo + kBandDiags - 1);
+        const unsigned tpro = act ? (unsigned)(kBK - dlo) + dmax + 1 : 0u;
+        const int tau0 = (int)(wave_min_u32(tlo) & ~3u);
+        const int tau_end = (int)wave_max_u32(thi);
+        const int tau_pro = (int)((wave_max_u32(tpro) + 3) & ~3u);
+        lds_fence();
+        if (tau_end == 0) continue;   // no active group in this wavefront
+
+        const int d0 = dlo + 2 * q;
+        int tb[2], te[2];
+        unsigned bval[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int d = d0 + p;
+            const int ad = d < 0 ? -d : d;
+            tb[p] = kBK - dlo + ad;
+            bval[p] = pk(E * ad, E * ad);
+            const int iend = La < Lb - d ? La : Lb - d;
+            const int ilo = 1 - d > 1 ? 1 - d : 1;
+            te[p] = iend >= ilo ? kBK - dlo + 2 * iend + d : -1;
+        }
+        unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
+        unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + q;
+
+        unsigned Hp0 = 0u, Hp1 = 0u, MoP = NEG2, XP = NEG2, YP = NEG2;
+        unsigned cap0 = NEG2, cap1 = NEG2;
+        // LDS code cursors of the block starting at tau4: rows i0, i0 + 1; columns j0 .. j0 + 2
+        auto ibase = [&](int tau4) { return (tau4 - kBK) / 2 - q; };
+        const uint16_t* ap = acd + kAPad + ibase(tau0);
+        const unsigned char* jp = pcd + kJPad + (ibase(tau0) + dlo + 2 * q);
+        auto load_scores = [&](unsigned* s) {
+            const int a0 = ap[0], a1 = ap[1];
+            const int j0 = jp[0], j1 = jp[1], j2 = jp[2];
+            s[0] = *(const unsigned*)((const unsigned char*)tab + a0 + j0);
+            s[1] = *(const unsigned*)((const unsigned char*)tab + a0 + j1);
+            s[2] = *(const unsigned*)((const unsigned char*)tab + a1 + j1);
+            s[3] = *(const unsigned*)((const unsigned char*)tab + a1 + j2);
+            ap += 2;   // rows and columns both advance by 2 per 4 steps
+            jp += 2;
+        };
+        unsigned sc[4], sn[4];
+        load_scores(sc);
+
+        auto step = [&](int tau, auto Uc, auto PROc, unsigned& acc) {
+            constexpr int U = decltype(Uc)::value;
+            constexpr int P = U & 1;
+            constexpr bool PRO = decltype(PROc)::value;
+            unsigned X, Y, d1, d2;
+            if constexpr (P == 0) {
+                // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
+                const unsigned Ml = row_shr1(NEG2, MoP), Xl = row_shr1(NEG2, XP);
+                X = max2(Ml, Xl);
+                d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
+                Y = max2(MoP, YP);
+                d1 = sub2(YP, MoP);    // sign: Y opens
+            } else {
+                // up = lane q+1's d0 one step back; left = own diagonal d0
+                const unsigned Mu = row_shl1(NEG2, MoP), Yu = row_shl1(NEG2, YP);
+                Y = max2(Mu, Yu);
+                d1 = sub2(Yu, Mu);
+                X = max2(MoP, XP);
+                d2 = sub2(XP, MoP);
+            }
+            unsigned M = add2(P ? Hp1 : Hp0, sc[U]);
+            const unsigned mxy = max2(X, Y);
+            unsigned H = max2(M, mxy);
+            const unsigned d3 = sub2(Y, X);     // sign: X > Y
+            const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
+            if constexpr (PRO) {
+                if (tau == tb[P]) {   // DP boundary cell (row 0 / column 0): M = 0, X = Y = -inf
+                    M = bval[P];
+                    H = M;
+                    X = NEG2;
+                    Y = NEG2;
+                }
+            }
+            if constexpr (P == 0) Hp0 = H; else Hp1 = H;
+            MoP = sub2(M, OE2);
+            XP = X;
+            YP = Y;
+            if constexpr (P == 0) cap0 = tau == te[0] ? M : cap0;
+            else cap1 = tau == te[1] ? M : cap1;
+            const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
+            const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
+            acc = and_or(tt, mT[U], acc);
+            acc = and_or(uu, mU[U], acc);
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        auto block = [&](int tau4, auto PROc) {
+            load_scores(sn);   // next block's scores (LDS latency hidden by this block)
+            unsigned acc = 0u;
+            step(tau4, I0{}, PROc, acc);
+            step(tau4 + 1, I1{}, PROc, acc);
+            step(tau4 + 2, I2{}, PROc, acc);
+            step(tau4 + 3, I3{}, PROc, acc);
+            const int w = (tau4 - tau0) >> 2;
+            if (act && w < NW) bits[w * kBL] = acc;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sc[u] = sn[u];
+        };
+        int tau4 = tau0;
+        for (; tau4 < tau_pro; tau4 += 4) block(tau4, std::true_type{});
+        for (; tau4 <= tau_end; tau4 += 4) block(tau4, std::false_type{});
+
+        if (act) {
+            unsigned* caps = (unsigned*)(region + kHdrBytes);
+            caps[2 * q] = cap0;
+            caps[2 * q + 1] = cap1;
+            if (q == 0) *(int4*)region = make_int4(tau0, dlo, flags, 0);
+        }
+    }
+}
+
+// ============================================================================
+// Walk + emit: one wavefront per read (sorted order), latency-bound.
+// ============================================================================
+constexpr int kBandReadCap = 1024;
+__host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
+__host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 4 + kBandReadCap + 256; }
+
+__global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int La = a.La, E = a.gap_extend;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
+    unsigned char* lut_lds = smem;
+    unsigned char* amp_lds = smem + 256;
+    unsigned* rowpos = (unsigned*)(smem + 256 + align16(La + 16));
+    for (int k = tid; k < 256; k += blockDim.x) lut_lds[k] = a.lut[k];
+    for (int k = tid; k < La; k += blockDim.x) {
+        amp_lds[k] = a.amp[k];
+        rowpos[k] = a.rowpos[k];
+    }
+    __syncthreads();
+    unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes();
+    unsigned* runs = (unsigned*)wb;
+    unsigned char* rbuf = wb + kStreamRunsCap * 4;
+
+    const long long klo = 2 * a.band_pair_lo;
+    const long long khi = 2 * a.band_pair_hi < a.n ? 2 * a.band_pair_hi : a.n;
+    for (long long k = klo + (long long)blockIdx.x * wpb + wave; k < khi; k += (long long)gridDim.x * wpb) {
+        const long long rd = a.band_order[k];
+        const long long g = k >> 1;
+        const int h = (int)(k & 1);
+        const long long rp = (k ^ 1) < a.n ? a.band_order[k ^ 1] : rd;
+        const long long off = a.offsets[rd];
+        const int Lb = (int)(a.offsets[rd + 1] - off);
+        if (Lb <= 0) {
+            if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; a.stats[rd] = z; }
+            continue;
+        }
+        const int Lp = (int)(a.offsets[rp + 1] - a.offsets[rp]);
+        int dlo;
+        if (Lp != Lb || Lb > a.band_lb_cap || !band_geometry(La, Lb, &dlo)) {
+            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+            continue;
+        }
+        const unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
+        const unsigned char* raw = a.reads + off;
+        // the read's bytes -> LDS (DMA, one dword per lane) for the emit
+        const bool cached = Lb <= kBandReadCap;
+        const int mis = (int)((uintptr_t)raw & 3);
+        if (cached) {
+            const unsigned char* src = raw - mis;
+            for (int m = 0; m < Lb + mis; m += 256)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + m + 4 * lane),
+                                                 (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
+        }
+        const int4 hdr = *(const int4*)region;
+        const int tau0 = hdr.x;
+        // start cell: the last cell of each band diagonal is on the last row or column
+        unsigned k32 = 0u;
+        if (lane < kBandDiags) {
+            const int d = dlo + lane;
+            const int iend = La < Lb - d ? La : Lb - d;
+            const int ilo = 1 - d > 1 ? 1 - d : 1;
+            if (iend >= ilo) {
+                const unsigned cw = ((const unsigned*)(region + kHdrBytes))[lane];
+                const int v = half(cw, h) - E * (2 * iend + d);
+                const int jend = iend + d;
+                k32 = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
+                      : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
+            }
+        }
+        int score, ei, ej;
+        decode_end(end_key_widen(wave_max_u32(k32)), La, Lb, &score, &ei, &ej);
+        // certificate: every alignment leaving the band scores <= UB < score
+        const int dhi = dlo + kBandDiags - 1;
+        int pmax = -1;
+        if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
+        if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
+        const bool certified = pmax < 0 || score > a.band_maxsub * pmax;
+        if ((hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) || !certified) {
+            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            continue;
+        }
+        const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
+        const int tb0 = kBK - dlo + 2 - tau0;
+        auto nib = [&](int ai, int bjj, bool* oob) -> unsigned {
+            const int kd = bjj - ai - dlo;
+            if ((unsigned)kd >= (unsigned)kBandDiags) { *oob = true; return 0u; }
+            *oob = false;
+            const int tau = ai + bjj + tb0;
+            const unsigned w = bits[(tau >> 2) * kBL + (kd >> 1)];
+            const int s = tau & 3;
+            const int hb = 8 * h + s, lb = 8 * h + 4 + s;
+            const unsigned yop = (w >> hb) & 1u, xgy = (w >> lb) & 1u;
+            const unsigned xop = (w >> (16 + hb)) & 1u, notm = (w >> (16 + lb)) & 1u;
+            return notm | (xgy << 1) | (xop << 2) | (yop << 3);
+        };
+        const int nruns = walk_runs_wide<NW_BAND_WALK_CPL>(nib, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
+        if (nruns < 0) {
+            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+            continue;
+        }
+        lds_fence();
+        auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
+        emit_alignment(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, a.out + rd * 3 * a.stride,
+                       a.stride, score, ei, ej, a.stats + rd, lane);
+        lds_fence();
+    }
+}
+
+// ---- host-side helpers -------------------------------------------------------
+int band_fill_lds_bytes(int La, int wpb) {
+    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * band_pcs(La);
+}
+int band_walk_lds_bytes(int La, int wpb) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(); }
+int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }
+int64_t band_region_bytes(int La, int Lb_max) { return band_region_stride(La, Lb_max); }
+bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb, dlo); }
+
+hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(fill_blocks, nw_band_fill, 64 * fill_wpb, fill_lds);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_band_walk, 64 * walk_wpb, walk_lds);
+}
+
+hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(nw_band_hist, dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nw_band_scan, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(nw_band_scatter, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_band(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+                       hipEvent_t after_fill) {
+    hipLaunchKernelGGL(nw_band_fill, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(nw_band_walk, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace nw

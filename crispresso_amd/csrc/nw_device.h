@@ -52,10 +52,21 @@ struct KernelArgs {
     // stream fill, per-read profile path: prof (int16) + 2 * gap_extend, the
     // diagonal step of the (r + c) * extend biased recurrence (nw_stream.hip)
     const int16_t* prof_fill;
+    // certified diagonal-band kernels (nw_band.hip)
+    const int32_t* band_order;     // read indices sorted by length; sorted positions 2g, 2g+1 = pair g
+    int64_t band_pair_lo, band_pair_hi;   // pairs of this pass
+    uint8_t* band_region;          // per-pair regions of the pass (band_stride bytes each)
+    int64_t band_stride;
+    int32_t band_words;            // traceback words per lane and pair
+    int32_t band_lb_cap;           // longest read the band kernels take; longer ones sort last
+    int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
+    const uint32_t* band_tab;      // [6 amplicon codes][6][6 read codes] packed int16x2 score + 2 E
+    const uint32_t* rowpos;        // [La] codes each amplicon row scores > 0 against (markup ':')
+    int32_t* sort_hist;            // [band_lb_cap + 2] length buckets of the counting sort
 };
 
 // Traceback storage of a kernel instantiation.
-enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3, TB_STREAM = 4 };
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3, TB_STREAM = 4, TB_DIAG = 5 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
@@ -97,5 +108,18 @@ hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const Launc
                          hipEvent_t after_fill);
 hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds,
                             int* fill_blocks, int* walk_blocks);
+
+// certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
+// two equal-length reads per 16-lane row, reads sorted by length on the device.
+constexpr int kBandDiags = 32;
+int band_fill_lds_bytes(int La, int wpb);
+int band_walk_lds_bytes(int La, int wpb);
+int band_region_words(int La, int Lb_max);
+int64_t band_region_bytes(int La, int Lb_max);
+bool band_pair_geometry(int La, int Lb, int* dlo);
+hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks);
+hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
+hipError_t launch_band(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+                       hipEvent_t after_fill);
 
 }  // namespace nw

@@ -119,6 +119,15 @@ struct nw_ctx {
     nw::LaunchCfg pair_cfg{};         // packed int16 two-reads-per-wave kernel
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
+    // certified diagonal-band kernels (nw_band.hip): the default path
+    bool amp_in_table = false;         // amplicon within A C G T N / unknown (the band score table)
+    bool use_diag = false;
+    nw::LaunchCfg diag_fill{}, diag_walk{};
+    DevBuf<uint32_t> d_btab, d_rowpos;
+    DevBuf<int32_t> d_order, d_sort_hist;
+    DevBuf<uint8_t> d_bregion;
+    int64_t diag_pass_pairs = 0, diag_stride = 0;
+    int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
     bool ran = false;
 };
 
@@ -174,6 +183,21 @@ int build_profile(nw_ctx* c) {
     const int bias2 = 2 * c->gap_extend;
     std::vector<int16_t> prof16f(prof16.size());
     for (size_t q = 0; q < prof16.size(); ++q) prof16f[q] = (int16_t)(prof16[q] + bias2);
+    // ascii -> A T G C N pad/unknown (0..5), 6 = other IUPAC codes: the alphabet of
+    // the stream kernel's pair table and of the certified-band score table
+    {
+        const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+        uint8_t lut6[256];
+        for (int q = 0; q < 256; ++q) {
+            const int code = code_of((unsigned char)q);
+            int r = nw::kPairCodes;   // not in the table
+            for (int i = 0; i < nw::kPairCodes; ++i)
+                if (codes[i] == code) r = i;
+            lut6[q] = (uint8_t)r;
+        }
+        HIP_OR_FAIL(c, c->d_lut6.reserve(256));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut6.p, lut6, 256, hipMemcpyHostToDevice, c->stream));
+    }
     // pair-code table of the stream kernel: for every (code of read A, code of
     // read B) over A T G C N pad, each lane's 4 rows as packed int16x2 (biased)
     c->have_ptab = false;
@@ -189,20 +213,44 @@ int build_profile(nw_ctx* c) {
                         const uint16_t sb = (uint16_t)prof16f[(size_t)codes[ib] * 64 * R4 + src];
                         ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
                     }
-        uint8_t lut6[256];
-        for (int q = 0; q < 256; ++q) {
-            const int code = code_of((unsigned char)q);
-            int r = nw::kPairCodes;   // not in the table
-            for (int i = 0; i < nw::kPairCodes; ++i)
-                if (codes[i] == code) r = i;
-            lut6[q] = (uint8_t)r;
-        }
         HIP_OR_FAIL(c, c->d_ptab.reserve(ptab.size()));
-        HIP_OR_FAIL(c, c->d_lut6.reserve(256));
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_ptab.p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut6.p, lut6, 256, hipMemcpyHostToDevice, c->stream));
         const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
         c->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
+    }
+    // certified-band score table: [amplicon code][read A code][read B code] over
+    // A T G C N pad/unknown, packed int16x2 + 2 * extend (biased recurrence), and
+    // per amplicon row the codes it scores > 0 against (markup ':')
+    {
+        const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+        auto sub6 = [&](int x, int y) {
+            const int cx = codes6[x], cy = codes6[y];
+            return (cx < 16 && cy < 16) ? kEdna[cx][cy] * c->scale : 0;
+        };
+        std::vector<uint32_t> btab(216);
+        for (int x = 0; x < 6; ++x)
+            for (int ya = 0; ya < 6; ++ya)
+                for (int yb = 0; yb < 6; ++yb) {
+                    const uint16_t sa = (uint16_t)(int16_t)(sub6(x, ya) + 2 * c->gap_extend);
+                    const uint16_t sb = (uint16_t)(int16_t)(sub6(x, yb) + 2 * c->gap_extend);
+                    btab[(size_t)x * 36 + ya * 6 + yb] = sa | ((uint32_t)sb << 16);
+                }
+        std::vector<uint32_t> rowpos((size_t)La);
+        c->amp_in_table = true;
+        for (int ai = 0; ai < La; ++ai) {
+            const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+            uint32_t m = 0;
+            for (int code = 0; code < nw::NCODE; ++code)
+                if (ca < 16 && code < 16 && kEdna[ca][code] > 0) m |= 1u << code;
+            rowpos[(size_t)ai] = m;
+            bool in6 = false;
+            for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
+            c->amp_in_table = c->amp_in_table && in6;
+        }
+        HIP_OR_FAIL(c, c->d_btab.reserve(btab.size()));
+        HIP_OR_FAIL(c, c->d_rowpos.reserve(rowpos.size()));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_btab.p, btab.data(), btab.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_rowpos.p, rowpos.data(), rowpos.size() * 4, hipMemcpyHostToDevice, c->stream));
     }
     HIP_OR_FAIL(c, c->d_prof16.reserve(prof16.size()));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16.p, prof16.data(), prof16.size() * 2, hipMemcpyHostToDevice, c->stream));
@@ -293,14 +341,54 @@ int configure(nw_ctx* c) {
             c->use_pair = true;
         }
     }
-    // streaming fill + walk kernels (default when the scores fit int16)
+    // certified diagonal band (default): scores and biases within int16, amplicon
+    // within the band table's alphabet, non-negative gap costs (the certificate)
+    c->use_diag = false;
+    const bool want_diag = !kern || std::strcmp(kern, "diag") == 0;
+    const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
+    if (want_diag && c->amp_in_table && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
+        c->gap_open >= c->gap_extend) {
+        nw::LaunchCfg f{}, w{};
+        f.R = w.R = R;
+        f.tb_mode = w.tb_mode = nw::TB_DIAG;
+        f.wpb = 8;
+        w.wpb = 8;
+        f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb);
+        w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb);
+        int fb = 0, wb = 0;
+        if (f.lds_bytes <= kMaxLds && w.lds_bytes <= kMaxLds)
+            HIP_OR_FAIL(c, nw::band_occupancy(f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb));
+        if (fb > 0 && wb > 0) {
+            const int64_t pairs = (c->n + 1) / 2;
+            c->diag_lb_cap = La + nw::kBandDiags - 1;
+            c->diag_words = nw::band_region_words(La, c->lb_max);
+            c->diag_stride = nw::band_region_bytes(La, c->lb_max);
+            int64_t cap_bytes = 16ll << 30;
+            if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
+            c->diag_pass_pairs = std::max<int64_t>(4, std::min<int64_t>(pairs, cap_bytes / c->diag_stride));
+            c->diag_pass_pairs = (c->diag_pass_pairs + 3) & ~(int64_t)3;
+            const int64_t pass_pairs = std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs);
+            f.grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pass_pairs + 3) / 4 + f.wpb - 1) / f.wpb,
+                                                                 (int64_t)c->num_cus * fb));
+            w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((2 * pass_pairs + w.wpb - 1) / w.wpb,
+                                                                 (int64_t)c->num_cus * wb));
+            c->diag_sort_grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 255) / 256, 4ll * c->num_cus));
+            HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)(pass_pairs * c->diag_stride)));
+            HIP_OR_FAIL(c, c->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->d_sort_hist.reserve((size_t)c->diag_lb_cap + 2));
+            c->diag_fill = f;
+            c->diag_walk = w;
+            c->use_diag = true;
+        }
+    }
+    // streaming fill + walk kernels (when the certified band does not apply)
     c->use_stream = false;
     const bool want_stream = !kern || std::strcmp(kern, "stream") == 0;
     // the stream fill's values carry a bias of up to (rows + span) * extend
     const int64_t nl_rows = (int64_t)((La + R - 1) / R) * R;
     const int64_t bias_max = (nl_rows + std::max<int64_t>(c->lb_max, 64) + 8) * c->gap_extend;
     const bool fits16s = fits16 && hi + bias_max + c->gap_open < 16000;
-    if (want_stream && fits16s && c->stream_slots > 0) {
+    if (want_stream && fits16s && c->stream_slots > 0 && !c->use_diag) {
         nw::LaunchCfg f{}, w{};
         f.R = w.R = R;
         f.tb_mode = w.tb_mode = nw::TB_STREAM;
@@ -374,6 +462,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
     c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
+    c->d_btab.release(); c->d_rowpos.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_bregion.release();
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -500,6 +589,35 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.fallback_list = c->d_fallback.p + base;
     a.fallback_count = c->d_fallback_count.p;
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
+    if (c->use_diag) {
+        // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
+        if (c->n <= 0) return NW_OK;
+        a.lut6 = c->d_lut6.p;
+        a.band_order = c->d_order.p;
+        a.band_region = c->d_bregion.p;
+        a.band_stride = c->diag_stride;
+        a.band_words = c->diag_words;
+        a.band_lb_cap = c->diag_lb_cap;
+        a.band_maxsub = 5 * c->scale;
+        a.band_tab = c->d_btab.p;
+        a.rowpos = c->d_rowpos.p;
+        a.sort_hist = c->d_sort_hist.p;
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_sort_hist.p, 0, sizeof(int32_t) * ((size_t)c->diag_lb_cap + 2), c->stream));
+        HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->stream));
+        const int64_t pairs = (c->n + 1) / 2;
+        for (int64_t lo = 0; lo < pairs; lo += c->diag_pass_pairs) {
+            nw::KernelArgs ap = a;
+            ap.band_pair_lo = lo;
+            ap.band_pair_hi = std::min(pairs, lo + c->diag_pass_pairs);
+            HIP_OR_FAIL(c, nw::launch_band(ap, c->diag_fill, c->diag_walk, c->stream, lo == 0 ? c->ev_fill : nullptr));
+            if (lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+        }
+        a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
+        a.work_count = c->d_fallback_count.p;
+        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+        return NW_OK;
+    }
     if (c->use_stream) {
         // passes of at most pass_reads reads (the per-pair regions of one pass stay resident)
         const int64_t passes = std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads);
@@ -619,7 +737,7 @@ int nw_batch_kernel_times(nw_ctx* c, float* fill_ms, float* walk_ms, float* rest
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     float total = 0.0f, f = 0.0f, w = 0.0f;
     HIP_OR_FAIL(c, hipEventElapsedTime(&total, c->ev0, c->ev1));
-    if (c->use_stream && c->n > 0) {
+    if ((c->use_stream || c->use_diag) && c->n > 0) {
         HIP_OR_FAIL(c, hipEventElapsedTime(&f, c->ev0, c->ev_fill));
         HIP_OR_FAIL(c, hipEventElapsedTime(&w, c->ev_fill, c->ev_walk));
     } else {
@@ -645,7 +763,7 @@ int nw_batch_device_output(nw_ctx* c, void** d_aln, int64_t* stride, void** d_st
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
-    const nw::LaunchCfg& k = c->use_stream ? c->stream_fill
+    const nw::LaunchCfg& k = c->use_diag ? c->diag_fill : c->use_stream ? c->stream_fill
                              : (c->use_pair ? c->pair_cfg : (c->use_band ? c->band_cfg : c->cfg));
     if (rows_per_lane) *rows_per_lane = k.R;
     if (waves_per_block) *waves_per_block = k.wpb;
@@ -659,8 +777,8 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
     if (!c || !c->ran) return -1;
     (void)hipSetDevice(c->device);
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
-    if (!(c->use_band || c->use_pair || c->use_stream)) return 0;
-    const int64_t passes = c->use_stream ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
+    if (!(c->use_band || c->use_pair || c->use_stream || c->use_diag)) return 0;
+    const int64_t passes = (c->use_stream && !c->use_diag) ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     std::vector<int32_t> v((size_t)(4 * passes));
     if (hipMemcpy(v.data(), c->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;

@@ -12,8 +12,8 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["stream", "stream-profile", "pair", "band", "full"]
-BANDED = {"stream": "stream-int16", "pair": "pair-band-int16"}
+KERNELS = ["diag", "stream", "stream-profile", "pair", "band", "full"]
+BANDED = {"diag": "diag-int16", "stream": "stream-int16", "pair": "pair-band-int16"}
 
 
 @pytest.fixture(params=KERNELS)
@@ -153,6 +153,7 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
 @pytest.mark.parametrize("slots", ["0", "8", "24"])
 def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
     """Same answers with the band off (full storage only) or very narrow (mostly fallbacks)."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
     monkeypatch.setenv("CRISPR_NW_BAND_SLOTS", slots)
     amp = synth.random_amplicon(250, 1)
     buf, off = synth.reads_from(amp, 600, 12, synth.PARITY_MIX)
@@ -323,3 +324,105 @@ def test_pooled_multi_amplicon(gpu_aligner_factory, oracle):
     buf, off = synth.reads_from(amp, 500, 999, synth.PARITY_MIX)
     al.set_reference(amp)
     assert_same(oracle, amp, buf, off, al.align_packed(buf, off), "after-multi")
+
+
+# ---------------------------------------------------------------- certified band (nw_band.hip)
+
+def test_diag_is_default_and_certifies_c2(gpu_aligner_factory, oracle):
+    """The default path is the certified diagonal band; on the C2 mix almost every
+    read is certified (no fallback) and all are bit-identical to the oracle."""
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 4001, 2)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "diag-int16"
+    # sorted by length, only a pair straddling two lengths (at most one per length) and
+    # the rare uncertified read go to the exact kernel
+    assert a.fallbacks() <= 2 * len(np.unique(np.diff(off))) + 4
+    assert_same(oracle, amp, buf, off, batch, "diag-c2")
+
+
+def test_diag_certificate_failures_fall_back(gpu_aligner_factory, oracle):
+    """Reads the band cannot certify -- chimeras, shifted or unrelated reads, length
+    differences beyond the band, IUPAC codes -- go to the exact kernel."""
+    amp = synth.random_amplicon(250, 3)
+    rng = np.random.Generator(np.random.PCG64(5))
+    reads = [amp[:60] + synth.random_amplicon(70, 6) + amp[130:],          # junk block, same length
+             amp[:100] + amp[140:], amp[:125] + synth.random_amplicon(35, 7) + amp[125:],  # |Lb - La| > 31
+             amp[40:] + amp[:40], synth.random_amplicon(250, 8), amp[::-1],
+             amp[:80] + "R" + amp[81:], amp[:20] + "-" + amp[21:]]
+    reads += [amp] * 7 + [amp[:100] + amp[101:]] * 5
+    buf0, off0 = synth.reads_from(amp, 300, 9, synth.PARITY_MIX)
+    reads += synth.unpack(buf0, off0)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.fallbacks() >= 6
+    assert_same(oracle, amp, buf, off, batch, "diag-fallback")
+
+
+def test_diag_multiple_passes_and_odd_counts(gpu_aligner_factory, oracle, monkeypatch):
+    """Region budget below the batch: several fill + walk passes over the sorted
+    pairs; an odd read count leaves the last sorted read without a partner."""
+    monkeypatch.setenv("CRISPR_NW_REGION_MB", "1")
+    amp = synth.random_amplicon(250, 8)
+    buf, off = synth.reads_from(amp, 1003, 9, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "diag-int16"
+    assert_same(oracle, amp, buf, off, batch, "diag-passes")
+    t = a.kernel_times()
+    assert t["fill_ms"] > 0 and t["walk_ms"] > 0
+
+
+@pytest.mark.parametrize("La", [40, 150, 333, 700, 1024])
+def test_diag_lengths_around_the_band(gpu_aligner_factory, oracle, La):
+    """Read lengths from La - 40 to La + 40 (inside and outside the band's reach),
+    empty reads, and single reads of a length."""
+    amp = synth.random_amplicon(La, 500 + La)
+    rng = np.random.Generator(np.random.PCG64(La))
+    reads = []
+    for k in range(240):
+        D = int(rng.integers(-40, 41))
+        L = max(0, La + D)
+        if k % 17 == 0:
+            L = 0
+        base = amp if D <= 0 else amp + synth.random_amplicon(D, k)
+        s = int(rng.integers(0, len(base) - L + 1)) if L < len(base) else 0
+        r = list(base[s:s + L])
+        for _ in range(int(rng.integers(0, 4))):
+            if r:
+                r[int(rng.integers(0, len(r)))] = "ACGT"[int(rng.integers(0, 4))]
+        reads.append("".join(r))
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"diag La={La}")
+
+
+def test_diag_homopolymer_ties(gpu_aligner_factory, oracle):
+    """Indels inside homopolymer runs and tandem repeats: co-optimal placements,
+    decided by the tie rules -- the band must reproduce them."""
+    unit = "ACGTTTTTGCAAAAACGCGCGTCA"
+    amp = (unit * 11)[:250]
+    rng = np.random.Generator(np.random.PCG64(13))
+    reads = []
+    for k in range(400):
+        r = list(amp)
+        for _ in range(int(rng.integers(1, 4))):
+            p = int(rng.integers(1, len(r) - 1))
+            op = rng.integers(0, 3)
+            if op == 0:
+                del r[p]
+            elif op == 1:
+                r.insert(p, r[p])
+            else:
+                r[p] = "ACGT"[int(rng.integers(0, 4))]
+        reads.append("".join(r))
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "diag-homopolymer")
