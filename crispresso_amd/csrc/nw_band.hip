@@ -49,6 +49,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "nw_common.h"
@@ -67,17 +68,23 @@ __device__ __forceinline__ s16x2 as_v(unsigned u) { return __builtin_bit_cast(s1
 __device__ __forceinline__ unsigned as_u(s16x2 v) { return __builtin_bit_cast(unsigned, v); }
 __device__ __forceinline__ unsigned pk(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
 __device__ __forceinline__ int half(unsigned w, int h) { return (int)(short)(w >> (16 * h)); }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// The fill keeps every value + kBias16 (unsigned, -inf = 0): max is v_pk_max_u16 and
+// a DPP lane without a source reads 0 (bound_ctrl) -- no "old" operand to set up.
+// Sums and differences are the same bits as in the signed domain.
+constexpr int kBias16 = 16384;
 __device__ __forceinline__ unsigned max2(unsigned a, unsigned b) {
-    return as_u(__builtin_elementwise_max(as_v(a), as_v(b)));
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
 }
 __device__ __forceinline__ unsigned add2(unsigned a, unsigned b) { return as_u(as_v(a) + as_v(b)); }
 __device__ __forceinline__ unsigned sub2(unsigned a, unsigned b) { return as_u(as_v(a) - as_v(b)); }
-// DPP within 16-lane rows; lanes without a source keep `old` (-inf: outside the band)
-__device__ __forceinline__ unsigned row_shr1(unsigned old, unsigned v) {
-    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x111, 0xf, 0xf, false);
+// DPP within 16-lane rows; a lane without a source reads 0 (= -inf: outside the band)
+__device__ __forceinline__ unsigned row_shr1(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, true);
 }
-__device__ __forceinline__ unsigned row_shl1(unsigned old, unsigned v) {
-    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x101, 0xf, 0xf, false);
+__device__ __forceinline__ unsigned row_shl1(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, true);
 }
 __device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
     unsigned d;
@@ -108,7 +115,8 @@ constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [
 constexpr int kJPad = 96;             // pair codes: index j + kJPad, j in [-79, La + 79]
 constexpr int kPadCode = 5;           // lut6: A T G C N pad
 constexpr int kTabBytes = 896;        // [6][36] packed scores (864 B)
-constexpr int kHdrBytes = 16;         // tau_base, dlo, flags, -
+constexpr int kHdrBytes = 48;         // {tau0, dlo, flags, -}, {ra, rb, LbA, LbB}, {offA, offB}
+constexpr int kPairInactive = 4;      // header flag: the pair was not filled (walk: empty / fallback)
 constexpr int kCapBytes = kBandDiags * 4;
 
 __host__ __device__ inline int band_acd_elems(int La) { return La + kAPad + 64; }
@@ -126,40 +134,158 @@ __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max) {
 
 // ============================================================================
 // Counting sort of the reads by length (bucket cap + 1 holds longer reads).
-// Wave-aggregated atomics: one atomic per distinct length per wavefront.
+// Block b owns the reads [b * chunk, (b + 1) * chunk): LDS histogram, a
+// bucket-major table of per-block counts, one exclusive scan over it, then each
+// block scatters through its own LDS cursors -- no global atomics.
 // ============================================================================
 __device__ __forceinline__ int len_bucket(const int64_t* offsets, long long r, int cap) {
     const long long L = offsets[r + 1] - offsets[r];
     return L <= cap ? (int)L : cap + 1;
 }
 
-__global__ __launch_bounds__(256) void nw_band_hist(const KernelArgs a) {
-    const int lane = threadIdx.x & 63;
-    for (long long base = (long long)blockIdx.x * blockDim.x; base < a.n; base += (long long)gridDim.x * blockDim.x) {
-        const long long r = base + threadIdx.x;
-        bool pending = r < a.n;
-        const int b = pending ? len_bucket(a.offsets, r, a.band_lb_cap) : 0;
-        for (;;) {
-            const unsigned long long act = __ballot(pending);
-            if (!act) break;
-            const int leader = (int)__builtin_ctzll(act);
-            const int key = __builtin_amdgcn_readlane(b, leader);
-            const bool mine = pending && b == key;
-            const unsigned long long m = __ballot(mine);
-            if (lane == leader) atomicAdd(&a.sort_hist[key], (int)__popcll(m));
-            if (mine) pending = false;
+// Sort key of every read: its length bucket, or cap + 2 for a read identical to the
+// amplicon (case-insensitive, A C G T only).  Such a read needs no DP: its full
+// diagonal scores S = maxsub * La, every other alignment pairs at most La - 1
+// residues (S > UB of the one-diagonal band, the certificate above), so the
+// alignment is the diagonal and the start cell the corner: this kernel writes its
+// strings and record right away, and the sort keeps it out of the band passes.
+// One wavefront per read, 16 reads in flight; 4 bytes per lane and compare:
+// (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
+__device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
+
+constexpr int kClassifyReads = 16;
+
+__global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
+    extern __shared__ unsigned amp_lo[];   // folded amplicon dwords, zero-padded
+    const int La = a.La, nd = (La + 3) / 4;
+    for (int k = threadIdx.x; k < nd; k += blockDim.x) {
+        unsigned w = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int q = 4 * k + b;
+            const unsigned char c = q < La ? upcase(a.amp[q]) : 0;
+            w |= (unsigned)((c == 'A' || c == 'C' || c == 'G' || c == 'T') ? (c | 0x20) : 0) << (8 * b);
+        }
+        amp_lo[k] = w;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
+    const int sd = (int)(a.stride / 4);
+    const long long step = (long long)gridDim.x * wpb * kClassifyReads;
+    for (long long r0 = ((long long)blockIdx.x * wpb + (threadIdx.x >> 6)) * kClassifyReads; r0 < a.n; r0 += step) {
+        // lanes 0..kClassifyReads-1 load the batch's offsets in one coalesced round trip
+        long long my_off = 0;
+        int my_len = -1;
+        if (lane < kClassifyReads && r0 + lane < a.n) {
+            my_off = a.offsets[r0 + lane];
+            my_len = (int)(a.offsets[r0 + lane + 1] - my_off);
+        }
+        long long off[kClassifyReads];
+        bool same[kClassifyReads];
+        int Lb[kClassifyReads];
+#pragma unroll
+        for (int u = 0; u < kClassifyReads; ++u) {
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
+            off[u] = (long long)(((unsigned long long)hi << 32) | lo);
+            Lb[u] = __builtin_amdgcn_readlane(my_len, u);
+            same[u] = Lb[u] == La;
+        }
+        for (int c0 = 0; c0 < nd; c0 += 64) {
+            const int k4 = c0 + lane;
+            unsigned diff[kClassifyReads];
+#pragma unroll
+            for (int u = 0; u < kClassifyReads; ++u) {
+                diff[u] = 0u;
+                if (same[u] && k4 < nd) {
+                    const uint8_t* base = a.reads + (off[u] & ~3ll) + 4 * k4;
+                    const unsigned w = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off[u] & 3)) | 0x20202020u;
+                    diff[u] = (w ^ amp_lo[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kClassifyReads; ++u) same[u] = same[u] && __ballot(diff[u] != 0u) == 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kClassifyReads; ++u) {
+            const long long r = r0 + u;
+            if (r >= a.n) break;
+            if (lane == 0) a.sort_key[r] = same[u] ? a.band_lb_cap + 2 : (Lb[u] <= a.band_lb_cap ? Lb[u] : a.band_lb_cap + 1);
+            if (!same[u]) continue;
+            // the diagonal: amplicon, '|' markup, read; rows as dwords up to round4(La) (within the stride)
+            unsigned* o = (unsigned*)(a.out + r * 3 * a.stride);
+            const uint8_t* base = a.reads + (off[u] & ~3ll);
+            for (int k4 = lane; k4 < nd; k4 += 64) {
+                o[k4] = ld_dw(a.amp + 4 * k4);
+                o[sd + k4] = 0x7c7c7c7cu;   // '|'
+                o[2 * sd + k4] = __builtin_amdgcn_alignbyte(ld_dw(base + 4 * k4 + 4), ld_dw(base + 4 * k4), (int)(off[u] & 3));
+            }
+            if (lane == 0) {
+                Stat st;
+                st.aln_len = La;
+                st.n_ident = La;
+                st.n_sim = La;
+                st.n_gaps = 0;
+                st.score = a.band_maxsub * La;
+                st.end_i = La;
+                st.end_j = La;
+                st.flags = 0;
+                a.stats[r] = st;
+            }
         }
     }
 }
 
-// exclusive scan of sort_hist[0 .. cap + 1] in place (one block of 1024 threads)
-__global__ __launch_bounds__(1024) void nw_band_scan(const KernelArgs a) {
+__device__ __forceinline__ void sort_chunk(const KernelArgs& a, long long* lo, long long* hi) {
+    const long long chunk = (a.n + gridDim.x - 1) / gridDim.x;
+    *lo = (long long)blockIdx.x * chunk;
+    *hi = *lo + chunk < a.n ? *lo + chunk : a.n;
+}
+
+__global__ __launch_bounds__(256) void nw_band_hist(const KernelArgs a) {
+    extern __shared__ int hist[];
+    const int nb = a.band_lb_cap + 3;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    long long lo, hi;
+    sort_chunk(a, &lo, &hi);
+    for (long long r = lo + threadIdx.x; r < hi; r += blockDim.x) atomicAdd(&hist[a.sort_key[r]], 1);
+    __syncthreads();
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) a.sort_hist[(long long)k * gridDim.x + blockIdx.x] = hist[k];
+}
+
+// exclusive scan of each bucket's row of per-block counts (one wavefront per
+// bucket); the row total goes to the base array after the table
+__global__ __launch_bounds__(64) void nw_band_rowscan(const KernelArgs a, int grid) {
+    const int lane = threadIdx.x;
+    int* row = a.sort_hist + (long long)blockIdx.x * grid;
+    const int per = (grid + 63) / 64;
+    const int lo = lane * per, hi = lo + per < grid ? lo + per : grid;
+    int s = 0;
+    for (int k = lo; k < hi; ++k) s += row[k];
+    int incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    int run = incl - s;
+    for (int k = lo; k < hi; ++k) {
+        const int c = row[k];
+        row[k] = run;
+        run += c;
+    }
+    if (lane == 63) a.sort_hist[(long long)(a.band_lb_cap + 3) * grid + blockIdx.x] = incl;
+}
+
+// exclusive scan of the bucket totals (one block)
+__global__ __launch_bounds__(1024) void nw_band_scan(const KernelArgs a, int grid) {
     __shared__ int part[1024];
-    const int nb = a.band_lb_cap + 2;
+    int* base = a.sort_hist + (long long)(a.band_lb_cap + 3) * grid;
+    const int nb = a.band_lb_cap + 3;
     const int per = (nb + 1023) / 1024;
     const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
     int s = 0;
-    for (int k = lo; k < hi; ++k) s += a.sort_hist[k];
+    for (int k = lo; k < hi; ++k) s += base[k];
     part[threadIdx.x] = s;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -170,35 +296,23 @@ __global__ __launch_bounds__(1024) void nw_band_scan(const KernelArgs a) {
     }
     int run = part[threadIdx.x] - s;
     for (int k = lo; k < hi; ++k) {
-        const int c = a.sort_hist[k];
-        a.sort_hist[k] = run;
+        const int c = base[k];
+        base[k] = run;
         run += c;
     }
 }
 
 __global__ __launch_bounds__(256) void nw_band_scatter(const KernelArgs a) {
-    const int lane = threadIdx.x & 63;
+    extern __shared__ int cur[];
+    const int nb = a.band_lb_cap + 3;
+    const int* base = a.sort_hist + (long long)nb * gridDim.x;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) cur[k] = base[k] + a.sort_hist[(long long)k * gridDim.x + blockIdx.x];
+    __syncthreads();
     int32_t* order = const_cast<int32_t*>(a.band_order);
-    for (long long base = (long long)blockIdx.x * blockDim.x; base < a.n; base += (long long)gridDim.x * blockDim.x) {
-        const long long r = base + threadIdx.x;
-        bool pending = r < a.n;
-        const int b = pending ? len_bucket(a.offsets, r, a.band_lb_cap) : 0;
-        for (;;) {
-            const unsigned long long act = __ballot(pending);
-            if (!act) break;
-            const int leader = (int)__builtin_ctzll(act);
-            const int key = __builtin_amdgcn_readlane(b, leader);
-            const bool mine = pending && b == key;
-            const unsigned long long m = __ballot(mine);
-            int pos = 0;
-            if (lane == leader) pos = atomicAdd(&a.sort_hist[key], (int)__popcll(m));
-            pos = __builtin_amdgcn_readlane(pos, leader);
-            if (mine) {
-                order[pos + (int)__popcll(m & ((1ull << lane) - 1ull))] = (int32_t)r;
-                pending = false;
-            }
-        }
-    }
+    long long lo, hi;
+    sort_chunk(a, &lo, &hi);
+    for (long long r = lo + threadIdx.x; r < hi; r += blockDim.x)
+        order[atomicAdd(&cur[a.sort_key[r]], 1)] = (int32_t)r;
 }
 
 // ============================================================================
@@ -210,7 +324,7 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
     const int O = a.gap_open, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
     const int q = lane & (kBL - 1), grp = lane / kBL;
-    const unsigned NEG2 = pk(-16384, -16384);
+    const unsigned NEG2 = 0u;                    // -inf in the kBias16 domain
     const unsigned OE2 = pk(O - E, O - E);
 
     uint32_t* tab = (uint32_t*)smem;
@@ -236,21 +350,25 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    const long long npairs = a.band_pair_hi - a.band_pair_lo;
-    const long long nwork = (npairs + kBPW - 1) / kBPW;
+    // sorted positions [0, count) hold the reads that need the DP (the rest are exact copies)
+    const long long count = *a.band_count;
+    const long long pair_hi = min(a.band_pair_hi, (count + 1) / 2);
+    const long long npairs = pair_hi - a.band_pair_lo;
+    const long long nwork = npairs > 0 ? (npairs + kBPW - 1) / kBPW : 0;
     const int NW = a.band_words;
     for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nwork; wv += (long long)gridDim.x * wpb) {
         const long long g = a.band_pair_lo + wv * kBPW + grp;
         int Lb = La, dlo = 0;
         bool act = false;
-        long long offA = 0, offB = 0;
-        if (g < a.band_pair_hi) {
-            const long long ra = a.band_order[2 * g];
-            const long long rb = (2 * g + 1 < a.n) ? a.band_order[2 * g + 1] : ra;
+        long long offA = 0, offB = 0, ra = 0, rb = 0;
+        int LbA = 0, LbB = 0;
+        if (g < pair_hi) {
+            ra = a.band_order[2 * g];
+            rb = (2 * g + 1 < count) ? a.band_order[2 * g + 1] : ra;
             offA = a.offsets[ra];
             offB = a.offsets[rb];
-            const int LbA = (int)(a.offsets[ra + 1] - offA);
-            const int LbB = (int)(a.offsets[rb + 1] - offB);
+            LbA = (int)(a.offsets[ra + 1] - offA);
+            LbB = (int)(a.offsets[rb + 1] - offB);
             act = LbA == LbB && LbA <= a.band_lb_cap && band_geometry(La, LbA, &dlo);
             if (act) Lb = LbA;
         }
@@ -281,8 +399,16 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         const unsigned tpro = act ? (unsigned)(kBK - dlo) + dmax + 1 : 0u;
         const int tau0 = (int)(wave_min_u32(tlo) & ~3u);
         const int tau_end = (int)wave_max_u32(thi);
-        const int tau_pro = (int)((wave_max_u32(tpro) + 3) & ~3u);
+        const int tau_pro = (int)wave_max_u32(tpro);
         lds_fence();
+        unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
+        if (q == 0 && g < pair_hi) {
+            // everything the walk needs to find the pair's reads: one 48-byte load
+            int4* hp = (int4*)region;
+            hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive), 0);
+            hp[1] = make_int4((int)ra, (int)rb, LbA, LbB);
+            hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
+        }
         if (tau_end == 0) continue;   // no active group in this wavefront
 
         const int d0 = dlo + 2 * q;
@@ -293,15 +419,17 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             const int d = d0 + p;
             const int ad = d < 0 ? -d : d;
             tb[p] = kBK - dlo + ad;
-            bval[p] = pk(E * ad, E * ad);
+            bval[p] = pk(E * ad + kBias16, E * ad + kBias16);
             const int iend = La < Lb - d ? La : Lb - d;
             const int ilo = 1 - d > 1 ? 1 - d : 1;
-            te[p] = iend >= ilo ? kBK - dlo + 2 * iend + d : -1;
+            te[p] = (act && iend >= ilo) ? kBK - dlo + 2 * iend + d : -1;
         }
-        unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
+        // capture window: the steps at which some lane's diagonal reaches the last row
+        // or column; blocks before it skip the capture selects
+        const int te_lo = (int)wave_min_u32(min((unsigned)te[0], (unsigned)te[1]));
         unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + q;
 
-        unsigned Hp0 = 0u, Hp1 = 0u, MoP = NEG2, XP = NEG2, YP = NEG2;
+        unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
         unsigned cap0 = NEG2, cap1 = NEG2;
         // LDS code cursors of the block starting at tau4: rows i0, i0 + 1; columns j0 .. j0 + 2
         auto ibase = [&](int tau4) { return (tau4 - kBK) / 2 - q; };
@@ -320,27 +448,28 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         unsigned sc[4], sn[4];
         load_scores(sc);
 
-        auto step = [&](int tau, auto Uc, auto PROc, unsigned& acc) {
+        auto step = [&](int tau, auto Uc, auto PROc, auto CAPc, const unsigned* scr, unsigned& acc) {
             constexpr int U = decltype(Uc)::value;
             constexpr int P = U & 1;
             constexpr bool PRO = decltype(PROc)::value;
+            constexpr bool CAP = decltype(CAPc)::value;
             unsigned X, Y, d1, d2;
             if constexpr (P == 0) {
                 // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
-                const unsigned Ml = row_shr1(NEG2, MoP), Xl = row_shr1(NEG2, XP);
+                const unsigned Ml = row_shr1(MoP), Xl = row_shr1(XP);
                 X = max2(Ml, Xl);
                 d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
                 Y = max2(MoP, YP);
                 d1 = sub2(YP, MoP);    // sign: Y opens
             } else {
                 // up = lane q+1's d0 one step back; left = own diagonal d0
-                const unsigned Mu = row_shl1(NEG2, MoP), Yu = row_shl1(NEG2, YP);
+                const unsigned Mu = row_shl1(MoP), Yu = row_shl1(YP);
                 Y = max2(Mu, Yu);
                 d1 = sub2(Yu, Mu);
                 X = max2(MoP, XP);
                 d2 = sub2(XP, MoP);
             }
-            unsigned M = add2(P ? Hp1 : Hp0, sc[U]);
+            unsigned M = add2(P ? Hp1 : Hp0, scr[U]);
             const unsigned mxy = max2(X, Y);
             unsigned H = max2(M, mxy);
             const unsigned d3 = sub2(Y, X);     // sign: X > Y
@@ -357,8 +486,10 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             MoP = sub2(M, OE2);
             XP = X;
             YP = Y;
-            if constexpr (P == 0) cap0 = tau == te[0] ? M : cap0;
-            else cap1 = tau == te[1] ? M : cap1;
+            if constexpr (CAP) {
+                if constexpr (P == 0) cap0 = tau == te[0] ? M : cap0;
+                else cap1 = tau == te[1] ? M : cap1;
+            }
             const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
             const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
             acc = and_or(tt, mT[U], acc);
@@ -368,27 +499,42 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        auto block = [&](int tau4, auto PROc) {
-            load_scores(sn);   // next block's scores (LDS latency hidden by this block)
+        // one block = 4 steps = one bit word; the next block's scores load meanwhile
+        // (into the other buffer: blocks go in pairs, so no register copies)
+        auto block = [&](int tau4, auto PROc, auto CAPc, const unsigned* cur, unsigned* nxt) {
+            load_scores(nxt);
             unsigned acc = 0u;
-            step(tau4, I0{}, PROc, acc);
-            step(tau4 + 1, I1{}, PROc, acc);
-            step(tau4 + 2, I2{}, PROc, acc);
-            step(tau4 + 3, I3{}, PROc, acc);
+            step(tau4, I0{}, PROc, CAPc, cur, acc);
+            step(tau4 + 1, I1{}, PROc, CAPc, cur, acc);
+            step(tau4 + 2, I2{}, PROc, CAPc, cur, acc);
+            step(tau4 + 3, I3{}, PROc, CAPc, cur, acc);
             const int w = (tau4 - tau0) >> 2;
             if (act && w < NW) bits[w * kBL] = acc;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) sc[u] = sn[u];
         };
+        // phases in whole block pairs (8 steps) from tau0: prologue (boundary cells,
+        // captures of short reads), bulk, capture window to tau_end (may run up to 7
+        // steps past it: cells outside the matrix, bits beyond NW not stored)
+        auto up8 = [&](int t) { return tau0 + ((t - tau0 + 7) & ~7); };
+        const int p1 = up8(tau_pro);
+        const int p2 = max(p1, tau0 + ((te_lo - tau0) & ~7));
         int tau4 = tau0;
-        for (; tau4 < tau_pro; tau4 += 4) block(tau4, std::true_type{});
-        for (; tau4 <= tau_end; tau4 += 4) block(tau4, std::false_type{});
+        for (; tau4 < p1; tau4 += 8) {
+            block(tau4, std::true_type{}, std::true_type{}, sc, sn);
+            block(tau4 + 4, std::true_type{}, std::true_type{}, sn, sc);
+        }
+        for (; tau4 < p2; tau4 += 8) {
+            block(tau4, std::false_type{}, std::false_type{}, sc, sn);
+            block(tau4 + 4, std::false_type{}, std::false_type{}, sn, sc);
+        }
+        for (; tau4 <= tau_end; tau4 += 8) {
+            block(tau4, std::false_type{}, std::true_type{}, sc, sn);
+            block(tau4 + 4, std::false_type{}, std::true_type{}, sn, sc);
+        }
 
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
             caps[2 * q] = cap0;
             caps[2 * q + 1] = cap1;
-            if (q == 0) *(int4*)region = make_int4(tau0, dlo, flags, 0);
         }
     }
 }
@@ -417,26 +563,43 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     unsigned* runs = (unsigned*)wb;
     unsigned char* rbuf = wb + kStreamRunsCap * 4;
 
+    const long long count = *a.band_count;
     const long long klo = 2 * a.band_pair_lo;
-    const long long khi = 2 * a.band_pair_hi < a.n ? 2 * a.band_pair_hi : a.n;
-    for (long long k = klo + (long long)blockIdx.x * wpb + wave; k < khi; k += (long long)gridDim.x * wpb) {
-        const long long rd = a.band_order[k];
-        const long long g = k >> 1;
+    const long long khi = 2 * a.band_pair_hi < count ? 2 * a.band_pair_hi : count;
+    // per read: the pair header (reads, lengths, offsets, geometry) and the 32
+    // captures come in one round trip; the next read's are loaded during this one
+    const long long kstep = (long long)gridDim.x * wpb;
+    auto region_of = [&](long long k) { return a.band_region + ((k >> 1) - a.band_pair_lo) * a.band_stride; };
+    int4 n0 = make_int4(0, 0, 0, 0), n1 = n0, n2 = n0;
+    unsigned ncw = 0u;
+    auto prefetch = [&](long long k) {
+        const unsigned char* rg = region_of(k);
+        n0 = ((const int4*)rg)[0];
+        n1 = ((const int4*)rg)[1];
+        n2 = ((const int4*)rg)[2];
+        ncw = lane < kBandDiags ? ((const unsigned*)(rg + kHdrBytes))[lane] : 0u;
+    };
+    long long k = klo + (long long)blockIdx.x * wpb + wave;
+    if (k < khi) prefetch(k);
+    for (; k < khi; k += kstep) {
+        const int4 hdr = n0, hr = n1, ho = n2;
+        const unsigned cw = ncw;
+        if (k + kstep < khi) prefetch(k + kstep);
         const int h = (int)(k & 1);
-        const long long rp = (k ^ 1) < a.n ? a.band_order[k ^ 1] : rd;
-        const long long off = a.offsets[rd];
-        const int Lb = (int)(a.offsets[rd + 1] - off);
+        const long long rd = h ? hr.y : hr.x;
+        const int Lb = h ? hr.w : hr.z;
+        const long long off = h ? (long long)(((unsigned long long)(unsigned)ho.w << 32) | (unsigned)ho.z)
+                                : (long long)(((unsigned long long)(unsigned)ho.y << 32) | (unsigned)ho.x);
         if (Lb <= 0) {
             if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; a.stats[rd] = z; }
             continue;
         }
-        const int Lp = (int)(a.offsets[rp + 1] - a.offsets[rp]);
-        int dlo;
-        if (Lp != Lb || Lb > a.band_lb_cap || !band_geometry(La, Lb, &dlo)) {
+        if (hdr.z & kPairInactive) {   // unequal lengths, too long, or outside the band's reach
             if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
             continue;
         }
-        const unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
+        const int dlo = hdr.y;
+        const unsigned char* region = region_of(k);
         const unsigned char* raw = a.reads + off;
         // the read's bytes -> LDS (DMA, one dword per lane) for the emit
         const bool cached = Lb <= kBandReadCap;
@@ -447,7 +610,6 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + m + 4 * lane),
                                                  (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
         }
-        const int4 hdr = *(const int4*)region;
         const int tau0 = hdr.x;
         // start cell: the last cell of each band diagonal is on the last row or column
         unsigned k32 = 0u;
@@ -456,8 +618,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             const int iend = La < Lb - d ? La : Lb - d;
             const int ilo = 1 - d > 1 ? 1 - d : 1;
             if (iend >= ilo) {
-                const unsigned cw = ((const unsigned*)(region + kHdrBytes))[lane];
-                const int v = half(cw, h) - E * (2 * iend + d);
+                const int v = half(cw, h) - kBias16 - E * (2 * iend + d);
                 const int jend = iend + d;
                 k32 = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
                       : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
@@ -519,10 +680,17 @@ hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_band_walk, 64 * walk_wpb, walk_lds);
 }
 
+// a.sort_hist holds (band_lb_cap + 3) * (grid + 1) ints: the count table, then the bucket
+// bases; a.band_count points at the base of the exact bucket (= reads that need the DP)
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(nw_band_hist, dim3(grid), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(nw_band_scan, dim3(1), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(nw_band_scatter, dim3(grid), dim3(256), 0, s, a);
+    const int nb = a.band_lb_cap + 3;
+    const size_t lds = sizeof(int) * (size_t)nb;
+    hipLaunchKernelGGL(nw_band_classify, dim3(std::max(1, std::min(2048, (int)((a.n + 63) / 64)))), dim3(256),
+                       (size_t)(4 * ((a.La + 3) / 4)), s, a);
+    hipLaunchKernelGGL(nw_band_hist, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(nw_band_rowscan, dim3(nb), dim3(64), 0, s, a, grid);
+    hipLaunchKernelGGL(nw_band_scan, dim3(1), dim3(1024), 0, s, a, grid);
+    hipLaunchKernelGGL(nw_band_scatter, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 

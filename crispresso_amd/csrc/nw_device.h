@@ -62,7 +62,9 @@ struct KernelArgs {
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
     const uint32_t* band_tab;      // [6 amplicon codes][6][6 read codes] packed int16x2 score + 2 E
     const uint32_t* rowpos;        // [La] codes each amplicon row scores > 0 against (markup ':')
-    int32_t* sort_hist;            // [band_lb_cap + 2] length buckets of the counting sort
+    int32_t* sort_hist;            // [band_lb_cap + 3][sort grid + 1] per-block bucket counts, bucket bases
+    int32_t* sort_key;             // [n] bucket of every read: length, band_lb_cap + 1 (longer), + 2 (exact copy)
+    const int32_t* band_count;     // device: sorted reads that need the DP (the exact copies follow)
 };
 
 // Traceback storage of a kernel instantiation.

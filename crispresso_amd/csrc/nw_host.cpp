@@ -124,7 +124,7 @@ struct nw_ctx {
     bool use_diag = false;
     nw::LaunchCfg diag_fill{}, diag_walk{};
     DevBuf<uint32_t> d_btab, d_rowpos;
-    DevBuf<int32_t> d_order, d_sort_hist;
+    DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
     DevBuf<uint8_t> d_bregion;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
@@ -372,10 +372,11 @@ int configure(nw_ctx* c) {
                                                                  (int64_t)c->num_cus * fb));
             w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((2 * pass_pairs + w.wpb - 1) / w.wpb,
                                                                  (int64_t)c->num_cus * wb));
-            c->diag_sort_grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 255) / 256, 4ll * c->num_cus));
+            c->diag_sort_grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 1023) / 1024, 1024));
             HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)(pass_pairs * c->diag_stride)));
             HIP_OR_FAIL(c, c->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->d_sort_hist.reserve((size_t)c->diag_lb_cap + 2));
+            HIP_OR_FAIL(c, c->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
+            HIP_OR_FAIL(c, c->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
             c->diag_fill = f;
             c->diag_walk = w;
             c->use_diag = true;
@@ -462,7 +463,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
     c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
-    c->d_btab.release(); c->d_rowpos.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_bregion.release();
+    c->d_btab.release(); c->d_rowpos.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -603,7 +604,8 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.band_tab = c->d_btab.p;
         a.rowpos = c->d_rowpos.p;
         a.sort_hist = c->d_sort_hist.p;
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_sort_hist.p, 0, sizeof(int32_t) * ((size_t)c->diag_lb_cap + 2), c->stream));
+        a.sort_key = c->d_sort_key.p;
+        a.band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->stream));
         const int64_t pairs = (c->n + 1) / 2;
         for (int64_t lo = 0; lo < pairs; lo += c->diag_pass_pairs) {

@@ -426,3 +426,21 @@ def test_diag_homopolymer_ties(gpu_aligner_factory, oracle):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off), "diag-homopolymer")
+
+
+def test_diag_exact_copies(gpu_aligner_factory, oracle):
+    """Reads identical to the amplicon (any case) take the no-DP path; near-copies
+    (one N, one substitution, U for T, one base short) and an amplicon with N do not."""
+    amp = synth.random_amplicon(200, 31)
+    reads = [amp, amp.lower(), amp[:50].lower() + amp[50:], amp] * 5
+    reads += [amp[:70] + "N" + amp[71:], amp[:70] + ("A" if amp[70] != "A" else "C") + amp[71:],
+              amp.replace("T", "U"), amp[:-1], amp[1:], amp + "A", ""]
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert_same(oracle, amp, buf, off, batch, "exact")
+    amp_n = amp[:100] + "N" + amp[101:]
+    a.set_reference(amp_n)
+    buf, off = pack_reads([amp_n, amp_n.lower(), amp] * 3)
+    assert_same(oracle, amp_n, buf, off, a.align_packed(buf, off), "exact-N")
