@@ -206,11 +206,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
 #pragma unroll
             for (int u = 0; u < kClassifyReads; ++u) same[u] = same[u] && __ballot(diff[u] != 0u) == 0ull;
         }
+        // keys of the batch: lane u stores read r0 + u's
+        int my_key = 0;
+#pragma unroll
+        for (int u = 0; u < kClassifyReads; ++u)
+            if (lane == u) my_key = same[u] ? a.band_lb_cap + 2 : (Lb[u] <= a.band_lb_cap ? Lb[u] : a.band_lb_cap + 1);
+        if (lane < kClassifyReads && r0 + lane < a.n) a.sort_key[r0 + lane] = my_key;
 #pragma unroll
         for (int u = 0; u < kClassifyReads; ++u) {
             const long long r = r0 + u;
             if (r >= a.n) break;
-            if (lane == 0) a.sort_key[r] = same[u] ? a.band_lb_cap + 2 : (Lb[u] <= a.band_lb_cap ? Lb[u] : a.band_lb_cap + 1);
             if (!same[u]) continue;
             // the diagonal: amplicon, '|' markup, read; rows as dwords up to round4(La) (within the stride)
             unsigned* o = (unsigned*)(a.out + r * 3 * a.stride);
