@@ -149,14 +149,12 @@ __device__ __forceinline__ int len_bucket(const int64_t* offsets, long long r, i
 // residues (S > UB of the one-diagonal band, the certificate above), so the
 // alignment is the diagonal and the start cell the corner: this kernel writes its
 // strings and record right away, and the sort keeps it out of the band passes.
-// One wavefront per read, 16 reads in flight; 4 bytes per lane and compare:
+// Wavefront batches of 64 reads, 4 compares in flight; 4 bytes per lane and compare:
 // (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
 __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
 
-constexpr int kClassifyReads = 16;
-
 __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
-    extern __shared__ unsigned amp_lo[];   // folded amplicon dwords, zero-padded
+    extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     const int La = a.La, nd = (La + 3) / 4;
     for (int k = threadIdx.x; k < nd; k += blockDim.x) {
         unsigned w = 0;
@@ -165,77 +163,72 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             const unsigned char c = q < La ? upcase(a.amp[q]) : 0;
             w |= (unsigned)((c == 'A' || c == 'C' || c == 'G' || c == 'T') ? (c | 0x20) : 0) << (8 * b);
         }
-        amp_lo[k] = w;
+        amp_sh[k] = w;
+        amp_sh[nd + k] = ld_dw(a.amp + 4 * k);
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
-    const long long step = (long long)gridDim.x * wpb * kClassifyReads;
-    for (long long r0 = ((long long)blockIdx.x * wpb + (threadIdx.x >> 6)) * kClassifyReads; r0 < a.n; r0 += step) {
-        // lanes 0..kClassifyReads-1 load the batch's offsets in one coalesced round trip
-        long long my_off = 0;
-        int my_len = -1;
-        if (lane < kClassifyReads && r0 + lane < a.n) {
-            my_off = a.offsets[r0 + lane];
-            my_len = (int)(a.offsets[r0 + lane + 1] - my_off);
-        }
-        long long off[kClassifyReads];
-        bool same[kClassifyReads];
-        int Lb[kClassifyReads];
+    // wavefront batches of 64 reads: lane u holds read r0 + u's offset and length
+    for (long long r0 = ((long long)blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; r0 < a.n;
+         r0 += (long long)gridDim.x * wpb * 64) {
+        const long long r = r0 + lane;
+        const long long my_off = r < a.n ? a.offsets[r] : 0;
+        const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
+        unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
+        unsigned long long exact = 0ull;
+        // compare 4 candidates at a time (their loads in flight together)
+        while (cand) {
+            int us[4];
+            unsigned diff[4];
 #pragma unroll
-        for (int u = 0; u < kClassifyReads; ++u) {
-            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
-            off[u] = (long long)(((unsigned long long)hi << 32) | lo);
-            Lb[u] = __builtin_amdgcn_readlane(my_len, u);
-            same[u] = Lb[u] == La;
-        }
-        for (int c0 = 0; c0 < nd; c0 += 64) {
-            const int k4 = c0 + lane;
-            unsigned diff[kClassifyReads];
+            for (int t = 0; t < 4; ++t) {
+                us[t] = cand ? (int)__builtin_ctzll(cand) : -1;
+                if (cand) cand &= cand - 1;
+                diff[t] = 0u;
+            }
+            for (int c0 = 0; c0 < nd; c0 += 64) {
+                const int k4 = c0 + lane;
 #pragma unroll
-            for (int u = 0; u < kClassifyReads; ++u) {
-                diff[u] = 0u;
-                if (same[u] && k4 < nd) {
-                    const uint8_t* base = a.reads + (off[u] & ~3ll) + 4 * k4;
-                    const unsigned w = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off[u] & 3)) | 0x20202020u;
-                    diff[u] = (w ^ amp_lo[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
+                for (int t = 0; t < 4; ++t) {
+                    if (us[t] < 0 || k4 >= nd) continue;
+                    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, us[t]);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), us[t]);
+                    const long long off = (long long)(((unsigned long long)hi << 32) | lo);
+                    const uint8_t* base = a.reads + (off & ~3ll) + 4 * k4;
+                    const unsigned w = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off & 3)) | 0x20202020u;
+                    diff[t] |= (w ^ amp_sh[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kClassifyReads; ++u) same[u] = same[u] && __ballot(diff[u] != 0u) == 0ull;
+            for (int t = 0; t < 4; ++t)
+                if (us[t] >= 0 && __ballot(diff[t] != 0u) == 0ull) exact |= 1ull << us[t];
         }
-        // keys of the batch: lane u stores read r0 + u's
-        int my_key = 0;
-#pragma unroll
-        for (int u = 0; u < kClassifyReads; ++u)
-            if (lane == u) my_key = same[u] ? a.band_lb_cap + 2 : (Lb[u] <= a.band_lb_cap ? Lb[u] : a.band_lb_cap + 1);
-        if (lane < kClassifyReads && r0 + lane < a.n) a.sort_key[r0 + lane] = my_key;
-#pragma unroll
-        for (int u = 0; u < kClassifyReads; ++u) {
-            const long long r = r0 + u;
-            if (r >= a.n) break;
-            if (!same[u]) continue;
-            // the diagonal: amplicon, '|' markup, read; rows as dwords up to round4(La) (within the stride)
-            unsigned* o = (unsigned*)(a.out + r * 3 * a.stride);
-            const uint8_t* base = a.reads + (off[u] & ~3ll);
+        if (r < a.n)
+            a.sort_key[r] = ((exact >> lane) & 1ull) ? a.band_lb_cap + 2 : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+        // the diagonal of every exact copy: amplicon, '|' markup, read; rows as dwords up to
+        // round4(La) (within the row stride)
+        while (exact) {
+            const int u = (int)__builtin_ctzll(exact);
+            exact &= exact - 1;
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
+            const long long off = (long long)(((unsigned long long)hi << 32) | lo);
+            const uint8_t* base = a.reads + (off & ~3ll);
+            unsigned* o = (unsigned*)(a.out + (r0 + u) * 3 * a.stride);
             for (int k4 = lane; k4 < nd; k4 += 64) {
-                o[k4] = ld_dw(a.amp + 4 * k4);
+                o[k4] = amp_sh[nd + k4];
                 o[sd + k4] = 0x7c7c7c7cu;   // '|'
-                o[2 * sd + k4] = __builtin_amdgcn_alignbyte(ld_dw(base + 4 * k4 + 4), ld_dw(base + 4 * k4), (int)(off[u] & 3));
+                o[2 * sd + k4] = __builtin_amdgcn_alignbyte(ld_dw(base + 4 * k4 + 4), ld_dw(base + 4 * k4), (int)(off & 3));
             }
-            if (lane == 0) {
-                Stat st;
-                st.aln_len = La;
-                st.n_ident = La;
-                st.n_sim = La;
-                st.n_gaps = 0;
-                st.score = a.band_maxsub * La;
-                st.end_i = La;
-                st.end_j = La;
-                st.flags = 0;
-                a.stats[r] = st;
+            if (lane < 8) {
+                // the record (nw::Stat): aln_len, n_ident, n_sim, n_gaps, score, end_i, end_j, flags
+                const int v[8] = {La, La, La, 0, a.band_maxsub * La, La, La, 0};
+                int x = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) x = lane == t ? v[t] : x;
+                ((int*)(a.stats + r0 + u))[lane] = x;
             }
         }
     }
@@ -690,8 +683,8 @@ hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s) {
     const int nb = a.band_lb_cap + 3;
     const size_t lds = sizeof(int) * (size_t)nb;
-    hipLaunchKernelGGL(nw_band_classify, dim3(std::max(1, std::min(2048, (int)((a.n + 63) / 64)))), dim3(256),
-                       (size_t)(4 * ((a.La + 3) / 4)), s, a);
+    hipLaunchKernelGGL(nw_band_classify, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))), dim3(256),
+                       (size_t)(8 * ((a.La + 3) / 4)), s, a);
     hipLaunchKernelGGL(nw_band_hist, dim3(grid), dim3(256), lds, s, a);
     hipLaunchKernelGGL(nw_band_rowscan, dim3(nb), dim3(64), 0, s, a, grid);
     hipLaunchKernelGGL(nw_band_scan, dim3(1), dim3(1024), 0, s, a, grid);
