@@ -540,6 +540,77 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
 // ============================================================================
 // Walk + emit: one wavefront per read (sorted order), latency-bound.
 // ============================================================================
+// The run-based traceback of nw_common.h (walk_runs_wide), written for a
+// wave-uniform state machine: state, i, j live in SGPRs, every lane tests CPL
+// cells of the current run with branch-free lookups, one ballot per round.
+// Same results (runs in end->start order; -1 when the walk leaves the band or
+// needs more than `cap` runs).
+template <int CPL, class Code>
+__device__ int band_walk_runs(const Code& code_at, int La, int Lb, int ei, int ej, unsigned* runs, int cap, int lane) {
+    int nruns = 0, last_type = -1;
+    bool full = false;
+    auto push = [&](int type, int n) {
+        if (n <= 0) return;
+        if (type == last_type) {
+            if (lane == 0) runs[nruns - 1] += (unsigned)n;
+        } else if (nruns < cap) {
+            if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
+            ++nruns;
+            last_type = type;
+        } else {
+            full = true;
+        }
+    };
+    if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
+    else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
+    constexpr int W = 64 * CPL;
+    int i = __builtin_amdgcn_readfirstlane(ei), j = __builtin_amdgcn_readfirstlane(ej), state = RUN_M;
+    while (i > 0 && j > 0) {
+        // cells tested: M: (i-1-k, j-1-k); X: (i, j-k); Y: (i-k, j)   (1-based, k = 0..W-1)
+        const int off = state == RUN_M ? 1 : 0;
+        const int dI = state == RUN_X ? 0 : 1, dJ = state == RUN_Y ? 0 : 1;
+        const unsigned gobit = state == RUN_X ? 4u : 8u;
+        int first = CPL, first_best = RUN_M, first_oob = 0;
+        unsigned c[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int kk = lane * CPL + u;
+            c[u] = code_at(i - off - dI * kk - 1, j - off - dJ * kk - 1);
+        }
+#pragma unroll
+        for (int u = CPL - 1; u >= 0; --u) {
+            const int kk = lane * CPL + u;
+            const bool valid = i - off - dI * kk >= 1 && j - off - dJ * kk >= 1;
+            const int best = (c[u] & 1u) ? ((c[u] & 2u) ? RUN_X : RUN_Y) : RUN_M;
+            const bool go = state == RUN_M ? best == RUN_M : (c[u] & gobit) == 0u;
+            const bool oob = (c[u] & 16u) != 0u;
+            if (!valid || oob || !go) {
+                first = u;
+                first_oob = valid && oob;
+                first_best = best;
+            }
+        }
+        const unsigned long long m = __ballot(first < CPL);
+        if (m == 0) {
+            push(state, W);
+            if (state != RUN_Y) j -= W;
+            if (state != RUN_X) i -= W;
+            continue;
+        }
+        const int L = (int)__builtin_ctzll(m);
+        const int k0 = L * CPL + __builtin_amdgcn_readlane(first, L);
+        const int nb = __builtin_amdgcn_readlane(first_best, L);
+        if (__builtin_amdgcn_readlane(first_oob, L) || full) return -1;
+        push(state, k0 + 1);
+        if (state != RUN_Y) j -= k0 + 1;
+        if (state != RUN_X) i -= k0 + 1;
+        state = (state == RUN_M) ? nb : RUN_M;
+    }
+    if (i > 0) push(RUN_Y, i);
+    if (j > 0) push(RUN_X, j);
+    return full ? -1 : nruns;
+}
+
 constexpr int kBandReadCap = 1024;
 __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
 __host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 4 + kBandReadCap + 256; }
@@ -637,19 +708,22 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
         const int tb0 = kBK - dlo + 2 - tau0;
-        auto nib = [&](int ai, int bjj, bool* oob) -> unsigned {
+        // 4-bit cell code of 0-based cell (ai, bjj), bit 4 = outside the band; branch-free
+        // (cells that are not tested read a clamped, harmless word)
+        const int nw_max = a.band_words - 1;
+        auto code_at = [&](int ai, int bjj) -> unsigned {
             const int kd = bjj - ai - dlo;
-            if ((unsigned)kd >= (unsigned)kBandDiags) { *oob = true; return 0u; }
-            *oob = false;
+            const unsigned oob = (unsigned)kd >= (unsigned)kBandDiags ? 16u : 0u;
             const int tau = ai + bjj + tb0;
-            const unsigned w = bits[(tau >> 2) * kBL + (kd >> 1)];
+            const int wi = min(max(tau >> 2, 0), nw_max);
+            const unsigned w = bits[wi * kBL + ((kd & (kBandDiags - 1)) >> 1)];
             const int s = tau & 3;
             const int hb = 8 * h + s, lb = 8 * h + 4 + s;
             const unsigned yop = (w >> hb) & 1u, xgy = (w >> lb) & 1u;
             const unsigned xop = (w >> (16 + hb)) & 1u, notm = (w >> (16 + lb)) & 1u;
-            return notm | (xgy << 1) | (xop << 2) | (yop << 3);
+            return notm | (xgy << 1) | (xop << 2) | (yop << 3) | oob;
         };
-        const int nruns = walk_runs_wide<NW_BAND_WALK_CPL>(nib, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        const int nruns = band_walk_runs<NW_BAND_WALK_CPL>(code_at, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
             if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;

@@ -247,7 +247,7 @@ __device__ void emit_alignment(const unsigned* runs, int nruns, const unsigned c
     int col = 0, ia = 0, jb = 0;
     int n_id = 0, n_sim = 0, n_gap = 0;
     for (int q = nruns - 1; q >= 0; --q) {
-        const unsigned rc = runs[q];
+        const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)runs[q]);   // uniform: scalar branches
         const int type = (int)(rc >> 28);
         const int n = (int)(rc & 0x0fffffffu);
         for (int p = lane; p < n; p += 64) {
