@@ -22,14 +22,14 @@
 //   traceback, bit for bit.
 //
 // Reads that fail the certificate (S <= UB: chimeras, off-target, large indels),
-// whose length differs from the amplicon's by more than 31, or that hold IUPAC
-// codes other than N go to the exact int32 kernel's fallback list.
+// whose pair's lengths span more than the band, or that hold IUPAC codes other
+// than N go to the exact int32 kernel's fallback list.
 //
 // Layout / schedule:
 //   * reads are sorted by length on the device (counting sort, nw_band_hist /
-//     _scan / _scatter); sorted positions (2g, 2g+1) form pair g, both reads of a
-//     pair have the same length (unequal pairs fall back), so they share one
-//     geometry and run packed in int16x2 (read A low, B high);
+//     _scan / _scatter); sorted positions (2g, 2g+1) form pair g, packed in int16x2
+//     (read A low, B high) on one band that holds both reads' start and end
+//     diagonals; the sort keeps the wavefront's pairs at similar lengths;
 //   * one read pair per 16-lane DPP row, 4 pairs per wavefront; lane q owns
 //     diagonals d0 = dlo + 2q and d0 + 1; the wave sweeps anti-diagonals t = i + j
 //     and at each step every lane computes one cell (the diagonal whose parity
@@ -96,15 +96,20 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) { return ~wave_max_
 }  // namespace
 
 // ---- geometry shared by fill, walk and host --------------------------------------
-__host__ __device__ inline bool band_geometry(int La, int Lb, int* dlo) {
-    const int D = Lb - La;
-    const int lo0 = D < 0 ? D : 0, hi0 = D > 0 ? D : 0;
+// Band of a read pair: it must hold both reads' start (diagonal 0's neighbourhood)
+// and end diagonals (Lb - La); the spare diagonals are split evenly.  An empty
+// read imposes nothing.  False when the band cannot hold them or both are empty.
+__host__ __device__ inline bool band_geometry2(int La, int LbA, int LbB, int* dlo) {
+    int lo0 = 0, hi0 = 0;
+    if (LbA > 0) { lo0 = min(lo0, LbA - La); hi0 = max(hi0, LbA - La); }
+    if (LbB > 0) { lo0 = min(lo0, LbB - La); hi0 = max(hi0, LbB - La); }
     const int extra = kBandDiags - (hi0 - lo0 + 1);
     *dlo = 0;
-    if (Lb <= 0 || extra < 0) return false;
+    if ((LbA <= 0 && LbB <= 0) || extra < 0) return false;
     *dlo = lo0 - extra / 2;
     return true;
 }
+__host__ __device__ inline bool band_geometry(int La, int Lb, int* dlo) { return band_geometry2(La, Lb, Lb, dlo); }
 
 namespace {
 
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
     const int NW = a.band_words;
     for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nwork; wv += (long long)gridDim.x * wpb) {
         const long long g = a.band_pair_lo + wv * kBPW + grp;
-        int Lb = La, dlo = 0;
+        int dlo = 0;
         bool act = false;
         long long offA = 0, offB = 0, ra = 0, rb = 0;
         int LbA = 0, LbB = 0;
@@ -367,19 +372,22 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             offB = a.offsets[rb];
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
-            act = LbA == LbB && LbA <= a.band_lb_cap && band_geometry(La, LbA, &dlo);
-            if (act) Lb = LbA;
+            act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo);
         }
-        if (!act) band_geometry(La, La, &dlo);   // neutral geometry, nothing stored
+        if (!act) {   // neutral geometry, nothing stored
+            band_geometry(La, La, &dlo);
+            LbA = LbB = 0;
+        }
+        const int Lmax = max(LbA, LbB);
 
         // pair codes of the group's columns (j = 1..Lb real, the rest pad)
         bool badA = false, badB = false;
         for (int k = q; k < PCS; k += kBL) {
             const int j = k - kJPad;
             int cA = kPadCode, cB = kPadCode;
-            if (act && j >= 1 && j <= Lb) {
-                cA = a.lut6[a.reads[offA + j - 1]];
-                cB = a.lut6[a.reads[offB + j - 1]];
+            if (j >= 1 && j <= Lmax) {
+                cA = j <= LbA ? a.lut6[a.reads[offA + j - 1]] : kPadCode;
+                cB = j <= LbB ? a.lut6[a.reads[offB + j - 1]] : kPadCode;
                 // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
                 if (cA > kPadCode) { badA = true; cA = kPadCode; }
                 if (cB > kPadCode) { badB = true; cB = kPadCode; }
@@ -392,7 +400,7 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
 
         // wave-uniform tau range; per lane: boundary and capture steps
         const unsigned tlo = act ? (unsigned)(kBK - dlo) : 0xffffffffu;
-        const unsigned thi = act ? (unsigned)(kBK - dlo + La + Lb) : 0u;
+        const unsigned thi = act ? (unsigned)(kBK - dlo + La + Lmax) : 0u;
         const unsigned dmax = (unsigned)(-dlo > dlo + kBandDiags - 1 ? -dlo : dlo + kBandDiags - 1);
         const unsigned tpro = act ? (unsigned)(kBK - dlo) + dmax + 1 : 0u;
         const int tau0 = (int)(wave_min_u32(tlo) & ~3u);
@@ -404,13 +412,13 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             // everything the walk needs to find the pair's reads: one 48-byte load
             int4* hp = (int4*)region;
             hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive), 0);
-            hp[1] = make_int4((int)ra, (int)rb, LbA, LbB);
+            hp[1] = make_int4((int)ra, (int)rb, (int)(a.offsets[ra + 1] - offA), (int)(a.offsets[rb + 1] - offB));
             hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
         }
         if (tau_end == 0) continue;   // no active group in this wavefront
 
         const int d0 = dlo + 2 * q;
-        int tb[2], te[2];
+        int tb[2], te[2], teB[2];
         unsigned bval[2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -418,17 +426,20 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             const int ad = d < 0 ? -d : d;
             tb[p] = kBK - dlo + ad;
             bval[p] = pk(E * ad + kBias16, E * ad + kBias16);
-            const int iend = La < Lb - d ? La : Lb - d;
             const int ilo = 1 - d > 1 ? 1 - d : 1;
-            te[p] = (act && iend >= ilo) ? kBK - dlo + 2 * iend + d : -1;
+            // step at which diagonal d reaches read A's / read B's last row or column
+            const int ieA = La < LbA - d ? La : LbA - d, ieB = La < LbB - d ? La : LbB - d;
+            te[p] = (LbA > 0 && ieA >= ilo) ? kBK - dlo + 2 * ieA + d : -1;
+            teB[p] = (LbB > 0 && ieB >= ilo) ? kBK - dlo + 2 * ieB + d : -1;
         }
         // capture window: the steps at which some lane's diagonal reaches the last row
         // or column; blocks before it skip the capture selects
-        const int te_lo = (int)wave_min_u32(min((unsigned)te[0], (unsigned)te[1]));
+        const int te_lo = (int)wave_min_u32(min(min((unsigned)te[0], (unsigned)te[1]),
+                                                min((unsigned)teB[0], (unsigned)teB[1])));
         unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + q;
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
-        unsigned cap0 = NEG2, cap1 = NEG2;
+        unsigned cap0 = NEG2, cap1 = NEG2, capB0 = NEG2, capB1 = NEG2;   // read A's (low) / B's (high half)
         // LDS code cursors of the block starting at tau4: rows i0, i0 + 1; columns j0 .. j0 + 2
         auto ibase = [&](int tau4) { return (tau4 - kBK) / 2 - q; };
         const uint16_t* ap = acd + kAPad + ibase(tau0);
@@ -485,8 +496,13 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             XP = X;
             YP = Y;
             if constexpr (CAP) {
-                if constexpr (P == 0) cap0 = tau == te[0] ? M : cap0;
-                else cap1 = tau == te[1] ? M : cap1;
+                if constexpr (P == 0) {
+                    cap0 = tau == te[0] ? M : cap0;
+                    capB0 = tau == teB[0] ? M : capB0;
+                } else {
+                    cap1 = tau == te[1] ? M : cap1;
+                    capB1 = tau == teB[1] ? M : capB1;
+                }
             }
             const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
             const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
@@ -531,8 +547,8 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
 
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
-            caps[2 * q] = cap0;
-            caps[2 * q + 1] = cap1;
+            caps[2 * q] = (cap0 & 0xffffu) | (capB0 & 0xffff0000u);
+            caps[2 * q + 1] = (cap1 & 0xffffu) | (capB1 & 0xffff0000u);
         }
     }
 }
