@@ -79,12 +79,15 @@ __device__ __forceinline__ unsigned max2(unsigned a, unsigned b) {
 }
 __device__ __forceinline__ unsigned add2(unsigned a, unsigned b) { return as_u(as_v(a) + as_v(b)); }
 __device__ __forceinline__ unsigned sub2(unsigned a, unsigned b) { return as_u(as_v(a) - as_v(b)); }
-// DPP within 16-lane rows; a lane without a source reads 0 (= -inf: outside the band)
-__device__ __forceinline__ unsigned row_shr1(unsigned v) {
-    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, true);
+// DPP within 16-lane rows by S lanes; a lane without a source reads 0 (= -inf:
+// outside the band).  S = 2 when two read pairs share a row (interleaved lanes).
+template <int S>
+__device__ __forceinline__ unsigned row_shr(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x110 + S, 0xf, 0xf, true);
 }
-__device__ __forceinline__ unsigned row_shl1(unsigned v) {
-    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, true);
+template <int S>
+__device__ __forceinline__ unsigned row_shl(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x100 + S, 0xf, 0xf, true);
 }
 __device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
     unsigned d;
@@ -99,11 +102,11 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) { return ~wave_max_
 // Band of a read pair: it must hold both reads' start (diagonal 0's neighbourhood)
 // and end diagonals (Lb - La); the spare diagonals are split evenly.  An empty
 // read imposes nothing.  False when the band cannot hold them or both are empty.
-__host__ __device__ inline bool band_geometry2(int La, int LbA, int LbB, int* dlo) {
+__host__ __device__ inline bool band_geometry2(int La, int LbA, int LbB, int* dlo, int W = kBandDiags) {
     int lo0 = 0, hi0 = 0;
     if (LbA > 0) { lo0 = min(lo0, LbA - La); hi0 = max(hi0, LbA - La); }
     if (LbB > 0) { lo0 = min(lo0, LbB - La); hi0 = max(hi0, LbB - La); }
-    const int extra = kBandDiags - (hi0 - lo0 + 1);
+    const int extra = W - (hi0 - lo0 + 1);
     *dlo = 0;
     if ((LbA <= 0 && LbB <= 0) || extra < 0) return false;
     *dlo = lo0 - extra / 2;
@@ -113,8 +116,15 @@ __host__ __device__ inline bool band_geometry(int La, int Lb, int* dlo) { return
 
 namespace {
 
-constexpr int kBL = kBandDiags / 2;   // lanes per read pair (one DPP row)
-constexpr int kBPW = 64 / kBL;        // read pairs per wavefront
+// band of W diagonals: L = W / 2 lanes per read pair, PR pairs per 16-lane DPP row
+// (interleaved: pair = lane % PR, q = lane / PR within the row), PW pairs per wavefront
+template <int W> struct BandGeo {
+    static constexpr int L = W / 2;
+    static constexpr int PR = 16 / L;
+    static constexpr int PW = 4 * PR;
+    static constexpr int CapBytes = W * 4;
+    static constexpr unsigned RowMask = PR == 1 ? 0xffffu : 0x5555u;
+};
 constexpr int kBK = 64;               // tau = t - dlo + kBK: >= 0 and even
 constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [-17, La + 48]
 constexpr int kJPad = 96;             // pair codes: index j + kJPad, j in [-79, La + 79]
@@ -122,7 +132,6 @@ constexpr int kPadCode = 5;           // lut6: A T G C N pad
 constexpr int kTabBytes = 896;        // [6][36] packed scores (864 B)
 constexpr int kHdrBytes = 48;         // {tau0, dlo, flags, -}, {ra, rb, LbA, LbB}, {offA, offB}
 constexpr int kPairInactive = 4;      // header flag: the pair was not filled (walk: empty / fallback)
-constexpr int kCapBytes = kBandDiags * 4;
 
 __host__ __device__ inline int band_acd_elems(int La) { return La + kAPad + 64; }
 __host__ __device__ inline int band_pcs(int La) { return align16(La + kJPad + 96); }
@@ -133,8 +142,8 @@ __host__ __device__ inline int band_words(int La, int Lb_max) {
     const int Lbm = Lb_max < La + kBandDiags - 1 ? Lb_max : La + kBandDiags - 1;
     return (La + Lbm + 80) / 4 + 2;
 }
-__host__ __device__ inline int64_t band_region_stride(int La, int Lb_max) {
-    return ((int64_t)kHdrBytes + kCapBytes + (int64_t)band_words(La, Lb_max) * kBL * 4 + 255) & ~(int64_t)255;
+__host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W) {
+    return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max) * (W / 2) * 4 + 255) & ~(int64_t)255;
 }
 
 // ============================================================================
@@ -321,12 +330,15 @@ __global__ __launch_bounds__(256) void nw_band_scatter(const KernelArgs a) {
 // ============================================================================
 // Fill
 // ============================================================================
+template <int W>
 __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
+    using G = BandGeo<W>;
+    constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
-    const int q = lane & (kBL - 1), grp = lane / kBL;
+    const int q = (lane & 15) / G::PR, grp = (lane >> 4) * G::PR + (lane & 15) % G::PR;
     const unsigned NEG2 = 0u;                    // -inf in the kBias16 domain
     const unsigned OE2 = pk(O - E, O - E);
 
@@ -372,10 +384,10 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             offB = a.offsets[rb];
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
-            act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo);
+            act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo, W);
         }
         if (!act) {   // neutral geometry, nothing stored
-            band_geometry(La, La, &dlo);
+            band_geometry2(La, La, La, &dlo, W);
             LbA = LbB = 0;
         }
         const int Lmax = max(LbA, LbB);
@@ -395,13 +407,13 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             pcd[k] = (unsigned char)((cA * 6 + cB) * 4);
         }
         const unsigned long long bA = __ballot(badA), bB = __ballot(badB);
-        const int flags = (((bA >> (grp * kBL)) & 0xffffull) ? REGION_BAD_A : 0) |
-                          (((bB >> (grp * kBL)) & 0xffffull) ? REGION_BAD_B : 0);
+        const unsigned long long gmask = (unsigned long long)G::RowMask << ((lane & ~15) + (lane & 15) % G::PR);
+        const int flags = ((bA & gmask) ? REGION_BAD_A : 0) | ((bB & gmask) ? REGION_BAD_B : 0);
 
         // wave-uniform tau range; per lane: boundary and capture steps
         const unsigned tlo = act ? (unsigned)(kBK - dlo) : 0xffffffffu;
         const unsigned thi = act ? (unsigned)(kBK - dlo + La + Lmax) : 0u;
-        const unsigned dmax = (unsigned)(-dlo > dlo + kBandDiags - 1 ? -dlo : dlo + kBandDiags - 1);
+        const unsigned dmax = (unsigned)(-dlo > dlo + W - 1 ? -dlo : dlo + W - 1);
         const unsigned tpro = act ? (unsigned)(kBK - dlo) + dmax + 1 : 0u;
         const int tau0 = (int)(wave_min_u32(tlo) & ~3u);
         const int tau_end = (int)wave_max_u32(thi);
@@ -465,14 +477,14 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             unsigned X, Y, d1, d2;
             if constexpr (P == 0) {
                 // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
-                const unsigned Ml = row_shr1(MoP), Xl = row_shr1(XP);
+                const unsigned Ml = row_shr<G::PR>(MoP), Xl = row_shr<G::PR>(XP);
                 X = max2(Ml, Xl);
                 d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
                 Y = max2(MoP, YP);
                 d1 = sub2(YP, MoP);    // sign: Y opens
             } else {
                 // up = lane q+1's d0 one step back; left = own diagonal d0
-                const unsigned Mu = row_shl1(MoP), Yu = row_shl1(YP);
+                const unsigned Mu = row_shl<G::PR>(MoP), Yu = row_shl<G::PR>(YP);
                 Y = max2(Mu, Yu);
                 d1 = sub2(Yu, Mu);
                 X = max2(MoP, XP);
@@ -631,7 +643,16 @@ constexpr int kBandReadCap = 1024;
 __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
 __host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 4 + kBandReadCap + 256; }
 
+// W < kBandDiags: a first level; reads it cannot certify go to the redo list of the
+// next (wider) level.  W = kBandDiags: they go to the exact int32 kernel.
+template <int W>
 __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
+    using G = BandGeo<W>;
+    constexpr int kBL = G::L, kCapBytes = G::CapBytes;
+    auto give_up = [&](long long rd, bool retry) {
+        if (W < kBandDiags && retry) a.redo_list[atomicAdd(a.redo_count, 1)] = (int32_t)rd;
+        else a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+    };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int La = a.La, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
@@ -662,7 +683,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         n0 = ((const int4*)rg)[0];
         n1 = ((const int4*)rg)[1];
         n2 = ((const int4*)rg)[2];
-        ncw = lane < kBandDiags ? ((const unsigned*)(rg + kHdrBytes))[lane] : 0u;
+        ncw = lane < W ? ((const unsigned*)(rg + kHdrBytes))[lane] : 0u;
     };
     long long k = klo + (long long)blockIdx.x * wpb + wave;
     if (k < khi) prefetch(k);
@@ -679,8 +700,8 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; a.stats[rd] = z; }
             continue;
         }
-        if (hdr.z & kPairInactive) {   // unequal lengths, too long, or outside the band's reach
-            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+        if (hdr.z & kPairInactive) {   // too long, or the pair's lengths do not fit the band
+            if (lane == 0) give_up(rd, true);
             continue;
         }
         const int dlo = hdr.y;
@@ -698,7 +719,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const int tau0 = hdr.x;
         // start cell: the last cell of each band diagonal is on the last row or column
         unsigned k32 = 0u;
-        if (lane < kBandDiags) {
+        if (lane < W) {
             const int d = dlo + lane;
             const int iend = La < Lb - d ? La : Lb - d;
             const int ilo = 1 - d > 1 ? 1 - d : 1;
@@ -712,13 +733,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         int score, ei, ej;
         decode_end(end_key_widen(wave_max_u32(k32)), La, Lb, &score, &ei, &ej);
         // certificate: every alignment leaving the band scores <= UB < score
-        const int dhi = dlo + kBandDiags - 1;
+        const int dhi = dlo + W - 1;
         int pmax = -1;
         if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
         if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
         const bool certified = pmax < 0 || score > a.band_maxsub * pmax;
-        if ((hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) || !certified) {
-            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+        const bool bad_code = (hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) != 0;
+        if (bad_code || !certified) {
+            if (lane == 0) give_up(rd, !bad_code);   // IUPAC codes: no band helps
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             continue;
         }
@@ -729,10 +751,10 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const int nw_max = a.band_words - 1;
         auto code_at = [&](int ai, int bjj) -> unsigned {
             const int kd = bjj - ai - dlo;
-            const unsigned oob = (unsigned)kd >= (unsigned)kBandDiags ? 16u : 0u;
+            const unsigned oob = (unsigned)kd >= (unsigned)W ? 16u : 0u;
             const int tau = ai + bjj + tb0;
             const int wi = min(max(tau >> 2, 0), nw_max);
-            const unsigned w = bits[wi * kBL + ((kd & (kBandDiags - 1)) >> 1)];
+            const unsigned w = bits[wi * kBL + ((kd & (W - 1)) >> 1)];
             const int s = tau & 3;
             const int hb = 8 * h + s, lb = 8 * h + 4 + s;
             const unsigned yop = (w >> hb) & 1u, xgy = (w >> lb) & 1u;
@@ -742,7 +764,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const int nruns = band_walk_runs<NW_BAND_WALK_CPL>(code_at, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
-            if (lane == 0) a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
+            if (lane == 0) give_up(rd, true);
             continue;
         }
         lds_fence();
@@ -754,18 +776,21 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
 }
 
 // ---- host-side helpers -------------------------------------------------------
-int band_fill_lds_bytes(int La, int wpb) {
-    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * band_pcs(La);
+int band_fill_lds_bytes(int La, int wpb, int W) {
+    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La);
 }
 int band_walk_lds_bytes(int La, int wpb) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(); }
 int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }
-int64_t band_region_bytes(int La, int Lb_max) { return band_region_stride(La, Lb_max); }
+int64_t band_region_bytes(int La, int Lb_max, int W) { return band_region_stride(La, Lb_max, W); }
 bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb, dlo); }
 
-hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(fill_blocks, nw_band_fill, 64 * fill_wpb, fill_lds);
+hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
+                          int* walk_blocks) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        fill_blocks, W == 16 ? (const void*)nw_band_fill<16> : (const void*)nw_band_fill<32>, 64 * fill_wpb, fill_lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(walk_blocks, nw_band_walk, 64 * walk_wpb, walk_lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        walk_blocks, W == 16 ? (const void*)nw_band_walk<16> : (const void*)nw_band_walk<32>, 64 * walk_wpb, walk_lds);
 }
 
 // a.sort_hist holds (band_lb_cap + 3) * (grid + 1) ints: the count table, then the bucket
@@ -782,13 +807,19 @@ hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_band(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {
-    hipLaunchKernelGGL(nw_band_fill, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    if (W == 16)
+        hipLaunchKernelGGL(nw_band_fill<16>, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL(nw_band_fill<32>, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nw_band_walk, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    if (W == 16)
+        hipLaunchKernelGGL(nw_band_walk<16>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL(nw_band_walk<32>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     return hipGetLastError();
 }
 

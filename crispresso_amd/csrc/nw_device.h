@@ -64,7 +64,10 @@ struct KernelArgs {
     const uint32_t* rowpos;        // [La] codes each amplicon row scores > 0 against (markup ':')
     int32_t* sort_hist;            // [band_lb_cap + 3][sort grid + 1] per-block bucket counts, bucket bases
     int32_t* sort_key;             // [n] bucket of every read: length, band_lb_cap + 1 (longer), + 2 (exact copy)
-    const int32_t* band_count;     // device: sorted reads that need the DP (the exact copies follow)
+    const int32_t* band_count;     // device: entries of band_order to align (sorted reads that need the DP,
+                                   // or the previous level's redo count)
+    int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
+    int32_t* redo_count;
 };
 
 // Traceback storage of a kernel instantiation.
@@ -114,14 +117,15 @@ hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, 
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
 constexpr int kBandDiags = 32;
-int band_fill_lds_bytes(int La, int wpb);
+int band_fill_lds_bytes(int La, int wpb, int W);
 int band_walk_lds_bytes(int La, int wpb);
 int band_region_words(int La, int Lb_max);
-int64_t band_region_bytes(int La, int Lb_max);
+int64_t band_region_bytes(int La, int Lb_max, int W);
 bool band_pair_geometry(int La, int Lb, int* dlo);
-hipError_t band_occupancy(int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks, int* walk_blocks);
+hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
+                          int* walk_blocks);
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
-hipError_t launch_band(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
+hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
 
 }  // namespace nw

@@ -122,7 +122,10 @@ struct nw_ctx {
     // certified diagonal-band kernels (nw_band.hip): the default path
     bool amp_in_table = false;         // amplicon within A C G T N / unknown (the band score table)
     bool use_diag = false;
-    nw::LaunchCfg diag_fill{}, diag_walk{};
+    nw::LaunchCfg diag_fill{}, diag_walk{};          // 32-diagonal level (the certificate's last resort)
+    nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
+    int64_t diag16_pass_pairs = 0, diag16_stride = 0;
+    DevBuf<int32_t> d_redo;                          // reads the first level could not certify
     DevBuf<uint32_t> d_btab, d_rowpos;
     DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
     DevBuf<uint8_t> d_bregion;
@@ -348,37 +351,50 @@ int configure(nw_ctx* c) {
     const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
     if (want_diag && c->amp_in_table && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
         c->gap_open >= c->gap_extend) {
-        nw::LaunchCfg f{}, w{};
-        f.R = w.R = R;
-        f.tb_mode = w.tb_mode = nw::TB_DIAG;
-        f.wpb = 8;
-        w.wpb = 8;
-        f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb);
-        w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb);
-        int fb = 0, wb = 0;
-        if (f.lds_bytes <= kMaxLds && w.lds_bytes <= kMaxLds)
-            HIP_OR_FAIL(c, nw::band_occupancy(f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb));
-        if (fb > 0 && wb > 0) {
-            const int64_t pairs = (c->n + 1) / 2;
-            c->diag_lb_cap = La + nw::kBandDiags - 1;
-            c->diag_words = nw::band_region_words(La, c->lb_max);
-            c->diag_stride = nw::band_region_bytes(La, c->lb_max);
-            int64_t cap_bytes = 16ll << 30;
-            if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
-            c->diag_pass_pairs = std::max<int64_t>(4, std::min<int64_t>(pairs, cap_bytes / c->diag_stride));
-            c->diag_pass_pairs = (c->diag_pass_pairs + 3) & ~(int64_t)3;
-            const int64_t pass_pairs = std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs);
-            f.grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pass_pairs + 3) / 4 + f.wpb - 1) / f.wpb,
+        const int64_t pairs = (c->n + 1) / 2;
+        int64_t cap_bytes = 16ll << 30;
+        if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
+        c->diag_lb_cap = La + nw::kBandDiags - 1;
+        c->diag_words = nw::band_region_words(La, c->lb_max);
+        // one level: fill + walk launch configs, region stride and pairs per pass
+        auto level = [&](int W, nw::LaunchCfg& f, nw::LaunchCfg& w, int64_t& stride, int64_t& pass_pairs) -> int {
+            f = nw::LaunchCfg{};
+            w = nw::LaunchCfg{};
+            f.R = w.R = R;
+            f.tb_mode = w.tb_mode = nw::TB_DIAG;
+            f.wpb = 8;
+            w.wpb = 8;
+            f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb, W);
+            w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb);
+            int fb = 0, wb = 0;
+            if (f.lds_bytes > kMaxLds || w.lds_bytes > kMaxLds) return 0;
+            if (nw::band_occupancy(W, f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb) != hipSuccess || fb <= 0 ||
+                wb <= 0)
+                return 0;
+            const int ppw = W == 16 ? 8 : 4;   // read pairs per wavefront
+            stride = nw::band_region_bytes(La, c->lb_max, W);
+            pass_pairs = std::max<int64_t>(ppw, std::min<int64_t>(pairs, cap_bytes / stride));
+            pass_pairs = (pass_pairs + ppw - 1) / ppw * ppw;
+            const int64_t pp = std::min<int64_t>(std::max<int64_t>(pairs, 1), pass_pairs);
+            f.grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pp + ppw - 1) / ppw + f.wpb - 1) / f.wpb,
                                                                  (int64_t)c->num_cus * fb));
-            w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((2 * pass_pairs + w.wpb - 1) / w.wpb,
-                                                                 (int64_t)c->num_cus * wb));
+            w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((2 * pp + w.wpb - 1) / w.wpb, (int64_t)c->num_cus * wb));
+            return 1;
+        };
+        const char* w16 = std::getenv("CRISPR_NW_DIAG16");   // "0": 32-diagonal level only
+        const bool use16 = !(w16 && std::strcmp(w16, "0") == 0) &&
+                           level(16, c->diag16_fill, c->diag16_walk, c->diag16_stride, c->diag16_pass_pairs);
+        if (!use16) c->diag16_fill.grid = 0;
+        if (level(32, c->diag_fill, c->diag_walk, c->diag_stride, c->diag_pass_pairs)) {
             c->diag_sort_grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 1023) / 1024, 1024));
-            HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)(pass_pairs * c->diag_stride)));
+            const int64_t rbytes = std::max(std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs) * c->diag_stride,
+                                            use16 ? std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag16_pass_pairs) *
+                                                        c->diag16_stride : 0);
+            HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)rbytes));
             HIP_OR_FAIL(c, c->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
             HIP_OR_FAIL(c, c->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            c->diag_fill = f;
-            c->diag_walk = w;
             c->use_diag = true;
         }
     }
@@ -463,7 +479,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
     c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
-    c->d_btab.release(); c->d_rowpos.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
+    c->d_btab.release(); c->d_rowpos.release(); c->d_redo.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -608,12 +624,31 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->stream));
         const int64_t pairs = (c->n + 1) / 2;
-        for (int64_t lo = 0; lo < pairs; lo += c->diag_pass_pairs) {
-            nw::KernelArgs ap = a;
-            ap.band_pair_lo = lo;
-            ap.band_pair_hi = std::min(pairs, lo + c->diag_pass_pairs);
-            HIP_OR_FAIL(c, nw::launch_band(ap, c->diag_fill, c->diag_walk, c->stream, lo == 0 ? c->ev_fill : nullptr));
-            if (lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+        // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
+        // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
+        // ranges to the device-side counts.
+        const bool two = c->diag16_fill.grid > 0;
+        a.redo_list = c->d_redo.p;
+        a.redo_count = c->d_fallback_count.p + 2;
+        for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
+            nw::KernelArgs al = a;
+            const int W = lvl == 0 ? 16 : 32;
+            if (lvl == 1 && two) {
+                al.band_order = c->d_redo.p;
+                al.band_count = a.redo_count;
+            }
+            al.band_stride = lvl == 0 ? c->diag16_stride : c->diag_stride;
+            const int64_t pp = lvl == 0 ? c->diag16_pass_pairs : c->diag_pass_pairs;
+            const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
+            const nw::LaunchCfg& wc = lvl == 0 ? c->diag16_walk : c->diag_walk;
+            const bool first = lvl == (two ? 0 : 1);
+            for (int64_t lo = 0; lo < pairs; lo += pp) {
+                nw::KernelArgs ap = al;
+                ap.band_pair_lo = lo;
+                ap.band_pair_hi = std::min(pairs, lo + pp);
+                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->stream, first && lo == 0 ? c->ev_fill : nullptr));
+                if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+            }
         }
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
         a.work_count = c->d_fallback_count.p;

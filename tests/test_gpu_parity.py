@@ -443,3 +443,25 @@ def test_diag_exact_copies(gpu_aligner_factory, oracle):
     a.set_reference(amp_n)
     buf, off = pack_reads([amp_n, amp_n.lower(), amp] * 3)
     assert_same(oracle, amp_n, buf, off, a.align_packed(buf, off), "exact-N")
+
+
+@pytest.mark.parametrize("levels", ["16+32", "32"])
+def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
+    """The 16-diagonal first level hands what it cannot certify (indels of 8+,
+    noisy and junk reads) to the 32-diagonal level, which hands the rest to the
+    exact kernel; with the first level off the 32-diagonal level sees every read."""
+    if levels == "32":
+        monkeypatch.setenv("CRISPR_NW_DIAG16", "0")
+    amp = synth.random_amplicon(250, 44)
+    rng = np.random.Generator(np.random.PCG64(45))
+    reads = synth.unpack(*synth.reads_from(amp, 1500, 46, synth.PARITY_MIX))
+    for g in (6, 9, 14, 17, 24, 29, 35):      # deletions around both bands' reach
+        p = int(rng.integers(30, 200))
+        reads += [amp[:p] + amp[p + g:]] * 3
+        reads += [amp[:p] + synth.random_amplicon(g, g) + amp[p:]] * 2
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.geometry()["tb_mode"] == "diag-int16"
+    assert_same(oracle, amp, buf, off, batch, f"levels={levels}")
