@@ -88,7 +88,7 @@ def pmc_traffic(*prefixes, required=None):
                 summ = json.load(f)
         except (OSError, ValueError):
             continue
-        if required and not any(k.startswith(required) for k in summ):
+        if required and not any(required in k for k in summ):
             continue
         vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
                 if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
@@ -248,7 +248,7 @@ def main():
     diag = geo["tb_mode"].startswith("diag")
     if diag:
         traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                           required="nw::nw_band_fill")
+                                           required="nw::nw_band_fill<16>")
     elif geo["tb_mode"].startswith("stream"):
         traffic, traffic_src = pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk", "void nw::nw_align_kernel",
                                            required="void nw::nw_stream_fill")
@@ -287,8 +287,9 @@ def main():
                 "traffic": traffic,
                 "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench "
                                   "command, per launch of fill + walk + fallback)",
-                "kernel": ("nw_band_hist/scan/scatter (length sort) + nw_band_fill + nw_band_walk "
-                           "(certified 32-diagonal band) + nw_align_kernel on the uncertified reads" if diag
+                "kernel": ("nw_band_classify (exact copies, no DP) + length sort + nw_band_fill<16> + "
+                           "nw_band_walk<16> (certified 16-diagonal band) + nw_band_fill/walk<32> on its redo list "
+                           "+ nw_align_kernel on what neither band certifies" if diag
                            else f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
                            if geo["tb_mode"].startswith("stream")
                            else f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>"),
@@ -302,7 +303,8 @@ def main():
                     "gcups": gcups,
                     "cells_per_launch": cells,
                     "note": ("gcups counts the full La x Lb matrix of every read (the work the reference's needle "
-                             "does); the certified band computes 32 diagonals per read and proves the rest cannot "
+                             "does); the certified bands compute 16 (or 32) diagonals per read, exact copies none, and "
+                             "prove the rest cannot "
                              "change the result (DESIGN.md §4)" if diag else
                              "the DP is a dependent integer recurrence: VALU-bound, HBM frac is small by construction"),
                 },

@@ -127,7 +127,7 @@ template <int W> struct BandGeo {
 };
 constexpr int kBK = 64;               // tau = t - dlo + kBK: >= 0 and even
 constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [-17, La + 48]
-constexpr int kJPad = 96;             // pair codes: index j + kJPad, j in [-79, La + 79]
+constexpr int kJPad = 95;             // pair codes: index j + kJPad, j in [-48, La + 80]; j = 1 is 4-aligned
 constexpr int kPadCode = 5;           // lut6: A T G C N pad
 constexpr int kTabBytes = 896;        // [6][36] packed scores (864 B)
 constexpr int kHdrBytes = 48;         // {tau0, dlo, flags, -}, {ra, rb, LbA, LbB}, {offA, offB}
@@ -345,8 +345,11 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
     uint32_t* tab = (uint32_t*)smem;
     uint16_t* acd = (uint16_t*)(smem + kTabBytes);
     const int PCS = band_pcs(La);
-    unsigned char* pcd = smem + kTabBytes + align16(2 * band_acd_elems(La)) + (wave * kBPW + grp) * PCS;
+    unsigned char* pcd_wave = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wave * kBPW * PCS;
+    unsigned char* pcd = pcd_wave + grp * PCS;
+    unsigned char* lut6 = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * PCS;
     for (int k = tid; k < 216; k += blockDim.x) tab[k] = a.band_tab[k];
+    for (int k = tid; k < 256; k += blockDim.x) lut6[k] = a.lut6[k];
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
         const int i = k - kAPad;   // row i = amplicon residue i - 1
         const int c = (i >= 1 && i <= La) ? a.lut6[a.amp[i - 1]] : kPadCode;   // host: amplicon codes <= 5
@@ -392,23 +395,61 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         }
         const int Lmax = max(LbA, LbB);
 
-        // pair codes of the group's columns (j = 1..Lb real, the rest pad)
-        bool badA = false, badB = false;
-        for (int k = q; k < PCS; k += kBL) {
-            const int j = k - kJPad;
-            int cA = kPadCode, cB = kPadCode;
-            if (j >= 1 && j <= Lmax) {
-                cA = j <= LbA ? a.lut6[a.reads[offA + j - 1]] : kPadCode;
-                cB = j <= LbB ? a.lut6[a.reads[offB + j - 1]] : kPadCode;
-                // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
-                if (cA > kPadCode) { badA = true; cA = kPadCode; }
-                if (cB > kPadCode) { badB = true; cB = kPadCode; }
+        // pair codes of the wavefront's pairs' columns (j = 1..Lb real, the rest pad):
+        // all 64 lanes stage one pair at a time, 4 columns per lane from coalesced dword
+        // loads of both reads (all pairs' loads issued before any is used)
+        for (int k4 = lane; k4 < kBPW * PCS / 4; k4 += 64) ((unsigned*)pcd_wave)[k4] = 0x8c8c8c8cu;   // pad pair
+        const int Lw = (int)wave_max_u32((unsigned)Lmax);
+        unsigned bad_mask = 0u;   // bit p: pair p has a read A / B code outside A C G T N (bits 0-15 / 16-31)
+        for (int c0 = 0; c0 < Lw; c0 += 256) {
+            const int k4 = (c0 >> 2) + lane;
+            unsigned wA[kBPW], wB[kBPW];
+            int lenA[kBPW], lenB[kBPW];
+#pragma unroll
+            for (int p = 0; p < kBPW; ++p) {
+                const int src = (p / G::PR) * 16 + p % G::PR;   // lane q = 0 of pair p
+                const unsigned oAl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offA, src);
+                const unsigned oAh = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(offA >> 32), src);
+                const unsigned oBl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offB, src);
+                const unsigned oBh = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(offB >> 32), src);
+                lenA[p] = __builtin_amdgcn_readlane(LbA, src);
+                lenB[p] = __builtin_amdgcn_readlane(LbB, src);
+                const long long oA = (long long)(((unsigned long long)oAh << 32) | oAl);
+                const long long oB = (long long)(((unsigned long long)oBh << 32) | oBl);
+                wA[p] = wB[p] = 0u;
+                if (4 * k4 < lenA[p]) {
+                    const uint8_t* b = a.reads + (oA & ~3ll) + 4 * k4;
+                    wA[p] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oA & 3));
+                }
+                if (4 * k4 < lenB[p]) {
+                    const uint8_t* b = a.reads + (oB & ~3ll) + 4 * k4;
+                    wB[p] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oB & 3));
+                }
             }
-            pcd[k] = (unsigned char)((cA * 6 + cB) * 4);
+#pragma unroll
+            for (int p = 0; p < kBPW; ++p) {
+                const int Lm = max(lenA[p], lenB[p]);
+                if (4 * k4 >= Lm) continue;
+                unsigned packed = 0u;
+                bool bA = false, bB = false;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int j0 = 4 * k4 + b;   // 0-based column
+                    int cA = j0 < lenA[p] ? lut6[(wA[p] >> (8 * b)) & 0xffu] : kPadCode;
+                    int cB = j0 < lenB[p] ? lut6[(wB[p] >> (8 * b)) & 0xffu] : kPadCode;
+                    // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
+                    bA = bA || cA > kPadCode;
+                    bB = bB || cB > kPadCode;
+                    cA = min(cA, kPadCode);
+                    cB = min(cB, kPadCode);
+                    packed |= (unsigned)((cA * 6 + cB) * 4) << (8 * b);
+                }
+                *(unsigned*)(pcd_wave + p * PCS + kJPad + 1 + 4 * k4) = packed;
+                if (__ballot(bA)) bad_mask |= 1u << p;
+                if (__ballot(bB)) bad_mask |= 1u << (16 + p);
+            }
         }
-        const unsigned long long bA = __ballot(badA), bB = __ballot(badB);
-        const unsigned long long gmask = (unsigned long long)G::RowMask << ((lane & ~15) + (lane & 15) % G::PR);
-        const int flags = ((bA & gmask) ? REGION_BAD_A : 0) | ((bB & gmask) ? REGION_BAD_B : 0);
+        const int flags = (((bad_mask >> grp) & 1u) ? REGION_BAD_A : 0) | (((bad_mask >> (16 + grp)) & 1u) ? REGION_BAD_B : 0);
 
         // wave-uniform tau range; per lane: boundary and capture steps
         const unsigned tlo = act ? (unsigned)(kBK - dlo) : 0xffffffffu;
@@ -777,7 +818,8 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
 
 // ---- host-side helpers -------------------------------------------------------
 int band_fill_lds_bytes(int La, int wpb, int W) {
-    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La);
+    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La) +
+           256;
 }
 int band_walk_lds_bytes(int La, int wpb) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(); }
 int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }
