@@ -680,6 +680,113 @@ __device__ int band_walk_runs(const Code& code_at, int La, int Lb, int ei, int e
     return full ? -1 : nruns;
 }
 
+// band_walk_runs specialised per run type (the state is wave-uniform, so each round
+// takes one scalar branch): an M run follows one diagonal (its band membership is
+// uniform, tau falls by 2 per cell); X / Y runs move along a row / column.  Each
+// lane tests CPL cells; the round's first stop is found with one ballot.  `word(tau,
+// kd)` returns the band dword of anti-diagonal step tau (relative to the stored
+// range) and band diagonal kd; bit positions of read h at sub-step s: Y opens hb,
+// X > Y hb + 4, X opens 16 + hb, M < max(X, Y) 20 + hb, with hb = 8 h + s.
+template <int CPL, int W, class Word>
+__device__ int band_walk_runs2(const Word& word, int La, int Lb, int ei, int ej, int dlo, int tb0, int h,
+                               unsigned* runs, int cap, int lane) {
+    int nruns = 0, last_type = -1;
+    bool full = false;
+    auto push = [&](int type, int n) {
+        if (n <= 0) return;
+        if (type == last_type) {
+            if (lane == 0) runs[nruns - 1] += (unsigned)n;
+        } else if (nruns < cap) {
+            if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
+            ++nruns;
+            last_type = type;
+        } else {
+            full = true;
+        }
+    };
+    if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
+    else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
+    constexpr int WR = 64 * CPL;
+    int i = __builtin_amdgcn_readfirstlane(ei), j = __builtin_amdgcn_readfirstlane(ej), state = RUN_M;
+    const int hb = 8 * h;
+    while (i > 0 && j > 0) {
+        int k0;            // cells of the current run before the stop (the run is k0 + 1 long)
+        int nb = RUN_M;    // M runs: the state the stop cell continues in
+        if (state == RUN_M) {
+            // cells (i-1-k, j-1-k), 1-based; diagonal kd = j - i - dlo for all of them
+            const int kd = j - i - dlo;
+            if ((unsigned)kd >= (unsigned)W) return -1;
+            const int lim = min(i, j) - 1;          // k < lim: cell inside the matrix
+            const int t0 = i + j - 4 + tb0;         // tau of cell k = 0
+            unsigned stop = 0u, xgy = 0u;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int kk = lane * CPL + u;
+                const int tau = t0 - 2 * kk;
+                const unsigned w = word(max(tau, 0), kd);
+                const int sh = hb + (tau & 3);
+                const bool nm = ((w >> (20 + sh)) & 1u) != 0u;
+                stop |= (unsigned)(kk >= lim || nm) << u;
+                xgy |= ((w >> (4 + sh)) & 1u) << u;
+            }
+            const unsigned long long m = __ballot(stop != 0u);
+            if (m == 0) {
+                push(RUN_M, WR);
+                i -= WR;
+                j -= WR;
+                continue;
+            }
+            const int L = (int)__builtin_ctzll(m);
+            const unsigned sL = (unsigned)__builtin_amdgcn_readlane((int)stop, L);
+            const int u0 = (int)__builtin_ctz(sL);
+            k0 = L * CPL + u0;
+            nb = (((unsigned)__builtin_amdgcn_readlane((int)xgy, L) >> u0) & 1u) ? RUN_X : RUN_Y;
+            push(RUN_M, k0 + 1);
+            i -= k0 + 1;
+            j -= k0 + 1;
+            state = nb;
+        } else {
+            // X: cells (i, j-k), diagonal kd = j - k - i - dlo; Y: cells (i-k, j), kd = j - i + k - dlo
+            const bool isX = state == RUN_X;
+            const int lim = isX ? j : i;             // k < lim: inside the matrix
+            const int kd0 = j - i - dlo;
+            const int t0 = i + j - 2 + tb0;          // tau of cell k = 0
+            const int bit = isX ? 16 : 0;            // "opens" bit of the run's gap type
+            unsigned stop = 0u, oob = 0u;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int kk = lane * CPL + u;
+                const int kd = isX ? kd0 - kk : kd0 + kk;
+                const int tau = t0 - kk;
+                const bool out = (unsigned)kd >= (unsigned)W;
+                const unsigned w = word(max(tau, 0), kd & (W - 1));
+                const bool opens = ((w >> (bit + hb + (tau & 3))) & 1u) != 0u;
+                const bool valid = kk < lim;
+                stop |= (unsigned)(!valid || out || opens) << u;
+                oob |= (unsigned)(valid && out) << u;
+            }
+            const unsigned long long m = __ballot(stop != 0u);
+            if (m == 0) {
+                push(state, WR);
+                if (isX) j -= WR; else i -= WR;
+                continue;
+            }
+            const int L = (int)__builtin_ctzll(m);
+            const unsigned sL = (unsigned)__builtin_amdgcn_readlane((int)stop, L);
+            const int u0 = (int)__builtin_ctz(sL);
+            if (((unsigned)__builtin_amdgcn_readlane((int)oob, L) >> u0) & 1u) return -1;
+            k0 = L * CPL + u0;
+            push(state, k0 + 1);
+            if (isX) j -= k0 + 1; else i -= k0 + 1;
+            state = RUN_M;
+        }
+        if (full) return -1;
+    }
+    if (i > 0) push(RUN_Y, i);
+    if (j > 0) push(RUN_X, j);
+    return full ? -1 : nruns;
+}
+
 constexpr int kBandReadCap = 1024;
 __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
 __host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 4 + kBandReadCap + 256; }
@@ -787,22 +894,9 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
         const int tb0 = kBK - dlo + 2 - tau0;
-        // 4-bit cell code of 0-based cell (ai, bjj), bit 4 = outside the band; branch-free
-        // (cells that are not tested read a clamped, harmless word)
         const int nw_max = a.band_words - 1;
-        auto code_at = [&](int ai, int bjj) -> unsigned {
-            const int kd = bjj - ai - dlo;
-            const unsigned oob = (unsigned)kd >= (unsigned)W ? 16u : 0u;
-            const int tau = ai + bjj + tb0;
-            const int wi = min(max(tau >> 2, 0), nw_max);
-            const unsigned w = bits[wi * kBL + ((kd & (W - 1)) >> 1)];
-            const int s = tau & 3;
-            const int hb = 8 * h + s, lb = 8 * h + 4 + s;
-            const unsigned yop = (w >> hb) & 1u, xgy = (w >> lb) & 1u;
-            const unsigned xop = (w >> (16 + hb)) & 1u, notm = (w >> (16 + lb)) & 1u;
-            return notm | (xgy << 1) | (xop << 2) | (yop << 3) | oob;
-        };
-        const int nruns = band_walk_runs<NW_BAND_WALK_CPL>(code_at, La, Lb, ei, ej, runs, kStreamRunsCap, lane);
+        auto word = [&](int tau, int kd) -> unsigned { return bits[min(tau >> 2, nw_max) * kBL + (kd >> 1)]; };
+        const int nruns = band_walk_runs2<NW_BAND_WALK_CPL, W>(word, La, Lb, ei, ej, dlo, tb0, h, runs, kStreamRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
             if (lane == 0) give_up(rd, true);
