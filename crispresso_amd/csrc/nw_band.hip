@@ -192,15 +192,20 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
         unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
         unsigned long long exact = 0ull;
-        // compare 4 candidates at a time (their loads in flight together)
+        // compare 4 candidates at a time (their loads in flight together); when the read
+        // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
+        // away from the words already in registers
+        const bool one_chunk = nd <= 64;
+        unsigned long long emit_later = 0ull;
         while (cand) {
             int us[4];
-            unsigned diff[4];
+            unsigned diff[4], raw[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 us[t] = cand ? (int)__builtin_ctzll(cand) : -1;
                 if (cand) cand &= cand - 1;
                 diff[t] = 0u;
+                raw[t] = 0u;
             }
             for (int c0 = 0; c0 < nd; c0 += 64) {
                 const int k4 = c0 + lane;
@@ -211,21 +216,38 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), us[t]);
                     const long long off = (long long)(((unsigned long long)hi << 32) | lo);
                     const uint8_t* base = a.reads + (off & ~3ll) + 4 * k4;
-                    const unsigned w = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off & 3)) | 0x20202020u;
-                    diff[t] |= (w ^ amp_sh[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
+                    raw[t] = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off & 3));
+                    diff[t] |= ((raw[t] | 0x20202020u) ^ amp_sh[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
                 }
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (us[t] >= 0 && __ballot(diff[t] != 0u) == 0ull) exact |= 1ull << us[t];
+            for (int t = 0; t < 4; ++t) {
+                if (us[t] < 0 || __ballot(diff[t] != 0u) != 0ull) continue;
+                exact |= 1ull << us[t];
+                if (!one_chunk) {
+                    emit_later |= 1ull << us[t];
+                    continue;
+                }
+                unsigned* o = (unsigned*)(a.out + (r0 + us[t]) * 3 * a.stride);
+                if (lane < nd) {
+                    o[lane] = amp_sh[nd + lane];
+                    o[sd + lane] = 0x7c7c7c7cu;   // '|'
+                    o[2 * sd + lane] = raw[t];
+                }
+                if (lane < 8) {
+                    // the record (nw::Stat): aln_len, n_ident, n_sim, n_gaps, score, end_i, end_j, flags
+                    const int v = lane == 3 || lane == 7 ? 0 : (lane == 4 ? a.band_maxsub * La : La);
+                    ((int*)(a.stats + r0 + us[t]))[lane] = v;
+                }
+            }
         }
         if (r < a.n)
             a.sort_key[r] = ((exact >> lane) & 1ull) ? a.band_lb_cap + 2 : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
-        // the diagonal of every exact copy: amplicon, '|' markup, read; rows as dwords up to
-        // round4(La) (within the row stride)
-        while (exact) {
-            const int u = (int)__builtin_ctzll(exact);
-            exact &= exact - 1;
+        // the diagonal of every exact copy longer than one chunk: amplicon, '|' markup,
+        // read; rows as dwords up to round4(La) (within the row stride)
+        while (emit_later) {
+            const int u = (int)__builtin_ctzll(emit_later);
+            emit_later &= emit_later - 1;
             const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
             const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
             const long long off = (long long)(((unsigned long long)hi << 32) | lo);
