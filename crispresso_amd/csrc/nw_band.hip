@@ -423,42 +423,46 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         for (int k4 = lane; k4 < kBPW * PCS / 4; k4 += 64) ((unsigned*)pcd_wave)[k4] = 0x8c8c8c8cu;   // pad pair
         const int Lw = (int)wave_max_u32((unsigned)Lmax);
         unsigned bad_mask = 0u;   // bit p: pair p has a read A / B code outside A C G T N (bits 0-15 / 16-31)
-        for (int c0 = 0; c0 < Lw; c0 += 256) {
+        constexpr int kSub = kBPW < 4 ? kBPW : 4;   // pairs staged together (loads in flight)
+        for (int c0 = 0; c0 < Lw; c0 += 256)
+        for (int p0 = 0; p0 < kBPW; p0 += kSub) {
             const int k4 = (c0 >> 2) + lane;
-            unsigned wA[kBPW], wB[kBPW];
-            int lenA[kBPW], lenB[kBPW];
+            unsigned wA[kSub], wB[kSub];
+            int lenA[kSub], lenB[kSub];
 #pragma unroll
-            for (int p = 0; p < kBPW; ++p) {
+            for (int pp = 0; pp < kSub; ++pp) {
+                const int p = p0 + pp;
                 const int src = (p / G::PR) * 16 + p % G::PR;   // lane q = 0 of pair p
                 const unsigned oAl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offA, src);
                 const unsigned oAh = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(offA >> 32), src);
                 const unsigned oBl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offB, src);
                 const unsigned oBh = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(offB >> 32), src);
-                lenA[p] = __builtin_amdgcn_readlane(LbA, src);
-                lenB[p] = __builtin_amdgcn_readlane(LbB, src);
+                lenA[pp] = __builtin_amdgcn_readlane(LbA, src);
+                lenB[pp] = __builtin_amdgcn_readlane(LbB, src);
                 const long long oA = (long long)(((unsigned long long)oAh << 32) | oAl);
                 const long long oB = (long long)(((unsigned long long)oBh << 32) | oBl);
-                wA[p] = wB[p] = 0u;
-                if (4 * k4 < lenA[p]) {
+                wA[pp] = wB[pp] = 0u;
+                if (4 * k4 < lenA[pp]) {
                     const uint8_t* b = a.reads + (oA & ~3ll) + 4 * k4;
-                    wA[p] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oA & 3));
+                    wA[pp] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oA & 3));
                 }
-                if (4 * k4 < lenB[p]) {
+                if (4 * k4 < lenB[pp]) {
                     const uint8_t* b = a.reads + (oB & ~3ll) + 4 * k4;
-                    wB[p] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oB & 3));
+                    wB[pp] = __builtin_amdgcn_alignbyte(*(const unsigned*)(b + 4), *(const unsigned*)b, (int)(oB & 3));
                 }
             }
 #pragma unroll
-            for (int p = 0; p < kBPW; ++p) {
-                const int Lm = max(lenA[p], lenB[p]);
+            for (int pp = 0; pp < kSub; ++pp) {
+                const int p = p0 + pp;
+                const int Lm = max(lenA[pp], lenB[pp]);
                 if (4 * k4 >= Lm) continue;
                 unsigned packed = 0u;
                 bool bA = false, bB = false;
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     const int j0 = 4 * k4 + b;   // 0-based column
-                    int cA = j0 < lenA[p] ? lut6[(wA[p] >> (8 * b)) & 0xffu] : kPadCode;
-                    int cB = j0 < lenB[p] ? lut6[(wB[p] >> (8 * b)) & 0xffu] : kPadCode;
+                    int cA = j0 < lenA[pp] ? lut6[(wA[pp] >> (8 * b)) & 0xffu] : kPadCode;
+                    int cB = j0 < lenB[pp] ? lut6[(wB[pp] >> (8 * b)) & 0xffu] : kPadCode;
                     // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
                     bA = bA || cA > kPadCode;
                     bB = bB || cB > kPadCode;
