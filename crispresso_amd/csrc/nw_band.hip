@@ -42,8 +42,10 @@
 //     the score table; Mo = M - (O - E);
 //   * 4 traceback bits per cell and read, 4 steps per dword: the same byte-plane
 //     packing as the stream kernels; per pair region: header, the M of each
-//     diagonal's last cell (= the last row / last column cells), bits
-//     [words][16 lanes];
+//     diagonal's last cell (= the last row / last column cells), bits in tiles
+//     [words / 4][lanes][4 words]: the fill writes 16 steps of a pair's lanes as one
+//     contiguous dwordx4 row, an M run of the walk reads 16 steps of its diagonal
+//     pair with one dwordx4 per lane;
 //   * nw_band_walk: one wavefront per read: start cell from the 32 captures,
 //     certificate, the run-based walk of nw_common.h over the band, strings.
 #include <hip/hip_runtime.h>
@@ -140,7 +142,7 @@ __host__ __device__ inline int band_pcs(int La) { return align16(La + kJPad + 96
 
 __host__ __device__ inline int band_words(int La, int Lb_max) {
     const int Lbm = Lb_max < La + kBandDiags - 1 ? Lb_max : La + kBandDiags - 1;
-    return (La + Lbm + 80) / 4 + 2;
+    return (((La + Lbm + 80) / 4 + 2) + 3) & ~3;   // column length: whole dwordx4 of the walk
 }
 __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W) {
     return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max) * (W / 2) * 4 + 255) & ~(int64_t)255;
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(256) void nw_band_scatter(const KernelArgs a) {
 // Fill
 // ============================================================================
 template <int W>
-__global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -370,6 +372,8 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
     unsigned char* pcd_wave = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wave * kBPW * PCS;
     unsigned char* pcd = pcd_wave + grp * PCS;
     unsigned char* lut6 = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * PCS;
+    // a tile row's four words per lane wait here (not in VGPRs) until its dwordx4 store
+    unsigned* stage = (unsigned*)(lut6 + 256) + wave * 256 + 4 * lane;
     for (int k = tid; k < 216; k += blockDim.x) tab[k] = a.band_tab[k];
     for (int k = tid; k < 256; k += blockDim.x) lut6[k] = a.lut6[k];
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
@@ -455,22 +459,25 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             for (int pp = 0; pp < kSub; ++pp) {
                 const int p = p0 + pp;
                 const int Lm = max(lenA[pp], lenB[pp]);
-                if (4 * k4 >= Lm) continue;
-                unsigned packed = 0u;
                 bool bA = false, bB = false;
+                if (4 * k4 < Lm) {
+                    unsigned packed = 0u;
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int j0 = 4 * k4 + b;   // 0-based column
-                    int cA = j0 < lenA[pp] ? lut6[(wA[pp] >> (8 * b)) & 0xffu] : kPadCode;
-                    int cB = j0 < lenB[pp] ? lut6[(wB[pp] >> (8 * b)) & 0xffu] : kPadCode;
-                    // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
-                    bA = bA || cA > kPadCode;
-                    bB = bB || cB > kPadCode;
-                    cA = min(cA, kPadCode);
-                    cB = min(cB, kPadCode);
-                    packed |= (unsigned)((cA * 6 + cB) * 4) << (8 * b);
+                    for (int b = 0; b < 4; ++b) {
+                        const int j0 = 4 * k4 + b;   // 0-based column
+                        int cA = j0 < lenA[pp] ? lut6[(wA[pp] >> (8 * b)) & 0xffu] : kPadCode;
+                        int cB = j0 < lenB[pp] ? lut6[(wB[pp] >> (8 * b)) & 0xffu] : kPadCode;
+                        // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
+                        bA = bA || cA > kPadCode;
+                        bB = bB || cB > kPadCode;
+                        cA = min(cA, kPadCode);
+                        cB = min(cB, kPadCode);
+                        packed |= (unsigned)((cA * 6 + cB) * 4) << (8 * b);
+                    }
+                    *(unsigned*)(pcd_wave + p * PCS + kJPad + 1 + 4 * k4) = packed;
                 }
-                *(unsigned*)(pcd_wave + p * PCS + kJPad + 1 + 4 * k4) = packed;
+                // ballots with every lane active: bad_mask must be the same in all lanes
+                // (pair p's header is written by its own q = 0 lane)
                 if (__ballot(bA)) bad_mask |= 1u << p;
                 if (__ballot(bB)) bad_mask |= 1u << (16 + p);
             }
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         // or column; blocks before it skip the capture selects
         const int te_lo = (int)wave_min_u32(min(min((unsigned)te[0], (unsigned)te[1]),
                                                 min((unsigned)teB[0], (unsigned)teB[1])));
-        unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + q;
+        unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q;   // this lane's slot of each tile
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
         unsigned cap0 = NEG2, cap1 = NEG2, capB0 = NEG2, capB1 = NEG2;   // read A's (low) / B's (high half)
@@ -601,8 +608,21 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
             step(tau4 + 1, I1{}, PROc, CAPc, cur, acc);
             step(tau4 + 2, I2{}, PROc, CAPc, cur, acc);
             step(tau4 + 3, I3{}, PROc, CAPc, cur, acc);
-            const int w = (tau4 - tau0) >> 2;
-            if (act && w < NW) bits[w * kBL] = acc;
+            return acc;
+        };
+        // four blocks = one tile row: words w .. w + 3 of every lane (w % 4 == 0)
+        // a block pair (8 steps) is half a tile row; its words wait in LDS and the
+        // second half stores the row (the phases may split a row: the stage carries it)
+        auto flush = [&](int tau4) {
+            asm volatile("" ::: "memory");
+            const int w = ((tau4 - tau0) >> 2) & ~3;
+            if (act && w < NW) *(uint4*)(bits + w * kBL) = *(const uint4*)stage;
+        };
+        auto pair8 = [&](int tau4, auto PROc, auto CAPc) {
+            const int h2 = ((tau4 - tau0) >> 2) & 2;
+            stage[h2] = block(tau4, PROc, CAPc, sc, sn);
+            stage[h2 + 1] = block(tau4 + 4, PROc, CAPc, sn, sc);
+            if (h2) flush(tau4);
         };
         // phases in whole block pairs (8 steps) from tau0: prologue (boundary cells,
         // captures of short reads), bulk, capture window to tau_end (may run up to 7
@@ -612,17 +632,15 @@ __global__ __launch_bounds__(512) void nw_band_fill(const KernelArgs a) {
         const int p2 = max(p1, tau0 + ((te_lo - tau0) & ~7));
         int tau4 = tau0;
         for (; tau4 < p1; tau4 += 8) {
-            block(tau4, std::true_type{}, std::true_type{}, sc, sn);
-            block(tau4 + 4, std::true_type{}, std::true_type{}, sn, sc);
+            pair8(tau4, std::true_type{}, std::true_type{});
         }
         for (; tau4 < p2; tau4 += 8) {
-            block(tau4, std::false_type{}, std::false_type{}, sc, sn);
-            block(tau4 + 4, std::false_type{}, std::false_type{}, sn, sc);
+            pair8(tau4, std::false_type{}, std::false_type{});
         }
         for (; tau4 <= tau_end; tau4 += 8) {
-            block(tau4, std::false_type{}, std::true_type{}, sc, sn);
-            block(tau4 + 4, std::false_type{}, std::true_type{}, sn, sc);
+            pair8(tau4, std::false_type{}, std::true_type{});
         }
+        if (((tau4 - tau0) >> 2) & 2) flush(tau4 - 8);   // a half row left: its other half is past tau_end
 
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
@@ -713,8 +731,8 @@ __device__ int band_walk_runs(const Code& code_at, int La, int Lb, int ei, int e
 // kd)` returns the band dword of anti-diagonal step tau (relative to the stored
 // range) and band diagonal kd; bit positions of read h at sub-step s: Y opens hb,
 // X > Y hb + 4, X opens 16 + hb, M < max(X, Y) 20 + hb, with hb = 8 h + s.
-template <int CPL, int W, class Word>
-__device__ int band_walk_runs2(const Word& word, int La, int Lb, int ei, int ej, int dlo, int tb0, int h,
+template <int CPL, int W>
+__device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int ei, int ej, int dlo, int tb0, int h,
                                unsigned* runs, int cap, int lane) {
     int nruns = 0, last_type = -1;
     bool full = false;
@@ -733,40 +751,50 @@ __device__ int band_walk_runs2(const Word& word, int La, int Lb, int ei, int ej,
     if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
     else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
     constexpr int WR = 64 * CPL;
+    constexpr int WM = 64 * 8;   // M rounds: 8 cells per lane from one dwordx4
     int i = __builtin_amdgcn_readfirstlane(ei), j = __builtin_amdgcn_readfirstlane(ej), state = RUN_M;
     const int hb = 8 * h;
     while (i > 0 && j > 0) {
         int k0;            // cells of the current run before the stop (the run is k0 + 1 long)
         int nb = RUN_M;    // M runs: the state the stop cell continues in
         if (state == RUN_M) {
-            // cells (i-1-k, j-1-k), 1-based; diagonal kd = j - i - dlo for all of them
+            // cells (i-1-k, j-1-k), 1-based, all on diagonal kd = j - i - dlo: one column.
+            // Lane l reads the 4 words [W0 - 4l, W0 - 4l + 3] (16 steps, 8 cells of the
+            // run's parity): cell u has tau = 4 (W0 - 4l) + 14 + p - 2u, run index k_l + u.
             const int kd = j - i - dlo;
             if ((unsigned)kd >= (unsigned)W) return -1;
             const int lim = min(i, j) - 1;          // k < lim: cell inside the matrix
             const int t0 = i + j - 4 + tb0;         // tau of cell k = 0
-            unsigned stop = 0u, xgy = 0u;
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                const int kk = lane * CPL + u;
-                const int tau = t0 - 2 * kk;
-                const unsigned w = word(max(tau, 0), kd);
-                const int sh = hb + (tau & 3);
-                const bool nm = ((w >> (20 + sh)) & 1u) != 0u;
-                stop |= (unsigned)(kk >= lim || nm) << u;
-                xgy |= ((w >> (4 + sh)) & 1u) << u;
-            }
+            const int p = t0 & 1;
+            const int W0 = (t0 >> 2) & ~3;
+            const int tl = min(max((W0 >> 2) - lane, 0), (NW >> 2) - 1);   // lane's tile row
+            const uint4 v = *(const uint4*)(bits + tl * (2 * W) + 4 * (kd >> 1));
+            const int k0l = (t0 - p - 4 * W0 - 14) >> 1;   // lane 0's k of cell u = 0, in [-7, 0]
+            const int kl = k0l + 8 * lane;
+            const int se = 20 + hb + 2 + p, so = 20 + hb + p;   // "M < max" bit of even / odd u
+            unsigned nm = 0u;
+            nm |= ((v.w >> se) & 1u) | (((v.w >> so) & 1u) << 1);
+            nm |= (((v.z >> se) & 1u) << 2) | (((v.z >> so) & 1u) << 3);
+            nm |= (((v.y >> se) & 1u) << 4) | (((v.y >> so) & 1u) << 5);
+            nm |= (((v.x >> se) & 1u) << 6) | (((v.x >> so) & 1u) << 7);
+            const int sz = min(max(-kl, 0), 8), sl = min(max(lim - kl, 0), 8);
+            const unsigned ge0 = (0xffu << sz) & 0xffu, gel = (0xffu << sl) & 0xffu;
+            const unsigned stop = (nm | gel) & ge0;
             const unsigned long long m = __ballot(stop != 0u);
-            if (m == 0) {
-                push(RUN_M, WR);
-                i -= WR;
-                j -= WR;
+            if (m == 0) {   // cells k < k0l + WM tested (k0l <= 0)
+                push(RUN_M, WM + k0l);
+                i -= WM + k0l;
+                j -= WM + k0l;
                 continue;
             }
             const int L = (int)__builtin_ctzll(m);
             const unsigned sL = (unsigned)__builtin_amdgcn_readlane((int)stop, L);
             const int u0 = (int)__builtin_ctz(sL);
-            k0 = L * CPL + u0;
-            nb = (((unsigned)__builtin_amdgcn_readlane((int)xgy, L) >> u0) & 1u) ? RUN_X : RUN_Y;
+            k0 = k0l + 8 * L + u0;
+            const int q = u0 >> 1;
+            const unsigned wq = (unsigned)__builtin_amdgcn_readlane(
+                (int)(q == 0 ? v.w : (q == 1 ? v.z : (q == 2 ? v.y : v.x))), L);
+            nb = ((wq >> (4 + hb + ((u0 & 1) ? p : 2 + p))) & 1u) ? RUN_X : RUN_Y;
             push(RUN_M, k0 + 1);
             i -= k0 + 1;
             j -= k0 + 1;
@@ -785,7 +813,8 @@ __device__ int band_walk_runs2(const Word& word, int La, int Lb, int ei, int ej,
                 const int kd = isX ? kd0 - kk : kd0 + kk;
                 const int tau = t0 - kk;
                 const bool out = (unsigned)kd >= (unsigned)W;
-                const unsigned w = word(max(tau, 0), kd & (W - 1));
+                const int wd = min(max(tau, 0) >> 2, NW - 1);
+                const unsigned w = bits[(wd >> 2) * (2 * W) + 4 * ((kd & (W - 1)) >> 1) + (wd & 3)];
                 const bool opens = ((w >> (bit + hb + (tau & 3))) & 1u) != 0u;
                 const bool valid = kk < lim;
                 stop |= (unsigned)(!valid || out || opens) << u;
@@ -822,7 +851,7 @@ __host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 
 template <int W>
 __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
-    constexpr int kBL = G::L, kCapBytes = G::CapBytes;
+    constexpr int kCapBytes = G::CapBytes;
     auto give_up = [&](long long rd, bool retry) {
         if (W < kBandDiags && retry) a.redo_list[atomicAdd(a.redo_count, 1)] = (int32_t)rd;
         else a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
@@ -920,9 +949,8 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
         const int tb0 = kBK - dlo + 2 - tau0;
-        const int nw_max = a.band_words - 1;
-        auto word = [&](int tau, int kd) -> unsigned { return bits[min(tau >> 2, nw_max) * kBL + (kd >> 1)]; };
-        const int nruns = band_walk_runs2<NW_BAND_WALK_CPL, W>(word, La, Lb, ei, ej, dlo, tb0, h, runs, kStreamRunsCap, lane);
+        const int nruns =
+            band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs, kStreamRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
             if (lane == 0) give_up(rd, true);
@@ -939,7 +967,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
 // ---- host-side helpers -------------------------------------------------------
 int band_fill_lds_bytes(int La, int wpb, int W) {
     return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La) +
-           256;
+           256 + wpb * 1024;
 }
 int band_walk_lds_bytes(int La, int wpb) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(); }
 int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }

@@ -465,3 +465,31 @@ def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
     batch = a.align_packed(buf, off)
     assert a.geometry()["tb_mode"] == "diag-int16"
     assert_same(oracle, amp, buf, off, batch, f"levels={levels}")
+
+
+@pytest.mark.parametrize("levels", ["16+32", "32"])
+def test_diag_iupac_in_every_pair_slot(gpu_aligner_factory, oracle, monkeypatch, levels):
+    """Reads with codes outside the band's score table (IUPAC, '-') in every pair
+    slot of the fill's wavefronts: each must leave the band for the exact kernel
+    (the per-pair flag is taken by a ballot that every lane must see)."""
+    if levels == "32":
+        monkeypatch.setenv("CRISPR_NW_DIAG16", "0")
+    amp = synth.random_amplicon(250, 7)
+    rng = np.random.Generator(np.random.PCG64(71))
+    reads = []
+    for k in range(512):
+        L = int(rng.integers(20, 250))
+        s = int(rng.integers(0, 250 - L + 1))
+        r = list(amp[s:s + L])
+        if k % 3 == 0:
+            for _ in range(int(rng.integers(1, 3))):
+                r[int(rng.integers(0, L))] = "RYKMSWBDHV-"[int(rng.integers(0, 11))]
+        elif k % 3 == 1:
+            r[int(rng.integers(0, L))] = "ACGT"[int(rng.integers(0, 4))]
+        reads.append("".join(r))
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert a.fallbacks() >= 512 // 3
+    assert_same(oracle, amp, buf, off, batch, f"diag-iupac {levels}")
