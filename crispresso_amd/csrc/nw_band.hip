@@ -844,7 +844,79 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
 
 constexpr int kBandReadCap = 1024;
 __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
-__host__ __device__ inline int band_walk_wave_bytes() { return kStreamRunsCap * 4 + kBandReadCap + 256; }
+constexpr int kBandRunsCap = 256;     // traceback runs per read (more: the read goes to the next level)
+__host__ __device__ inline int band_walk_row(int La, int lb_max) { return (La + lb_max + 15) & ~15; }   // = stride_for()
+__host__ __device__ inline int band_walk_rcap(int lb_max) { return min(kBandReadCap, (lb_max + 255) & ~255); }
+// per wave: runs, the read's bytes, the three output rows
+__host__ __device__ inline int band_walk_wave_bytes(int La, int lb_max) {
+    return kBandRunsCap * 4 + band_walk_rcap(lb_max) + 256 + 3 * band_walk_row(La, lb_max);
+}
+
+// emit_alignment (nw_common.h) with the three rows built in LDS (byte writes) and
+// written out as dwordx4 rows: 16 B per lane instead of a byte store per column.
+// The rows are padded to 16 B; the host reads aln_len columns of each.
+template <class Score>
+__device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* amp, const unsigned char* raw,
+                          const unsigned char* lut, const Score& sim_score, unsigned char* rows, int row,
+                          unsigned char* o_ref, int64_t stride, int score, int ei, int ej, Stat* st, int lane) {
+    int col = 0, ia = 0, jb = 0;
+    int n_id = 0, n_sim = 0, n_gap = 0;
+    for (int q = nruns - 1; q >= 0; --q) {
+        const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)runs[q]);
+        const int type = (int)(rc >> 28);
+        const int n = (int)(rc & 0x0fffffffu);
+        for (int p = lane; p < n; p += 64) {
+            unsigned char ca = '-', cb = '-', mk = ' ';
+            if (type != RUN_X) ca = amp[ia + p];
+            if (type != RUN_Y) cb = raw[jb + p];
+            const bool gapcol = ca == '-' || cb == '-';   // an input '-' counts as a gap (CORE:1846)
+            n_gap += gapcol;
+            if (type == RUN_M && !gapcol) {
+                const bool id = upcase(ca) == upcase(cb);
+                const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
+                mk = id ? '|' : (sim ? ':' : '.');
+                n_id += id;
+                n_sim += sim;
+            }
+            rows[col + p] = ca;
+            rows[row + col + p] = mk;
+            rows[2 * row + col + p] = cb;
+        }
+        col += n;
+        if (type != RUN_X) ia += n;
+        if (type != RUN_Y) jb += n;
+    }
+    lds_fence();
+    for (int c = 16 * lane; c < col; c += 1024) {
+        const uint4 r0 = *(const uint4*)(rows + c), r1 = *(const uint4*)(rows + row + c),
+                    r2 = *(const uint4*)(rows + 2 * row + c);
+        *(uint4*)(o_ref + c) = r0;
+        *(uint4*)(o_ref + stride + c) = r1;
+        *(uint4*)(o_ref + 2 * stride + c) = r2;
+    }
+    if (col < 1024) {
+        const unsigned t = wave_sum_u32((unsigned)n_id | ((unsigned)n_sim << 10) | ((unsigned)n_gap << 20));
+        n_id = (int)(t & 1023u);
+        n_sim = (int)((t >> 10) & 1023u);
+        n_gap = (int)(t >> 20);
+    } else {
+        n_id = wave_sum(n_id);
+        n_sim = wave_sum(n_sim);
+        n_gap = wave_sum(n_gap);
+    }
+    if (lane == 0) {
+        Stat s;
+        s.aln_len = col;
+        s.n_ident = n_id;
+        s.n_sim = n_sim;
+        s.n_gaps = n_gap;
+        s.score = score;
+        s.end_i = ei;
+        s.end_j = ej;
+        s.flags = 0;
+        *st = s;
+    }
+}
 
 // W < kBandDiags: a first level; reads it cannot certify go to the redo list of the
 // next (wider) level.  W = kBandDiags: they go to the exact int32 kernel.
@@ -868,9 +940,12 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         rowpos[k] = a.rowpos[k];
     }
     __syncthreads();
-    unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes();
+    const int row = band_walk_row(La, a.Lb_max);   // columns <= La + Lb
+    const int rcap = band_walk_rcap(a.Lb_max);
+    unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes(La, a.Lb_max);
     unsigned* runs = (unsigned*)wb;
-    unsigned char* rbuf = wb + kStreamRunsCap * 4;
+    unsigned char* rbuf = wb + kBandRunsCap * 4;
+    unsigned char* rows = rbuf + rcap + 256;
 
     const long long count = *a.band_count;
     const long long klo = 2 * a.band_pair_lo;
@@ -911,7 +986,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const unsigned char* region = region_of(k);
         const unsigned char* raw = a.reads + off;
         // the read's bytes -> LDS (DMA, one dword per lane) for the emit
-        const bool cached = Lb <= kBandReadCap;
+        const bool cached = Lb <= rcap;
         const int mis = (int)((uintptr_t)raw & 3);
         if (cached) {
             const unsigned char* src = raw - mis;
@@ -950,7 +1025,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
         const int tb0 = kBK - dlo + 2 - tau0;
         const int nruns =
-            band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs, kStreamRunsCap, lane);
+            band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs, kBandRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
             if (lane == 0) give_up(rd, true);
@@ -958,8 +1033,8 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         lds_fence();
         auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
-        emit_alignment(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, a.out + rd * 3 * a.stride,
-                       a.stride, score, ei, ej, a.stats + rd, lane);
+        band_emit(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, rows, row, a.out + rd * 3 * a.stride,
+                  a.stride, score, ei, ej, a.stats + rd, lane);
         lds_fence();
     }
 }
@@ -969,7 +1044,7 @@ int band_fill_lds_bytes(int La, int wpb, int W) {
     return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La) +
            256 + wpb * 1024;
 }
-int band_walk_lds_bytes(int La, int wpb) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(); }
+int band_walk_lds_bytes(int La, int wpb, int lb_max) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max); }
 int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }
 int64_t band_region_bytes(int La, int Lb_max, int W) { return band_region_stride(La, Lb_max, W); }
 bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb, dlo); }

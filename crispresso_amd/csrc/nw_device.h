@@ -118,7 +118,7 @@ hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, 
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
 constexpr int kBandDiags = 32;
 int band_fill_lds_bytes(int La, int wpb, int W);
-int band_walk_lds_bytes(int La, int wpb);
+int band_walk_lds_bytes(int La, int wpb, int lb_max);
 int band_region_words(int La, int Lb_max);
 int64_t band_region_bytes(int La, int Lb_max, int W);
 bool band_pair_geometry(int La, int Lb, int* dlo);

@@ -365,7 +365,7 @@ int configure(nw_ctx* c) {
             f.wpb = 8;
             w.wpb = 8;
             f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb, W);
-            w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb);
+            w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb, c->lb_max);
             int fb = 0, wb = 0;
             if (f.lds_bytes > kMaxLds || w.lds_bytes > kMaxLds) return 0;
             if (nw::band_occupancy(W, f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb) != hipSuccess || fb <= 0 ||
