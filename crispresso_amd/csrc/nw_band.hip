@@ -379,7 +379,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
         const int i = k - kAPad;   // row i = amplicon residue i - 1
         const int c = (i >= 1 && i <= La) ? a.lut6[a.amp[i - 1]] : kPadCode;   // host: amplicon codes <= 5
-        acd[k] = (uint16_t)(c * 36 * 4);
+        // the score table's LDS address is folded in: a0 + j0 is the entry's LDS address
+        acd[k] = (uint16_t)(c * 36 * 4 + (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)tab);
     }
     __syncthreads();
 
@@ -533,10 +534,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         auto load_scores = [&](unsigned* s) {
             const int a0 = ap[0], a1 = ap[1];
             const int j0 = jp[0], j1 = jp[1], j2 = jp[2];
-            s[0] = *(const unsigned*)((const unsigned char*)tab + a0 + j0);
-            s[1] = *(const unsigned*)((const unsigned char*)tab + a0 + j1);
-            s[2] = *(const unsigned*)((const unsigned char*)tab + a1 + j1);
-            s[3] = *(const unsigned*)((const unsigned char*)tab + a1 + j2);
+            using LdsU = const __attribute__((address_space(3))) unsigned;
+            s[0] = *(LdsU*)(uintptr_t)(a0 + j0);
+            s[1] = *(LdsU*)(uintptr_t)(a0 + j1);
+            s[2] = *(LdsU*)(uintptr_t)(a1 + j1);
+            s[3] = *(LdsU*)(uintptr_t)(a1 + j2);
             ap += 2;   // rows and columns both advance by 2 per 4 steps
             jp += 2;
         };
@@ -865,22 +867,41 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
         const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)runs[q]);
         const int type = (int)(rc >> 28);
         const int n = (int)(rc & 0x0fffffffu);
-        for (int p = lane; p < n; p += 64) {
-            unsigned char ca = '-', cb = '-', mk = ' ';
-            if (type != RUN_X) ca = amp[ia + p];
-            if (type != RUN_Y) cb = raw[jb + p];
-            const bool gapcol = ca == '-' || cb == '-';   // an input '-' counts as a gap (CORE:1846)
-            n_gap += gapcol;
-            if (type == RUN_M && !gapcol) {
-                const bool id = upcase(ca) == upcase(cb);
-                const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
-                mk = id ? '|' : (sim ? ':' : '.');
-                n_id += id;
-                n_sim += sim;
+        if (type == RUN_M) {
+            int same = 0;   // columns with identical bytes (not '-'): '|', identical and similar
+            for (int p = lane; p < n; p += 64) {
+                const unsigned char ca = amp[ia + p], cb = raw[jb + p];
+                unsigned char mk = '|';
+                if (ca != cb || ca == '-') {   // rare: a mismatch, a case difference or an input '-'
+                    mk = ' ';
+                    if (ca == '-' || cb == '-') {   // an input '-' counts as a gap (CORE:1846)
+                        ++n_gap;
+                    } else {
+                        const bool id = upcase(ca) == upcase(cb);
+                        const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
+                        mk = id ? '|' : (sim ? ':' : '.');
+                        n_id += id;
+                        n_sim += sim;
+                    }
+                } else {
+                    ++same;
+                }
+                rows[col + p] = ca;
+                rows[row + col + p] = mk;
+                rows[2 * row + col + p] = cb;
             }
-            rows[col + p] = ca;
-            rows[row + col + p] = mk;
-            rows[2 * row + col + p] = cb;
+            n_id += same;
+            n_sim += same;
+        } else {   // gap run: every column is a gap
+            const unsigned char* src = type == RUN_X ? raw + jb : amp + ia;
+            unsigned char* dst = rows + (type == RUN_X ? 2 * row : 0) + col;
+            unsigned char* gap = rows + (type == RUN_X ? 0 : 2 * row) + col;
+            for (int p = lane; p < n; p += 64) {
+                dst[p] = src[p];
+                rows[row + col + p] = ' ';
+                gap[p] = '-';
+                ++n_gap;
+            }
         }
         col += n;
         if (type != RUN_X) ia += n;
