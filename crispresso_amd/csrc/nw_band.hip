@@ -844,7 +844,7 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
     return full ? -1 : nruns;
 }
 
-constexpr int kBandReadCap = 1024;
+constexpr int kBandReadCap = 1280;   // >= the band length cap (La + 31, La <= 1024): every walked read fits
 __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
 constexpr int kBandRunsCap = 256;     // traceback runs per read (more: the read goes to the next level)
 __host__ __device__ inline int band_walk_row(int La, int lb_max) { return (La + lb_max + 15) & ~15; }   // = stride_for()
@@ -1007,14 +1007,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const unsigned char* region = region_of(k);
         const unsigned char* raw = a.reads + off;
         // the read's bytes -> LDS (DMA, one dword per lane) for the emit
-        const bool cached = Lb <= rcap;
-        const int mis = (int)((uintptr_t)raw & 3);
-        if (cached) {
-            const unsigned char* src = raw - mis;
-            for (int m = 0; m < Lb + mis; m += 256)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + m + 4 * lane),
-                                                 (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
+        if (Lb > rcap) {   // not reached: rcap covers the band length cap
+            if (lane == 0) give_up(rd, false);
+            continue;
         }
+        const int mis = (int)((uintptr_t)raw & 3);
+        for (int m = 0; m < Lb + mis; m += 256)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(raw - mis + m + 4 * lane),
+                                             (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
         const int tau0 = hdr.x;
         // start cell: the last cell of each band diagonal is on the last row or column
         unsigned k32 = 0u;
@@ -1054,8 +1054,8 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         lds_fence();
         auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
-        band_emit(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, rows, row, a.out + rd * 3 * a.stride,
-                  a.stride, score, ei, ej, a.stats + rd, lane);
+        band_emit(runs, nruns, amp_lds, rbuf + mis, lut_lds, sim, rows, row, a.out + rd * 3 * a.stride, a.stride, score, ei,
+                  ej, a.stats + rd, lane);
         lds_fence();
     }
 }
