@@ -750,6 +750,16 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
             full = true;
         }
     };
+    // the state machine is wave-uniform: keep its inputs in SGPRs so every branch
+    // below is a scalar branch (values loaded through VGPRs are not provably uniform)
+    La = __builtin_amdgcn_readfirstlane(La);
+    Lb = __builtin_amdgcn_readfirstlane(Lb);
+    ei = __builtin_amdgcn_readfirstlane(ei);
+    ej = __builtin_amdgcn_readfirstlane(ej);
+    dlo = __builtin_amdgcn_readfirstlane(dlo);
+    tb0 = __builtin_amdgcn_readfirstlane(tb0);
+    NW = __builtin_amdgcn_readfirstlane(NW);
+    h = __builtin_amdgcn_readfirstlane(h);
     if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
     else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
     constexpr int WR = 64 * CPL;
@@ -757,6 +767,8 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
     int i = __builtin_amdgcn_readfirstlane(ei), j = __builtin_amdgcn_readfirstlane(ej), state = RUN_M;
     const int hb = 8 * h;
     while (i > 0 && j > 0) {
+        nruns = __builtin_amdgcn_readfirstlane(nruns);   // uniform (see above)
+        last_type = __builtin_amdgcn_readfirstlane(last_type);
         int k0;            // cells of the current run before the stop (the run is k0 + 1 long)
         int nb = RUN_M;    // M runs: the state the stop cell continues in
         if (state == RUN_M) {
@@ -986,8 +998,12 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     };
     long long k = klo + (long long)blockIdx.x * wpb + wave;
     if (k < khi) prefetch(k);
+    auto uni = [](int4 v) {   // the prefetched header is wave-uniform: SGPRs, scalar branches
+        return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                         __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+    };
     for (; k < khi; k += kstep) {
-        const int4 hdr = n0, hr = n1, ho = n2;
+        const int4 hdr = uni(n0), hr = uni(n1), ho = uni(n2);
         const unsigned cw = ncw;
         if (k + kstep < khi) prefetch(k + kstep);
         const int h = (int)(k & 1);
@@ -1031,6 +1047,9 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         int score, ei, ej;
         decode_end(end_key_widen(wave_max_u32(k32)), La, Lb, &score, &ei, &ej);
+        score = __builtin_amdgcn_readfirstlane(score);
+        ei = __builtin_amdgcn_readfirstlane(ei);
+        ej = __builtin_amdgcn_readfirstlane(ej);
         // certificate: every alignment leaving the band scores <= UB < score
         const int dhi = dlo + W - 1;
         int pmax = -1;
