@@ -881,26 +881,29 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
         const int n = (int)(rc & 0x0fffffffu);
         if (type == RUN_M) {
             int same = 0;   // columns with identical bytes (not '-'): '|', identical and similar
-            for (int p = lane; p < n; p += 64) {
-                const unsigned char ca = amp[ia + p], cb = raw[jb + p];
-                unsigned char mk = '|';
-                if (ca != cb || ca == '-') {   // rare: a mismatch, a case difference or an input '-'
-                    mk = ' ';
-                    if (ca == '-' || cb == '-') {   // an input '-' counts as a gap (CORE:1846)
-                        ++n_gap;
+            for (int c0 = 0; c0 < n; c0 += 64) {   // uniform trip count: scalar loop
+                const int p = c0 + lane;
+                if (p < n) {
+                    const unsigned char ca = amp[ia + p], cb = raw[jb + p];
+                    unsigned char mk = '|';
+                    if (ca != cb || ca == '-') {   // rare: a mismatch, a case difference or an input '-'
+                        mk = ' ';
+                        if (ca == '-' || cb == '-') {   // an input '-' counts as a gap (CORE:1846)
+                            ++n_gap;
+                        } else {
+                            const bool id = upcase(ca) == upcase(cb);
+                            const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
+                            mk = id ? '|' : (sim ? ':' : '.');
+                            n_id += id;
+                            n_sim += sim;
+                        }
                     } else {
-                        const bool id = upcase(ca) == upcase(cb);
-                        const bool sim = id || sim_score(ia + p, (int)lut[cb]) > 0;
-                        mk = id ? '|' : (sim ? ':' : '.');
-                        n_id += id;
-                        n_sim += sim;
+                        ++same;
                     }
-                } else {
-                    ++same;
+                    rows[col + p] = ca;
+                    rows[row + col + p] = mk;
+                    rows[2 * row + col + p] = cb;
                 }
-                rows[col + p] = ca;
-                rows[row + col + p] = mk;
-                rows[2 * row + col + p] = cb;
             }
             n_id += same;
             n_sim += same;
@@ -908,11 +911,14 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
             const unsigned char* src = type == RUN_X ? raw + jb : amp + ia;
             unsigned char* dst = rows + (type == RUN_X ? 2 * row : 0) + col;
             unsigned char* gap = rows + (type == RUN_X ? 0 : 2 * row) + col;
-            for (int p = lane; p < n; p += 64) {
-                dst[p] = src[p];
-                rows[row + col + p] = ' ';
-                gap[p] = '-';
-                ++n_gap;
+            for (int c0 = 0; c0 < n; c0 += 64) {
+                const int p = c0 + lane;
+                if (p < n) {
+                    dst[p] = src[p];
+                    rows[row + col + p] = ' ';
+                    gap[p] = '-';
+                    ++n_gap;
+                }
             }
         }
         col += n;
