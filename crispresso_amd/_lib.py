@@ -48,6 +48,17 @@ QUANT_EXPORTS = (
 )
 
 
+# Every symbol include/crispr_flash.h declares.
+FLASH_EXPORTS = ("nwf_merge_batch", "nwf_last_error")
+NWF_COMBINED, NWF_OUTIE = 1, 2
+
+
+class NwfParams(ctypes.Structure):
+    """nwf_params (include/crispr_flash.h)."""
+    _fields_ = [("min_overlap", c_int32), ("max_overlap", c_int32), ("max_mismatch_density", c_float),
+                ("allow_outies", c_int32), ("phred_offset", c_int32), ("cap_mismatch_quals", c_int32)]
+
+
 class NwqParams(ctypes.Structure):
     """nwq_params (include/crispr_quant.h)."""
     _fields_ = [("len_amplicon", c_int32), ("include_mask", c_void_p), ("exon_mask", c_void_p),
@@ -104,6 +115,9 @@ def load() -> ctypes.CDLL:
                                    c_void_p, c_int64, c_void_p]),
         "nw_required_stride_multi": (c_int64, [c_void_p, c_int32, c_int32]),
         "nw_batch_device_output": (c_int, [ctx_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)]),
+        "nwf_merge_batch": (c_int, [c_int, POINTER(NwfParams)] + [c_void_p] * 6 + [c_int64] + [c_void_p] * 4
+                            + [POINTER(c_float)]),
+        "nwf_last_error": (c_char_p, []),
         "nwq_create": (c_int, [c_int, POINTER(c_void_p)]),
         "nwq_destroy": (None, [ctx_p]),
         "nwq_last_error": (c_char_p, [ctx_p]),
@@ -131,7 +145,7 @@ def exported_symbols() -> dict:
     """Map of each declared symbol to whether the loaded library exports it."""
     lib = load()
     out = {}
-    for name in EXPORTS + QUANT_EXPORTS:
+    for name in EXPORTS + QUANT_EXPORTS + FLASH_EXPORTS:
         try:
             getattr(lib, name)
             out[name] = True
