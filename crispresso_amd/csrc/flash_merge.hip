@@ -97,14 +97,20 @@ __global__ __launch_bounds__(64 * kWpb) void nwf_merge_kernel(const Args a) {
             if (last < first || nb < a.min_ov) return;
             for (int pos = first + lane; pos <= last; pos += 64) {
                 const int eff = min(min(na - pos, nb), a.max_ov);
+                // past lim mismatches the density exceeds max_density by more than 1/eff
+                // (far above fp32 rounding): the overlap can never be taken, and when no
+                // overlap can be, the pair stays uncombined whichever is "best" -- stop
+                const int lim = (int)(a.max_density * (float)eff) + 1;
                 int mm = 0, qt = 0;
                 for (int k = 0; k < eff; ++k) {
                     const int qa_k = (int)(signed char)qa[pos + k], qb_k = (int)(signed char)qb[k];
                     if (ra[pos + k] != rb[k]) {
                         ++mm;
                         qt += min(qa_k, qb_k);
+                        if (mm > lim) break;
                     }
                 }
+                if (mm > lim) continue;
                 const float fe = (float)eff;
                 const float d = (float)mm / fe, qs = (float)qt / fe;
                 const Cand c = {ord32(d), ord32(qs), order0 + (unsigned)pos};

@@ -79,12 +79,25 @@ def merge_pairs(seq1: List[bytes], qual1: List[bytes], seq2: List[bytes], qual2:
     for s, q in zip(seq1 + seq2, qual1 + qual2):
         if len(s) != len(q):
             raise FlashError("merge_pairs: a sequence and its quality line differ in length")
-    o = options or FlashOptions()
     s1, off1 = _pack(seq1)
     q1, _ = _pack(qual1)
     s2, off2 = _pack(seq2)
     q2, _ = _pack(qual2)
-    n = len(seq1)
+    return merge_packed(s1, q1, off1, s2, q2, off2, options, device)
+
+
+def merge_packed(s1: np.ndarray, q1: np.ndarray, off1: np.ndarray, s2: np.ndarray, q2: np.ndarray,
+                 off2: np.ndarray, options: Optional[FlashOptions] = None, device: int = 0) -> MergeResult:
+    """merge_pairs on packed inputs: uint8 sequence / quality buffers and int64
+    offsets (n + 1, from 0) per mate."""
+    o = options or FlashOptions()
+    s1, q1, s2, q2 = (np.ascontiguousarray(x, dtype=np.uint8) for x in (s1, q1, s2, q2))
+    off1 = np.ascontiguousarray(off1, dtype=np.int64)
+    off2 = np.ascontiguousarray(off2, dtype=np.int64)
+    if len(off1) != len(off2) or len(off1) < 1 or off1[-1] > len(s1) or off2[-1] > len(s2) or \
+            len(q1) < off1[-1] or len(q2) < off2[-1]:
+        raise FlashError("merge_packed: offsets do not match the buffers")
+    n = len(off1) - 1
     total = int(off1[-1] + off2[-1])
     out_seq = np.zeros(max(total, 1), dtype=np.uint8)
     out_qual = np.zeros(max(total, 1), dtype=np.uint8)
