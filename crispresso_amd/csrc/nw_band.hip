@@ -56,8 +56,8 @@
 
 #include "nw_common.h"
 
-#ifndef NW_BAND_WALK_CPL
-#define NW_BAND_WALK_CPL 2
+#ifndef NW_BAND_WALK_CPL   // gap-run cells per lane and round (a gap run inside the band is < W <= 64 cells)
+#define NW_BAND_WALK_CPL 1
 #endif
 
 namespace nw {
