@@ -102,15 +102,36 @@ __global__ __launch_bounds__(64 * kWpb) void nwf_merge_kernel(const Args a) {
                 // overlap can be, the pair stays uncombined whichever is "best" -- stop
                 const int lim = (int)(a.max_density * (float)eff) + 1;
                 int mm = 0, qt = 0;
-                for (int k = 0; k < eff; ++k) {
-                    const int qa_k = (int)(signed char)qa[pos + k], qb_k = (int)(signed char)qb[k];
-                    if (ra[pos + k] != rb[k]) {
-                        ++mm;
-                        qt += min(qa_k, qb_k);
-                        if (mm > lim) break;
+                // 4 bases per step: b's dword is aligned, a's is assembled from two
+                // aligned dwords (v_alignbyte); mismatching bytes = nonzero bytes of a ^ b
+                const unsigned* a32 = (const unsigned*)ra;
+                const unsigned* b32 = (const unsigned*)rb;
+                const unsigned* qa32 = (const unsigned*)qa;
+                const unsigned* qb32 = (const unsigned*)qb;
+                auto mism = [&](int k, int ak) {   // mismatch flags (bit 7 of each byte) of bases k .. k+3
+                    const unsigned x =
+                        __builtin_amdgcn_alignbyte(a32[(ak >> 2) + 1], a32[ak >> 2], ak & 3) ^ b32[k >> 2];
+                    unsigned m = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+                    const int rem = eff - k;
+                    return rem < 4 ? m & ((1u << (8 * rem)) - 1u) : m;
+                };
+                // pass 1: mismatches only, abandoned past lim (most positions)
+                for (int k = 0; k < eff && mm <= lim; k += 4) mm += __builtin_popcount(mism(k, pos + k));
+                if (mm > lim) continue;
+                // pass 2 (positions that can be taken): the qualities at the mismatches
+                for (int k = 0; k < eff; k += 4) {
+                    const int ak = pos + k;
+                    unsigned m = mism(k, ak);
+                    if (m) {
+                        const unsigned qaw = __builtin_amdgcn_alignbyte(qa32[(ak >> 2) + 1], qa32[ak >> 2], ak & 3);
+                        const unsigned qbw = qb32[k >> 2];
+                        do {   // signed: quality - offset
+                            const int b8 = (int)__builtin_ctz(m) - 7;   // 8 * byte index
+                            qt += min((int)(signed char)(qaw >> b8), (int)(signed char)(qbw >> b8));
+                            m &= m - 1u;
+                        } while (m);
                     }
                 }
-                if (mm > lim) continue;
                 const float fe = (float)eff;
                 const float d = (float)mm / fe, qs = (float)qt / fe;
                 const Cand c = {ord32(d), ord32(qs), order0 + (unsigned)pos};
