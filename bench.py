@@ -15,7 +15,10 @@ value = N * 1M * K / max-over-ranks time of K steps  ("scaling": "weak").
 Extra keys: "roofline" (HBM, algorithmic bytes per launch / kernel time from
 HIP events on the aligner's stream) with a VALU-side GCUPS figure, and
 "cpu_baseline" (the CPU oracle -- a port, not EMBOSS, which is absent -- on a
-bounded sample, rank 0 at N=1 only).
+bounded sample, rank 0 at N=1 only); informational legs either side of the
+path: "downstream_quantification" (process_df_chunk on the aligned batch) and,
+at N=1, "upstream_merge" (the paired-end merge, FLASH semantics, 1M 2 x 150 bp
+pairs; --no-merge skips it).
 """
 from __future__ import annotations
 
@@ -189,6 +192,38 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
     return out
 
 
+def merge_leg(device, n_pairs):
+    """The paired-end merge (crispresso_amd/flash.py, FLASH semantics) on synthetic pairs of the
+    same shape as scripts/bench_flash.py: 2 x 150 bp over a 250 bp amplicon, 1 % noise, seed 7,
+    CRISPResso's FLASH options.  Informational (upstream of the metric's path)."""
+    from crispresso_amd.flash import FlashOptions, merge_packed
+
+    L, amp_len = 150, 250
+    rng = np.random.Generator(np.random.PCG64(7))
+    alpha = np.frombuffer(b"ACGT", np.uint8)
+    amp = rng.choice(alpha, amp_len)
+    comp = np.zeros(256, np.uint8)
+    for x, y in zip(b"ACGT", b"TGCA"):
+        comp[x] = y
+    r1 = np.tile(amp[:L], (n_pairs, 1))
+    r2 = np.tile(comp[amp[::-1]][:L], (n_pairs, 1))
+    for r in (r1, r2):
+        m = rng.random(r.shape) < 0.01
+        r[m] = rng.choice(alpha, int(m.sum()))
+    q = rng.integers(53, 74, (n_pairs, L)).astype(np.uint8)
+    off = np.arange(n_pairs + 1, dtype=np.int64) * L
+    opts = FlashOptions(min_overlap=4, max_overlap=100, allow_outies=True)
+    merge_packed(r1[:1000].ravel(), q[:1000].ravel(), off[:1001], r2[:1000].ravel(), q[:1000].ravel(), off[:1001],
+                 opts, device)
+    t0 = time.perf_counter()
+    res = merge_packed(r1.ravel(), q.ravel(), off, r2.ravel(), q.ravel(), off, opts, device)
+    wall = time.perf_counter() - t0
+    return {"metric": "merged read pairs/s", "pairs": n_pairs, "read_len": L, "kernel_ms": res.kernel_ms,
+            "value": n_pairs / (res.kernel_ms / 1e3), "call_pairs_per_s": n_pairs / wall,
+            "combined": int((res.length > 0).sum()),
+            "note": "nwf_merge_batch kernel time (inputs resident); call_pairs_per_s includes PCIe and allocation"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,6 +235,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-quant", action="store_true", help="skip the downstream quantification leg")
     ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
+    ap.add_argument("--no-merge", action="store_true", help="skip the paired-end merge leg (N = 1 only)")
+    ap.add_argument("--merge-pairs", type=int, default=1_000_000)
     args = ap.parse_args()
 
     rank, local, world, dist = dist_setup(args.gpus)
@@ -248,6 +285,13 @@ def main():
     if not args.no_quant:
         quant = quant_leg(al, amplicon, args.reads, args.steps, args.warmup, dist, local, rank, world,
                           args.quant_cpu_sample, args.no_cpu)
+
+    merge = None
+    if rank == 0 and world == 1 and not args.no_merge:
+        try:
+            merge = merge_leg(local, args.merge_pairs)
+        except Exception as exc:   # informational leg: never costs the bench line
+            merge = {"error": f"{type(exc).__name__}: {exc}"}
 
     diag = geo["tb_mode"].startswith("diag")
     if diag:
@@ -315,6 +359,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "downstream_quantification": quant,
+            "upstream_merge": merge,
         }
         print(json.dumps(line), flush=True)
     al.close()
