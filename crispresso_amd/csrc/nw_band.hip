@@ -782,9 +782,10 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
             const int p = t0 & 1;
             const int W0 = (t0 >> 2) & ~3;
             const int tl = min(max((W0 >> 2) - lane, 0), (NW >> 2) - 1);   // lane's tile row
-            const uint4 v = *(const uint4*)(bits + tl * (2 * W) + 4 * (kd >> 1));
             const int k0l = (t0 - p - 4 * W0 - 14) >> 1;   // lane 0's k of cell u = 0, in [-7, 0]
             const int kl = k0l + 8 * lane;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);   // lanes past the matrix edge stop without a load
+            if (kl < lim) v = *(const uint4*)(bits + tl * (2 * W) + 4 * (kd >> 1));
             const int se = 20 + hb + 2 + p, so = 20 + hb + p;   // "M < max" bit of even / odd u
             unsigned nm = 0u;
             nm |= ((v.w >> se) & 1u) | (((v.w >> so) & 1u) << 1);
@@ -828,7 +829,8 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
                 const int tau = t0 - kk;
                 const bool out = (unsigned)kd >= (unsigned)W;
                 const int wd = min(max(tau, 0) >> 2, NW - 1);
-                const unsigned w = bits[(wd >> 2) * (2 * W) + 4 * ((kd & (W - 1)) >> 1) + (wd & 3)];
+                const unsigned w = (kk < lim && !out) ? bits[(wd >> 2) * (2 * W) + 4 * ((kd & (W - 1)) >> 1) + (wd & 3)]
+                                                      : 0u;   // cells that stop anyway: no load
                 const bool opens = ((w >> (bit + hb + (tau & 3))) & 1u) != 0u;
                 const bool valid = kk < lim;
                 stop |= (unsigned)(!valid || out || opens) << u;
