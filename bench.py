@@ -39,7 +39,8 @@ READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summary of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic
 # (newest first: the aligner kernels' latest summary, then the one that also holds the quantification kernels)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_v23", "pmc_summary.json"),
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_v24", "pmc_summary.json"),
+                 os.path.join(ROOT, "profiles", "r01_v23", "pmc_summary.json"),
                  os.path.join(ROOT, "profiles", "r01_v22", "pmc_summary.json"),
                  os.path.join(ROOT, "profiles", "r01_v21", "pmc_summary.json"),
                  os.path.join(ROOT, "profiles", "r01_v19", "pmc_summary.json"),
