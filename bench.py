@@ -2,23 +2,30 @@
 """Benchmark: aligned reads/sec, 250 bp amplicon x 1M synthetic reads per GPU.
 
 BASELINE.json metric: "aligned reads/sec (250 bp amplicon x 1M reads) at
-1/2/4/8 MI355X".  One step = one pass of the GPU aligner (the kernel that
-replaces EMBOSS needle, CRISPRessoCORE.py:1791-1806) over the rank's batch of
-1M reads that is already resident in HBM; outputs (three alignment strings
-and per-read statistics) are written to HBM.
+1/2/4/8 MI355X".  SURVEY.md 8d defines it at the boundary of the process it
+replaces (CRISPRessoCORE.py:1791-1806: reads in, alignments out): the read count
+over the wall time of the aligner call, host batch in -> per-read records in
+host memory.  One step = one nw_align_ops call (include/crispr_nw.h) on the
+rank's 1M C2 reads held in pinned host memory: chunks of reads pipelined over
+PCIe and through the kernels, every read's record (nw_stat) and traceback runs
+copied back to pinned host memory (an exact copy is one run; the host rebuilds
+the rows with nw_expand_ops, timed separately as "expand").
 
 N GPUs: one process per GPU (torch.distributed.run), each aligning its own 1M
 read shard (reads are independent, no collective on the data
-path; the only collectives are the timing barrier and the max-over-ranks).
-value = N * 1M * K / max-over-ranks time of K steps  ("scaling": "weak").
+path).  The timing barrier and the max-over-ranks run over a gloo process group
+on the host: this process never initialises torch's HIP runtime (libcrispr_nw.so
+owns the GPU).  value = N * 1M * K / max-over-ranks time of K steps ("weak").
 
-Extra keys: "roofline" (HBM, algorithmic bytes per launch / kernel time from
-HIP events on the aligner's stream) with a VALU-side GCUPS figure, and
-"cpu_baseline" (the CPU oracle -- a port, not EMBOSS, which is absent -- on a
-bounded sample, rank 0 at N=1 only); informational legs either side of the
-path: "downstream_quantification" (process_df_chunk on the aligned batch) and,
-at N=1, "upstream_merge" (the paired-end merge, FLASH semantics, 1M 2 x 150 bp
-pairs; --no-merge skips it).
+Extra keys: "kernel_rate" (the same kernels + compaction on the batch resident in
+HBM, HIP events), "pcie" (upload span and bytes each way of the timed call),
+"sample_check" (every 100th read of the timed batch re-aligned by the CPU oracle,
+outside the timed region), "roofline" (HBM: algorithmic bytes per pass over the
+kernel-resident pass time; VALU: issue fraction of nw_band_fill<16>),
+"cpu_baseline" (the CPU oracle -- a port, EMBOSS is absent -- on bounded samples,
+1 thread and the box's CPU share, rank 0 at N = 1 only); legs either side of the
+path at N = 1: "dual_alignment" (C3, CORE:1808-1828), "downstream_quantification",
+"upstream_merge".
 """
 from __future__ import annotations
 
@@ -34,19 +41,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s (x1e12)
+# VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md "Wave scheduling")
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
 READS_PER_GPU = 1_000_000
-# rocprofv3 --pmc summary of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
-# 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic
-# (newest first: the aligner kernels' latest summary, then the one that also holds the quantification kernels)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "r01_v24", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_v23", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_v22", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_v21", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_v19", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_diag_pmc", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_bias_pmc", "pmc_summary.json"),
-                 os.path.join(ROOT, "profiles", "r01_quant", "pmc_summary.json")]
+# rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
+# 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
+# VALU instruction count per fill launch (newest first)
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
+                 for d in ("r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
 AMPLICON_LEN = 250
 
 
@@ -54,42 +56,50 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus):
+def dist_setup():
+    """(rank, local, world, dist) -- gloo on the host; torch.cuda is never touched."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 0, 0, 1, None
-    import torch
     import torch.distributed as dist
 
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl")
+    dist.init_process_group("gloo")
     return rank, local, world, dist
 
 
-def barrier(dist, local):
-    if dist is None:
-        return
-    import torch
-
-    dist.barrier(device_ids=[local])
-    torch.cuda.synchronize()
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
 
 
-def max_over_ranks(dist, local, value):
+def max_over_ranks(dist, value):
     if dist is None:
         return value
     import torch
 
-    t = torch.tensor([value], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
+def pmc_summary(required):
+    """(summary dict, path) of the newest PMC summary holding a kernel whose name contains `required`."""
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if any(required in k for k in summ):
+            return summ, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def pmc_traffic(*prefixes, required=None):
     """(HBM bytes per launch of the kernels whose names start with `prefixes`, source file), from the
-    first summary in PMC_SUMMARIES that holds them (and a kernel starting with `required`)."""
+    first summary in PMC_SUMMARIES that holds them (and a kernel containing `required`)."""
     for path in PMC_SUMMARIES:
         try:
             with open(path) as f:
@@ -105,32 +115,92 @@ def pmc_traffic(*prefixes, required=None):
     return None, None
 
 
-def cpu_baseline(amplicon, buf, offsets, n_sample, threads):
+def sample_reads(buf, offsets, idx):
+    """Packed sub-batch of reads `idx`."""
+    lens = (offsets[idx + 1] - offsets[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    parts = [buf[offsets[i]:offsets[i + 1]] for i in idx]
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), off
+
+
+def sample_check(amplicon, buf, offsets, ob, every, threads):
+    """Every `every`-th read of the timed batch: its record and the rows expanded from its
+    runs against the CPU oracle (outside the timed region)."""
+    from crispresso_amd.aligner import OpsBatch
     from oracle import oracle_py
 
-    sub = offsets[: n_sample + 1]
+    n = len(offsets) - 1
+    idx = np.arange(0, n, every, dtype=np.int64)
+    sbuf, soff = sample_reads(buf, offsets, idx)
+    runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in idx]
+    sops_off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum([len(r) for r in runs], out=sops_off[1:])
+    sub = OpsBatch(ob.stats[idx], np.concatenate(runs) if runs else np.zeros(0, np.uint32), sops_off,
+                   np.diff(soff), ob.scale)
+    got = sub.expand(amplicon, sbuf, soff)
+    res, aln = oracle_py.align_batch(amplicon, sbuf, soff, nthreads=threads)
+    bad = np.zeros(len(idx), bool)
+    for f in ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j"):
+        bad |= got.stats[f] != res[f]
+    for i in np.flatnonzero(~bad):
+        L = int(res["aln_len"][i])
+        bad[i] = got.aln[i, :, :L].tobytes() != aln[i, :, :L].tobytes()
+    return {"reads_checked": int(len(idx)), "every": every, "sample_mismatches": int(bad.sum()),
+            "what": "record (length, identity, similarity, gaps, score, start cell) and the three rows expanded "
+                    "from the runs, vs oracle/nw_oracle.c on the same reads"}
+
+
+def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t):
+    from oracle import oracle_py
+
     t0 = time.perf_counter()
-    oracle_py.align_batch(amplicon, buf, sub, nthreads=threads)
+    oracle_py.align_batch(amplicon, buf, offsets[: n_sample + 1], nthreads=threads)
     dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    oracle_py.align_batch(amplicon, buf, offsets[: n_sample_1t + 1], nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {
         "value": n_sample / dt,
         "unit": "aligned reads/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {n_sample} reads of the same synthetic C2 batch, CPU oracle (oracle/nw_oracle.c, "
-                  f"scalar Gotoh + traceback per read) on {threads} host threads, {dt:.2f} s wall; "
-                  "EMBOSS needle itself is not installed on the box",
+        "one_thread": {"value": n_sample_1t / dt1, "cores": 1, "reads": n_sample_1t, "seconds": dt1},
+        "sample": f"first {n_sample} reads of the same synthetic C2 batch, CPU oracle (oracle/nw_oracle.c, scalar "
+                  f"Gotoh + traceback per read) on {threads} host threads (the box's CPU share; os.cpu_count() = "
+                  f"{os.cpu_count()}), {dt:.2f} s wall; one_thread: first {n_sample_1t} reads, 1 thread; EMBOSS "
+                  "needle itself is not installed on the box",
     }
 
 
-def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cpu_sample, no_cpu):
+def kernel_pass(al, buf, offsets, steps, warmup):
+    """The call's kernels + ops compaction on the batch resident in HBM (upload once)."""
+    al.set_output("ops")
+    al.upload(buf, offsets)
+    for _ in range(warmup):
+        al.run_async()
+        al.sync()
+    kms, phases = [], []
+    for _ in range(max(steps, 1)):
+        al.run_async()
+        kms.append(al.sync())
+        phases.append(al.phase_times())
+    ph = {k: float(np.mean([d[k] for d in phases])) for k in phases[0]}
+    return float(np.mean(kms)), ph, al.path_counts(), al.algo_bytes(), al.geometry()
+
+
+def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, cpu_sample, no_cpu):
     """Downstream quantification (process_df_chunk, CORE:428-753) of this rank's
-    aligned reads, straight from the aligner's HBM output (nwq_run_device).
+    aligned reads, straight from the aligner's HBM rows (nwq_run_device).
     Settings: one guide cutting mid-amplicon, CRISPResso defaults otherwise
     (window_around_sgrna 1, exclude 15 bp each side)."""
     from crispresso_amd import quantify
     from crispresso_amd.devmem import DeviceBuffer
 
+    al.set_output("rows")
+    al.upload(buf, offsets)
+    al.run_async()
+    al.sync()
     d_aln, stride, d_stats = al.device_output()
     batch = al.download(n_reads, AMPLICON_LEN + 64)
     lens = batch.stats["aln_len"].astype(np.int64)
@@ -140,27 +210,25 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
                               window_around_sgrna=1, exclude_bp_from_left=15, exclude_bp_from_right=15,
                               coding_seq=None, expected_hdr_amplicon_seq=None)
     g = quantify.globals_from_args(args)
-    q = quantify.GpuQuantifier(local)
+    q = quantify.GpuQuantifier(al.device)
     q.set_params(g, args)
     pre = quantify.pre_flags(um)
-    d_pre = DeviceBuffer.from_array(pre, local)
-    d_out = DeviceBuffer(16 * n_reads, local)
+    d_pre = DeviceBuffer.from_array(pre, al.device)
+    d_out = DeviceBuffer(16 * n_reads, al.device)
     for _ in range(warmup):
         q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
-    barrier(dist, local)
     kms = []
     t0 = time.perf_counter()
     for _ in range(steps):
         q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
         kms.append(q.last_kernel_ms)
-    barrier(dist, local)
-    elapsed = max_over_ranks(dist, local, time.perf_counter() - t0)
+    elapsed = time.perf_counter() - t0
     algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
     kavg = float(np.mean(kms))
     q_traffic, q_src = pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce")
     out = {
         "metric": "quantified reads/s (process_df_chunk on the aligned C2 batch, device-resident)",
-        "value": n_reads * world * steps / elapsed,
+        "value": n_reads * steps / elapsed,
         "unit": "reads/s",
         "ms_per_step": elapsed / steps * 1e3,
         "kernel": "nwq::quant_kernel + nwq::quant_reduce",
@@ -190,6 +258,50 @@ def quant_leg(al, amplicon, n_reads, steps, warmup, dist, local, rank, world, cp
     d_pre.free()
     d_out.free()
     q.close()
+    return out
+
+
+def dual_leg(device, n_reads, steps, warmup):
+    """C3: every read against the amplicon (records + runs) and against the HDR
+    amplicon (records only: the repair pass reads scores, CORE:1808-1828 with just_score)."""
+    from crispresso_amd import _lib, synth
+    from crispresso_amd.aligner import GpuAligner
+
+    amp, hdr, buf, off = synth.c3_workload(n_reads)
+    n = len(off) - 1
+    pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
+    stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
+    stats2 = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
+    ops_off = _lib.PinnedBuffer(n + 1, np.int64)
+    ops_off2 = _lib.PinnedBuffer(n + 1, np.int64)
+    ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
+    a_ref, a_hdr = GpuAligner(device), GpuAligner(device)
+    a_ref.set_reference(amp)
+    a_hdr.set_reference(hdr)
+
+    def step():
+        a_ref.align_ops(pb.array, po.array, out=(stats.array, ops.array, ops_off.array))
+        rc = a_hdr.lib.nw_align_ops(a_hdr._h, _lib.ptr(pb.array), _lib.ptr(po.array), n, None, 0,
+                                    _lib.ptr(ops_off2.array), _lib.ptr(stats2.array))
+        a_hdr._check(rc, "nw_align_ops (records only)")
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    hdr_better = int((stats2.array["n_ident"] * stats.array["aln_len"] >
+                      stats.array["n_ident"] * stats2.array["aln_len"]).sum())
+    out = {"metric": "dual-aligned reads/s (C3: 1M reads x amplicon + HDR amplicon, 1 GPU)",
+           "value": n / dt, "unit": "reads/s", "ms_per_step": dt * 1e3, "reads": n,
+           "reads_closer_to_hdr": hdr_better,
+           "note": "per step: nw_align_ops vs the amplicon (records + runs) then vs the HDR amplicon (records "
+                   "only), pinned host buffers, both calls synchronous"}
+    for b in (pb, po, stats, stats2, ops_off, ops_off2, ops):
+        b.close()
+    a_ref.close()
+    a_hdr.close()
     return out
 
 
@@ -225,6 +337,13 @@ def merge_leg(device, n_pairs):
             "note": "nwf_merge_batch kernel time (inputs resident); call_pairs_per_s includes PCIe and allocation"}
 
 
+def band_cells(counts, La, mean_len):
+    """DP cells the band path computes per pass: W diagonals x (La + Lb) / 2 anti-diagonal steps per read
+    and level (16 and 32), the full La x Lb matrix for the exact kernel, none for exact copies."""
+    steps = (La + mean_len) / 2.0
+    return (counts["band16"] * 16 * steps + counts["band32"] * 32 * steps + counts["exact_kernel"] * La * mean_len)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -232,79 +351,91 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--reads", type=int, default=READS_PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=300_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-1t", type=int, default=20_000)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="threads of the CPU baseline (default: the box's CPU share, at most 16)")
+    ap.add_argument("--sample-every", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the oracle sample check of the timed batch")
     ap.add_argument("--no-quant", action="store_true", help="skip the downstream quantification leg")
     ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
-    ap.add_argument("--no-merge", action="store_true", help="skip the paired-end merge leg (N = 1 only)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the C3 / merge legs (N = 1 only)")
     ap.add_argument("--merge-pairs", type=int, default=1_000_000)
     args = ap.parse_args()
 
-    rank, local, world, dist = dist_setup(args.gpus)
-    from crispresso_amd import synth
+    rank, local, world, dist = dist_setup()
+    from crispresso_amd import _lib, synth
     from crispresso_amd.aligner import GpuAligner
 
     amplicon = synth.random_amplicon(AMPLICON_LEN, 1)
     seed = 2 if world == 1 else 10 + rank
     t0 = time.perf_counter()
     buf, offsets = synth.reads_from(amplicon, args.reads, seed)
-    log(f"[rank {rank}] generated {args.reads} reads in {time.perf_counter() - t0:.1f}s")
+    n = len(offsets) - 1
+    log(f"[rank {rank}] generated {n} reads in {time.perf_counter() - t0:.1f}s")
 
     al = GpuAligner(local)
     al.set_reference(amplicon)
-    al.upload(buf, offsets)
+    # the host batch and the outputs in pinned memory (an ingest pipeline reads FASTQ straight into such buffers)
+    pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(offsets)
+    p_stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
+    p_off = _lib.PinnedBuffer(n + 1, np.int64)
+    p_ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
+    out = (p_stats.array, p_ops.array, p_off.array)
     for _ in range(args.warmup):
-        al.run_async()
-        al.sync()
+        al.align_ops(pb.array, po.array, out=out)
 
-    barrier(dist, local)
-    kernel_ms = []
-    split = []
+    barrier(dist)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        al.run_async()
-        kernel_ms.append(al.sync())
-        split.append(al.kernel_times())
-    barrier(dist, local)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(dist, local, elapsed)
+        ob = al.align_ops(pb.array, po.array, out=out)   # synchronous: records + runs are in host memory
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    pcie = al.ops_times()
+    n_runs = int(ob.ops_off[n])
 
-    algo_bytes = al.algo_bytes()       # per launch, from this batch's own results
-    cells = al.cells()
-    geo = al.geometry()
-    geo["fallback_reads"] = al.fallbacks()
-    avg_ms = float(np.mean(kernel_ms))
-    split_ms = {k: float(np.mean([d[k] for d in split])) for k in split[0]} if split else {}
-    achieved_gbs = algo_bytes / (avg_ms * 1e-3) / 1e9
-    gcups = cells / (avg_ms * 1e-3) / 1e9
+    t1 = time.perf_counter()
+    ob.expand(amplicon, pb.array, po.array, nthreads=args.cpu_threads)
+    expand_s = time.perf_counter() - t1
+
+    check = None if args.no_check else sample_check(amplicon, buf, offsets, ob, args.sample_every, args.cpu_threads)
+
+    kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
+    geo["fallback_reads"] = counts["exact_kernel"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(amplicon, buf, offsets, min(args.cpu_sample, args.reads), args.cpu_threads)
+        cpu = cpu_baseline(amplicon, buf, offsets, min(args.cpu_sample, n), args.cpu_threads,
+                           min(args.cpu_sample_1t, n))
 
     quant = None
     if not args.no_quant:
-        quant = quant_leg(al, amplicon, args.reads, args.steps, args.warmup, dist, local, rank, world,
-                          args.quant_cpu_sample, args.no_cpu)
+        quant = quant_leg(al, amplicon, buf, offsets, n, args.steps, args.warmup, rank, world, args.quant_cpu_sample,
+                          args.no_cpu)
 
-    merge = None
-    if rank == 0 and world == 1 and not args.no_merge:
-        try:
-            merge = merge_leg(local, args.merge_pairs)
-        except Exception as exc:   # informational leg: never costs the bench line
-            merge = {"error": f"{type(exc).__name__}: {exc}"}
+    dual = merge = None
+    if rank == 0 and world == 1 and not args.no_legs:
+        for name in ("dual", "merge"):
+            try:   # informational legs: never cost the bench line
+                if name == "dual":
+                    dual = dual_leg(local, args.reads, args.steps, args.warmup)
+                else:
+                    merge = merge_leg(local, args.merge_pairs)
+            except Exception as exc:
+                r = {"error": f"{type(exc).__name__}: {exc}"}
+                dual, merge = (r, merge) if name == "dual" else (dual, r)
 
-    diag = geo["tb_mode"].startswith("diag")
-    if diag:
-        traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                           required="nw::nw_band_fill<16>")
-    elif geo["tb_mode"].startswith("stream"):
-        traffic, traffic_src = pmc_traffic("void nw::nw_stream_fill", "void nw::nw_stream_walk", "void nw::nw_align_kernel",
-                                           required="void nw::nw_stream_fill")
-    else:
-        traffic, traffic_src = None, None
-    total_reads = args.reads * world * args.steps
-    value = total_reads / elapsed
+    traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
+                                       "nw::nw_ops_", required="nw::nw_band_fill<16>")
+    summ, summ_src = pmc_summary("nw_band_fill<16>")
+    fill_valu = None
+    if summ:
+        fill_valu = next((v.get("SQ_INSTS_VALU") for k, v in summ.items() if "nw_band_fill<16>" in k), None)
+    lens = np.diff(offsets)
+    cells = band_cells(counts, AMPLICON_LEN, float(lens.mean()) if n else 0.0)
+    pass_gbs = algo_bytes / (kms * 1e-3) / 1e9
+    fill_ms = phases["fill16_ms"]
+    value = n * world * args.steps / elapsed
     if rank == 0:
         line = {
             "metric": "aligned reads/sec (250 bp amplicon x 1M reads) at 1/2/4/8 MI355X",
@@ -317,52 +448,75 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int16x2" if geo["tb_mode"].startswith(("pair", "stream", "diag")) else "int32",
+            "dtype": "int16x2",
             "data": "synthetic (SURVEY 8d C2 mix: 60% exact, 20% 1-3 subs, 10% del, 5% ins, 5% 1% noise)",
             "config": {
-                "workload": f"C2: {args.reads} synthetic ~250 bp reads x 250 bp amplicon per GPU, "
-                            "EMBOSS needle semantics (EDNAFULL, gapopen 10, gapextend 0.5, free end gaps)",
-                "reads_per_gpu": args.reads,
+                "workload": f"C2: {n} synthetic ~250 bp reads x 250 bp amplicon per GPU, EMBOSS needle semantics "
+                            "(EDNAFULL, gapopen 10, gapextend 0.5, free end gaps); step = one nw_align_ops call, "
+                            "pinned host reads in -> records + traceback runs in pinned host memory",
+                "reads_per_gpu": n,
                 "amplicon_len": AMPLICON_LEN,
-                "parallelism": f"read shards x{world} (no collective on the data path)",
+                "parallelism": f"read shards x{world} (no collective on the data path; gloo host barrier)",
                 "kernel_geometry": geo,
             },
+            "pcie": {
+                "h2d_ms": pcie["h2d_ms"], "h2d_bytes": pcie["h2d_bytes"],
+                "h2d_gbs": pcie["h2d_bytes"] / max(pcie["h2d_ms"], 1e-9) / 1e6,
+                "d2h_bytes": pcie["d2h_bytes"], "compute_ms_in_call": pcie["compute_ms"],
+                "runs_per_read": n_runs / max(n, 1),
+                "note": "last timed call: upload span on the copy stream; d2h = records (32 B) + run offsets (8 B) "
+                        "per read + 4 B per run; compute = the chunks' kernel spans summed (overlapped with the copies)",
+            },
+            "kernel_rate": {
+                "value": n / (kms * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms, "phases_ms": phases,
+                "path_counts": counts,
+                "note": "the call's kernels + ops compaction on the batch resident in HBM, outputs left in HBM "
+                        "(HIP events on the aligner's stream)",
+            },
+            "expand": {"ms": expand_s * 1e3, "reads_per_s": n / expand_s, "threads": args.cpu_threads,
+                       "note": "nw_expand_ops: the three rows of every read rebuilt from its runs on the host "
+                               "(not in value)"},
+            "sample_check": check,
             "roofline": {
                 "bound": "hbm",
-                "achieved": achieved_gbs,
+                "achieved": pass_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "frac": pass_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same bench "
-                                  "command, per launch of fill + walk + fallback)",
-                "kernel": ("nw_band_classify (exact copies, no DP) + length sort + nw_band_fill<16> + "
-                           "nw_band_walk<16> (certified 16-diagonal band) + nw_band_fill/walk<32> on its redo list "
-                           "+ nw_align_kernel on what neither band certifies" if diag
-                           else f"nw_stream_fill<{geo['rows_per_lane']}> + nw_stream_walk<{geo['rows_per_lane']}>"
-                           if geo["tb_mode"].startswith("stream")
-                           else f"nw_align_kernel<{geo['rows_per_lane']},{geo['tb_mode']}>"),
-                "kernel_ms_avg": avg_ms,
-                "kernel_ms_split": split_ms,
-                "achieved_def": "algorithmic bytes / device time of the whole batch (fill + walk + fallback "
-                                "kernels, HIP events on the aligner's stream)",
+                "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the bench "
+                                  "command, per pass of the band kernels + exact kernel + compaction)",
+                "kernel": "one aligner pass: nw_band_classify + length sort + nw_band_fill<16> + nw_band_walk<16> "
+                          "+ the 32-diagonal level on its redo list + nw_align_kernel on what neither band "
+                          "certifies + nw_ops compaction",
+                "kernel_ms_avg": kms,
+                "achieved_def": "algorithmic bytes of the pass / its device time (HIP events on the aligner's "
+                                "stream, batch resident in HBM)",
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",
                 "valu": {
-                    "gcups": gcups,
-                    "cells_per_launch": cells,
-                    "note": ("gcups counts the full La x Lb matrix of every read (the work the reference's needle "
-                             "does); the certified bands compute 16 (or 32) diagonals per read, exact copies none, and "
-                             "prove the rest cannot "
-                             "change the result (DESIGN.md §4)" if diag else
-                             "the DP is a dependent integer recurrence: VALU-bound, HBM frac is small by construction"),
+                    "kernel": "nw_band_fill<16> (the largest phase)",
+                    "fill16_ms": fill_ms,
+                    "valu_instructions_per_launch": fill_valu,
+                    "valu_source": summ_src,
+                    "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
+                    "issue_peak_per_s": VALU_ISSUE_PEAK,
+                    "band_cells_per_pass": cells,
+                    "band_gcups": cells / (kms * 1e-3) / 1e9,
+                    "note": "issue_frac = SQ_INSTS_VALU of one fill<16> launch (PMC, chip total) / its live HIP-event "
+                            "time / (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); band cells = "
+                            "cells the bands and the exact kernel actually compute (W x (La + Lb)/2 per read and "
+                            "level), not the La x Lb matrices the certificate makes unnecessary",
                 },
             },
             "cpu_baseline": cpu,
+            "dual_alignment": dual,
             "downstream_quantification": quant,
             "upstream_merge": merge,
         }
         print(json.dumps(line), flush=True)
+    for b in (pb, po, p_stats, p_off, p_ops):
+        b.close()
     al.close()
     if dist is not None:
         dist.destroy_process_group()

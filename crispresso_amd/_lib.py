@@ -24,9 +24,12 @@ NW_E_UNSUPPORTED = -3
 NW_E_HIP = -4
 NW_E_NOMEM = -5
 NW_E_STATE = -6
+NW_E_CAPACITY = -7
 NW_TIE_EMBOSS = 0
 NW_FLAG_EMPTY = 1
-TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 3: "pair-band-int16", 4: "stream-int16", 5: "diag-int16"}
+NW_OUT_ROWS, NW_OUT_OPS = 0, 1
+NW_RUN_M, NW_RUN_X, NW_RUN_Y = 0, 1, 2
+TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 4: "stream-int16", 5: "diag-int16"}
 
 # Field order of nw_stat (include/crispr_nw.h).
 STAT_FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j", "flags")
@@ -39,6 +42,8 @@ EXPORTS = (
     "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
+    "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
+    "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -115,6 +120,18 @@ def load() -> ctypes.CDLL:
                                    c_void_p, c_int64, c_void_p]),
         "nw_required_stride_multi": (c_int64, [c_void_p, c_int32, c_int32]),
         "nw_batch_device_output": (c_int, [ctx_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)]),
+        "nw_batch_set_output": (c_int, [ctx_p, c_int]),
+        "nw_batch_phase_times": (c_int, [ctx_p, c_void_p]),
+        "nw_batch_path_counts": (c_int, [ctx_p, c_void_p]),
+        "nw_batch_download_ops": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p]),
+        "nw_align_ops": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
+        "nw_ops_times": (c_int, [ctx_p, POINTER(c_float), POINTER(c_float), POINTER(c_int64), POINTER(c_int64)]),
+        "nw_host_alloc": (c_int, [c_int64, POINTER(c_void_p)]),
+        "nw_host_free": (None, [c_void_p]),
+        "nw_host_register": (c_int, [c_void_p, c_int64]),
+        "nw_host_unregister": (c_int, [c_void_p]),
+        "nw_expand_ops": (c_int, [c_char_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_int32]),
         "nwf_merge_batch": (c_int, [c_int, POINTER(NwfParams)] + [c_void_p] * 6 + [c_int64] + [c_void_p] * 4
                             + [POINTER(c_float)]),
         "nwf_last_error": (c_char_p, []),
@@ -156,3 +173,39 @@ def exported_symbols() -> dict:
 
 def ptr(a: np.ndarray) -> int:
     return a.ctypes.data if a is not None else 0
+
+
+class PinnedBuffer:
+    """Page-locked host memory (nw_host_alloc) viewed as a numpy array; freed with
+    the object.  Batches in pinned memory let nw_align_ops copy at PCIe rate."""
+
+    def __init__(self, shape, dtype):
+        self.lib = load()
+        dtype = np.dtype(dtype)
+        count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+        nbytes = max(count * dtype.itemsize, 1)
+        p = ctypes.c_void_p()
+        if self.lib.nw_host_alloc(nbytes, ctypes.byref(p)) != NW_OK:
+            raise NativeLibraryError(f"nw_host_alloc({nbytes}) failed")
+        self._p = p.value
+        raw = (ctypes.c_uint8 * nbytes).from_address(self._p)
+        self.array = np.frombuffer(raw, dtype=np.uint8)[: count * dtype.itemsize].view(dtype).reshape(shape)
+
+    def close(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            self.lib.nw_host_free(self._p)
+            self._p = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pinned_copy(a: np.ndarray) -> PinnedBuffer:
+    """A pinned copy of `a` (same shape and dtype)."""
+    pb = PinnedBuffer(a.shape, a.dtype)
+    pb.array[...] = a
+    return pb

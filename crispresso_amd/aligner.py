@@ -11,6 +11,7 @@ srspair text, plus the text itself when a file is wanted.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple
 
@@ -86,6 +87,57 @@ class AlignmentBatch:
 
     def empty(self, i: int) -> bool:
         return bool(self.stats["flags"][i] & _lib.NW_FLAG_EMPTY)
+
+
+@dataclass
+class OpsBatch:
+    """Alignments of one batch as traceback runs (nw_align_ops): what crosses PCIe.
+
+    Read r's runs are ``ops[ops_off[r]:ops_off[r + 1]]`` (``type << 28 | length``,
+    start -> end; ``_lib.NW_RUN_M / X / Y``).  :meth:`expand` rebuilds the three
+    alignment rows on the host (``nw_expand_ops``)."""
+
+    stats: np.ndarray        # structured, _lib.STAT_DTYPE
+    ops: np.ndarray          # uint32 runs
+    ops_off: np.ndarray      # int64 [n + 1]
+    read_lens: np.ndarray    # int64 [n]
+    scale: int
+    awidth: int = 5000
+
+    def __len__(self) -> int:
+        return len(self.stats)
+
+    def runs(self, i: int) -> List[Tuple[int, int]]:
+        seg = self.ops[self.ops_off[i]:self.ops_off[i + 1]]
+        return [(int(v) >> 28, int(v) & 0x0FFFFFFF) for v in seg]
+
+    def expand(self, reference: str, buf: np.ndarray, offsets: np.ndarray, nthreads: int = 0,
+               rows: Optional[np.ndarray] = None) -> "AlignmentBatch":
+        """The three rows per read (host C++, ``nthreads`` threads; 0 = all cores)."""
+        lib = _lib.load()
+        n = len(self)
+        ref = reference.encode("ascii")
+        max_len = int(self.read_lens.max()) if n else 1
+        stride = (len(ref) + max(max_len, 1) + 15) & ~15
+        if rows is None:
+            rows = np.zeros((n, 3, stride), dtype=np.uint8)
+        buf = np.ascontiguousarray(buf)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        ops = np.ascontiguousarray(self.ops, dtype=np.uint32)
+        rc = lib.nw_expand_ops(ref, len(ref), _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(ops) if len(ops) else None,
+                               _lib.ptr(self.ops_off), _lib.ptr(rows), rows.shape[2], int(nthreads))
+        if rc != _lib.NW_OK:
+            raise NeedleError(f"nw_expand_ops: runs do not match the reads (code {rc})")
+        return AlignmentBatch(self.stats, rows, self.read_lens, self.scale, self.awidth)
+
+
+def default_output_mode() -> str:
+    """``CRISPR_NW_OUTPUT``: "ops" (default: runs over PCIe, rows built on the host)
+    or "rows" (the kernels write the rows, which cross PCIe)."""
+    mode = os.environ.get("CRISPR_NW_OUTPUT", "ops")
+    if mode not in ("ops", "rows"):
+        raise ValueError(f"CRISPR_NW_OUTPUT={mode!r}: expected 'ops' or 'rows'")
+    return mode
 
 
 class GpuAligner:
@@ -176,6 +228,18 @@ class GpuAligner:
                     "nw_batch_kernel_times")
         return dict(zip(("fill_ms", "walk_ms", "rest_ms"), (float(v.value) for v in vals)))
 
+    def phase_times(self) -> dict:
+        """Device ms of the last run by band-path phase (nw_batch_phase_times)."""
+        v = np.zeros(5, np.float32)
+        self._check(self.lib.nw_batch_phase_times(self._h, _lib.ptr(v)), "nw_batch_phase_times")
+        return dict(zip(("sort_ms", "fill16_ms", "walk16_ms", "level32_ms", "rest_ms"), map(float, v)))
+
+    def path_counts(self) -> dict:
+        """Reads of the last run by path (nw_batch_path_counts)."""
+        v = np.zeros(4, np.int64)
+        self._check(self.lib.nw_batch_path_counts(self._h, _lib.ptr(v)), "nw_batch_path_counts")
+        return dict(zip(("exact_copies", "band16", "band32", "exact_kernel"), map(int, v)))
+
     def device_output(self):
         """(d_aln, stride, d_stats) device pointers of the last run's resident output
         (nw_batch_device_output); valid until the next upload / align."""
@@ -193,12 +257,70 @@ class GpuAligner:
         lens = np.diff(self._off)
         return AlignmentBatch(stats, aln, lens, self.scale, self.options.awidth)
 
+    def set_output(self, mode: str) -> None:
+        """Output mode of the upload/run path: "rows" (default) or "ops"; from the next upload."""
+        self._check(self.lib.nw_batch_set_output(self._h, _lib.NW_OUT_OPS if mode == "ops" else _lib.NW_OUT_ROWS),
+                    "nw_batch_set_output")
+
+    def download_ops(self, n: int) -> OpsBatch:
+        stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+        ops_off = np.zeros(n + 1, dtype=np.int64)
+        cap = 2 * n + 4096
+        ops = np.empty(cap, dtype=np.uint32)
+        rc = self.lib.nw_batch_download_ops(self._h, _lib.ptr(ops), cap, _lib.ptr(ops_off), _lib.ptr(stats))
+        if rc == _lib.NW_E_CAPACITY:
+            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            rc = self.lib.nw_batch_download_ops(self._h, _lib.ptr(ops), len(ops), _lib.ptr(ops_off), _lib.ptr(stats))
+        self._check(rc, "nw_batch_download_ops")
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(self._off), self.scale, self.options.awidth)
+
     # -- synchronous path ----------------------------------------------------
-    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True) -> AlignmentBatch:
-        """Align a packed batch.  ``strings=False`` copies back only the per-read
-        records (identity, score, ...): what a ``just_score`` pass (CORE:1740-1741) reads."""
+    def align_ops(self, buf: np.ndarray, offsets: np.ndarray, out: Optional[tuple] = None) -> OpsBatch:
+        """The call-level path (nw_align_ops): host reads in, records + runs out.
+
+        ``out`` = (stats, ops, ops_off) preallocated (e.g. pinned) arrays; by default
+        they are allocated here.  An ops array too small for the batch is replaced."""
         if self.reference is None:
             raise NeedleError("no amplicon set")
+        n = len(offsets) - 1
+        if out is None:
+            stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+            ops_off = np.zeros(n + 1, dtype=np.int64)
+            ops = np.empty(2 * n + 4096, dtype=np.uint32)
+        else:
+            stats, ops, ops_off = out
+        rc = self.lib.nw_align_ops(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(ops), len(ops),
+                                   _lib.ptr(ops_off), _lib.ptr(stats))
+        if rc == _lib.NW_E_CAPACITY:   # rare: more runs than the buffer holds; run again with the size it said
+            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            rc = self.lib.nw_align_ops(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(ops), len(ops),
+                                       _lib.ptr(ops_off), _lib.ptr(stats))
+        self._check(rc, "nw_align_ops")
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(offsets), self.scale, self.options.awidth)
+
+    def ops_times(self) -> dict:
+        """Last align_ops: upload span (ms), summed kernel spans (ms), bytes each way."""
+        h2d, comp = ctypes.c_float(), ctypes.c_float()
+        hb, db = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.nw_ops_times(self._h, ctypes.byref(h2d), ctypes.byref(comp), ctypes.byref(hb),
+                                          ctypes.byref(db)), "nw_ops_times")
+        return {"h2d_ms": float(h2d.value), "compute_ms": float(comp.value), "h2d_bytes": int(hb.value),
+                "d2h_bytes": int(db.value)}
+
+    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True,
+                     mode: Optional[str] = None) -> AlignmentBatch:
+        """Align a packed batch.  ``strings=False`` copies back only the per-read
+        records (identity, score, ...): what a ``just_score`` pass (CORE:1740-1741) reads.
+        ``mode`` "ops" (default, :func:`default_output_mode`): runs cross PCIe and the
+        rows are built on the host; "rows": the kernels write the rows."""
+        if self.reference is None:
+            raise NeedleError("no amplicon set")
+        if (mode or default_output_mode()) == "ops":
+            ob = self.align_ops(buf, offsets)
+            if not strings:
+                return AlignmentBatch(ob.stats, np.empty((len(ob), 3, 0), np.uint8), ob.read_lens, self.scale,
+                                      self.options.awidth)
+            return ob.expand(self.reference, buf, offsets)
         n = len(offsets) - 1
         lens = np.diff(offsets)
         max_len = int(lens.max()) if n else 1

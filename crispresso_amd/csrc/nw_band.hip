@@ -226,6 +226,17 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             for (int t = 0; t < 4; ++t) {
                 if (us[t] < 0 || __ballot(diff[t] != 0u) != 0ull) continue;
                 exact |= 1ull << us[t];
+                if (a.ops) {   // ops output: one M run of La columns, no rows
+                    if (lane == 0) {
+                        a.ops[(r0 + us[t]) * a.ops_slot] = ((unsigned)RUN_M << 28) | (unsigned)La;
+                        a.nops[r0 + us[t]] = 1;
+                    }
+                    if (lane < 8) {
+                        const int v = lane == 3 || lane == 7 ? 0 : (lane == 4 ? a.band_maxsub * La : La);
+                        ((int*)(a.stats + r0 + us[t]))[lane] = v;
+                    }
+                    continue;
+                }
                 if (!one_chunk) {
                     emit_later |= 1ull << us[t];
                     continue;
@@ -871,7 +882,7 @@ __host__ __device__ inline int band_walk_wave_bytes(int La, int lb_max) {
 // emit_alignment (nw_common.h) with the three rows built in LDS (byte writes) and
 // written out as dwordx4 rows: 16 B per lane instead of a byte store per column.
 // The rows are padded to 16 B; the host reads aln_len columns of each.
-template <class Score>
+template <bool ROWS, class Score>
 __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* amp, const unsigned char* raw,
                           const unsigned char* lut, const Score& sim_score, unsigned char* rows, int row,
                           unsigned char* o_ref, int64_t stride, int score, int ei, int ej, Stat* st, int lane) {
@@ -902,13 +913,17 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
                     } else {
                         ++same;
                     }
-                    rows[col + p] = ca;
-                    rows[row + col + p] = mk;
-                    rows[2 * row + col + p] = cb;
+                    if constexpr (ROWS) {
+                        rows[col + p] = ca;
+                        rows[row + col + p] = mk;
+                        rows[2 * row + col + p] = cb;
+                    }
                 }
             }
             n_id += same;
             n_sim += same;
+        } else if constexpr (!ROWS) {   // gap run: n gap columns
+            if (lane == 0) n_gap += n;
         } else {   // gap run: every column is a gap
             const unsigned char* src = type == RUN_X ? raw + jb : amp + ia;
             unsigned char* dst = rows + (type == RUN_X ? 2 * row : 0) + col;
@@ -927,8 +942,8 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
         if (type != RUN_X) ia += n;
         if (type != RUN_Y) jb += n;
     }
-    lds_fence();
-    for (int c = 16 * lane; c < col; c += 1024) {
+    if constexpr (ROWS) lds_fence();
+    for (int c = 16 * lane; ROWS && c < col; c += 1024) {
         const uint4 r0 = *(const uint4*)(rows + c), r1 = *(const uint4*)(rows + row + c),
                     r2 = *(const uint4*)(rows + 2 * row + c);
         *(uint4*)(o_ref + c) = r0;
@@ -1081,8 +1096,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         lds_fence();
         auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
-        band_emit(runs, nruns, amp_lds, rbuf + mis, lut_lds, sim, rows, row, a.out + rd * 3 * a.stride, a.stride, score, ei,
-                  ej, a.stats + rd, lane);
+        if (a.ops) {
+            store_ops(a, rd, runs, nruns, lane);
+            band_emit<false>(runs, nruns, amp_lds, rbuf + mis, lut_lds, sim, rows, row, nullptr, 0, score, ei, ej,
+                             a.stats + rd, lane);
+        } else {
+            band_emit<true>(runs, nruns, amp_lds, rbuf + mis, lut_lds, sim, rows, row, a.out + rd * 3 * a.stride, a.stride,
+                            score, ei, ej, a.stats + rd, lane);
+        }
         lds_fence();
     }
 }

@@ -238,10 +238,35 @@ __device__ int walk_runs_wide(const Nib& nib, int La, int Lb, int ei, int ej, un
 // Writes the aligned amplicon / markup / aligned read for the runs (forward
 // order) and the per-read record.  `sim_score(ai, code)` is the substitution
 // score of amplicon row ai against residue code (only its sign matters).
+// Ops output (KernelArgs::ops): the runs (LDS, end -> start order) of read rd, start
+// -> end, into its slot, or -- more runs than a slot holds -- into the spill area
+// (bump-allocated, the position in slot[0]).  A full spill area sets ops_ctl[1]
+// (the host reports it).  Rows are not written in this mode.
+__device__ inline void store_ops(const KernelArgs& a, long long rd, const unsigned* runs, int nruns, int lane) {
+    uint32_t* slot = a.ops + rd * a.ops_slot;
+    uint32_t* dst = slot;
+    if (nruns > a.ops_slot) {
+        int pos = 0;
+        if (lane == 0) pos = atomicAdd(a.ops_ctl, nruns);
+        pos = __builtin_amdgcn_readfirstlane(pos);
+        if ((long long)pos + nruns > a.spill_cap) {
+            if (lane == 0) {
+                atomicOr(a.ops_ctl + 1, 1);
+                a.nops[rd] = 0;
+            }
+            return;
+        }
+        if (lane == 0) slot[0] = (uint32_t)pos;
+        dst = a.spill + pos;
+    }
+    if (lane == 0) a.nops[rd] = nruns;
+    for (int q = lane; q < nruns; q += 64) dst[q] = runs[nruns - 1 - q];
+}
+
 template <class Score>
 __device__ void emit_alignment(const unsigned* runs, int nruns, const unsigned char* amp, const unsigned char* raw,
                                const unsigned char* lut, const Score& sim_score, unsigned char* o_ref,
-                               int64_t stride, int score, int ei, int ej, Stat* st, int lane) {
+                               int64_t stride, int score, int ei, int ej, Stat* st, int lane, bool rows = true) {
     unsigned char* o_mk = o_ref + stride;
     unsigned char* o_rd = o_mk + stride;
     int col = 0, ia = 0, jb = 0;
@@ -265,9 +290,11 @@ __device__ void emit_alignment(const unsigned* runs, int nruns, const unsigned c
                 n_id += id;
                 n_sim += sim;
             }
-            o_ref[col + p] = ca;
-            o_mk[col + p] = mk;
-            o_rd[col + p] = cb;
+            if (rows) {
+                o_ref[col + p] = ca;
+                o_mk[col + p] = mk;
+                o_rd[col + p] = cb;
+            }
         }
         col += n;
         if (type != RUN_X) ia += n;

@@ -11,6 +11,7 @@ constexpr int NCODE = 17;
 constexpr int NCODE_PAD = 16;   // code used for columns past the end of a read
 
 enum : int32_t { FLAG_EMPTY = 1 };
+constexpr int kOpsSlot = 64;    // runs kept per read in its ops slot (more: spill area)
 
 // Per-read record written by the kernel; layout matches nw_stat in include/crispr_nw.h.
 struct Stat {
@@ -68,10 +69,20 @@ struct KernelArgs {
                                    // or the previous level's redo count)
     int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
     int32_t* redo_count;
+    // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
+    // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
+    // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
+    // spill area (bump-allocated words, the position in slot[0]).  null ops = rows.
+    uint32_t* ops;
+    int32_t ops_slot;
+    int32_t* nops;                 // [n] runs per read (0: empty read)
+    uint32_t* spill;
+    int64_t spill_cap;             // words
+    int32_t* ops_ctl;              // [0] spill words used, [1] error flag (spill area full)
 };
 
 // Traceback storage of a kernel instantiation.
-enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_PAIR_BAND = 3, TB_STREAM = 4, TB_DIAG = 5 };
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_STREAM = 4, TB_DIAG = 5 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
@@ -86,13 +97,6 @@ int profile_rp(int R);
 int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb);
 int tb_bytes_per_wave(int R, int Lb_max);
 hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
-
-// two-reads-per-wave packed int16 kernel (nw_pair.hip); band storage only.
-// Blocks may hold up to kPairMaxThreads threads (its __launch_bounds__).
-constexpr int kPairMaxThreads = 512;
-int pair_lds_bytes_for(int R, int La, int Lb_max, int band_slots, int wpb);
-int pair_profile_bytes_per_lane(int R);
-hipError_t launch_pair(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
 // streaming fill + walk kernels (nw_stream.hip).  Pair p's region starts at
 // region + p * stride: traceback band [8 lane groups][slots][8 lanes][NG] words, captures
@@ -127,5 +131,23 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
+
+// ops compaction (nw_ops.hip): per-read slots -> one contiguous run array.
+// ctl (int64, kOpsCtl): [0] running base over the chunks of a call (in/out), [1] this chunk's
+// base, [2] this chunk's total, [3] errors (1: staging full, 2: spill area full, from
+// opsctl[1]); running over the call: [4] exact-kernel reads, [5] second band level reads,
+// [6] reads that needed the DP (OpsCounts: the device counters of the chunk's kernels).
+// blk: ceil(n / kOpsBlockReads) int64.
+constexpr int kOpsBlockReads = 1024;
+constexpr int kOpsCtl = 8;
+struct OpsCounts {
+    const int32_t* fallback;   // [4 * passes]: [4 q] exact-kernel reads of pass q
+    int passes;
+    const int32_t* redo;       // second band level reads (null: one level)
+    const int32_t* band;       // reads that needed the DP (null: not the band path)
+};
+hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
+                              int64_t* blk, int64_t* ctl, int64_t* ops_off, uint32_t* staging, int64_t staging_cap,
+                              const int32_t* opsctl, const OpsCounts& cnt, hipStream_t s);
 
 }  // namespace nw

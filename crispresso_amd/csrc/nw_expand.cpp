@@ -1,0 +1,124 @@
+// nw_expand.cpp -- host expansion of the ops output into alignment rows.
+//
+// nw_align_ops returns every read's traceback as runs (include/crispr_nw.h); the
+// rows EMBOSS needle prints -- aligned amplicon, markup, aligned read, the strings
+// parse_needle_output slices out of the srspair block (CRISPRessoCORE.py:1747-1754)
+// -- are a function of the runs and the two sequences.  This builds them exactly as
+// the kernels do in NW_OUT_ROWS mode (nw_common.h emit_alignment):
+//   M column: '|' when the residues are equal ignoring case, ':' when EDNAFULL scores
+//             the pair > 0, '.' otherwise; a '-' already in the input (RC-retry reads,
+//             CORE:1846) is printed as is with markup ' ';
+//   X / Y column: '-' opposite the residue, markup ' '.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/crispr_nw.h"
+#include "nw_edna.h"
+
+namespace {
+
+struct Tables {
+    unsigned char up[256];
+    uint8_t code[256];
+    bool pos[17][256];   // EDNAFULL(code a, byte b) > 0
+    Tables() {
+        for (int b = 0; b < 256; ++b) {
+            up[b] = (unsigned char)std::toupper(b);
+            code[b] = nw::code_of((unsigned char)b);
+        }
+        for (int a = 0; a < 17; ++a)
+            for (int b = 0; b < 256; ++b) pos[a][b] = a < 16 && code[b] < 16 && nw::kEdna[a][code[b]] > 0;
+    }
+};
+
+const Tables& tables() {
+    static const Tables t;
+    return t;
+}
+
+// one read; false when the runs do not cover both sequences or overflow the row
+bool expand_one(const Tables& T, const unsigned char* ref, int64_t La, const uint8_t* acode, const unsigned char* rd,
+                int64_t Lb, const uint32_t* ops, int64_t nops, char* o0, int64_t stride) {
+    char* o1 = o0 + stride;
+    char* o2 = o1 + stride;
+    int64_t col = 0, ia = 0, jb = 0;
+    for (int64_t q = 0; q < nops; ++q) {
+        const uint32_t type = NW_RUN_TYPE(ops[q]);
+        const int64_t len = NW_RUN_LEN(ops[q]);
+        if (col + len > stride) return false;
+        if (type == NW_RUN_M) {
+            if (ia + len > La || jb + len > Lb) return false;
+            std::memcpy(o0 + col, ref + ia, (size_t)len);
+            std::memcpy(o2 + col, rd + jb, (size_t)len);
+            for (int64_t k = 0; k < len; ++k) {
+                const unsigned char ca = ref[ia + k], cb = rd[jb + k];
+                char mk = '|';
+                if (ca != cb || ca == '-') {
+                    if (ca == '-' || cb == '-') mk = ' ';
+                    else if (T.up[ca] == T.up[cb]) mk = '|';
+                    else mk = T.pos[acode[ia + k]][cb] ? ':' : '.';
+                }
+                o1[col + k] = mk;
+            }
+            ia += len;
+            jb += len;
+        } else if (type == NW_RUN_X) {
+            if (jb + len > Lb) return false;
+            std::memset(o0 + col, '-', (size_t)len);
+            std::memset(o1 + col, ' ', (size_t)len);
+            std::memcpy(o2 + col, rd + jb, (size_t)len);
+            jb += len;
+        } else if (type == NW_RUN_Y) {
+            if (ia + len > La) return false;
+            std::memcpy(o0 + col, ref + ia, (size_t)len);
+            std::memset(o1 + col, ' ', (size_t)len);
+            std::memset(o2 + col, '-', (size_t)len);
+            ia += len;
+        } else {
+            return false;
+        }
+        col += len;
+    }
+    return ia == La && jb == Lb;
+}
+
+}  // namespace
+
+extern "C" int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
+                             const uint32_t* ops, const int64_t* ops_off, char* aln_out, int64_t stride,
+                             int32_t nthreads) {
+    if (n < 0 || ref_len <= 0 || !ref || (n > 0 && (!reads || !offsets || !ops_off || !aln_out))) return NW_E_INVALID;
+    const Tables& T = tables();
+    std::vector<uint8_t> acode((size_t)ref_len);
+    for (int32_t i = 0; i < ref_len; ++i) acode[(size_t)i] = T.code[(unsigned char)ref[i]];
+    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
+    std::atomic<int> bad{0};
+    auto work = [&](int64_t lo, int64_t hi) {
+        for (int64_t r = lo; r < hi; ++r) {
+            const int64_t Lb = offsets[r + 1] - offsets[r];
+            const int64_t k0 = ops_off[r], k1 = ops_off[r + 1];
+            if (Lb == 0 && k1 == k0) continue;   // empty read: no alignment
+            if (k1 < k0 || !ops ||
+                !expand_one(T, (const unsigned char*)ref, ref_len, acode.data(),
+                            (const unsigned char*)reads + offsets[r], Lb, ops + k0, k1 - k0, aln_out + r * 3 * stride,
+                            stride))
+                bad.store(1, std::memory_order_relaxed);
+        }
+    };
+    if (nt == 1) {
+        work(0, n);
+    } else {
+        std::vector<std::thread> pool;
+        const int64_t per = (n + nt - 1) / nt;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t lo = t * per, hi = std::min(n, lo + per);
+            if (lo < hi) pool.emplace_back(work, lo, hi);
+        }
+        for (auto& th : pool) th.join();
+    }
+    return bad.load() ? NW_E_INVALID : NW_OK;
+}

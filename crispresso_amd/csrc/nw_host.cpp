@@ -19,34 +19,9 @@
 
 #include "../../include/crispr_nw.h"
 #include "nw_device.h"
+#include "nw_edna.h"
 
 namespace {
-
-// EDNAFULL (NCBI NUC.4.4), order A T G C S W R Y K M B V H D N U.
-const signed char kEdna[16][16] = {
-    {5, -4, -4, -4, -4, 1, 1, -4, -4, 1, -4, -1, -1, -1, -2, -4},
-    {-4, 5, -4, -4, -4, 1, -4, 1, 1, -4, -1, -4, -1, -1, -2, 5},
-    {-4, -4, 5, -4, 1, -4, 1, -4, 1, -4, -1, -1, -4, -1, -2, -4},
-    {-4, -4, -4, 5, 1, -4, -4, 1, -4, 1, -1, -1, -1, -4, -2, -4},
-    {-4, -4, 1, 1, -1, -4, -2, -2, -2, -2, -1, -1, -3, -3, -1, -4},
-    {1, 1, -4, -4, -4, -1, -2, -2, -2, -2, -3, -3, -1, -1, -1, 1},
-    {1, -4, 1, -4, -2, -2, -1, -4, -2, -2, -3, -1, -3, -1, -1, -4},
-    {-4, 1, -4, 1, -2, -2, -4, -1, -2, -2, -1, -3, -1, -3, -1, 1},
-    {-4, 1, 1, -4, -2, -2, -2, -2, -1, -4, -1, -3, -3, -1, -1, 1},
-    {1, -4, -4, 1, -2, -2, -2, -2, -4, -1, -3, -1, -1, -3, -1, -4},
-    {-4, -1, -1, -1, -1, -3, -3, -1, -1, -3, -1, -2, -2, -2, -1, -1},
-    {-1, -4, -1, -1, -1, -3, -1, -3, -3, -1, -2, -1, -2, -2, -1, -4},
-    {-1, -1, -4, -1, -3, -1, -3, -1, -3, -1, -2, -2, -1, -2, -1, -1},
-    {-1, -1, -1, -4, -3, -1, -1, -3, -1, -3, -2, -2, -2, -1, -1, -1},
-    {-2, -2, -2, -2, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -2},
-    {-4, 5, -4, -4, -4, 1, -4, 1, 1, -4, -1, -4, -1, -1, -2, 5},
-};
-const char kAlphabet[] = "ATGCSWRYKMBVHDNU";
-
-uint8_t code_of(unsigned char c) {
-    const char* p = std::strchr(kAlphabet, std::toupper(c));
-    return (c && p) ? (uint8_t)(p - kAlphabet) : (uint8_t)nw::NCODE_PAD;
-}
 
 constexpr int kMaxRef = 1024;
 constexpr int kMaxLds = 160 * 1024;
@@ -79,6 +54,8 @@ struct nw_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_fill = nullptr, ev_walk = nullptr;   // after the fill / walk kernels
+    hipEvent_t ev_sort = nullptr, ev_l2 = nullptr;     // band path: after the sort, after the second level
+    bool phases = false;                               // record the phase events (nw_batch_run_async)
     std::string err;
     // params
     float gap_open_f = 10.0f, gap_extend_f = 0.5f;
@@ -107,16 +84,13 @@ struct nw_ctx {
     DevBuf<int64_t> d_fallback;       // reads re-run with full traceback storage
     DevBuf<int32_t> d_fallback_count; // [0] fallback count, [1] pair-kernel work counter
     int band_slots = 64;              // 0 disables the banded kernels
-    int pair_slots = 56;
     bool use_band = false;
-    bool use_pair = false;
     bool use_stream = false;
     int stream_slots = 56;
     int64_t pass_reads = 0;            // reads per fill+walk pass (region memory bound)
     nw::StreamRegion region{};
     DevBuf<uint8_t> d_region;          // per-pair traceback regions of the streaming kernels
     nw::LaunchCfg stream_fill{}, stream_walk{};
-    nw::LaunchCfg pair_cfg{};         // packed int16 two-reads-per-wave kernel
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
     // certified diagonal-band kernels (nw_band.hip): the default path
@@ -132,6 +106,24 @@ struct nw_ctx {
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
     bool ran = false;
+    // ops output (nw_align_ops / nw_batch_set_output(NW_OUT_OPS)): per-read run slots,
+    // spill area, compaction scratch; the pipelined call's copy streams and events
+    int out_mode = NW_OUT_ROWS;
+    int64_t reads_bias = 0;            // kernels index reads with the caller's offsets minus this
+    DevBuf<uint32_t> d_slots, d_spill, d_staging[2];
+    DevBuf<int32_t> d_nops, d_opsctl;
+    DevBuf<int64_t> d_ctl64, d_blk, d_opsoff;
+    int64_t spill_cap = 0, staging_cap = 0;
+    int ops_slot = nw::kOpsSlot;       // runs per read slot (CRISPR_NW_OPS_SLOT: tests force spills)
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    std::vector<hipEvent_t> ev_in, ev_cs, ev_ce, ev_out;
+    hipEvent_t ev_h0 = nullptr;
+    int64_t* h_ctl = nullptr;          // pinned: per chunk ctl[0..3] copied back
+    int64_t h_ctl_chunks = 0;
+    float ops_h2d_ms = 0.0f, ops_compute_ms = 0.0f;
+    bool call_done = false;            // the last operation was nw_align_ops: the getters report its counts
+    int64_t call_counts[4] = {0, 0, 0, 0};
+    int64_t ops_h2d_bytes = 0, ops_d2h_bytes = 0;
 };
 
 namespace {
@@ -161,9 +153,9 @@ int build_profile(nw_ctx* c) {
     const int RP = nw::profile_rp(R);
     std::vector<int8_t> prof((size_t)nw::NCODE * 64 * RP, 0);
     for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+        const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
         for (int code = 0; code < nw::NCODE; ++code) {
-            int s = (ca < 16 && code < 16) ? kEdna[ca][code] * c->scale : 0;
+            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * c->scale : 0;
             prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
         }
     }
@@ -173,10 +165,10 @@ int build_profile(nw_ctx* c) {
     const int nl = (La + R - 1) / R, F = nl * R - La;
     std::vector<int16_t> prof16((size_t)nw::NCODE * 64 * R4, 0);
     for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+        const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
         const int g = ai + F;
         for (int code = 0; code < nw::NCODE; ++code) {
-            int s = (ca < 16 && code < 16) ? kEdna[ca][code] * c->scale : 0;
+            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * c->scale : 0;
             prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
         }
     }
@@ -192,7 +184,7 @@ int build_profile(nw_ctx* c) {
         const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
         uint8_t lut6[256];
         for (int q = 0; q < 256; ++q) {
-            const int code = code_of((unsigned char)q);
+            const int code = nw::code_of((unsigned char)q);
             int r = nw::kPairCodes;   // not in the table
             for (int i = 0; i < nw::kPairCodes; ++i)
                 if (codes[i] == code) r = i;
@@ -228,7 +220,7 @@ int build_profile(nw_ctx* c) {
         const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
         auto sub6 = [&](int x, int y) {
             const int cx = codes6[x], cy = codes6[y];
-            return (cx < 16 && cy < 16) ? kEdna[cx][cy] * c->scale : 0;
+            return (cx < 16 && cy < 16) ? nw::kEdna[cx][cy] * c->scale : 0;
         };
         std::vector<uint32_t> btab(216);
         for (int x = 0; x < 6; ++x)
@@ -241,10 +233,10 @@ int build_profile(nw_ctx* c) {
         std::vector<uint32_t> rowpos((size_t)La);
         c->amp_in_table = true;
         for (int ai = 0; ai < La; ++ai) {
-            const uint8_t ca = code_of((unsigned char)c->ref[ai]);
+            const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
             uint32_t m = 0;
             for (int code = 0; code < nw::NCODE; ++code)
-                if (ca < 16 && code < 16 && kEdna[ca][code] > 0) m |= 1u << code;
+                if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
             rowpos[(size_t)ai] = m;
             bool in6 = false;
             for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
@@ -260,7 +252,7 @@ int build_profile(nw_ctx* c) {
     HIP_OR_FAIL(c, c->d_prof16f.reserve(prof16f.size()));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16f.p, prof16f.data(), prof16f.size() * 2, hipMemcpyHostToDevice, c->stream));
     uint8_t lut[256];
-    for (int q = 0; q < 256; ++q) lut[q] = code_of((unsigned char)q);
+    for (int q = 0; q < 256; ++q) lut[q] = nw::code_of((unsigned char)q);
     HIP_OR_FAIL(c, c->d_prof.reserve(prof.size()));
     HIP_OR_FAIL(c, c->d_lut.reserve(256));
     HIP_OR_FAIL(c, c->d_amp.reserve((size_t)La + 16));
@@ -272,9 +264,13 @@ int build_profile(nw_ctx* c) {
     return NW_OK;
 }
 
+int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n);
+
 int64_t stride_for(int La, int32_t lb_max) { return ((int64_t)La + lb_max + 15) & ~(int64_t)15; }
 
 int configure(nw_ctx* c) {
+    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))   // tests: band width of the full-matrix kernels
+        c->band_slots = c->stream_slots = std::max(0, std::atoi(bs));
     const int La = (int)c->ref.size();
     const int R = c->R;
     // full-storage kernel: every alignment (band disabled) or only the fallbacks
@@ -317,33 +313,9 @@ int configure(nw_ctx* c) {
             c->use_band = true;
         }
     }
-    // packed int16 pair kernel: scores must fit int16 with room for differences
-    c->use_pair = false;
-    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "pair" | "band" | "full" (tests/diagnostics)
-    const bool want_pair = kern && std::strcmp(kern, "pair") == 0;
+    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" | "stream" | "band" | "full" (tests/diagnostics)
     const int64_t hi = 5ll * c->scale * La;
     const bool fits16 = hi + c->gap_extend < 16000 && 9ll * c->scale * La + c->gap_open + c->gap_extend < 32000;
-    if (want_pair && fits16 && c->pair_slots > 0) {
-        nw::LaunchCfg p{};
-        p.R = R;
-        p.tb_mode = nw::TB_PAIR_BAND;
-        // waves per block that maximise resident waves per CU (LDS-limited; the
-        // kernel's registers allow 3 waves per SIMD = 12 per CU at R <= 4)
-        int best_waves = 0;
-        for (int wpb = 1; wpb <= nw::kPairMaxThreads / 64; ++wpb) {
-            const int b = nw::pair_lds_bytes_for(R, La, c->lb_max, c->pair_slots, wpb);
-            if (b <= 0 || b > kMaxLds) break;
-            const int waves = std::min(wpb * (kMaxLds / b), 12);
-            if (waves > best_waves) { best_waves = waves; p.wpb = wpb; p.lds_bytes = b; }
-        }
-        if (best_waves > 0) {
-            per_cu = std::max(1, best_waves / p.wpb);
-            const int64_t want = ((c->n + 1) / 2 + p.wpb - 1) / p.wpb;
-            p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
-            c->pair_cfg = p;
-            c->use_pair = true;
-        }
-    }
     // certified diagonal band (default): scores and biases within int16, amplicon
     // within the band table's alphabet, non-negative gap costs (the certificate)
     c->use_diag = false;
@@ -435,7 +407,6 @@ int configure(nw_ctx* c) {
             c->stream_fill = f;
             c->stream_walk = w;
             c->use_stream = true;
-            c->use_pair = false;
         }
     }
     if (kern && std::strcmp(kern, "full") == 0) c->use_band = false;
@@ -458,8 +429,11 @@ int nw_create(int device, nw_ctx** out) {
     nw_ctx* c = new nw_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&c->ev_h0) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess) {
+        hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess ||
+        hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess) {
         delete c;
         return NW_E_HIP;
     }
@@ -480,7 +454,19 @@ void nw_destroy(nw_ctx* c) {
     c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
     c->d_btab.release(); c->d_rowpos.release(); c->d_redo.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
+    c->d_slots.release(); c->d_spill.release(); c->d_staging[0].release(); c->d_staging[1].release();
+    c->d_nops.release(); c->d_opsctl.release(); c->d_ctl64.release(); c->d_blk.release(); c->d_opsoff.release();
+    if (c->s_in) (void)hipStreamSynchronize(c->s_in);
+    if (c->s_out) (void)hipStreamSynchronize(c->s_out);
+    for (auto* v : {&c->ev_in, &c->ev_cs, &c->ev_ce, &c->ev_out})
+        for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->ev_h0) (void)hipEventDestroy(c->ev_h0);
+    if (c->s_in) (void)hipStreamDestroy(c->s_in);
+    if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
+    if (c->ev_sort) (void)hipEventDestroy(c->ev_sort);
+    if (c->ev_l2) (void)hipEventDestroy(c->ev_l2);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -529,6 +515,7 @@ int nw_set_reference(nw_ctx* c, const char* ref, int32_t ref_len) {
     (void)hipSetDevice(c->device);
     c->ref.assign(ref, ref + ref_len);
     c->ran = false;
+    c->call_done = false;
     return build_profile(c);
 }
 
@@ -541,8 +528,6 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     if (!c) return NW_E_INVALID;
     if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || !reads))) return fail(c, NW_E_INVALID, "bad batch");
-    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))
-        c->band_slots = c->pair_slots = c->stream_slots = std::max(0, std::atoi(bs));
     (void)hipSetDevice(c->device);
     const int La = (int)c->ref.size();
     int32_t lb_max = 1;
@@ -565,14 +550,17 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     c->stride = stride_for(La, lb_max);
     HIP_OR_FAIL(c, c->d_reads.reserve((size_t)nbytes + 512));   // the walk DMAs whole 256-B chunks
     HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
-    HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
+    if (c->out_mode == NW_OUT_ROWS) HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
     if (nbytes) HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, reads + base, (size_t)nbytes, hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, rel.data(), sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->reads_bias = 0;
     int rc = configure(c);
     if (rc) return rc;
+    if (c->out_mode == NW_OUT_OPS && (rc = ops_reserve(c, n, n))) return rc;
     c->ran = false;
+    c->call_done = false;
     return NW_OK;
 }
 
@@ -585,7 +573,7 @@ namespace {
 // Everything is queued on c->stream; nothing synchronises.
 int launch_range(nw_ctx* c, int64_t base) {
     nw::KernelArgs a{};
-    a.reads = c->d_reads.p;
+    a.reads = c->d_reads.p - c->reads_bias;
     a.offsets = c->d_offsets.p + base;
     a.n = c->n;
     a.prof = c->d_prof.p;
@@ -605,6 +593,18 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.band_slots = c->band_slots;
     a.fallback_list = c->d_fallback.p + base;
     a.fallback_count = c->d_fallback_count.p;
+    if (c->out_mode == NW_OUT_OPS) {
+        // runs into chunk-relative slots; rows are not written
+        a.out = nullptr;
+        a.ops = c->d_slots.p;
+        a.ops_slot = c->ops_slot;
+        a.nops = c->d_nops.p;
+        a.spill = c->d_spill.p;
+        a.spill_cap = c->spill_cap;
+        a.ops_ctl = c->d_opsctl.p;
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_nops.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(c->n, 1), c->stream));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_opsctl.p, 0, 2 * sizeof(int32_t), c->stream));
+    }
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
@@ -623,6 +623,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.sort_key = c->d_sort_key.p;
         a.band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->stream));
+        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->stream));
         const int64_t pairs = (c->n + 1) / 2;
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
@@ -650,6 +651,7 @@ int launch_range(nw_ctx* c, int64_t base) {
                 if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
             }
         }
+        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->stream));
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
         a.work_count = c->d_fallback_count.p;
         HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
@@ -664,8 +666,12 @@ int launch_range(nw_ctx* c, int64_t base) {
             nw::KernelArgs ap = a;
             ap.offsets = a.offsets + lo;
             ap.n = hi - lo;
-            ap.out = a.out + lo * 3 * c->stride;
+            ap.out = a.out ? a.out + lo * 3 * c->stride : nullptr;
             ap.stats = a.stats + lo;
+            if (a.ops) {
+                ap.ops = a.ops + lo * a.ops_slot;
+                ap.nops = a.nops + lo;
+            }
             ap.prof = (const int8_t*)c->d_prof16.p;
             ap.prof_fill = c->d_prof16f.p;
             ap.band_slots = c->stream_slots;
@@ -682,6 +688,8 @@ int launch_range(nw_ctx* c, int64_t base) {
             af.n = ap.n;
             af.out = ap.out;
             af.stats = ap.stats;
+            af.ops = ap.ops;
+            af.nops = ap.nops;
             af.work_list = ap.fallback_list;    // exact int32 kernel on what left the band
             af.work_count = ap.fallback_count;
             HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->stream));
@@ -691,14 +699,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
     a.work_counter = c->d_fallback_count.p + 1;
     if (c->n > 0) {
-        if (c->use_pair) {
-            nw::KernelArgs ap = a;
-            ap.prof = (const int8_t*)c->d_prof16.p;
-            ap.band_slots = c->pair_slots;
-            HIP_OR_FAIL(c, nw::launch_pair(ap, c->pair_cfg, c->stream));
-            a.work_list = a.fallback_list;      // re-run what left the band
-            a.work_count = c->d_fallback_count.p;
-        } else if (c->use_band) {
+        if (c->use_band) {
             HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
             a.work_list = a.fallback_list;
             a.work_count = c->d_fallback_count.p;
@@ -708,6 +709,91 @@ int launch_range(nw_ctx* c, int64_t base) {
     return NW_OK;
 }
 
+
+// Ops-mode buffers for chunks of up to `chunk` reads of a call over n reads:
+// slots and counts per chunk (reused chunk after chunk, the compaction copies them
+// out in-stream), the spill area, and two staging arrays (chunk c compacts into
+// staging[c % 2] while the copy of chunk c - 1's runs may still be in flight).
+int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
+    chunk = std::max<int64_t>(chunk, 1);
+    int64_t spill_mb = 64;
+    if (const char* e = std::getenv("CRISPR_NW_SPILL_MB")) spill_mb = std::max(1ll, std::atoll(e));
+    c->ops_slot = nw::kOpsSlot;
+    if (const char* e = std::getenv("CRISPR_NW_OPS_SLOT")) c->ops_slot = std::max(1, std::atoi(e));
+    c->spill_cap = (spill_mb << 20) / 4;
+    if (const char* e = std::getenv("CRISPR_NW_SPILL_WORDS")) c->spill_cap = std::max(1ll, std::atoll(e));   // tests
+    c->staging_cap = chunk * c->ops_slot + c->spill_cap;
+    HIP_OR_FAIL(c, c->d_slots.reserve((size_t)(chunk * c->ops_slot)));
+    HIP_OR_FAIL(c, c->d_nops.reserve((size_t)chunk));
+    HIP_OR_FAIL(c, c->d_spill.reserve((size_t)c->spill_cap));
+    HIP_OR_FAIL(c, c->d_opsctl.reserve(2));
+    HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtl));
+    HIP_OR_FAIL(c, c->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
+    HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));
+    HIP_OR_FAIL(c, c->d_staging[0].reserve((size_t)c->staging_cap));
+    HIP_OR_FAIL(c, c->d_staging[1].reserve((size_t)c->staging_cap));
+    return NW_OK;
+}
+
+// Kernels of c->n reads starting at read `base`, then their compaction into
+// staging[which]: ops_off of those reads (global: the call's running base in
+// ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
+int launch_range_ops(nw_ctx* c, int64_t base, int which) {
+    int rc = launch_range(c, base);
+    if (rc) return rc;
+    nw::OpsCounts cnt{};
+    cnt.fallback = c->d_fallback_count.p;
+    cnt.passes = (c->use_stream && !c->use_diag) ? (int)std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
+    if (c->use_diag && c->n > 0) {
+        cnt.band = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+        if (c->diag16_fill.grid > 0) cnt.redo = c->d_fallback_count.p + 2;
+    }
+    if (c->n <= 0) cnt.fallback = nullptr;
+    HIP_OR_FAIL(c, nw::launch_ops_compact(c->d_nops.p, c->d_slots.p, c->ops_slot, c->d_spill.p, c->n, c->d_blk.p,
+                                          c->d_ctl64.p, c->d_opsoff.p + base, c->d_staging[which].p, c->staging_cap,
+                                          c->d_opsctl.p, cnt, c->stream));
+    return NW_OK;
+}
+
+// NW_OUT_ROWS for the scope of a rows-only entry point (nw_align_batch, nw_align_multi)
+struct RowsMode {
+    nw_ctx* c;
+    int saved;
+    explicit RowsMode(nw_ctx* ctx) : c(ctx), saved(ctx->out_mode) { c->out_mode = NW_OUT_ROWS; }
+    ~RowsMode() { c->out_mode = saved; }
+};
+
+int ops_events(nw_ctx* c, size_t chunks) {
+    auto grow = [&](std::vector<hipEvent_t>& v, unsigned flags) -> hipError_t {
+        while (v.size() < chunks) {
+            hipEvent_t e = nullptr;
+            hipError_t r = hipEventCreateWithFlags(&e, flags);
+            if (r != hipSuccess) return r;
+            v.push_back(e);
+        }
+        return hipSuccess;
+    };
+    HIP_OR_FAIL(c, grow(c->ev_in, hipEventDefault));
+    HIP_OR_FAIL(c, grow(c->ev_cs, hipEventDefault));
+    HIP_OR_FAIL(c, grow(c->ev_ce, hipEventDefault));
+    HIP_OR_FAIL(c, grow(c->ev_out, hipEventDisableTiming));
+    if ((int64_t)chunks > c->h_ctl_chunks) {
+        if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+        c->h_ctl = nullptr;
+        c->h_ctl_chunks = 0;
+        HIP_OR_FAIL(c, hipHostMalloc((void**)&c->h_ctl, sizeof(int64_t) * nw::kOpsCtl * chunks, hipHostMallocDefault));
+        c->h_ctl_chunks = (int64_t)chunks;
+    }
+    return NW_OK;
+}
+
+int ops_error(nw_ctx* c, int64_t err) {
+    if (err & 2) return fail(c, NW_E_NOMEM, "ops spill area full: reads with more than %d traceback runs need more "
+                                            "than CRISPR_NW_SPILL_MB (%lld MB)", c->ops_slot,
+                             (long long)(c->spill_cap * 4 >> 20));
+    if (err & 1) return fail(c, NW_E_NOMEM, "ops staging array full");
+    return NW_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -717,7 +803,21 @@ int nw_batch_run_async(nw_ctx* c) {
     if (c->ref.empty() || !c->d_offsets.p) return fail(c, NW_E_STATE, "no batch uploaded");
     (void)hipSetDevice(c->device);
     HIP_OR_FAIL(c, hipEventRecord(c->ev0, c->stream));
-    int rc = launch_range(c, 0);
+    int rc;
+    c->call_done = false;
+    c->phases = true;
+    struct PhasesOff {
+        nw_ctx* c;
+        ~PhasesOff() { c->phases = false; }
+    } phases_off{c};
+    if (c->out_mode == NW_OUT_OPS) {
+        if (!c->d_slots.p || c->d_nops.cap < (size_t)std::max<int64_t>(c->n, 1))
+            return fail(c, NW_E_STATE, "batch uploaded before nw_batch_set_output(NW_OUT_OPS)");
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
+        rc = launch_range_ops(c, 0, 0);
+    } else {
+        rc = launch_range(c, 0);
+    }
     if (rc) return rc;
     HIP_OR_FAIL(c, hipEventRecord(c->ev1, c->stream));
     c->ran = true;
@@ -741,6 +841,7 @@ int nw_batch_download(nw_ctx* c, char* aln_out, int64_t stride, nw_stat* stats) 
     (void)hipSetDevice(c->device);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     if (c->n == 0) return NW_OK;
+    if (aln_out && c->out_mode == NW_OUT_OPS) return fail(c, NW_E_STATE, "ops output: use nw_batch_download_ops");
     if (stats)
         HIP_OR_FAIL(c, hipMemcpy(stats, c->d_stats.p, sizeof(nw::Stat) * (size_t)c->n, hipMemcpyDeviceToHost));
     if (aln_out) {
@@ -801,7 +902,7 @@ int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_pe
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
     const nw::LaunchCfg& k = c->use_diag ? c->diag_fill : c->use_stream ? c->stream_fill
-                             : (c->use_pair ? c->pair_cfg : (c->use_band ? c->band_cfg : c->cfg));
+                             : (c->use_band ? c->band_cfg : c->cfg);
     if (rows_per_lane) *rows_per_lane = k.R;
     if (waves_per_block) *waves_per_block = k.wpb;
     if (grid) *grid = k.grid;
@@ -811,10 +912,11 @@ int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_pe
 }
 
 int64_t nw_batch_fallbacks(nw_ctx* c) {
+    if (c && c->call_done) return c->call_counts[3];
     if (!c || !c->ran) return -1;
     (void)hipSetDevice(c->device);
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
-    if (!(c->use_band || c->use_pair || c->use_stream || c->use_diag)) return 0;
+    if (!(c->use_band || c->use_stream || c->use_diag)) return 0;
     const int64_t passes = (c->use_stream && !c->use_diag) ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     std::vector<int32_t> v((size_t)(4 * passes));
     if (hipMemcpy(v.data(), c->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -826,6 +928,8 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
 
 int nw_align_batch(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, char* aln_out,
                    int64_t stride, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    RowsMode rows_mode(c);
     int rc = nw_batch_upload(c, reads, offsets, n);
     if (rc) return rc;
     if ((rc = nw_batch_run_async(c))) return rc;
@@ -843,6 +947,7 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
                    const int64_t* offsets, const int32_t* ref_of_read, int64_t n, char* aln_out, int64_t stride,
                    nw_stat* stats) {
     if (!c) return NW_E_INVALID;
+    RowsMode rows_mode(c);
     if (n_refs <= 0 || !refs || !ref_offsets) return fail(c, NW_E_INVALID, "no amplicons");
     if (n < 0 || (n > 0 && (!reads || !offsets || !ref_of_read))) return fail(c, NW_E_INVALID, "bad batch");
     for (int32_t g = 0; g < n_refs; ++g) {
@@ -928,6 +1033,7 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
     }
     c->n = 0;          // the per-batch getters describe nw_batch_upload batches only
     c->ran = false;
+    c->call_done = false;
     return NW_OK;
 }
 
@@ -937,6 +1043,245 @@ int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int
     for (int32_t g = 0; g < n_refs; ++g)
         st = std::max(st, stride_for((int)(ref_offsets[g + 1] - ref_offsets[g]), std::max(max_read_len, 1)));
     return st;
+}
+
+int nw_batch_set_output(nw_ctx* c, int mode) {
+    if (!c) return NW_E_INVALID;
+    if (mode != NW_OUT_ROWS && mode != NW_OUT_OPS) return fail(c, NW_E_INVALID, "output mode %d", mode);
+    c->out_mode = mode;
+    c->ran = false;
+    c->call_done = false;
+    return NW_OK;
+}
+
+int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (!c->ran || c->out_mode != NW_OUT_OPS) return fail(c, NW_E_STATE, "no ops-mode run (nw_batch_set_output)");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    int64_t ctl[nw::kOpsCtl];
+    HIP_OR_FAIL(c, hipMemcpy(ctl, c->d_ctl64.p, sizeof ctl, hipMemcpyDeviceToHost));
+    int rc = ops_error(c, ctl[3]);
+    if (rc) return rc;
+    if (c->n > 0) {
+        if (stats) HIP_OR_FAIL(c, hipMemcpy(stats, c->d_stats.p, sizeof(nw::Stat) * (size_t)c->n, hipMemcpyDeviceToHost));
+        if (ops_off) HIP_OR_FAIL(c, hipMemcpy(ops_off, c->d_opsoff.p, sizeof(int64_t) * (size_t)c->n, hipMemcpyDeviceToHost));
+    }
+    if (ops_off) ops_off[c->n] = ctl[2];
+    if (ctl[2] > ops_cap)
+        return fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs", (long long)ops_cap, (long long)ctl[2]);
+    if (ctl[2] > 0 && ops_out)
+        HIP_OR_FAIL(c, hipMemcpy(ops_out, c->d_staging[0].p, sizeof(uint32_t) * (size_t)ctl[2], hipMemcpyDeviceToHost));
+    return NW_OK;
+}
+
+// The call-level path (host batch in -> per-read records in host
+// memory).  Chunks of reads flow through three streams: every chunk's reads and
+// offsets are queued on s_in up front; chunk k's kernels + compaction wait for its
+// upload on the compute stream; its records and offsets go back on s_out as soon as
+// they exist, its runs once the host has read the chunk's run total (the host waits
+// for chunk k - 1 while chunk k computes).  Compute of chunk k + 2 reuses chunk k's
+// staging array after its copy.  Host buffers should be pinned (nw_host_alloc /
+// nw_host_register) for the copies to run asynchronously at PCIe rate.
+int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                 int64_t* ops_off, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
+    if (n < 0 || (n > 0 && (!offsets || !reads || !stats)) || !ops_off)
+        return fail(c, NW_E_INVALID, "bad batch");
+    (void)hipSetDevice(c->device);
+    const int La = (int)c->ref.size();
+    int32_t lb_max = 1;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t len = offsets[r + 1] - offsets[r];
+        if (len < 0 || len > (1 << 20)) return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
+        lb_max = std::max<int32_t>(lb_max, (int32_t)len);
+    }
+    int64_t chunk = 131072;
+    if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
+    chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
+    const int mode_before = c->out_mode;
+    c->out_mode = NW_OUT_OPS;
+    c->ran = false;
+    c->call_done = false;
+    c->lb_max = lb_max;
+    c->stride = stride_for(La, lb_max);
+    c->cells = 0;
+    c->n = chunk;
+    int rc = configure(c);
+    if (!rc) rc = ops_reserve(c, chunk, n);
+    const int64_t base0 = n ? offsets[0] : 0;
+    const int64_t nbytes = n ? offsets[n] - base0 : 0;
+    const int64_t nchunks = n ? (n + chunk - 1) / chunk : 0;
+    auto restore = [&](int code) {
+        c->out_mode = mode_before;
+        c->n = 0;
+        return code;
+    };
+    if (rc) return restore(rc);
+    if (c->d_reads.reserve((size_t)nbytes + 512) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
+        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess ||
+        c->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+        return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
+    if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
+    c->reads_bias = base0;
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
+    // every upload queued up front: the copy engine streams the batch while chunks compute
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
+    for (int64_t k = 0; k < nchunks; ++k) {
+        const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
+        const int64_t b0 = offsets[lo], b1 = offsets[hi];
+        if (b1 > b0)
+            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p + (b0 - base0), reads + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice,
+                                          c->s_in));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
+                                      hipMemcpyHostToDevice, c->s_in));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
+    }
+    int64_t total = 0, err = 0;
+    bool cap_short = false;
+    // chunk k's runs: once its total is known on the host
+    auto copy_runs = [&](int64_t k) -> int {
+        HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
+        const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
+        err |= h[3];
+        const int64_t cb = h[1], tot = h[2];
+        if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
+        } else if (cb + tot > ops_cap) cap_short = true;
+        else if (tot > 0)
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->d_staging[k & 1].p, sizeof(uint32_t) * (size_t)tot,
+                                          hipMemcpyDeviceToHost, c->s_out));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
+        total = cb + tot;
+        if (ops_out) c->ops_d2h_bytes += 4 * tot;
+        return NW_OK;
+    };
+    c->ops_d2h_bytes = 0;
+    for (int64_t k = 0; k < nchunks; ++k) {
+        const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_in[(size_t)k], 0));
+        if (k >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_out[(size_t)(k - 2)], 0));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->stream));
+        c->n = hi - lo;
+        if ((rc = launch_range_ops(c, lo, (int)(k & 1)))) return restore(rc);
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
+                                      hipMemcpyDeviceToHost, c->stream));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->stream));
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
+        HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
+                                      hipMemcpyDeviceToHost, c->s_out));
+        HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
+                                      hipMemcpyDeviceToHost, c->s_out));
+        c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
+        if (k >= 1 && (rc = copy_runs(k - 1))) return restore(rc);
+    }
+    if (nchunks > 0 && (rc = copy_runs(nchunks - 1))) return restore(rc);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
+    ops_off[n] = total;
+    if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)
+        const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);
+        const bool two = c->use_diag && c->diag16_fill.grid > 0;
+        c->call_counts[0] = c->use_diag ? n - h[6] : 0;
+        c->call_counts[1] = two ? h[6] : 0;
+        c->call_counts[2] = c->use_diag ? (two ? h[5] : h[6]) : 0;
+        c->call_counts[3] = h[4];
+    }
+    c->call_done = true;
+    // device times: the upload span on s_in, the chunks' compute spans summed
+    c->ops_h2d_ms = 0.0f;
+    c->ops_compute_ms = 0.0f;
+    c->ops_h2d_bytes = nbytes + (int64_t)sizeof(int64_t) * (n + nchunks);
+    if (nchunks > 0) {
+        HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)(nchunks - 1)]));
+        for (int64_t k = 0; k < nchunks; ++k) {
+            float ms = 0.0f;
+            HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
+            c->ops_compute_ms += ms;
+        }
+    }
+    if ((rc = ops_error(c, err))) return restore(rc);
+    if (cap_short)
+        return restore(fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs (ops_off holds the offsets)", (long long)ops_cap,
+                            (long long)total));
+    return restore(NW_OK);
+}
+
+int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes) {
+    if (!c) return NW_E_INVALID;
+    if (h2d_ms) *h2d_ms = c->ops_h2d_ms;
+    if (compute_ms) *compute_ms = c->ops_compute_ms;
+    if (h2d_bytes) *h2d_bytes = c->ops_h2d_bytes;
+    if (d2h_bytes) *d2h_bytes = c->ops_d2h_bytes;
+    return NW_OK;
+}
+
+int nw_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return NW_E_INVALID;
+    *out = nullptr;
+    return hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault) == hipSuccess ? NW_OK
+                                                                                                     : NW_E_NOMEM;
+}
+
+void nw_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int nw_host_register(void* p, int64_t bytes) {
+    if (!p || bytes <= 0) return NW_E_INVALID;
+    return hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault) == hipSuccess ? NW_OK : NW_E_HIP;
+}
+
+int nw_host_unregister(void* p) {
+    if (!p) return NW_E_INVALID;
+    return hipHostUnregister(p) == hipSuccess ? NW_OK : NW_E_HIP;
+}
+
+int nw_batch_phase_times(nw_ctx* c, float* ms5) {
+    if (!c || !ms5) return NW_E_INVALID;
+    if (!c->ran) return fail(c, NW_E_STATE, "nothing has run");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 5; ++k) ms5[k] = 0.0f;
+    if (!c->use_diag || c->n <= 0) {
+        HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[4], c->ev0, c->ev1));
+        return NW_OK;
+    }
+    const bool two = c->diag16_fill.grid > 0;
+    HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[0], c->ev0, c->ev_sort));
+    HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[1], c->ev_sort, c->ev_fill));
+    HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[2], c->ev_fill, c->ev_walk));
+    HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[3], c->ev_walk, c->ev_l2));
+    HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[4], c->ev_l2, c->ev1));
+    if (!two) {   // one level: ms5[1..2] are the 32-diagonal level's, ms5[3] is empty
+        ms5[3] = 0.0f;
+    }
+    return NW_OK;
+}
+
+int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
+    if (!c || !counts4) return NW_E_INVALID;
+    if (c->call_done) {
+        for (int k = 0; k < 4; ++k) counts4[k] = c->call_counts[k];
+        return NW_OK;
+    }
+    if (!c->ran) return fail(c, NW_E_STATE, "nothing has run");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 4; ++k) counts4[k] = 0;
+    if (!c->use_diag) {
+        counts4[3] = nw_batch_fallbacks(c);
+        return NW_OK;
+    }
+    int32_t fb[4] = {0, 0, 0, 0}, need = 0;
+    const int32_t* band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+    HIP_OR_FAIL(c, hipMemcpy(fb, c->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
+    HIP_OR_FAIL(c, hipMemcpy(&need, band_count, sizeof need, hipMemcpyDeviceToHost));
+    const bool two = c->diag16_fill.grid > 0;
+    counts4[0] = c->n - need;             // exact copies (no DP)
+    counts4[1] = two ? need : 0;          // first level (16 diagonals)
+    counts4[2] = two ? fb[2] : need;      // second level (32 diagonals)
+    counts4[3] = fb[0];                   // exact int32 kernel
+    return NW_OK;
 }
 
 }  // extern "C"

@@ -328,8 +328,9 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         auto sim = [&](int ai, int code) {
             return (int)(signed char)prof_lds[code * 64 * RP + (ai / R) * RP + (ai % R)];
         };
+        if (args.ops) store_ops(args, rd, runs, nruns, lane);
         emit_alignment(runs, nruns, amp_lds, raw, lut_lds, sim, args.out + rd * 3 * args.stride, args.stride,
-                       score, ei, ej, st, lane);
+                       score, ei, ej, st, lane, !args.ops);
         lds_fence();
     }
 }

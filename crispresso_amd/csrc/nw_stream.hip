@@ -660,8 +660,9 @@ __global__ __launch_bounds__(512, NW_WALK_WAVES_PER_SIMD) void nw_stream_walk(co
             continue;
         }
         auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
+        if (args.ops) store_ops(args, rd, runs, nruns, lane);
         emit_alignment(runs, nruns, amp_lds, cached ? rbuf + mis : raw, lut_lds, sim, args.out + rd * 3 * args.stride,
-                       args.stride, score, ei, ej, args.stats + rd, lane);
+                       args.stride, score, ei, ej, args.stats + rd, lane, !args.ops);
         lds_fence();
     }
 }

@@ -34,15 +34,35 @@ extern "C" {
 #define NW_E_HIP (-4)          /* HIP runtime error or no device */
 #define NW_E_NOMEM (-5)        /* device or host allocation failed */
 #define NW_E_STATE (-6)        /* call out of order (e.g. run before upload) */
+#define NW_E_CAPACITY (-7)     /* caller's ops buffer too small: ops_off[n] holds the runs needed */
 
-/* Traceback tie policy.  NW_TIE_EMBOSS: EMBOSS needle's strict rules
- * (M wins only when strictly greater than X and Y, X beats Y only when strictly
- * greater, gap open wins ties with extend; start cell = corner, then last column
- * bottom->top, then last row right->left).  DESIGN.md "EMBOSS semantics". */
+/* Traceback tie policy.  NW_TIE_EMBOSS, the rule pinned against real EMBOSS 6.6.0
+ * output by the reference's end-to-end assertions (oracle/nw_oracle.c):
+ * the predecessor of an M cell is M when M >= X and M >= Y (ties stay on the
+ * diagonal), else X when X > Y, else Y; a gap run was opened at a cell only when
+ * open > extend there (ties extend the gap).  Start cell: the best M on the last
+ * row / column, scanned corner, then last column bottom->top, then last row
+ * right->left; the first strict maximum wins. */
 #define NW_TIE_EMBOSS 0
 
 /* nw_stat.flags */
 #define NW_FLAG_EMPTY 1        /* zero-length read: no alignment (needle skips it) */
+
+/* Output of the upload/run API (nw_batch_set_output).  NW_OUT_ROWS: the three
+ * alignment strings per read in HBM ([n][3][stride], nw_batch_download /
+ * nw_batch_device_output).  NW_OUT_OPS: the traceback runs per read (below). */
+#define NW_OUT_ROWS 0
+#define NW_OUT_OPS 1
+
+/* A run of the ops output: type << 28 | length.  M pairs a residue of each
+ * sequence (match or mismatch), X is a gap in the amplicon (read residue), Y a
+ * gap in the read (amplicon residue).  A read's runs go start -> end; end gaps are
+ * runs like any other. */
+#define NW_RUN_M 0u
+#define NW_RUN_X 1u
+#define NW_RUN_Y 2u
+#define NW_RUN_TYPE(op) ((op) >> 28)
+#define NW_RUN_LEN(op) ((op) & 0x0fffffffu)
 
 typedef struct nw_ctx nw_ctx;
 
@@ -136,6 +156,52 @@ int nw_align_multi(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, in
                    const char* reads, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
                    char* aln_out, int64_t stride, nw_stat* stats);
 int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int32_t max_read_len);
+
+/* Device time of the last nw_batch_run_async by phase of the band path (synchronises):
+ * [0] classify + length sort, [1] nw_band_fill<16>, [2] nw_band_walk<16>, [3] the
+ * 32-diagonal level, [4] the exact kernel + ops compaction.  Other paths: all in [4]. */
+int nw_batch_phase_times(nw_ctx* ctx, float* ms5);
+/* Reads of the last run by path: [0] exact copies (no DP), [1] first band level,
+ * [2] second band level, [3] exact int32 kernel (synchronises). */
+int nw_batch_path_counts(nw_ctx* ctx, int64_t* counts4);
+
+/* Output mode of the upload/run API (NW_OUT_ROWS default).  Takes effect from
+ * the next nw_batch_upload. */
+int nw_batch_set_output(nw_ctx* ctx, int mode);
+/* After an NW_OUT_OPS run: records, per-read run offsets (n + 1 entries; read r's
+ * runs are ops_out[ops_off[r] .. ops_off[r + 1])) and the runs.  NW_E_CAPACITY when
+ * ops_cap is short (ops_off is filled; ops_off[n] is the count needed). */
+int nw_batch_download_ops(nw_ctx* ctx, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+
+/* The call that replaces one `needle` pass end to end (CRISPRessoCORE.py:1791-1806:
+ * FASTA in, alignments out; the SURVEY.md 8b nw_align_batch with ops output):
+ * host reads in -> per-read records + traceback runs in host memory.  Chunks of
+ * reads are pipelined over PCIe both ways and the kernels; only the runs cross back
+ * (an exact copy is one run), nw_expand_ops rebuilds the strings on the host.
+ * Host buffers should be pinned (nw_host_alloc / nw_host_register).  Synchronous.
+ * Returns NW_E_CAPACITY when ops_cap is short (ops_off filled, ops_off[n] = needed).
+ * ops_out = NULL: records and offsets only (a scores-only pass such as the HDR
+ * repair alignment, CRISPRessoCORE.py:1808-1828 with just_score). */
+int nw_align_ops(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out,
+                 int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* Last nw_align_ops: span of the uploads on the copy stream, sum of the chunks'
+ * kernel spans, bytes each way. */
+int nw_ops_times(const nw_ctx* ctx, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes);
+
+/* Page-locked host memory for the batch buffers (hipHostMalloc / hipHostRegister). */
+int nw_host_alloc(int64_t bytes, void** out);
+void nw_host_free(void* p);
+int nw_host_register(void* p, int64_t bytes);
+int nw_host_unregister(void* p);
+
+/* The three alignment rows of n reads from their runs (host, nthreads threads;
+ * <= 0: all cores): for read r at aln_out + r*3*stride the aligned amplicon, the
+ * markup and the aligned read, stats[r].aln_len bytes each -- the bytes the kernels
+ * write in NW_OUT_ROWS mode.  ref = the amplicon; reads/offsets as aligned.  Rows of
+ * empty reads are left untouched.  Returns 0, or NW_E_INVALID when a read's runs do
+ * not cover the amplicon and the read or exceed stride. */
+int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
+                  const uint32_t* ops, const int64_t* ops_off, char* aln_out, int64_t stride, int32_t nthreads);
 
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated

@@ -14,10 +14,13 @@ def load_bench():
     return mod
 
 
+def newest_summary(b):
+    return next(p for p in b.PMC_SUMMARIES if os.path.exists(p))
+
+
 def test_pmc_summaries_exist_and_newest_first():
     b = load_bench()
-    assert os.path.exists(b.PMC_SUMMARIES[0])
-    with open(b.PMC_SUMMARIES[0]) as f:
+    with open(newest_summary(b)) as f:
         summ = json.load(f)
     assert any("nw_band_fill<16>" in k for k in summ)
     assert any("nw_band_walk<16>" in k for k in summ)
@@ -27,11 +30,44 @@ def test_band_traffic_from_committed_profile():
     b = load_bench()
     traffic, src = b.pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
                                  required="nw::nw_band_fill<16>")
-    assert traffic is not None and traffic > 1e9   # ~3.3 GB per 1M C2 reads
-    assert src == os.path.relpath(b.PMC_SUMMARIES[0], ROOT)
+    assert traffic is not None and traffic > 5e8   # ~1-3 GB per 1M C2 reads
+    assert src == os.path.relpath(newest_summary(b), ROOT)
+    summ, src2 = b.pmc_summary("nw_band_fill<16>")
+    assert src2 == src and any("SQ_INSTS_VALU" in v for v in summ.values())
 
 
 def test_quant_traffic_available():
     b = load_bench()
     traffic, _ = b.pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce")
     assert traffic is not None and traffic > 0
+
+
+def _bench_rank(rank, world, port, out_dir):
+    """bench.py's multi-process plumbing (gloo barrier, max over ranks) never
+    initialises torch's HIP runtime: libcrispr_nw.so owns the GPU in that process."""
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    b = load_bench()
+    r, local, w, dist = b.dist_setup()
+    assert (r, local, w) == (rank, rank, world)
+    b.barrier(dist)
+    m = b.max_over_ranks(dist, float(rank + 1))
+    assert m == float(world)
+    assert not torch.cuda.is_initialized()
+    with open(os.path.join(out_dir, f"ok{rank}"), "w") as f:
+        f.write(str(m))
+    dist.destroy_process_group()
+
+
+def test_bench_multi_rank_path_is_torch_cuda_free(tmp_path):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_bench_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="fork")
+    assert (tmp_path / "ok0").read_text() == "2.0" and (tmp_path / "ok1").read_text() == "2.0"

@@ -1,0 +1,133 @@
+"""GPU parity of the call-level ops path (nw_align_ops): records + traceback runs
+cross PCIe, the rows are rebuilt on the host (nw_expand_ops).  Bit-exact against
+the CPU oracle: chunk boundaries of the pipeline, slot spills, the device-resident
+ops mode, pinned buffers, the capacity protocol and its errors."""
+import numpy as np
+import pytest
+
+from crispresso_amd import _lib, synth
+from crispresso_amd.aligner import NeedleError, pack_reads
+from tests.test_gpu_parity import FIELDS, assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _reads(amp, seed):
+    buf0, off0 = synth.reads_from(amp, 1500, seed, synth.PARITY_MIX)
+    reads = synth.unpack(buf0, off0)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    # reads with many gap runs (slot spills), empty reads, junk, exact copies
+    for k in range(40):
+        r = list(amp)
+        for _ in range(int(rng.integers(5, 40))):
+            p = int(rng.integers(1, len(r) - 1))
+            if rng.random() < 0.5:
+                del r[p]
+            else:
+                r.insert(p, "ACGT"[int(rng.integers(0, 4))])
+        reads.append("".join(r))
+    reads += ["", amp, amp.lower(), synth.random_amplicon(250, seed + 5), amp[:10], "-" + amp[1:]]
+    return reads
+
+
+@pytest.mark.parametrize("chunk", ["1", "613", "100000"])
+@pytest.mark.parametrize("slot", ["1", "3", "64"])
+def test_align_ops_chunks_and_spills(gpu_aligner_factory, oracle, monkeypatch, chunk, slot):
+    monkeypatch.setenv("CRISPR_NW_CHUNK", chunk if chunk != "1" else "257")
+    monkeypatch.setenv("CRISPR_NW_OPS_SLOT", slot)
+    amp = synth.random_amplicon(250, 61)
+    buf, off = pack_reads(_reads(amp, 62))
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops(buf, off)
+    assert ob.ops_off[0] == 0 and np.all(np.diff(ob.ops_off) >= 0)
+    lens = np.diff(off)
+    assert np.all((np.diff(ob.ops_off) == 0) == (lens == 0))
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), f"ops chunk={chunk} slot={slot}")
+    t = a.ops_times()
+    assert t["h2d_bytes"] >= int(off[-1]) and t["compute_ms"] > 0
+
+
+def test_exact_copy_is_one_run(gpu_aligner_factory):
+    amp = synth.random_amplicon(230, 3)
+    buf, off = pack_reads([amp, amp.lower(), amp[:-1], ""])
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops(buf, off)
+    assert ob.runs(0) == [(_lib.NW_RUN_M, 230)] and ob.runs(1) == [(_lib.NW_RUN_M, 230)]
+    assert ob.runs(3) == []
+    assert ob.stats["flags"][3] & _lib.NW_FLAG_EMPTY
+
+
+def test_ops_pinned_buffers_and_capacity(gpu_aligner_factory, oracle):
+    """Pinned inputs/outputs (the bench's setup); an ops buffer that is too small
+    returns NW_E_CAPACITY with the size needed in ops_off[n]."""
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 5000, 2)
+    n = len(off) - 1
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
+    stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
+    ops_off = _lib.PinnedBuffer(n + 1, np.int64)
+    small = np.empty(10, np.uint32)
+    rc = a.lib.nw_align_ops(a._h, _lib.ptr(pb.array), _lib.ptr(po.array), n, _lib.ptr(small), len(small),
+                            _lib.ptr(ops_off.array), _lib.ptr(stats.array))
+    assert rc == _lib.NW_E_CAPACITY
+    need = int(ops_off.array[n])
+    assert need > 10
+    ops = _lib.PinnedBuffer(need, np.uint32)
+    ob = a.align_ops(pb.array, po.array, out=(stats.array, ops.array, ops_off.array))
+    assert int(ob.ops_off[n]) == need
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "pinned")
+    for b in (pb, po, stats, ops_off, ops):
+        b.close()
+
+
+def test_spill_area_full_raises(gpu_aligner_factory, monkeypatch):
+    monkeypatch.setenv("CRISPR_NW_OPS_SLOT", "1")
+    monkeypatch.setenv("CRISPR_NW_SPILL_WORDS", "8")
+    amp = synth.random_amplicon(250, 61)
+    buf, off = pack_reads(_reads(amp, 63))
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    with pytest.raises(NeedleError, match="spill area full"):
+        a.align_ops(buf, off)
+    monkeypatch.delenv("CRISPR_NW_SPILL_WORDS")
+    monkeypatch.delenv("CRISPR_NW_OPS_SLOT")
+    a.align_ops(buf, off)   # the context recovers
+
+
+def test_device_resident_ops_mode(gpu_aligner_factory, oracle):
+    """nw_batch_set_output(NW_OUT_OPS) + upload/run/download_ops: the bench's
+    kernel-resident pass is the same kernels + compaction as the call."""
+    amp = synth.random_amplicon(250, 1)
+    buf, off = pack_reads(_reads(amp, 64))
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    a.set_output("ops")
+    a.upload(buf, off)
+    for _ in range(2):
+        a.run_async()
+        assert a.sync() > 0
+    ob = a.download_ops(len(off) - 1)
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "resident-ops")
+    with pytest.raises(NeedleError):
+        a.download(len(off) - 1, 300)           # rows are not produced in ops mode
+    a.set_output("rows")
+    a.upload(buf, off)
+    a.run_async()
+    a.sync()
+    rows = a.download(len(off) - 1, int(np.diff(off).max()))
+    for f in FIELDS:
+        assert np.array_equal(rows.stats[f], ob.stats[f])
+
+
+def test_rows_api_unaffected_by_ops_mode(gpu_aligner_factory, oracle):
+    """nw_align_batch / nw_align_multi always produce rows, whatever the upload mode."""
+    amp = synth.random_amplicon(200, 5)
+    buf, off = synth.reads_from(amp, 700, 6, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    a.set_output("ops")
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off, mode="rows"), "rows-after-ops")

@@ -12,16 +12,20 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["diag", "stream", "stream-profile", "pair", "band", "full"]
-BANDED = {"diag": "diag-int16", "stream": "stream-int16", "pair": "pair-band-int16"}
+KERNELS = ["diag", "stream", "stream-profile", "band", "full"]
+BANDED = {"diag": "diag-int16", "stream": "stream-int16"}
 
 
-@pytest.fixture(params=KERNELS)
+@pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")])
 def kernel(request, monkeypatch):
     """Run a test once per kernel family (CRISPR_NW_KERNEL selects it;
-    stream-profile = the stream kernel without the pair-code score table)."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", request.param.split("-")[0])
-    if request.param == "stream-profile":
+    stream-profile = the stream kernel without the pair-code score table) and
+    output mode (ops: runs over PCIe + host expansion, the default; rows: the
+    kernels write the three strings)."""
+    fam, mode = request.param.split("/")
+    monkeypatch.setenv("CRISPR_NW_KERNEL", fam.split("-")[0])
+    monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
+    if fam == "stream-profile":
         monkeypatch.setenv("CRISPR_NW_PAIR_TABLE", "0")
     return request.param
 
@@ -270,7 +274,7 @@ def test_stream_multiple_passes(gpu_aligner_factory, oracle, monkeypatch):
     buf, off = synth.reads_from(amp, 1001, 9, synth.PARITY_MIX)
     a = gpu_aligner_factory()
     a.set_reference(amp)
-    batch = a.align_packed(buf, off)
+    batch = a.align_packed(buf, off, mode="rows")   # kernel_times describe an upload/run pass
     assert_same(oracle, amp, buf, off, batch, "passes")
     t = a.kernel_times()
     assert t["fill_ms"] > 0 and t["walk_ms"] > 0 and t["rest_ms"] >= 0
@@ -370,11 +374,13 @@ def test_diag_multiple_passes_and_odd_counts(gpu_aligner_factory, oracle, monkey
     buf, off = synth.reads_from(amp, 1003, 9, synth.PARITY_MIX)
     a = gpu_aligner_factory()
     a.set_reference(amp)
-    batch = a.align_packed(buf, off)
+    batch = a.align_packed(buf, off, mode="rows")   # kernel_times describe an upload/run pass
     assert a.geometry()["tb_mode"] == "diag-int16"
     assert_same(oracle, amp, buf, off, batch, "diag-passes")
     t = a.kernel_times()
     assert t["fill_ms"] > 0 and t["walk_ms"] > 0
+    ob = a.align_ops(buf, off)
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "diag-passes-ops")
 
 
 @pytest.mark.parametrize("La", [40, 150, 333, 700, 1024])
