@@ -974,19 +974,77 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
     }
 }
 
+// Overlap of diagonal d = j - i (pairs of the alignment that stays on it).
+__device__ __forceinline__ int diag_pairs(int La, int Lb, int d) { return d >= 0 ? min(La, Lb - d) : min(Lb, La + d); }
+
+// True when every single-diagonal alignment outside [dlo, dhi] whose overlap could
+// reach `score` (maxsub * P(d) >= score) scores below it.  A (6-code) score table
+// lookup per pair: amplicon / read bytes in LDS, codes by lut6, scores from band_tab
+// (packed with + 2E, entry [x][y][y]).
+__device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned char* amp, const unsigned char* rd,
+                                            int La, int Lb, int dlo, int dhi, int score, int lane) {
+    const int E2 = 2 * a.gap_extend;
+    for (int side = 0; side < 2; ++side) {
+        for (int k = 1;; ++k) {
+            const int d = side == 0 ? dhi + k : dlo - k;
+            const int P = diag_pairs(La, Lb, d);
+            if (P <= 0 || a.band_maxsub * P < score) break;
+            const int i0 = d >= 0 ? 0 : -d, j0 = d >= 0 ? d : 0;   // 0-based first pair
+            int sum = 0;
+            for (int t = lane; t < P; t += 64) {
+                const int x = a.lut6[amp[i0 + t]], y = a.lut6[rd[j0 + t]];
+                const unsigned w = a.band_tab[(x < 6 ? x : 5) * 36 + (y < 6 ? y : 5) * 7];
+                sum += (int)(short)(w & 0xffffu) - E2;
+            }
+            if (wave_sum(sum) >= score) return false;
+        }
+    }
+    return true;
+}
+
 // W < kBandDiags: a first level; reads it cannot certify go to the redo list of the
 // next (wider) level.  W = kBandDiags: they go to the exact int32 kernel.
 template <int W>
 __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
-    auto give_up = [&](long long rd, bool retry) {
-        if (W < kBandDiags && retry) a.redo_list[atomicAdd(a.redo_count, 1)] = (int32_t)rd;
-        else a.fallback_list[atomicAdd(a.fallback_count, 1)] = rd;
-    };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int La = a.La, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
+    // Reads handed on (next level's redo list, or the exact kernel's list) wait in a
+    // lane of the wavefront (entry p in lane p) and go out 64 at a time: one atomic
+    // per 64 reads and one coalesced store (a per-read atomic on one counter serialises
+    // when most reads are handed on, e.g. the HDR pass).  Called wave-uniformly.
+    int redo_n = 0, fb_n = 0;
+    int redo_v = 0;
+    long long fb_v = 0;
+    auto flush_redo = [&]() {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(a.redo_count, redo_n);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (lane < redo_n) a.redo_list[base + lane] = redo_v;
+        redo_n = 0;
+    };
+    auto flush_fb = [&]() {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(a.fallback_count, fb_n);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (lane < fb_n) a.fallback_list[base + lane] = fb_v;
+        fb_n = 0;
+    };
+    auto give_up = [&](long long k, long long rd, bool retry) {
+        if (W < kBandDiags && retry && a.redo_flags) {
+            // the next level's list keeps the sorted order (nw_band_redo_* compaction):
+            // its pairs are reads of similar length, as on this level
+            if (lane == 0) a.redo_flags[k] = 1;
+        } else if (W < kBandDiags && retry) {
+            if (lane == redo_n) redo_v = (int)rd;
+            if (++redo_n == 64) flush_redo();
+        } else {
+            if (lane == fb_n) fb_v = rd;
+            if (++fb_n == 64) flush_fb();
+        }
+    };
     unsigned char* lut_lds = smem;
     unsigned char* amp_lds = smem + 256;
     unsigned* rowpos = (unsigned*)(smem + 256 + align16(La + 16));
@@ -1039,7 +1097,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             continue;
         }
         if (hdr.z & kPairInactive) {   // too long, or the pair's lengths do not fit the band
-            if (lane == 0) give_up(rd, true);
+            give_up(k, rd, true);
             continue;
         }
         const int dlo = hdr.y;
@@ -1047,7 +1105,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const unsigned char* raw = a.reads + off;
         // the read's bytes -> LDS (DMA, one dword per lane) for the emit
         if (Lb > rcap) {   // not reached: rcap covers the band length cap
-            if (lane == 0) give_up(rd, false);
+            give_up(k, rd, false);
             continue;
         }
         const int mis = (int)((uintptr_t)raw & 3);
@@ -1078,10 +1136,20 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         int pmax = -1;
         if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
         if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
-        const bool certified = pmax < 0 || score > a.band_maxsub * pmax;
+        bool certified = pmax < 0 || score > a.band_maxsub * pmax;
         const bool bad_code = (hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) != 0;
+        if (!certified && !bad_code && score > a.band_maxsub * pmax - a.gap_open) {
+            // Refined bound: an alignment leaving the band with an internal gap pays at
+            // least the gap open, so it scores <= maxsub * pmax - O < score; one without
+            // internal gaps is a single diagonal d (free end gaps), paired over its whole
+            // overlap P(d): its score S_d is computed exactly, for the few diagonals beyond
+            // the band with maxsub * P(d) >= score (P falls by one per diagonal: at most
+            // about two per side, as score > maxsub * (pmax - 2)).
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the read's bytes are in LDS
+            certified = band_single_diagonals_below(a, amp_lds, rbuf + mis, La, Lb, dlo, dhi, score, lane);
+        }
         if (bad_code || !certified) {
-            if (lane == 0) give_up(rd, !bad_code);   // IUPAC codes: no band helps
+            give_up(k, rd, !bad_code);   // IUPAC codes: no band helps
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             continue;
         }
@@ -1091,7 +1159,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs, kBandRunsCap, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         if (nruns < 0) {
-            if (lane == 0) give_up(rd, true);
+            give_up(k, rd, true);
             continue;
         }
         lds_fence();
@@ -1106,6 +1174,94 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         lds_fence();
     }
+    if (redo_n) flush_redo();
+    if (fb_n) flush_fb();
+}
+
+// ============================================================================
+// Redo list of the second level: the sorted positions the first level flagged,
+// compacted in sorted order (block sums, one scan block, scatter): no atomics,
+// deterministic, and consecutive entries (the second level's pairs) have similar
+// lengths.  Positions [0, *band_count) are the first level's.
+// ============================================================================
+constexpr int kRedoBlock = 1024;   // positions per block (256 threads x 4)
+
+__device__ int block_excl_scan_i32(int v, int* total) {
+    __shared__ int wsum[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        before += w < wave ? wsum[w] : 0;
+        all += wsum[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + incl - v;
+}
+
+__global__ __launch_bounds__(256) void nw_band_redo_blocksum(const KernelArgs a) {
+    const long long n = *a.band_count;
+    const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s += k0 + t < n ? a.redo_flags[k0 + t] : 0;
+    int total;
+    block_excl_scan_i32(s, &total);
+    if (threadIdx.x == 0) a.redo_blk[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void nw_band_redo_scan(const KernelArgs a, int nblk) {
+    __shared__ int part[1024];
+    int carry = 0;
+    for (int t0 = 0; t0 < nblk; t0 += 1024) {
+        const int t = t0 + (int)threadIdx.x;
+        const int v = t < nblk ? a.redo_blk[t] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int u = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += u;
+            __syncthreads();
+        }
+        if (t < nblk) a.redo_blk[t] = carry + part[threadIdx.x] - v;
+        carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *a.redo_count = carry;
+}
+
+__global__ __launch_bounds__(256) void nw_band_redo_scatter(const KernelArgs a) {
+    const long long n = *a.band_count;
+    const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
+    int f[4], s = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        f[t] = k0 + t < n ? a.redo_flags[k0 + t] : 0;
+        s += f[t];
+    }
+    int total;
+    int pos = a.redo_blk[blockIdx.x] + block_excl_scan_i32(s, &total);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        if (f[t]) a.redo_list[pos++] = a.band_order[k0 + t];
+}
+
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s) {
+    const int nblk = (int)std::max<int64_t>(1, (nmax + kRedoBlock - 1) / kRedoBlock);
+    hipLaunchKernelGGL(nw_band_redo_blocksum, dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nw_band_redo_scan, dim3(1), dim3(1024), 0, s, a, nblk);
+    hipLaunchKernelGGL(nw_band_redo_scatter, dim3(nblk), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 // ---- host-side helpers -------------------------------------------------------

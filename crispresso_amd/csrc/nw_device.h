@@ -69,6 +69,8 @@ struct KernelArgs {
                                    // or the previous level's redo count)
     int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
     int32_t* redo_count;
+    uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
+    int32_t* redo_blk;             // [ceil(n / 1024)] compaction scratch
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
     // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
     // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
@@ -131,6 +133,9 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
+// the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
+// nmax >= the number of sorted positions (grid size)
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s);
 
 // ops compaction (nw_ops.hip): per-read slots -> one contiguous run array.
 // ctl (int64, kOpsCtl): [0] running base over the chunks of a call (in/out), [1] this chunk's

@@ -100,6 +100,8 @@ struct nw_ctx {
     nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
     DevBuf<int32_t> d_redo;                          // reads the first level could not certify
+    DevBuf<uint8_t> d_redo_flags;                    // per sorted position: handed to the second level
+    DevBuf<int32_t> d_redo_blk;
     DevBuf<uint32_t> d_btab, d_rowpos;
     DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
     DevBuf<uint8_t> d_bregion;
@@ -365,6 +367,8 @@ int configure(nw_ctx* c) {
             HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)rbytes));
             HIP_OR_FAIL(c, c->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->d_redo_blk.reserve((size_t)std::max<int64_t>((c->n + 1023) / 1024, 1)));
             HIP_OR_FAIL(c, c->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
             HIP_OR_FAIL(c, c->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
             c->use_diag = true;
@@ -453,7 +457,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
     c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
     c->d_ptab.release(); c->d_lut6.release();
-    c->d_btab.release(); c->d_rowpos.release(); c->d_redo.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
+    c->d_btab.release(); c->d_rowpos.release(); c->d_redo.release(); c->d_redo_flags.release(); c->d_redo_blk.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
     c->d_slots.release(); c->d_spill.release(); c->d_staging[0].release(); c->d_staging[1].release();
     c->d_nops.release(); c->d_opsctl.release(); c->d_ctl64.release(); c->d_blk.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
@@ -631,10 +635,16 @@ int launch_range(nw_ctx* c, int64_t base) {
         const bool two = c->diag16_fill.grid > 0;
         a.redo_list = c->d_redo.p;
         a.redo_count = c->d_fallback_count.p + 2;
+        if (two) {
+            a.redo_flags = c->d_redo_flags.p;
+            a.redo_blk = c->d_redo_blk.p;
+            HIP_OR_FAIL(c, hipMemsetAsync(c->d_redo_flags.p, 0, (size_t)c->n, c->stream));
+        }
         for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
+                HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->stream));
                 al.band_order = c->d_redo.p;
                 al.band_count = a.redo_count;
             }

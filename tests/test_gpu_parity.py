@@ -499,3 +499,21 @@ def test_diag_iupac_in_every_pair_slot(gpu_aligner_factory, oracle, monkeypatch,
     batch = a.align_packed(buf, off)
     assert a.fallbacks() >= 512 // 3
     assert_same(oracle, amp, buf, off, batch, f"diag-iupac {levels}")
+
+
+@pytest.mark.parametrize("block", [6, 10, 12, 20])
+def test_diag_refined_certificate_clustered_mismatches(gpu_aligner_factory, oracle, block):
+    """Reads with a block of mismatches (the HDR pass of CRISPResso: reference-derived
+    reads against the HDR amplicon, CORE:1808-1828) fail the plain certificate; the
+    refined one (gapped escapes pay the gap open, single diagonals scored exactly)
+    keeps most of them on the band.  Bit-exact either way."""
+    amp = synth.random_amplicon(250, 4)
+    hdr = synth.hdr_amplicon(amp, 4, 120, block)
+    buf, off = synth.reads_from(amp, 1200, 5)
+    a = gpu_aligner_factory()
+    a.set_reference(hdr)
+    ob = a.align_ops(buf, off)
+    assert_same(oracle, hdr, buf, off, ob.expand(hdr, buf, off), f"hdr-block{block}")
+    counts = a.path_counts()
+    if block <= 10:
+        assert counts["exact_kernel"] < 0.05 * (len(off) - 1), counts
