@@ -275,27 +275,43 @@ class GpuAligner:
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(self._off), self.scale, self.options.awidth)
 
     # -- synchronous path ----------------------------------------------------
-    def align_ops(self, buf: np.ndarray, offsets: np.ndarray, out: Optional[tuple] = None) -> OpsBatch:
+    def align_ops(self, buf: Optional[np.ndarray], offsets: np.ndarray, out: Optional[tuple] = None,
+                  resident: bool = False, records_only: bool = False) -> OpsBatch:
         """The call-level path (nw_align_ops): host reads in, records + runs out.
 
         ``out`` = (stats, ops, ops_off) preallocated (e.g. pinned) arrays; by default
-        they are allocated here.  An ops array too small for the batch is replaced."""
+        they are allocated here.  An ops array too small for the batch is replaced.
+        ``resident``: align the batch this aligner's last call uploaded (still in HBM;
+        ``buf`` unused) against the current amplicon (nw_align_ops_resident) -- the HDR
+        pass over the same reads.  ``records_only``: no runs are copied back (a
+        scores-only pass); the returned batch has no runs."""
         if self.reference is None:
             raise NeedleError("no amplicon set")
         n = len(offsets) - 1
         if out is None:
             stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
             ops_off = np.zeros(n + 1, dtype=np.int64)
-            ops = np.empty(2 * n + 4096, dtype=np.uint32)
+            ops = np.empty(0 if records_only else 2 * n + 4096, dtype=np.uint32)
         else:
             stats, ops, ops_off = out
-        rc = self.lib.nw_align_ops(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(ops), len(ops),
-                                   _lib.ptr(ops_off), _lib.ptr(stats))
+
+        def call(ops_arr):
+            o = None if records_only else _lib.ptr(ops_arr)
+            cap = 0 if records_only else len(ops_arr)
+            if resident:
+                return self.lib.nw_align_ops_resident(self._h, _lib.ptr(offsets), n, o, cap, _lib.ptr(ops_off),
+                                                      _lib.ptr(stats))
+            return self.lib.nw_align_ops(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, o, cap, _lib.ptr(ops_off),
+                                         _lib.ptr(stats))
+
+        rc = call(ops)
         if rc == _lib.NW_E_CAPACITY:   # rare: more runs than the buffer holds; run again with the size it said
             ops = np.empty(int(ops_off[n]), dtype=np.uint32)
-            rc = self.lib.nw_align_ops(self._h, _lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(ops), len(ops),
-                                       _lib.ptr(ops_off), _lib.ptr(stats))
+            rc = call(ops)
         self._check(rc, "nw_align_ops")
+        if records_only:
+            return OpsBatch(stats, np.zeros(0, np.uint32), np.zeros(n + 1, np.int64), np.diff(offsets), self.scale,
+                            self.options.awidth)
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(offsets), self.scale, self.options.awidth)
 
     def ops_times(self) -> dict:

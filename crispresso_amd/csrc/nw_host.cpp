@@ -124,6 +124,8 @@ struct nw_ctx {
     int64_t h_ctl_chunks = 0;
     float ops_h2d_ms = 0.0f, ops_compute_ms = 0.0f;
     bool call_done = false;            // the last operation was nw_align_ops: the getters report its counts
+    bool resident_ok = false;          // d_reads / d_offsets hold the last nw_align_ops batch
+    int64_t resident_n = 0, resident_lo = 0, resident_hi = 0;
     int64_t call_counts[4] = {0, 0, 0, 0};
     int64_t ops_h2d_bytes = 0, ops_d2h_bytes = 0;
 };
@@ -556,6 +558,7 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
     if (c->out_mode == NW_OUT_ROWS) HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
+    c->resident_ok = false;
     if (nbytes) HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, reads + base, (size_t)nbytes, hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, rel.data(), sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
@@ -993,6 +996,7 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
         const int64_t r = order[(size_t)s];
         std::memcpy(sreads.data() + soff[(size_t)s], reads + offsets[r], (size_t)(offsets[r + 1] - offsets[r]));
     }
+    c->resident_ok = false;
     HIP_OR_FAIL(c, c->d_reads.reserve(sreads.size() + 512));
     HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
     HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * stride_all));
@@ -1093,12 +1097,22 @@ int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t
 // for chunk k - 1 while chunk k computes).  Compute of chunk k + 2 reuses chunk k's
 // staging array after its copy.  Host buffers should be pinned (nw_host_alloc /
 // nw_host_register) for the copies to run asynchronously at PCIe rate.
-int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
-                 int64_t* ops_off, nw_stat* stats) {
+}  // extern "C"
+
+namespace {
+
+// nw_align_ops (upload = true) and nw_align_ops_resident (the batch the last call
+// uploaded, still in HBM: no upload).
+int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+             int64_t* ops_off, nw_stat* stats, bool upload) {
     if (!c) return NW_E_INVALID;
     if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
-    if (n < 0 || (n > 0 && (!offsets || !reads || !stats)) || !ops_off)
+    if (n < 0 || (n > 0 && (!offsets || (upload && !reads) || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
+    if (!upload && !(c->resident_ok && c->resident_n == n && (n == 0 || (c->resident_lo == offsets[0] &&
+                                                                          c->resident_hi == offsets[n]))))
+        return fail(c, NW_E_STATE, "no resident batch of these %lld reads (nw_align_ops uploads one)", (long long)n);
+    if (upload) c->resident_ok = false;
     (void)hipSetDevice(c->device);
     const int La = (int)c->ref.size();
     int32_t lb_max = 1;
@@ -1138,7 +1152,7 @@ int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
     // every upload queued up front: the copy engine streams the batch while chunks compute
     HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
-    for (int64_t k = 0; k < nchunks; ++k) {
+    for (int64_t k = 0; upload && k < nchunks; ++k) {
         const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
         if (b1 > b0)
@@ -1169,7 +1183,7 @@ int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n
     c->ops_d2h_bytes = 0;
     for (int64_t k = 0; k < nchunks; ++k) {
         const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
-        HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_in[(size_t)k], 0));
+        if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_in[(size_t)k], 0));
         if (k >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_out[(size_t)(k - 2)], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->stream));
         c->n = hi - lo;
@@ -1200,20 +1214,38 @@ int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n
     // device times: the upload span on s_in, the chunks' compute spans summed
     c->ops_h2d_ms = 0.0f;
     c->ops_compute_ms = 0.0f;
-    c->ops_h2d_bytes = nbytes + (int64_t)sizeof(int64_t) * (n + nchunks);
+    c->ops_h2d_bytes = upload ? nbytes + (int64_t)sizeof(int64_t) * (n + nchunks) : 0;
     if (nchunks > 0) {
-        HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)(nchunks - 1)]));
+        if (upload) HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)(nchunks - 1)]));
         for (int64_t k = 0; k < nchunks; ++k) {
             float ms = 0.0f;
             HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
             c->ops_compute_ms += ms;
         }
     }
+    c->resident_ok = true;   // the batch stays in HBM for nw_align_ops_resident
+    c->resident_n = n;
+    c->resident_lo = base0;
+    c->resident_hi = base0 + nbytes;
     if ((rc = ops_error(c, err))) return restore(rc);
     if (cap_short)
         return restore(fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs (ops_off holds the offsets)", (long long)ops_cap,
                             (long long)total));
     return restore(NW_OK);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                 int64_t* ops_off, nw_stat* stats) {
+    return ops_call(c, reads, offsets, n, ops_out, ops_cap, ops_off, stats, true);
+}
+
+int nw_align_ops_resident(nw_ctx* c, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                          int64_t* ops_off, nw_stat* stats) {
+    return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, false);
 }
 
 int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes) {

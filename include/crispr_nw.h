@@ -184,6 +184,11 @@ int nw_batch_download_ops(nw_ctx* ctx, uint32_t* ops_out, int64_t ops_cap, int64
  * repair alignment, CRISPRessoCORE.py:1808-1828 with just_score). */
 int nw_align_ops(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out,
                  int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* nw_align_ops on the batch the last nw_align_ops of this context uploaded (still in
+ * HBM: no upload), against the current reference -- the second pass of the same reads
+ * (HDR amplicon, CRISPRessoCORE.py:1808-1828).  offsets / n must be that batch's. */
+int nw_align_ops_resident(nw_ctx* ctx, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                          int64_t* ops_off, nw_stat* stats);
 /* Last nw_align_ops: span of the uploads on the copy stream, sum of the chunks'
  * kernel spans, bytes each way. */
 int nw_ops_times(const nw_ctx* ctx, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes);

@@ -131,3 +131,24 @@ def test_rows_api_unaffected_by_ops_mode(gpu_aligner_factory, oracle):
     a.set_reference(amp)
     a.set_output("ops")
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off, mode="rows"), "rows-after-ops")
+
+
+def test_resident_second_pass_hdr(gpu_aligner_factory, oracle):
+    """The HDR pass over the same reads (nw_align_ops_resident): no upload, records
+    equal to a fresh call against the HDR amplicon; a different batch is refused."""
+    from crispresso_amd import synth as sy
+
+    amp, hdr, buf, off = sy.c3_workload(3000)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    first = a.align_ops(buf, off)
+    assert_same(oracle, amp, buf, off, first.expand(amp, buf, off), "c3-amp")
+    a.set_reference(hdr)
+    again = a.align_ops(None, off, resident=True)
+    assert a.ops_times()["h2d_bytes"] == 0
+    assert_same(oracle, hdr, buf, off, again.expand(hdr, buf, off), "c3-hdr-resident")
+    rec = a.align_ops(None, off, resident=True, records_only=True)
+    for f in FIELDS:
+        assert np.array_equal(rec.stats[f], again.stats[f])
+    with pytest.raises(NeedleError):
+        a.align_ops(None, off[:101], resident=True)
