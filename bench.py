@@ -24,8 +24,8 @@ outside the timed region), "roofline" (HBM: algorithmic bytes per pass over the
 kernel-resident pass time; VALU: issue fraction of nw_band_fill<16>),
 "cpu_baseline" (the CPU oracle -- a port, EMBOSS is absent -- on bounded samples,
 1 thread and the box's CPU share, rank 0 at N = 1 only); legs either side of the
-path at N = 1: "dual_alignment" (C3, CORE:1808-1828), "downstream_quantification",
-"upstream_merge".
+path at N = 1: "dual_alignment" (C3, CORE:1808-1828), "pooled" (C5, 96 amplicons,
+CRISPRessoPooled.py:882-908), "downstream_quantification", "upstream_merge".
 """
 from __future__ import annotations
 
@@ -304,6 +304,60 @@ def dual_leg(device, n_reads, steps, warmup):
     return out
 
 
+def pooled_workload(n_amplicons, reads_per_amplicon):
+    """C5: 96 amplicons of U[150, 300] bp (seed 5), reads from each with the C2 mix
+    (seed 100 + g), grouped by amplicon as CRISPRessoPooled's demultiplexing leaves them."""
+    from crispresso_amd import synth
+
+    amps = synth.pooled_amplicons(n_amplicons, 5)
+    bufs, lens = [], []
+    for g, amp in enumerate(amps):
+        b, o = synth.reads_from(amp, reads_per_amplicon, 100 + g)
+        bufs.append(b)
+        lens.append(np.diff(o))
+    lens = np.concatenate(lens)
+    off = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    which = np.repeat(np.arange(n_amplicons, dtype=np.int32), reads_per_amplicon)
+    return amps, np.concatenate(bufs), off, which
+
+
+def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
+    """C5 on one GPU: one nw_align_multi_ops call over all amplicons' reads (pinned host
+    buffers in, records + runs out), next to the same number of C2 single-amplicon reads."""
+    from crispresso_amd import _lib
+    from crispresso_amd.aligner import GpuAligner
+
+    amps, buf, off, which = pooled_workload(n_amplicons, reads_per_amplicon)
+    n = len(off) - 1
+    pb, po, pw = _lib.pinned_copy(buf), _lib.pinned_copy(off), _lib.pinned_copy(which)
+    stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
+    ops_off = _lib.PinnedBuffer(n + 1, np.int64)
+    ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
+    out = (stats.array, ops.array, ops_off.array)
+    al = GpuAligner(device)
+    for _ in range(warmup):
+        al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ob = al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
+    dt = (time.perf_counter() - t0) / steps
+    lens = np.diff(off)
+    amp_len = np.array([len(a) for a in amps])[which]
+    res = {"metric": "pooled aligned reads/s (C5: 96 amplicons x reads, 150-300 bp, 1 GPU)", "value": n / dt,
+           "unit": "aligned reads/s", "ms_per_step": dt * 1e3, "reads": n, "amplicons": n_amplicons,
+           "reads_per_amplicon": reads_per_amplicon, "mean_read_len": float(lens.mean()),
+           "cells_full_matrices": int((amp_len * lens).sum()), "path_counts": al.path_counts(),
+           "pcie": al.ops_times(), "runs_per_read": int(ob.ops_off[n]) / n,
+           "algo_bytes_per_step": int(lens.sum() + 3 * stats.array["aln_len"].astype(np.int64).sum() + 16 * n),
+           "note": "step = one nw_align_multi_ops call: every amplicon's tables uploaded once, reads (grouped by "
+                   "amplicon, as demultiplexed) pipelined in chunks of one amplicon each"}
+    for b in (pb, po, pw, stats, ops_off, ops):
+        b.close()
+    al.close()
+    return res
+
+
 def merge_leg(device, n_pairs):
     """The paired-end merge (crispresso_amd/flash.py, FLASH semantics) on synthetic pairs of the
     same shape as scripts/bench_flash.py: 2 x 150 bp over a 250 bp amplicon, 1 % noise, seed 7,
@@ -360,6 +414,8 @@ def main():
     ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
     ap.add_argument("--no-legs", action="store_true", help="skip the C3 / merge legs (N = 1 only)")
     ap.add_argument("--merge-pairs", type=int, default=1_000_000)
+    ap.add_argument("--pooled-amplicons", type=int, default=96)
+    ap.add_argument("--pooled-reads", type=int, default=100_000, help="C5 reads per amplicon")
     args = ap.parse_args()
 
     rank, local, world, dist = dist_setup()
@@ -412,17 +468,18 @@ def main():
         quant = quant_leg(al, amplicon, buf, offsets, n, args.steps, args.warmup, rank, world, args.quant_cpu_sample,
                           args.no_cpu)
 
-    dual = merge = None
+    legs = {"dual": None, "pooled": None, "merge": None}
     if rank == 0 and world == 1 and not args.no_legs:
-        for name in ("dual", "merge"):
+        for name in legs:
             try:   # informational legs: never cost the bench line
                 if name == "dual":
-                    dual = dual_leg(local, args.reads, args.steps, args.warmup)
+                    legs[name] = dual_leg(local, args.reads, args.steps, args.warmup)
+                elif name == "pooled":
+                    legs[name] = pooled_leg(local, args.pooled_amplicons, args.pooled_reads, 2, 1)
                 else:
-                    merge = merge_leg(local, args.merge_pairs)
+                    legs[name] = merge_leg(local, args.merge_pairs)
             except Exception as exc:
-                r = {"error": f"{type(exc).__name__}: {exc}"}
-                dual, merge = (r, merge) if name == "dual" else (dual, r)
+                legs[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
     traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
                                        "nw::nw_ops_", required="nw::nw_band_fill<16>")
@@ -509,9 +566,10 @@ def main():
                 },
             },
             "cpu_baseline": cpu,
-            "dual_alignment": dual,
+            "dual_alignment": legs["dual"],
+            "pooled": legs["pooled"],
             "downstream_quantification": quant,
-            "upstream_merge": merge,
+            "upstream_merge": legs["merge"],
         }
         print(json.dumps(line), flush=True)
     for b in (pb, po, p_stats, p_off, p_ops):

@@ -354,6 +354,40 @@ class GpuAligner:
         buf, offsets = pack_reads(reads)
         return self.align_packed(buf, offsets)
 
+    def align_multi_ops(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
+                        amplicon_of_read: np.ndarray, out: Optional[tuple] = None) -> OpsBatch:
+        """Pooled batch, ops output (nw_align_multi_ops): read r against
+        amplicons[amplicon_of_read[r]]; records and runs in read order.  Reads grouped
+        by amplicon are aligned in place.  Leaves no amplicon set on this aligner."""
+        amps = [a.strip().upper() for a in amplicons]
+        refs = "".join(amps).encode()
+        roff = np.zeros(len(amps) + 1, dtype=np.int64)
+        roff[1:] = np.cumsum([len(a) for a in amps])
+        idx = np.ascontiguousarray(amplicon_of_read, dtype=np.int32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(offsets) - 1
+        if len(idx) != n:
+            raise NeedleError(f"{len(idx)} amplicon indices for {n} reads")
+        if out is None:
+            stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+            ops_off = np.zeros(n + 1, dtype=np.int64)
+            ops = np.empty(2 * n + 4096, dtype=np.uint32)
+        else:
+            stats, ops, ops_off = out
+
+        def call(o):
+            return self.lib.nw_align_multi_ops(self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf),
+                                               _lib.ptr(offsets), _lib.ptr(idx), n, _lib.ptr(o), len(o),
+                                               _lib.ptr(ops_off), _lib.ptr(stats))
+
+        rc = call(ops)
+        if rc == _lib.NW_E_CAPACITY:
+            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            rc = call(ops)
+        self.reference = None
+        self._check(rc, "nw_align_multi_ops")
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(offsets), self.scale, self.options.awidth)
+
     def align_multi(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
                     amplicon_of_read: np.ndarray) -> AlignmentBatch:
         """Pooled batch: read r against amplicons[amplicon_of_read[r]] (nw_align_multi).

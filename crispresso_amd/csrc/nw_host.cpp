@@ -48,6 +48,19 @@ struct DevBuf {
 
 }  // namespace
 
+// One amplicon's device tables (pointers into nw_ctx::d_arena).
+struct Profile {
+    const int8_t* prof = nullptr;      // [NCODE][64][RP] int8: exact kernel
+    const int16_t* prof16 = nullptr;   // stream walk (rows padded on top)
+    const int16_t* prof16f = nullptr;  // stream fill: prof16 + 2 * extend (biased recurrence)
+    const uint32_t* ptab = nullptr;    // stream fill: pair-code score table (R <= 4)
+    const uint32_t* rowpos = nullptr;  // band walk: codes each row scores > 0 against
+    const uint8_t* amp = nullptr;      // amplicon bytes (+16 pad)
+    int R = 0;
+    bool amp_in_table = false;         // amplicon within A C G T N (the band score table)
+    bool have_ptab = false;
+};
+
 struct nw_ctx {
     int device = 0;
     int num_cus = 256;
@@ -62,14 +75,9 @@ struct nw_ctx {
     int scale = 2, gap_open = 20, gap_extend = 1;
     // reference
     std::string ref;
-    int R = 0;
-    DevBuf<int8_t> d_prof;
-    DevBuf<int16_t> d_prof16;         // pair kernel: int16, rows padded on top
-    DevBuf<int16_t> d_prof16f;        // stream fill: d_prof16 + 2 * extend (biased recurrence)
-    DevBuf<uint32_t> d_ptab;          // stream kernel: pair-code score table (R <= 4)
-    DevBuf<uint8_t> d_lut6;
-    bool have_ptab = false;
-    DevBuf<uint8_t> d_lut, d_amp;
+    DevBuf<uint8_t> d_arena;          // every amplicon's tables (upload_profiles)
+    Profile cur{};                    // the amplicon being aligned
+    DevBuf<uint8_t> d_lut6, d_lut;
     // batch
     int64_t n = 0;
     int32_t lb_max = 0;
@@ -94,7 +102,6 @@ struct nw_ctx {
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
     // certified diagonal-band kernels (nw_band.hip): the default path
-    bool amp_in_table = false;         // amplicon within A C G T N / unknown (the band score table)
     bool use_diag = false;
     nw::LaunchCfg diag_fill{}, diag_walk{};          // 32-diagonal level (the certificate's last resort)
     nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
@@ -102,7 +109,7 @@ struct nw_ctx {
     DevBuf<int32_t> d_redo;                          // reads the first level could not certify
     DevBuf<uint8_t> d_redo_flags;                    // per sorted position: handed to the second level
     DevBuf<int32_t> d_redo_blk;
-    DevBuf<uint32_t> d_btab, d_rowpos;
+    DevBuf<uint32_t> d_btab;
     DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
     DevBuf<uint8_t> d_bregion;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -150,121 +157,179 @@ int fail(nw_ctx* c, int code, const char* fmt, ...) {
                         "%s failed: %s", #expr, hipGetErrorString(e_));               \
     } while (0)
 
-int build_profile(nw_ctx* c) {
-    const int La = (int)c->ref.size();
+// One amplicon's score tables (host side): the int8 profile of the exact kernel,
+// the int16 profiles and pair-code table of the stream kernels, the markup bits of
+// the band walk (codes each row scores > 0 against).
+struct AmpTables {
+    int R = 0;
+    bool amp_in_table = true;   // amplicon within A C G T N / unknown (the band score table)
+    bool have_ptab = false;
+    std::vector<int8_t> prof;
+    std::vector<int16_t> prof16, prof16f;
+    std::vector<uint32_t> ptab, rowpos;
+};
+
+bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
+    const int La = (int)ref.size();
     const int R = nw::rows_per_lane_for(La);
-    if (R < 0) return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", La, kMaxRef);
+    if (R < 0) return false;
+    t->R = R;
     const int RP = nw::profile_rp(R);
-    std::vector<int8_t> prof((size_t)nw::NCODE * 64 * RP, 0);
+    t->prof.assign((size_t)nw::NCODE * 64 * RP, 0);
     for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
+        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
         for (int code = 0; code < nw::NCODE; ++code) {
-            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * c->scale : 0;
-            prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
+            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * scale : 0;
+            t->prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
         }
     }
-    // int16 profile of the pair kernel: rows padded on top so that the last
+    // int16 profile of the stream kernels: rows padded on top so that the last
     // amplicon row is the bottom row of the last lane
     const int R4 = (R + 3) & ~3;
     const int nl = (La + R - 1) / R, F = nl * R - La;
-    std::vector<int16_t> prof16((size_t)nw::NCODE * 64 * R4, 0);
+    t->prof16.assign((size_t)nw::NCODE * 64 * R4, 0);
     for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
+        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
         const int g = ai + F;
         for (int code = 0; code < nw::NCODE; ++code) {
-            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * c->scale : 0;
-            prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
+            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * scale : 0;
+            t->prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
         }
     }
     // The stream fill runs the recurrence on values biased by (r + c) * extend
     // (nw_stream.hip): the diagonal step then gains 2 * extend, folded into its
-    // scores here.  prof16 itself stays unbiased (walk, pair kernel).
-    const int bias2 = 2 * c->gap_extend;
-    std::vector<int16_t> prof16f(prof16.size());
-    for (size_t q = 0; q < prof16.size(); ++q) prof16f[q] = (int16_t)(prof16[q] + bias2);
-    // ascii -> A T G C N pad/unknown (0..5), 6 = other IUPAC codes: the alphabet of
-    // the stream kernel's pair table and of the certified-band score table
-    {
-        const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
-        uint8_t lut6[256];
-        for (int q = 0; q < 256; ++q) {
-            const int code = nw::code_of((unsigned char)q);
-            int r = nw::kPairCodes;   // not in the table
-            for (int i = 0; i < nw::kPairCodes; ++i)
-                if (codes[i] == code) r = i;
-            lut6[q] = (uint8_t)r;
-        }
-        HIP_OR_FAIL(c, c->d_lut6.reserve(256));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut6.p, lut6, 256, hipMemcpyHostToDevice, c->stream));
-    }
+    // scores here.  prof16 itself stays unbiased (walk).
+    t->prof16f.resize(t->prof16.size());
+    for (size_t q = 0; q < t->prof16.size(); ++q) t->prof16f[q] = (int16_t)(t->prof16[q] + 2 * E);
     // pair-code table of the stream kernel: for every (code of read A, code of
     // read B) over A T G C N pad, each lane's 4 rows as packed int16x2 (biased)
-    c->have_ptab = false;
+    t->have_ptab = false;
+    t->ptab.clear();
     if (R4 == 4) {
         const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
-        std::vector<uint32_t> ptab((size_t)nw::kPairCodes * nw::kPairCodes * 64 * 4, 0u);
+        t->ptab.assign((size_t)nw::kPairCodes * nw::kPairCodes * 64 * 4, 0u);
         for (int ia = 0; ia < nw::kPairCodes; ++ia)
             for (int ib = 0; ib < nw::kPairCodes; ++ib)
                 for (int ln = 0; ln < 64; ++ln)
                     for (int k = 0; k < 4; ++k) {
                         const size_t src = (size_t)ln * R4 + k;
-                        const uint16_t sa = (uint16_t)prof16f[(size_t)codes[ia] * 64 * R4 + src];
-                        const uint16_t sb = (uint16_t)prof16f[(size_t)codes[ib] * 64 * R4 + src];
-                        ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
+                        const uint16_t sa = (uint16_t)t->prof16f[(size_t)codes[ia] * 64 * R4 + src];
+                        const uint16_t sb = (uint16_t)t->prof16f[(size_t)codes[ib] * 64 * R4 + src];
+                        t->ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
                     }
-        HIP_OR_FAIL(c, c->d_ptab.reserve(ptab.size()));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_ptab.p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice, c->stream));
         const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
-        c->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
+        t->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
     }
-    // certified-band score table: [amplicon code][read A code][read B code] over
-    // A T G C N pad/unknown, packed int16x2 + 2 * extend (biased recurrence), and
     // per amplicon row the codes it scores > 0 against (markup ':')
-    {
-        const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
-        auto sub6 = [&](int x, int y) {
-            const int cx = codes6[x], cy = codes6[y];
-            return (cx < 16 && cy < 16) ? nw::kEdna[cx][cy] * c->scale : 0;
-        };
-        std::vector<uint32_t> btab(216);
-        for (int x = 0; x < 6; ++x)
-            for (int ya = 0; ya < 6; ++ya)
-                for (int yb = 0; yb < 6; ++yb) {
-                    const uint16_t sa = (uint16_t)(int16_t)(sub6(x, ya) + 2 * c->gap_extend);
-                    const uint16_t sb = (uint16_t)(int16_t)(sub6(x, yb) + 2 * c->gap_extend);
-                    btab[(size_t)x * 36 + ya * 6 + yb] = sa | ((uint32_t)sb << 16);
-                }
-        std::vector<uint32_t> rowpos((size_t)La);
-        c->amp_in_table = true;
-        for (int ai = 0; ai < La; ++ai) {
-            const uint8_t ca = nw::code_of((unsigned char)c->ref[ai]);
-            uint32_t m = 0;
-            for (int code = 0; code < nw::NCODE; ++code)
-                if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
-            rowpos[(size_t)ai] = m;
-            bool in6 = false;
-            for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
-            c->amp_in_table = c->amp_in_table && in6;
-        }
-        HIP_OR_FAIL(c, c->d_btab.reserve(btab.size()));
-        HIP_OR_FAIL(c, c->d_rowpos.reserve(rowpos.size()));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_btab.p, btab.data(), btab.size() * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_rowpos.p, rowpos.data(), rowpos.size() * 4, hipMemcpyHostToDevice, c->stream));
+    const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+    t->rowpos.resize((size_t)La);
+    t->amp_in_table = true;
+    for (int ai = 0; ai < La; ++ai) {
+        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
+        uint32_t m = 0;
+        for (int code = 0; code < nw::NCODE; ++code)
+            if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
+        t->rowpos[(size_t)ai] = m;
+        bool in6 = false;
+        for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
+        t->amp_in_table = t->amp_in_table && in6;
     }
-    HIP_OR_FAIL(c, c->d_prof16.reserve(prof16.size()));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16.p, prof16.data(), prof16.size() * 2, hipMemcpyHostToDevice, c->stream));
-    HIP_OR_FAIL(c, c->d_prof16f.reserve(prof16f.size()));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof16f.p, prof16f.data(), prof16f.size() * 2, hipMemcpyHostToDevice, c->stream));
-    uint8_t lut[256];
-    for (int q = 0; q < 256; ++q) lut[q] = nw::code_of((unsigned char)q);
-    HIP_OR_FAIL(c, c->d_prof.reserve(prof.size()));
+    return true;
+}
+
+// The tables every amplicon shares (they depend on the penalties only): ascii ->
+// A T G C N pad/unknown (0..5, 6 = other IUPAC: the band / pair-table alphabet),
+// ascii -> EDNAFULL code, and the certified-band score table [amplicon code][read A
+// code][read B code] over A T G C N pad, packed int16x2 + 2 * extend.
+int upload_shared(nw_ctx* c) {
+    const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+    std::vector<uint8_t> lut6(256), lut(256);
+    for (int q = 0; q < 256; ++q) {
+        const int code = nw::code_of((unsigned char)q);
+        int r = nw::kPairCodes;
+        for (int i = 0; i < nw::kPairCodes; ++i)
+            if (codes6[i] == code) r = i;
+        lut6[(size_t)q] = (uint8_t)r;
+        lut[(size_t)q] = (uint8_t)code;
+    }
+    auto sub6 = [&](int x, int y) {
+        const int cx = codes6[x], cy = codes6[y];
+        return (cx < 16 && cy < 16) ? nw::kEdna[cx][cy] * c->scale : 0;
+    };
+    std::vector<uint32_t> btab(216);
+    for (int x = 0; x < 6; ++x)
+        for (int ya = 0; ya < 6; ++ya)
+            for (int yb = 0; yb < 6; ++yb) {
+                const uint16_t sa = (uint16_t)(int16_t)(sub6(x, ya) + 2 * c->gap_extend);
+                const uint16_t sb = (uint16_t)(int16_t)(sub6(x, yb) + 2 * c->gap_extend);
+                btab[(size_t)x * 36 + ya * 6 + yb] = sa | ((uint32_t)sb << 16);
+            }
+    HIP_OR_FAIL(c, c->d_lut6.reserve(256));
     HIP_OR_FAIL(c, c->d_lut.reserve(256));
-    HIP_OR_FAIL(c, c->d_amp.reserve((size_t)La + 16));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_prof.p, prof.data(), prof.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lut.p, lut, 256, hipMemcpyHostToDevice, c->stream));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_amp.p, c->ref.data(), La, hipMemcpyHostToDevice, c->stream));
-    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
-    c->R = R;
+    HIP_OR_FAIL(c, c->d_btab.reserve(btab.size()));
+    HIP_OR_FAIL(c, hipMemcpy(c->d_lut6.p, lut6.data(), 256, hipMemcpyHostToDevice));
+    HIP_OR_FAIL(c, hipMemcpy(c->d_lut.p, lut.data(), 256, hipMemcpyHostToDevice));
+    HIP_OR_FAIL(c, hipMemcpy(c->d_btab.p, btab.data(), btab.size() * 4, hipMemcpyHostToDevice));
+    return NW_OK;
+}
+
+// Every amplicon's tables in one device arena (one upload): profs[g] points into it.
+int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector<Profile>* profs) {
+    std::vector<AmpTables> tabs(refs.size());
+    size_t total = 0;
+    auto sec = [&](size_t bytes) {
+        const size_t at = total;
+        total += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    struct Off { size_t prof, prof16, prof16f, ptab, rowpos, amp; };
+    std::vector<Off> offs(refs.size());
+    for (size_t g = 0; g < refs.size(); ++g) {
+        if (!amp_tables(refs[g], c->scale, c->gap_extend, &tabs[g]))
+            return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", (int)refs[g].size(), kMaxRef);
+        const AmpTables& t = tabs[g];
+        const size_t o1 = sec(t.prof.size()), o2 = sec(t.prof16.size() * 2), o3 = sec(t.prof16f.size() * 2);
+        const size_t o4 = sec(t.ptab.size() * 4), o5 = sec(t.rowpos.size() * 4), o6 = sec(refs[g].size() + 16);
+        offs[g] = {o1, o2, o3, o4, o5, o6};
+    }
+    std::vector<uint8_t> host(std::max<size_t>(total, 256), 0);
+    for (size_t g = 0; g < refs.size(); ++g) {
+        const AmpTables& t = tabs[g];
+        const Off& o = offs[g];
+        std::memcpy(host.data() + o.prof, t.prof.data(), t.prof.size());
+        std::memcpy(host.data() + o.prof16, t.prof16.data(), t.prof16.size() * 2);
+        std::memcpy(host.data() + o.prof16f, t.prof16f.data(), t.prof16f.size() * 2);
+        if (!t.ptab.empty()) std::memcpy(host.data() + o.ptab, t.ptab.data(), t.ptab.size() * 4);
+        std::memcpy(host.data() + o.rowpos, t.rowpos.data(), t.rowpos.size() * 4);
+        std::memcpy(host.data() + o.amp, refs[g].data(), refs[g].size());
+    }
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));   // no kernel may still read the old arena
+    HIP_OR_FAIL(c, c->d_arena.reserve(host.size()));
+    HIP_OR_FAIL(c, hipMemcpy(c->d_arena.p, host.data(), host.size(), hipMemcpyHostToDevice));
+    profs->resize(refs.size());
+    for (size_t g = 0; g < refs.size(); ++g) {
+        const Off& o = offs[g];
+        uint8_t* b = c->d_arena.p;
+        Profile& p = (*profs)[g];
+        p.prof = (const int8_t*)(b + o.prof);
+        p.prof16 = (const int16_t*)(b + o.prof16);
+        p.prof16f = (const int16_t*)(b + o.prof16f);
+        p.ptab = tabs[g].ptab.empty() ? nullptr : (const uint32_t*)(b + o.ptab);
+        p.rowpos = (const uint32_t*)(b + o.rowpos);
+        p.amp = b + o.amp;
+        p.R = tabs[g].R;
+        p.amp_in_table = tabs[g].amp_in_table;
+        p.have_ptab = tabs[g].have_ptab && p.ptab;
+    }
+    return NW_OK;
+}
+
+int build_profile(nw_ctx* c) {
+    int rc = upload_shared(c);
+    if (rc) return rc;
+    std::vector<Profile> one;
+    if ((rc = upload_profiles(c, {c->ref}, &one))) return rc;
+    c->cur = one[0];
     return NW_OK;
 }
 
@@ -276,7 +341,7 @@ int configure(nw_ctx* c) {
     if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))   // tests: band width of the full-matrix kernels
         c->band_slots = c->stream_slots = std::max(0, std::atoi(bs));
     const int La = (int)c->ref.size();
-    const int R = c->R;
+    const int R = c->cur.R;
     // full-storage kernel: every alignment (band disabled) or only the fallbacks
     nw::LaunchCfg cfg{};
     cfg.R = R;
@@ -325,7 +390,7 @@ int configure(nw_ctx* c) {
     c->use_diag = false;
     const bool want_diag = !kern || std::strcmp(kern, "diag") == 0;
     const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
-    if (want_diag && c->amp_in_table && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
+    if (want_diag && c->cur.amp_in_table && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
         c->gap_open >= c->gap_extend) {
         const int64_t pairs = (c->n + 1) / 2;
         int64_t cap_bytes = 16ll << 30;
@@ -393,9 +458,9 @@ int configure(nw_ctx* c) {
         w.lds_bytes = nw::stream_walk_lds_bytes(La, w.wpb);
         int fb = 0, wb = 0, best = -1;
         for (int wpb : {4, 8, 10}) {
-            const int lds = nw::stream_fill_lds_bytes(R, c->have_ptab, wpb);
+            const int lds = nw::stream_fill_lds_bytes(R, c->cur.have_ptab, wpb);
             int b = 0, wb2 = 0;
-            HIP_OR_FAIL(c, nw::stream_occupancy(R, c->have_ptab, wpb, w.wpb, lds, w.lds_bytes, &b, &wb2));
+            HIP_OR_FAIL(c, nw::stream_occupancy(R, c->cur.have_ptab, wpb, w.wpb, lds, w.lds_bytes, &b, &wb2));
             if (b * wpb > best) { best = b * wpb; fb = b; wb = wb2; f.wpb = wpb; f.lds_bytes = lds; }
         }
         if (fb > 0 && wb > 0) {
@@ -454,12 +519,12 @@ void nw_destroy(nw_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    c->d_prof.release(); c->d_lut.release(); c->d_amp.release();
+    c->d_arena.release(); c->d_lut.release();
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
     c->d_stats.release(); c->d_tb.release(); c->d_region.release();
-    c->d_prof16.release(); c->d_prof16f.release(); c->d_fallback.release(); c->d_fallback_count.release();
-    c->d_ptab.release(); c->d_lut6.release();
-    c->d_btab.release(); c->d_rowpos.release(); c->d_redo.release(); c->d_redo_flags.release(); c->d_redo_blk.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
+    c->d_fallback.release(); c->d_fallback_count.release();
+    c->d_lut6.release();
+    c->d_btab.release(); c->d_redo.release(); c->d_redo_flags.release(); c->d_redo_blk.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
     c->d_slots.release(); c->d_spill.release(); c->d_staging[0].release(); c->d_staging[1].release();
     c->d_nops.release(); c->d_opsctl.release(); c->d_ctl64.release(); c->d_blk.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
@@ -583,11 +648,11 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.reads = c->d_reads.p - c->reads_bias;
     a.offsets = c->d_offsets.p + base;
     a.n = c->n;
-    a.prof = c->d_prof.p;
+    a.prof = c->cur.prof;
     a.ptab = nullptr;
     a.lut6 = nullptr;
     a.lut = c->d_lut.p;
-    a.amp = c->d_amp.p;
+    a.amp = c->cur.amp;
     a.La = (int32_t)c->ref.size();
     a.gap_open = c->gap_open;
     a.gap_extend = c->gap_extend;
@@ -596,7 +661,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.stride = c->stride;
     a.stats = c->d_stats.p + base;
     a.tb_global = c->d_tb.p;
-    a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->R, c->lb_max) : 0;
+    a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
     a.band_slots = c->band_slots;
     a.fallback_list = c->d_fallback.p + base;
     a.fallback_count = c->d_fallback_count.p;
@@ -625,7 +690,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.band_lb_cap = c->diag_lb_cap;
         a.band_maxsub = 5 * c->scale;
         a.band_tab = c->d_btab.p;
-        a.rowpos = c->d_rowpos.p;
+        a.rowpos = c->cur.rowpos;
         a.sort_hist = c->d_sort_hist.p;
         a.sort_key = c->d_sort_key.p;
         a.band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
@@ -685,11 +750,11 @@ int launch_range(nw_ctx* c, int64_t base) {
                 ap.ops = a.ops + lo * a.ops_slot;
                 ap.nops = a.nops + lo;
             }
-            ap.prof = (const int8_t*)c->d_prof16.p;
-            ap.prof_fill = c->d_prof16f.p;
+            ap.prof = (const int8_t*)c->cur.prof16;
+            ap.prof_fill = c->cur.prof16f;
             ap.band_slots = c->stream_slots;
             ap.region = c->d_region.p;
-            ap.ptab = c->have_ptab ? c->d_ptab.p : nullptr;
+            ap.ptab = c->cur.have_ptab ? c->cur.ptab : nullptr;
             ap.lut6 = c->d_lut6.p;
             ap.fallback_list = a.fallback_list + lo;
             ap.fallback_count = c->d_fallback_count.p + 4 * q;
@@ -1101,12 +1166,21 @@ int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t
 
 namespace {
 
-// nw_align_ops (upload = true) and nw_align_ops_resident (the batch the last call
-// uploaded, still in HBM: no upload).
+// Amplicon groups of a pooled call: reads [first[g], first[g + 1]) align against
+// refs[g] (tables profs[g] in the arena).
+struct Groups {
+    const std::vector<std::string>* refs;
+    const std::vector<Profile>* profs;
+    const std::vector<int64_t>* first;
+};
+
+// nw_align_ops (upload = true), nw_align_ops_resident (the batch the last call
+// uploaded, still in HBM: no upload) and nw_align_multi_ops (groups: chunks never
+// straddle two amplicons; each chunk's kernels use its amplicon's tables).
 int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
-             int64_t* ops_off, nw_stat* stats, bool upload) {
+             int64_t* ops_off, nw_stat* stats, bool upload, const Groups* groups = nullptr) {
     if (!c) return NW_E_INVALID;
-    if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
+    if (!groups && c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || (upload && !reads) || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
     if (!upload && !(c->resident_ok && c->resident_n == n && (n == 0 || (c->resident_lo == offsets[0] &&
@@ -1114,7 +1188,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return fail(c, NW_E_STATE, "no resident batch of these %lld reads (nw_align_ops uploads one)", (long long)n);
     if (upload) c->resident_ok = false;
     (void)hipSetDevice(c->device);
-    const int La = (int)c->ref.size();
     int32_t lb_max = 1;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t len = offsets[r + 1] - offsets[r];
@@ -1124,19 +1197,40 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     int64_t chunk = 131072;
     if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
     chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
+    // chunks [lo, hi) of one amplicon group each
+    struct Chunk { int64_t lo, hi; int g; };
+    std::vector<Chunk> chunks;
+    const int ngroups = groups ? (int)groups->refs->size() : 1;
+    for (int g = 0; g < ngroups; ++g) {
+        const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
+        for (int64_t lo = g0; lo < g1; lo += chunk) chunks.push_back({lo, std::min(g1, lo + chunk), g});
+    }
     const int mode_before = c->out_mode;
     c->out_mode = NW_OUT_OPS;
     c->ran = false;
     c->call_done = false;
     c->lb_max = lb_max;
-    c->stride = stride_for(La, lb_max);
     c->cells = 0;
-    c->n = chunk;
-    int rc = configure(c);
+    auto use_group = [&](int g, int64_t reads_in_chunk) {
+        if (groups) {
+            c->ref = (*groups->refs)[(size_t)g];
+            c->cur = (*groups->profs)[(size_t)g];
+        }
+        c->stride = stride_for((int)c->ref.size(), lb_max);
+        c->n = reads_in_chunk;
+        return configure(c);
+    };
+    int rc = NW_OK;
+    // configure every group once up front: the buffers reach their largest size before
+    // anything is queued (no allocation inside the pipeline)
+    for (int g = 0; g < ngroups && !rc; ++g) {
+        const int64_t gn = groups ? (*groups->first)[(size_t)g + 1] - (*groups->first)[(size_t)g] : n;
+        if (gn > 0 || ngroups == 1) rc = use_group(g, std::max<int64_t>(1, std::min(chunk, gn)));
+    }
     if (!rc) rc = ops_reserve(c, chunk, n);
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
-    const int64_t nchunks = n ? (n + chunk - 1) / chunk : 0;
+    const int64_t nchunks = (int64_t)chunks.size();
     auto restore = [&](int code) {
         c->out_mode = mode_before;
         c->n = 0;
@@ -1153,7 +1247,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // every upload queued up front: the copy engine streams the batch while chunks compute
     HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
     for (int64_t k = 0; upload && k < nchunks; ++k) {
-        const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
+        const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
         if (b1 > b0)
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p + (b0 - base0), reads + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice,
@@ -1181,12 +1275,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
+    bool any_diag = false;
     for (int64_t k = 0; k < nchunks; ++k) {
-        const int64_t lo = k * chunk, hi = std::min(n, lo + chunk);
+        const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_in[(size_t)k], 0));
         if (k >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_out[(size_t)(k - 2)], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->stream));
-        c->n = hi - lo;
+        if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
+        any_diag = any_diag || c->use_diag;
         if ((rc = launch_range_ops(c, lo, (int)(k & 1)))) return restore(rc);
         HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
                                       hipMemcpyDeviceToHost, c->stream));
@@ -1204,10 +1300,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     ops_off[n] = total;
     if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)
         const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);
-        const bool two = c->use_diag && c->diag16_fill.grid > 0;
-        c->call_counts[0] = c->use_diag ? n - h[6] : 0;
+        const bool two = any_diag && c->diag16_fill.grid > 0;
+        c->call_counts[0] = any_diag ? n - h[6] : 0;
         c->call_counts[1] = two ? h[6] : 0;
-        c->call_counts[2] = c->use_diag ? (two ? h[5] : h[6]) : 0;
+        c->call_counts[2] = any_diag ? (two ? h[5] : h[6]) : 0;
         c->call_counts[3] = h[4];
     }
     c->call_done = true;
@@ -1246,6 +1342,85 @@ int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n
 int nw_align_ops_resident(nw_ctx* c, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
                           int64_t* ops_off, nw_stat* stats) {
     return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, false);
+}
+
+// Pooled batch, ops output (CRISPRessoPooled.py:882-908 runs one CRISPResso -- one
+// needle per pass -- per amplicon): one call, every amplicon's tables uploaded once,
+// chunks of one amplicon each pipelined as in nw_align_ops.  Reads grouped by
+// amplicon (ref_of_read non-decreasing, as the demultiplexed per-amplicon read sets
+// arrive) are used in place; otherwise they are grouped on the host first and the
+// outputs put back in the caller's order.
+int nw_align_multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
+                       const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                       int64_t* ops_off, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (n_refs <= 0 || !refs || !ref_offsets) return fail(c, NW_E_INVALID, "no amplicons");
+    if (n < 0 || (n > 0 && (!reads || !offsets || !ref_of_read || !stats)) || !ops_off)
+        return fail(c, NW_E_INVALID, "bad batch");
+    std::vector<std::string> amps((size_t)n_refs);
+    for (int32_t g = 0; g < n_refs; ++g) {
+        const int64_t L = ref_offsets[g + 1] - ref_offsets[g];
+        if (L <= 0 || L > kMaxRef) return fail(c, NW_E_UNSUPPORTED, "amplicon %d has length %lld", g, (long long)L);
+        amps[(size_t)g].assign(refs + ref_offsets[g], refs + ref_offsets[g + 1]);
+    }
+    (void)hipSetDevice(c->device);
+    std::vector<int64_t> first((size_t)n_refs + 1, 0);
+    bool grouped = true;
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t g = ref_of_read[r];
+        if (g < 0 || g >= n_refs) return fail(c, NW_E_INVALID, "read %lld has amplicon index %d", (long long)r, g);
+        ++first[(size_t)g + 1];
+        grouped = grouped && (r == 0 || g >= ref_of_read[r - 1]);
+    }
+    for (int32_t g = 0; g < n_refs; ++g) first[(size_t)g + 1] += first[(size_t)g];
+    int rc = upload_shared(c);
+    std::vector<Profile> profs;
+    if (!rc) rc = upload_profiles(c, amps, &profs);
+    if (rc) return rc;
+    c->ref.clear();   // the context has no single amplicon afterwards (nw_set_reference again)
+    c->cur = Profile{};
+    Groups grp{&amps, &profs, &first};
+    if (grouped) {
+        rc = ops_call(c, reads, offsets, n, ops_out, ops_cap, ops_off, stats, true, &grp);
+        c->ref.clear();
+        c->cur = Profile{};
+        return rc;
+    }
+    // group on the host (stable), align, then back to the caller's order
+    std::vector<int64_t> order((size_t)n), fill(first.begin(), first.end() - 1);
+    for (int64_t r = 0; r < n; ++r) order[(size_t)fill[(size_t)ref_of_read[r]]++] = r;
+    std::vector<int64_t> soff((size_t)n + 1, 0);
+    for (int64_t s2 = 0; s2 < n; ++s2)
+        soff[(size_t)s2 + 1] = soff[(size_t)s2] + (offsets[order[(size_t)s2] + 1] - offsets[order[(size_t)s2]]);
+    std::vector<char> sreads((size_t)std::max<int64_t>(soff[(size_t)n], 1));
+    for (int64_t s2 = 0; s2 < n; ++s2) {
+        const int64_t r = order[(size_t)s2];
+        std::memcpy(sreads.data() + soff[(size_t)s2], reads + offsets[r], (size_t)(offsets[r + 1] - offsets[r]));
+    }
+    std::vector<nw::Stat> sst((size_t)std::max<int64_t>(n, 1));
+    std::vector<int64_t> sopo((size_t)n + 1);
+    std::vector<uint32_t> sops((size_t)std::max<int64_t>(ops_out ? std::max<int64_t>(ops_cap, 0) : 0, 1));
+    rc = ops_call(c, sreads.data(), soff.data(), n, ops_out ? sops.data() : nullptr, ops_out ? ops_cap : 0,
+                  sopo.data(), (nw_stat*)sst.data(), true, &grp);
+    c->ref.clear();
+    c->cur = Profile{};
+    if (rc && rc != NW_E_CAPACITY) return rc;
+    // caller order: records, run counts -> offsets, runs
+    std::vector<int64_t> cnt((size_t)n);
+    for (int64_t s2 = 0; s2 < n; ++s2) {
+        const int64_t r = order[(size_t)s2];
+        std::memcpy(&stats[r], &sst[(size_t)s2], sizeof(nw::Stat));
+        cnt[(size_t)r] = sopo[(size_t)s2 + 1] - sopo[(size_t)s2];
+    }
+    ops_off[0] = 0;
+    for (int64_t r = 0; r < n; ++r) ops_off[r + 1] = ops_off[r] + cnt[(size_t)r];
+    if (rc == NW_E_CAPACITY) return rc;
+    if (ops_out)
+        for (int64_t s2 = 0; s2 < n; ++s2) {
+            const int64_t r = order[(size_t)s2];
+            std::memcpy(ops_out + ops_off[r], sops.data() + sopo[(size_t)s2], sizeof(uint32_t) * (size_t)cnt[(size_t)r]);
+        }
+    return NW_OK;
 }
 
 int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes) {

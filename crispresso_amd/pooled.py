@@ -8,6 +8,11 @@ aligner at once: ``nw_align_multi`` uploads them grouped by amplicon, queues
 each group's kernels back to back on one stream and returns all alignments in
 the callers' order, so a 96-amplicon run is one host call instead of 96
 process start-ups, 96 FASTA round trips and 96 single-threaded aligners.
+
+With the ops output (the default, ``CRISPR_NW_OUTPUT``) the call is
+``nw_align_multi_ops``: every amplicon's tables uploaded once, the reads (already
+grouped by amplicon) pipelined over PCIe in chunks of one amplicon each, runs
+back; each amplicon's rows are rebuilt on the host (``nw_expand_ops``).
 """
 from __future__ import annotations
 
@@ -15,7 +20,7 @@ from typing import List, Sequence, Union
 
 import numpy as np
 
-from .aligner import AlignmentBatch, pack_reads
+from .aligner import AlignmentBatch, OpsBatch, default_output_mode, pack_reads
 
 Reads = Union[Sequence[str], tuple]
 
@@ -45,6 +50,17 @@ def align_pooled(amplicons: Sequence[str], reads_per_amplicon: Sequence[Reads], 
     buf = np.concatenate(bufs) if bufs else np.zeros(0, dtype=np.uint8)
     offsets = np.concatenate(offs)
     which = np.repeat(np.arange(len(amplicons), dtype=np.int32), counts)
+    if hasattr(aligner, "align_multi_ops") and default_output_mode() == "ops":
+        ob = aligner.align_multi_ops(list(amplicons), buf, offsets, which)
+        out, lo = [], 0
+        for g, k in enumerate(counts):
+            o0, o1 = int(ob.ops_off[lo]), int(ob.ops_off[lo + k])
+            sub = OpsBatch(ob.stats[lo:lo + k].copy(), ob.ops[o0:o1], ob.ops_off[lo:lo + k + 1] - o0,
+                           ob.read_lens[lo:lo + k], ob.scale, ob.awidth)
+            gbuf, goff = parts[g]
+            out.append(sub.expand(amplicons[g], np.asarray(gbuf, dtype=np.uint8), np.asarray(goff, dtype=np.int64)))
+            lo += k
+        return out
     whole = aligner.align_multi(list(amplicons), buf, offsets, which)
     out, lo = [], 0
     for g, k in enumerate(counts):

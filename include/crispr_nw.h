@@ -156,6 +156,14 @@ int nw_align_multi(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, in
                    const char* reads, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
                    char* aln_out, int64_t stride, nw_stat* stats);
 int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int32_t max_read_len);
+/* Pooled batch with ops output (nw_align_ops semantics; outputs in the caller's read
+ * order): every amplicon's tables uploaded once, chunks of one amplicon each pipelined
+ * through one set of streams.  Reads grouped by amplicon (ref_of_read non-decreasing)
+ * are used in place, others are grouped on the host first.  Leaves the context without
+ * a reference (nw_set_reference before nw_align_ops). */
+int nw_align_multi_ops(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
+                       const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out,
+                       int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
 
 /* Device time of the last nw_batch_run_async by phase of the band path (synchronises):
  * [0] classify + length sort, [1] nw_band_fill<16>, [2] nw_band_walk<16>, [3] the

@@ -152,3 +152,54 @@ def test_resident_second_pass_hdr(gpu_aligner_factory, oracle):
         assert np.array_equal(rec.stats[f], again.stats[f])
     with pytest.raises(NeedleError):
         a.align_ops(None, off[:101], resident=True)
+
+
+@pytest.mark.parametrize("grouped", [True, False])
+def test_multi_ops_96_amplicons(gpu_aligner_factory, oracle, grouped):
+    """nw_align_multi_ops on the C5 shape scaled down: 96 amplicons of 150-300 bp,
+    ~50 reads each (some empty groups, one group over a chunk boundary), grouped or
+    interleaved read order; every read bit-exact against the oracle with its amplicon."""
+    from crispresso_amd import synth as sy
+
+    amps = sy.pooled_amplicons(96, 5)
+    rng = np.random.Generator(np.random.PCG64(96))
+    bufs, offs, which = [], [], []
+    for g, amp in enumerate(amps):
+        k = 0 if g % 31 == 7 else (400 if g == 50 else int(rng.integers(20, 80)))
+        if k:
+            b, o = sy.reads_from(amp, k, 1000 + g, sy.PARITY_MIX)
+            bufs.append(b)
+            offs.append(o)
+            which += [g] * k
+    reads = []
+    for b, o in zip(bufs, offs):
+        reads += sy.unpack(b, o)
+    which = np.array(which, np.int32)
+    if not grouped:
+        perm = rng.permutation(len(reads))
+        reads = [reads[i] for i in perm]
+        which = which[perm]
+    buf, off = pack_reads(reads)
+    import os
+    os.environ["CRISPR_NW_CHUNK"] = "300"
+    try:
+        a = gpu_aligner_factory()
+        ob = a.align_multi_ops(amps, buf, off, which)
+    finally:
+        del os.environ["CRISPR_NW_CHUNK"]
+    assert a.reference is None
+    for g, amp in enumerate(amps):
+        sel = np.flatnonzero(which == g)
+        if not len(sel):
+            continue
+        gb, go = pack_reads([reads[i] for i in sel])
+        runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in sel]
+        goo = np.zeros(len(sel) + 1, np.int64)
+        goo[1:] = np.cumsum([len(r) for r in runs])
+        from crispresso_amd.aligner import OpsBatch
+        sub = OpsBatch(ob.stats[sel], np.concatenate(runs), goo, np.diff(go), ob.scale)
+        assert_same(oracle, amp, gb, go, sub.expand(amp, gb, go), f"multi g={g}")
+    amp = amps[3]
+    a.set_reference(amp)
+    b, o = sy.reads_from(amp, 300, 7, sy.PARITY_MIX)
+    assert_same(oracle, amp, b, o, a.align_packed(b, o), "after-multi-ops")
