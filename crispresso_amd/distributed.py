@@ -6,13 +6,19 @@ There is no collective on the data path.
   context per device (ctypes releases the GIL during the GPU calls).  This is
   what the CRISPResso host uses on an 8-GPU node: a single run aligns its reads
   on every GPU.
-* :func:`align_sharded` -- one process per GPU under torch.distributed
-  (``torchrun``; RCCL on GPUs, gloo on CPU): each rank aligns its shard, rank 0
-  gathers the records in read order.  Used when the host pipeline itself is
-  run per rank.
+* :func:`align_sharded` / :func:`align_pooled_sharded` -- one process per GPU
+  under torch.distributed (``torchrun``; the host-side process group is gloo:
+  the data never touches a collective, only the compact results are gathered):
+  each rank aligns its shard, rank 0 gathers the records and traceback runs
+  (about 45 B per read, not the rows) in read order.
 
-Both take an aligner factory so tests can run the sharding on CPU with the
-oracle-backed stand-in.
+Balance: single-amplicon batches split into equal read counts; pooled batches
+(C5: 96 amplicons of 150-300 bp) split by DP cells, ``len(amplicon) * len(read)``
+per read (:func:`cell_partition`), contiguous in the grouped read order so each
+device aligns whole amplicon groups plus at most two partial ones.
+
+All entry points take an aligner (or a factory) so tests can run the sharding on
+CPU with the oracle-backed stand-in.
 """
 from __future__ import annotations
 
@@ -21,7 +27,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .aligner import AlignmentBatch
+from .aligner import AlignmentBatch, OpsBatch
 
 
 def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -29,6 +35,30 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
     base, extra = divmod(n, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+def cell_partition(costs: np.ndarray, world: int) -> List[Tuple[int, int]]:
+    """Contiguous [lo, hi) ranges of the reads whose summed costs are as equal as a
+    contiguous split allows: boundaries where the running cost crosses k / world of the
+    total (each part is within one read's cost of the ideal share)."""
+    costs = np.asarray(costs, dtype=np.float64)
+    n = len(costs)
+    if n == 0 or world == 1:
+        return [shard_range(n, world, r) for r in range(world)]
+    cum = np.cumsum(costs)
+    total = cum[-1]
+    cuts = [0]
+    for k in range(1, world):
+        cuts.append(max(cuts[-1], int(np.searchsorted(cum, total * k / world, side="left")) + 1))
+    cuts.append(n)
+    cuts = [min(c, n) for c in cuts]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def pooled_costs(amplicons: Sequence[str], offsets: np.ndarray, amplicon_of_read: np.ndarray) -> np.ndarray:
+    """DP cells of every read of a pooled batch: len(its amplicon) x len(read)."""
+    amp_len = np.array([len(a) for a in amplicons], dtype=np.int64)
+    return amp_len[np.asarray(amplicon_of_read)] * np.diff(np.asarray(offsets, dtype=np.int64))
 
 
 def slice_batch(buf: np.ndarray, offsets: np.ndarray, lo: int, hi: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -46,6 +76,19 @@ def concat_batches(parts: Sequence[AlignmentBatch]) -> AlignmentBatch:
         r += len(p)
     return AlignmentBatch(np.concatenate([p.stats for p in parts]), aln,
                           np.concatenate([p.read_lens for p in parts]), parts[0].scale, parts[0].awidth)
+
+
+def concat_ops(parts: Sequence[OpsBatch]) -> OpsBatch:
+    """Shards' records and runs in read order (run offsets rebased)."""
+    parts = list(parts)
+    offs, base = [np.zeros(1, np.int64)], 0
+    for p in parts:
+        offs.append(p.ops_off[1:] - p.ops_off[0] + base)
+        base += int(p.ops_off[-1] - p.ops_off[0])
+    return OpsBatch(np.concatenate([p.stats for p in parts]),
+                    np.concatenate([p.ops for p in parts]) if parts else np.zeros(0, np.uint32),
+                    np.concatenate(offs), np.concatenate([p.read_lens for p in parts]),
+                    parts[0].scale, parts[0].awidth)
 
 
 class MultiGpuAligner:
@@ -68,15 +111,35 @@ class MultiGpuAligner:
             a.set_reference(seq)
         self.reference = seq
 
-    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True) -> AlignmentBatch:
-        n = len(offsets) - 1
+    def _shards(self, n: int, costs: Optional[np.ndarray] = None):
         world = len(self.aligners)
+        return cell_partition(costs, world) if costs is not None else [shard_range(n, world, r) for r in range(world)]
+
+    def align_packed(self, buf: np.ndarray, offsets: np.ndarray, strings: bool = True) -> AlignmentBatch:
         jobs = []
-        for rank, al in enumerate(self.aligners):
-            lo, hi = shard_range(n, world, rank)
+        for al, (lo, hi) in zip(self.aligners, self._shards(len(offsets) - 1)):
             b, o = slice_batch(buf, offsets, lo, hi)
             jobs.append(self._pool.submit(al.align_packed, b, o, strings))
         return concat_batches([j.result() for j in jobs])
+
+    def align_ops(self, buf: np.ndarray, offsets: np.ndarray) -> OpsBatch:
+        """Records + runs of every read (nw_align_ops per device, shards in parallel)."""
+        jobs = []
+        for al, (lo, hi) in zip(self.aligners, self._shards(len(offsets) - 1)):
+            b, o = slice_batch(buf, offsets, lo, hi)
+            jobs.append(self._pool.submit(al.align_ops, b, o))
+        return concat_ops([j.result() for j in jobs])
+
+    def align_multi_ops(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
+                        amplicon_of_read: np.ndarray) -> OpsBatch:
+        """Pooled batch over the devices, split by DP cells."""
+        which = np.asarray(amplicon_of_read, dtype=np.int32)
+        jobs = []
+        for al, (lo, hi) in zip(self.aligners, self._shards(len(offsets) - 1,
+                                                             pooled_costs(amplicons, offsets, which))):
+            b, o = slice_batch(buf, offsets, lo, hi)
+            jobs.append(self._pool.submit(al.align_multi_ops, list(amplicons), b, o, which[lo:hi]))
+        return concat_ops([j.result() for j in jobs])
 
     def close(self) -> None:
         for a in self.aligners:
@@ -84,13 +147,25 @@ class MultiGpuAligner:
         self._pool.shutdown()
 
 
+def _gather_ops(mine: OpsBatch, dist, rank: int, world: int) -> Optional[OpsBatch]:
+    """Rank 0 receives every rank's records + runs (compact payload) in rank order."""
+    payload = (mine.stats, mine.ops, mine.ops_off, mine.read_lens)
+    got: List = [None] * world if rank == 0 else None
+    dist.gather_object(payload, got, dst=0)
+    if rank != 0:
+        return None
+    return concat_ops([OpsBatch(s, o, f, l, mine.scale, mine.awidth) for s, o, f, l in got])
+
+
 def align_sharded(amplicon: str, buf: np.ndarray, offsets: np.ndarray, aligner, dist=None,
-                  gather: bool = True) -> Optional[AlignmentBatch]:
+                  gather: bool = True):
     """One rank's share of a torch.distributed alignment job.
 
     Every rank holds the same (buf, offsets) description of the job (or at
     least its own slice), aligns reads [lo, hi) with its local aligner and, if
-    `gather`, rank 0 receives all shards in read order (others get None).
+    `gather`, rank 0 receives all shards in read order (others get None): an
+    :class:`OpsBatch` (records + runs; ``.expand`` builds the rows) when the aligner
+    has the ops path, else an :class:`AlignmentBatch`.
     """
     world = dist.get_world_size() if dist is not None else 1
     rank = dist.get_rank() if dist is not None else 0
@@ -98,14 +173,31 @@ def align_sharded(amplicon: str, buf: np.ndarray, offsets: np.ndarray, aligner, 
     b, o = slice_batch(buf, offsets, lo, hi)
     if aligner.reference != amplicon:
         aligner.set_reference(amplicon)
-    mine = aligner.align_packed(b, o)
-    if dist is None or world == 1:
+    ops = hasattr(aligner, "align_ops")
+    mine = aligner.align_ops(b, o) if ops else aligner.align_packed(b, o)
+    if dist is None or world == 1 or not gather:
         return mine
-    if not gather:
-        return mine
+    if ops:
+        return _gather_ops(mine, dist, rank, world)
     payload = (mine.stats, mine.aln, mine.read_lens)
     got: List = [None] * world if rank == 0 else None
     dist.gather_object(payload, got, dst=0)
     if rank != 0:
         return None
     return concat_batches([AlignmentBatch(s, a, l, mine.scale, mine.awidth) for s, a, l in got])
+
+
+def align_pooled_sharded(amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
+                         amplicon_of_read: np.ndarray, aligner, dist=None, gather: bool = True) -> Optional[OpsBatch]:
+    """One rank's share of a pooled job (C5): reads split by DP cells
+    (:func:`cell_partition`), each rank aligns its range with one
+    ``align_multi_ops`` call, rank 0 gathers records + runs in read order."""
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
+    which = np.asarray(amplicon_of_read, dtype=np.int32)
+    lo, hi = cell_partition(pooled_costs(amplicons, offsets, which), world)[rank]
+    b, o = slice_batch(buf, offsets, lo, hi)
+    mine = aligner.align_multi_ops(list(amplicons), b, o, which[lo:hi])
+    if dist is None or world == 1 or not gather:
+        return mine
+    return _gather_ops(mine, dist, rank, world)

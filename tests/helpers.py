@@ -6,7 +6,7 @@ logic around the aligner; the GPU path itself is covered by the -m gpu tests.
 import numpy as np
 
 from crispresso_amd import _lib
-from crispresso_amd.aligner import AlignmentBatch, pack_reads
+from crispresso_amd.aligner import AlignmentBatch, OpsBatch, pack_reads
 from crispresso_amd.needle_options import NeedleOptions
 from oracle import oracle_py
 
@@ -26,6 +26,30 @@ def oracle_batch(amplicon, buf, offsets, awidth=5000, gap_open=10.0, gap_extend=
     return AlignmentBatch(stats, out, lens, p.scale, awidth)
 
 
+def runs_from_rows(ref_row: bytes, read_row: bytes):
+    """Runs of an alignment whose inputs hold no '-' (then '-' marks a gap)."""
+    out = []
+    for a, b in zip(ref_row, read_row):
+        t = _lib.NW_RUN_X if a == ord("-") else (_lib.NW_RUN_Y if b == ord("-") else _lib.NW_RUN_M)
+        if out and out[-1][0] == t:
+            out[-1][1] += 1
+        else:
+            out.append([t, 1])
+    return [(t << 28) | n for t, n in out]
+
+
+def ops_from_batch(batch: AlignmentBatch) -> OpsBatch:
+    """The ops form of a rows batch (inputs without '-')."""
+    ops, off = [], [0]
+    for i in range(len(batch)):
+        L = int(batch.stats["aln_len"][i])
+        if not batch.empty(i):
+            ops += runs_from_rows(batch.aln[i, 0, :L].tobytes(), batch.aln[i, 2, :L].tobytes())
+        off.append(len(ops))
+    return OpsBatch(batch.stats, np.array(ops, np.uint32), np.array(off, np.int64), batch.read_lens, batch.scale,
+                    batch.awidth)
+
+
 class OracleAligner:
     """Stand-in for GpuAligner (same methods the host code calls)."""
 
@@ -43,6 +67,12 @@ class OracleAligner:
 
     def align(self, reads):
         return self.align_packed(*pack_reads(reads))
+
+    def align_ops(self, buf, offsets):
+        return ops_from_batch(self.align_packed(buf, offsets))
+
+    def align_multi_ops(self, amplicons, buf, offsets, amplicon_of_read):
+        return ops_from_batch(self.align_multi(amplicons, buf, offsets, amplicon_of_read))
 
     def align_multi(self, amplicons, buf, offsets, amplicon_of_read):
         """Per-amplicon oracle runs, reassembled in read order (reference for nw_align_multi)."""

@@ -8,7 +8,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from crispresso_amd import synth
-from crispresso_amd.distributed import MultiGpuAligner, align_sharded, shard_range
+from crispresso_amd.distributed import (MultiGpuAligner, align_pooled_sharded, align_sharded, cell_partition,
+                                        pooled_costs, shard_range)
 
 
 def test_shard_ranges_cover_everything():
@@ -59,12 +60,35 @@ def _worker(rank, world, port, out_dir):
     buf, off = synth.reads_from(amp, 97, 6, synth.PARITY_MIX)
     res = align_sharded(amp, buf, off, OracleAligner(), dist)
     if rank == 0:
-        np.save(os.path.join(out_dir, "stats.npy"), res.stats)
-        np.save(os.path.join(out_dir, "aln.npy"), res.aln)
+        rows = res.expand(amp, buf, off, nthreads=1)   # rank 0 got records + runs, not rows
+        np.save(os.path.join(out_dir, "stats.npy"), rows.stats)
+        np.save(os.path.join(out_dir, "aln.npy"), rows.aln)
     else:
         assert res is None
+    # pooled: cell-count partition, records + runs gathered in read order
+    amps, pbuf, poff, which = _pooled()
+    pres = align_pooled_sharded(amps, pbuf, poff, which, OracleAligner(), dist)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "pstats.npy"), pres.stats)
+        np.save(os.path.join(out_dir, "pops.npy"), pres.ops)
+        np.save(os.path.join(out_dir, "poff.npy"), pres.ops_off)
+    else:
+        assert pres is None
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _pooled():
+    amps = synth.pooled_amplicons(5, 9)
+    parts = [synth.reads_from(a, 7 + 13 * g, 20 + g) for g, a in enumerate(amps)]
+    reads = []
+    for b, o in parts:
+        reads += synth.unpack(b, o)
+    which = np.repeat(np.arange(len(amps), dtype=np.int32), [len(o) - 1 for _, o in parts])
+    from crispresso_amd.aligner import pack_reads
+
+    buf, off = pack_reads(reads)
+    return amps, buf, off, which
 
 
 def test_gloo_world2_gathers_in_read_order(tmp_path):
@@ -82,3 +106,47 @@ def test_gloo_world2_gathers_in_read_order(tmp_path):
     for i in range(len(stats)):
         L = int(stats["aln_len"][i])
         assert np.array_equal(aln[i, :, :L], ref.aln[i, :, :L])
+    amps, pbuf, poff, which = _pooled()
+    want = OracleAligner().align_multi_ops(amps, pbuf, poff, which)
+    assert np.array_equal(np.load(tmp_path / "pstats.npy"), want.stats)
+    assert np.array_equal(np.load(tmp_path / "pops.npy"), want.ops)
+    assert np.array_equal(np.load(tmp_path / "poff.npy"), want.ops_off)
+
+
+def test_cell_partition_balances_pooled_work():
+    amps = synth.pooled_amplicons(96, 5)
+    rng = np.random.Generator(np.random.PCG64(1))
+    counts = rng.integers(0, 2000, 96)
+    which = np.repeat(np.arange(96, dtype=np.int32), counts)
+    lens = np.concatenate([rng.integers(len(a) - 30, len(a) + 10, c) for a, c in zip(amps, counts)])
+    off = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    costs = pooled_costs(amps, off, which)
+    for world in (1, 2, 3, 8):
+        parts = cell_partition(costs, world)
+        assert parts[0][0] == 0 and parts[-1][1] == len(costs)
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        share = costs.sum() / world
+        for lo, hi in parts:
+            assert abs(costs[lo:hi].sum() - share) <= costs.max() + 1   # within one read of the ideal share
+    assert cell_partition(np.zeros(0), 4) == [(0, 0)] * 4
+
+
+def test_multi_device_ops_and_pooled_equal_single():
+    from tests.helpers import OracleAligner
+
+    amp = synth.random_amplicon(150, 3)
+    buf, off = synth.reads_from(amp, 301, 4)
+    single = OracleAligner()
+    single.set_reference(amp)
+    ref = single.align_ops(buf, off)
+    multi = MultiGpuAligner([0, 1, 2], factory=lambda d, o: OracleAligner(d, o))
+    multi.set_reference(amp)
+    got = multi.align_ops(buf, off)
+    assert np.array_equal(got.stats, ref.stats) and np.array_equal(got.ops, ref.ops)
+    assert np.array_equal(got.ops_off, ref.ops_off)
+    amps, pbuf, poff, which = _pooled()
+    want = single.align_multi_ops(amps, pbuf, poff, which)
+    got = multi.align_multi_ops(amps, pbuf, poff, which)
+    assert np.array_equal(got.stats, want.stats) and np.array_equal(got.ops, want.ops)
+    multi.close()

@@ -203,3 +203,33 @@ def test_multi_ops_96_amplicons(gpu_aligner_factory, oracle, grouped):
     a.set_reference(amp)
     b, o = sy.reads_from(amp, 300, 7, sy.PARITY_MIX)
     assert_same(oracle, amp, b, o, a.align_packed(b, o), "after-multi-ops")
+
+
+def test_multi_gpu_aligner_threads_on_one_device(oracle):
+    """MultiGpuAligner with two contexts on device 0 (threads, shards in parallel):
+    single-amplicon and pooled (cell-count partition) results equal one context's."""
+    from crispresso_amd import synth as sy
+    from crispresso_amd.aligner import GpuAligner
+    from crispresso_amd.distributed import MultiGpuAligner
+
+    amp = sy.random_amplicon(250, 1)
+    buf, off = sy.reads_from(amp, 5001, 2, sy.PARITY_MIX)
+    multi = MultiGpuAligner([0, 0])
+    multi.set_reference(amp)
+    got = multi.align_ops(buf, off)
+    assert_same(oracle, amp, buf, off, got.expand(amp, buf, off), "multi-threads")
+    amps = sy.pooled_amplicons(12, 5)
+    parts = [sy.reads_from(a, 200, 30 + g) for g, a in enumerate(amps)]
+    reads = []
+    for b, o in parts:
+        reads += sy.unpack(b, o)
+    which = np.repeat(np.arange(12, dtype=np.int32), 200)
+    pbuf, poff = pack_reads(reads)
+    one = GpuAligner(0)
+    want = one.align_multi_ops(amps, pbuf, poff, which)
+    got = multi.align_multi_ops(amps, pbuf, poff, which)
+    for f in FIELDS:
+        assert np.array_equal(got.stats[f], want.stats[f])
+    assert np.array_equal(got.ops, want.ops) and np.array_equal(got.ops_off, want.ops_off)
+    one.close()
+    multi.close()
