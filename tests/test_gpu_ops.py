@@ -233,3 +233,35 @@ def test_multi_gpu_aligner_threads_on_one_device(oracle):
     assert np.array_equal(got.ops, want.ops) and np.array_equal(got.ops_off, want.ops_off)
     one.close()
     multi.close()
+
+
+@pytest.mark.parametrize("chunk", ["97", "100000"])
+def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk):
+    """nw_align_ops_packed: 2-bit bases + exceptions (N, IUPAC, U, '-', lower case) give
+    the same records and runs as the text path and the oracle; a batch whose offsets
+    start mid-buffer; chunk edges inside packed bytes; the resident second pass after it."""
+    from crispresso_amd.aligner import pack_2bit
+
+    monkeypatch.setenv("CRISPR_NW_CHUNK", chunk)
+    amp = synth.random_amplicon(250, 61)
+    reads = _reads(amp, 65)
+    reads += ["acgtNNNNtttgacca", "T-C-A", "ACGTRYKMSWBDHVNU", amp.lower()[:77] + "u" + amp[78:], "n" * 30]
+    full, foff = pack_reads(["PREFIX"] + reads)
+    off = foff[1:]                       # offsets start at 6: the batch is a slice of a bigger buffer
+    buf, off0 = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    pr = pack_2bit(full, off)
+    ob = a.align_ops_packed(pr)
+    assert a.ops_times()["h2d_bytes"] < (int(off[-1]) - int(off[0])) // 2
+    assert_same(oracle, amp, buf, off0, ob.expand(amp, full, off), f"packed chunk={chunk}")
+    text = a.align_ops(buf, off0)
+    for f in FIELDS + ("flags",):
+        assert np.array_equal(ob.stats[f], text.stats[f])
+    assert np.array_equal(ob.ops, text.ops) and np.array_equal(ob.ops_off, text.ops_off)
+    # resident pass after a packed upload
+    a.align_ops_packed(pr)
+    hdr = synth.hdr_amplicon(amp, 4)
+    a.set_reference(hdr)
+    again = a.align_ops(None, off, resident=True)
+    assert_same(oracle, hdr, buf, off0, again.expand(hdr, full, off), "packed-resident")
