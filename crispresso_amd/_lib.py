@@ -45,6 +45,7 @@ EXPORTS = (
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_ops_packed", "nw_pack_reads",
+    "nw_fastq_read", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -127,6 +128,12 @@ def load() -> ctypes.CDLL:
         "nw_batch_download_ops": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops_resident": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
+        "nw_fastq_read": (c_int, [c_char_p, POINTER(c_void_p)]),
+        "nw_fastq_count": (c_int64, [c_void_p]),
+        "nw_fastq_seqs": (c_void_p, [c_void_p]),
+        "nw_fastq_offsets": (c_void_p, [c_void_p]),
+        "nw_fastq_names": (c_void_p, [c_void_p, POINTER(c_int64)]),
+        "nw_fastq_free": (None, [c_void_p]),
         "nw_align_ops_packed": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
                                         c_int64, c_void_p, c_void_p]),
         "nw_pack_reads": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,

@@ -84,7 +84,7 @@ struct Scratch {
         d_opsctl.release(); d_blk.release();
     }
 };
-constexpr int kScratchSets = 2;
+constexpr int kScratchSets = 3;
 
 struct nw_ctx {
     int device = 0;
@@ -93,7 +93,7 @@ struct nw_ctx {
     Scratch sc[kScratchSets];
     Scratch* s = &sc[0];                               // the set launch_range / configure use
     hipStream_t cs = nullptr;                          // the stream launch_range queues on
-    hipStream_t stream2 = nullptr;                     // second compute stream (pipelined calls)
+    hipStream_t cstream[kScratchSets] = {};            // compute stream of each set ([0] = stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_fill = nullptr, ev_walk = nullptr;   // after the fill / walk kernels
     hipEvent_t ev_sort = nullptr, ev_l2 = nullptr;     // band path: after the sort, after the second level
@@ -522,7 +522,8 @@ int nw_create(int device, nw_ctx** out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->cstream[1], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->cstream[2], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&c->ev_h0) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -532,6 +533,7 @@ int nw_create(int device, nw_ctx** out) {
         return NW_E_HIP;
     }
     c->cs = c->stream;
+    c->cstream[0] = c->stream;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
@@ -552,7 +554,8 @@ void nw_destroy(nw_ctx* c) {
     for (Scratch& S : c->sc) S.release();
     c->d_ctl64.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (int k = 1; k < kScratchSets; ++k)
+        if (c->cstream[k]) (void)hipStreamSynchronize(c->cstream[k]);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out);
     for (auto* v : {&c->ev_in, &c->ev_cs, &c->ev_ce, &c->ev_out})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
@@ -560,7 +563,8 @@ void nw_destroy(nw_ctx* c) {
     if (c->ev_h0) (void)hipEventDestroy(c->ev_h0);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->s_in) (void)hipStreamDestroy(c->s_in);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (int k = 1; k < kScratchSets; ++k)
+        if (c->cstream[k]) (void)hipStreamDestroy(c->cstream[k]);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
     if (c->ev_sort) (void)hipEventDestroy(c->ev_sort);
@@ -1250,9 +1254,38 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     struct Chunk { int64_t lo, hi; int g; };
     std::vector<Chunk> chunks;
     const int ngroups = groups ? (int)groups->refs->size() : 1;
+    // sizes ramp up and down at both ends of the call (chunk / 4, chunk / 2, ...): the
+    // first chunk's upload and the last chunk's records are the pipeline's serial head
+    // and tail; every chunk in between is a full chunk
+    auto sizes = [&](int64_t len) {
+        std::vector<int64_t> v;
+        if (len <= chunk) {
+            v.push_back(len);
+            return v;
+        }
+        std::vector<int64_t> head, tail;
+        int64_t left = len;
+        for (int64_t part : {chunk / 4, chunk / 2}) {
+            if (part >= 1024 && left > 2 * (part + chunk)) {
+                head.push_back(part);
+                tail.push_back(part);
+                left -= 2 * part;
+            }
+        }
+        for (int64_t x : head) v.push_back(x);
+        const int64_t mid = (left + chunk - 1) / chunk;
+        for (int64_t q = 0; q < mid; ++q) v.push_back(left / mid + (q < left % mid ? 1 : 0));
+        for (auto it = tail.rbegin(); it != tail.rend(); ++it) v.push_back(*it);
+        return v;
+    };
     for (int g = 0; g < ngroups; ++g) {
         const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
-        for (int64_t lo = g0; lo < g1; lo += chunk) chunks.push_back({lo, std::min(g1, lo + chunk), g});
+        int64_t lo = g0;
+        for (int64_t len : sizes(g1 - g0)) {
+            if (len <= 0) continue;
+            chunks.push_back({lo, lo + len, g});
+            lo += len;
+        }
     }
     const int mode_before = c->out_mode;
     c->out_mode = NW_OUT_OPS;
@@ -1282,7 +1315,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     int rc = NW_OK;
     // configure every group once up front: the buffers reach their largest size before
     // anything is queued (no allocation inside the pipeline)
-    const int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? kScratchSets : 1;
+    int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? kScratchSets : 1;
+    if (const char* e = std::getenv("CRISPR_NW_SETS")) nsets = std::max(1, std::min(kScratchSets, std::atoi(e)));
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
         configured = -1;
@@ -1363,7 +1397,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
         } else if (cb + tot > ops_cap) cap_short = true;
         else if (tot > 0)
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[nsets > 1 ? (k & 1) : 0].d_staging.p, sizeof(uint32_t) * (size_t)tot,
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)tot,
                                           hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
         total = cb + tot;
@@ -1375,11 +1409,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
     HIP_OR_FAIL(c, hipEventRecord(c->ev_start, c->stream));
-    HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+    for (int k = 1; k < nsets; ++k) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cstream[k], c->ev_start, 0));
     for (int64_t k = 0; k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
-        c->s = &c->sc[nsets > 1 ? (k & 1) : 0];
-        c->cs = (nsets > 1 && (k & 1)) ? c->stream2 : c->stream;
+        c->s = &c->sc[k % nsets];
+        c->cs = c->cstream[k % nsets];
         if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)k], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
         if (pk && upload) {   // the chunk's bases -> bytes, then its exception bytes
@@ -1391,19 +1425,22 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         any_diag = any_diag || c->use_diag;
-        if ((rc = launch_range_ops(c, lo, k >= 2 ? c->ev_out[(size_t)(k - 2)] : nullptr,
+        if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr)))
             return restore(rc);
         HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
                                       hipMemcpyDeviceToHost, c->cs));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
+        // s_out order: chunk k - 1's runs (their size is known once k - 1 is done), then
+        // chunk k's records and offsets -- so the runs a later compaction waits for are
+        // never queued behind records that wait for a chunk still computing
+        if (k >= 1 && (rc = copy_runs(k - 1))) return restore(rc);
         HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
         HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
-        if (k >= 1 && (rc = copy_runs(k - 1))) return restore(rc);
     }
     if (nchunks > 0 && (rc = copy_runs(nchunks - 1))) return restore(rc);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import gzip
 import io
+import os
 import re
 from typing import List, Tuple
 
@@ -42,7 +43,36 @@ def fasta_name(header_line: bytes) -> str:
 
 
 def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
-    """-> (fasta names, packed sequences, offsets) in file order."""
+    """-> (fasta names, packed sequences, offsets) in file order.
+
+    Native ingest (``nw_fastq_read``, zlib + one C++ pass); the semantics are those
+    of :func:`fastq_bytes_as_fasta` below (the Python restatement the tests hold the
+    native reader to)."""
+    import ctypes
+
+    from . import _lib
+
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    if lib.nw_fastq_read(os.fsencode(path), ctypes.byref(h)) != _lib.NW_OK:
+        raise OSError(f"cannot read FASTQ {path}")
+    try:
+        n = int(lib.nw_fastq_count(h))
+        off = np.ctypeslib.as_array((ctypes.c_int64 * (n + 1)).from_address(lib.nw_fastq_offsets(h))).copy()
+        nb = int(off[-1])
+        seqs = (np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(lib.nw_fastq_seqs(h))).copy()
+                if nb else np.zeros(0, np.uint8))
+        nm = ctypes.c_int64()
+        p = lib.nw_fastq_names(h, ctypes.byref(nm))
+        text = ctypes.string_at(p, nm.value).decode("ascii", "replace") if nm.value else ""
+    finally:
+        lib.nw_fastq_free(h)
+    names = text.split("\n")[:-1] if n else []
+    return names, seqs, off
+
+
+def read_fastq_as_fasta_py(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
+    """The Python restatement (gzip + :func:`fastq_bytes_as_fasta`)."""
     with _open(path) as f:
         data = f.read()
     return fastq_bytes_as_fasta(data)

@@ -231,6 +231,18 @@ int nw_host_unregister(void* p);
 int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
                   const uint32_t* ops, const int64_t* ops_off, char* aln_out, int64_t stride, int32_t nthreads);
 
+/* FASTQ(.gz) ingest (CRISPRessoCORE.py:1791-1797: gunzip | awk | sed 's/:/_/g', then
+ * EMBOSS's FASTA reader): every record's name (first word of the header, ':' -> '_')
+ * and the sequence bytes EMBOSS keeps (letters and * . ~ ? # + -), packed with n + 1
+ * offsets.  The handle owns the buffers. */
+typedef struct nw_fastq nw_fastq;
+int nw_fastq_read(const char* path, nw_fastq** out);
+int64_t nw_fastq_count(const nw_fastq* q);
+const char* nw_fastq_seqs(const nw_fastq* q);
+const int64_t* nw_fastq_offsets(const nw_fastq* q);
+const char* nw_fastq_names(const nw_fastq* q, int64_t* bytes);   /* each name followed by '\n' */
+void nw_fastq_free(nw_fastq* q);
+
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated
  * read ids, concatenated.  Writes at most cap bytes; returns the number of
