@@ -1315,7 +1315,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     int rc = NW_OK;
     // configure every group once up front: the buffers reach their largest size before
     // anything is queued (no allocation inside the pipeline)
-    int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? kScratchSets : 1;
+    // two sets overlap a chunk's tail with the next chunk's bulk; a third measured slower
+    // (328M vs 306M reads/s at 262144-read chunks, scripts/gpu_sets_sweep.sh)
+    int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? 2 : 1;
     if (const char* e = std::getenv("CRISPR_NW_SETS")) nsets = std::max(1, std::min(kScratchSets, std::atoi(e)));
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
