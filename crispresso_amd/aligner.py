@@ -190,6 +190,8 @@ def default_output_mode() -> str:
 class GpuAligner:
     """One GPU context aligning reads to one amplicon at a time."""
 
+    ops_native = True   # align_ops runs on the device (host code may take the ops path)
+
     def __init__(self, device: int = 0, options: Optional[NeedleOptions] = None):
         self.lib = _lib.load()
         self.options = options or NeedleOptions()

@@ -87,6 +87,64 @@ bool expand_one(const Tables& T, const unsigned char* ref, int64_t La, const uin
 
 }  // namespace
 
+template <class F>
+void parallel_for(int64_t n, int32_t nthreads, const F& f) {
+    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
+    if (nt == 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const int64_t per = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t lo = t * per, hi = std::min(n, lo + per);
+        if (lo < hi) pool.emplace_back(f, lo, hi);
+    }
+    for (auto& th : pool) th.join();
+}
+
+extern "C" int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
+                                    const int64_t* idx, int64_t m, const uint32_t* ops, const int64_t* ops_off,
+                                    char* aln_out, int64_t stride, int32_t nthreads) {
+    if (m < 0 || ref_len <= 0 || !ref || (m > 0 && (!reads || !offsets || !idx || !ops_off || !aln_out)))
+        return NW_E_INVALID;
+    const Tables& T = tables();
+    std::vector<uint8_t> acode((size_t)ref_len);
+    for (int32_t i = 0; i < ref_len; ++i) acode[(size_t)i] = T.code[(unsigned char)ref[i]];
+    std::atomic<int> bad{0};
+    parallel_for(m, nthreads, [&](int64_t lo, int64_t hi) {
+        for (int64_t q = lo; q < hi; ++q) {
+            const int64_t r = idx[q];
+            const int64_t Lb = offsets[r + 1] - offsets[r];
+            const int64_t k0 = ops_off[r], k1 = ops_off[r + 1];
+            if (Lb == 0 && k1 == k0) continue;
+            if (k1 < k0 || !ops ||
+                !expand_one(T, (const unsigned char*)ref, ref_len, acode.data(), (const unsigned char*)reads + offsets[r],
+                            Lb, ops + k0, k1 - k0, aln_out + q * 3 * stride, stride))
+                bad.store(1, std::memory_order_relaxed);
+        }
+    });
+    return bad.load() ? NW_E_INVALID : NW_OK;
+}
+
+extern "C" int64_t nw_reads_equal_ref(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
+                                      int64_t n, uint8_t* equal, int32_t nthreads) {
+    if (n < 0 || !ref || (n > 0 && (!reads || !offsets || !equal))) return NW_E_INVALID;
+    std::atomic<int64_t> count{0};
+    parallel_for(n, nthreads, [&](int64_t lo, int64_t hi) {
+        int64_t c = 0;
+        for (int64_t r = lo; r < hi; ++r) {
+            const bool e = offsets[r + 1] - offsets[r] == ref_len &&
+                           std::memcmp(reads + offsets[r], ref, (size_t)ref_len) == 0;
+            equal[r] = (uint8_t)e;
+            c += e;
+        }
+        count += c;
+    });
+    return count.load();
+}
+
 extern "C" int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
                              const uint32_t* ops, const int64_t* ops_off, char* aln_out, int64_t stride,
                              int32_t nthreads) {

@@ -42,7 +42,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib, fastq
-from .aligner import AlignmentBatch, GpuAligner, NeedleError, format_srspair, printed_percent
+from .aligner import AlignmentBatch, GpuAligner, NeedleError, OpsBatch, format_srspair, printed_percent
 from .needle_options import DEFAULT_NEEDLE_OPTIONS, NeedleOptions, UnsupportedNeedleOption
 
 
@@ -199,6 +199,65 @@ def batch_to_dataframe(batch: AlignmentBatch, names: Sequence[str], name: str = 
                         ).set_index("ID")
 
 
+def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.ndarray, names: Sequence[str],
+                     name: str = "seq", just_score: bool = False, nthreads: int = 0) -> pd.DataFrame:
+    """batch_to_dataframe from the ops output: the same DataFrame, built without the
+    rows of reads that are byte-for-byte the amplicon (CRISPResso's unmodified reads,
+    most of a typical run): they share one ``ref_seq`` / ``align_str`` / ``align_seq``
+    string.  The other reads' rows are expanded on the host (nw_expand_ops) for them only."""
+    st = ob.stats
+    keep = np.flatnonzero((st["flags"] & _lib.NW_FLAG_EMPTY) == 0)
+    ids = _ids_of(names, keep)
+    ident = _printed_percents(st["n_ident"][keep], st["aln_len"][keep]).tolist()
+    if just_score:
+        return pd.DataFrame({"ID": ids, "score_" + name: ident}).set_index("ID")
+    lib = _lib.load()
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    ref = amplicon.encode("ascii")
+    La = len(ref)
+    # reads identical to the amplicon (unmodified, same case): one shared string per column
+    eq = np.zeros(len(offsets) - 1, np.uint8)
+    if La <= ob.awidth:
+        lib.nw_reads_equal_ref(ref, La, _lib.ptr(buf), _lib.ptr(offsets), len(eq), _lib.ptr(eq), nthreads)
+    same = eq[keep].astype(bool)
+    other = np.flatnonzero(~same)
+    ref_col = np.empty(len(keep), dtype=object)
+    str_col = np.empty(len(keep), dtype=object)
+    seq_col = np.empty(len(keep), dtype=object)
+    len_col = np.empty(len(keep), dtype=object)
+    if same.any():
+        ref_col[same] = amplicon
+        str_col[same] = "|" * La
+        seq_col[same] = amplicon
+        len_col[same] = _INT_STR[La] if La < len(_INT_STR) else str(La)
+    if len(other):
+        rd = np.ascontiguousarray(keep[other], dtype=np.int64)
+        cols = np.minimum(st["aln_len"][rd], ob.awidth).astype(np.int64)
+        stride = (La + int((offsets[rd + 1] - offsets[rd]).max()) + 15) & ~15
+        rows = np.zeros((len(rd), 3, stride), np.uint8)
+        ops = np.ascontiguousarray(ob.ops, dtype=np.uint32)
+        rc = lib.nw_expand_ops_subset(ref, La, _lib.ptr(buf), _lib.ptr(offsets), _lib.ptr(rd), len(rd),
+                                      _lib.ptr(ops) if len(ops) else None, _lib.ptr(ob.ops_off), _lib.ptr(rows),
+                                      stride, nthreads)
+        if rc != _lib.NW_OK:
+            raise NeedleException("Failed to build the alignment rows")
+        ends = np.empty(len(rd), dtype=np.int64)
+        w = max(int(cols.max()), 1)
+        pos = np.arange(w)[None, :]
+        for lo in range(0, len(rd), 65536):
+            blk = rows[lo:lo + 65536, 2, :w]
+            ends[lo:lo + 65536] = np.count_nonzero((blk != ord("-")) & (pos < cols[lo:lo + 65536, None]), axis=1)
+        ref_col[other] = _rows_to_str(rows[:, 0, :], cols)
+        str_col[other] = _rows_to_str(rows[:, 1, :], cols)
+        seq_col[other] = _rows_to_str(rows[:, 2, :], cols)
+        len_col[other] = [_INT_STR[e] if e < len(_INT_STR) else str(e) for e in ends.tolist()]
+    data = {"ID": ids, "score_" + name: ident, "length": len_col, "ref_seq": ref_col, "align_str": str_col,
+            "align_seq": seq_col}
+    return pd.DataFrame(data, columns=["ID", "score_" + name, "length", "ref_seq", "align_str", "align_seq"]
+                        ).set_index("ID")
+
+
 # ----------------------------------------------------------------- passes
 
 SRSPAIR_HEADER = (
@@ -212,9 +271,15 @@ SRSPAIR_TRAILER = "#---------------------------------------\n#------------------
 @dataclass
 class PassResult:
     names: List[str]
-    batch: AlignmentBatch
+    batch: Optional[AlignmentBatch]
+    ops: Optional[OpsBatch] = None          # the ops path: runs + the inputs to build rows from
+    amplicon: str = ""
+    buf: Optional[np.ndarray] = None
+    offsets: Optional[np.ndarray] = None
 
     def dataframe(self, name: str = "ref", just_score: bool = False) -> pd.DataFrame:
+        if self.ops is not None:
+            return ops_to_dataframe(self.ops, self.amplicon, self.buf, self.offsets, self.names, name, just_score)
         return batch_to_dataframe(self.batch, self.names, name, just_score)
 
 
@@ -228,13 +293,21 @@ def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: n
     ``just_score``: the caller reads only identities (the repair passes,
     CORE:1740-1741), so the alignment strings stay on the GPU unless a file is written.
     """
+    from .aligner import default_output_mode
+
+    use_ops = getattr(aligner, "ops_native", False) and default_output_mode() == "ops"
     try:
         if aligner.reference != amplicon:
             aligner.set_reference(amplicon)
-        batch = aligner.align_packed(buf, offsets, strings=not just_score or bool(outfile))
+        if use_ops:
+            ob = aligner.align_ops(buf, offsets, records_only=just_score and not outfile)
+            res = PassResult(list(names), None, ob, amplicon, buf, offsets)
+            batch = ob.expand(amplicon, buf, offsets) if outfile else None
+        else:
+            batch = aligner.align_packed(buf, offsets, strings=not just_score or bool(outfile))
+            res = PassResult(list(names), batch)
     except (NeedleError, UnsupportedNeedleOption) as exc:
         raise NeedleException("Needle failed to run, please check the log file.") from exc
-    res = PassResult(list(names), batch)
     if outfile:
         text = format_srspair(batch, amplicon_id, res.names, aligner.options)
         with gzip.open(outfile, "wt") as fh:

@@ -243,6 +243,16 @@ const int64_t* nw_fastq_offsets(const nw_fastq* q);
 const char* nw_fastq_names(const nw_fastq* q, int64_t* bytes);   /* each name followed by '\n' */
 void nw_fastq_free(nw_fastq* q);
 
+/* nw_expand_ops for the reads idx[0 .. m) only: read idx[q]'s rows at aln_out + q*3*stride. */
+int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
+                         const int64_t* idx, int64_t m, const uint32_t* ops, const int64_t* ops_off, char* aln_out,
+                         int64_t stride, int32_t nthreads);
+/* equal[r] = read r is byte for byte the amplicon (its three rows are the amplicon, a
+ * row of '|' and the amplicon: the DataFrame shares one string for them).  Returns the
+ * count. */
+int64_t nw_reads_equal_ref(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
+                           uint8_t* equal, int32_t nthreads);
+
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated
  * read ids, concatenated.  Writes at most cap bytes; returns the number of

@@ -2,13 +2,11 @@
 """Host-inclusive timings of the aligner path: what a CRISPResso
 run sees, as opposed to bench.py's device-resident `value`.
 
-Stages for N synthetic C2 reads (and the C3 HDR variant), one MI355X:
-  fastq      FASTQ text -> names + packed reads (crispresso_amd.fastq)
-  upload     nw_batch_upload (H2D of reads + offsets)
-  kernels    nw_batch_run_async + sync (device time, HIP events)
-  download   nw_batch_download (D2H of the three strings + records)
-  dataframe  batch_to_dataframe (the DataFrame parse_needle_output would give)
-  align_reads  CRISPRessoCORE.py:1788-2000 end to end (fastq .. filtered DataFrame)
+Stages for N synthetic C3 reads (85 % from the amplicon, 15 % from the HDR amplicon), one MI355X:
+  fastq_gz / fastq_gz_py  FASTQ.gz -> names + packed reads: native (nw_fastq_read) / Python restatement
+  align_ops     nw_align_ops: reads in, records + runs out (the call-level path)
+  dataframe_ops ops_to_dataframe (the DataFrame parse_needle_output would give)
+  align_reads   CRISPRessoCORE.py:1788-2000 end to end (FASTQ.gz .. filtered DataFrame), C2 and C3
 Usage: e2e_timing.py [n_reads] [out.json]
 """
 import json
@@ -24,12 +22,14 @@ sys.path.insert(0, ROOT)
 
 from crispresso_amd import fastq, synth  # noqa: E402
 from crispresso_amd.aligner import GpuAligner  # noqa: E402
-from crispresso_amd.needle import AlignArgs, align_reads, batch_to_dataframe  # noqa: E402
+from crispresso_amd.needle import AlignArgs, align_reads, ops_to_dataframe  # noqa: E402
 
 
 def write_fastq(path, buf, offsets):
+    import gzip
+
     n = len(offsets) - 1
-    with open(path, "wb") as f:
+    with gzip.open(path, "wb", compresslevel=1) as f:
         for lo in range(0, n, 100_000):
             hi = min(n, lo + 100_000)
             parts = []
@@ -51,28 +51,24 @@ def main():
     amp, hdr, buf, off = synth.c3_workload(n)
     res = {"n_reads": n, "amplicon_len": len(amp)}
     with tempfile.TemporaryDirectory() as td:
-        fq = os.path.join(td, "reads.fastq")
+        fq = os.path.join(td, "reads.fastq.gz")
         _, res["write_fastq_s"] = timed(write_fastq, fq, buf, off)
-        (names, b2, o2), res["fastq_s"] = timed(fastq.read_fastq_as_fasta, fq)
+        (names, b2, o2), res["fastq_gz_s"] = timed(fastq.read_fastq_as_fasta, fq)
+        _, res["fastq_gz_py_s"] = timed(fastq.read_fastq_as_fasta_py, fq)
         with GpuAligner(0) as al:
             al.set_reference(amp)
-            al.align_packed(b2[: o2[min(n, 1000)]], o2[: min(n, 1000) + 1])   # warm-up
-            _, res["upload_s"] = timed(al.upload, b2, o2)
-            al.run_async()
-            res["kernels_ms"] = al.sync()
-            maxlen = int(np.diff(o2).max())
-            batch, res["download_s"] = timed(al.download, n, maxlen)
-            _, res["dataframe_s"] = timed(batch_to_dataframe, batch, names, "ref")
-            _, res["align_packed_s"] = timed(al.align_packed, b2, o2)
-            _, res["align_packed_scores_only_s"] = timed(al.align_packed, b2, o2, False)
+            al.align_ops(b2[: o2[min(n, 1000)]], o2[: min(n, 1000) + 1])   # warm-up
+            ob, res["align_ops_s"] = timed(al.align_ops, b2, o2)
+            res["align_ops_pcie"] = al.ops_times()
+            _, res["dataframe_ops_s"] = timed(ops_to_dataframe, ob, amp, b2, o2, names, "ref")
             df, res["align_reads_c2_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp), fq, al)
             res["align_reads_c2_rows"] = int(len(df))
             df, res["align_reads_c3_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp,
                                                                        expected_hdr_amplicon_seq=hdr), fq, al)
             res["align_reads_c3_rows"] = int(len(df))
-    res["pcie_inclusive_reads_per_s"] = n / (res["upload_s"] + res["kernels_ms"] * 1e-3 + res["download_s"])
     res["align_reads_c2_reads_per_s"] = n / res["align_reads_c2_s"]
     res["align_reads_c3_reads_per_s"] = n / res["align_reads_c3_s"]
+    res["align_reads_c2_without_fastq_reads_per_s"] = n / (res["align_reads_c2_s"] - res["fastq_gz_s"])
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

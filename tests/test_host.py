@@ -124,3 +124,33 @@ def test_needle_cli_rejects_bad_options(capsys):
 
     assert main(["-asequence=a", "-bsequence=b", "-endweight"]) == 1
     assert "endweight" in capsys.readouterr().err
+
+
+def test_ops_to_dataframe_equals_rows_dataframe():
+    """The ops-path DataFrame (shared strings for reads identical to the amplicon,
+    rows expanded only for the others) equals batch_to_dataframe's, column by column."""
+    import numpy as np
+
+    from crispresso_amd import synth
+    from crispresso_amd.aligner import pack_reads
+    from crispresso_amd.needle import batch_to_dataframe, ops_to_dataframe
+    from tests.helpers import OracleAligner, ops_from_batch
+
+    amp = synth.random_amplicon(230, 8)
+    buf0, off0 = synth.reads_from(amp, 600, 9)
+    reads = synth.unpack(buf0, off0) + ["", amp.lower(), amp, amp[:-1], "NNNN"]
+    buf, off = pack_reads(reads)
+    names = [f"@r_{i}" for i in range(len(reads))]
+    al = OracleAligner()
+    al.set_reference(amp)
+    rows = al.align_packed(buf, off)
+    ob = ops_from_batch(rows)
+    want = batch_to_dataframe(rows, names, "ref")
+    got = ops_to_dataframe(ob, amp, buf, off, names, "ref")
+    assert list(got.columns) == list(want.columns) and list(got.index) == list(want.index)
+    for c in want.columns:
+        assert got[c].tolist() == want[c].tolist(), c
+    assert got["score_ref"].dtype == want["score_ref"].dtype
+    js = ops_to_dataframe(ob, amp, buf, off, names, "repaired", just_score=True)
+    assert js.equals(batch_to_dataframe(rows, names, "repaired", just_score=True))
+    assert int((np.asarray(got["ref_seq"].tolist(), dtype=object) == amp).sum()) >= 300
