@@ -1105,13 +1105,22 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
     if (!sreads.empty())
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, sreads.data(), sreads.size(), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, soff.data(), sizeof(int64_t) * soff.size(), hipMemcpyHostToDevice, c->stream));
-    // one group per amplicon: profile (ordered after the previous group's kernels), geometry, kernels
+    // every amplicon's tables uploaded once (one arena); then one kernel group per amplicon,
+    // queued back to back on the stream (configure() may grow buffers between groups)
+    std::vector<std::string> amps((size_t)n_refs);
+    for (int32_t g = 0; g < n_refs; ++g) amps[(size_t)g].assign(refs + ref_offsets[g], refs + ref_offsets[g + 1]);
+    std::vector<Profile> profs;
+    {
+        int rc = upload_shared(c);
+        if (!rc) rc = upload_profiles(c, amps, &profs);
+        if (rc) return rc;
+    }
     for (int32_t g = 0; g < n_refs; ++g) {
         const int64_t lo = first[(size_t)g], hi = first[(size_t)g + 1];
         if (hi == lo) continue;
-        c->ref.assign(refs + ref_offsets[g], refs + ref_offsets[g + 1]);
-        int rc = build_profile(c);
-        if (rc) return rc;
+        c->ref = amps[(size_t)g];
+        c->cur = profs[(size_t)g];
+        int rc = NW_OK;
         int32_t lb = 1;
         int64_t cells = 0;
         for (int64_t s = lo; s < hi; ++s) {
@@ -1147,6 +1156,8 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
     }
     c->n = 0;          // the per-batch getters describe nw_batch_upload batches only
     c->ran = false;
+    c->ref.clear();    // the arena holds every amplicon: nw_set_reference before single-amplicon calls
+    c->cur = Profile{};
     c->call_done = false;
     return NW_OK;
 }

@@ -32,13 +32,21 @@ class FlashError(RuntimeError):
 
 @dataclass
 class FlashOptions:
-    """FLASH's options as CRISPResso passes them (CORE:1655-1670)."""
-    min_overlap: int = 10
-    max_overlap: int = 65
+    """FLASH's options, defaulting to what CRISPResso passes (CORE:1655-1670 with the
+    argparse defaults CORE:4119-4138: ``--allow-outies --max-overlap 100 --min-overlap 4``;
+    FLASH's -x stays 0.25).  FLASH's own defaults (-m 10, -M 65, no outies) are
+    ``FlashOptions.flash_defaults()``."""
+    min_overlap: int = 4
+    max_overlap: int = 100
     max_mismatch_density: float = 0.25
-    allow_outies: bool = False
+    allow_outies: bool = True
     phred_offset: int = 33
     cap_mismatch_quals: bool = False
+
+    @staticmethod
+    def flash_defaults() -> "FlashOptions":
+        """FLASH 1.2.11 run without options: -m 10 -M 65 -x 0.25, innies only."""
+        return FlashOptions(min_overlap=10, max_overlap=65, allow_outies=False)
 
     @staticmethod
     def max_overlap_for(read_len: float, fragment_len: float, fragment_len_stddev: float) -> int:

@@ -150,8 +150,10 @@ int nw_batch_device_output(nw_ctx* ctx, void** d_aln, int64_t* stride, void** d_
  * CRISPRessoPooled.py:882-908): n_refs amplicons packed in `refs` with
  * ref_offsets[n_refs + 1]; read r is aligned against amplicon ref_of_read[r].
  * Outputs as nw_align_batch, in the callers' read order; `stride` at least
- * nw_required_stride_multi(ref_offsets, n_refs, longest read).  Synchronous.
- * Leaves the context without an uploaded batch (the nw_batch_* getters). */
+ * nw_required_stride_multi(ref_offsets, n_refs, longest read).  Synchronous: every
+ * amplicon's tables are uploaded once, each amplicon's kernels are queued back to back.
+ * Leaves the context without an uploaded batch (the nw_batch_* getters) and without a
+ * reference (nw_set_reference before single-amplicon calls). */
 int nw_align_multi(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
                    const char* reads, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
                    char* aln_out, int64_t stride, nw_stat* stats);
