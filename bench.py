@@ -338,13 +338,28 @@ def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
     ops_off = _lib.PinnedBuffer(n + 1, np.int64)
     ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     out = (stats.array, ops.array, ops_off.array)
+    from crispresso_amd.aligner import pack_2bit
+
     al = GpuAligner(device)
     for _ in range(warmup):
         al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
     t0 = time.perf_counter()
     for _ in range(steps):
         ob = al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
+    dt_text = (time.perf_counter() - t0) / steps
+    text_pcie = al.ops_times()
+    text_ops = (ob.ops_off.copy(), ob.ops.copy(), stats.array.copy())
+    # the same batch 2-bit packed (what the headline's call takes): nw_align_multi_ops_packed
+    p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
+    pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
+    for _ in range(warmup):
+        al.align_multi_ops(amps, pr, None, pw.array, out=out)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ob = al.align_multi_ops(amps, pr, None, pw.array, out=out)
     dt = (time.perf_counter() - t0) / steps
+    same = bool(np.array_equal(ob.ops_off, text_ops[0]) and np.array_equal(ob.ops, text_ops[1])
+                and np.array_equal(stats.array, text_ops[2]))
     lens = np.diff(off)
     amp_len = np.array([len(a) for a in amps])[which]
     res = {"metric": "pooled aligned reads/s (C5: 96 amplicons x reads, 150-300 bp, 1 GPU)", "value": n / dt,
@@ -352,10 +367,13 @@ def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
            "reads_per_amplicon": reads_per_amplicon, "mean_read_len": float(lens.mean()),
            "cells_full_matrices": int((amp_len * lens).sum()), "path_counts": al.path_counts(),
            "pcie": al.ops_times(), "runs_per_read": int(ob.ops_off[n]) / n,
+           "text_input": {"value": n / dt_text, "ms_per_step": dt_text * 1e3, "pcie": text_pcie,
+                          "same_output_as_packed": same},
            "algo_bytes_per_step": int(lens.sum() + 3 * stats.array["aln_len"].astype(np.int64).sum() + 16 * n),
-           "note": "step = one nw_align_multi_ops call: every amplicon's tables uploaded once, reads (grouped by "
-                   "amplicon, as demultiplexed) pipelined in chunks of one amplicon each"}
-    for b in (pb, po, pw, stats, ops_off, ops):
+           "note": "step = one nw_align_multi_ops_packed call (2-bit reads + exceptions in, pinned): every "
+                   "amplicon's tables uploaded once, reads (grouped by amplicon, as demultiplexed) pipelined in "
+                   "chunks of one amplicon each; text_input = nw_align_multi_ops on the text"}
+    for b in (pb, po, pw, stats, ops_off, ops, p_packed):
         b.close()
     al.close()
     return res

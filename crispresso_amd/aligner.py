@@ -429,11 +429,16 @@ class GpuAligner:
         buf, offsets = pack_reads(reads)
         return self.align_packed(buf, offsets)
 
-    def align_multi_ops(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
+    def align_multi_ops(self, amplicons: Sequence[str], buf, offsets: np.ndarray,
                         amplicon_of_read: np.ndarray, out: Optional[tuple] = None) -> OpsBatch:
         """Pooled batch, ops output (nw_align_multi_ops): read r against
         amplicons[amplicon_of_read[r]]; records and runs in read order.  Reads grouped
-        by amplicon are aligned in place.  Leaves no amplicon set on this aligner."""
+        by amplicon are aligned in place.  Leaves no amplicon set on this aligner.
+        ``buf`` a :class:`PackedReads` (offsets its own): nw_align_multi_ops_packed,
+        reads grouped by amplicon."""
+        packed = isinstance(buf, PackedReads)
+        if packed:
+            offsets = buf.offsets
         amps = [a.strip().upper() for a in amplicons]
         refs = "".join(amps).encode()
         roff = np.zeros(len(amps) + 1, dtype=np.int64)
@@ -451,6 +456,12 @@ class GpuAligner:
             stats, ops, ops_off = out
 
         def call(o):
+            if packed:
+                return self.lib.nw_align_multi_ops_packed(
+                    self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf.packed), _lib.ptr(offsets),
+                    _lib.ptr(idx), n, _lib.ptr(buf.exc_pos) if len(buf.exc_pos) else None,
+                    _lib.ptr(buf.exc_byte) if len(buf.exc_byte) else None, len(buf.exc_pos), _lib.ptr(o), len(o),
+                    _lib.ptr(ops_off), _lib.ptr(stats))
             return self.lib.nw_align_multi_ops(self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf),
                                                _lib.ptr(offsets), _lib.ptr(idx), n, _lib.ptr(o), len(o),
                                                _lib.ptr(ops_off), _lib.ptr(stats))
@@ -460,7 +471,7 @@ class GpuAligner:
             ops = np.empty(int(ops_off[n]), dtype=np.uint32)
             rc = call(ops)
         self.reference = None
-        self._check(rc, "nw_align_multi_ops")
+        self._check(rc, "nw_align_multi_ops_packed" if packed else "nw_align_multi_ops")
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
 
     def align_multi(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,

@@ -1518,12 +1518,16 @@ int nw_align_ops_resident(nw_ctx* c, const int64_t* offsets, int64_t n, uint32_t
 // amplicon (ref_of_read non-decreasing, as the demultiplexed per-amplicon read sets
 // arrive) are used in place; otherwise they are grouped on the host first and the
 // outputs put back in the caller's order.
-int nw_align_multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
-                       const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out, int64_t ops_cap,
-                       int64_t* ops_off, nw_stat* stats) {
+}  // extern "C"
+
+namespace {
+
+int multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
+              const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+              int64_t* ops_off, nw_stat* stats, const PackedInput* pk) {
     if (!c) return NW_E_INVALID;
     if (n_refs <= 0 || !refs || !ref_offsets) return fail(c, NW_E_INVALID, "no amplicons");
-    if (n < 0 || (n > 0 && (!reads || !offsets || !ref_of_read || !stats)) || !ops_off)
+    if (n < 0 || (n > 0 && (!(reads || pk) || !offsets || !ref_of_read || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
     std::vector<std::string> amps((size_t)n_refs);
     for (int32_t g = 0; g < n_refs; ++g) {
@@ -1549,11 +1553,12 @@ int nw_align_multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, 
     c->cur = Profile{};
     Groups grp{&amps, &profs, &first};
     if (grouped) {
-        rc = ops_call(c, reads, offsets, n, ops_out, ops_cap, ops_off, stats, true, &grp);
+        rc = ops_call(c, reads, offsets, n, ops_out, ops_cap, ops_off, stats, true, &grp, pk);
         c->ref.clear();
         c->cur = Profile{};
         return rc;
     }
+    if (pk) return fail(c, NW_E_INVALID, "packed pooled batches must be grouped by amplicon (ref_of_read ascending)");
     // group on the host (stable), align, then back to the caller's order
     std::vector<int64_t> order((size_t)n), fill(first.begin(), first.end() - 1);
     for (int64_t r = 0; r < n; ++r) order[(size_t)fill[(size_t)ref_of_read[r]]++] = r;
@@ -1589,6 +1594,28 @@ int nw_align_multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, 
             std::memcpy(ops_out + ops_off[r], sops.data() + sopo[(size_t)s2], sizeof(uint32_t) * (size_t)cnt[(size_t)r]);
         }
     return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_align_multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
+                       const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out, int64_t ops_cap,
+                       int64_t* ops_off, nw_stat* stats) {
+    return multi_ops(c, refs, ref_offsets, n_refs, reads, offsets, ref_of_read, n, ops_out, ops_cap, ops_off, stats,
+                     nullptr);
+}
+
+int nw_align_multi_ops_packed(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
+                              const uint8_t* packed, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
+                              const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out,
+                              int64_t ops_cap, int64_t* ops_off, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (n_exc < 0 || (n > 0 && !packed)) return fail(c, NW_E_INVALID, "bad packed batch");
+    const PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    return multi_ops(c, refs, ref_offsets, n_refs, nullptr, offsets, ref_of_read, n, ops_out, ops_cap, ops_off, stats,
+                     &pk);
 }
 
 int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes) {

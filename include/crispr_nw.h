@@ -166,6 +166,14 @@ int64_t nw_required_stride_multi(const int64_t* ref_offsets, int32_t n_refs, int
 int nw_align_multi_ops(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs, const char* reads,
                        const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out,
                        int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* nw_align_multi_ops with the reads 2-bit packed (nw_align_ops_packed's layout): the
+ * pooled C5 batch crosses PCIe at a quarter of the bytes.  Reads must be grouped by
+ * amplicon (ref_of_read non-decreasing; NW_E_INVALID otherwise -- a packed batch is
+ * not regrouped on the host). */
+int nw_align_multi_ops_packed(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
+                              const uint8_t* packed, const int64_t* offsets, const int32_t* ref_of_read, int64_t n,
+                              const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out,
+                              int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
 
 /* Device time of the last nw_batch_run_async by phase of the band path (synchronises):
  * [0] classify + length sort, [1] nw_band_fill<16>, [2] nw_band_walk<16>, [3] the

@@ -103,7 +103,7 @@ def test_gpu_merge_matches_golden(setting):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kw", [dict(min_overlap=4, max_overlap=100, allow_outies=True),
-                                dict(min_overlap=10, max_overlap=65),
+                                dict(min_overlap=10, max_overlap=65, allow_outies=False),
                                 dict(min_overlap=6, max_overlap=30, allow_outies=True, cap_mismatch_quals=True,
                                      max_mismatch_density=0.1)])
 def test_gpu_merge_matches_oracle_synthetic(kw):

@@ -185,6 +185,17 @@ def test_multi_ops_96_amplicons(gpu_aligner_factory, oracle, grouped):
     try:
         a = gpu_aligner_factory()
         ob = a.align_multi_ops(amps, buf, off, which)
+        # the same batch 2-bit packed (nw_align_multi_ops_packed): grouped reads only
+        from crispresso_amd.aligner import pack_2bit
+        pr = pack_2bit(buf, off)
+        if grouped:
+            pk = a.align_multi_ops(amps, pr, None, which)
+            for f in FIELDS + ("flags",):
+                assert np.array_equal(pk.stats[f], ob.stats[f])
+            assert np.array_equal(pk.ops, ob.ops) and np.array_equal(pk.ops_off, ob.ops_off)
+        else:
+            with pytest.raises(NeedleError):
+                a.align_multi_ops(amps, pr, None, which)
     finally:
         del os.environ["CRISPR_NW_CHUNK"]
     assert a.reference is None
