@@ -46,7 +46,7 @@ EXPORTS = (
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
-    "nw_expand_ops_subset", "nw_reads_equal_ref",
+    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -132,6 +132,8 @@ def load() -> ctypes.CDLL:
         "nw_fastq_read": (c_int, [c_char_p, POINTER(c_void_p)]),
         "nw_expand_ops_subset": (c_int, [c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_int32]),
+        "nw_ops_rows_concat": (c_int, [c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
         "nw_reads_equal_ref": (c_int64, [c_char_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int32]),
         "nw_fastq_count": (c_int64, [c_void_p]),
         "nw_fastq_seqs": (c_void_p, [c_void_p]),

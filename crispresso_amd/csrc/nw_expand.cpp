@@ -128,6 +128,68 @@ extern "C" int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char
     return bad.load() ? NW_E_INVALID : NW_OK;
 }
 
+// The rows of reads idx[0..m) concatenated column by column (read q's row in
+// [row_off[q], row_off[q + 1]) of each buffer: its first row_off[q + 1] - row_off[q]
+// columns, the `awidth` cut of parse_needle_output's first line), the non-'-' bytes of
+// its read row in that span (the "length" column, CORE:1750) and whether its amplicon
+// row is the amplicon itself (no read-side gap column: every such row can share one
+// string).  What ops_to_dataframe builds its string columns from in one pass.  A read
+// byte outside ASCII is an error (the columns are str; the FASTQ reader keeps letters).
+extern "C" int nw_ops_rows_concat(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
+                                  const int64_t* idx, int64_t m, const uint32_t* ops, const int64_t* ops_off,
+                                  const int64_t* row_off, char* ref_rows, char* markup_rows, char* read_rows,
+                                  int32_t* read_chars, uint8_t* ref_is_amplicon, int32_t nthreads) {
+    if (m < 0 || ref_len <= 0 || !ref ||
+        (m > 0 && (!reads || !offsets || !idx || !ops_off || !row_off || !ref_rows || !markup_rows || !read_rows ||
+                   !read_chars || !ref_is_amplicon)))
+        return NW_E_INVALID;
+    const Tables& T = tables();
+    std::vector<uint8_t> acode((size_t)ref_len);
+    for (int32_t i = 0; i < ref_len; ++i) acode[(size_t)i] = T.code[(unsigned char)ref[i]];
+    std::atomic<int> bad{0};
+    parallel_for(m, nthreads, [&](int64_t lo, int64_t hi) {
+        std::vector<char> tmp;
+        for (int64_t q = lo; q < hi; ++q) {
+            const int64_t r = idx[q];
+            const int64_t Lb = offsets[r + 1] - offsets[r];
+            const int64_t k0 = ops_off[r], k1 = ops_off[r + 1];
+            const int64_t cols = row_off[q + 1] - row_off[q];
+            int64_t aln = 0;
+            bool gap_in_ref = false;
+            for (int64_t k = k0; k < k1; ++k) {
+                aln += NW_RUN_LEN(ops[k]);
+                gap_in_ref |= NW_RUN_TYPE(ops[k]) == NW_RUN_X;
+            }
+            if (k1 < k0 || cols < 0 || cols > aln || (k1 > k0 && !ops)) {
+                bad.store(1, std::memory_order_relaxed);
+                continue;
+            }
+            if ((int64_t)tmp.size() < 3 * aln) tmp.resize((size_t)(3 * aln));
+            if (aln > 0 && !expand_one(T, (const unsigned char*)ref, ref_len, acode.data(),
+                                       (const unsigned char*)reads + offsets[r], Lb, ops + k0, k1 - k0, tmp.data(),
+                                       aln)) {
+                bad.store(1, std::memory_order_relaxed);
+                continue;
+            }
+            const int64_t o = row_off[q];
+            std::memcpy(ref_rows + o, tmp.data(), (size_t)cols);
+            std::memcpy(markup_rows + o, tmp.data() + aln, (size_t)cols);
+            const char* rr = tmp.data() + 2 * aln;
+            std::memcpy(read_rows + o, rr, (size_t)cols);
+            int32_t nc = 0;
+            unsigned char hi = 0;
+            for (int64_t k = 0; k < cols; ++k) {
+                nc += rr[k] != '-';
+                hi |= (unsigned char)rr[k];
+            }
+            if (hi & 0x80) bad.store(1, std::memory_order_relaxed);   // the columns are ASCII strings
+            read_chars[q] = nc;
+            ref_is_amplicon[q] = (uint8_t)(!gap_in_ref && cols == aln && aln == ref_len);
+        }
+    });
+    return bad.load() ? NW_E_INVALID : NW_OK;
+}
+
 extern "C" int64_t nw_reads_equal_ref(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
                                       int64_t n, uint8_t* equal, int32_t nthreads) {
     if (n < 0 || !ref || (n > 0 && (!reads || !offsets || !equal))) return NW_E_INVALID;

@@ -42,6 +42,18 @@ def fasta_name(header_line: bytes) -> str:
     return tok[0].decode("ascii", "replace") if tok else ""
 
 
+class NameList(list):
+    """The record names (a list of str) plus ``raw``: the same names as one uint8
+    block, each followed by '\\n' -- what the native reader produced, kept so the
+    DataFrame's ID column is built from it in bulk (needle._ids_of)."""
+
+    raw: np.ndarray
+
+    def __init__(self, names, raw: np.ndarray):
+        super().__init__(names)
+        self.raw = raw
+
+
 def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
     """-> (fasta names, packed sequences, offsets) in file order.
 
@@ -64,11 +76,13 @@ def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
                 if nb else np.zeros(0, np.uint8))
         nm = ctypes.c_int64()
         p = lib.nw_fastq_names(h, ctypes.byref(nm))
-        text = ctypes.string_at(p, nm.value).decode("ascii", "replace") if nm.value else ""
+        raw = (np.ctypeslib.as_array((ctypes.c_uint8 * nm.value).from_address(p)).copy() if nm.value
+               else np.zeros(0, np.uint8))
     finally:
         lib.nw_fastq_free(h)
+    text = raw.tobytes().decode("ascii", "replace") if len(raw) else ""
     names = text.split("\n")[:-1] if n else []
-    return names, seqs, off
+    return NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), seqs, off
 
 
 def read_fastq_as_fasta_py(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:

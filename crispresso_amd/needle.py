@@ -119,33 +119,76 @@ def _is_gzip(path: str) -> bool:
         return f.read(2) == b"\x1f\x8b"
 
 
-def _ids_of(names: Sequence[str], keep: np.ndarray) -> List[str]:
-    """``line.split()[-1].replace("_", ":")`` of each kept name (CORE:1725), in bulk."""
+def _ids_of(names: Sequence[str], keep: np.ndarray) -> np.ndarray:
+    """``line.split()[-1].replace("_", ":")`` of each kept name (CORE:1725), in bulk,
+    as an object array.  Names read natively (:class:`fastq.NameList`) are converted
+    from their byte block without a per-name Python step."""
+    raw = getattr(names, "raw", None)
+    if raw is not None and len(raw) and not _WS_BYTES[raw].any():
+        nl = np.flatnonzero(raw == 10)
+        if len(nl) == len(names):
+            ids = np.where(raw == ord("_"), np.uint8(ord(":")), raw)[raw != 10]
+            off = np.zeros(len(nl) + 1, np.int64)
+            off[1:] = nl - np.arange(len(nl))
+            allids = _strings(ids, off, ascii_checked=True)
+            return allids if len(keep) == len(names) else allids[keep]
     sel = [names[i] for i in keep] if len(keep) != len(names) else list(names)
     joined = "\n".join(sel)
     if joined.count("\n") == max(len(sel) - 1, 0) and not _WS.search(joined):
-        return joined.replace("_", ":").split("\n") if sel else []
-    return [nm.split()[-1].replace("_", ":") if nm.split() else "" for nm in sel]
+        out = joined.replace("_", ":").split("\n") if sel else []
+    else:
+        out = [nm.split()[-1].replace("_", ":") if nm.split() else "" for nm in sel]
+    arr = np.empty(len(out), dtype=object)
+    arr[:] = out
+    return arr
 
 
 _WS = __import__("re").compile(r"[ \t\r\f\v\x0b\x1c-\x1f\x85\xa0]")
+_WS_BYTES = np.zeros(256, dtype=bool)
+for _b in b" \t\r\f\v\x0b\x1c\x1d\x1e\x1f\x85\xa0":
+    _WS_BYTES[_b] = True
 
 
-def _rows_to_str(mat: np.ndarray, lens: np.ndarray) -> List[str]:
-    """Row i's first lens[i] bytes as str, for every row: one decode of the whole
-    block, then one slice per row."""
+def _strings(data: np.ndarray, off: np.ndarray, take: Optional[np.ndarray] = None,
+             ascii_checked: bool = False) -> np.ndarray:
+    """Object array of the ASCII strings data[off[i]:off[i + 1]] (only those i in
+    ``take`` when given): built by pyarrow in one native pass when it is importable,
+    else one decode + a slice per string."""
+    n = len(off) - 1
+    if n <= 0 or (take is not None and len(take) == 0):
+        return np.empty(0, dtype=object)
+    if not ascii_checked and len(data) and int(data.max()) >= 128:
+        raise NeedleException("alignment row is not ASCII")
+    try:
+        import pyarrow as pa
+    except ImportError:   # pragma: no cover - pyarrow is in the image
+        pa = None
+    if pa is not None:
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        o = np.ascontiguousarray(off - off[0], dtype=np.int64)
+        arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(o), pa.py_buffer(d[int(off[0]):int(off[-1])]))
+        if take is not None:
+            arr = arr.take(pa.array(np.asarray(take, dtype=np.int64)))
+        return arr.to_numpy(zero_copy_only=False)
+    big = np.ascontiguousarray(data).tobytes().decode("ascii")
+    idx = range(n) if take is None else np.asarray(take).tolist()
+    offl = off.tolist()
+    out = np.empty(len(idx), dtype=object)
+    out[:] = [big[offl[i]:offl[i + 1]] for i in idx]
+    return out
+
+
+def _rows_to_str(mat: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """Row i's first lens[i] bytes as str, for every row (object array): the rows'
+    bytes gathered contiguous by one mask, then :func:`_strings`."""
     n = mat.shape[0]
     if n == 0:
-        return []
+        return np.empty(0, dtype=object)
     w = max(int(lens.max()), 1)
-    big = np.ascontiguousarray(mat[:, :w]).tobytes().decode("latin-1")
-    starts = np.arange(n, dtype=np.int64) * w
-    out = [big[a:b] for a, b in zip(starts.tolist(), (starts + lens).tolist())]
-    if not big.isascii():   # bytes past a row's end may be anything; the rows themselves must be ASCII
-        for i, r in enumerate(out):
-            if not r.isascii():
-                raise UnicodeDecodeError("ascii", r.encode("latin-1"), 0, len(r), "alignment row is not ASCII")
-    return out
+    data = mat[:, :w][np.arange(w)[None, :] < lens[:, None]]
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    return _strings(data, off)
 
 
 def _printed_percents(num: np.ndarray, den: np.ndarray) -> np.ndarray:
@@ -204,13 +247,16 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
     """batch_to_dataframe from the ops output: the same DataFrame, built without the
     rows of reads that are byte-for-byte the amplicon (CRISPResso's unmodified reads,
     most of a typical run): they share one ``ref_seq`` / ``align_str`` / ``align_seq``
-    string.  The other reads' rows are expanded on the host (nw_expand_ops) for them only."""
+    string, as do the ``ref_seq`` of every read whose amplicon row has no gap.  The other
+    rows come from nw_ops_rows_concat (runs -> rows cut to ``awidth``, one C++ pass) and
+    become strings in bulk (:func:`_strings`)."""
     st = ob.stats
     keep = np.flatnonzero((st["flags"] & _lib.NW_FLAG_EMPTY) == 0)
     ids = _ids_of(names, keep)
-    ident = _printed_percents(st["n_ident"][keep], st["aln_len"][keep]).tolist()
+    ident = _printed_percents(st["n_ident"][keep], st["aln_len"][keep])
+    index = pd.Index(ids, dtype=object, name="ID")
     if just_score:
-        return pd.DataFrame({"ID": ids, "score_" + name: ident}).set_index("ID")
+        return pd.DataFrame({"score_" + name: ident}, index=index)
     lib = _lib.load()
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -225,37 +271,54 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
     ref_col = np.empty(len(keep), dtype=object)
     str_col = np.empty(len(keep), dtype=object)
     seq_col = np.empty(len(keep), dtype=object)
-    len_col = np.empty(len(keep), dtype=object)
+    ends = np.full(len(keep), La, dtype=np.int64)
     if same.any():
         ref_col[same] = amplicon
         str_col[same] = "|" * La
         seq_col[same] = amplicon
-        len_col[same] = _INT_STR[La] if La < len(_INT_STR) else str(La)
     if len(other):
         rd = np.ascontiguousarray(keep[other], dtype=np.int64)
         cols = np.minimum(st["aln_len"][rd], ob.awidth).astype(np.int64)
-        stride = (La + int((offsets[rd + 1] - offsets[rd]).max()) + 15) & ~15
-        rows = np.zeros((len(rd), 3, stride), np.uint8)
+        row_off = np.zeros(len(rd) + 1, np.int64)
+        np.cumsum(cols, out=row_off[1:])
+        tot = int(row_off[-1])
+        r0, r1, r2 = (np.empty(max(tot, 1), np.uint8) for _ in range(3))
+        nchar = np.empty(len(rd), np.int32)
+        is_amp = np.empty(len(rd), np.uint8)
         ops = np.ascontiguousarray(ob.ops, dtype=np.uint32)
-        rc = lib.nw_expand_ops_subset(ref, La, _lib.ptr(buf), _lib.ptr(offsets), _lib.ptr(rd), len(rd),
-                                      _lib.ptr(ops) if len(ops) else None, _lib.ptr(ob.ops_off), _lib.ptr(rows),
-                                      stride, nthreads)
+        rc = lib.nw_ops_rows_concat(ref, La, _lib.ptr(buf), _lib.ptr(offsets), _lib.ptr(rd), len(rd),
+                                    _lib.ptr(ops) if len(ops) else None, _lib.ptr(ob.ops_off), _lib.ptr(row_off),
+                                    _lib.ptr(r0), _lib.ptr(r1), _lib.ptr(r2), _lib.ptr(nchar), _lib.ptr(is_amp),
+                                    nthreads)
         if rc != _lib.NW_OK:
-            raise NeedleException("Failed to build the alignment rows")
-        ends = np.empty(len(rd), dtype=np.int64)
-        w = max(int(cols.max()), 1)
-        pos = np.arange(w)[None, :]
-        for lo in range(0, len(rd), 65536):
-            blk = rows[lo:lo + 65536, 2, :w]
-            ends[lo:lo + 65536] = np.count_nonzero((blk != ord("-")) & (pos < cols[lo:lo + 65536, None]), axis=1)
-        ref_col[other] = _rows_to_str(rows[:, 0, :], cols)
-        str_col[other] = _rows_to_str(rows[:, 1, :], cols)
-        seq_col[other] = _rows_to_str(rows[:, 2, :], cols)
-        len_col[other] = [_INT_STR[e] if e < len(_INT_STR) else str(e) for e in ends.tolist()]
-    data = {"ID": ids, "score_" + name: ident, "length": len_col, "ref_seq": ref_col, "align_str": str_col,
+            raise NeedleException("Failed to build the alignment rows (runs inconsistent with the reads, "
+                                  "or a byte outside ASCII in a read)")
+        amp_row = is_amp.astype(bool)
+        refs = np.empty(len(rd), dtype=object)
+        refs[amp_row] = amplicon
+        if not amp_row.all():   # the gapped amplicon rows
+            sub = np.flatnonzero(~amp_row)
+            refs[sub] = _strings(r0, row_off, take=sub, ascii_checked=True)
+        ref_col[other] = refs
+        str_col[other] = _strings(r1, row_off, ascii_checked=True)
+        seq_col[other] = _strings(r2, row_off, ascii_checked=True)
+        ends[other] = nchar
+    len_col = _int_strings(ends)
+    data = {"score_" + name: ident, "length": len_col, "ref_seq": ref_col, "align_str": str_col,
             "align_seq": seq_col}
-    return pd.DataFrame(data, columns=["ID", "score_" + name, "length", "ref_seq", "align_str", "align_seq"]
-                        ).set_index("ID")
+    return pd.DataFrame(data, index=index, columns=["score_" + name, "length", "ref_seq", "align_str", "align_seq"])
+
+
+_INT_OBJ = np.array(_INT_STR, dtype=object)
+
+
+def _int_strings(v: np.ndarray) -> np.ndarray:
+    """str(v[i]) for every i as an object array (one shared string per value < 4096)."""
+    if len(v) and int(v.max()) < len(_INT_OBJ) and int(v.min()) >= 0:
+        return _INT_OBJ[v]
+    out = np.empty(len(v), dtype=object)
+    out[:] = [str(e) for e in v.tolist()]
+    return out
 
 
 # ----------------------------------------------------------------- passes
@@ -301,11 +364,11 @@ def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: n
             aligner.set_reference(amplicon)
         if use_ops:
             ob = aligner.align_ops(buf, offsets, records_only=just_score and not outfile)
-            res = PassResult(list(names), None, ob, amplicon, buf, offsets)
+            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
             batch = ob.expand(amplicon, buf, offsets) if outfile else None
         else:
             batch = aligner.align_packed(buf, offsets, strings=not just_score or bool(outfile))
-            res = PassResult(list(names), batch)
+            res = PassResult(names if isinstance(names, list) else list(names), batch)
     except (NeedleError, UnsupportedNeedleOption) as exc:
         raise NeedleException("Needle failed to run, please check the log file.") from exc
     if outfile:

@@ -257,6 +257,15 @@ void nw_fastq_free(nw_fastq* q);
 int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
                          const int64_t* idx, int64_t m, const uint32_t* ops, const int64_t* ops_off, char* aln_out,
                          int64_t stride, int32_t nthreads);
+/* The rows of reads idx[0 .. m) from the runs, concatenated: read q's first
+ * row_off[q + 1] - row_off[q] columns (<= its alignment length; the awidth cut) at
+ * [row_off[q], row_off[q + 1]) of ref_rows / markup_rows / read_rows; read_chars[q] =
+ * non-'-' bytes of that read-row span; ref_is_amplicon[q] = 1 when the amplicon row is
+ * the amplicon itself (no gap in it, not cut).  The DataFrame hand-off's one pass. */
+int nw_ops_rows_concat(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, const int64_t* idx,
+                       int64_t m, const uint32_t* ops, const int64_t* ops_off, const int64_t* row_off, char* ref_rows,
+                       char* markup_rows, char* read_rows, int32_t* read_chars, uint8_t* ref_is_amplicon,
+                       int32_t nthreads);
 /* equal[r] = read r is byte for byte the amplicon (its three rows are the amplicon, a
  * row of '|' and the amplicon: the DataFrame shares one string for them).  Returns the
  * count. */

@@ -154,3 +154,16 @@ def test_ops_to_dataframe_equals_rows_dataframe():
     js = ops_to_dataframe(ob, amp, buf, off, names, "repaired", just_score=True)
     assert js.equals(batch_to_dataframe(rows, names, "repaired", just_score=True))
     assert int((np.asarray(got["ref_seq"].tolist(), dtype=object) == amp).sum()) >= 300
+    # names as the native FASTQ reader returns them (IDs built from the byte block), and
+    # rows cut at a narrow -awidth3: still the same frame, dtypes included
+    import pandas as pd
+
+    from crispresso_amd.fastq import NameList
+    raw = np.frombuffer(("\n".join(names) + "\n").encode(), np.uint8).copy()
+    for awidth in (5000, 100):
+        rows.awidth = awidth
+        ob.awidth = awidth
+        want = batch_to_dataframe(rows, names, "ref")
+        got = ops_to_dataframe(ob, amp, buf, off, NameList(names, raw), "ref")
+        pd.testing.assert_frame_equal(got, want)
+        assert got.index.tolist()[:2] == ["@r:0", "@r:1"]
