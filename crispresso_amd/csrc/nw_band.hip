@@ -1033,6 +1033,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         fb_n = 0;
     };
     auto give_up = [&](long long k, long long rd, bool retry) {
+        if (a.band_last) retry = false;
         if (W < kBandDiags && retry && a.redo_flags) {
             // the next level's list keeps the sorted order (nw_band_redo_* compaction):
             // its pairs are reads of similar length, as on this level

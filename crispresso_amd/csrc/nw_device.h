@@ -42,6 +42,8 @@ struct KernelArgs {
     // work list (full-storage kernel re-running the fallbacks); null = all reads
     const int64_t* work_list;
     const int32_t* work_count;
+    int32_t work_lo;           // first work-list entry this kernel takes (the one-wave kernel after the
+                               // multi-wave one: entries [0, exact grid) are the multi-wave kernel's)
     int32_t* work_counter;     // dynamic chunk queue of the pair/stream kernels (zeroed per run)
     // streaming kernels: per-pair traceback regions in HBM (StreamRegion layout)
     uint8_t* region;
@@ -71,6 +73,7 @@ struct KernelArgs {
     int32_t* redo_count;
     uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
     int32_t* redo_blk;             // [ceil(n / 1024)] compaction scratch
+    int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
     // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
     // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
@@ -81,6 +84,9 @@ struct KernelArgs {
     uint32_t* spill;
     int64_t spill_cap;             // words
     int32_t* ops_ctl;              // [0] spill words used, [1] error flag (spill area full)
+    // exact multi-wave kernel (nw_exact.hip): [17 amplicon codes][4] dwords, the scaled
+    // EDNAFULL scores against read codes 0..15 as int8 (byte j of dword q: code 4q + j)
+    const uint32_t* sub16;
 };
 
 // Traceback storage of a kernel instantiation.
@@ -140,6 +146,18 @@ hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int
 // the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
 // nmax >= the number of sorted positions (grid size)
 hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s);
+
+// exact int32 kernel for work lists (nw_exact.hip): one workgroup of exact_waves(La)
+// wavefronts per read; traceback slots in LDS (tb_lds) or a per-block HBM slab of
+// exact_slab_bytes at a.tb_global.  La <= 8192.
+int exact_rows_per_lane(int La);
+int exact_waves(int La);
+int exact_lds_bytes(int La, int Lb_max, bool tb_lds);
+int64_t exact_slab_bytes(int La, int Lb_max);
+// cap: take work-list entries [0, min(count, grid)) only (the one-wave kernel the rest);
+// a null work list = every read of the batch.
+hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_lds, int64_t slab_bytes, bool cap,
+                        hipStream_t s);
 
 // ops compaction (nw_ops.hip): per-read slots -> one contiguous run array.
 // ctl (int64, kOpsCtl): [0] running base over the chunks of a call (in/out), [1] this chunk's

@@ -23,7 +23,8 @@
 
 namespace {
 
-constexpr int kMaxRef = 1024;
+constexpr int kMaxRef = 8192;       // the exact multi-wave kernel (nw_exact.hip)
+constexpr int kMaxRefWave = 1024;   // the band, stream and one-wave kernels
 constexpr int kMaxLds = 160 * 1024;
 
 template <class T>
@@ -134,6 +135,12 @@ struct nw_ctx {
     nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
     DevBuf<uint32_t> d_btab;
+    DevBuf<uint32_t> d_sub16;         // exact multi-wave kernel's score rows
+    // exact multi-wave kernel on work lists (0 grid: the one-wave kernel, cfg)
+    int exact_grid = 0, exact_lds = 0;
+    bool exact_tb_lds = true;
+    bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
+    int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
     bool ran = false;
@@ -192,9 +199,25 @@ struct AmpTables {
 
 bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
     const int La = (int)ref.size();
-    const int R = nw::rows_per_lane_for(La);
-    if (R < 0) return false;
+    if (La > kMaxRef) return false;
+    // markup bits and the band alphabet test first: an amplicon longer than the
+    // one-wave kernels take (R = 0) has only these (the multi-wave kernel aligns it)
+    const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+    t->rowpos.resize((size_t)La);
+    t->amp_in_table = true;
+    for (int ai = 0; ai < La; ++ai) {
+        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
+        uint32_t m = 0;
+        for (int code = 0; code < nw::NCODE; ++code)
+            if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
+        t->rowpos[(size_t)ai] = m;
+        bool in6 = false;
+        for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
+        t->amp_in_table = t->amp_in_table && in6;
+    }
+    const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
+    if (R <= 0) return true;
     const int RP = nw::profile_rp(R);
     t->prof.assign((size_t)nw::NCODE * 64 * RP, 0);
     for (int ai = 0; ai < La; ++ai) {
@@ -241,20 +264,6 @@ bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
         const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
         t->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
     }
-    // per amplicon row the codes it scores > 0 against (markup ':')
-    const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
-    t->rowpos.resize((size_t)La);
-    t->amp_in_table = true;
-    for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
-        uint32_t m = 0;
-        for (int code = 0; code < nw::NCODE; ++code)
-            if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
-        t->rowpos[(size_t)ai] = m;
-        bool in6 = false;
-        for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
-        t->amp_in_table = t->amp_in_table && in6;
-    }
     return true;
 }
 
@@ -285,6 +294,13 @@ int upload_shared(nw_ctx* c) {
                 const uint16_t sb = (uint16_t)(int16_t)(sub6(x, yb) + 2 * c->gap_extend);
                 btab[(size_t)x * 36 + ya * 6 + yb] = sa | ((uint32_t)sb << 16);
             }
+    std::vector<uint32_t> sub16((size_t)nw::NCODE * 4, 0u);
+    for (int ca = 0; ca < 16; ++ca)
+        for (int code = 0; code < 16; ++code)
+            sub16[(size_t)ca * 4 + code / 4] |= (uint32_t)(uint8_t)(int8_t)(nw::kEdna[ca][code] * c->scale)
+                                                << (8 * (code % 4));
+    HIP_OR_FAIL(c, c->d_sub16.reserve(sub16.size()));
+    HIP_OR_FAIL(c, hipMemcpy(c->d_sub16.p, sub16.data(), sub16.size() * 4, hipMemcpyHostToDevice));
     HIP_OR_FAIL(c, c->d_lut6.reserve(256));
     HIP_OR_FAIL(c, c->d_lut.reserve(256));
     HIP_OR_FAIL(c, c->d_btab.reserve(btab.size()));
@@ -358,11 +374,46 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n);
 
 int64_t stride_for(int La, int32_t lb_max) { return ((int64_t)La + lb_max + 15) & ~(int64_t)15; }
 
+// Amplicons longer than the one-wave kernels take (kMaxRefWave < La <= kMaxRef):
+// every read through the exact multi-wave kernel (nw_exact.hip), one workgroup per
+// read, as many workgroups as the CUs hold.
+int configure_long(nw_ctx* c) {
+    const int La = (int)c->ref.size();
+    c->use_band = c->use_stream = c->use_diag = false;
+    c->diag16_fill.grid = 0;
+    c->cfg = nw::LaunchCfg{};
+    c->exact_tb_lds = true;
+    c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, true);
+    c->exact_slab = 0;
+    const int W = nw::exact_waves(La);
+    int per_cu = std::max(1, 32 / W);   // 32 wavefronts per CU
+    if (c->exact_lds > kMaxLds) {
+        c->exact_tb_lds = false;
+        c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, false);
+        c->exact_slab = (nw::exact_slab_bytes(La, c->lb_max) + 255) & ~(int64_t)255;
+    }
+    if (c->exact_lds <= 0 || c->exact_lds > kMaxLds)
+        return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel for a %d bp amplicon", c->lb_max, La);
+    per_cu = std::max(1, std::min(per_cu, kMaxLds / c->exact_lds));
+    int64_t grid = std::max<int64_t>(1, std::min<int64_t>((int64_t)c->num_cus * per_cu, std::max<int64_t>(c->n, 1)));
+    if (!c->exact_tb_lds) {
+        grid = std::max<int64_t>(1, std::min<int64_t>(grid, (2ll << 30) / c->exact_slab));
+        HIP_OR_FAIL(c, c->s->d_tb.reserve((size_t)(c->exact_slab * grid)));
+    }
+    c->exact_grid = (int)grid;
+    c->exact_full = true;
+    HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
+    return NW_OK;
+}
+
 int configure(nw_ctx* c) {
     if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))   // tests: band width of the full-matrix kernels
         c->band_slots = c->stream_slots = std::max(0, std::atoi(bs));
     const int La = (int)c->ref.size();
     const int R = c->cur.R;
+    c->exact_full = false;
+    if (R <= 0) return configure_long(c);
     // full-storage kernel: every alignment (band disabled) or only the fallbacks
     nw::LaunchCfg cfg{};
     cfg.R = R;
@@ -387,6 +438,27 @@ int configure(nw_ctx* c) {
         HIP_OR_FAIL(c, c->s->d_tb.reserve((size_t)per_wave * cfg.grid * cfg.wpb));
     }
     c->cfg = cfg;
+    // exact multi-wave kernel for the work lists (the reads no band certifies)
+    c->exact_grid = 0;
+    // Off by default: at the ~15 reads per 1M C2 reads it is not faster than the one-wave
+    // kernel (both are VALU-issue bound), so it serves the long amplicons
+    const char* ex = std::getenv("CRISPR_NW_EXACT");   // "multi": fallbacks through it (tests/diagnostics)
+    if (nw::exact_rows_per_lane(La) > 0 && ex && std::strcmp(ex, "multi") == 0) {
+        c->exact_tb_lds = true;
+        c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, true);
+        c->exact_slab = 0;
+        int grid = c->num_cus;
+        if (c->exact_lds > kMaxLds) {
+            c->exact_tb_lds = false;
+            c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, false);
+            c->exact_slab = (nw::exact_slab_bytes(La, c->lb_max) + 255) & ~(int64_t)255;
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (1ll << 30) / std::max<int64_t>(c->exact_slab, 1)));
+            HIP_OR_FAIL(c, c->s->d_tb.reserve((size_t)(c->exact_slab * grid)));
+        }
+        if (const char* eg = std::getenv("CRISPR_NW_EXACT_GRID"))   // tests: split the list between the kernels
+            grid = std::max(1, std::min(grid, std::atoi(eg)));
+        if (c->exact_lds > 0 && c->exact_lds <= kMaxLds) c->exact_grid = grid;
+    }
     // banded kernel
     c->use_band = false;
     if (c->band_slots > 0) {
@@ -551,6 +623,7 @@ void nw_destroy(nw_ctx* c) {
     c->d_stats.release();
     c->d_lut6.release();
     c->d_btab.release();
+    c->d_sub16.release();
     for (Scratch& S : c->sc) S.release();
     c->d_ctl64.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
@@ -671,6 +744,20 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
 
 namespace {
 
+// The exact int32 kernel over a device work list (a.work_list / a.work_count): the
+// multi-wave kernel (nw_exact.hip) when configured, else the one-wave kernel.
+// Entries [0, exact_grid) go to the multi-wave kernel (one read per workgroup: the
+// latency of a few reads), the rest, if any, to the one-wave kernel (throughput when
+// many reads need the exact DP, e.g. an unrelated amplicon's HDR pass).
+hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
+    if (c->exact_grid <= 0) return nw::launch(a, c->cfg, c->cs);
+    hipError_t e = nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, true, c->cs);
+    if (e != hipSuccess) return e;
+    nw::KernelArgs rest = a;
+    rest.work_lo = c->exact_grid;
+    return nw::launch(rest, c->cfg, c->cs);
+}
+
 // Launches the kernels for the c->n reads that start at read `base` of the
 // uploaded arrays (outputs, records and fallback queue at the same index).
 // Everything is queued on c->stream; nothing synchronises.
@@ -692,6 +779,8 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.stride = c->stride;
     a.stats = c->d_stats.p + base;
     a.tb_global = c->s->d_tb.p;
+    a.sub16 = c->d_sub16.p;
+    a.rowpos = c->cur.rowpos;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
     a.band_slots = c->band_slots;
     a.fallback_list = c->s->d_fallback.p + base;
@@ -732,15 +821,19 @@ int launch_range(nw_ctx* c, int64_t base) {
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
         // ranges to the device-side counts.
         const bool two = c->diag16_fill.grid > 0;
+        // CRISPR_NW_LEVELS=16: the first level's give-ups go straight to the exact kernel
+        const char* lv = std::getenv("CRISPR_NW_LEVELS");
+        const bool only16 = two && lv && std::strcmp(lv, "16") == 0;
         a.redo_list = c->s->d_redo.p;
         a.redo_count = c->s->d_fallback_count.p + 2;
-        if (two) {
+        if (two && !only16) {
             a.redo_flags = c->s->d_redo_flags.p;
             a.redo_blk = c->s->d_redo_blk.p;
             HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_redo_flags.p, 0, (size_t)c->n, c->cs));
         }
-        for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
+        for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
             nw::KernelArgs al = a;
+            al.band_last = only16;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
                 HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->cs));
@@ -763,7 +856,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
         a.work_count = c->s->d_fallback_count.p;
-        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
+        HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
     if (c->use_stream) {
@@ -801,19 +894,27 @@ int launch_range(nw_ctx* c, int64_t base) {
             af.nops = ap.nops;
             af.work_list = ap.fallback_list;    // exact int32 kernel on what left the band
             af.work_count = ap.fallback_count;
-            HIP_OR_FAIL(c, nw::launch(af, c->cfg, c->cs));
+            HIP_OR_FAIL(c, launch_work(c, af));
         }
         return NW_OK;
     }
     HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
     a.work_counter = c->s->d_fallback_count.p + 1;
+    if (c->exact_full) {   // long amplicon: every read through the multi-wave kernel
+        if (c->n > 0)
+            HIP_OR_FAIL(c, nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, false,
+                                            c->cs));
+        return NW_OK;
+    }
     if (c->n > 0) {
         if (c->use_band) {
             HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->cs));
             a.work_list = a.fallback_list;
             a.work_count = c->s->d_fallback_count.p;
+            HIP_OR_FAIL(c, launch_work(c, a));
+        } else {
+            HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
         }
-        HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
     }
     return NW_OK;
 }

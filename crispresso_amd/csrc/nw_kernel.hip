@@ -161,6 +161,9 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wpb = blockDim.x >> 6;
+    const long long nwork = args.work_list ? (long long)*args.work_count : args.n;
+    // a work list shorter than the grid: blocks past its end leave before any set-up
+    if (args.work_list && args.work_lo + (long long)blockIdx.x * wpb >= nwork) return;
 
     // ---- shared per-block state: profile, ascii->code LUT, amplicon bytes ----
     unsigned char* prof_lds = smem;
@@ -194,8 +197,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int prof_lane = lane * RP;
     const int pad_coff = NCODE_PAD * 64 * RP;   // offset of the all-zero pad code
 
-    const long long nwork = args.work_list ? (long long)*args.work_count : args.n;
-    for (long long wi = gw; wi < nwork; wi += nwaves) {
+    for (long long wi = (args.work_list ? args.work_lo : 0) + gw; wi < nwork; wi += nwaves) {
         const long long rd = args.work_list ? args.work_list[wi] : wi;
         const long long off = args.offsets[rd];
         const int Lb = (int)(args.offsets[rd + 1] - off);

@@ -94,7 +94,8 @@ int nw_set_params(nw_ctx* ctx, float gap_open, float gap_extend, int end_weight,
 int nw_score_scale(const nw_ctx* ctx);
 
 /* The amplicon (needle -asequence; CRISPRessoCORE.py:1695-1696 / 1704-1705 /
- * 1885-1907).  Uploads the substitution profile.  1 <= ref_len <= 1024. */
+ * 1885-1907).  Uploads the substitution profile.  1 <= ref_len <= 8192 (amplicons over
+ * 1024 bp go through the exact multi-wave kernel only). */
 int nw_set_reference(nw_ctx* ctx, const char* ref, int32_t ref_len);
 
 /* Bytes per string slot a caller must provide for reads up to max_read_len. */

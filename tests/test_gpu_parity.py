@@ -154,6 +154,62 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
     assert_same(oracle, amp, buf, off, batch, "band-fallback")
 
 
+@pytest.mark.parametrize("exact", ["multi", "split", "wave"])
+@pytest.mark.parametrize("La", [1, 5, 63, 64, 65, 200, 250, 333, 600, 1000, 1024])
+def test_exact_kernel_work_list(gpu_aligner_factory, oracle, monkeypatch, La, exact):
+    """Every read through the exact int32 kernel's work list (a one-slot band hands
+    nearly all of them on): the multi-wave kernel (nw_exact.hip: one row per lane, up
+    to 16 waves, LDS ring hand-off between waves), the one-wave kernel, and the two
+    splitting one list (the multi-wave kernel takes the first grid entries) give the
+    oracle's alignments -- IUPAC, '-' and lower-case reads, reads longer and shorter
+    than the amplicon, big indels."""
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "band")
+    monkeypatch.setenv("CRISPR_NW_BAND_SLOTS", "1")
+    if exact != "wave":
+        monkeypatch.setenv("CRISPR_NW_EXACT", "multi")
+    if exact == "split":   # 7 reads to the multi-wave kernel, the rest to the one-wave kernel
+        monkeypatch.setenv("CRISPR_NW_EXACT_GRID", "7")
+    amp = synth.random_amplicon(La, 500 + La)
+    rng = np.random.Generator(np.random.PCG64(La))
+    reads = [amp, amp.lower(), amp[: max(1, La // 2)], "ACGTRYKMSWBDHVNU", "T-C-A" * 3, "N" * 9]
+    for L in (1, 3, La + 40, 2 * La + 5):
+        reads.append(synth.random_amplicon(L, int(rng.integers(1 << 30))))
+    if La > 60:
+        d = La // 5
+        reads += [amp[:La // 3] + amp[La // 3 + d:], amp[:La // 2] + synth.random_amplicon(d, 7) + amp[La // 2:]]
+    sub, soff = synth.reads_from(amp, 60, La + 3, synth.PARITY_MIX)
+    reads += synth.unpack(sub, soff)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert_same(oracle, amp, buf, off, batch, f"exact-{exact} La={La}")
+    # reads whose length differs from the amplicon's cannot fit a one-slot band
+    assert a.fallbacks() >= int((np.diff(off) != La).sum()) - 1
+
+
+@pytest.mark.parametrize("mode", ["ops", "rows"])
+@pytest.mark.parametrize("La", [1025, 1500, 2100, 4100])
+def test_long_amplicons(gpu_aligner_factory, oracle, monkeypatch, La, mode):
+    """Amplicons past the band / one-wave kernels' 1024 bp: every read through the
+    multi-wave exact kernel (R = 2 / 4 / 8 rows per lane, up to 16 waves), traceback in
+    an HBM slab -- bit-identical to the oracle, rows and ops output."""
+    monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
+    amp = synth.random_amplicon(La, 900 + La)
+    rng = np.random.Generator(np.random.PCG64(La))
+    reads = [amp, amp[: La // 3], amp[La // 2:], amp[:100] + amp[400:], "ACGTRYKMSWBDHVNU", "",
+             amp[:La // 2] + synth.random_amplicon(60, 3) + amp[La // 2:], synth.random_amplicon(300, 5)]
+    for _ in range(6):
+        r = bytearray(amp.encode())
+        for p in rng.integers(0, La, 12):
+            r[p] = ord("ACGT"[int(rng.integers(4))])
+        reads.append(r.decode())
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"long La={La}")
+
+
 @pytest.mark.parametrize("slots", ["0", "8", "24"])
 def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
     """Same answers with the band off (full storage only) or very narrow (mostly fallbacks)."""
