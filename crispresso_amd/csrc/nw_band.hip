@@ -172,6 +172,10 @@ __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const uns
 __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     const int La = a.La, nd = (La + 3) / 4;
+    // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
+    // here, the first kernel of the chain, instead of by memset launches
+    if (blockIdx.x == 0 && threadIdx.x < 4) a.fallback_count[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 2 && a.ops) a.ops_ctl[threadIdx.x] = 0;
     for (int k = threadIdx.x; k < nd; k += blockDim.x) {
         unsigned w = 0;
         for (int b = 0; b < 4; ++b) {
@@ -1093,8 +1097,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const int Lb = h ? hr.w : hr.z;
         const long long off = h ? (long long)(((unsigned long long)(unsigned)ho.w << 32) | (unsigned)ho.z)
                                 : (long long)(((unsigned long long)(unsigned)ho.y << 32) | (unsigned)ho.x);
+        if (W < kBandDiags && a.redo_flags && lane == 0) a.redo_flags[k] = 0;   // give_up may set it
         if (Lb <= 0) {
-            if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; a.stats[rd] = z; }
+            if (lane == 0) {
+                Stat z = {};
+                z.flags = FLAG_EMPTY;
+                a.stats[rd] = z;
+                if (a.ops) a.nops[rd] = 0;
+            }
             continue;
         }
         if (hdr.z & kPairInactive) {   // too long, or the pair's lengths do not fit the band

@@ -139,7 +139,12 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
         const unsigned char* rp = a.reads + off;
         Stat* st = a.stats + rd;
         if (Lb <= 0) {
-            if (tid == 0) { Stat z = {}; z.flags = FLAG_EMPTY; *st = z; }
+            if (tid == 0) {
+                Stat z = {};
+                z.flags = FLAG_EMPTY;
+                *st = z;
+                if (a.ops) a.nops[rd] = 0;
+            }
             continue;
         }
         const int steps = Lb + nl + kExK * (W - 1) - 1;

@@ -794,14 +794,18 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.spill = c->s->d_spill.p;
         a.spill_cap = c->spill_cap;
         a.ops_ctl = c->s->d_opsctl.p;
-        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_nops.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(c->n, 1), c->cs));
-        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_opsctl.p, 0, 2 * sizeof(int32_t), c->cs));
+        // the band path writes every read's run count and zeroes its counters in its
+        // first kernel (nw_band_classify): no memset launches in the chunk's chain
+        if (!c->use_diag || c->n <= 0) {
+            HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_nops.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(c->n, 1), c->cs));
+            HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_opsctl.p, 0, 2 * sizeof(int32_t), c->cs));
+        }
     }
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
-        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
-        if (c->n <= 0) return NW_OK;
+        if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs) == hipSuccess
+                                  ? NW_OK : fail(c, NW_E_HIP, "hipMemsetAsync failed");
         a.lut6 = c->d_lut6.p;
         a.band_order = c->s->d_order.p;
         a.band_region = c->s->d_bregion.p;
@@ -828,8 +832,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.redo_count = c->s->d_fallback_count.p + 2;
         if (two && !only16) {
             a.redo_flags = c->s->d_redo_flags.p;
-            a.redo_blk = c->s->d_redo_blk.p;
-            HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_redo_flags.p, 0, (size_t)c->n, c->cs));
+            a.redo_blk = c->s->d_redo_blk.p;   // flags: the first level's walk writes every position's
         }
         for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
             nw::KernelArgs al = a;

@@ -203,7 +203,12 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         const int Lb = (int)(args.offsets[rd + 1] - off);
         Stat* st = args.stats + rd;
         if (Lb <= 0) {
-            if (lane == 0) { Stat z = {}; z.flags = FLAG_EMPTY; *st = z; }
+            if (lane == 0) {
+                Stat z = {};
+                z.flags = FLAG_EMPTY;
+                *st = z;
+                if (args.ops) args.nops[rd] = 0;
+            }
             continue;
         }
         if constexpr (MODE == TB_BAND) {
