@@ -45,7 +45,7 @@ EXPORTS = (
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
-    "nw_fastq_read", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
+    "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
     "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat",
 )
 
@@ -130,6 +130,9 @@ def load() -> ctypes.CDLL:
         "nw_align_ops": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops_resident": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_fastq_read": (c_int, [c_char_p, POINTER(c_void_p)]),
+        "nw_fastq_read_filtered": (c_int, [c_char_p, c_int32, c_int32, POINTER(c_void_p)]),
+        "nw_fastq_dropped": (c_int64, [c_void_p]),
+        "nw_fastq_pass": (c_void_p, [c_void_p, POINTER(c_int64)]),
         "nw_expand_ops_subset": (c_int, [c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_int32]),
         "nw_ops_rows_concat": (c_int, [c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

@@ -165,9 +165,11 @@ __device__ __forceinline__ int len_bucket(const int64_t* offsets, long long r, i
 // residues (S > UB of the one-diagonal band, the certificate above), so the
 // alignment is the diagonal and the start cell the corner: this kernel writes its
 // strings and record right away, and the sort keeps it out of the band passes.
-// Wavefront batches of 64 reads, 4 compares in flight; 4 bytes per lane and compare:
+// Wavefront batches of 64 reads, kCand compares in flight; 4 bytes per lane and compare:
 // (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
 __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
+
+constexpr int kCand = 8;   // exact-copy candidates compared together (2 dword loads each in flight)
 
 __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
@@ -198,16 +200,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
         unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
         unsigned long long exact = 0ull;
-        // compare 4 candidates at a time (their loads in flight together); when the read
+        // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
         // away from the words already in registers
         const bool one_chunk = nd <= 64;
         unsigned long long emit_later = 0ull;
         while (cand) {
-            int us[4];
-            unsigned diff[4], raw[4];
+            int us[kCand];
+            unsigned diff[kCand], raw[kCand];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kCand; ++t) {
                 us[t] = cand ? (int)__builtin_ctzll(cand) : -1;
                 if (cand) cand &= cand - 1;
                 diff[t] = 0u;
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             for (int c0 = 0; c0 < nd; c0 += 64) {
                 const int k4 = c0 + lane;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
+                for (int t = 0; t < kCand; ++t) {
                     if (us[t] < 0 || k4 >= nd) continue;
                     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, us[t]);
                     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), us[t]);
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 }
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < kCand; ++t) {
                 if (us[t] < 0 || __ballot(diff[t] != 0u) != 0ull) continue;
                 exact |= 1ull << us[t];
                 if (a.ops) {   // ops output: one M run of La columns, no rows
@@ -874,7 +876,9 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
 }
 
 constexpr int kBandReadCap = 1280;   // >= the band length cap (La + 31, La <= 1024): every walked read fits
-__host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La); }
+// lut, amplicon bytes, markup rows, the EDNAFULL score rows (17 x 16 int8: the
+// single-diagonal test)
+__host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + align16(La + 16) + align16(4 * La) + 17 * 16; }
 constexpr int kBandRunsCap = 256;     // traceback runs per read (more: the read goes to the next level)
 __host__ __device__ inline int band_walk_row(int La, int lb_max) { return (La + lb_max + 15) & ~15; }   // = stride_for()
 __host__ __device__ inline int band_walk_rcap(int lb_max) { return min(kBandReadCap, (lb_max + 255) & ~255); }
@@ -1053,12 +1057,19 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     unsigned char* lut_lds = smem;
     unsigned char* amp_lds = smem + 256;
     unsigned* rowpos = (unsigned*)(smem + 256 + align16(La + 16));
+    unsigned* sub_lds = rowpos + align16(4 * La) / 4;   // [17][4]: EDNAFULL(a, b) * scale, int8, b = 0..15
     for (int k = tid; k < 256; k += blockDim.x) lut_lds[k] = a.lut[k];
     for (int k = tid; k < La; k += blockDim.x) {
         amp_lds[k] = a.amp[k];
         rowpos[k] = a.rowpos[k];
     }
+    for (int k = tid; k < 17 * 4; k += blockDim.x) sub_lds[k] = a.sub16[k];
     __syncthreads();
+    // substitution score of amplicon byte x against read byte y (0 for codes outside EDNAFULL)
+    auto sub_of = [&](unsigned char x, unsigned char y) {
+        const int cx = lut_lds[x], cy = lut_lds[y];
+        return cy < 16 ? (int)(signed char)(sub_lds[cx * 4 + (cy >> 2)] >> (8 * (cy & 3))) : 0;
+    };
     const int row = band_walk_row(La, a.Lb_max);   // columns <= La + Lb
     const int rcap = band_walk_rcap(a.Lb_max);
     unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes(La, a.Lb_max);
@@ -1164,11 +1175,32 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             continue;
         }
-        const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
-        const int tb0 = kBK - dlo + 2 - tau0;
-        const int nruns =
-            band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs, kBandRunsCap, lane);
+        // Single-diagonal fast path: when the start cell's score equals the plain sum of
+        // substitution scores down its diagonal to the matrix edge, D(ei, ej), the
+        // traceback is that diagonal (M(i, j) >= D(i, j) everywhere, so H = M = D on
+        // each of its cells, and M wins ties), with the end gaps around it: no band bits
+        // are read.  Reads with substitutions only (most non-identical reads) take it.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
+        int nruns;
+        const int nd = min(ei, ej);
+        int dsum = 0;
+        for (int t = lane; t < nd; t += 64) dsum += sub_of(amp_lds[ei - 1 - t], rbuf[mis + ej - 1 - t]);
+        if (wave_sum(dsum) == score) {
+            if (lane == 0) {
+                int q = 0;
+                if (ei == La && ej < Lb) runs[q++] = ((unsigned)RUN_X << 28) | (unsigned)(Lb - ej);
+                else if (ej == Lb && ei < La) runs[q++] = ((unsigned)RUN_Y << 28) | (unsigned)(La - ei);
+                runs[q++] = ((unsigned)RUN_M << 28) | (unsigned)nd;
+                if (ei > nd) runs[q++] = ((unsigned)RUN_Y << 28) | (unsigned)(ei - nd);
+                else if (ej > nd) runs[q++] = ((unsigned)RUN_X << 28) | (unsigned)(ej - nd);
+            }
+            nruns = 1 + ((ei == La && ej < Lb) || (ej == Lb && ei < La)) + (ei > nd || ej > nd);
+        } else {
+            const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
+            const int tb0 = kBK - dlo + 2 - tau0;
+            nruns = band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs,
+                                                         kBandRunsCap, lane);
+        }
         if (nruns < 0) {
             give_up(k, rd, true);
             continue;

@@ -14,6 +14,15 @@
 // One pass over the decompressed stream (zlib gzread: plain files read through as
 // well), 64 MB at a time: headers -> names ('\n'-joined), sequence lines filtered
 // straight into one packed buffer + offsets, quality lines skipped by memchr.
+//
+// Optional read quality filter (nw_fastq_read_filtered), the one CRISPResso applies
+// before anything else when --min_average_read_quality / --min_single_bp_quality are
+// set (filter_se_fastq_by_qual, CRISPRessoCORE.py:270-308, called at 1547-1583): a
+// record is kept when the mean of its Phred+33 qualities is >= min_avg and their
+// minimum >= min_single (integer test sum >= min_avg * n: exact, as numpy's float mean
+// of integers is here); a record with an empty quality line is dropped (its numpy mean
+// is NaN).  A dropped record's name and bases are rolled back.  pass[] keeps every
+// record's verdict for the paired-end filter (by read id, in Python).
 #include <zlib.h>
 
 #include <algorithm>
@@ -28,6 +37,8 @@ struct nw_fastq {
     std::vector<char> seqs;
     std::vector<int64_t> offsets{0};
     std::vector<char> names;   // record names joined by '\n'
+    std::vector<uint8_t> pass; // quality verdict of every record read (filtered reads only)
+    int64_t dropped = 0;
     std::string err;
 };
 
@@ -57,6 +68,11 @@ struct Parser {
     int64_t line = 0;           // index of the line being read
     bool name_started = false, name_done = false;
     int64_t headers = 0, seq_lines = 0;
+    // quality filter (filter = false: quality lines are skipped unread)
+    bool filter = false;
+    int64_t min_avg = 0, min_single = 0;
+    int64_t qsum = 0, qn = 0, qmin = 1 << 30;
+    size_t name_mark = 0;       // names.size() before the current record
 
     void end_line() {
         const int k = (int)(line & 3);
@@ -66,9 +82,36 @@ struct Parser {
         } else if (k == 1) {
             q->offsets.push_back((int64_t)q->seqs.size());
             ++seq_lines;
+        } else if (k == 3 && filter) {
+            end_record();
         }
         ++line;
         name_started = name_done = false;
+    }
+    // the record's quality verdict; a failing record is taken back out
+    void end_record() {
+        const bool keep = qn > 0 && qsum >= min_avg * qn && qmin >= min_single;
+        q->pass.push_back((uint8_t)keep);
+        if (!keep) {
+            q->names.resize(name_mark);
+            q->offsets.pop_back();
+            q->seqs.resize((size_t)q->offsets.back());
+            --headers;
+            --seq_lines;
+            ++q->dropped;
+        }
+        name_mark = q->names.size();
+        qsum = qn = 0;
+        qmin = 1 << 30;
+    }
+    void feed_quality(const unsigned char* p, const unsigned char* e) {
+        for (; p < e; ++p) {
+            if (*p == '\r') continue;
+            const int64_t v = (int64_t)*p - 33;
+            qsum += v;
+            qmin = v < qmin ? v : qmin;
+            ++qn;
+        }
     }
     // bytes [p, e) of the current line (no '\n'; a line may arrive in several pieces)
     void feed(const unsigned char* p, const unsigned char* e) {
@@ -102,7 +145,7 @@ struct Parser {
 
 extern "C" {
 
-int nw_fastq_read(const char* path, nw_fastq** out) {
+int nw_fastq_read_filtered(const char* path, int32_t min_avg_quality, int32_t min_single_quality, nw_fastq** out) {
     if (!path || !out) return NW_E_INVALID;
     *out = nullptr;
     gzFile f = gzopen(path, "rb");
@@ -110,6 +153,9 @@ int nw_fastq_read(const char* path, nw_fastq** out) {
     (void)gzbuffer(f, 1 << 20);
     nw_fastq* q = new nw_fastq();
     Parser ps{q};
+    ps.filter = min_avg_quality > 0 || min_single_quality > 0;
+    ps.min_avg = min_avg_quality;
+    ps.min_single = min_single_quality;
     std::vector<unsigned char> buf((size_t)64 << 20);
     bool pending = false;   // bytes of an unterminated line seen
     for (;;) {
@@ -126,6 +172,7 @@ int nw_fastq_read(const char* path, nw_fastq** out) {
         const unsigned char* e = p + got;
         while (p < e) {
             const unsigned char* nl = (const unsigned char*)std::memchr(p, '\n', (size_t)(e - p));
+            if ((ps.line & 3) == 3 && ps.filter) ps.feed_quality(p, nl ? nl : e);
             if ((ps.line & 3) >= 2) {   // quality / '+' lines: skip to the end of the line
                 if (!nl) {
                     pending = true;
@@ -155,8 +202,20 @@ int nw_fastq_read(const char* path, nw_fastq** out) {
         q->offsets.push_back((int64_t)q->seqs.size());
         ++ps.seq_lines;
     }
+    // a record cut off before its quality line: no qualities (mean NaN), dropped
+    if (ps.filter && (ps.line & 3) != 0) ps.end_record();
     *out = q;
     return NW_OK;
+}
+
+int nw_fastq_read(const char* path, nw_fastq** out) { return nw_fastq_read_filtered(path, 0, 0, out); }
+
+int64_t nw_fastq_dropped(const nw_fastq* q) { return q ? q->dropped : -1; }
+// quality verdict of every record of the file (nw_fastq_read_filtered with a threshold)
+const uint8_t* nw_fastq_pass(const nw_fastq* q, int64_t* n) {
+    if (!q) return nullptr;
+    if (n) *n = (int64_t)q->pass.size();
+    return q->pass.data();
 }
 
 int64_t nw_fastq_count(const nw_fastq* q) { return q ? (int64_t)q->offsets.size() - 1 : -1; }

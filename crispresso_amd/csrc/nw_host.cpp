@@ -1522,6 +1522,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
+    const int64_t lag = std::max(1, nsets - 1);
     bool any_diag = false;
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
@@ -1548,10 +1549,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
                                       hipMemcpyDeviceToHost, c->cs));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
-        // s_out order: chunk k - 1's runs (their size is known once k - 1 is done), then
-        // chunk k's records and offsets -- so the runs a later compaction waits for are
-        // never queued behind records that wait for a chunk still computing
-        if (k >= 1 && (rc = copy_runs(k - 1))) return restore(rc);
+        // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
+        // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
+        // k's records and offsets
+        if (k >= lag && (rc = copy_runs(k - lag))) return restore(rc);
         HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
         HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
@@ -1559,7 +1560,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                       hipMemcpyDeviceToHost, c->s_out));
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
     }
-    if (nchunks > 0 && (rc = copy_runs(nchunks - 1))) return restore(rc);
+    for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k)
+        if ((rc = copy_runs(k))) return restore(rc);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ops_off[n] = total;
     if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)

@@ -54,19 +54,23 @@ class NameList(list):
         self.raw = raw
 
 
-def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
+def read_fastq_as_fasta(path: str, min_bp_quality: int = 0,
+                        min_single_bp_quality: int = 0) -> Tuple[List[str], np.ndarray, np.ndarray]:
     """-> (fasta names, packed sequences, offsets) in file order.
 
     Native ingest (``nw_fastq_read``, zlib + one C++ pass); the semantics are those
     of :func:`fastq_bytes_as_fasta` below (the Python restatement the tests hold the
-    native reader to)."""
+    native reader to).  With a quality threshold only the records
+    filter_se_fastq_by_qual (``CORE:270-308``) keeps are returned
+    (``nw_fastq_read_filtered``; restated by :func:`quality_pass`)."""
     import ctypes
 
     from . import _lib
 
     lib = _lib.load()
     h = ctypes.c_void_p()
-    if lib.nw_fastq_read(os.fsencode(path), ctypes.byref(h)) != _lib.NW_OK:
+    if lib.nw_fastq_read_filtered(os.fsencode(path), int(min_bp_quality), int(min_single_bp_quality),
+                                  ctypes.byref(h)) != _lib.NW_OK:
         raise OSError(f"cannot read FASTQ {path}")
     try:
         n = int(lib.nw_fastq_count(h))
@@ -85,14 +89,28 @@ def read_fastq_as_fasta(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
     return NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), seqs, off
 
 
-def read_fastq_as_fasta_py(path: str) -> Tuple[List[str], np.ndarray, np.ndarray]:
+def read_fastq_as_fasta_py(path: str, min_bp_quality: int = 0,
+                           min_single_bp_quality: int = 0) -> Tuple[List[str], np.ndarray, np.ndarray]:
     """The Python restatement (gzip + :func:`fastq_bytes_as_fasta`)."""
     with _open(path) as f:
         data = f.read()
-    return fastq_bytes_as_fasta(data)
+    return fastq_bytes_as_fasta(data, min_bp_quality, min_single_bp_quality)
 
 
-def fastq_bytes_as_fasta(data: bytes) -> Tuple[List[str], np.ndarray, np.ndarray]:
+def quality_pass(qual_lines: List[bytes], min_bp_quality: int, min_single_bp_quality: int) -> List[bool]:
+    """filter_se_fastq_by_qual's test per record (``CORE:296-305``): keep when
+    ``mean(phred) >= min_bp_quality and min(phred) >= min_single_bp_quality``, Phred+33
+    as Biopython's "fastq" parser reads it.  An empty quality line has a NaN mean: the
+    record is not kept (the test short-circuits before ``min()``)."""
+    out = []
+    for q in qual_lines:
+        ph = np.frombuffer(q.rstrip(b"\r"), dtype=np.uint8).astype(np.int64) - 33
+        out.append(bool(len(ph)) and ph.mean() >= min_bp_quality and ph.min() >= min_single_bp_quality)
+    return out
+
+
+def fastq_bytes_as_fasta(data: bytes, min_bp_quality: int = 0,
+                         min_single_bp_quality: int = 0) -> Tuple[List[str], np.ndarray, np.ndarray]:
     lines = data.split(b"\n")
     if lines and lines[-1] == b"":
         lines.pop()
@@ -100,8 +118,83 @@ def fastq_bytes_as_fasta(data: bytes) -> Tuple[List[str], np.ndarray, np.ndarray
     seqs = lines[1::4][: len(headers)]
     if len(seqs) < len(headers):  # awk prints a header even without a sequence line
         seqs += [b""] * (len(headers) - len(seqs))
+    if min_bp_quality > 0 or min_single_bp_quality > 0:
+        quals = lines[3::4]
+        quals += [b""] * (len(headers) - len(quals))
+        keep = quality_pass(quals, min_bp_quality, min_single_bp_quality)
+        headers = [h for h, k in zip(headers, keep) if k]
+        seqs = [s for s, k in zip(seqs, keep) if k]
     names = [fasta_name(h) for h in headers]
     return (names,) + pack_filtered(seqs)
+
+
+def _records(path: str) -> List[Tuple[bytes, bytes, bytes]]:
+    """(header, sequence, quality) lines of every 4-line record."""
+    with _open(path) as f:
+        lines = f.read().split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    lines += [b""] * ((-len(lines)) % 4)
+    return list(zip(lines[0::4], lines[1::4], lines[3::4]))
+
+
+def _record_id(header: bytes) -> str:
+    """Biopython's record.id: the title after '@' up to the first whitespace."""
+    tok = header[1:].rstrip(b"\r").split()
+    return tok[0].decode("ascii", "replace") if tok else ""
+
+
+def get_ids_reads_to_remove(fastq_filename: str, min_bp_quality: int = 20, min_single_bp_quality: int = 0) -> set:
+    """get_ids_reads_to_remove (``CORE:162-193``): ids of the records whose mean
+    Phred quality is < min_bp_quality or whose lowest is < min_single_bp_quality."""
+    out = set()
+    for h, _, q in _records(fastq_filename):
+        ph = np.frombuffer(q.rstrip(b"\r"), dtype=np.uint8).astype(np.int64) - 33
+        if len(ph) == 0:
+            raise ValueError(f"record {_record_id(h)} has no qualities")   # numpy: min() of an empty array
+        if ph.mean() < min_bp_quality or ph.min() < min_single_bp_quality:
+            out.add(_record_id(h))
+    return out
+
+
+def _write_records(path: str, recs) -> None:
+    """Records as Biopython's FASTQ writer prints them: '@title', sequence, '+', qualities."""
+    import gzip as _gz
+
+    with _gz.open(path, "wb") as f:
+        f.write(b"".join(h.rstrip(b"\r") + b"\n" + s.rstrip(b"\r") + b"\n+\n" + q.rstrip(b"\r") + b"\n"
+                         for h, s, q in recs))
+
+
+def _filtered_name(fastq_filename: str) -> str:
+    return fastq_filename.replace(".fastq", "").replace(".gz", "") + "_filtered.fastq.gz"
+
+
+def filter_se_fastq_by_qual(fastq_filename: str, output_filename: str = None, min_bp_quality: int = 20,
+                            min_single_bp_quality: int = 0) -> str:
+    """filter_se_fastq_by_qual (``CORE:270-308``): writes the records with mean
+    quality >= min_bp_quality and none < min_single_bp_quality; returns the file name.
+    (:func:`read_fastq_as_fasta` with the thresholds gives the same reads in memory.)"""
+    output_filename = output_filename or _filtered_name(fastq_filename)
+    recs = _records(fastq_filename)
+    keep = quality_pass([q for _, _, q in recs], min_bp_quality, min_single_bp_quality)
+    _write_records(output_filename, [r for r, k in zip(recs, keep) if k])
+    return output_filename
+
+
+def filter_pe_fastq_by_qual(fastq_r1: str, fastq_r2: str, output_filename_r1: str = None,
+                            output_filename_r2: str = None, min_bp_quality: int = 20,
+                            min_single_bp_quality: int = 0) -> Tuple[str, str]:
+    """filter_pe_fastq_by_qual (``CORE:196-267``): a pair goes when either mate's id is
+    in either file's get_ids_reads_to_remove set; returns the two file names."""
+    drop = get_ids_reads_to_remove(fastq_r1, min_bp_quality, min_single_bp_quality) | \
+        get_ids_reads_to_remove(fastq_r2, min_bp_quality, min_single_bp_quality)
+    outs = []
+    for src, dst in ((fastq_r1, output_filename_r1), (fastq_r2, output_filename_r2)):
+        dst = dst or _filtered_name(src)
+        _write_records(dst, [r for r in _records(src) if _record_id(r[0]) not in drop])
+        outs.append(dst)
+    return outs[0], outs[1]
 
 
 def pack_filtered(seqs: List[bytes]) -> Tuple[np.ndarray, np.ndarray]:

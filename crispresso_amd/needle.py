@@ -390,6 +390,10 @@ class AlignArgs:
     needle_options_string: str = DEFAULT_NEEDLE_OPTIONS
     keep_intermediate: bool = False
     dump: bool = False
+    # --min_average_read_quality / --min_single_bp_quality: the reads the quality filter
+    # keeps (filter_se_fastq_by_qual, CORE:1547-1583) are the ones aligned
+    min_average_read_quality: int = 0
+    min_single_bp_quality: int = 0
 
 
 def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Optional[GpuAligner] = None,
@@ -412,7 +416,8 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
     keep_files = bool(output_dir) and (args.keep_intermediate or args.dump)
     _jp = (lambda f: os.path.join(output_dir, f)) if output_dir else (lambda f: f)
     try:
-        names, buf, offsets = fastq.read_fastq_as_fasta(processed_output_filename)
+        names, buf, offsets = fastq.read_fastq_as_fasta(processed_output_filename, args.min_average_read_quality,
+                                                        args.min_single_bp_quality)
         fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
                           _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None)
         if args.expected_hdr_amplicon_seq:

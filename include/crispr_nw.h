@@ -253,6 +253,13 @@ const char* nw_fastq_seqs(const nw_fastq* q);
 const int64_t* nw_fastq_offsets(const nw_fastq* q);
 const char* nw_fastq_names(const nw_fastq* q, int64_t* bytes);   /* each name followed by '\n' */
 void nw_fastq_free(nw_fastq* q);
+/* nw_fastq_read keeping only the records whose Phred+33 qualities average >=
+ * min_avg_quality with none < min_single_quality -- CRISPResso's read quality filter
+ * (filter_se_fastq_by_qual, CRISPRessoCORE.py:270-308; --min_average_read_quality /
+ * --min_single_bp_quality, 1547-1583).  Thresholds <= 0 both: no filter. */
+int nw_fastq_read_filtered(const char* path, int32_t min_avg_quality, int32_t min_single_quality, nw_fastq** out);
+int64_t nw_fastq_dropped(const nw_fastq* q);                    /* records the filter removed */
+const uint8_t* nw_fastq_pass(const nw_fastq* q, int64_t* n);    /* every record's verdict (1 = kept), file order */
 
 /* nw_expand_ops for the reads idx[0 .. m) only: read idx[q]'s rows at aln_out + q*3*stride. */
 int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,

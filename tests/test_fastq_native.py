@@ -61,3 +61,64 @@ def test_long_lines_across_read_chunks(tmp_path):
     with gzip.open(p, "wb", compresslevel=1) as f:
         f.write(b"".join(parts))
     assert len(_same(str(p))) == 3
+
+
+# ---- read quality filter (CORE:162-308, applied at 1547-1583) ----------------------------
+
+R1 = os.path.join(GOLDEN, "test_L001_R1_001.fastq.gz")   # the reference's own test data
+R2 = os.path.join(GOLDEN, "test_L001_R2_001.fastq.gz")
+
+
+def test_ids_reads_to_remove_known_answers():
+    """The reference's test_get_ids_reads_to_remove (tests/crispresso_tests.py:77-88)."""
+    assert fastq.get_ids_reads_to_remove(R1, 23) == {"M06879:15:000000000-DFF22:1:1101:25894:23776",
+                                                      "M06879:15:000000000-DFF22:1:1101:24046:20708"}
+    assert fastq.get_ids_reads_to_remove(R2, 15) == {"M06879:15:000000000-DFF22:1:1102:22078:15849"}
+
+
+@pytest.mark.parametrize("q", [(20, 0), (23, 0), (30, 0), (30, 10), (35, 20), (0, 15), (41, 0)])
+@pytest.mark.parametrize("path", [R1, R2])
+def test_native_quality_filter_matches_restatement(path, q):
+    """nw_fastq_read_filtered keeps exactly the records filter_se_fastq_by_qual keeps
+    (Python restatement of CORE:296-305), names and bases."""
+    got = fastq.read_fastq_as_fasta(path, *q)
+    want = fastq.read_fastq_as_fasta_py(path, *q)
+    assert list(got[0]) == list(want[0])
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
+    # the dropped records are the ones get_ids_reads_to_remove names (SE test = PE test per file)
+    allnames = fastq.read_fastq_as_fasta(path)[0]
+    dropped = set(allnames) - set(got[0])
+    ids = {("@" + i).split()[0].replace(":", "_") for i in fastq.get_ids_reads_to_remove(path, *q)}
+    assert dropped == ids
+
+
+def test_quality_filter_edge_cases(tmp_path):
+    """Empty quality line (NaN mean: dropped), a record cut before its quality line,
+    CRLF line ends, a quality exactly at the threshold (kept: mean >= q)."""
+    text = (b"@a\nACGT\n+\nIIII\n"      # Q40
+            b"@b\nACGT\n+\n\n"          # no qualities
+            b"@c\r\nACGT\r\n+\r\n5555\r\n"   # Q20 exactly
+            b"@d\nACGT\n+\n5554\n"      # mean 19.75
+            b"@e\nAC\n+\n!I\n"           # min 0, mean 20
+            b"@f\nACGTAC\n")             # truncated
+    p = tmp_path / "q.fastq"
+    p.write_bytes(text)
+    for q in [(20, 0), (20, 1), (1, 0), (0, 1)]:
+        got = fastq.read_fastq_as_fasta(str(p), *q)
+        want = fastq.read_fastq_as_fasta_py(str(p), *q)
+        assert list(got[0]) == list(want[0]), q
+        assert np.array_equal(got[2], want[2])
+    assert list(fastq.read_fastq_as_fasta(str(p), 20, 0)[0]) == ["@a", "@c", "@e"]
+
+
+def test_filter_se_pe_files(tmp_path):
+    """The reference's file-writing filters: outputs re-read to the same reads the
+    in-memory filter gives; the PE pair drops a read from both files when either mate fails."""
+    out = fastq.filter_se_fastq_by_qual(R1, str(tmp_path / "se.fastq.gz"), min_bp_quality=30)
+    assert list(fastq.read_fastq_as_fasta(out)[0]) == list(fastq.read_fastq_as_fasta(R1, 30)[0])
+    o1, o2 = fastq.filter_pe_fastq_by_qual(R1, R2, str(tmp_path / "r1.fastq.gz"), str(tmp_path / "r2.fastq.gz"),
+                                           min_bp_quality=30)
+    n1, n2 = fastq.read_fastq_as_fasta(o1)[0], fastq.read_fastq_as_fasta(o2)[0]
+    drop = fastq.get_ids_reads_to_remove(R1, 30) | fastq.get_ids_reads_to_remove(R2, 30)
+    assert len(n1) == len(n2) == len(fastq.read_fastq_as_fasta(R1)[0]) - len(drop)
+    assert fastq.filter_se_fastq_by_qual.__defaults__[1:] == (20, 0)   # the reference's defaults
