@@ -1184,8 +1184,20 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         int nruns;
         const int nd = min(ei, ej);
         int dsum = 0;
-        for (int t = lane; t < nd; t += 64) dsum += sub_of(amp_lds[ei - 1 - t], rbuf[mis + ej - 1 - t]);
-        if (wave_sum(dsum) == score) {
+        unsigned cnt = 0u;   // identical | similar << 10 | gap columns << 20 of the diagonal (band_emit's counts)
+        for (int t = lane; t < nd; t += 64) {
+            const unsigned char ca = amp_lds[ei - 1 - t], cb = rbuf[mis + ej - 1 - t];
+            const int sc = sub_of(ca, cb);
+            dsum += sc;
+            const bool gapc = ca == '-' || cb == '-';   // an input '-' prints as a gap (CORE:1846)
+            const bool id = !gapc && upcase(ca) == upcase(cb);
+            const bool sim = !gapc && (id || sc > 0);
+            cnt += (unsigned)id | ((unsigned)sim << 10) | ((unsigned)gapc << 20);
+        }
+        const bool diag = wave_sum(dsum) == score;
+        if (diag) {
+            const bool endg = (ei == La && ej < Lb) || (ej == Lb && ei < La);
+            const int lead = max(ei, ej) - nd;   // leading gap run (Y when ei > nd, X when ej > nd)
             if (lane == 0) {
                 int q = 0;
                 if (ei == La && ej < Lb) runs[q++] = ((unsigned)RUN_X << 28) | (unsigned)(Lb - ej);
@@ -1194,7 +1206,28 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
                 if (ei > nd) runs[q++] = ((unsigned)RUN_Y << 28) | (unsigned)(ei - nd);
                 else if (ej > nd) runs[q++] = ((unsigned)RUN_X << 28) | (unsigned)(ej - nd);
             }
-            nruns = 1 + ((ei == La && ej < Lb) || (ej == Lb && ei < La)) + (ei > nd || ej > nd);
+            nruns = 1 + (int)endg + (lead > 0);
+            if (a.ops && nd < 1024) {
+                // ops output: the record comes from the diagonal's counts; no emit pass
+                lds_fence();
+                store_ops(a, rd, runs, nruns, lane);
+                const unsigned t = wave_sum_u32(cnt);
+                if (lane == 0) {
+                    const int endlen = endg ? (ei == La ? Lb - ej : La - ei) : 0;
+                    Stat r;
+                    r.aln_len = nd + endlen + lead;
+                    r.n_ident = (int)(t & 1023u);
+                    r.n_sim = (int)((t >> 10) & 1023u);
+                    r.n_gaps = (int)(t >> 20) + endlen + lead;
+                    r.score = score;
+                    r.end_i = ei;
+                    r.end_j = ej;
+                    r.flags = 0;
+                    a.stats[rd] = r;
+                }
+                lds_fence();
+                continue;
+            }
         } else {
             const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
             const int tb0 = kBK - dlo + 2 - tau0;
