@@ -87,7 +87,17 @@ struct KernelArgs {
     // exact multi-wave kernel (nw_exact.hip): [17 amplicon codes][4] dwords, the scaled
     // EDNAFULL scores against read codes 0..15 as int8 (byte j of dword q: code 4q + j)
     const uint32_t* sub16;
+    // needle -endweight (the exact kernels only): an end gap of k residues costs
+    // end_open + (k - 1) * end_extend (scaled) instead of nothing
+    int32_t end_weight, end_open, end_extend;
 };
+
+// Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and
+// the penalty of a trailing one.
+__host__ __device__ inline int end_lead(const KernelArgs& a, int k) {
+    return (a.end_weight && k > 0) ? -(a.end_open + (k - 1) * a.end_extend) : 0;
+}
+__host__ __device__ inline int end_trail(const KernelArgs& a, int k) { return -end_lead(a, k); }
 
 // Traceback storage of a kernel instantiation.
 enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_STREAM = 4, TB_DIAG = 5 };

@@ -116,7 +116,10 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
     // and the column's read code) or the previous wave's ring
     const int4* src = rings + (w > 0 ? w - 1 : 0) * kExRing;
     auto fill_at = [&](int t) -> int4 {
-        if (w == 0) return make_int4(-O, NEG, 0, (int)topc[t]);
+        if (w == 0) {   // top boundary at column t: H = leading end gap of t + 1 (0: free)
+            const int h = end_lead(a, t + 1);
+            return make_int4(h - O, NEG, h, (int)topc[t]);
+        }
         return src[(t - 1 - kExK) & (kExRing - 1)];
     };
     int4* ring_out = w + 1 < W ? rings + w * kExRing : nullptr;
@@ -154,10 +157,13 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
         for (int t = tid; t < nblk * kExB + kExP + 1; t += blockDim.x)
             topc[t] = (unsigned char)(t < Lb ? a.lut[rp[t]] : NCODE_PAD);
         __syncthreads();
-        int Mol[R], Xl[R], Hold[R];
+        int Mol[R], Xl[R], Hold[R];   // column -1: H = M = leading end gap of the row (0: free)
 #pragma unroll
-        for (int k = 0; k < R; ++k) { Mol[k] = -O; Xl[k] = NEG; Hold[k] = 0; }
-        int sMo = -O, sY = NEG, sH = 0, sC = NCODE_PAD, Htop = 0;
+        for (int k = 0; k < R; ++k) {
+            const int h0 = end_lead(a, g * R + k + 1);
+            Mol[k] = h0 - O; Xl[k] = NEG; Hold[k] = h0;
+        }
+        int sMo = Mol[R - 1], sY = NEG, sH = Hold[R - 1], sC = NCODE_PAD, Htop = end_lead(a, g * R);
         int4 f0 = fill_at(0), f1 = fill_at(1);
         for (int b = 0; b < nblk; ++b) {
             __syncthreads();   // ring entries of the earlier blocks are visible
@@ -223,16 +229,16 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 const int ai = g * R + k;
-                if (ai < La) {
+                if (ai < La) {   // -endweight: minus the trailing end gap of the rows below
                     const long long prio = (ai == La - 1) ? (3ll << 24) : ((2ll << 24) | ai);
-                    const long long kk = ((long long)(Mol[k] + O) << 32) | prio;
+                    const long long kk = ((long long)(Mol[k] + O - end_trail(a, La - 1 - ai)) << 32) | prio;
                     key = kk > key ? kk : key;
                 }
             }
         }
         if (w == 0)
             for (int q = lane; q < Lb - 1; q += 64) {
-                const long long kk = ((long long)lastrow[q] << 32) | ((1ll << 24) | q);
+                const long long kk = ((long long)(lastrow[q] - end_trail(a, Lb - 1 - q)) << 32) | ((1ll << 24) | q);
                 key = kk > key ? kk : key;
             }
         key = wave_max_i64(key);

@@ -103,6 +103,8 @@ struct nw_ctx {
     // params
     float gap_open_f = 10.0f, gap_extend_f = 0.5f;
     int scale = 2, gap_open = 20, gap_extend = 1;
+    bool end_weight = false;           // needle -endweight: end gaps cost end_open + (k-1) end_extend
+    int end_open = 20, end_extend = 1; // scaled
     // reference
     std::string ref;
     DevBuf<uint8_t> d_arena;          // every amplicon's tables (upload_profiles)
@@ -475,6 +477,15 @@ int configure(nw_ctx* c) {
             c->use_band = true;
         }
     }
+    // -endweight: the band certificate and the stream kernels assume free end gaps;
+    // every read goes through the exact kernel (nw_align_kernel), which takes both
+    if (c->end_weight) {
+        c->use_band = c->use_stream = c->use_diag = false;
+        c->diag16_fill.grid = 0;
+        HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
+        HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
+        return NW_OK;
+    }
     const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" | "stream" | "band" | "full" (tests/diagnostics)
     const int64_t hi = 5ll * c->scale * La;
     const bool fits16 = hi + c->gap_extend < 16000 && 9ll * c->scale * La + c->gap_open + c->gap_extend < 32000;
@@ -653,28 +664,36 @@ const char* nw_last_error(const nw_ctx* c) { return c ? c->err.c_str() : "null c
 
 int nw_set_params(nw_ctx* c, float gap_open, float gap_extend, int end_weight, float end_open,
                   float end_extend, const char* matrix, int tie_policy) {
-    (void)end_open; (void)end_extend;
     if (!c) return NW_E_INVALID;
     if (matrix && *matrix) {
         std::string m(matrix);
         for (auto& ch : m) ch = (char)std::toupper((unsigned char)ch);
         if (m != "EDNAFULL") return fail(c, NW_E_UNSUPPORTED, "matrix %s not supported (EDNAFULL only)", matrix);
     }
-    if (end_weight) return fail(c, NW_E_UNSUPPORTED, "-endweight is not supported (needle default is off)");
     if (tie_policy != NW_TIE_EMBOSS) return fail(c, NW_E_UNSUPPORTED, "tie policy %d not supported", tie_policy);
     if (!(gap_open >= 0.0f) || !(gap_extend >= 0.0f) || gap_open > 1000.0f || gap_extend > 1000.0f)
         return fail(c, NW_E_INVALID, "gap penalties out of range: %g %g", gap_open, gap_extend);
+    if (end_weight && (!(end_open >= 0.0f) || !(end_extend >= 0.0f) || end_open > 1000.0f || end_extend > 1000.0f))
+        return fail(c, NW_E_INVALID, "end gap penalties out of range: %g %g", end_open, end_extend);
     int scale = 0;
     for (int s = 1; s <= 16; s *= 2) {
         double o = (double)gap_open * s, e = (double)gap_extend * s;
-        if (o == std::floor(o) && e == std::floor(e)) { scale = s; break; }
+        double eo = end_weight ? (double)end_open * s : 0.0, ee = end_weight ? (double)end_extend * s : 0.0;
+        if (o == std::floor(o) && e == std::floor(e) && eo == std::floor(eo) && ee == std::floor(ee)) {
+            scale = s;
+            break;
+        }
     }
-    if (!scale) return fail(c, NW_E_INEXACT, "gap penalties %g/%g are not multiples of 1/16", gap_open, gap_extend);
+    if (!scale) return fail(c, NW_E_INEXACT, "gap penalties %g/%g (end %g/%g) are not multiples of 1/16", gap_open,
+                            gap_extend, end_open, end_extend);
     c->gap_open_f = gap_open;
     c->gap_extend_f = gap_extend;
     c->scale = scale;
     c->gap_open = (int)std::lround((double)gap_open * scale);
     c->gap_extend = (int)std::lround((double)gap_extend * scale);
+    c->end_weight = end_weight != 0;
+    c->end_open = end_weight ? (int)std::lround((double)end_open * scale) : 0;
+    c->end_extend = end_weight ? (int)std::lround((double)end_extend * scale) : 0;
     if (!c->ref.empty()) {
         (void)hipSetDevice(c->device);
         return build_profile(c);
@@ -781,6 +800,9 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.tb_global = c->s->d_tb.p;
     a.sub16 = c->d_sub16.p;
     a.rowpos = c->cur.rowpos;
+    a.end_weight = c->end_weight;
+    a.end_open = c->end_open;
+    a.end_extend = c->end_extend;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
     a.band_slots = c->band_slots;
     a.fallback_list = c->s->d_fallback.p + base;

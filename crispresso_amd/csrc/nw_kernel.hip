@@ -232,11 +232,16 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         lds_fence();
 
         // ---- DP fill ----
+        // column -1 (left boundary): H = M = 0 with free end gaps, the leading end-gap
+        // value of row ai + 1 with -endweight; X = -inf
         int Mol[R], Xl[R], Hold[R];
 #pragma unroll
-        for (int k = 0; k < R; ++k) { Mol[k] = -O; Xl[k] = NEG; Hold[k] = 0; }
-        int sMo = -O, sY = NEG, sH = 0;    // what this lane's bottom row sends down
-        int Htop = 0;                       // H[row above][column-1]
+        for (int k = 0; k < R; ++k) {
+            const int h0 = end_lead(args, ai0 + k + 1);
+            Mol[k] = h0 - O; Xl[k] = NEG; Hold[k] = h0;
+        }
+        int sMo = Mol[R - 1], sY = NEG, sH = Hold[R - 1];   // what this lane's bottom row sends down
+        int Htop = end_lead(args, ai0);                      // H[row above][column-1]
         const int nsteps = Lb + nl - 1;
         // prefetch pipeline: coff for bj+1 loaded one step ahead, scores for bj loaded one step ahead
         int bj0 = -lane;
@@ -246,9 +251,11 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         int slot = tb.slot(lane, bj0);
         for (int t = 0; t < nsteps; ++t, ++slot) {
             const int bj = t - lane;
-            const int rMo = shr1(sMo, -O);
+            // lane 0's row above is the top boundary at column t (leading end gap of t + 1)
+            const int top = end_lead(args, t + 1);
+            const int rMo = shr1(sMo, top - O);
             const int rY = shr1(sY, NEG);
-            const int rH = shr1(sH, 0);
+            const int rH = shr1(sH, top);
             // issue next loads before the compute that hides their latency
             int sc_n[RP / 4];
             load_prof<R>(prof_lds, c_next + prof_lane, sc_n);
@@ -299,16 +306,16 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 const int ai = ai0 + k;
-                if (ai < La) {
+                if (ai < La) {   // -endweight: minus the trailing end gap of the rows below
                     const long long prio = (ai == La - 1) ? (3ll << 24) : ((2ll << 24) | ai);
-                    const long long kk = ((long long)(Mol[k] + O) << 32) | prio;
+                    const long long kk = ((long long)(Mol[k] + O - end_trail(args, La - 1 - ai)) << 32) | prio;
                     key = kk > key ? kk : key;
                 }
             }
         }
         tb_fence<MODE>();
         for (int q = lane; q < Lb - 1; q += 64) {
-            const long long kk = ((long long)lastrow[q] << 32) | ((1ll << 24) | q);
+            const long long kk = ((long long)(lastrow[q] - end_trail(args, Lb - 1 - q)) << 32) | ((1ll << 24) | q);
             key = kk > key ? kk : key;
         }
         key = wave_max_i64(key);

@@ -7,7 +7,9 @@ The reference splices the string verbatim into the ``needle`` command line
 ``-qualifier value``; booleans as ``-endweight``, ``-endweight=Y``, ``-noendweight``.
 Options that change the alignment and that the GPU path does not implement
 raise :class:`UnsupportedNeedleOption` (the reference would run needle with
-them; we refuse loudly rather than silently ignore).
+them; we refuse loudly rather than silently ignore).  ``-endweight`` with
+``-endopen`` / ``-endextend`` is implemented by the exact kernels (DESIGN.md 2.9;
+parity vs EMBOSS unpinned: CRISPResso never sets it).
 """
 from __future__ import annotations
 
@@ -85,8 +87,8 @@ class NeedleOptions:
                 raise UnsupportedNeedleOption(f"needle option -{key} is not supported by the GPU aligner")
         if o.matrix.upper() != "EDNAFULL":
             raise UnsupportedNeedleOption(f"-datafile {o.matrix}: only EDNAFULL is supported")
-        if o.end_weight:
-            raise UnsupportedNeedleOption("-endweight is not supported (needle default is off)")
+        if o.end_weight and (o.end_open < 0 or o.end_extend < 0):
+            raise UnsupportedNeedleOption("-endopen / -endextend must be non-negative")
         if o.awidth <= 0:
             raise UnsupportedNeedleOption("-awidth3 must be positive")
         return o

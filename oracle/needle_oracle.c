@@ -71,21 +71,26 @@ static const char* opt_value(int argc, char** argv, int* i, const char* key) {
 
 int main(int argc, char** argv) {
     const char *afile = NULL, *bfile = NULL, *ofile = "stdout";
-    float gapopen = 10.0f, gapextend = 0.5f;
+    float gapopen = 10.0f, gapextend = 0.5f, endopen = 10.0f, endextend = 0.5f;
+    int endweight = 0;
     for (int i = 1; i < argc; i++) {
         const char* v;
+        if (strcmp(argv[i], "-endweight") == 0) { endweight = 1; continue; }
+        if (strcmp(argv[i], "-noendweight") == 0) { endweight = 0; continue; }
         if ((v = opt_value(argc, argv, &i, "asequence"))) afile = v;
         else if ((v = opt_value(argc, argv, &i, "bsequence"))) bfile = v;
         else if ((v = opt_value(argc, argv, &i, "outfile"))) ofile = v;
         else if ((v = opt_value(argc, argv, &i, "gapopen"))) gapopen = strtof(v, NULL);
         else if ((v = opt_value(argc, argv, &i, "gapextend"))) gapextend = strtof(v, NULL);
+        else if ((v = opt_value(argc, argv, &i, "endopen"))) endopen = strtof(v, NULL);
+        else if ((v = opt_value(argc, argv, &i, "endextend"))) endextend = strtof(v, NULL);
         else if ((v = opt_value(argc, argv, &i, "awidth3"))) (void)v;
         else if (strcmp(argv[i], "-auto") == 0 || strcmp(argv[i], "-stdout") == 0) continue;
         else { fprintf(stderr, "needle_oracle: unsupported option %s\n", argv[i]); return 1; }
     }
     if (!afile || !bfile) { fprintf(stderr, "needle_oracle: -asequence and -bsequence required\n"); return 1; }
     oracle_params P;
-    if (oracle_params_init(&P, gapopen, gapextend)) {
+    if (oracle_params_init_end(&P, gapopen, gapextend, endweight, endopen, endextend)) {
         fprintf(stderr, "needle_oracle: penalties not representable\n");
         return 1;
     }

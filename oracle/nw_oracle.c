@@ -24,6 +24,12 @@
  *  - Free end gaps (needle -endweight defaults to false; CRISPResso never sets it):
  *    row 0 / column 0 hold M = 0, X = Y = -inf.  This reproduces EMBOSS's first
  *    row/column initialisation (m = match, ix/iy = -gapopen).
+ *  - -endweight (PARITY UNPINNED): an end gap of k residues costs
+ *    endopen + (k-1) * endextend.  Leading: row 0 / column 0 hold M = -(endopen +
+ *    (k-1) * endextend) for the k residues before the cell (M[0][0] = 0); trailing:
+ *    the start-cell scan compares M of a last-column cell minus the penalty of the
+ *    la - i amplicon residues after it (last row: lb - j read residues), and that
+ *    penalised value is the reported score.
  *  - The walk starts at the best M cell of the last row or last column
  *    (scan: corner, then last column bottom->top, then last row right->left,
  *    strict >); the unmatched tail is emitted as end gaps first, the unmatched
@@ -80,19 +86,33 @@ int oracle_sub(int ca, int cb) {
     return kEdnaFull[ca][cb];
 }
 
-int oracle_params_init(oracle_params* p, float gap_open, float gap_extend) {
+int oracle_params_init_end(oracle_params* p, float gap_open, float gap_extend, int end_weight, float end_open,
+                           float end_extend) {
     for (int scale = 1; scale <= 64; scale *= 2) {
         double o = (double)gap_open * scale, e = (double)gap_extend * scale;
-        if (o == floor(o) && e == floor(e)) {
+        double eo = end_weight ? (double)end_open * scale : 0.0, ee = end_weight ? (double)end_extend * scale : 0.0;
+        if (o == floor(o) && e == floor(e) && eo == floor(eo) && ee == floor(ee)) {
             p->scale = scale;
             p->gap_open = (int32_t)o;
             p->gap_extend = (int32_t)e;
             p->gap_open_f = gap_open;
             p->gap_extend_f = gap_extend;
+            p->end_weight = end_weight != 0;
+            p->end_open = (int32_t)eo;
+            p->end_extend = (int32_t)ee;
             return 0;
         }
     }
     return -1;
+}
+
+int oracle_params_init(oracle_params* p, float gap_open, float gap_extend) {
+    return oracle_params_init_end(p, gap_open, gap_extend, 0, 10.0f, 0.5f);
+}
+
+/* Penalty of an end gap of k residues (0 without -endweight). */
+static inline int32_t end_gap(const oracle_params* p, int32_t k) {
+    return (p->end_weight && k > 0) ? p->end_open + (k - 1) * p->end_extend : 0;
 }
 
 #define NEG_INF (-(1 << 28))
@@ -132,10 +152,10 @@ static void fill(const int* ca, int32_t la, const int* cb, int32_t lb,
     const int64_t W = lb + 1;
     const int32_t O = p->gap_open, E = p->gap_extend, S = p->scale;
     int32_t *M = d->M, *X = d->X, *Y = d->Y;
-    for (int32_t j = 0; j <= lb; j++) { M[j] = 0; X[j] = NEG_INF; Y[j] = NEG_INF; }
+    for (int32_t j = 0; j <= lb; j++) { M[j] = -end_gap(p, j); X[j] = NEG_INF; Y[j] = NEG_INF; }
     for (int32_t i = 1; i <= la; i++) {
         int64_t r = i * W, u = r - W;
-        M[r] = 0; X[r] = NEG_INF; Y[r] = NEG_INF;
+        M[r] = -end_gap(p, i); X[r] = NEG_INF; Y[r] = NEG_INF;
         const signed char* srow = kEdnaFull[ca[i - 1] < 16 ? ca[i - 1] : 0];
         const int unk_a = ca[i - 1] > 15;
         for (int32_t j = 1; j <= lb; j++) {
@@ -154,18 +174,20 @@ static void fill(const int* ca, int32_t la, const int* cb, int32_t lb,
 
 /* Start cell: corner, then last column bottom->top, then last row right->left,
  * first strict maximum wins. */
-static void pick_end(const dp_mats* d, int32_t la, int32_t lb, int32_t* ei, int32_t* ej) {
+static int32_t pick_end(const dp_mats* d, int32_t la, int32_t lb, const oracle_params* p, int32_t* ei,
+                        int32_t* ej) {
     const int64_t W = lb + 1;
     int32_t bi = la, bj = lb, best = d->M[la * W + lb];
     for (int32_t i = la - 1; i >= 1; i--) {
-        int32_t v = d->M[i * W + lb];
+        int32_t v = d->M[i * W + lb] - end_gap(p, la - i);
         if (v > best) { best = v; bi = i; bj = lb; }
     }
     for (int32_t j = lb - 1; j >= 1; j--) {
-        int32_t v = d->M[la * W + j];
+        int32_t v = d->M[la * W + j] - end_gap(p, lb - j);
         if (v > best) { best = v; bi = la; bj = j; }
     }
     *ei = bi; *ej = bj;
+    return best;
 }
 
 int32_t oracle_score(const char* a, int32_t la, const char* b, int32_t lb,
@@ -179,8 +201,7 @@ int32_t oracle_score(const char* a, int32_t la, const char* b, int32_t lb,
     if (mats_reserve(&d, (int64_t)(la + 1) * (lb + 1))) { free(ca); free(cb); return NEG_INF; }
     fill(ca, la, cb, lb, p, &d);
     int32_t ei, ej;
-    pick_end(&d, la, lb, &ei, &ej);
-    int32_t s = d.M[(int64_t)ei * (lb + 1) + ej];
+    const int32_t s = pick_end(&d, la, lb, p, &ei, &ej);
     mats_free(&d); free(ca); free(cb);
     return s;
 }
@@ -194,7 +215,7 @@ static int align_with(const char* a, int32_t la, const int* ca, const char* b,
     const int64_t W = lb + 1;
     const int32_t O = p->gap_open, E = p->gap_extend;
     int32_t ei, ej;
-    pick_end(d, la, lb, &ei, &ej);
+    const int32_t best = pick_end(d, la, lb, p, &ei, &ej);
 
     /* Columns are produced end -> start into the tail of the buffers. */
     const int32_t cap = la + lb;
@@ -250,7 +271,7 @@ static int align_with(const char* a, int32_t la, const int* ca, const char* b,
     out->n_ident = ident;
     out->n_sim = sim;
     out->n_gaps = gaps;
-    out->score = d->M[(int64_t)ei * W + ej];
+    out->score = best;
     out->end_i = ei;
     out->end_j = ej;
     out->read_end = nb;

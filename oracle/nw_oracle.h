@@ -39,6 +39,13 @@ typedef struct {
     int32_t gap_extend;  /* scaled */
     float gap_open_f;    /* as given, for the report header */
     float gap_extend_f;
+    /* needle -endweight / -endopen / -endextend (EMBOSS defaults N / 10.0 / 0.5):
+     * with end_weight, an end gap of k residues costs end_open + (k-1) * end_extend
+     * (scaled) instead of nothing.  PARITY UNPINNED: CRISPResso never sets these, the
+     * reference holds no output made with them, and EMBOSS is absent. */
+    int32_t end_weight;
+    int32_t end_open;    /* scaled */
+    int32_t end_extend;  /* scaled */
 } oracle_params;
 
 typedef struct {
@@ -60,6 +67,9 @@ int oracle_sub(int ca, int cb);
 
 /* Derive scale/open/extend from EMBOSS float penalties. 0 ok, -1 inexact. */
 int oracle_params_init(oracle_params* p, float gap_open, float gap_extend);
+/* The same with -endweight / -endopen / -endextend (one scale for all four). */
+int oracle_params_init_end(oracle_params* p, float gap_open, float gap_extend, int end_weight, float end_open,
+                           float end_extend);
 
 /* Align read b (columns) against amplicon a (rows).  The three output buffers
  * must hold la+lb+1 bytes; they are NUL-terminated.  Returns 0, or -1 when

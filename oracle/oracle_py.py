@@ -21,7 +21,8 @@ CLI = os.path.join(BUILD, "needle_oracle")
 
 class OracleParams(ctypes.Structure):
     _fields_ = [("scale", c_int32), ("gap_open", c_int32), ("gap_extend", c_int32),
-                ("gap_open_f", c_float), ("gap_extend_f", c_float)]
+                ("gap_open_f", c_float), ("gap_extend_f", c_float), ("end_weight", c_int32),
+                ("end_open", c_int32), ("end_extend", c_int32)]
 
 
 class OracleResult(ctypes.Structure):
@@ -48,6 +49,8 @@ def load():
     lib = ctypes.CDLL(LIB)
     lib.oracle_params_init.argtypes = [POINTER(OracleParams), c_float, c_float]
     lib.oracle_params_init.restype = c_int
+    lib.oracle_params_init_end.argtypes = [POINTER(OracleParams), c_float, c_float, c_int, c_float, c_float]
+    lib.oracle_params_init_end.restype = c_int
     lib.oracle_align.argtypes = [c_char_p, c_int32, c_char_p, c_int32, POINTER(OracleParams),
                                  POINTER(OracleResult), c_void_p, c_void_p, c_void_p]
     lib.oracle_align.restype = c_int
@@ -67,9 +70,11 @@ def load():
     return lib
 
 
-def params(gap_open: float = 10.0, gap_extend: float = 0.5) -> OracleParams:
+def params(gap_open: float = 10.0, gap_extend: float = 0.5, end_weight: bool = False, end_open: float = 10.0,
+           end_extend: float = 0.5) -> OracleParams:
     p = OracleParams()
-    if load().oracle_params_init(ctypes.byref(p), gap_open, gap_extend) != 0:
+    if load().oracle_params_init_end(ctypes.byref(p), gap_open, gap_extend, int(bool(end_weight)), end_open,
+                                     end_extend) != 0:
         raise ValueError("penalties not representable")
     return p
 

@@ -32,8 +32,8 @@ def kernel(request, monkeypatch):
 FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j")
 
 
-def assert_same(oracle, amplicon, buf, offsets, batch, label=""):
-    res, aln = oracle.align_batch(amplicon, buf, offsets, nthreads=8)
+def assert_same(oracle, amplicon, buf, offsets, batch, label="", params=None):
+    res, aln = oracle.align_batch(amplicon, buf, offsets, params, nthreads=8)
     n = len(offsets) - 1
     assert len(batch) == n
     lens = np.diff(offsets)
@@ -208,6 +208,34 @@ def test_long_amplicons(gpu_aligner_factory, oracle, monkeypatch, La, mode):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"long La={La}")
+
+
+@pytest.mark.parametrize("mode", ["ops", "rows"])
+@pytest.mark.parametrize("ends", [(10.0, 0.5), (3.0, 1.0), (0.5, 0.25), (40.0, 0.0)])
+@pytest.mark.parametrize("La", [60, 250, 1100])
+def test_endweight(gpu_aligner_factory, oracle, monkeypatch, La, ends, mode):
+    """needle -endweight -endopen -endextend: end gaps cost endopen +
+    (k-1) endextend; every read through the exact kernels (one-wave, and the multi-wave
+    kernel for an amplicon over 1024 bp) -- bit-identical to the oracle's restatement.
+    Parity vs EMBOSS itself is unpinned (CRISPResso never sets these options)."""
+    from crispresso_amd.needle_options import NeedleOptions
+
+    monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
+    eo, ee = ends
+    opts = NeedleOptions.parse(f"-gapopen=10 -gapextend=0.5 -endweight -endopen={eo} -endextend={ee}")
+    amp = synth.random_amplicon(La, 700 + La)
+    reads = [amp, amp[La // 4:], amp[: 3 * La // 4], "ACGTACGT" + amp, amp + "TTGCA", amp[10:-10],
+             amp[:La // 2] + amp[La // 2 + 7:], "ACGTRYKMSWBDHVNU", "A"]
+    sub, soff = synth.reads_from(amp, 80, La + 11, synth.PARITY_MIX)
+    reads += synth.unpack(sub, soff)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory(opts)
+    a.set_reference(amp)
+    p = oracle.params(10.0, 0.5, True, eo, ee)
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"endweight {ends} La={La}", params=p)
+    # and the free-end-gap answer differs for an overhanging read (the option is applied)
+    free = oracle.align(amp, amp[La // 4:])[0]
+    assert free["score"] != oracle.align(amp, amp[La // 4:], p)[0]["score"]
 
 
 @pytest.mark.parametrize("slots", ["0", "8", "24"])

@@ -29,7 +29,16 @@ def test_needle_option_forms(text, expect):
     assert (o.gap_open, o.gap_extend) == expect
 
 
-@pytest.mark.parametrize("text", ["-endweight", "-endweight=Y", "-datafile=EBLOSUM62", "-bogus 3", "stray"])
+def test_endweight_options():
+    o = NeedleOptions.parse("-gapopen=10 -gapextend=0.5 -endweight -endopen=3 -endextend 1.5")
+    assert (o.end_weight, o.end_open, o.end_extend) == (True, 3.0, 1.5)
+    o = NeedleOptions.parse("-endweight=N -endopen=3")
+    assert not o.end_weight
+    o = NeedleOptions.parse("-endweight=Y")
+    assert (o.end_weight, o.end_open, o.end_extend) == (True, 10.0, 0.5)   # EMBOSS defaults
+
+
+@pytest.mark.parametrize("text", ["-datafile=EBLOSUM62", "-bogus 3", "stray", "-endweight -endopen=-1"])
 def test_unsupported_needle_options_raise(text):
     with pytest.raises(UnsupportedNeedleOption):
         NeedleOptions.parse(text)
@@ -122,8 +131,8 @@ def test_needle_cli_argument_split():
 def test_needle_cli_rejects_bad_options(capsys):
     from crispresso_amd.needle_cli import main
 
-    assert main(["-asequence=a", "-bsequence=b", "-endweight"]) == 1
-    assert "endweight" in capsys.readouterr().err
+    assert main(["-asequence=a", "-bsequence=b", "-datafile=EBLOSUM62"]) == 1
+    assert "EDNAFULL" in capsys.readouterr().err
 
 
 def test_ops_to_dataframe_equals_rows_dataframe():

@@ -196,3 +196,77 @@ def test_cli_matches_library(oracle, tmp_path):
     for k, r in enumerate(reads):
         res, ra, mk, rb = oracle.align(amp, r)
         assert oracle.srspair("AMPL", f"r{k}", res, ra, mk, rb) in out
+
+
+# ---- -endweight (parity unpinned vs EMBOSS) -------------------------------
+
+def model_score_end(oracle, ra, rb, EO, EE, O=20, E=1, S=2):
+    """Score under the -endweight model: the leading and the trailing single-type gap
+    run cost EO + (k-1)EE each, every other gap run O + (k-1)E."""
+    cols = ["P" if (x != "-" and y != "-") else ("A" if y == "-" else "B") for x, y in zip(ra, rb)]
+    lo, hi, s = 0, len(cols), 0
+    for side in (0, 1):
+        q = lo if side == 0 else hi - 1
+        if lo < hi and cols[q] != "P":
+            t, k = cols[q], 0
+            while lo < hi and cols[lo if side == 0 else hi - 1] == t:
+                k += 1
+                if side == 0:
+                    lo += 1
+                else:
+                    hi -= 1
+            s -= EO + (k - 1) * EE
+    q = lo
+    while q < hi:
+        if cols[q] == "P":
+            s += S * sub(oracle, ra[q], rb[q])
+            q += 1
+        else:
+            t, k = cols[q], 0
+            while q < hi and cols[q] == t:
+                k += 1
+                q += 1
+            s -= O + (k - 1) * E
+    return s
+
+
+def brute_best_end(oracle, a, b, EO, EE):
+    best = None
+    for ra, rb in all_alignments(a, b):
+        cols = ["P" if (x != "-" and y != "-") else ("A" if y == "-" else "B") for x, y in zip(ra, rb)]
+        if "P" not in cols:
+            continue
+        last = max(k for k, c in enumerate(cols) if c == "P")
+        if len(set(cols[last + 1:])) > 1:   # the DP's start cell: a pair, then one end-gap run
+            continue
+        s = model_score_end(oracle, ra, rb, EO, EE)
+        best = s if best is None or s > best else best
+    return best
+
+
+@pytest.mark.parametrize("eo,ee", [(10.0, 0.5), (3.0, 1.0), (0.5, 0.0), (25.0, 4.0)])
+def test_endweight_brute_force_optimum(oracle, eo, ee):
+    """With -endweight the DP optimum (start-cell score) equals the best end-penalised
+    score over every column sequence the model admits; the traceback re-scores to it."""
+    p = oracle.params(10.0, 0.5, True, eo, ee)
+    EO, EE = int(eo * p.scale), int(ee * p.scale)
+    rng = np.random.Generator(np.random.PCG64(int(eo * 10 + ee)))
+    for _ in range(200):
+        la, lb = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        a = "".join(rng.choice(list("ACGTN" if rng.random() < 0.3 else "ACGT"), la))
+        b = "".join(rng.choice(list("ACGT"), lb))
+        assert oracle.score(a, b, p) == brute_best_end(oracle, a, b, EO, EE), (a, b)
+    amp = synth.random_amplicon(90, 5)
+    buf, off = synth.reads_from(amp, 120, 6, synth.PARITY_MIX)
+    for read in synth.unpack(buf, off)[:120] + [amp[20:70], amp[:40] + amp[60:], "ACGT" + amp]:
+        res, ra, mk, rb = oracle.align(amp, read, p)
+        assert ra.replace("-", "") == amp and rb.replace("-", "") == read
+        assert model_score_end(oracle, ra, rb, EO, EE) == res["score"], (read, ra, rb)
+        assert res["score"] == oracle.score(amp, read, p)
+
+
+def test_endweight_off_is_free_end_gaps(oracle):
+    p0, p1 = oracle.params(), oracle.params(10.0, 0.5, False, 3.0, 1.0)
+    amp = synth.random_amplicon(60, 8)
+    for read in [amp[10:], amp[:30], "TT" + amp + "GG"]:
+        assert oracle.align(amp, read, p0) == oracle.align(amp, read, p1)
