@@ -217,15 +217,26 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             }
             for (int c0 = 0; c0 < nd; c0 += 64) {
                 const int k4 = c0 + lane;
+                // every candidate's loads issued before any is used (branch-free: a missing
+                // candidate re-reads candidate 0, lanes past the read re-read its last dword)
+                const int kc = k4 < nd ? k4 : nd - 1;
+                uint2 w[kCand];
+                int sh[kCand];
 #pragma unroll
                 for (int t = 0; t < kCand; ++t) {
-                    if (us[t] < 0 || k4 >= nd) continue;
-                    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, us[t]);
-                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), us[t]);
+                    const int u = us[t] < 0 ? us[0] : us[t];
+                    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
                     const long long off = (long long)(((unsigned long long)hi << 32) | lo);
-                    const uint8_t* base = a.reads + (off & ~3ll) + 4 * k4;
-                    raw[t] = __builtin_amdgcn_alignbyte(ld_dw(base + 4), ld_dw(base), (int)(off & 3));
-                    diff[t] |= ((raw[t] | 0x20202020u) ^ amp_sh[k4]) & (k4 == nd - 1 ? tail_mask : 0xffffffffu);
+                    w[t] = *(const uint2*)(a.reads + (off & ~3ll) + 4 * kc);   // 4-aligned dwordx2
+                    sh[t] = (int)(off & 3);
+                }
+                const unsigned am = k4 < nd ? amp_sh[kc] : 0u;
+                const unsigned msk = k4 < nd ? (k4 == nd - 1 ? tail_mask : 0xffffffffu) : 0u;
+#pragma unroll
+                for (int t = 0; t < kCand; ++t) {
+                    raw[t] = __builtin_amdgcn_alignbyte(w[t].y, w[t].x, sh[t]);
+                    diff[t] |= ((raw[t] | 0x20202020u) ^ am) & msk;
                 }
             }
 #pragma unroll
