@@ -46,12 +46,16 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md "Wave scheduling")
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
+# measured issue rate of the 8-byte VOP3 / VOP3P / DPP encodings the fill is made of:
+# 0.224 wave-instructions per SIMD per nominal 2.4 GHz cycle (scripts/ubench/issue_rate.hip,
+# profiles/r02_ubench/ubench_issue_rate.txt)
+VALU_ISSUE_MEASURED = 1024 * 2.4e9 * 0.224
 READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
 # VALU instruction count per fill launch (newest first)
 PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
-                 for d in ("r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
+                 for d in ("r02_v3", "r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
 AMPLICON_LEN = 250
 
 
@@ -617,10 +621,16 @@ def main():
                     "valu_source": summ_src,
                     "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
                     "issue_peak_per_s": VALU_ISSUE_PEAK,
+                    "issue_frac_measured_ceiling": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_MEASURED)
+                    if fill_valu and fill_ms else None,
+                    "issue_measured_ceiling_per_s": VALU_ISSUE_MEASURED,
                     "band_cells_per_pass": cells,
                     "band_gcups": cells / (kms * 1e-3) / 1e9,
                     "note": "issue_frac = SQ_INSTS_VALU of one fill<16> launch (PMC, chip total) / its live HIP-event "
-                            "time / (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); band cells = "
+                            "time / (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); "
+                            "issue_frac_measured_ceiling: the same over the measured issue rate of the VOP3/VOP3P/"
+                            "DPP encodings the fill is made of (0.224 per SIMD per cycle, profiles/r02_ubench); "
+                            "band cells = "
                             "cells the bands and the exact kernel actually compute (W x (La + Lb)/2 per read and "
                             "level), not the La x Lb matrices the certificate makes unnecessary",
                 },
