@@ -72,7 +72,20 @@ def dist_setup():
 
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    dist.init_process_group("gloo")
+    # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (several ranks share a device)
+    if os.environ.get("CRISPR_BENCH_DEVICES"):
+        local %= max(1, int(os.environ["CRISPR_BENCH_DEVICES"]))
+    # gloo prints its connection report on the C stdout: keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     return rank, local, world, dist
 
 
