@@ -142,6 +142,7 @@ struct nw_ctx {
     int exact_grid = 0, exact_lds = 0;
     bool exact_tb_lds = true;
     bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
+    bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
@@ -429,6 +430,13 @@ int configure(nw_ctx* c) {
             cfg.lds_bytes = b;
             break;
         }
+    }
+    // traceback in HBM instead of LDS (more wavefronts per CU for a bulk exact list) measured
+    // no faster on the HDR pass (the kernel is VALU-issue bound there): diagnostics only
+    const char* tbe = std::getenv("CRISPR_NW_EXACT_TB");   // "global"
+    if (cfg.tb_mode == nw::TB_LDS_FULL && tbe && std::strcmp(tbe, "global") == 0) {
+        cfg.tb_mode = nw::TB_GLOBAL_FULL;
+        cfg.wpb = 4;
     }
     if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, 0, cfg.wpb);
     if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
@@ -846,7 +854,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
         // ranges to the device-side counts.
-        const bool two = c->diag16_fill.grid > 0;
+        const bool two = c->diag16_fill.grid > 0 && !c->skip16;
         // CRISPR_NW_LEVELS=16: the first level's give-ups go straight to the exact kernel
         const char* lv = std::getenv("CRISPR_NW_LEVELS");
         const bool only16 = two && lv && std::strcmp(lv, "16") == 0;
@@ -985,7 +993,8 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     cnt.passes = (c->use_stream && !c->use_diag) ? (int)std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     if (c->use_diag && c->n > 0) {
         cnt.band = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-        if (c->diag16_fill.grid > 0) cnt.redo = c->s->d_fallback_count.p + 2;
+        // second-level reads; a chunk run on the 32-diagonal level alone counts all its DP reads there
+        if (c->diag16_fill.grid > 0) cnt.redo = c->skip16 ? cnt.band : c->s->d_fallback_count.p + 2;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n, c->s->d_blk.p,
@@ -1472,7 +1481,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
     const int64_t nchunks = (int64_t)chunks.size();
+    c->skip16 = false;
+    const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
+    const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
     auto restore = [&](int code) {
+        c->skip16 = false;
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1565,6 +1578,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         any_diag = any_diag || c->use_diag;
+        // adaptive first level: when most of the DP reads of the chunks done so far needed the
+        // 32-diagonal level (e.g. the HDR pass: a 10-bp block substitution costs two 10-bp gaps
+        // or 10 mismatches, beyond what 16 diagonals certify), the next chunks skip the
+        // 16-diagonal level (its fill and walk would be spent on reads it hands on)
+        if (adaptive && k >= lag + 1 && !groups) {
+            const int64_t* h = c->h_ctl + nw::kOpsCtl * (k - lag - 1);   // synchronised in copy_runs
+            c->skip16 = h[6] >= 4096 && 2 * h[5] > h[6];
+        }
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr)))
             return restore(rc);

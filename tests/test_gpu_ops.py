@@ -276,3 +276,29 @@ def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk):
     a.set_reference(hdr)
     again = a.align_ops(None, off, resident=True)
     assert_same(oracle, hdr, buf, off0, again.expand(hdr, full, off), "packed-resident")
+
+
+def test_adaptive_first_level_hdr_pass(gpu_aligner_factory, oracle, monkeypatch):
+    """The HDR pass (most DP reads need the 32-diagonal level): after the first chunks
+    the pipeline skips the 16-diagonal level; records and runs are unchanged (same as
+    with both levels on every chunk, CRISPR_NW_ADAPT=0) and bit-identical to the oracle."""
+    amp, hdr, buf, off = synth.c3_workload(24000)
+    monkeypatch.setenv("CRISPR_NW_CHUNK", "2048")
+    a = gpu_aligner_factory()
+    a.set_reference(hdr)
+    ob = a.align_ops(buf, off)
+    paths = a.path_counts()
+    assert paths["band32"] > paths["band16"] // 2   # the skipped chunks count their DP reads on level 2
+    monkeypatch.setenv("CRISPR_NW_ADAPT", "0")
+    both = a.align_ops(buf, off)
+    for f in FIELDS + ("flags",):
+        assert np.array_equal(ob.stats[f], both.stats[f])
+    assert np.array_equal(ob.ops, both.ops) and np.array_equal(ob.ops_off, both.ops_off)
+    sel = np.arange(0, len(off) - 1, 7)
+    sb, so = pack_reads([bytes(buf[off[i]:off[i + 1]]).decode() for i in sel])
+    runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in sel]
+    roff = np.zeros(len(sel) + 1, np.int64)
+    roff[1:] = np.cumsum([len(r) for r in runs])
+    from crispresso_amd.aligner import OpsBatch
+    sub = OpsBatch(ob.stats[sel], np.concatenate(runs), roff, np.diff(so), ob.scale)
+    assert_same(oracle, hdr, sb, so, sub.expand(hdr, sb, so), "adaptive-hdr")
