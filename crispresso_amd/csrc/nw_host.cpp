@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cctype>
 #include <cmath>
 #include <cstdarg>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "../../include/crispr_nw.h"
+#include "host_pool.h"
 #include "nw_device.h"
 #include "nw_edna.h"
 
@@ -108,6 +110,10 @@ struct nw_ctx {
     // reference
     std::string ref;
     DevBuf<uint8_t> d_arena;          // every amplicon's tables (upload_profiles)
+    // what d_arena / the shared tables hold (a repeated pooled call reuses them)
+    std::vector<std::string> arena_refs;
+    std::vector<Profile> arena_profs;
+    std::string arena_key, shared_key;
     Profile cur{};                    // the amplicon being aligned
     DevBuf<uint8_t> d_lut6, d_lut;
     // batch
@@ -275,6 +281,9 @@ bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
 // ascii -> EDNAFULL code, and the certified-band score table [amplicon code][read A
 // code][read B code] over A T G C N pad, packed int16x2 + 2 * extend.
 int upload_shared(nw_ctx* c) {
+    const std::string key = std::to_string(c->scale) + "/" + std::to_string(c->gap_extend);
+    if (key == c->shared_key && c->d_sub16.p) return NW_OK;
+    c->shared_key.clear();
     const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
     std::vector<uint8_t> lut6(256), lut(256);
     for (int q = 0; q < 256; ++q) {
@@ -310,11 +319,20 @@ int upload_shared(nw_ctx* c) {
     HIP_OR_FAIL(c, hipMemcpy(c->d_lut6.p, lut6.data(), 256, hipMemcpyHostToDevice));
     HIP_OR_FAIL(c, hipMemcpy(c->d_lut.p, lut.data(), 256, hipMemcpyHostToDevice));
     HIP_OR_FAIL(c, hipMemcpy(c->d_btab.p, btab.data(), btab.size() * 4, hipMemcpyHostToDevice));
+    c->shared_key = key;
     return NW_OK;
 }
 
 // Every amplicon's tables in one device arena (one upload): profs[g] points into it.
 int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector<Profile>* profs) {
+    // the tables depend on the amplicons, the scaled extend penalty and the pair-table switch
+    const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
+    const std::string key = std::to_string(c->scale) + "/" + std::to_string(c->gap_extend) + "/" + (pt ? pt : "");
+    if (key == c->arena_key && refs == c->arena_refs && c->d_arena.p) {
+        *profs = c->arena_profs;
+        return NW_OK;
+    }
+    c->arena_key.clear();
     std::vector<AmpTables> tabs(refs.size());
     size_t total = 0;
     auto sec = [&](size_t bytes) {
@@ -361,6 +379,9 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         p.amp_in_table = tabs[g].amp_in_table;
         p.have_ptab = tabs[g].have_ptab && p.ptab;
     }
+    c->arena_refs = refs;
+    c->arena_profs = *profs;
+    c->arena_key = key;
     return NW_OK;
 }
 
@@ -1347,6 +1368,60 @@ int nw_batch_download_ops(nw_ctx* c, uint32_t* ops_out, int64_t ops_cap, int64_t
 
 namespace {
 
+// CRISPR_NW_HOST_TIMING=1: where a pipelined call's host time goes (stderr; diagnostics)
+struct HostTimer {
+    bool on = false;
+    const char* what;
+    double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // ops_call: scan, configure, setup, uploads, launch, wait, sync
+    std::chrono::steady_clock::time_point t0, last;
+    explicit HostTimer(const char* w) : what(w) {
+        const char* e = std::getenv("CRISPR_NW_HOST_TIMING");
+        on = e && std::strcmp(e, "1") == 0;
+        t0 = last = std::chrono::steady_clock::now();
+    }
+    void lap(int k) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        t[k] += std::chrono::duration<double, std::milli>(now - last).count();
+        last = now;
+    }
+    ~HostTimer() {
+        if (!on) return;
+        t[7] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "nw host ms (%s): %.2f %.2f %.2f %.2f %.2f %.2f %.2f total %.2f\n", what, t[0], t[1], t[2],
+                     t[3], t[4], t[5], t[6], t[7]);
+    }
+};
+
+// What configure() decides for one amplicon (launch configurations, path choice,
+// geometry): a pooled call configures every group once up front and restores these
+// per chunk instead of re-running configure (its occupancy queries are host API calls).
+struct CfgState {
+    nw::LaunchCfg cfg, band_cfg, diag_fill, diag_walk, diag16_fill, diag16_walk, stream_fill, stream_walk;
+    bool use_band, use_diag, use_stream, exact_tb_lds, exact_full;
+    int exact_grid, exact_lds, diag_words, diag_lb_cap, diag_sort_grid, band_slots, stream_slots;
+    int64_t exact_slab, diag16_pass_pairs, diag16_stride, diag_pass_pairs, diag_stride, pass_reads, stride;
+    nw::StreamRegion region;
+};
+CfgState save_cfg(const nw_ctx* c) {
+    return CfgState{c->cfg, c->band_cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->stream_fill,
+                    c->stream_walk, c->use_band, c->use_diag, c->use_stream, c->exact_tb_lds, c->exact_full,
+                    c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap, c->diag_sort_grid, c->band_slots,
+                    c->stream_slots, c->exact_slab, c->diag16_pass_pairs, c->diag16_stride, c->diag_pass_pairs,
+                    c->diag_stride, c->pass_reads, c->stride, c->region};
+}
+void load_cfg(nw_ctx* c, const CfgState& st) {
+    c->cfg = st.cfg; c->band_cfg = st.band_cfg; c->diag_fill = st.diag_fill; c->diag_walk = st.diag_walk;
+    c->diag16_fill = st.diag16_fill; c->diag16_walk = st.diag16_walk; c->stream_fill = st.stream_fill;
+    c->stream_walk = st.stream_walk; c->use_band = st.use_band; c->use_diag = st.use_diag;
+    c->use_stream = st.use_stream; c->exact_tb_lds = st.exact_tb_lds; c->exact_full = st.exact_full;
+    c->exact_grid = st.exact_grid; c->exact_lds = st.exact_lds; c->diag_words = st.diag_words;
+    c->diag_lb_cap = st.diag_lb_cap; c->diag_sort_grid = st.diag_sort_grid; c->band_slots = st.band_slots;
+    c->stream_slots = st.stream_slots; c->exact_slab = st.exact_slab; c->diag16_pass_pairs = st.diag16_pass_pairs;
+    c->diag16_stride = st.diag16_stride; c->diag_pass_pairs = st.diag_pass_pairs; c->diag_stride = st.diag_stride;
+    c->pass_reads = st.pass_reads; c->stride = st.stride; c->region = st.region;
+}
+
 // 2-bit packed batch (nw_align_ops_packed): bases by batch position, exceptions ascending.
 struct PackedInput {
     const uint8_t* packed;
@@ -1370,6 +1445,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
              int64_t* ops_off, nw_stat* stats, bool upload, const Groups* groups = nullptr,
              const PackedInput* pk = nullptr) {
     if (!c) return NW_E_INVALID;
+    HostTimer ht("scan configure setup uploads launch wait sync");
     if (!groups && c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || (upload && !reads && !(pk && pk->packed)) || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
@@ -1379,12 +1455,28 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return fail(c, NW_E_STATE, "no resident batch of these %lld reads (nw_align_ops uploads one)", (long long)n);
     if (upload) c->resident_ok = false;
     (void)hipSetDevice(c->device);
-    // longest / shortest read: one vectorisable pass (the exact read is found only on error)
+    // longest / shortest read: a vectorisable pass, split over the host pool for large
+    // batches (memory-bound; the exact read is found only on error)
     int64_t mx = 1, mn = 0;
-    for (int64_t r = 0; r < n; ++r) {
-        const int64_t len = offsets[r + 1] - offsets[r];
-        mx = len > mx ? len : mx;
-        mn = len < mn ? len : mn;
+    {
+        nw_host::Pool& pool = nw_host::Pool::get();
+        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 17));
+        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
+        pool.run(parts, [&](int q) {
+            int64_t lo, hi, a = 1, b = 0;
+            nw_host::Pool::range(n, parts, q, &lo, &hi);
+            for (int64_t r = lo; r < hi; ++r) {
+                const int64_t len = offsets[r + 1] - offsets[r];
+                a = len > a ? len : a;
+                b = len < b ? len : b;
+            }
+            pmx[(size_t)q] = a;
+            pmn[(size_t)q] = b;
+        });
+        for (int q = 0; q < parts; ++q) {
+            mx = std::max(mx, pmx[(size_t)q]);
+            mn = std::min(mn, pmn[(size_t)q]);
+        }
     }
     if (mn < 0 || mx > (1 << 20))
         for (int64_t r = 0; r < n; ++r) {
@@ -1393,6 +1485,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                 return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
         }
     const int32_t lb_max = (int32_t)mx;
+    ht.lap(0);
     int64_t chunk = 262144;
     if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
     chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
@@ -1442,6 +1535,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // launch configuration of a chunk: configure() for its amplicon group once (grids sized
     // for a full chunk also serve a shorter last chunk: the kernels clamp to the counts)
     int configured = -1;
+    std::vector<CfgState> gcfg;        // per group, from the dry pass (pooled calls)
+    std::vector<char> have_cfg((size_t)ngroups, 0);
+    if (groups) gcfg.resize((size_t)ngroups);
     auto use_group = [&](int g, int64_t reads_in_chunk) {
         if (g == configured) {
             c->n = reads_in_chunk;
@@ -1450,6 +1546,12 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (groups) {
             c->ref = (*groups->refs)[(size_t)g];
             c->cur = (*groups->profs)[(size_t)g];
+            if (have_cfg[(size_t)g]) {   // restored, not re-derived (buffers were sized by the dry pass)
+                load_cfg(c, gcfg[(size_t)g]);
+                c->n = reads_in_chunk;
+                configured = g;
+                return (int)NW_OK;
+            }
         }
         c->stride = stride_for((int)c->ref.size(), lb_max);
         c->n = std::max(reads_in_chunk, std::min<int64_t>(chunk, n));
@@ -1471,11 +1573,16 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         for (int g = 0; g < ngroups && !rc; ++g) {
             const int64_t gn = groups ? (*groups->first)[(size_t)g + 1] - (*groups->first)[(size_t)g] : n;
             if (gn > 0 || ngroups == 1) rc = use_group(g, std::max<int64_t>(1, std::min(chunk, gn)));
+            if (!rc && groups && si == nsets - 1 && gn > 0) {   // every set's buffers sized: keep the decisions
+                gcfg[(size_t)g] = save_cfg(c);
+                have_cfg[(size_t)g] = 1;
+            }
         }
         if (!rc) rc = ops_reserve(c, chunk, n);
         if (!rc && c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
             rc = fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n);
     }
+    ht.lap(1);
     if (ngroups > 1) configured = -1;   // the pipeline configures each group again
     c->s = &c->sc[0];
     const int64_t base0 = n ? offsets[0] : 0;
@@ -1506,6 +1613,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
         return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
     if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
+    ht.lap(2);
     if (upload) c->reads_bias = pk ? (base0 & ~(int64_t)15) : base0;
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
     // every upload queued up front: the copy engine streams the batch while chunks compute
@@ -1538,11 +1646,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
         HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
     }
+    ht.lap(3);
     int64_t total = 0, err = 0;
     bool cap_short = false;
     // chunk k's runs: once its total is known on the host
     auto copy_runs = [&](int64_t k) -> int {
+        ht.lap(4);
         HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
+        ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
         err |= h[3];
         const int64_t cb = h[1], tot = h[2];
@@ -1605,7 +1716,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     }
     for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k)
         if ((rc = copy_runs(k))) return restore(rc);
+    ht.lap(4);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
+    ht.lap(6);
     ops_off[n] = total;
     if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)
         const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);
@@ -1675,6 +1788,7 @@ int multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n
               const int64_t* offsets, const int32_t* ref_of_read, int64_t n, uint32_t* ops_out, int64_t ops_cap,
               int64_t* ops_off, nw_stat* stats, const PackedInput* pk) {
     if (!c) return NW_E_INVALID;
+    HostTimer ht("index-scan tables");
     if (n_refs <= 0 || !refs || !ref_offsets) return fail(c, NW_E_INVALID, "no amplicons");
     if (n < 0 || (n > 0 && (!(reads || pk) || !offsets || !ref_of_read || !stats)) || !ops_off)
         return fail(c, NW_E_INVALID, "bad batch");
@@ -1685,19 +1799,48 @@ int multi_ops(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n
         amps[(size_t)g].assign(refs + ref_offsets[g], refs + ref_offsets[g + 1]);
     }
     (void)hipSetDevice(c->device);
+    // reads per amplicon and whether the reads come grouped: per part of the host pool
+    // (memory-bound), a bad index located afterwards
     std::vector<int64_t> first((size_t)n_refs + 1, 0);
     bool grouped = true;
-    for (int64_t r = 0; r < n; ++r) {
-        const int32_t g = ref_of_read[r];
-        if (g < 0 || g >= n_refs) return fail(c, NW_E_INVALID, "read %lld has amplicon index %d", (long long)r, g);
-        ++first[(size_t)g + 1];
-        grouped = grouped && (r == 0 || g >= ref_of_read[r - 1]);
+    {
+        nw_host::Pool& pool = nw_host::Pool::get();
+        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 17));
+        std::vector<std::vector<int64_t>> cnt((size_t)parts);
+        std::vector<char> pbad((size_t)parts, 0), psorted((size_t)parts, 1);
+        pool.run(parts, [&](int q) {
+            int64_t lo, hi;
+            nw_host::Pool::range(n, parts, q, &lo, &hi);
+            std::vector<int64_t>& h = cnt[(size_t)q];
+            h.assign((size_t)n_refs + 1, 0);
+            uint32_t bad = 0, desc = 0;
+            for (int64_t r = lo; r < hi; ++r) {
+                const int32_t g = ref_of_read[r];
+                const bool out = (uint32_t)g >= (uint32_t)n_refs;
+                bad |= out;
+                ++h[out ? (size_t)n_refs : (size_t)g];
+                desc |= r > lo && g < ref_of_read[r - 1];
+            }
+            pbad[(size_t)q] = bad != 0;
+            psorted[(size_t)q] = desc == 0 && (lo == 0 || hi == lo || ref_of_read[lo] >= ref_of_read[lo - 1]);
+        });
+        for (int q = 0; q < parts; ++q)
+            if (pbad[(size_t)q])
+                for (int64_t r = 0; r < n; ++r)
+                    if ((uint32_t)ref_of_read[r] >= (uint32_t)n_refs)
+                        return fail(c, NW_E_INVALID, "read %lld has amplicon index %d", (long long)r, ref_of_read[r]);
+        for (int q = 0; q < parts; ++q) {
+            grouped = grouped && psorted[(size_t)q];
+            for (int32_t g = 0; g < n_refs; ++g) first[(size_t)g + 1] += cnt[(size_t)q][(size_t)g];
+        }
     }
     for (int32_t g = 0; g < n_refs; ++g) first[(size_t)g + 1] += first[(size_t)g];
+    ht.lap(0);
     int rc = upload_shared(c);
     std::vector<Profile> profs;
     if (!rc) rc = upload_profiles(c, amps, &profs);
     if (rc) return rc;
+    ht.lap(1);
     c->ref.clear();   // the context has no single amplicon afterwards (nw_set_reference again)
     c->cur = Profile{};
     Groups grp{&amps, &profs, &first};
