@@ -1740,6 +1740,15 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
             c->ops_compute_ms += ms;
         }
+        if (ht.on)   // per chunk (ms from the first upload): upload done, compute start, compute end
+            for (int64_t k = 0; k < nchunks; ++k) {
+                float a = 0, b = 0, e = 0;
+                if (upload) (void)hipEventElapsedTime(&a, c->ev_h0, c->ev_in[(size_t)k]);
+                (void)hipEventElapsedTime(&b, c->ev_h0, c->ev_cs[(size_t)k]);
+                (void)hipEventElapsedTime(&e, c->ev_h0, c->ev_ce[(size_t)k]);
+                std::fprintf(stderr, "  chunk %lld [%lld reads]: in %.3f start %.3f end %.3f\n", (long long)k,
+                             (long long)(chunks[(size_t)k].hi - chunks[(size_t)k].lo), a, b, e);
+            }
     }
     c->resident_ok = true;   // the batch stays in HBM for nw_align_ops_resident
     c->resident_n = n;

@@ -1,0 +1,57 @@
+"""In-process A/B of the headline call (nw_align_ops_packed, C2 1M reads) under two settings
+of env knobs the library reads per call: calls alternate A, B, A, B ... so that box-level
+drift (PCIe, host load) hits both alike.
+Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds]   (an empty string = defaults)"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from crispresso_amd import _lib, synth  # noqa: E402
+from crispresso_amd.aligner import GpuAligner, pack_2bit  # noqa: E402
+
+
+def parse(spec):
+    return dict(kv.split("=", 1) for kv in spec.split(",") if kv)
+
+
+A, B = parse(sys.argv[1]), parse(sys.argv[2])
+rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+nr = bench.READS_PER_GPU
+amplicon = synth.random_amplicon(bench.AMPLICON_LEN, 1)
+buf, off = synth.reads_from(amplicon, nr, 2)
+pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
+stats = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
+ops_off = _lib.PinnedBuffer(nr + 1, np.int64)
+ops = _lib.PinnedBuffer(4 * nr + 4096, np.uint32)
+p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
+pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
+al = GpuAligner(0)
+al.set_reference(amplicon)
+keys = set(A) | set(B)
+times = {"A": [], "B": []}
+ref = None
+for i in range(2 * rounds + 4):
+    which = "A" if i % 2 == 0 else "B"
+    for k in keys:
+        os.environ.pop(k, None)
+    os.environ.update(A if which == "A" else B)
+    t0 = time.perf_counter()
+    al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
+    dt = time.perf_counter() - t0
+    if i >= 4:
+        times[which].append(dt * 1e3)
+    out = (stats.array.tobytes(), ops_off.array.tobytes())
+    if ref is None:
+        ref = out
+    elif out != ref:
+        print("OUTPUT DIFFERS at call", i, which)
+        sys.exit(1)
+for w, spec in (("A", sys.argv[1]), ("B", sys.argv[2])):
+    t = np.array(times[w])
+    print(f"{w} [{spec}]: median {np.median(t):.3f} ms  min {t.min():.3f}  p90 {np.percentile(t, 90):.3f}  "
+          f"-> {nr / np.median(t) / 1e3:.1f} M reads/s (median)")
+al.close()
