@@ -992,7 +992,11 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(chunk * c->ops_slot)));
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
-    HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));
+    {   // [0..1] the kernels' flags, [2] the compaction's block counter: zero from allocation on
+        const int32_t* before = c->s->d_opsctl.p;
+        HIP_OR_FAIL(c, c->s->d_opsctl.reserve(4));
+        if (c->s->d_opsctl.p != before) HIP_OR_FAIL(c, hipMemset(c->s->d_opsctl.p, 0, 4 * sizeof(int32_t)));
+    }
     HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtl));
     HIP_OR_FAIL(c, c->s->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
     HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));
@@ -1003,7 +1007,8 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
 // Kernels of c->n reads starting at read `base`, then their compaction into
 // staging[which]: ops_off of those reads (global: the call's running base in
 // ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
-int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr) {
+int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr,
+                     int64_t* hctl = nullptr) {
     int rc = launch_range(c, base);
     if (rc) return rc;
     // only the compaction writes the set's staging array: it waits for the copy of the
@@ -1022,7 +1027,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n, c->s->d_blk.p,
                                           c->d_ctl64.p, c->d_opsoff.p + base, c->s->d_staging.p, c->staging_cap,
-                                          c->s->d_opsctl.p, cnt, c->cs));
+                                          c->s->d_opsctl.p, cnt, c->cs, hctl));
     return NW_OK;
 }
 
@@ -1705,11 +1710,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             const int64_t beyond = h[5] + h[4];   // reads the first level handed on
             c->only16 = !c->skip16 && done >= 32768 && beyond * 100 <= done && beyond * (hi - lo) <= kOnly16Reads * done;
         }
+        // the compaction writes the chunk's ctl into h_ctl[k] itself
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
-                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr)))
+                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k)))
             return restore(rc);
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->h_ctl + nw::kOpsCtl * k, c->d_ctl64.p, nw::kOpsCtl * sizeof(int64_t),
-                                      hipMemcpyDeviceToHost, c->cs));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
