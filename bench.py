@@ -544,7 +544,7 @@ def main():
                 if name == "dual":
                     legs[name] = dual_leg(local, args.reads, args.steps, args.warmup)
                 elif name == "pooled":
-                    legs[name] = pooled_leg(local, args.pooled_amplicons, args.pooled_reads, 2, 1)
+                    legs[name] = pooled_leg(local, args.pooled_amplicons, args.pooled_reads, 5, 2)
                 else:
                     legs[name] = merge_leg(local, args.merge_pairs)
             except Exception as exc:

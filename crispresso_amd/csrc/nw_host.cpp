@@ -1703,7 +1703,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // instead few reads reach the second level (C2: ~0.3 %, ~600 per chunk), its fill and
         // walk are two latency-bound launches for a handful of waves: those reads go straight
         // to the exact kernel, one wave each (the chunk's chain is 3 % shorter per call)
-        if (adaptive && k >= lag + 1 && !groups) {
+        if (adaptive && k >= lag + 1) {   // pooled calls too: one library's amplicons, one read source
             const int64_t* h = c->h_ctl + nw::kOpsCtl * (k - lag - 1);   // synchronised in copy_runs
             const int64_t done = chunks[(size_t)(k - lag - 1)].hi;         // reads of chunks 0 .. k - lag - 1
             c->skip16 = h[6] >= 4096 && 2 * h[5] > h[6];

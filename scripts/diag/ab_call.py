@@ -1,7 +1,8 @@
 """In-process A/B of the headline call (nw_align_ops_packed, C2 1M reads) under two settings
 of env knobs the library reads per call: calls alternate A, B, A, B ... so that box-level
 drift (PCIe, host load) hits both alike.
-Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds]   (an empty string = defaults)"""
+Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds] [pooled]   (an empty string = defaults;
+pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads)"""
 import os
 import sys
 import time
@@ -20,9 +21,15 @@ def parse(spec):
 
 A, B = parse(sys.argv[1]), parse(sys.argv[2])
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-nr = bench.READS_PER_GPU
-amplicon = synth.random_amplicon(bench.AMPLICON_LEN, 1)
-buf, off = synth.reads_from(amplicon, nr, 2)
+pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
+if pooled:
+    amps, buf, off, which = bench.pooled_workload(96, 100_000)
+    pw = _lib.pinned_copy(which)
+    nr = len(off) - 1
+else:
+    nr = bench.READS_PER_GPU
+    amplicon = synth.random_amplicon(bench.AMPLICON_LEN, 1)
+    buf, off = synth.reads_from(amplicon, nr, 2)
 pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
 stats = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
 ops_off = _lib.PinnedBuffer(nr + 1, np.int64)
@@ -30,7 +37,8 @@ ops = _lib.PinnedBuffer(4 * nr + 4096, np.uint32)
 p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
 pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
 al = GpuAligner(0)
-al.set_reference(amplicon)
+if not pooled:
+    al.set_reference(amplicon)
 keys = set(A) | set(B)
 times = {"A": [], "B": []}
 ref = None
@@ -40,7 +48,10 @@ for i in range(2 * rounds + 4):
         os.environ.pop(k, None)
     os.environ.update(A if which == "A" else B)
     t0 = time.perf_counter()
-    al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
+    if pooled:
+        al.align_multi_ops(amps, pr, None, pw.array, out=(stats.array, ops.array, ops_off.array))
+    else:
+        al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
     dt = time.perf_counter() - t0
     if i >= 4:
         times[which].append(dt * 1e3)
