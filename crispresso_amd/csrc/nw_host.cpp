@@ -88,7 +88,6 @@ struct Scratch {
     }
 };
 constexpr int kScratchSets = 3;
-constexpr int64_t kOnly16Reads = 1024;   // expected second-level reads per chunk under which it is skipped
 
 struct nw_ctx {
     int device = 0;
@@ -150,7 +149,6 @@ struct nw_ctx {
     bool exact_tb_lds = true;
     bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
     bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
-    bool only16 = false;              // this chunk: the 16-diagonal level's give-ups straight to the exact kernel
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
@@ -880,7 +878,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         const bool two = c->diag16_fill.grid > 0 && !c->skip16;
         // CRISPR_NW_LEVELS=16: the first level's give-ups go straight to the exact kernel
         const char* lv = std::getenv("CRISPR_NW_LEVELS");
-        const bool only16 = two && ((lv && std::strcmp(lv, "16") == 0) || c->only16);
+        const bool only16 = two && lv && std::strcmp(lv, "16") == 0;
         a.redo_list = c->s->d_redo.p;
         a.redo_count = c->s->d_fallback_count.p + 2;
         if (two && !only16) {
@@ -1595,11 +1593,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
     const int64_t nchunks = (int64_t)chunks.size();
-    c->skip16 = c->only16 = false;
+    c->skip16 = false;
     const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
     const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
     auto restore = [&](int code) {
-        c->skip16 = c->only16 = false;
+        c->skip16 = false;
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1699,16 +1697,16 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // adaptive first level: when most of the DP reads of the chunks done so far needed the
         // 32-diagonal level (e.g. the HDR pass: a 10-bp block substitution costs two 10-bp gaps
         // or 10 mismatches, beyond what 16 diagonals certify), the next chunks skip the
-        // 16-diagonal level (its fill and walk would be spent on reads it hands on).  When
-        // instead few reads reach the second level (C2: ~0.3 %, ~600 per chunk), its fill and
-        // walk are two latency-bound launches for a handful of waves: those reads go straight
-        // to the exact kernel, one wave each (the chunk's chain is 3 % shorter per call)
+        // 16-diagonal level (its fill and walk would be spent on reads it hands on).  (The
+        // converse -- sending the first level's give-ups straight to the exact kernel when few
+        // reach the second level -- measured 3 % on C2 but is not safe to choose from earlier
+        // chunks: with the HDR reads last (synth.c3_workload), the last chunks sent tens of
+        // thousands of reads to the exact kernel, 15 -> 24 ms per C3 step.  The same choice
+        // made on the device from the chunk's own count measured no gain: the skipped
+        // level's launches remain.)
         if (adaptive && k >= lag + 1) {   // pooled calls too: one library's amplicons, one read source
             const int64_t* h = c->h_ctl + nw::kOpsCtl * (k - lag - 1);   // synchronised in copy_runs
-            const int64_t done = chunks[(size_t)(k - lag - 1)].hi;         // reads of chunks 0 .. k - lag - 1
             c->skip16 = h[6] >= 4096 && 2 * h[5] > h[6];
-            const int64_t beyond = h[5] + h[4];   // reads the first level handed on
-            c->only16 = !c->skip16 && done >= 32768 && beyond * 100 <= done && beyond * (hi - lo) <= kOnly16Reads * done;
         }
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,

@@ -304,32 +304,17 @@ def test_adaptive_first_level_hdr_pass(gpu_aligner_factory, oracle, monkeypatch)
     assert_same(oracle, hdr, sb, so, sub.expand(hdr, sb, so), "adaptive-hdr")
 
 
-def test_adaptive_second_level_skip(gpu_aligner_factory, oracle, monkeypatch):
-    """C2 reads (~0.3 % need the 32-diagonal level): once the finished chunks show that few
-    reads reach it, later chunks send the first level's give-ups straight to the exact
-    kernel.  Records and runs equal both levels on every chunk (CRISPR_NW_ADAPT=0) and the
-    oracle."""
-    amp = synth.random_amplicon(250, 1)
-    buf, off = synth.reads_from(amp, 60000, 77)
-    monkeypatch.setenv("CRISPR_NW_CHUNK", "8192")
+def test_adaptive_levels_sorted_input(gpu_aligner_factory, monkeypatch):
+    """Reads whose character changes part-way (synth.c3_workload puts the HDR reads last):
+    the adaptive level choice, made from finished chunks, must not send the late chunks'
+    second-level reads to the exact kernel (a rule that did measured 15 -> 24 ms per C3
+    step)."""
+    amp, _, buf, off = synth.c3_workload(100000)
+    monkeypatch.setenv("CRISPR_NW_CHUNK", "16384")
     a = gpu_aligner_factory()
     a.set_reference(amp)
-    ob = a.align_ops(buf, off)
+    a.align_ops(buf, off)
     paths = a.path_counts()
-    monkeypatch.setenv("CRISPR_NW_ADAPT", "0")
-    both = a.align_ops(buf, off)
-    fixed = a.path_counts()
-    assert paths["exact_kernel"] > fixed["exact_kernel"]   # later chunks skipped the second level
-    assert paths["band32"] < fixed["band32"]
-    for f in FIELDS + ("flags",):
-        assert np.array_equal(ob.stats[f], both.stats[f])
-    assert np.array_equal(ob.ops, both.ops) and np.array_equal(ob.ops_off, both.ops_off)
-    # a sample plus the lowest-scoring reads (the ones the bands hand on), against the oracle
-    sel = np.unique(np.concatenate([np.arange(0, len(off) - 1, 50), np.argsort(ob.stats["score"], kind="stable")[:300]]))
-    sb, so = pack_reads([bytes(buf[off[i]:off[i + 1]]).decode() for i in sel])
-    runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in sel]
-    roff = np.zeros(len(sel) + 1, np.int64)
-    roff[1:] = np.cumsum([len(r) for r in runs])
-    from crispresso_amd.aligner import OpsBatch
-    sub = OpsBatch(ob.stats[sel], np.concatenate(runs), roff, np.diff(so), ob.scale)
-    assert_same(oracle, amp, sb, so, sub.expand(amp, sb, so), "adaptive-second-level")
+    assert paths["band32"] > 5000                       # the HDR reads took the second level
+    assert paths["exact_kernel"] < 0.005 * (len(off) - 1)
+
