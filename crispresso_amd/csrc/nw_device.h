@@ -174,9 +174,8 @@ hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_ld
 // base, [2] this chunk's total, [3] errors (1: staging full, 2: spill area full, from
 // opsctl[1]); running over the call: [4] exact-kernel reads, [5] second band level reads,
 // [6] reads that needed the DP (OpsCounts: the device counters of the chunk's kernels).
-// blk: ceil(n / kOpsBlockReads) int64.  opsctl: [0..1] the kernels' flags, [2] the
-// compaction's block counter (zero between launches).  hctl: pinned host copy of ctl
-// written by the compaction (or null).
+// blk: ceil(n / kOpsBlockReads) int64.  opsctl: the kernels' flags.  hctl: pinned host
+// copy of ctl written by the compaction (or null).
 constexpr int kOpsBlockReads = 1024;
 constexpr int kOpsCtl = 8;
 struct OpsCounts {

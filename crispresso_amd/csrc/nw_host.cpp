@@ -990,11 +990,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(chunk * c->ops_slot)));
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
-    {   // [0..1] the kernels' flags, [2] the compaction's block counter: zero from allocation on
-        const int32_t* before = c->s->d_opsctl.p;
-        HIP_OR_FAIL(c, c->s->d_opsctl.reserve(4));
-        if (c->s->d_opsctl.p != before) HIP_OR_FAIL(c, hipMemset(c->s->d_opsctl.p, 0, 4 * sizeof(int32_t)));
-    }
+    HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));
     HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtl));
     HIP_OR_FAIL(c, c->s->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
     HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));

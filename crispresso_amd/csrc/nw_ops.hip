@@ -3,17 +3,16 @@
 // In ops mode (KernelArgs::ops, include/crispr_nw.h nw_align_ops) every aligner
 // kernel leaves a read's traceback runs in its fixed slot (or the spill area) and
 // the run count in nops[r].  What crosses PCIe is one contiguous run array plus
-// the per-read start offsets: two launches per chunk of reads --
-//   sums:    runs per block of kOpsBlockReads reads; the last block to finish (a
-//            counter per scratch set) scans the block sums and updates ctl: the
-//            chunk's base is the running total of the call's earlier chunks (ctl[0],
-//            in-stream), and the chunk's ctl goes straight to the caller's pinned
-//            host mirror (no copy launch in the chunk's chain),
-//   compact: per-read offsets (ops_off = chunk base + local offset) and the
-//            copy of every read's runs into the staging array at its local offset.
+// the per-read start offsets: three launches per chunk of reads --
+//   blocksum: runs per block of kOpsBlockReads reads,
+//   scan:     exclusive scan of the block sums (one block); the chunk's base is
+//             the running total of the call's earlier chunks (ctl[0], in-stream);
+//             the chunk's ctl also goes straight to the caller's pinned host mirror
+//             (no copy launch in the chunk's chain),
+//   compact:  per-read offsets (ops_off = chunk base + local offset) and the
+//             copy of every read's runs into the staging array at its local offset.
 // The host copies staging[0, ctl[2]) to ops_out + ctl[1].
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <stdint.h>
 
 #include "nw_common.h"
@@ -48,36 +47,34 @@ __device__ long long block_excl_scan(long long v, long long* total) {
     return before + incl - v;
 }
 
-// grid = max(nblk, 1) blocks; done: this set's counter (0 between launches: the last
-// block resets it); hctl: pinned host mirror of ctl for this chunk (or null)
-__global__ __launch_bounds__(kOpsThreads) void nw_ops_sums(const int32_t* nops, int64_t n, int nblk, int64_t* blk,
-                                                           int32_t* done, int64_t* ctl, const int32_t* opsctl,
-                                                           OpsCounts cnt, int64_t* hctl) {
-    __shared__ int last;
-    if ((int)blockIdx.x < nblk) {
-        const long long r0 = (long long)blockIdx.x * kOpsBlockReads + threadIdx.x * kOpsPerThread;
-        long long s = 0;
+__global__ __launch_bounds__(kOpsThreads) void nw_ops_blocksum(const int32_t* nops, int64_t n, int64_t* blk) {
+    const long long r0 = (long long)blockIdx.x * kOpsBlockReads + threadIdx.x * kOpsPerThread;
+    long long s = 0;
 #pragma unroll
-        for (int k = 0; k < kOpsPerThread; ++k) s += r0 + k < n ? nops[r0 + k] : 0;
-        long long total;
-        block_excl_scan(s, &total);
-        if (threadIdx.x == 0) blk[blockIdx.x] = total;
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();   // this block's sum is visible device-wide before it is counted
-        last = atomicAdd(done, 1) == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();       // every block's sum is visible to the last one
+    for (int k = 0; k < kOpsPerThread; ++k) s += r0 + k < n ? nops[r0 + k] : 0;
+    long long total;
+    block_excl_scan(s, &total);
+    if (threadIdx.x == 0) blk[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void nw_ops_scan(int64_t* blk, int nblk, int64_t* ctl, const int32_t* opsctl,
+                                                    OpsCounts cnt, int64_t* hctl) {
+    __shared__ long long part[1024];
     long long carry = 0;
-    for (int t0 = 0; t0 < nblk; t0 += kOpsThreads) {
+    for (int t0 = 0; t0 < nblk; t0 += 1024) {
         const int t = t0 + (int)threadIdx.x;
         const long long v = t < nblk ? blk[t] : 0;
-        long long tile;
-        const long long ex = block_excl_scan(v, &tile);
-        if (t < nblk) blk[t] = carry + ex;
-        carry += tile;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const long long u = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += u;
+            __syncthreads();
+        }
+        if (t < nblk) blk[t] = carry + part[threadIdx.x] - v;
+        carry += part[1023];
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
         ctl[1] = ctl[0];
@@ -90,7 +87,6 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_sums(const int32_t* nops, 
         ctl[4] += fb;
         if (cnt.redo) ctl[5] += *cnt.redo;
         if (cnt.band) ctl[6] += *cnt.band;
-        *done = 0;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];
     }
@@ -138,12 +134,15 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
                               int64_t* blk, int64_t* ctl, int64_t* ops_off, uint32_t* staging, int64_t staging_cap,
                               int32_t* opsctl, const OpsCounts& cnt, hipStream_t s, int64_t* hctl) {
-    const int nblk = (int)std::max<int64_t>(0, (n + kOpsBlockReads - 1) / kOpsBlockReads);
-    hipLaunchKernelGGL(nw_ops_sums, dim3(std::max(nblk, 1)), dim3(kOpsThreads), 0, s, nops, n, nblk, blk, opsctl + 2,
-                       ctl, opsctl, cnt, hctl);
-    if (nblk > 0)
-        hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, spill, n, blk, ctl,
-                           ops_off, staging, staging_cap, hctl);
+    const int nblk = (int)((n + kOpsBlockReads - 1) / kOpsBlockReads);
+    if (nblk <= 0) {
+        hipLaunchKernelGGL(nw_ops_scan, dim3(1), dim3(1024), 0, s, blk, 0, ctl, opsctl, cnt, hctl);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(nw_ops_blocksum, dim3(nblk), dim3(kOpsThreads), 0, s, nops, n, blk);
+    hipLaunchKernelGGL(nw_ops_scan, dim3(1), dim3(1024), 0, s, blk, nblk, ctl, opsctl, cnt, hctl);
+    hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, spill, n, blk, ctl,
+                       ops_off, staging, staging_cap, hctl);
     return hipGetLastError();
 }
 
