@@ -55,7 +55,7 @@ READS_PER_GPU = 1_000_000
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
 # VALU instruction count per fill launch (newest first)
 PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
-                 for d in ("r02_v3", "r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
+                 for d in ("r02_v4", "r02_v3", "r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
 AMPLICON_LEN = 250
 
 
@@ -281,14 +281,16 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
     return out
 
 
-def dual_leg(device, n_reads, steps, warmup):
+def dual_leg(al, n_reads, steps, warmup):
     """C3: every read against the amplicon (records + runs) and against the HDR
     amplicon (records only: the repair pass reads scores, CORE:1808-1828 with just_score).
     One context: the reads cross PCIe once, 2-bit packed as in the headline
     (nw_align_ops_packed), the HDR pass re-aligns the batch still in HBM
-    (nw_align_ops_resident) after switching the amplicon."""
+    (nw_align_ops_resident) after switching the amplicon.  `al`: the headline's aligner (one
+    context per process: a second one's streams would share the GPU's hardware queues with
+    the first's; measured 10.3 vs 9.7 ms per step)."""
     from crispresso_amd import _lib, synth
-    from crispresso_amd.aligner import GpuAligner, pack_2bit
+    from crispresso_amd.aligner import pack_2bit
 
     amp, hdr, buf, off = synth.c3_workload(n_reads)
     n = len(off) - 1
@@ -300,7 +302,6 @@ def dual_leg(device, n_reads, steps, warmup):
     ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
     pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
-    al = GpuAligner(device)
 
     def step():
         al.set_reference(amp)
@@ -324,7 +325,6 @@ def dual_leg(device, n_reads, steps, warmup):
                    "synchronous; packing outside the timed region, as in the headline"}
     for b in (pb, po, stats, stats2, ops_off, ops_off2, ops, p_packed):
         b.close()
-    al.close()
     return out
 
 
@@ -346,11 +346,12 @@ def pooled_workload(n_amplicons, reads_per_amplicon):
     return amps, np.concatenate(bufs), off, which
 
 
-def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
+def pooled_leg(al, n_amplicons, reads_per_amplicon, steps, warmup):
     """C5 on one GPU: one nw_align_multi_ops call over all amplicons' reads (pinned host
-    buffers in, records + runs out), next to the same number of C2 single-amplicon reads."""
+    buffers in, records + runs out), next to the same number of C2 single-amplicon reads.
+    `al`: the headline's aligner (see dual_leg; 28.2 vs 24.4 ms per call with a second
+    context); the call leaves it without an amplicon."""
     from crispresso_amd import _lib
-    from crispresso_amd.aligner import GpuAligner
 
     amps, buf, off, which = pooled_workload(n_amplicons, reads_per_amplicon)
     n = len(off) - 1
@@ -361,7 +362,6 @@ def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
     out = (stats.array, ops.array, ops_off.array)
     from crispresso_amd.aligner import pack_2bit
 
-    al = GpuAligner(device)
     for _ in range(warmup):
         al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
     t0 = time.perf_counter()
@@ -396,7 +396,6 @@ def pooled_leg(device, n_amplicons, reads_per_amplicon, steps, warmup):
                    "chunks of one amplicon each; text_input = nw_align_multi_ops on the text"}
     for b in (pb, po, pw, stats, ops_off, ops, p_packed):
         b.close()
-    al.close()
     return res
 
 
@@ -546,9 +545,9 @@ def main():
         for name in legs:
             try:   # informational legs: never cost the bench line
                 if name == "dual":
-                    legs[name] = dual_leg(local, args.reads, args.steps, args.warmup)
+                    legs[name] = dual_leg(al, args.reads, args.steps, args.warmup)
                 elif name == "pooled":
-                    legs[name] = pooled_leg(local, args.pooled_amplicons, args.pooled_reads, 5, 2)
+                    legs[name] = pooled_leg(al, args.pooled_amplicons, args.pooled_reads, 5, 2)
                 else:
                     legs[name] = merge_leg(local, args.merge_pairs)
             except Exception as exc:
