@@ -2,7 +2,9 @@
 gunzip | awk | sed stage and EMBOSS's reader (fastq.fastq_bytes_as_fasta), on the
 reference's test reads, the golden fixtures and edge cases (no trailing newline, a
 header without its sequence line, CRLF, ':' and digits in sequences, lower case,
-whitespace-led headers, chunk-boundary-sized lines)."""
+whitespace-led headers, chunk-boundary-sized lines).  The reader has two decoders --
+libdeflate into one buffer parsed by several threads in parts cut at record boundaries,
+and zlib gzread (CRISPR_NW_FASTQ_ZLIB=1) -- held to the same outputs."""
 import gzip
 import os
 
@@ -122,3 +124,68 @@ def test_filter_se_pe_files(tmp_path):
     drop = fastq.get_ids_reads_to_remove(R1, 30) | fastq.get_ids_reads_to_remove(R2, 30)
     assert len(n1) == len(n2) == len(fastq.read_fastq_as_fasta(R1)[0]) - len(drop)
     assert fastq.filter_se_fastq_by_qual.__defaults__[1:] == (20, 0)   # the reference's defaults
+
+
+def _native(path, q=0, qs=0):
+    n, b, o = fastq.read_fastq_as_fasta(path, q, qs)
+    return list(n), b, o
+
+
+def _random_fastq(rng, n, odd=True):
+    """Records with the edge cases of test_edge_cases mixed in: '@' / '+' leading quality
+    lines, CRLF, empty sequence lines, long lines, ':' and spaces."""
+    alpha = np.frombuffer(b"ACGTNacgt:-*", np.uint8)
+    out = []
+    for i in range(n):
+        L = int(rng.integers(0, 40)) if odd and i % 97 == 5 else int(rng.integers(60, 300))
+        seq = rng.choice(alpha, L).tobytes()
+        qual = rng.integers(33, 75, L).astype(np.uint8).tobytes()
+        if odd and i % 13 == 0 and L:
+            qual = b"@" + qual[1:]                 # a quality line that starts like a header
+        if odd and i % 17 == 0 and L:
+            qual = b"+" + qual[1:]
+        eol = b"\r\n" if odd and i % 31 == 0 else b"\n"
+        out.append(b"@read:%d extra%s" % (i, eol) + seq + eol + b"+" + eol + qual + eol)
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("gz", [False, True])
+@pytest.mark.parametrize("q", [(0, 0), (30, 0), (25, 10)])
+@pytest.mark.parametrize("tail", [b"", b"@last\nACGT\n+\nII", b"@last\nACG", b"@last\n"])
+def test_parallel_parse_equals_serial(tmp_path, monkeypatch, gz, q, tail):
+    """Small files forced through the parallel parse (CRISPR_NW_FASTQ_PAR_MIN): parts cut
+    at record boundaries anywhere, the last part's open record or line carried on; equal
+    to the zlib streaming path and to the Python restatement, with and without the quality
+    filter."""
+    rng = np.random.Generator(np.random.PCG64(11 + len(tail)))
+    text = _random_fastq(rng, 3000) + tail
+    p = tmp_path / ("x.fastq.gz" if gz else "x.fastq")
+    if gz:
+        with gzip.open(p, "wb") as f:
+            f.write(text)
+    else:
+        p.write_bytes(text)
+    monkeypatch.setenv("CRISPR_NW_FASTQ_PAR_MIN", "1")
+    par = _native(str(p), *q)
+    monkeypatch.setenv("CRISPR_NW_FASTQ_ZLIB", "1")
+    ser = _native(str(p), *q)
+    py = fastq.read_fastq_as_fasta_py(str(p), *q)
+    for a in (ser, py):
+        assert par[0] == list(a[0])
+        assert np.array_equal(par[1], a[1]) and np.array_equal(par[2], a[2])
+
+
+def test_multi_member_gzip(tmp_path, monkeypatch):
+    """Concatenated gzip members (each its own libdeflate call) and trailing garbage after
+    the last member (ignored, as gzread does)."""
+    rng = np.random.Generator(np.random.PCG64(3))
+    p = tmp_path / "multi.fastq.gz"
+    blobs = [_random_fastq(rng, 500, odd=False) for _ in range(3)]
+    with open(p, "wb") as f:
+        for b in blobs:
+            f.write(gzip.compress(b))
+    fast = _native(str(p))
+    monkeypatch.setenv("CRISPR_NW_FASTQ_ZLIB", "1")
+    slow = _native(str(p))
+    assert fast[0] == slow[0] and len(fast[0]) == 1500
+    assert np.array_equal(fast[1], slow[1]) and np.array_equal(fast[2], slow[2])
