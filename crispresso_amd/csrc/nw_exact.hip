@@ -115,12 +115,14 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
     // this wave's fill: the row above the amplicon (wave 0: M - O = -O, Y = -inf, H = 0
     // and the column's read code) or the previous wave's ring
     const int4* src = rings + (w > 0 ? w - 1 : 0) * kExRing;
+    // branch-free (both loads issued, the wave-uniform w selects): a branch per step splits
+    // the unrolled block and keeps the compiler from interleaving the steps
     auto fill_at = [&](int t) -> int4 {
-        if (w == 0) {   // top boundary at column t: H = leading end gap of t + 1 (0: free)
-            const int h = end_lead(a, t + 1);
-            return make_int4(h - O, NEG, h, (int)topc[t]);
-        }
-        return src[(t - 1 - kExK) & (kExRing - 1)];
+        const int4 r = src[(t - 1 - kExK) & (kExRing - 1)];
+        const int h = end_lead(a, t + 1);   // top boundary at column t: H = leading end gap of t + 1 (0: free)
+        const int c = (int)topc[t];
+        const bool top = w == 0;
+        return make_int4(top ? h - O : r.x, top ? NEG : r.y, top ? h : r.z, top ? c : r.w);
     };
     int4* ring_out = w + 1 < W ? rings + w * kExRing : nullptr;
     // the rows' scores: EDNAFULL(amplicon code, read code 0..15) as 16 int8 in 4 dwords
@@ -175,7 +177,10 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
                 const int cb = shr1(sC, f0.w);
                 const int bj = t - lag;
                 unsigned acc = 0;
-                if (has_rows && (unsigned)bj < (unsigned)Lb) {
+                // every lane computes every step (no branch); lanes outside their rows' columns
+                // keep their state and contribute no traceback bits
+                const bool valid = has_rows && (unsigned)bj < (unsigned)Lb;
+                {
                     // score byte: codes 0..7 from dwords 0-1, 8..15 from 2-3, 16 -> 0 (selector 12)
                     const unsigned sel = cb < 16 ? (unsigned)(cb & 7) : 12u;
                     const bool hi = (cb & 8) != 0 && cb < 16;
@@ -199,16 +204,17 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
                         acc |= nib << (4 * k);
                         mlast = k == klast ? M : mlast;
                         Hd = Hold[k];
-                        Hold[k] = H;
-                        Mol[k] = M - O;
-                        Xl[k] = X;
+                        Hold[k] = valid ? H : Hold[k];
+                        Mol[k] = valid ? M - O : Mol[k];
+                        Xl[k] = valid ? X : Xl[k];
                         Mou = M - O;
                         Yu = Y;
                     }
-                    sMo = Mou;
-                    sY = Yu;
+                    acc = valid ? acc : 0u;
+                    sMo = valid ? Mou : sMo;
+                    sY = valid ? Yu : sY;
                     sH = Hold[R - 1];
-                    if (g == glast) lastrow[bj] = mlast;
+                    if (valid && g == glast) lastrow[bj] = mlast;
                 }
                 sC = cb;
                 Htop = rH;
