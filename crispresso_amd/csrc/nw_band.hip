@@ -131,7 +131,8 @@ constexpr int kBK = 64;               // tau = t - dlo + kBK: >= 0 and even
 constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [-17, La + 48]
 constexpr int kJPad = 95;             // pair codes: index j + kJPad, j in [-48, La + 80]; j = 1 is 4-aligned
 constexpr int kPadCode = 5;           // lut6: A T G C N pad
-constexpr int kTabBytes = 896;        // [6][36] packed scores (864 B)
+constexpr int kTabRows = NCODE;       // amplicon rows: every EDNAFULL code (IUPAC too) + pad/unknown
+constexpr int kTabBytes = 2448;       // [17][36] packed scores
 constexpr int kHdrBytes = 48;         // {tau0, dlo, flags, -}, {ra, rb, LbA, LbB}, {offA, offB}
 constexpr int kPairInactive = 4;      // header flag: the pair was not filled (walk: empty / fallback)
 
@@ -402,11 +403,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     unsigned char* lut6 = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * PCS;
     // a tile row's four words per lane wait here (not in VGPRs) until its dwordx4 store
     unsigned* stage = (unsigned*)(lut6 + 256) + wave * 256 + 4 * lane;
-    for (int k = tid; k < 216; k += blockDim.x) tab[k] = a.band_tab[k];
+    for (int k = tid; k < kTabRows * 36; k += blockDim.x) tab[k] = a.band_tab[k];
     for (int k = tid; k < 256; k += blockDim.x) lut6[k] = a.lut6[k];
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
         const int i = k - kAPad;   // row i = amplicon residue i - 1
-        const int c = (i >= 1 && i <= La) ? a.lut6[a.amp[i - 1]] : kPadCode;   // host: amplicon codes <= 5
+        // the amplicon's EDNAFULL code (IUPAC codes included: their row of the table), pad outside
+        const int c = (i >= 1 && i <= La) ? a.lut[a.amp[i - 1]] : NCODE_PAD;
         // the score table's LDS address is folded in: a0 + j0 is the entry's LDS address
         acd[k] = (uint16_t)(c * 36 * 4 + (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)tab);
     }
@@ -997,9 +999,9 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
 __device__ __forceinline__ int diag_pairs(int La, int Lb, int d) { return d >= 0 ? min(La, Lb - d) : min(Lb, La + d); }
 
 // True when every single-diagonal alignment outside [dlo, dhi] whose overlap could
-// reach `score` (maxsub * P(d) >= score) scores below it.  A (6-code) score table
-// lookup per pair: amplicon / read bytes in LDS, codes by lut6, scores from band_tab
-// (packed with + 2E, entry [x][y][y]).
+// reach `score` (maxsub * P(d) >= score) scores below it.  A score table lookup per
+// pair: amplicon / read bytes in LDS, the amplicon's EDNAFULL code (lut) and the read's
+// 6-code (lut6), scores from band_tab (packed with + 2E, entry [x][y][y]).
 __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned char* amp, const unsigned char* rd,
                                             int La, int Lb, int dlo, int dhi, int score, int lane) {
     const int E2 = 2 * a.gap_extend;
@@ -1011,8 +1013,8 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
             const int i0 = d >= 0 ? 0 : -d, j0 = d >= 0 ? d : 0;   // 0-based first pair
             int sum = 0;
             for (int t = lane; t < P; t += 64) {
-                const int x = a.lut6[amp[i0 + t]], y = a.lut6[rd[j0 + t]];
-                const unsigned w = a.band_tab[(x < 6 ? x : 5) * 36 + (y < 6 ? y : 5) * 7];
+                const int x = a.lut[amp[i0 + t]], y = a.lut6[rd[j0 + t]];
+                const unsigned w = a.band_tab[x * 36 + (y < 6 ? y : 5) * 7];
                 sum += (int)(short)(w & 0xffffu) - E2;
             }
             if (wave_sum(sum) >= score) return false;

@@ -63,7 +63,7 @@ struct KernelArgs {
     int32_t band_words;            // traceback words per lane and pair
     int32_t band_lb_cap;           // longest read the band kernels take; longer ones sort last
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
-    const uint32_t* band_tab;      // [6 amplicon codes][6][6 read codes] packed int16x2 score + 2 E
+    const uint32_t* band_tab;      // [17 amplicon codes (EDNAFULL, pad)][6][6 read codes] packed int16x2 score + 2 E
     const uint32_t* rowpos;        // [La] codes each amplicon row scores > 0 against (markup ':')
     int32_t* sort_hist;            // [band_lb_cap + 3][sort grid + 1] per-block bucket counts, bucket bases
     int32_t* sort_key;             // [n] bucket of every read: length, band_lb_cap + 1 (longer), + 2 (exact copy)

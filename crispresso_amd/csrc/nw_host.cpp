@@ -294,12 +294,14 @@ int upload_shared(nw_ctx* c) {
         lut6[(size_t)q] = (uint8_t)r;
         lut[(size_t)q] = (uint8_t)code;
     }
-    auto sub6 = [&](int x, int y) {
-        const int cx = codes6[x], cy = codes6[y];
+    // amplicon rows by EDNAFULL code (IUPAC amplicons keep the band path), read codes by the
+    // 6-code alphabet (reads with other IUPAC codes leave the band: REGION_BAD_*)
+    auto sub6 = [&](int cx, int y) {
+        const int cy = codes6[y];
         return (cx < 16 && cy < 16) ? nw::kEdna[cx][cy] * c->scale : 0;
     };
-    std::vector<uint32_t> btab(216);
-    for (int x = 0; x < 6; ++x)
+    std::vector<uint32_t> btab((size_t)nw::NCODE * 36);
+    for (int x = 0; x < nw::NCODE; ++x)
         for (int ya = 0; ya < 6; ++ya)
             for (int yb = 0; yb < 6; ++yb) {
                 const uint16_t sa = (uint16_t)(int16_t)(sub6(x, ya) + 2 * c->gap_extend);
@@ -523,7 +525,7 @@ int configure(nw_ctx* c) {
     c->use_diag = false;
     const bool want_diag = !kern || std::strcmp(kern, "diag") == 0;
     const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
-    if (want_diag && c->cur.amp_in_table && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
+    if (want_diag && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
         c->gap_open >= c->gap_extend) {
         const int64_t pairs = (c->n + 1) / 2;
         int64_t cap_bytes = 16ll << 30;

@@ -601,3 +601,29 @@ def test_diag_refined_certificate_clustered_mismatches(gpu_aligner_factory, orac
     counts = a.path_counts()
     if block <= 10:
         assert counts["exact_kernel"] < 0.05 * (len(off) - 1), counts
+
+
+@pytest.mark.parametrize("ops", [False, True])
+def test_iupac_amplicon_band_path(gpu_aligner_factory, oracle, ops):
+    """An amplicon with IUPAC codes (and a byte outside EDNAFULL) keeps the certified
+    band path: its rows score from the table's EDNAFULL rows.  Reads from it (ACGT at
+    the IUPAC positions, the parity mix of edits) equal the oracle, and few (~4 %) need
+    the exact kernel."""
+    base = synth.random_amplicon(250, 23)
+    amp = list(base)
+    for pos, code in zip((10, 57, 120, 121, 200, 233), "RYNKMS"):
+        amp[pos] = code
+    amp = "".join(amp)
+    reads = synth.unpack(*synth.reads_from(base, 3000, 24, synth.PARITY_MIX))
+    reads += [amp, amp.replace("N", "A"), base, "ACGTRYKMSWBDHVNU", ""]
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    if ops:
+        ob = a.align_ops(buf, off)
+        batch = ob.expand(amp, buf, off)
+    else:
+        batch = a.align_packed(buf, off)
+    paths = a.path_counts()
+    assert_same(oracle, amp, buf, off, batch, f"iupac-amplicon ops={ops}")
+    assert paths["band16"] > 1000 and paths["exact_kernel"] < 0.1 * len(reads)
