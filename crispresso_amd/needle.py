@@ -427,13 +427,15 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             df_database = fwd.dataframe("ref")
             df_database_repair = rep.dataframe("repaired", just_score=True)
             df_database_and_repair = df_database.join(df_database_repair)
+            # the reference's masks (CORE:1842-1851) as numpy arrays: a boolean Series would be
+            # aligned on the 1M-entry object index first (~0.06 s per mask, same rows)
             sr_not_aligned = df_database_and_repair.loc[
-                (df_database_and_repair.score_ref < args.min_identity_score)
-                & (df_database_and_repair.score_ref < args.min_identity_score)
+                ((df_database_and_repair.score_ref < args.min_identity_score)
+                 & (df_database_and_repair.score_ref < args.min_identity_score)).to_numpy()
             ].align_seq.apply(lambda x: x.replace("_", ""))
             df_database_and_repair = df_database_and_repair.loc[
-                (df_database_and_repair.score_ref > args.min_identity_score)
-                | (df_database_and_repair.score_repaired > args.min_identity_score)
+                ((df_database_and_repair.score_ref > args.min_identity_score)
+                 | (df_database_and_repair.score_repaired > args.min_identity_score)).to_numpy()
             ].copy()
             df_database_and_repair["score_diff"] = (
                 df_database_and_repair.score_ref - df_database_and_repair.score_repaired
@@ -442,9 +444,10 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
         else:
             df_needle_alignment = fwd.dataframe("ref")
             sr_not_aligned = df_needle_alignment.loc[
-                (df_needle_alignment.score_ref < args.min_identity_score)
+                (df_needle_alignment.score_ref < args.min_identity_score).to_numpy()
             ].align_seq.apply(lambda x: x.replace("_", ""))
-            df_needle_alignment = df_needle_alignment.loc[df_needle_alignment.score_ref > args.min_identity_score]
+            df_needle_alignment = df_needle_alignment.loc[
+                (df_needle_alignment.score_ref > args.min_identity_score).to_numpy()]
 
         if sr_not_aligned.count():
             fasta_text = "".join(f">{x0}\n{x1}\n" for x0, x1 in sr_not_aligned.items())
@@ -472,8 +475,8 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
                     df_repair_rc = rc_rep.dataframe("repaired", just_score=True)
                 df_database_and_repair_rc = rc.dataframe("ref").join(df_repair_rc)
                 df_database_and_repair_rc = df_database_and_repair_rc.loc[
-                    (df_database_and_repair_rc.score_ref > args.min_identity_score)
-                    | (df_database_and_repair_rc.score_repaired > args.min_identity_score)
+                    ((df_database_and_repair_rc.score_ref > args.min_identity_score)
+                     | (df_database_and_repair_rc.score_repaired > args.min_identity_score)).to_numpy()
                 ].copy()
                 df_database_and_repair_rc["score_diff"] = (
                     df_database_and_repair_rc.score_ref - df_database_and_repair_rc.score_repaired
@@ -482,7 +485,7 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             else:
                 df_needle_alignment_rc = rc.dataframe("ref")
                 df_needle_alignment_rc = df_needle_alignment_rc.loc[
-                    df_needle_alignment_rc.score_ref > args.min_identity_score
+                    (df_needle_alignment_rc.score_ref > args.min_identity_score).to_numpy()
                 ].copy()
             df_needle_alignment_rc["ref_seq"] = df_needle_alignment_rc["ref_seq"].apply(reverse_complement)
             df_needle_alignment_rc["align_seq"] = df_needle_alignment_rc["align_seq"].apply(reverse_complement)
