@@ -61,11 +61,16 @@ def main():
             ob, res["align_ops_s"] = timed(al.align_ops, b2, o2)
             res["align_ops_pcie"] = al.ops_times()
             _, res["dataframe_ops_s"] = timed(ops_to_dataframe, ob, amp, b2, o2, names, "ref")
-            df, res["align_reads_c2_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp), fq, al)
-            res["align_reads_c2_rows"] = int(len(df))
-            df, res["align_reads_c3_s"] = timed(align_reads, AlignArgs(amplicon_seq=amp,
-                                                                       expected_hdr_amplicon_seq=hdr), fq, al)
-            res["align_reads_c3_rows"] = int(len(df))
+            # first call (one-time costs: host pools, pinned staging) and the best of two more
+            c2 = [timed(align_reads, AlignArgs(amplicon_seq=amp), fq, al) for _ in range(3)]
+            res["align_reads_c2_first_s"] = c2[0][1]
+            res["align_reads_c2_s"] = min(t for _, t in c2[1:])
+            res["align_reads_c2_rows"] = int(len(c2[0][0]))
+            c3 = [timed(align_reads, AlignArgs(amplicon_seq=amp, expected_hdr_amplicon_seq=hdr), fq, al)
+                  for _ in range(3)]
+            res["align_reads_c3_first_s"] = c3[0][1]
+            res["align_reads_c3_s"] = min(t for _, t in c3[1:])
+            res["align_reads_c3_rows"] = int(len(c3[0][0]))
     res["align_reads_c2_reads_per_s"] = n / res["align_reads_c2_s"]
     res["align_reads_c3_reads_per_s"] = n / res["align_reads_c3_s"]
     res["align_reads_c2_without_fastq_reads_per_s"] = n / (res["align_reads_c2_s"] - res["fastq_gz_s"])
