@@ -243,7 +243,8 @@ def batch_to_dataframe(batch: AlignmentBatch, names: Sequence[str], name: str = 
 
 
 def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.ndarray, names: Sequence[str],
-                     name: str = "seq", just_score: bool = False, nthreads: int = 0) -> pd.DataFrame:
+                     name: str = "seq", just_score: bool = False, nthreads: int = 0,
+                     index: Optional[pd.Index] = None) -> pd.DataFrame:
     """batch_to_dataframe from the ops output: the same DataFrame, built without the
     rows of reads that are byte-for-byte the amplicon (CRISPResso's unmodified reads,
     most of a typical run): they share one ``ref_seq`` / ``align_str`` / ``align_seq``
@@ -252,9 +253,9 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
     become strings in bulk (:func:`_strings`)."""
     st = ob.stats
     keep = np.flatnonzero((st["flags"] & _lib.NW_FLAG_EMPTY) == 0)
-    ids = _ids_of(names, keep)
     ident = _printed_percents(st["n_ident"][keep], st["aln_len"][keep])
-    index = pd.Index(ids, dtype=object, name="ID")
+    if index is None or len(index) != len(keep) or len(keep) != len(st):
+        index = pd.Index(_ids_of(names, keep), dtype=object, name="ID")
     if just_score:
         return pd.DataFrame({"score_" + name: ident}, index=index)
     lib = _lib.load()
@@ -340,9 +341,14 @@ class PassResult:
     buf: Optional[np.ndarray] = None
     offsets: Optional[np.ndarray] = None
 
-    def dataframe(self, name: str = "ref", just_score: bool = False) -> pd.DataFrame:
+    def dataframe(self, name: str = "ref", just_score: bool = False,
+                  index: Optional[pd.Index] = None) -> pd.DataFrame:
+        """``index``: the ID index of another pass over the same reads, reused when this
+        pass keeps the same reads (one Index object: pandas hashes it once, and joins
+        two frames on it without a second hash table)."""
         if self.ops is not None:
-            return ops_to_dataframe(self.ops, self.amplicon, self.buf, self.offsets, self.names, name, just_score)
+            return ops_to_dataframe(self.ops, self.amplicon, self.buf, self.offsets, self.names, name, just_score,
+                                    index=index)
         return batch_to_dataframe(self.batch, self.names, name, just_score)
 
 
@@ -425,7 +431,8 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
                               _jp(f"needle_output_repair_{database_id}.txt.gz") if keep_files else None,
                               just_score=True)
             df_database = fwd.dataframe("ref")
-            df_database_repair = rep.dataframe("repaired", just_score=True)
+            # same reads, same (non-empty) rows: the repair frame shares the ID index
+            df_database_repair = rep.dataframe("repaired", just_score=True, index=df_database.index)
             df_database_and_repair = df_database.join(df_database_repair)
             # the reference's masks (CORE:1842-1851) as numpy arrays: a boolean Series would be
             # aligned on the 1M-entry object index first (~0.06 s per mask, same rows)
