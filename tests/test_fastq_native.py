@@ -189,3 +189,43 @@ def test_multi_member_gzip(tmp_path, monkeypatch):
     slow = _native(str(p))
     assert fast[0] == slow[0] and len(fast[0]) == 1500
     assert np.array_equal(fast[1], slow[1]) and np.array_equal(fast[2], slow[2])
+
+
+def _read_in_child(path, q):
+    n, b, o = fastq.read_fastq_as_fasta(path)
+    q.put((len(n), int(b.sum()), int(o[-1])))
+
+
+@pytest.mark.timeout(120)
+def test_host_pool_threads_and_fork(tmp_path, monkeypatch):
+    """The parallel parse's host pool: callers on several Python threads at once (one
+    job at a time: the others parse inline) and a forked child (the parked threads stay
+    in the parent: the child parses inline instead of waiting for them)."""
+    import multiprocessing as mp
+    import threading
+
+    rng = np.random.Generator(np.random.PCG64(29))
+    p = tmp_path / "t.fastq.gz"
+    with gzip.open(p, "wb") as f:
+        f.write(_random_fastq(rng, 4000))
+    monkeypatch.setenv("CRISPR_NW_FASTQ_PAR_MIN", "1")
+    ref = _native(str(p))
+    out = [None] * 6
+
+    def run(i):
+        out[i] = _native(str(p))
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(out))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for r in out:
+        assert r[0] == ref[0] and np.array_equal(r[1], ref[1]) and np.array_equal(r[2], ref[2])
+    q = mp.get_context("fork").Queue()
+    child = mp.get_context("fork").Process(target=_read_in_child, args=(str(p), q))
+    child.start()
+    got = q.get(timeout=60)
+    child.join(timeout=60)
+    assert child.exitcode == 0
+    assert got == (len(ref[0]), int(ref[1].sum()), int(ref[2][-1]))
