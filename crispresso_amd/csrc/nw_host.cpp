@@ -1586,7 +1586,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             rc = fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n);
     }
     ht.lap(1);
-    if (ngroups > 1) configured = -1;   // the pipeline configures each group again
+    if (ngroups > 1) configured = -1;   // the pipeline restores each group's saved configuration
     c->s = &c->sc[0];
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
