@@ -388,6 +388,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
@@ -1030,6 +1031,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
     const int La = a.La, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
     // Reads handed on (next level's redo list, or the exact kernel's list) wait in a

@@ -74,6 +74,11 @@ struct KernelArgs {
     uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
     int32_t* redo_blk;             // [ceil(n / 1024)] compaction scratch
     int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
+    // > 0: when the first level hands on at most this many reads (*redo_count), the second
+    // level's kernels return at once and the exact kernel takes them too (its fallback list,
+    // then the redo list): a few hundred reads cost the exact kernel's latency once, less
+    // than the second level's fill + walk ahead of it.  Decided on the device per chunk.
+    int32_t redo_direct;
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
     // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
     // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
@@ -98,6 +103,22 @@ __host__ __device__ inline int end_lead(const KernelArgs& a, int k) {
     return (a.end_weight && k > 0) ? -(a.end_open + (k - 1) * a.end_extend) : 0;
 }
 __host__ __device__ inline int end_trail(const KernelArgs& a, int k) { return -end_lead(a, k); }
+
+// KernelArgs::redo_direct: the chunk's second band level is skipped (read on the device
+// by the second level's kernels, the exact kernel and the ops counts alike).
+__host__ __device__ inline bool redo_direct_taken(const KernelArgs& a) {
+    return a.redo_direct > 0 && a.redo_count && *a.redo_count <= a.redo_direct;
+}
+// The exact kernel's work: entries [0, fallbacks) of the work list, then (direct) the redo list.
+__host__ __device__ inline long long exact_work_count(const KernelArgs& a) {
+    const long long nfb = a.work_list ? (long long)*a.work_count : a.n;
+    return a.work_list && redo_direct_taken(a) ? nfb + *a.redo_count : nfb;
+}
+__host__ __device__ inline long long exact_work_read(const KernelArgs& a, long long wi) {
+    if (!a.work_list) return wi;
+    const long long nfb = *a.work_count;
+    return wi < nfb ? a.work_list[wi] : (long long)a.redo_list[wi - nfb];
+}
 
 // Traceback storage of a kernel instantiation.
 enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_STREAM = 4, TB_DIAG = 5 };
@@ -183,6 +204,7 @@ struct OpsCounts {
     int passes;
     const int32_t* redo;       // second band level reads (null: one level)
     const int32_t* band;       // reads that needed the DP (null: not the band path)
+    int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
 };
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
                               int64_t* blk, int64_t* ctl, int64_t* ops_off, uint32_t* staging, int64_t staging_cap,

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // work-list entries (null list: every read); cap: [0, min(count, grid)), one per
     // block, the one-wave kernel takes the rest
-    long long count = a.work_list ? (long long)*a.work_count : a.n;
+    long long count = exact_work_count(a);
     if (cap) count = min(count, (long long)gridDim.x);
     if ((long long)blockIdx.x >= count) return;   // most blocks: nothing to do
     const int La = a.La, O = a.gap_open, E = a.gap_extend;
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
     const int lag = g + kExK * w;            // bj = t - lag
 
     for (long long wi = blockIdx.x; wi < count; wi += gridDim.x) {
-        const long long rd = a.work_list ? a.work_list[wi] : wi;
+        const long long rd = exact_work_read(a, wi);
         const long long off = a.offsets[rd];
         const int Lb = (int)(a.offsets[rd + 1] - off);
         const unsigned char* rp = a.reads + off;

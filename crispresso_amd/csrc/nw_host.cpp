@@ -149,6 +149,7 @@ struct nw_ctx {
     bool exact_tb_lds = true;
     bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
     bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
+    int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
@@ -887,9 +888,16 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.redo_flags = c->s->d_redo_flags.p;
             a.redo_blk = c->s->d_redo_blk.p;   // flags: the first level's walk writes every position's
         }
+        // a chunk whose first level hands on at most `direct` reads skips the second level on
+        // the device: the exact kernel takes them (CRISPR_NW_DIRECT=0: always both levels)
+        int direct = 1024;
+        if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
+        if (!two || only16) direct = 0;
+        c->redo_direct = direct;
         for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
             nw::KernelArgs al = a;
             al.band_last = only16;
+            al.redo_direct = lvl == 1 ? direct : 0;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
                 HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->cs));
@@ -912,6 +920,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
         a.work_count = c->s->d_fallback_count.p;
+        a.redo_direct = direct;
         HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
@@ -1019,6 +1028,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         cnt.band = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
         // second-level reads; a chunk run on the 32-diagonal level alone counts all its DP reads there
         if (c->diag16_fill.grid > 0) cnt.redo = c->skip16 ? cnt.band : c->s->d_fallback_count.p + 2;
+        cnt.direct = c->skip16 ? 0 : c->redo_direct;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n, c->s->d_blk.p,
@@ -1195,6 +1205,8 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
         return -1;
     int64_t total = 0;
     for (int64_t q = 0; q < passes; ++q) total += v[(size_t)(4 * q)];
+    // a skipped second level (KernelArgs::redo_direct): its reads went to the exact kernel
+    if (c->use_diag && c->diag16_fill.grid > 0 && c->redo_direct > 0 && v[2] <= c->redo_direct) total += v[2];
     return total;
 }
 
@@ -2000,8 +2012,10 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
     const bool two = c->diag16_fill.grid > 0;
     counts4[0] = c->n - need;             // exact copies (no DP)
     counts4[1] = two ? need : 0;          // first level (16 diagonals)
-    counts4[2] = two ? fb[2] : need;      // second level (32 diagonals)
-    counts4[3] = fb[0];                   // exact int32 kernel
+    // a skipped second level (KernelArgs::redo_direct) sent its reads to the exact kernel
+    const bool direct = two && c->redo_direct > 0 && fb[2] <= c->redo_direct;
+    counts4[2] = two ? (direct ? 0 : fb[2]) : need;   // second level (32 diagonals)
+    counts4[3] = fb[0] + (direct ? fb[2] : 0);        // exact int32 kernel
     return NW_OK;
 }
 

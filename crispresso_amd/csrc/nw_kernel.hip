@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wpb = blockDim.x >> 6;
-    const long long nwork = args.work_list ? (long long)*args.work_count : args.n;
+    const long long nwork = exact_work_count(args);
     // a work list shorter than the grid: blocks past its end leave before any set-up
     if (args.work_list && args.work_lo + (long long)blockIdx.x * wpb >= nwork) return;
 
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int pad_coff = NCODE_PAD * 64 * RP;   // offset of the all-zero pad code
 
     for (long long wi = (args.work_list ? args.work_lo : 0) + gw; wi < nwork; wi += nwaves) {
-        const long long rd = args.work_list ? args.work_list[wi] : wi;
+        const long long rd = exact_work_read(args, wi);
         const long long off = args.offsets[rd];
         const int Lb = (int)(args.offsets[rd + 1] - off);
         Stat* st = args.stats + rd;

@@ -84,8 +84,12 @@ __global__ __launch_bounds__(1024) void nw_ops_scan(int64_t* blk, int nblk, int6
         // the call's reads by path, summed over chunks (nw_batch_path_counts after nw_align_ops)
         long long fb = 0;
         for (int q = 0; cnt.fallback && q < cnt.passes; ++q) fb += cnt.fallback[4 * q];
+        // a chunk that skipped its second level (KernelArgs::redo_direct) sent the redo
+        // list to the exact kernel
+        const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
+        if (direct) fb += *cnt.redo;
         ctl[4] += fb;
-        if (cnt.redo) ctl[5] += *cnt.redo;
+        if (cnt.redo && !direct) ctl[5] += *cnt.redo;
         if (cnt.band) ctl[6] += *cnt.band;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];

@@ -316,5 +316,8 @@ def test_adaptive_levels_sorted_input(gpu_aligner_factory, monkeypatch):
     a.align_ops(buf, off)
     paths = a.path_counts()
     assert paths["band32"] > 5000                       # the HDR reads took the second level
-    assert paths["exact_kernel"] < 0.005 * (len(off) - 1)
+    # the exact kernel: the rare uncertified reads, plus the few (~0.3 %) first-level
+    # give-ups of the reference-like chunks (KernelArgs::redo_direct); the HDR chunks'
+    # tens of thousands stay on the second level
+    assert paths["exact_kernel"] < 0.01 * (len(off) - 1)
 

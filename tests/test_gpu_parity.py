@@ -416,17 +416,27 @@ def test_pooled_multi_amplicon(gpu_aligner_factory, oracle):
 
 # ---------------------------------------------------------------- certified band (nw_band.hip)
 
-def test_diag_is_default_and_certifies_c2(gpu_aligner_factory, oracle):
+@pytest.mark.parametrize("direct", ["0", None])
+def test_diag_is_default_and_certifies_c2(gpu_aligner_factory, oracle, monkeypatch, direct):
     """The default path is the certified diagonal band; on the C2 mix almost every
-    read is certified (no fallback) and all are bit-identical to the oracle."""
+    read is certified (no fallback) and all are bit-identical to the oracle.  With the
+    second level always run (CRISPR_NW_DIRECT=0) only the rare read neither band
+    certifies reaches the exact kernel; by default the first level's few give-ups
+    (~0.3 %) go there directly (KernelArgs::redo_direct)."""
+    if direct is not None:
+        monkeypatch.setenv("CRISPR_NW_DIRECT", direct)
     amp = synth.random_amplicon(250, 1)
     buf, off = synth.reads_from(amp, 4001, 2)
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
     assert a.geometry()["tb_mode"] == "diag-int16"
-    # only the rare uncertified read goes to the exact kernel
-    assert a.fallbacks() <= 4
+    paths = a.path_counts()
+    if direct == "0":
+        assert a.fallbacks() <= 4 and paths["band32"] > 0
+    else:
+        assert paths["band32"] == 0 and 0 < a.fallbacks() <= 0.01 * (len(off) - 1)
+    assert a.fallbacks() == paths["exact_kernel"]
     assert_same(oracle, amp, buf, off, batch, "diag-c2")
 
 
@@ -535,13 +545,17 @@ def test_diag_exact_copies(gpu_aligner_factory, oracle):
     assert_same(oracle, amp_n, buf, off, a.align_packed(buf, off), "exact-N")
 
 
-@pytest.mark.parametrize("levels", ["16+32", "32"])
+@pytest.mark.parametrize("levels", ["16+32", "32", "16+32 direct", "16+32 direct-small"])
 def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
     """The 16-diagonal first level hands what it cannot certify (indels of 8+,
     noisy and junk reads) to the 32-diagonal level, which hands the rest to the
-    exact kernel; with the first level off the 32-diagonal level sees every read."""
+    exact kernel; with the first level off the 32-diagonal level sees every read.
+    "direct": the second level skips itself on the device and the exact kernel takes
+    the first level's give-ups after its own list (threshold above / below the batch's
+    give-ups: both branches of KernelArgs::redo_direct)."""
     if levels == "32":
         monkeypatch.setenv("CRISPR_NW_DIAG16", "0")
+    monkeypatch.setenv("CRISPR_NW_DIRECT", {"16+32 direct": "100000", "16+32 direct-small": "1"}.get(levels, "0"))
     amp = synth.random_amplicon(250, 44)
     rng = np.random.Generator(np.random.PCG64(45))
     reads = synth.unpack(*synth.reads_from(amp, 1500, 46, synth.PARITY_MIX))
@@ -554,7 +568,16 @@ def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
     assert a.geometry()["tb_mode"] == "diag-int16"
+    paths = a.path_counts()
+    if levels == "16+32 direct":
+        assert paths["band32"] == 0 and paths["exact_kernel"] > 1
+    elif levels.startswith("16+32"):
+        assert paths["band32"] > 1
     assert_same(oracle, amp, buf, off, batch, f"levels={levels}")
+    if levels == "16+32 direct":   # ops output too (the chunked pipeline's counts)
+        ob = a.align_ops(buf, off)
+        assert a.path_counts()["band32"] == 0
+        assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "levels=direct ops")
 
 
 @pytest.mark.parametrize("levels", ["16+32", "32"])
@@ -586,11 +609,13 @@ def test_diag_iupac_in_every_pair_slot(gpu_aligner_factory, oracle, monkeypatch,
 
 
 @pytest.mark.parametrize("block", [6, 10, 12, 20])
-def test_diag_refined_certificate_clustered_mismatches(gpu_aligner_factory, oracle, block):
+def test_diag_refined_certificate_clustered_mismatches(gpu_aligner_factory, oracle, monkeypatch, block):
     """Reads with a block of mismatches (the HDR pass of CRISPResso: reference-derived
     reads against the HDR amplicon, CORE:1808-1828) fail the plain certificate; the
     refined one (gapped escapes pay the gap open, single diagonals scored exactly)
-    keeps most of them on the band.  Bit-exact either way."""
+    keeps most of them on the band.  Bit-exact either way.  (Both levels always run:
+    the counts below are the certificate's, not KernelArgs::redo_direct's.)"""
+    monkeypatch.setenv("CRISPR_NW_DIRECT", "0")
     amp = synth.random_amplicon(250, 4)
     hdr = synth.hdr_amplicon(amp, 4, 120, block)
     buf, off = synth.reads_from(amp, 1200, 5)
@@ -604,11 +629,12 @@ def test_diag_refined_certificate_clustered_mismatches(gpu_aligner_factory, orac
 
 
 @pytest.mark.parametrize("ops", [False, True])
-def test_iupac_amplicon_band_path(gpu_aligner_factory, oracle, ops):
+def test_iupac_amplicon_band_path(gpu_aligner_factory, oracle, monkeypatch, ops):
     """An amplicon with IUPAC codes (and a byte outside EDNAFULL) keeps the certified
     band path: its rows score from the table's EDNAFULL rows.  Reads from it (ACGT at
     the IUPAC positions, the parity mix of edits) equal the oracle, and few (~4 %) need
-    the exact kernel."""
+    the exact kernel (both levels always run: the certificate's count)."""
+    monkeypatch.setenv("CRISPR_NW_DIRECT", "0")
     base = synth.random_amplicon(250, 23)
     amp = list(base)
     for pos, code in zip((10, 57, 120, 121, 200, 233), "RYNKMS"):
