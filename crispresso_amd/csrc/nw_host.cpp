@@ -1511,6 +1511,21 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // sizes ramp up and down at both ends of the call (chunk / 4, chunk / 2, ...): the
     // first chunk's upload and the last chunk's records are the pipeline's serial head
     // and tail; every chunk in between is a full chunk
+    // ramp parts as divisors of the chunk, in call order (diagnostics: CRISPR_NW_RAMP_HEAD / _TAIL)
+    auto ramp = [&](const char* var, std::vector<int> dflt) {
+        const char* e = std::getenv(var);
+        if (!e) return dflt;
+        std::vector<int> v;
+        for (const char* p = e; *p;) {
+            const int d = std::atoi(p);
+            if (d > 0) v.push_back(d);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+        return v;
+    };
+    const std::vector<int> ramp_head = ramp("CRISPR_NW_RAMP_HEAD", {4, 2}), ramp_tail = ramp("CRISPR_NW_RAMP_TAIL", {2, 4});
+    const bool tuned_ramp = std::getenv("CRISPR_NW_RAMP_HEAD") || std::getenv("CRISPR_NW_RAMP_TAIL");
     auto sizes = [&](int64_t len) {
         std::vector<int64_t> v;
         if (len <= chunk) {
@@ -1519,11 +1534,26 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         std::vector<int64_t> head, tail;
         int64_t left = len;
-        for (int64_t part : {chunk / 4, chunk / 2}) {
-            if (part >= 1024 && left > 2 * (part + chunk)) {
+        if (!tuned_ramp)   // ramp parts in pairs (one at each end)
+            for (int64_t part : {chunk / 4, chunk / 2}) {
+                if (part >= 1024 && left > 2 * (part + chunk)) {
+                    head.push_back(part);
+                    tail.push_back(part);
+                    left -= 2 * part;
+                }
+            }
+        for (int d : tuned_ramp ? ramp_head : std::vector<int>{}) {
+            const int64_t part = chunk / d;
+            if (part >= 1024 && left > part + 2 * chunk) {
                 head.push_back(part);
+                left -= part;
+            }
+        }
+        for (auto it = ramp_tail.rbegin(); tuned_ramp && it != ramp_tail.rend(); ++it) {
+            const int64_t part = chunk / *it;
+            if (part >= 1024 && left > part + 2 * chunk) {
                 tail.push_back(part);
-                left -= 2 * part;
+                left -= part;
             }
         }
         for (int64_t x : head) v.push_back(x);
