@@ -1511,7 +1511,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // sizes ramp up and down at both ends of the call (chunk / 4, chunk / 2, ...): the
     // first chunk's upload and the last chunk's records are the pipeline's serial head
     // and tail; every chunk in between is a full chunk
-    // ramp parts as divisors of the chunk, in call order (diagnostics: CRISPR_NW_RAMP_HEAD / _TAIL)
+    // ramp parts as divisors of the chunk, in call order (diagnostics: CRISPR_NW_RAMP_HEAD / _TAIL, e.g. "8:4:2")
     auto ramp = [&](const char* var, std::vector<int> dflt) {
         const char* e = std::getenv(var);
         if (!e) return dflt;
@@ -1519,8 +1519,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         for (const char* p = e; *p;) {
             const int d = std::atoi(p);
             if (d > 0) v.push_back(d);
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
+            while (*p >= '0' && *p <= '9') ++p;
+            while (*p && (*p < '0' || *p > '9')) ++p;   // any separator (',' or ':')
         }
         return v;
     };
