@@ -554,7 +554,8 @@ def main():
                 legs[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
     traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                       "nw::nw_ops_", required="nw::nw_band_fill<16>")
+                                       "nw::nw_ops_", "nw::(anonymous namespace)::nw_ops_",
+                                       required="nw::nw_band_fill<16>")
     summ, summ_src = pmc_summary("nw_band_fill<16>")
     fill_valu = None
     if summ:
