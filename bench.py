@@ -19,6 +19,13 @@ read shard (reads are independent, no collective on the data
 path).  The timing barrier and the max-over-ranks run over a gloo process group
 on the host: this process never initialises torch's HIP runtime (libcrispr_nw.so
 owns the GPU).  value = N * 1M * K / max-over-ranks time of K steps ("weak").
+At every N the line also carries the two multi-GPU configs of BASELINE.json at
+their own shapes, timed the same way (barrier, max over ranks): "c4" (configs[3]:
+100M reads over the N GPUs, each rank aligning 100M / N reads of the C4 generator,
+seed 10 + rank, in calls of at most 12.5M reads; at N = 1 one 12.5M-read call,
+"c4_shard") and "pooled" (configs[4]: 96 amplicons x 100k reads split over the
+ranks by DP cells, crispresso_amd.distributed.cell_partition, one
+nw_align_multi_ops_packed call per rank).
 
 Extra keys: "kernel_rate" (the same kernels + compaction on the batch resident in
 HBM, HIP events), "pcie" (upload span and bytes each way of the timed call),
@@ -26,9 +33,10 @@ HBM, HIP events), "pcie" (upload span and bytes each way of the timed call),
 outside the timed region), "roofline" (HBM: algorithmic bytes per pass over the
 kernel-resident pass time; VALU: issue fraction of nw_band_fill<16>),
 "cpu_baseline" (the CPU oracle -- a port, EMBOSS is absent -- on bounded samples,
-1 thread and the box's CPU share, rank 0 at N = 1 only); legs either side of the
-path at N = 1: "dual_alignment" (C3, CORE:1808-1828), "pooled" (C5, 96 amplicons,
-CRISPRessoPooled.py:882-908), "downstream_quantification", "upstream_merge".
+1 thread and the process's CPU share, rank 0 at N = 1 only); legs either side of the
+path at N = 1: "e2e" (a 1M-read C2 FASTQ.gz through needle.align_reads to the
+DataFrame, CORE:1788-2000), "dual_alignment" (C3, CORE:1808-1828),
+"downstream_quantification", "upstream_merge".
 """
 from __future__ import annotations
 
@@ -46,10 +54,6 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md "Wave scheduling")
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
-# measured issue rate of the 8-byte VOP3 / VOP3P / DPP encodings the fill is made of:
-# 0.224 wave-instructions per SIMD per nominal 2.4 GHz cycle (scripts/ubench/issue_rate.hip,
-# profiles/r02_ubench/ubench_issue_rate.txt)
-VALU_ISSUE_MEASURED = 1024 * 2.4e9 * 0.224
 READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
@@ -59,8 +63,41 @@ PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
 AMPLICON_LEN = 250
 
 
+C4_TOTAL_READS = 100_000_000   # BASELINE.json configs[3]
+C4_CALL_READS = 12_500_000     # reads per call (100M / 8 GPUs: one call per rank at N = 8)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_share():
+    """(threads, detail): the CPUs this process may run on (sched_getaffinity), capped by the
+    cgroup's CPU quota when there is one (the GPU box shows the whole machine's CPUs to
+    os.cpu_count() and affinity, but gives a job a share of them)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, {"sched_getaffinity": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(),
+                 "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
 def dist_setup():
@@ -171,7 +208,7 @@ def sample_check(amplicon, buf, offsets, ob, every, threads):
                     "from the runs, vs oracle/nw_oracle.c on the same reads"}
 
 
-def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t):
+def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t, share_detail):
     from oracle import oracle_py
 
     t0 = time.perf_counter()
@@ -186,10 +223,12 @@ def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t):
         "cores": threads,
         "kind": "port",
         "one_thread": {"value": n_sample_1t / dt1, "cores": 1, "reads": n_sample_1t, "seconds": dt1},
+        "cpu_share": share_detail,
         "sample": f"first {n_sample} reads of the same synthetic C2 batch, CPU oracle (oracle/nw_oracle.c, scalar "
-                  f"Gotoh + traceback per read) on {threads} host threads (the box's CPU share; os.cpu_count() = "
-                  f"{os.cpu_count()}), {dt:.2f} s wall; one_thread: first {n_sample_1t} reads, 1 thread; EMBOSS "
-                  "needle itself is not installed on the box",
+                  f"Gotoh + traceback per read) on {threads} host threads (len(os.sched_getaffinity(0)) = "
+                  f"{share_detail['sched_getaffinity']}, capped by the cgroup CPU quota "
+                  f"{share_detail['cgroup_quota_cpus']}), {dt:.2f} s wall; one_thread: first {n_sample_1t} reads, "
+                  "1 thread; EMBOSS needle itself is not installed on the box",
     }
 
 
@@ -328,75 +367,227 @@ def dual_leg(al, n_reads, steps, warmup):
     return out
 
 
-def pooled_workload(n_amplicons, reads_per_amplicon):
+def timed_calls(dist, call, steps, warmup):
+    """warmup untimed calls, then `steps` timed ones between barriers; max over ranks (s)."""
+    for _ in range(warmup):
+        call()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    barrier(dist)
+    return max_over_ranks(dist, time.perf_counter() - t0)
+
+
+def pack_pinned(buf, offsets, threads):
+    """(PackedReads in pinned memory, its buffers): text batch -> 2 bits per base."""
+    from crispresso_amd import _lib
+    from crispresso_amd.aligner import PackedReads, pack_2bit
+
+    po = _lib.pinned_copy(offsets)
+    pp = _lib.PinnedBuffer((int(offsets[-1]) + 3) // 4 + 16, np.uint8)
+    pr = pack_2bit(buf, po.array, nthreads=threads, packed=pp.array)
+    return PackedReads(pr.packed, po.array, pr.exc_pos, pr.exc_byte), (po, pp)
+
+
+def c4_leg(al, amplicon, rank, world, dist, threads, steps, warmup, sample_every):
+    """BASELINE configs[3] (C4: 100M synthetic 250 bp reads over N GPUs, SURVEY 8d seeds 10 + g):
+    this rank aligns reads of the C4 generator, seed 10 + rank -- 100M / N of them in calls
+    of at most 12.5M reads (N > 1), or one 12.5M-read call, the N = 8 shard (N = 1, "c4_shard").
+    Inputs 2-bit packed in pinned memory before the timed region; outputs to pinned memory;
+    value = reads of all ranks / max-over-ranks time.  The native generator
+    (include/crispr_synth.h: the C2 mix, counter-based RNG) draws 12.5M reads in ~1 s."""
+    from crispresso_amd import _lib, synth
+
+    per_rank = C4_CALL_READS if world == 1 else C4_TOTAL_READS // world
+    ncalls = (per_rank + C4_CALL_READS - 1) // C4_CALL_READS
+    t0 = time.perf_counter()
+    batches, keep = [], []
+    scratch = np.empty(min(C4_CALL_READS, per_rank) * (len(amplicon) + 10), np.uint8)   # reads are <= La + 10
+    text = off = None
+    for k in range(ncalls):
+        m = min(C4_CALL_READS, per_rank - k * C4_CALL_READS)
+        text, off = synth.native_reads(amplicon, m, 10 + rank, first=k * C4_CALL_READS, buf=scratch)
+        pr, bufs = pack_pinned(text, off, threads)
+        batches.append(pr)
+        keep.append(bufs)
+    gen_s = time.perf_counter() - t0
+    m_out = min(C4_CALL_READS, per_rank)
+    out = (_lib.PinnedBuffer(m_out, _lib.STAT_DTYPE), _lib.PinnedBuffer(2 * m_out + 4096, np.uint32),
+           _lib.PinnedBuffer(m_out + 1, np.int64))
+    outs = tuple(b.array for b in out)
+    state = {}
+
+    def one_pass():
+        for pr in batches:
+            n = len(pr.offsets) - 1
+            state["ob"] = al.align_ops_packed(pr, out=(outs[0][:n], outs[1], outs[2][:n + 1]))
+
+    elapsed = timed_calls(dist, one_pass, steps, warmup)
+    pcie = al.ops_times()
+    ob = state["ob"]
+    check = None
+    if sample_every:
+        check = sample_check(amplicon, text, off, ob, sample_every, threads)
+    total = per_rank * world
+    res = {"metric": "aligned reads/s (C4: 100M synthetic 250 bp reads sharded across the GPUs)" if world > 1
+           else "aligned reads/s (C4 shard: 12.5M reads = 100M / 8 GPUs, one call, 1 GPU)",
+           "value": total * steps / elapsed, "unit": "aligned reads/s", "n_gpus": world,
+           "reads_per_rank": per_rank, "reads_total": total, "calls_per_rank": ncalls,
+           "ms_per_pass": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
+           "path_counts_last_call": al.path_counts(), "pcie_last_call": pcie, "sample_check_last_call": check,
+           "input_prep_s": gen_s,
+           "note": "pass = every call of this rank's share (inputs 2-bit packed in pinned host memory before the "
+                   "timed region; records + runs to pinned host memory); reads of the C4 generator (native, seed "
+                   "10 + rank, reads k*12.5M.. of its set for call k); barrier + max over ranks"}
+    for bufs in keep:
+        for b in bufs:
+            b.close()
+    for b in out:
+        b.close()
+    return res
+
+
+def pooled_workload(n_amplicons, reads_per_amplicon, lo=None, hi=None):
     """C5: 96 amplicons of U[150, 300] bp (seed 5), reads from each with the C2 mix
-    (seed 100 + g), grouped by amplicon as CRISPRessoPooled's demultiplexing leaves them."""
+    (native generator, seed 100 + g), grouped by amplicon as CRISPRessoPooled's
+    demultiplexing leaves them.  -> (amplicons, offsets of all reads, amplicon of each read,
+    bytes of reads [lo, hi) only (all by default))."""
     from crispresso_amd import synth
 
     amps = synth.pooled_amplicons(n_amplicons, 5)
-    bufs, lens = [], []
-    for g, amp in enumerate(amps):
-        b, o = synth.reads_from(amp, reads_per_amplicon, 100 + g)
-        bufs.append(b)
-        lens.append(np.diff(o))
-    lens = np.concatenate(lens)
+    lens = np.concatenate([np.diff(synth.native_offsets(a, reads_per_amplicon, 100 + g)) for g, a in enumerate(amps)])
     off = np.zeros(len(lens) + 1, np.int64)
     np.cumsum(lens, out=off[1:])
     which = np.repeat(np.arange(n_amplicons, dtype=np.int32), reads_per_amplicon)
-    return amps, np.concatenate(bufs), off, which
+    lo = 0 if lo is None else lo
+    hi = len(lens) if hi is None else hi
+    buf = np.empty(max(int(off[hi] - off[lo]), 1), np.uint8)
+    for g, amp in enumerate(amps):
+        a, b = max(lo, g * reads_per_amplicon), min(hi, (g + 1) * reads_per_amplicon)
+        if a < b:
+            seg = buf[off[a] - off[lo]:off[b] - off[lo]]
+            synth.native_reads(amp, b - a, 100 + g, first=a - g * reads_per_amplicon, buf=seg)
+    return amps, buf, off, which
 
 
-def pooled_leg(al, n_amplicons, reads_per_amplicon, steps, warmup):
-    """C5 on one GPU: one nw_align_multi_ops call over all amplicons' reads (pinned host
-    buffers in, records + runs out), next to the same number of C2 single-amplicon reads.
-    `al`: the headline's aligner (see dual_leg; 28.2 vs 24.4 ms per call with a second
-    context); the call leaves it without an amplicon."""
+def pooled_leg(al, rank, world, dist, n_amplicons, reads_per_amplicon, steps, warmup, threads, text_too):
+    """BASELINE configs[4] (C5: CRISPRessoPooled, 96 amplicons x 100k reads, 150-300 bp, over the
+    N GPUs): the reads are split by DP cells (distributed.cell_partition, the same split
+    align_pooled_sharded makes; CRISPRessoPooled.py:882-908 ran one CRISPResso per amplicon,
+    serially), each rank aligns its range with one nw_align_multi_ops_packed call (pinned
+    2-bit input).  value = all reads / max-over-ranks time.  `al` is the headline's context
+    (a second context's streams would share the hardware queues); the call leaves it
+    without an amplicon."""
     from crispresso_amd import _lib
+    from crispresso_amd.distributed import cell_partition, pooled_costs
 
-    amps, buf, off, which = pooled_workload(n_amplicons, reads_per_amplicon)
-    n = len(off) - 1
-    pb, po, pw = _lib.pinned_copy(buf), _lib.pinned_copy(off), _lib.pinned_copy(which)
-    stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
-    ops_off = _lib.PinnedBuffer(n + 1, np.int64)
-    ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
-    out = (stats.array, ops.array, ops_off.array)
-    from crispresso_amd.aligner import pack_2bit
+    from crispresso_amd import synth
 
-    for _ in range(warmup):
-        al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
+    amps = synth.pooled_amplicons(n_amplicons, 5)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        ob = al.align_multi_ops(amps, pb.array, po.array, pw.array, out=out)
-    dt_text = (time.perf_counter() - t0) / steps
-    text_pcie = al.ops_times()
-    text_ops = (ob.ops_off.copy(), ob.ops.copy(), stats.array.copy())
-    # the same batch 2-bit packed (what the headline's call takes): nw_align_multi_ops_packed
-    p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
-    pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
-    for _ in range(warmup):
-        al.align_multi_ops(amps, pr, None, pw.array, out=out)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ob = al.align_multi_ops(amps, pr, None, pw.array, out=out)
-    dt = (time.perf_counter() - t0) / steps
-    same = bool(np.array_equal(ob.ops_off, text_ops[0]) and np.array_equal(ob.ops, text_ops[1])
-                and np.array_equal(stats.array, text_ops[2]))
-    lens = np.diff(off)
-    amp_len = np.array([len(a) for a in amps])[which]
-    res = {"metric": "pooled aligned reads/s (C5: 96 amplicons x reads, 150-300 bp, 1 GPU)", "value": n / dt,
-           "unit": "aligned reads/s", "ms_per_step": dt * 1e3, "reads": n, "amplicons": n_amplicons,
-           "reads_per_amplicon": reads_per_amplicon, "mean_read_len": float(lens.mean()),
-           "cells_full_matrices": int((amp_len * lens).sum()), "path_counts": al.path_counts(),
-           "pcie": al.ops_times(), "runs_per_read": int(ob.ops_off[n]) / n,
-           "text_input": {"value": n / dt_text, "ms_per_step": dt_text * 1e3, "pcie": text_pcie,
-                          "same_output_as_packed": same},
-           "algo_bytes_per_step": int(lens.sum() + 3 * stats.array["aln_len"].astype(np.int64).sum() + 16 * n),
-           "note": "step = one nw_align_multi_ops_packed call (2-bit reads + exceptions in, pinned): every "
-                   "amplicon's tables uploaded once, reads (grouped by amplicon, as demultiplexed) pipelined in "
-                   "chunks of one amplicon each; text_input = nw_align_multi_ops on the text"}
-    for b in (pb, po, pw, stats, ops_off, ops, p_packed):
+    lens = np.concatenate([np.diff(synth.native_offsets(a, reads_per_amplicon, 100 + g)) for g, a in enumerate(amps)])
+    off_all = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off_all[1:])
+    which_all = np.repeat(np.arange(n_amplicons, dtype=np.int32), reads_per_amplicon)
+    parts = cell_partition(pooled_costs(amps, off_all, which_all), world)
+    lo, hi = parts[rank]
+    _, buf, _, _ = pooled_workload(n_amplicons, reads_per_amplicon, lo, hi)
+    off = off_all[lo:hi + 1] - off_all[lo]
+    which = which_all[lo:hi]
+    n = hi - lo
+    pr, bufs = pack_pinned(buf, off, threads)
+    pw = _lib.pinned_copy(which)
+    gen_s = time.perf_counter() - t0
+    out = (_lib.PinnedBuffer(n, _lib.STAT_DTYPE), _lib.PinnedBuffer(4 * n + 4096, np.uint32),
+           _lib.PinnedBuffer(n + 1, np.int64))
+    outs = tuple(b.array for b in out)
+    state = {}
+
+    def call():
+        state["ob"] = al.align_multi_ops(amps, pr, None, pw.array, out=outs)
+
+    elapsed = timed_calls(dist, call, steps, warmup)
+    ob = state["ob"]
+    res = {"metric": "pooled aligned reads/s (C5: 96 amplicons x 100k reads, 150-300 bp, over the GPUs)",
+           "value": len(lens) * steps / elapsed, "unit": "aligned reads/s", "n_gpus": world,
+           "ms_per_step": elapsed / steps * 1e3, "reads_total": int(len(lens)), "reads_this_rank": int(n),
+           "amplicons": n_amplicons, "reads_per_amplicon": reads_per_amplicon,
+           "partition": [[int(a), int(b)] for a, b in parts],
+           "cells_this_rank": int(pooled_costs(amps, off_all, which_all)[lo:hi].sum()),
+           "mean_read_len": float(lens.mean()), "path_counts": al.path_counts(), "pcie": al.ops_times(),
+           "runs_per_read": int(ob.ops_off[n]) / max(n, 1), "input_prep_s": gen_s,
+           "algo_bytes_this_rank": int((off[-1] - off[0]) + 3 * outs[0]["aln_len"].astype(np.int64).sum() + 16 * n),
+           "note": "step = one nw_align_multi_ops_packed call per rank on its cell_partition range (2-bit reads + "
+                   "exceptions in, pinned; every amplicon's tables uploaded once; chunks of one amplicon each); "
+                   "barrier + max over ranks"}
+    if text_too:   # the same call on the text: same records and runs
+        pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
+        packed_ops = (ob.ops_off.copy(), ob.ops[: int(ob.ops_off[n])].copy(), outs[0].copy())
+        t1 = time.perf_counter()
+        tob = al.align_multi_ops(amps, pb.array, po.array, pw.array)
+        dt = time.perf_counter() - t1
+        res["text_input"] = {"value": n / dt, "ms_per_step": dt * 1e3, "pcie": al.ops_times(),
+                             "same_output_as_packed": bool(np.array_equal(tob.ops_off, packed_ops[0])
+                                                           and np.array_equal(tob.ops, packed_ops[1])
+                                                           and np.array_equal(tob.stats, packed_ops[2]))}
+        pb.close()
+        po.close()
+    for b in bufs + (pw,) + out:
         b.close()
     return res
+
+
+def e2e_leg(al, amplicon, buf, offsets, threads, repeats=2):
+    """The product path end to end (CORE:1788-2000): a FASTQ.gz of the rank's 1M C2 reads through
+    needle.align_reads to the DataFrame parse_needle_output would build -- native ingest
+    (libdeflate + parallel parse + 2-bit packing into pinned memory), one nw_align_ops_packed
+    call, the DataFrame hand-off.  Reports the wall time and each stage's share."""
+    import gzip
+    import tempfile
+
+    from crispresso_amd.needle import AlignArgs, align_reads
+
+    n = len(offsets) - 1
+    tmp = tempfile.mkdtemp(prefix="crispr_e2e_")
+    path = os.path.join(tmp, "c2_reads.fastq.gz")
+    t0 = time.perf_counter()
+    seqs = bytes(buf).decode("ascii")
+    off = offsets.tolist()
+    qual = "I" * 400
+    with gzip.open(path, "wb", compresslevel=1) as f:
+        step = 100_000
+        for lo in range(0, n, step):
+            hi = min(n, lo + step)
+            f.write("".join(f"@SYN:1:FC{r // 65536}:1:{r % 65536}:{r} 1:N:0\n{seqs[off[r]:off[r + 1]]}\n+\n"
+                            f"{qual[: off[r + 1] - off[r]]}\n" for r in range(lo, hi)).encode("ascii"))
+    write_s = time.perf_counter() - t0
+    gz_bytes = os.path.getsize(path)
+    runs = []
+    rows = None
+    for _ in range(repeats):
+        tm = {}
+        t1 = time.perf_counter()
+        df = align_reads(AlignArgs(amplicon_seq=amplicon), path, aligner=al, timings=tm)
+        tm["wall_s"] = time.perf_counter() - t1
+        runs.append(tm)
+        rows = len(df)
+        del df
+    try:
+        os.remove(path)
+        os.rmdir(tmp)
+    except OSError:
+        pass
+    best = min(runs, key=lambda t: t["wall_s"])
+    return {"metric": "reads/s end to end (C2 FASTQ.gz -> DataFrame, needle.align_reads)",
+            "value": n / best["wall_s"], "unit": "reads/s", "reads": n, "rows": rows,
+            "seconds": best, "first_call_seconds": runs[0],
+            "aligner_call_ms": best["align_s"] * 1e3, "aligner_call_share": best["align_s"] / best["wall_s"],
+            "fastq_gz_bytes": gz_bytes, "write_s": write_s,
+            "note": "best of the runs; align_s = the nw_align_ops_packed call inside align_reads (pinned 2-bit batch "
+                    "from the ingest in, records + runs to pinned pool memory out); ingest_s = nw_fastq_read + "
+                    "nw_fastq_pack; dataframe_s = ops_to_dataframe; FASTQ.gz written with gzip level 1 outside the "
+                    "timing"}
 
 
 def merge_leg(device, n_pairs):
@@ -446,14 +637,17 @@ def main():
     ap.add_argument("--reads", type=int, default=READS_PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=300_000)
     ap.add_argument("--cpu-sample-1t", type=int, default=20_000)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
-                    help="threads of the CPU baseline (default: the box's CPU share, at most 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline and host packing (default: the process's CPU share: "
+                         "sched_getaffinity capped by the cgroup quota)")
     ap.add_argument("--sample-every", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="skip the oracle sample check of the timed batch")
+    ap.add_argument("--no-check", action="store_true", help="skip the oracle sample checks of the timed batches")
     ap.add_argument("--no-quant", action="store_true", help="skip the downstream quantification leg")
     ap.add_argument("--quant-cpu-sample", type=int, default=20_000)
-    ap.add_argument("--no-legs", action="store_true", help="skip the C3 / merge legs (N = 1 only)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the e2e / C3 / merge legs (N = 1 only)")
+    ap.add_argument("--no-multi", action="store_true", help="skip the C4 and pooled (C5) legs")
+    ap.add_argument("--multi-steps", type=int, default=3, help="timed passes of the C4 / pooled legs")
     ap.add_argument("--merge-pairs", type=int, default=1_000_000)
     ap.add_argument("--kernel-only", action="store_true",
                     help="profiling: only the kernel-resident pass (one launch of each kernel per step over the whole "
@@ -468,16 +662,19 @@ def main():
     from crispresso_amd import _lib, synth
     from crispresso_amd.aligner import GpuAligner
 
+    share, share_detail = cpu_share()
+    threads = args.cpu_threads or share
     amplicon = synth.random_amplicon(AMPLICON_LEN, 1)
     seed = 2 if world == 1 else 10 + rank
     t0 = time.perf_counter()
     buf, offsets = synth.reads_from(amplicon, args.reads, seed)
     n = len(offsets) - 1
-    log(f"[rank {rank}] generated {n} reads in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] generated {n} reads in {time.perf_counter() - t0:.1f}s; host threads {threads} {share_detail}")
 
     al = GpuAligner(local)
     al.set_reference(amplicon)
-    # the host batch and the outputs in pinned memory (an ingest pipeline reads FASTQ straight into such buffers)
+    # the host batch and the outputs in pinned memory (the native FASTQ ingest, nw_fastq_pack, hands the
+    # aligner exactly such a batch: the e2e leg)
     pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(offsets)
     p_packed = _lib.PinnedBuffer((int(offsets[-1]) + 3) // 4 + 16, np.uint8)
     p_stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
@@ -495,59 +692,77 @@ def main():
     from crispresso_amd.aligner import pack_2bit
 
     t1 = time.perf_counter()
-    pr = pack_2bit(pb.array, po.array, nthreads=args.cpu_threads, packed=p_packed.array)
+    pr = pack_2bit(pb.array, po.array, nthreads=threads, packed=p_packed.array)
     pack_s = time.perf_counter() - t1
-    for _ in range(args.warmup):
-        al.align_ops_packed(pr, out=out)
+    state = {}
 
-    barrier(dist)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ob = al.align_ops_packed(pr, out=out)   # synchronous: records + runs are in host memory
-    barrier(dist)
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    def headline_call():
+        state["ob"] = al.align_ops_packed(pr, out=out)   # synchronous: records + runs are in host memory
+
+    elapsed = timed_calls(dist, headline_call, args.steps, args.warmup)
+    ob = state["ob"]
     pcie = al.ops_times()
     n_runs = int(ob.ops_off[n])
+    call_counts = al.path_counts()
 
     if args.skip_kernel_pass:
         al.close()
         return
-    # the same call on the text (one byte per base over PCIe)
-    al.align_ops(pb.array, po.array, out=out)
+    # the timed call's own outputs against the oracle (before anything reuses the buffers)
+    check = None if args.no_check else sample_check(amplicon, buf, offsets, ob, args.sample_every, threads)
+
+    # the same call on the text (one byte per base over PCIe), into its own (pool) buffers
+    al.align_ops(pb.array, po.array)
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        ob_text = al.align_ops(pb.array, po.array, out=out)
+        ob_text = al.align_ops(pb.array, po.array)
     text_s = (time.perf_counter() - t1) / args.steps
     text_pcie = al.ops_times()
-    ob = ob_text                            # the same records and runs (the text call ran last)
+    text_same = bool(np.array_equal(ob_text.stats, ob.stats) and np.array_equal(ob_text.ops_off, ob.ops_off)
+                     and np.array_equal(ob_text.ops, ob.ops[:n_runs]))
+    del ob_text
 
     t1 = time.perf_counter()
-    ob.expand(amplicon, pb.array, po.array, nthreads=args.cpu_threads)
+    ob.expand(amplicon, pb.array, po.array, nthreads=threads)
     expand_s = time.perf_counter() - t1
-
-    check = None if args.no_check else sample_check(amplicon, buf, offsets, ob, args.sample_every, args.cpu_threads)
 
     kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
     geo["fallback_reads"] = counts["exact_kernel"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(amplicon, buf, offsets, min(args.cpu_sample, n), args.cpu_threads,
-                           min(args.cpu_sample_1t, n))
+        cpu = cpu_baseline(amplicon, buf, offsets, min(args.cpu_sample, n), threads, min(args.cpu_sample_1t, n),
+                           share_detail)
 
     quant = None
     if not args.no_quant:
         quant = quant_leg(al, amplicon, buf, offsets, n, args.steps, args.warmup, rank, world, args.quant_cpu_sample,
                           args.no_cpu)
 
-    legs = {"dual": None, "pooled": None, "merge": None}
+    # the multi-GPU configs at their own shapes (every rank takes part: barriers inside)
+    multi = {"c4": None, "pooled": None}
+    if not args.no_multi:
+        for name in multi:
+            try:   # never cost the bench line (the error is reported instead)
+                if name == "c4":
+                    al.set_reference(amplicon)
+                    multi[name] = c4_leg(al, amplicon, rank, world, dist, threads, args.multi_steps, 1,
+                                         0 if args.no_check else 1250)
+                else:
+                    multi[name] = pooled_leg(al, rank, world, dist, args.pooled_amplicons, args.pooled_reads,
+                                             args.multi_steps, 1, threads, text_too=world == 1)
+            except Exception as exc:
+                multi[name] = {"error": f"{type(exc).__name__}: {exc}"}
+
+    legs = {"e2e": None, "dual": None, "merge": None}
     if rank == 0 and world == 1 and not args.no_legs:
         for name in legs:
             try:   # informational legs: never cost the bench line
-                if name == "dual":
+                if name == "e2e":
+                    al.set_reference(amplicon)
+                    legs[name] = e2e_leg(al, amplicon, buf, offsets, threads)
+                elif name == "dual":
                     legs[name] = dual_leg(al, args.reads, args.steps, args.warmup)
-                elif name == "pooled":
-                    legs[name] = pooled_leg(al, args.pooled_amplicons, args.pooled_reads, 5, 2)
                 else:
                     legs[name] = merge_leg(local, args.merge_pairs)
             except Exception as exc:
@@ -563,6 +778,8 @@ def main():
     lens = np.diff(offsets)
     cells = band_cells(counts, AMPLICON_LEN, float(lens.mean()) if n else 0.0)
     pass_gbs = algo_bytes / (kms * 1e-3) / 1e9
+    ms_step = elapsed / args.steps * 1e3
+    call_gbs = algo_bytes / (ms_step * 1e-3) / 1e9
     fill_ms = phases["fill16_ms"]
     value = n * world * args.steps / elapsed
     if rank == 0:
@@ -573,7 +790,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -589,13 +806,14 @@ def main():
                 "parallelism": f"read shards x{world} (no collective on the data path; gloo host barrier)",
                 "kernel_geometry": geo,
             },
+            "path_counts": call_counts,
             "ingest_pack": {"ms": pack_s * 1e3, "bases_per_s": (int(offsets[-1]) - int(offsets[0])) / pack_s,
-                            "threads": args.cpu_threads, "exceptions": int(len(pr.exc_pos)),
-                            "note": "nw_pack_reads: the text batch -> 2 bits per base + exception list (host; part of "
-                                    "ingest, not in value)"},
+                            "threads": threads, "exceptions": int(len(pr.exc_pos)),
+                            "note": "nw_pack_reads: the text batch -> 2 bits per base + exception list (host; the "
+                                    "native FASTQ ingest does the same inside nw_fastq_pack, timed in e2e)"},
             "text_input": {"value": n / text_s, "ms_per_step": text_s * 1e3, "h2d_ms": text_pcie["h2d_ms"],
-                           "h2d_bytes": text_pcie["h2d_bytes"],
-                           "note": "nw_align_ops on the text batch (one byte per base over PCIe), same outputs"},
+                           "h2d_bytes": text_pcie["h2d_bytes"], "same_output_as_packed": text_same,
+                           "note": "nw_align_ops on the text batch (one byte per base over PCIe), own output buffers"},
             "pcie": {
                 "h2d_ms": pcie["h2d_ms"], "h2d_bytes": pcie["h2d_bytes"],
                 "h2d_gbs": pcie["h2d_bytes"] / max(pcie["h2d_ms"], 1e-9) / 1e6,
@@ -610,7 +828,7 @@ def main():
                 "note": "the call's kernels + ops compaction on the batch resident in HBM, outputs left in HBM "
                         "(HIP events on the aligner's stream)",
             },
-            "expand": {"ms": expand_s * 1e3, "reads_per_s": n / expand_s, "threads": args.cpu_threads,
+            "expand": {"ms": expand_s * 1e3, "reads_per_s": n / expand_s, "threads": threads,
                        "note": "nw_expand_ops: the three rows of every read rebuilt from its runs on the host "
                                "(not in value)"},
             "sample_check": check,
@@ -620,6 +838,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": pass_gbs / HBM_PEAK_GBS,
+                "call_achieved": call_gbs,
+                "call_frac": call_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the bench "
                                   "command, per pass of the band kernels + exact kernel + compaction)",
@@ -628,7 +848,8 @@ def main():
                           "certifies + nw_ops compaction",
                 "kernel_ms_avg": kms,
                 "achieved_def": "algorithmic bytes of the pass / its device time (HIP events on the aligner's "
-                                "stream, batch resident in HBM)",
+                                "stream, batch resident in HBM); call_achieved: the same bytes / ms_per_step (the "
+                                "whole call: PCIe both ways, host scan, every kernel)",
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",
                 "valu": {
@@ -638,23 +859,19 @@ def main():
                     "valu_source": summ_src,
                     "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
                     "issue_peak_per_s": VALU_ISSUE_PEAK,
-                    "issue_frac_measured_ceiling": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_MEASURED)
-                    if fill_valu and fill_ms else None,
-                    "issue_measured_ceiling_per_s": VALU_ISSUE_MEASURED,
                     "band_cells_per_pass": cells,
                     "band_gcups": cells / (kms * 1e-3) / 1e9,
                     "note": "issue_frac = SQ_INSTS_VALU of one fill<16> launch (PMC, chip total) / its live HIP-event "
-                            "time / (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); "
-                            "issue_frac_measured_ceiling: the same over the measured issue rate of the VOP3/VOP3P/"
-                            "DPP encodings the fill is made of (0.224 per SIMD per cycle, profiles/r02_ubench); "
-                            "band cells = "
+                            "time / (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); band cells = "
                             "cells the bands and the exact kernel actually compute (W x (La + Lb)/2 per read and "
                             "level), not the La x Lb matrices the certificate makes unnecessary",
                 },
             },
             "cpu_baseline": cpu,
+            "c4" if world > 1 else "c4_shard": multi["c4"],
+            "pooled": multi["pooled"],
+            "e2e": legs["e2e"],
             "dual_alignment": legs["dual"],
-            "pooled": legs["pooled"],
             "downstream_quantification": quant,
             "upstream_merge": legs["merge"],
         }

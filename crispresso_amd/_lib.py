@@ -29,7 +29,7 @@ NW_TIE_EMBOSS = 0
 NW_FLAG_EMPTY = 1
 NW_OUT_ROWS, NW_OUT_OPS = 0, 1
 NW_RUN_M, NW_RUN_X, NW_RUN_Y = 0, 1, 2
-TB_MODES = {0: "full-lds", 1: "full-global", 2: "band-lds", 4: "stream-int16", 5: "diag-int16"}
+TB_MODES = {0: "full-lds", 1: "full-global", 5: "diag-int16"}
 
 # Field order of nw_stat (include/crispr_nw.h).
 STAT_FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j", "flags")
@@ -46,7 +46,7 @@ EXPORTS = (
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
-    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat",
+    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat", "nw_fastq_pack",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -58,6 +58,9 @@ QUANT_EXPORTS = (
 
 # Every symbol include/crispr_flash.h declares.
 FLASH_EXPORTS = ("nwf_merge_batch", "nwf_last_error")
+
+# Every symbol include/crispr_synth.h declares (bench / test input generator).
+SYNTH_EXPORTS = ("nw_synth_offsets", "nw_synth_reads")
 NWF_COMBINED, NWF_OUTIE = 1, 2
 
 
@@ -143,6 +146,7 @@ def load() -> ctypes.CDLL:
         "nw_fastq_offsets": (c_void_p, [c_void_p]),
         "nw_fastq_names": (c_void_p, [c_void_p, POINTER(c_int64)]),
         "nw_fastq_free": (None, [c_void_p]),
+        "nw_fastq_pack": (c_int, [c_void_p, c_int32] + [POINTER(c_void_p)] * 4 + [POINTER(c_int64)]),
         "nw_align_ops_packed": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
                                         c_int64, c_void_p, c_void_p]),
         "nw_pack_reads": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
@@ -171,6 +175,10 @@ def load() -> ctypes.CDLL:
                             POINTER(c_float)]),
         "nwq_run_device": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                    c_void_p, POINTER(c_float)]),
+        "nw_synth_offsets": (c_int64, [c_char_p, c_int32, c_int64, c_int64, ctypes.c_uint64, c_void_p, c_void_p,
+                                        c_int32]),
+        "nw_synth_reads": (c_int, [c_char_p, c_int32, c_int64, c_int64, ctypes.c_uint64, c_void_p, c_void_p,
+                                   c_void_p, c_int32]),
         "nw_format_srspair": (
             c_int64,
             [c_void_p, c_int64, c_char_p, c_char_p, c_float, c_float, c_int32, c_int32, c_void_p, c_int64,
@@ -189,7 +197,7 @@ def exported_symbols() -> dict:
     """Map of each declared symbol to whether the loaded library exports it."""
     lib = load()
     out = {}
-    for name in EXPORTS + QUANT_EXPORTS + FLASH_EXPORTS:
+    for name in EXPORTS + QUANT_EXPORTS + FLASH_EXPORTS + SYNTH_EXPORTS:
         try:
             getattr(lib, name)
             out[name] = True
@@ -236,3 +244,80 @@ def pinned_copy(a: np.ndarray) -> PinnedBuffer:
     pb = PinnedBuffer(a.shape, a.dtype)
     pb.array[...] = a
     return pb
+
+
+class _Lease:
+    """One view of pinned memory handed out by :class:`PinnedPool`: numpy arrays made
+    from it (``np.asarray``) keep it alive through their ``base``; when the last one
+    goes the block returns to the pool (it is never freed while a view exists)."""
+
+    def __init__(self, pool: "PinnedPool", block: "PinnedBuffer", nbytes: int):
+        self._pool, self._block = pool, block
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "version": 3,
+                                    "data": (block._p, False)}
+
+    def __del__(self):  # pragma: no cover - runs at garbage collection
+        pool, block = getattr(self, "_pool", None), getattr(self, "_block", None)
+        if pool is not None and block is not None:
+            pool._release(block)
+
+
+class PinnedPool:
+    """Reusable page-locked blocks for the aligner's outputs (records, run offsets, runs).
+
+    A call's results must land in pinned memory for the copies to run at PCIe rate, but
+    page-locking a fresh buffer per call costs more than the call (hipHostMalloc of tens
+    of MB).  ``array(shape, dtype)`` leases a block at least that large (reusing a free
+    one); the block goes back to the pool when every array viewing it is gone, so results
+    a caller keeps are never overwritten.  Blocks are kept (not freed) for the process's
+    lifetime, up to ``keep_bytes`` of free blocks."""
+
+    def __init__(self, keep_bytes: int = 2 << 30):
+        import threading
+
+        self._free: list = []
+        self._keep = keep_bytes
+        self._mu = threading.Lock()
+
+    def array(self, shape, dtype) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+        nbytes = max(count * dtype.itemsize, 1)
+        with self._mu:
+            fits = [b for b in self._free if b.nbytes >= nbytes]
+            block = min(fits, key=lambda b: b.nbytes) if fits else None
+            if block is not None:
+                self._free.remove(block)
+        if block is None:
+            # rounded up (steps of 1/16 of the size) so a slightly bigger batch reuses the block
+            step = max(4096, 1 << max(0, nbytes.bit_length() - 4))
+            cap = (nbytes + step - 1) // step * step
+            block = PinnedBuffer(cap, np.uint8)
+            block.nbytes = cap
+        raw = np.asarray(_Lease(self, block, nbytes))
+        return raw[: count * dtype.itemsize].view(dtype).reshape(shape)
+
+    def _release(self, block: "PinnedBuffer") -> None:
+        with self._mu:
+            self._free.append(block)
+            total = sum(b.nbytes for b in self._free)
+            while total > self._keep and self._free:
+                big = max(self._free, key=lambda b: b.nbytes)
+                self._free.remove(big)
+                total -= big.nbytes
+                big.close()
+
+    def free_bytes(self) -> int:
+        with self._mu:
+            return sum(b.nbytes for b in self._free)
+
+
+_pool = None
+
+
+def pinned_pool() -> PinnedPool:
+    """The process-wide pool of pinned output blocks."""
+    global _pool
+    if _pool is None:
+        _pool = PinnedPool()
+    return _pool

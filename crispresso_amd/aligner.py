@@ -99,10 +99,11 @@ class OpsBatch:
     aligner call)."""
 
     def __init__(self, stats: np.ndarray, ops: np.ndarray, ops_off: np.ndarray, read_lens: Optional[np.ndarray],
-                 scale: int, awidth: int = 5000, offsets: Optional[np.ndarray] = None):
+                 scale: int, awidth: int = 5000, offsets: Optional[np.ndarray] = None, has_runs: bool = True):
         self.stats = stats             # structured, _lib.STAT_DTYPE
         self.ops = ops                 # uint32 runs
-        self.ops_off = ops_off         # int64 [n + 1]
+        self.ops_off = ops_off         # int64 [n + 1] (a records-only batch: the runs' offsets, no runs)
+        self.has_runs = has_runs
         self._read_lens = read_lens    # int64 [n]
         self._offsets = offsets
         self.scale = scale
@@ -176,6 +177,13 @@ def pack_2bit(buf: np.ndarray, offsets: np.ndarray, nthreads: int = 0, packed: O
             raise NeedleError(f"nw_pack_reads failed (code {rc})")
         return PackedReads(packed, offsets, pos[: cnt.value], byt[: cnt.value])
     raise NeedleError("nw_pack_reads: exception list kept growing")
+
+
+def _outputs(n: int, runs: bool = True):
+    """(stats, ops, ops_off) for an n-read call, leased from the pinned pool."""
+    pool = _lib.pinned_pool()
+    return (pool.array(n, _lib.STAT_DTYPE), pool.array(2 * n + 4096 if runs else 0, np.uint32),
+            pool.array(n + 1, np.int64))
 
 
 def default_output_mode() -> str:
@@ -329,7 +337,9 @@ class GpuAligner:
         """The call-level path (nw_align_ops): host reads in, records + runs out.
 
         ``out`` = (stats, ops, ops_off) preallocated (e.g. pinned) arrays; by default
-        they are allocated here.  An ops array too small for the batch is replaced.
+        they are leased from the process's pinned pool (:func:`_lib.pinned_pool`: the
+        copies back run at PCIe rate, and a block is reused once the returned arrays are
+        gone).  An ops array too small for the batch is replaced.
         ``resident``: align the batch this aligner's last call uploaded (still in HBM;
         ``buf`` unused) against the current amplicon (nw_align_ops_resident) -- the HDR
         pass over the same reads.  ``records_only``: no runs are copied back (a
@@ -338,9 +348,7 @@ class GpuAligner:
             raise NeedleError("no amplicon set")
         n = len(offsets) - 1
         if out is None:
-            stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
-            ops_off = np.zeros(n + 1, dtype=np.int64)
-            ops = np.empty(0 if records_only else 2 * n + 4096, dtype=np.uint32)
+            stats, ops, ops_off = _outputs(n, runs=not records_only)
         else:
             stats, ops, ops_off = out
 
@@ -355,12 +363,12 @@ class GpuAligner:
 
         rc = call(ops)
         if rc == _lib.NW_E_CAPACITY:   # rare: more runs than the buffer holds; run again with the size it said
-            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            ops = _lib.pinned_pool().array(int(ops_off[n]), np.uint32)
             rc = call(ops)
         self._check(rc, "nw_align_ops")
         if records_only:
-            return OpsBatch(stats, np.zeros(0, np.uint32), np.zeros(n + 1, np.int64), None, self.scale,
-                            self.options.awidth, offsets=offsets)
+            return OpsBatch(stats, np.zeros(0, np.uint32), ops_off, None, self.scale, self.options.awidth,
+                            offsets=offsets, has_runs=False)
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
 
     def align_ops_packed(self, pr: "PackedReads", out: Optional[tuple] = None) -> OpsBatch:
@@ -370,9 +378,7 @@ class GpuAligner:
         offsets = pr.offsets
         n = len(offsets) - 1
         if out is None:
-            stats = np.zeros(n, dtype=_lib.STAT_DTYPE)
-            ops_off = np.zeros(n + 1, dtype=np.int64)
-            ops = np.empty(2 * n + 4096, dtype=np.uint32)
+            stats, ops, ops_off = _outputs(n)
         else:
             stats, ops, ops_off = out
 
@@ -384,7 +390,7 @@ class GpuAligner:
 
         rc = call(ops)
         if rc == _lib.NW_E_CAPACITY:
-            ops = np.empty(int(ops_off[n]), dtype=np.uint32)
+            ops = _lib.pinned_pool().array(int(ops_off[n]), np.uint32)
             rc = call(ops)
         self._check(rc, "nw_align_ops_packed")
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)

@@ -1,6 +1,6 @@
 // nw_band.hip -- certified diagonal-band DP: the default aligner path.
 //
-// The stream kernels (nw_stream.hip) fill every cell of the La x Lb matrix.  A
+// The exact kernel (nw_kernel.hip) fills every cell of the La x Lb matrix.  A
 // CRISPResso read is a near-copy of its amplicon, so its optimal alignments stay
 // within a few diagonals of the main one.  These kernels fill only a band of
 // kBD = 32 diagonals [dlo, dlo + 31] around [min(0, Lb - La), max(0, Lb - La)]
@@ -37,11 +37,11 @@
 //     lane or its row neighbour one step back (DPP row_shr:1 / row_shl:1; the row
 //     edge reads -inf = outside the band).  Groups run at tau = t - dlo + kBK, so
 //     the step parity is wave-uniform;
-//   * biased recurrence as in nw_stream.hip: values carry + t * E, so X = max(Mo,
+//   * biased recurrence: values carry + t * E (t = anti-diagonal step), so X = max(Mo,
 //     X_left), Y = max(Mo, Y_up) with no "- extend"; the diagonal's + 2E is in
 //     the score table; Mo = M - (O - E);
-//   * 4 traceback bits per cell and read, 4 steps per dword: the same byte-plane
-//     packing as the stream kernels; per pair region: header, the M of each
+//   * 4 traceback bits per cell and read, 4 steps per dword (byte planes of the
+//     sign bits); per pair region: header, the M of each
 //     diagonal's last cell (= the last row / last column cells), bits in tiles
 //     [words / 4][lanes][4 words]: the fill writes 16 steps of a pair's lanes as one
 //     contiguous dwordx4 row, an M run of the walk reads 16 steps of its diagonal

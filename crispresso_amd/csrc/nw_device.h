@@ -35,26 +35,15 @@ struct KernelArgs {
     int64_t tb_wave_bytes;
     int32_t debug_mode;        // 0 = normal; diagnostic builds of the phases: 1 = stop after
                                // the start-cell search, 2 = stop after the traceback walk
-    // banded traceback storage (TB_BAND kernels)
-    int32_t band_slots;        // columns of traceback kept per lane
-    int64_t* fallback_list;    // reads whose traceback left the band are appended here
+    // exact kernel: reads whose walk failed are appended here (never with full storage)
+    int64_t* fallback_list;
     int32_t* fallback_count;
     // work list (full-storage kernel re-running the fallbacks); null = all reads
     const int64_t* work_list;
     const int32_t* work_count;
-    int32_t work_lo;           // first work-list entry this kernel takes (the one-wave kernel after the
-                               // multi-wave one: entries [0, exact grid) are the multi-wave kernel's)
-    int32_t* work_counter;     // dynamic chunk queue of the pair/stream kernels (zeroed per run)
-    // streaming kernels: per-pair traceback regions in HBM (StreamRegion layout)
-    uint8_t* region;
-    // pair-code score table (R <= 4): [36 code pairs][64 lanes][4 rows] packed
-    // int16x2 (read A's score low, read B's high) over the codes A T G C N and
-    // pad/unknown; null = per-read profile (any alphabet)
-    const uint32_t* ptab;
-    const uint8_t* lut6;       // [256] ascii -> 0..5 in that order, 6 = not in the table
-    // stream fill, per-read profile path: prof (int16) + 2 * gap_extend, the
-    // diagonal step of the (r + c) * extend biased recurrence (nw_stream.hip)
-    const int16_t* prof_fill;
+    int32_t work_lo;           // first work-list entry (or read, null list) this kernel takes (the one-wave
+                               // kernel after the multi-wave one: entries [0, exact grid) are the multi-wave kernel's)
+    const uint8_t* lut6;       // [256] ascii -> A T G C N pad in that order (0..5), 6 = other IUPAC code
     // certified diagonal-band kernels (nw_band.hip)
     const int32_t* band_order;     // read indices sorted by length; sorted positions 2g, 2g+1 = pair g
     int64_t band_pair_lo, band_pair_hi;   // pairs of this pass
@@ -121,7 +110,7 @@ __host__ __device__ inline long long exact_work_read(const KernelArgs& a, long l
 }
 
 // Traceback storage of a kernel instantiation.
-enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_BAND = 2, TB_STREAM = 4, TB_DIAG = 5 };
+enum TbMode : int { TB_LDS_FULL = 0, TB_GLOBAL_FULL = 1, TB_DIAG = 5 };
 
 struct LaunchCfg {
     int R;           // amplicon rows per lane
@@ -133,29 +122,11 @@ struct LaunchCfg {
 
 int rows_per_lane_for(int La);
 int profile_rp(int R);
-int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb);
+int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int wpb);
 int tb_bytes_per_wave(int R, int Lb_max);
 hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
-// streaming fill + walk kernels (nw_stream.hip).  Pair p's region starts at
-// region + p * stride: traceback band [8 lane groups][slots][8 lanes][NG] words, captures
-// (last-column Mo) [64 lanes][R], last amplicon row Mo [span] (both reads packed).
-constexpr int kStreamMinSpan = 64;   // stream columns per pair at least: at most one pair change per
-                                     // lane per 64-step block, few live descriptors
-constexpr int kStreamRunsCap = 512;  // traceback runs per read kept in LDS
-struct StreamRegion {
-    int64_t bits, caps, last, flags, stride;
-};
-constexpr int kPairCodes = 6;        // pair-table alphabet: A T G C N pad
-enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // read has a code outside the pair table
-int stream_fill_lds_bytes(int R, bool pair_table, int wpb);
-int stream_walk_lds_bytes(int La, int wpb);
-StreamRegion stream_region_for(int R, int band_slots, int Lb_max);
-// `after_fill` (may be null) is recorded between the two kernels.
-hipError_t launch_stream(const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                         hipEvent_t after_fill);
-hipError_t stream_occupancy(int R, bool pair_table, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds,
-                            int* fill_blocks, int* walk_blocks);
+enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // band pair header: read has a code outside A C G T N
 
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
@@ -193,18 +164,19 @@ hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_ld
 // ops compaction (nw_ops.hip): per-read slots -> one contiguous run array.
 // ctl (int64, kOpsCtl): [0] running base over the chunks of a call (in/out), [1] this chunk's
 // base, [2] this chunk's total, [3] errors (1: staging full, 2: spill area full, from
-// opsctl[1]); running over the call: [4] exact-kernel reads, [5] second band level reads,
-// [6] reads that needed the DP (OpsCounts: the device counters of the chunk's kernels).
+// opsctl[1]); running over the call: [4] exact-kernel reads, [5] second band level reads of
+// two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the second
+// level alone (OpsCounts: the device counters of the chunk's kernels).
 // blk: ceil(n / kOpsBlockReads) int64.  opsctl: the kernels' flags.  hctl: pinned host
 // copy of ctl written by the compaction (or null).
 constexpr int kOpsBlockReads = 1024;
 constexpr int kOpsCtl = 8;
 struct OpsCounts {
-    const int32_t* fallback;   // [4 * passes]: [4 q] exact-kernel reads of pass q
-    int passes;
+    const int32_t* fallback;   // [0]: exact-kernel reads of the chunk
     const int32_t* redo;       // second band level reads (null: one level)
     const int32_t* band;       // reads that needed the DP (null: not the band path)
     int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
+    int32_t one_level;         // the chunk ran the 32-diagonal level alone: its DP reads go to ctl[7]
 };
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
                               int64_t* blk, int64_t* ctl, int64_t* ops_off, uint32_t* staging, int64_t staging_cap,

@@ -1,7 +1,7 @@
 // nw_exact.hip -- exact int32 Gotoh/EDNAFULL aligner, one workgroup per read.
 //
 // Two uses:
-//   * amplicons longer than the band / stream / one-wave kernels take (1024 < La <=
+//   * amplicons longer than the band and one-wave kernels take (1024 < La <=
 //     8192 bp): every read of the batch goes through this kernel (configure_long in
 //     nw_host.cpp).  EMBOSS needle has no amplicon length limit; CRISPResso users
 //     with long amplicons (--needle_options_string) get the same

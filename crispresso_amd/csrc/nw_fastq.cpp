@@ -27,6 +27,13 @@
 // of integers is here); a record with an empty quality line is dropped (its numpy mean
 // is NaN).  A dropped record's name and bases are rolled back.  pass[] keeps every
 // record's verdict for the paired-end filter (by read id, in Python).
+//
+// nw_fastq_pack: the same reads as the aligner's packed input (nw_align_ops_packed: 2 bits
+// per base + exception list) and a copy of the offsets, in page-locked memory, built once
+// in parallel right after the parse -- what crosses PCIe (a quarter of the text's bytes)
+// is ready in pinned buffers when ingest returns; the text stays for the rows
+// (nw_expand_ops / the DataFrame hand-off).
+#include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -52,6 +59,21 @@ struct nw_fastq {
     std::vector<uint8_t> pass; // quality verdict of every record read (filtered reads only)
     int64_t dropped = 0;
     std::string err;
+    // nw_fastq_pack: packed bases, offsets copy, exceptions (pinned or malloc'd)
+    bool packed_done = false, packed_pinned = false;
+    uint8_t* pk = nullptr;
+    int64_t* pk_off = nullptr;
+    int64_t* exc_pos = nullptr;
+    uint8_t* exc_byte = nullptr;
+    int64_t n_exc = 0;
+    void* blocks[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~nw_fastq() {
+        for (void* b : blocks)
+            if (b) {
+                if (packed_pinned) (void)hipHostFree(b);
+                else std::free(b);
+            }
+    }
 };
 
 namespace {
@@ -489,5 +511,59 @@ const char* nw_fastq_names(const nw_fastq* q, int64_t* bytes) {
     return q->names.data();
 }
 void nw_fastq_free(nw_fastq* q) { delete q; }
+
+int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int64_t** offsets, const int64_t** exc_pos,
+                  const uint8_t** exc_byte, int64_t* n_exc) {
+    if (!q) return NW_E_INVALID;
+    if (q->packed_done && q->packed_pinned != (pinned != 0)) return NW_E_STATE;   // built the other way already
+    if (!q->packed_done) {
+        const int64_t n = (int64_t)q->offsets.size() - 1;
+        const int64_t nb = q->offsets.back();
+        auto get = [&](size_t bytes, int k) -> void* {
+            bytes = std::max<size_t>(bytes, 64);
+            void* p = nullptr;
+            if (pinned) {
+                if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
+            } else {
+                p = std::malloc(bytes);
+            }
+            q->blocks[k] = p;
+            return p;
+        };
+        q->packed_pinned = pinned != 0;
+        q->pk = (uint8_t*)get((size_t)(nb + 3) / 4 + 16, 0);
+        q->pk_off = (int64_t*)get(sizeof(int64_t) * (size_t)(n + 1), 1);
+        if (!q->pk || !q->pk_off) return NW_E_NOMEM;
+        std::memcpy(q->pk_off, q->offsets.data(), sizeof(int64_t) * (size_t)(n + 1));
+        // exceptions: N and other non-ACGT bytes, usually few; a second pass sizes a big list
+        int64_t cap = nb / 64 + 4096, got = 0;
+        std::vector<int64_t> pos((size_t)cap);
+        std::vector<uint8_t> byt((size_t)cap);
+        const int nt = nw_host::Pool::get().threads();
+        int rc = nw_pack_reads(q->seqs.data(), q->offsets.data(), n, q->pk, pos.data(), byt.data(), cap, &got, nt);
+        if (rc == NW_E_CAPACITY) {
+            cap = got;
+            pos.assign((size_t)cap, 0);
+            byt.assign((size_t)cap, 0);
+            rc = nw_pack_reads(q->seqs.data(), q->offsets.data(), n, q->pk, pos.data(), byt.data(), cap, &got, nt);
+        }
+        if (rc) return rc;
+        q->exc_pos = (int64_t*)get(sizeof(int64_t) * (size_t)got, 2);
+        q->exc_byte = (uint8_t*)get((size_t)got, 3);
+        if (!q->exc_pos || !q->exc_byte) return NW_E_NOMEM;
+        if (got) {
+            std::memcpy(q->exc_pos, pos.data(), sizeof(int64_t) * (size_t)got);
+            std::memcpy(q->exc_byte, byt.data(), (size_t)got);
+        }
+        q->n_exc = got;
+        q->packed_done = true;
+    }
+    if (packed) *packed = q->pk;
+    if (offsets) *offsets = q->pk_off;
+    if (exc_pos) *exc_pos = q->exc_pos;
+    if (exc_byte) *exc_byte = q->exc_byte;
+    if (n_exc) *n_exc = q->n_exc;
+    return NW_OK;
+}
 
 }  // extern "C"

@@ -54,14 +54,9 @@ struct DevBuf {
 // One amplicon's device tables (pointers into nw_ctx::d_arena).
 struct Profile {
     const int8_t* prof = nullptr;      // [NCODE][64][RP] int8: exact kernel
-    const int16_t* prof16 = nullptr;   // stream walk (rows padded on top)
-    const int16_t* prof16f = nullptr;  // stream fill: prof16 + 2 * extend (biased recurrence)
-    const uint32_t* ptab = nullptr;    // stream fill: pair-code score table (R <= 4)
     const uint32_t* rowpos = nullptr;  // band walk: codes each row scores > 0 against
     const uint8_t* amp = nullptr;      // amplicon bytes (+16 pad)
     int R = 0;
-    bool amp_in_table = false;         // amplicon within A C G T N (the band score table)
-    bool have_ptab = false;
 };
 
 // Device buffers of one chunk's kernels.  The pipelined calls alternate two sets on
@@ -70,8 +65,7 @@ struct Profile {
 struct Scratch {
     DevBuf<uint8_t> d_tb;              // exact kernel: traceback slabs when they do not fit LDS
     DevBuf<int64_t> d_fallback;        // reads re-run with full traceback storage
-    DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] work counter, [2] redo count
-    DevBuf<uint8_t> d_region;          // per-pair traceback regions of the streaming kernels
+    DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
     DevBuf<int32_t> d_redo_blk;
@@ -81,7 +75,7 @@ struct Scratch {
     DevBuf<int32_t> d_nops, d_opsctl;
     DevBuf<int64_t> d_blk;
     void release() {
-        d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_region.release(); d_redo.release();
+        d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_redo_blk.release(); d_order.release(); d_sort_hist.release(); d_sort_key.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release(); d_blk.release();
@@ -128,15 +122,7 @@ struct nw_ctx {
     DevBuf<int64_t> d_offsets;
     DevBuf<uint8_t> d_out;
     DevBuf<nw::Stat> d_stats;
-    int band_slots = 64;              // 0 disables the banded kernels
-    bool use_band = false;
-    bool use_stream = false;
-    int stream_slots = 56;
-    int64_t pass_reads = 0;            // reads per fill+walk pass (region memory bound)
-    nw::StreamRegion region{};
-    nw::LaunchCfg stream_fill{}, stream_walk{};
     nw::LaunchCfg cfg{};              // full-storage kernel
-    nw::LaunchCfg band_cfg{};         // banded kernel
     // certified diagonal-band kernels (nw_band.hip): the default path
     bool use_diag = false;
     nw::LaunchCfg diag_fill{}, diag_walk{};          // 32-diagonal level (the certificate's last resort)
@@ -195,35 +181,26 @@ int fail(nw_ctx* c, int code, const char* fmt, ...) {
                         "%s failed: %s", #expr, hipGetErrorString(e_));               \
     } while (0)
 
-// One amplicon's score tables (host side): the int8 profile of the exact kernel,
-// the int16 profiles and pair-code table of the stream kernels, the markup bits of
-// the band walk (codes each row scores > 0 against).
+// One amplicon's score tables (host side): the int8 profile of the exact kernel and
+// the markup bits of the band walk (codes each row scores > 0 against).
 struct AmpTables {
     int R = 0;
-    bool amp_in_table = true;   // amplicon within A C G T N / unknown (the band score table)
-    bool have_ptab = false;
     std::vector<int8_t> prof;
-    std::vector<int16_t> prof16, prof16f;
-    std::vector<uint32_t> ptab, rowpos;
+    std::vector<uint32_t> rowpos;
 };
 
-bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
+bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
     const int La = (int)ref.size();
     if (La > kMaxRef) return false;
-    // markup bits and the band alphabet test first: an amplicon longer than the
-    // one-wave kernels take (R = 0) has only these (the multi-wave kernel aligns it)
-    const int codes6[6] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
+    // markup bits first: an amplicon longer than the one-wave kernels take (R = 0) has
+    // only these (the multi-wave kernel aligns it)
     t->rowpos.resize((size_t)La);
-    t->amp_in_table = true;
     for (int ai = 0; ai < La; ++ai) {
         const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
         uint32_t m = 0;
         for (int code = 0; code < nw::NCODE; ++code)
             if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
         t->rowpos[(size_t)ai] = m;
-        bool in6 = false;
-        for (int x = 0; x < 6; ++x) in6 = in6 || codes6[x] == ca;
-        t->amp_in_table = t->amp_in_table && in6;
     }
     const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
@@ -236,43 +213,6 @@ bool amp_tables(const std::string& ref, int scale, int E, AmpTables* t) {
             int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * scale : 0;
             t->prof[(size_t)code * 64 * RP + (ai / R) * RP + ai % R] = (int8_t)s;
         }
-    }
-    // int16 profile of the stream kernels: rows padded on top so that the last
-    // amplicon row is the bottom row of the last lane
-    const int R4 = (R + 3) & ~3;
-    const int nl = (La + R - 1) / R, F = nl * R - La;
-    t->prof16.assign((size_t)nw::NCODE * 64 * R4, 0);
-    for (int ai = 0; ai < La; ++ai) {
-        const uint8_t ca = nw::code_of((unsigned char)ref[ai]);
-        const int g = ai + F;
-        for (int code = 0; code < nw::NCODE; ++code) {
-            int s = (ca < 16 && code < 16) ? nw::kEdna[ca][code] * scale : 0;
-            t->prof16[(size_t)code * 64 * R4 + (g / R) * R4 + g % R] = (int16_t)s;
-        }
-    }
-    // The stream fill runs the recurrence on values biased by (r + c) * extend
-    // (nw_stream.hip): the diagonal step then gains 2 * extend, folded into its
-    // scores here.  prof16 itself stays unbiased (walk).
-    t->prof16f.resize(t->prof16.size());
-    for (size_t q = 0; q < t->prof16.size(); ++q) t->prof16f[q] = (int16_t)(t->prof16[q] + 2 * E);
-    // pair-code table of the stream kernel: for every (code of read A, code of
-    // read B) over A T G C N pad, each lane's 4 rows as packed int16x2 (biased)
-    t->have_ptab = false;
-    t->ptab.clear();
-    if (R4 == 4) {
-        const int codes[nw::kPairCodes] = {0, 1, 2, 3, 14, nw::NCODE_PAD};
-        t->ptab.assign((size_t)nw::kPairCodes * nw::kPairCodes * 64 * 4, 0u);
-        for (int ia = 0; ia < nw::kPairCodes; ++ia)
-            for (int ib = 0; ib < nw::kPairCodes; ++ib)
-                for (int ln = 0; ln < 64; ++ln)
-                    for (int k = 0; k < 4; ++k) {
-                        const size_t src = (size_t)ln * R4 + k;
-                        const uint16_t sa = (uint16_t)t->prof16f[(size_t)codes[ia] * 64 * R4 + src];
-                        const uint16_t sb = (uint16_t)t->prof16f[(size_t)codes[ib] * 64 * R4 + src];
-                        t->ptab[(((size_t)ia * nw::kPairCodes + ib) * 64 + ln) * 4 + k] = sa | ((uint32_t)sb << 16);
-                    }
-        const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
-        t->have_ptab = !(pt && std::strcmp(pt, "0") == 0);
     }
     return true;
 }
@@ -289,8 +229,8 @@ int upload_shared(nw_ctx* c) {
     std::vector<uint8_t> lut6(256), lut(256);
     for (int q = 0; q < 256; ++q) {
         const int code = nw::code_of((unsigned char)q);
-        int r = nw::kPairCodes;
-        for (int i = 0; i < nw::kPairCodes; ++i)
+        int r = 6;
+        for (int i = 0; i < 6; ++i)
             if (codes6[i] == code) r = i;
         lut6[(size_t)q] = (uint8_t)r;
         lut[(size_t)q] = (uint8_t)code;
@@ -328,9 +268,8 @@ int upload_shared(nw_ctx* c) {
 
 // Every amplicon's tables in one device arena (one upload): profs[g] points into it.
 int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector<Profile>* profs) {
-    // the tables depend on the amplicons, the scaled extend penalty and the pair-table switch
-    const char* pt = std::getenv("CRISPR_NW_PAIR_TABLE");
-    const std::string key = std::to_string(c->scale) + "/" + std::to_string(c->gap_extend) + "/" + (pt ? pt : "");
+    // the tables depend on the amplicons and the score scale
+    const std::string key = std::to_string(c->scale);
     if (key == c->arena_key && refs == c->arena_refs && c->d_arena.p) {
         *profs = c->arena_profs;
         return NW_OK;
@@ -343,24 +282,20 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         total += (bytes + 255) & ~(size_t)255;
         return at;
     };
-    struct Off { size_t prof, prof16, prof16f, ptab, rowpos, amp; };
+    struct Off { size_t prof, rowpos, amp; };
     std::vector<Off> offs(refs.size());
     for (size_t g = 0; g < refs.size(); ++g) {
-        if (!amp_tables(refs[g], c->scale, c->gap_extend, &tabs[g]))
+        if (!amp_tables(refs[g], c->scale, &tabs[g]))
             return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", (int)refs[g].size(), kMaxRef);
         const AmpTables& t = tabs[g];
-        const size_t o1 = sec(t.prof.size()), o2 = sec(t.prof16.size() * 2), o3 = sec(t.prof16f.size() * 2);
-        const size_t o4 = sec(t.ptab.size() * 4), o5 = sec(t.rowpos.size() * 4), o6 = sec(refs[g].size() + 16);
-        offs[g] = {o1, o2, o3, o4, o5, o6};
+        const size_t o1 = sec(t.prof.size()), o5 = sec(t.rowpos.size() * 4), o6 = sec(refs[g].size() + 16);
+        offs[g] = {o1, o5, o6};
     }
     std::vector<uint8_t> host(std::max<size_t>(total, 256), 0);
     for (size_t g = 0; g < refs.size(); ++g) {
         const AmpTables& t = tabs[g];
         const Off& o = offs[g];
         std::memcpy(host.data() + o.prof, t.prof.data(), t.prof.size());
-        std::memcpy(host.data() + o.prof16, t.prof16.data(), t.prof16.size() * 2);
-        std::memcpy(host.data() + o.prof16f, t.prof16f.data(), t.prof16f.size() * 2);
-        if (!t.ptab.empty()) std::memcpy(host.data() + o.ptab, t.ptab.data(), t.ptab.size() * 4);
         std::memcpy(host.data() + o.rowpos, t.rowpos.data(), t.rowpos.size() * 4);
         std::memcpy(host.data() + o.amp, refs[g].data(), refs[g].size());
     }
@@ -373,14 +308,9 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         uint8_t* b = c->d_arena.p;
         Profile& p = (*profs)[g];
         p.prof = (const int8_t*)(b + o.prof);
-        p.prof16 = (const int16_t*)(b + o.prof16);
-        p.prof16f = (const int16_t*)(b + o.prof16f);
-        p.ptab = tabs[g].ptab.empty() ? nullptr : (const uint32_t*)(b + o.ptab);
         p.rowpos = (const uint32_t*)(b + o.rowpos);
         p.amp = b + o.amp;
         p.R = tabs[g].R;
-        p.amp_in_table = tabs[g].amp_in_table;
-        p.have_ptab = tabs[g].have_ptab && p.ptab;
     }
     c->arena_refs = refs;
     c->arena_profs = *profs;
@@ -406,7 +336,7 @@ int64_t stride_for(int La, int32_t lb_max) { return ((int64_t)La + lb_max + 15) 
 // read, as many workgroups as the CUs hold.
 int configure_long(nw_ctx* c) {
     const int La = (int)c->ref.size();
-    c->use_band = c->use_stream = c->use_diag = false;
+    c->use_diag = false;
     c->diag16_fill.grid = 0;
     c->cfg = nw::LaunchCfg{};
     c->exact_tb_lds = true;
@@ -435,8 +365,6 @@ int configure_long(nw_ctx* c) {
 }
 
 int configure(nw_ctx* c) {
-    if (const char* bs = std::getenv("CRISPR_NW_BAND_SLOTS"))   // tests: band width of the full-matrix kernels
-        c->band_slots = c->stream_slots = std::max(0, std::atoi(bs));
     const int La = (int)c->ref.size();
     const int R = c->cur.R;
     c->exact_full = false;
@@ -447,7 +375,7 @@ int configure(nw_ctx* c) {
     cfg.tb_mode = nw::TB_GLOBAL_FULL;
     cfg.wpb = 4;
     for (int wpb : {4, 2, 1}) {
-        int b = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_LDS_FULL, 0, wpb);
+        int b = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_LDS_FULL, wpb);
         if (b > 0 && b <= kMaxLds) {
             cfg.tb_mode = nw::TB_LDS_FULL;
             cfg.wpb = wpb;
@@ -462,7 +390,7 @@ int configure(nw_ctx* c) {
         cfg.tb_mode = nw::TB_GLOBAL_FULL;
         cfg.wpb = 4;
     }
-    if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, 0, cfg.wpb);
+    if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, cfg.wpb);
     if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
         return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel", c->lb_max);
     int per_cu = std::max(1, std::min(8, kMaxLds / cfg.lds_bytes));
@@ -493,34 +421,16 @@ int configure(nw_ctx* c) {
             grid = std::max(1, std::min(grid, std::atoi(eg)));
         if (c->exact_lds > 0 && c->exact_lds <= kMaxLds) c->exact_grid = grid;
     }
-    // banded kernel
-    c->use_band = false;
-    if (c->band_slots > 0) {
-        nw::LaunchCfg b{};
-        b.R = R;
-        b.tb_mode = nw::TB_BAND;
-        b.wpb = 4;
-        b.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_BAND, c->band_slots, b.wpb);
-        if (b.lds_bytes > 0 && b.lds_bytes <= kMaxLds) {
-            per_cu = std::max(1, std::min(8, kMaxLds / b.lds_bytes));
-            const int64_t want = (c->n + b.wpb - 1) / b.wpb;
-            b.grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)c->num_cus * per_cu));
-            c->band_cfg = b;
-            c->use_band = true;
-        }
-    }
-    // -endweight: the band certificate and the stream kernels assume free end gaps;
-    // every read goes through the exact kernel (nw_align_kernel), which takes both
+    // -endweight: the band certificate assumes free end gaps; every read goes through
+    // the exact kernel (nw_align_kernel), which takes both
     if (c->end_weight) {
-        c->use_band = c->use_stream = c->use_diag = false;
+        c->use_diag = false;
         c->diag16_fill.grid = 0;
         HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
         HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
         return NW_OK;
     }
-    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" | "stream" | "band" | "full" (tests/diagnostics)
-    const int64_t hi = 5ll * c->scale * La;
-    const bool fits16 = hi + c->gap_extend < 16000 && 9ll * c->scale * La + c->gap_open + c->gap_extend < 32000;
+    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" (default) | "full" (tests/diagnostics)
     // certified diagonal band (default): scores and biases within int16, amplicon
     // within the band table's alphabet, non-negative gap costs (the certificate)
     c->use_diag = false;
@@ -577,49 +487,8 @@ int configure(nw_ctx* c) {
             c->use_diag = true;
         }
     }
-    // streaming fill + walk kernels (when the certified band does not apply)
-    c->use_stream = false;
-    const bool want_stream = !kern || std::strcmp(kern, "stream") == 0;
-    // the stream fill's values carry a bias of up to (rows + span) * extend
-    const int64_t nl_rows = (int64_t)((La + R - 1) / R) * R;
-    const int64_t bias_max = (nl_rows + std::max<int64_t>(c->lb_max, 64) + 8) * c->gap_extend;
-    const bool fits16s = fits16 && hi + bias_max + c->gap_open < 16000;
-    if (want_stream && fits16s && c->stream_slots > 0 && !c->use_diag) {
-        nw::LaunchCfg f{}, w{};
-        f.R = w.R = R;
-        f.tb_mode = w.tb_mode = nw::TB_STREAM;
-        // fill: waves per block that maximise resident waves (the pair table is
-        // 36 KB of LDS per block, so bigger blocks share it among more waves)
-        w.wpb = 8;
-        w.lds_bytes = nw::stream_walk_lds_bytes(La, w.wpb);
-        int fb = 0, wb = 0, best = -1;
-        for (int wpb : {4, 8, 10}) {
-            const int lds = nw::stream_fill_lds_bytes(R, c->cur.have_ptab, wpb);
-            int b = 0, wb2 = 0;
-            HIP_OR_FAIL(c, nw::stream_occupancy(R, c->cur.have_ptab, wpb, w.wpb, lds, w.lds_bytes, &b, &wb2));
-            if (b * wpb > best) { best = b * wpb; fb = b; wb = wb2; f.wpb = wpb; f.lds_bytes = lds; }
-        }
-        if (fb > 0 && wb > 0) {
-            const int64_t pairs = (c->n + 1) / 2;
-            f.grid = (int)std::max<int64_t>(1, std::min<int64_t>((pairs + f.wpb - 1) / f.wpb, (int64_t)c->num_cus * fb));
-            w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + w.wpb - 1) / w.wpb, (int64_t)c->num_cus * wb));
-            if (const char* g = std::getenv("CRISPR_NW_STREAM_GRID"))   // tests: few long streams
-                f.grid = std::max(1, std::min(f.grid, std::atoi(g)));
-            c->region = nw::stream_region_for(R, c->stream_slots, c->lb_max);
-            int64_t cap_bytes = 16ll << 30;
-            if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
-            int64_t pass_pairs = std::max<int64_t>(1, std::min<int64_t>(pairs, cap_bytes / c->region.stride));
-            c->pass_reads = 2 * pass_pairs;
-            HIP_OR_FAIL(c, c->s->d_region.reserve((size_t)(pass_pairs * c->region.stride + 64 * 1024)));
-            c->stream_fill = f;
-            c->stream_walk = w;
-            c->use_stream = true;
-        }
-    }
-    if (kern && std::strcmp(kern, "full") == 0) c->use_band = false;
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    const int64_t passes = c->use_stream ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
-    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve((size_t)(4 * passes)));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
     return NW_OK;
 }
 
@@ -818,7 +687,6 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.offsets = c->d_offsets.p + base;
     a.n = c->n;
     a.prof = c->cur.prof;
-    a.ptab = nullptr;
     a.lut6 = nullptr;
     a.lut = c->d_lut.p;
     a.amp = c->cur.amp;
@@ -836,7 +704,6 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.end_open = c->end_open;
     a.end_extend = c->end_extend;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
-    a.band_slots = c->band_slots;
     a.fallback_list = c->s->d_fallback.p + base;
     a.fallback_count = c->s->d_fallback_count.p;
     if (c->out_mode == NW_OUT_OPS) {
@@ -924,63 +791,14 @@ int launch_range(nw_ctx* c, int64_t base) {
         HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
-    if (c->use_stream) {
-        // passes of at most pass_reads reads (the per-pair regions of one pass stay resident)
-        const int64_t passes = std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads);
-        HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * passes * sizeof(int32_t), c->cs));
-        for (int64_t q = 0; q < passes && c->n > 0; ++q) {
-            const int64_t lo = q * c->pass_reads, hi = std::min(c->n, lo + c->pass_reads);
-            nw::KernelArgs ap = a;
-            ap.offsets = a.offsets + lo;
-            ap.n = hi - lo;
-            ap.out = a.out ? a.out + lo * 3 * c->stride : nullptr;
-            ap.stats = a.stats + lo;
-            if (a.ops) {
-                ap.ops = a.ops + lo * a.ops_slot;
-                ap.nops = a.nops + lo;
-            }
-            ap.prof = (const int8_t*)c->cur.prof16;
-            ap.prof_fill = c->cur.prof16f;
-            ap.band_slots = c->stream_slots;
-            ap.region = c->s->d_region.p;
-            ap.ptab = c->cur.have_ptab ? c->cur.ptab : nullptr;
-            ap.lut6 = c->d_lut6.p;
-            ap.fallback_list = a.fallback_list + lo;
-            ap.fallback_count = c->s->d_fallback_count.p + 4 * q;
-            ap.work_counter = ap.fallback_count + 1;
-            HIP_OR_FAIL(c, nw::launch_stream(ap, c->stream_fill, c->stream_walk, c->cs, q == 0 ? c->ev_fill : nullptr));
-            if (q == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
-            nw::KernelArgs af = a;
-            af.offsets = ap.offsets;
-            af.n = ap.n;
-            af.out = ap.out;
-            af.stats = ap.stats;
-            af.ops = ap.ops;
-            af.nops = ap.nops;
-            af.work_list = ap.fallback_list;    // exact int32 kernel on what left the band
-            af.work_count = ap.fallback_count;
-            HIP_OR_FAIL(c, launch_work(c, af));
-        }
-        return NW_OK;
-    }
     HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
-    a.work_counter = c->s->d_fallback_count.p + 1;
     if (c->exact_full) {   // long amplicon: every read through the multi-wave kernel
         if (c->n > 0)
             HIP_OR_FAIL(c, nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, false,
                                             c->cs));
         return NW_OK;
     }
-    if (c->n > 0) {
-        if (c->use_band) {
-            HIP_OR_FAIL(c, nw::launch(a, c->band_cfg, c->cs));
-            a.work_list = a.fallback_list;
-            a.work_count = c->s->d_fallback_count.p;
-            HIP_OR_FAIL(c, launch_work(c, a));
-        } else {
-            HIP_OR_FAIL(c, nw::launch(a, c->cfg, c->cs));
-        }
-    }
+    if (c->n > 0) HIP_OR_FAIL(c, launch_work(c, a));   // every read (null work list)
     return NW_OK;
 }
 
@@ -1023,11 +841,12 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (prev_done) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, prev_done, 0));
     nw::OpsCounts cnt{};
     cnt.fallback = c->s->d_fallback_count.p;
-    cnt.passes = (c->use_stream && !c->use_diag) ? (int)std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
     if (c->use_diag && c->n > 0) {
         cnt.band = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-        // second-level reads; a chunk run on the 32-diagonal level alone counts all its DP reads there
-        if (c->diag16_fill.grid > 0) cnt.redo = c->skip16 ? cnt.band : c->s->d_fallback_count.p + 2;
+        // second-level reads of a two-level chunk; a chunk run on the 32-diagonal level alone
+        // counts its DP reads apart (ctl[7]: the adaptive choice reads two-level chunks only)
+        if (c->diag16_fill.grid > 0 && !c->skip16) cnt.redo = c->s->d_fallback_count.p + 2;
+        cnt.one_level = c->diag16_fill.grid > 0 && c->skip16;
         cnt.direct = c->skip16 ? 0 : c->redo_direct;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
@@ -1157,7 +976,7 @@ int nw_batch_kernel_times(nw_ctx* c, float* fill_ms, float* walk_ms, float* rest
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     float total = 0.0f, f = 0.0f, w = 0.0f;
     HIP_OR_FAIL(c, hipEventElapsedTime(&total, c->ev0, c->ev1));
-    if ((c->use_stream || c->use_diag) && c->n > 0) {
+    if (c->use_diag && c->n > 0) {
         HIP_OR_FAIL(c, hipEventElapsedTime(&f, c->ev0, c->ev_fill));
         HIP_OR_FAIL(c, hipEventElapsedTime(&w, c->ev_fill, c->ev_walk));
     } else {
@@ -1183,8 +1002,7 @@ int nw_batch_device_output(nw_ctx* c, void** d_aln, int64_t* stride, void** d_st
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;
-    const nw::LaunchCfg& k = c->use_diag ? c->diag_fill : c->use_stream ? c->stream_fill
-                             : (c->use_band ? c->band_cfg : c->cfg);
+    const nw::LaunchCfg& k = c->use_diag ? c->diag_fill : c->cfg;
     if (rows_per_lane) *rows_per_lane = k.R;
     if (waves_per_block) *waves_per_block = k.wpb;
     if (grid) *grid = k.grid;
@@ -1198,13 +1016,11 @@ int64_t nw_batch_fallbacks(nw_ctx* c) {
     if (!c || !c->ran) return -1;
     (void)hipSetDevice(c->device);
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
-    if (!(c->use_band || c->use_stream || c->use_diag)) return 0;
-    const int64_t passes = (c->use_stream && !c->use_diag) ? std::max<int64_t>(1, (c->n + c->pass_reads - 1) / c->pass_reads) : 1;
-    std::vector<int32_t> v((size_t)(4 * passes));
+    if (!c->use_diag) return 0;
+    std::vector<int32_t> v(4);
     if (hipMemcpy(v.data(), c->s->d_fallback_count.p, v.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
-    int64_t total = 0;
-    for (int64_t q = 0; q < passes; ++q) total += v[(size_t)(4 * q)];
+    int64_t total = v[0];
     // a skipped second level (KernelArgs::redo_direct): its reads went to the exact kernel
     if (c->use_diag && c->diag16_fill.grid > 0 && c->redo_direct > 0 && v[2] <= c->redo_direct) total += v[2];
     return total;
@@ -1412,29 +1228,24 @@ struct HostTimer {
 // geometry): a pooled call configures every group once up front and restores these
 // per chunk instead of re-running configure (its occupancy queries are host API calls).
 struct CfgState {
-    nw::LaunchCfg cfg, band_cfg, diag_fill, diag_walk, diag16_fill, diag16_walk, stream_fill, stream_walk;
-    bool use_band, use_diag, use_stream, exact_tb_lds, exact_full;
-    int exact_grid, exact_lds, diag_words, diag_lb_cap, diag_sort_grid, band_slots, stream_slots;
-    int64_t exact_slab, diag16_pass_pairs, diag16_stride, diag_pass_pairs, diag_stride, pass_reads, stride;
-    nw::StreamRegion region;
+    nw::LaunchCfg cfg, diag_fill, diag_walk, diag16_fill, diag16_walk;
+    bool use_diag, exact_tb_lds, exact_full;
+    int exact_grid, exact_lds, diag_words, diag_lb_cap, diag_sort_grid;
+    int64_t exact_slab, diag16_pass_pairs, diag16_stride, diag_pass_pairs, diag_stride, stride;
 };
 CfgState save_cfg(const nw_ctx* c) {
-    return CfgState{c->cfg, c->band_cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->stream_fill,
-                    c->stream_walk, c->use_band, c->use_diag, c->use_stream, c->exact_tb_lds, c->exact_full,
-                    c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap, c->diag_sort_grid, c->band_slots,
-                    c->stream_slots, c->exact_slab, c->diag16_pass_pairs, c->diag16_stride, c->diag_pass_pairs,
-                    c->diag_stride, c->pass_reads, c->stride, c->region};
+    return CfgState{c->cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->use_diag, c->exact_tb_lds,
+                    c->exact_full, c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap, c->diag_sort_grid,
+                    c->exact_slab, c->diag16_pass_pairs, c->diag16_stride, c->diag_pass_pairs, c->diag_stride,
+                    c->stride};
 }
 void load_cfg(nw_ctx* c, const CfgState& st) {
-    c->cfg = st.cfg; c->band_cfg = st.band_cfg; c->diag_fill = st.diag_fill; c->diag_walk = st.diag_walk;
-    c->diag16_fill = st.diag16_fill; c->diag16_walk = st.diag16_walk; c->stream_fill = st.stream_fill;
-    c->stream_walk = st.stream_walk; c->use_band = st.use_band; c->use_diag = st.use_diag;
-    c->use_stream = st.use_stream; c->exact_tb_lds = st.exact_tb_lds; c->exact_full = st.exact_full;
-    c->exact_grid = st.exact_grid; c->exact_lds = st.exact_lds; c->diag_words = st.diag_words;
-    c->diag_lb_cap = st.diag_lb_cap; c->diag_sort_grid = st.diag_sort_grid; c->band_slots = st.band_slots;
-    c->stream_slots = st.stream_slots; c->exact_slab = st.exact_slab; c->diag16_pass_pairs = st.diag16_pass_pairs;
-    c->diag16_stride = st.diag16_stride; c->diag_pass_pairs = st.diag_pass_pairs; c->diag_stride = st.diag_stride;
-    c->pass_reads = st.pass_reads; c->stride = st.stride; c->region = st.region;
+    c->cfg = st.cfg; c->diag_fill = st.diag_fill; c->diag_walk = st.diag_walk; c->diag16_fill = st.diag16_fill;
+    c->diag16_walk = st.diag16_walk; c->use_diag = st.use_diag; c->exact_tb_lds = st.exact_tb_lds;
+    c->exact_full = st.exact_full; c->exact_grid = st.exact_grid; c->exact_lds = st.exact_lds;
+    c->diag_words = st.diag_words; c->diag_lb_cap = st.diag_lb_cap; c->diag_sort_grid = st.diag_sort_grid;
+    c->exact_slab = st.exact_slab; c->diag16_pass_pairs = st.diag16_pass_pairs; c->diag16_stride = st.diag16_stride;
+    c->diag_pass_pairs = st.diag_pass_pairs; c->diag_stride = st.diag_stride; c->stride = st.stride;
 }
 
 // 2-bit packed batch (nw_align_ops_packed): bases by batch position, exceptions ascending.
@@ -1610,8 +1421,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // anything is queued (no allocation inside the pipeline)
     // two sets overlap a chunk's tail with the next chunk's bulk; a third measured slower
     // (328M vs 306M reads/s at 262144-read chunks, scripts/gpu_sets_sweep.sh)
-    int nsets = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1 ? 2 : 1;
+    const bool several = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1;
+    int nsets = several ? 2 : 1;
     if (const char* e = std::getenv("CRISPR_NW_SETS")) nsets = std::max(1, std::min(kScratchSets, std::atoi(e)));
+    // chunk k's compaction waits for the copy of the runs two sets back (ev_out[k - nsets]),
+    // recorded only once the host has read that chunk's total: one set cannot pipeline
+    // several chunks (its wait would come before the record)
+    if (several) nsets = std::max(nsets, 2);
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
         configured = -1;
@@ -1636,6 +1452,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->skip16 = false;
     const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
     const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
+    std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
     auto restore = [&](int code) {
         c->skip16 = false;
         c->out_mode = mode_before;
@@ -1744,10 +1561,22 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // thousands of reads to the exact kernel, 15 -> 24 ms per C3 step.  The same choice
         // made on the device from the chunk's own count measured no gain: the skipped
         // level's launches remain.)
+        // The newest chunk the host has read back (k - lag - 1, synchronised in copy_runs)
+        // decides from its own counts when it ran both levels; while the level is skipped
+        // every 4th chunk runs both again, so input that changes back is noticed.
         if (adaptive && k >= lag + 1) {   // pooled calls too: one library's amplicons, one read source
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * (k - lag - 1);   // synchronised in copy_runs
-            c->skip16 = h[6] >= 4096 && 2 * h[5] > h[6];
+            const int64_t j = k - lag - 1;
+            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
+            static const int64_t zero[nw::kOpsCtl] = {};
+            const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
+            if (!one_level[(size_t)j]) {
+                const int64_t dp = (h[6] - h[7]) - (hp[6] - hp[7]), l2 = h[5] - hp[5];
+                c->skip16 = dp >= 2048 && 2 * l2 > dp;
+            } else {
+                c->skip16 = (k & 3) != 0;
+            }
         }
+        one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k)))
@@ -1774,8 +1603,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);
         const bool two = any_diag && c->diag16_fill.grid > 0;
         c->call_counts[0] = any_diag ? n - h[6] : 0;
-        c->call_counts[1] = two ? h[6] : 0;
-        c->call_counts[2] = any_diag ? (two ? h[5] : h[6]) : 0;
+        c->call_counts[1] = two ? h[6] - h[7] : 0;                // first level: two-level chunks' DP reads
+        c->call_counts[2] = any_diag ? (two ? h[5] + h[7] : h[6]) : 0;
         c->call_counts[3] = h[4];
     }
     c->call_done = true;

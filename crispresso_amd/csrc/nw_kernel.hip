@@ -13,12 +13,11 @@
 //     lane l+1 with one DPP wave_shr:1 per value per step -- no LDS round trip.
 //   * substitution scores come from a per-amplicon profile in LDS laid out
 //     [code][lane][RP] int8, so one ds_read_b32/b64 yields a lane's R scores.
-//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend).
-//     TB_BAND keeps them only for a diagonal band (a few KB of LDS per read, so
-//     many waves fit a CU); a read whose walk leaves the band is queued on the
-//     device and re-run by the TB_LDS_FULL / TB_GLOBAL_FULL instantiation, which
-//     stores every cell.  Bits inside the band come from the full DP, so the
-//     banded result is exact whenever the walk stays inside.
+//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend), every
+//     cell stored: in LDS (TB_LDS_FULL) or a per-wave HBM slab (TB_GLOBAL_FULL).
+//     This is the exact fallback of the certified band path (nw_band.hip): the
+//     reads no band level certifies, rare codes, -endweight, and every read when
+//     the band does not apply (penalties outside its int16 range).
 //   * the walk is done by the whole wave in runs: 64 lanes test 64 cells of the
 //     current diagonal/row/column at once and a ballot finds where the run ends.
 //   * the three alignment strings are written straight to HBM.
@@ -63,7 +62,7 @@ struct WaveLds {
 
 __host__ __device__ inline int es_of(int R) { return R <= 2 ? 1 : (R <= 4 ? 2 : (R <= 8 ? 4 : 8)); }
 
-__host__ __device__ inline WaveLds wave_lds_layout(int R, int La, int Lb_max, int mode, int band_slots) {
+__host__ __device__ inline WaveLds wave_lds_layout(int R, int La, int Lb_max, int mode) {
     WaveLds w;
     int o = 0;
     w.raw = o;     o += align16(Lb_max + 4);
@@ -72,7 +71,6 @@ __host__ __device__ inline WaveLds wave_lds_layout(int R, int La, int Lb_max, in
     w.runs = o;    o += align16(4 * (La + Lb_max + 8));
     w.bits = o;
     if (mode == TB_LDS_FULL) o += align16(Lb_max * 64 * es_of(R));
-    else if (mode == TB_BAND) o += align16(band_slots * 64 * es_of(R));
     w.total = align16(o);
     return w;
 }
@@ -82,32 +80,19 @@ __host__ __device__ inline int shared_lds_bytes(int R, int La) {
     return align16(NCODE * 64 * RP) + 256 + align16(La + 4);
 }
 
-// Where the traceback bits of cell (ai, bj) live.  Full modes: column bj.
-// Banded: lane l keeps columns [l*R + dlo, l*R + dlo + slots).
-template <int R, int MODE>
+// Where the traceback bits of cell (ai, bj) live: column bj's slot, lane ai / R.
+template <int R>
 struct TbStore {
     unsigned char* base;
-    int dlo;
-    int slots;
-    __device__ __forceinline__ int slot(int lane, int bj) const {
-        if constexpr (MODE == TB_BAND) return bj - lane * R - dlo;
-        else return bj;
-    }
-    __device__ __forceinline__ bool inside(int s) const {
-        if constexpr (MODE == TB_BAND) return (unsigned)s < (unsigned)slots;
-        else return true;
-    }
     __device__ __forceinline__ unsigned char* at(int s, int lane) const {
         return base + ((size_t)s * 64 + lane) * Geo<R>::ES;
     }
-    // nibble of cell (ai, bj); *oob set when the cell is outside the band.
+    // nibble of cell (ai, bj) (every cell is stored: *oob is always false)
     __device__ __forceinline__ unsigned nibble(int ai, int bj, bool* oob) const {
         constexpr int ES = Geo<R>::ES;
         const int lane = ai / R, k = ai - lane * R;
-        const int s = slot(lane, bj);
-        if (!inside(s)) { *oob = true; return 0u; }
         *oob = false;
-        const unsigned char* p = at(s, lane);
+        const unsigned char* p = at(bj, lane);
         unsigned w;
         int nr, kk;
         if constexpr (ES == 1) { w = *p; nr = R; kk = k; }
@@ -162,8 +147,8 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int wave = tid >> 6;
     const int wpb = blockDim.x >> 6;
     const long long nwork = exact_work_count(args);
-    // a work list shorter than the grid: blocks past its end leave before any set-up
-    if (args.work_list && args.work_lo + (long long)blockIdx.x * wpb >= nwork) return;
+    // a work list (or batch) shorter than the grid: blocks past its end leave before any set-up
+    if (args.work_lo + (long long)blockIdx.x * wpb >= nwork) return;
 
     // ---- shared per-block state: profile, ascii->code LUT, amplicon bytes ----
     unsigned char* prof_lds = smem;
@@ -176,7 +161,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     for (int q = tid; q < La; q += blockDim.x) amp_lds[q] = args.amp[q];
     __syncthreads();
 
-    const WaveLds L = wave_lds_layout(R, La, args.Lb_max, MODE, args.band_slots);
+    const WaveLds L = wave_lds_layout(R, La, args.Lb_max, MODE);
     unsigned char* wbase = smem + shared_lds_bytes(R, La) + wave * L.total;
     unsigned char* raw = wbase + L.raw;
     unsigned short* coff = (unsigned short*)(wbase + L.coff);
@@ -184,11 +169,9 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     unsigned* runs = (unsigned*)(wbase + L.runs);
     const long long gw = (long long)blockIdx.x * wpb + wave;
     const long long nwaves = (long long)gridDim.x * wpb;
-    TbStore<R, MODE> tb;
+    TbStore<R> tb;
     if constexpr (MODE == TB_GLOBAL_FULL) tb.base = args.tb_global + gw * args.tb_wave_bytes;
     else tb.base = wbase + L.bits;
-    tb.slots = args.band_slots;
-    tb.dlo = 0;
 
     const int nl = (La + R - 1) / R;        // lanes holding real rows
     const int ai0 = lane * R;
@@ -197,7 +180,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int prof_lane = lane * RP;
     const int pad_coff = NCODE_PAD * 64 * RP;   // offset of the all-zero pad code
 
-    for (long long wi = (args.work_list ? args.work_lo : 0) + gw; wi < nwork; wi += nwaves) {
+    for (long long wi = args.work_lo + gw; wi < nwork; wi += nwaves) {
         const long long rd = exact_work_read(args, wi);
         const long long off = args.offsets[rd];
         const int Lb = (int)(args.offsets[rd + 1] - off);
@@ -210,17 +193,6 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                 if (args.ops) args.nops[rd] = 0;
             }
             continue;
-        }
-        if constexpr (MODE == TB_BAND) {
-            // diagonal band [min(0, Lb-La) - m, max(0, Lb-La) + m] widened to the slots we have
-            const int dl = Lb - La;
-            const int span = (dl < 0 ? -dl : dl) + R;
-            const int m = (args.band_slots - span) / 2;
-            if (m < 0) {
-                if (lane == 0) args.fallback_list[atomicAdd(args.fallback_count, 1)] = rd;
-                continue;
-            }
-            tb.dlo = (dl < 0 ? dl : 0) - m;
         }
         // ---- stage the read: raw bytes + profile offsets of each column ----
         const unsigned char* rp = args.reads + off;
@@ -248,8 +220,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         int c_next = coff[min(max(bj0 + 1, 0), Lb + 3)];
         int sc[RP / 4];
         load_prof<R>(prof_lds, coff[min(max(bj0, 0), Lb + 3)] + prof_lane, sc);
-        int slot = tb.slot(lane, bj0);
-        for (int t = 0; t < nsteps; ++t, ++slot) {
+        for (int t = 0; t < nsteps; ++t) {
             const int bj = t - lane;
             // lane 0's row above is the top boundary at column t (leading end gap of t + 1)
             const int top = end_lead(args, t + 1);
@@ -291,7 +262,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     Yu = Y;
                 }
                 sMo = Mou; sY = Yu; sH = Hold[R - 1];
-                if (tb.inside(slot)) store_bits<R>(tb.at(slot, lane), acc);
+                store_bits<R>(tb.at(bj, lane), acc);
                 if (lane == lr) lastrow[bj] = mlast;
             }
             Htop = rH;
@@ -361,14 +332,14 @@ static hipError_t launch_r(const KernelArgs& a, const LaunchCfg& c, hipStream_t 
     switch (c.tb_mode) {
         case TB_LDS_FULL: hipLaunchKernelGGL((nw_align_kernel<R, TB_LDS_FULL>), grid, block, c.lds_bytes, s, a); break;
         case TB_GLOBAL_FULL: hipLaunchKernelGGL((nw_align_kernel<R, TB_GLOBAL_FULL>), grid, block, c.lds_bytes, s, a); break;
-        default: hipLaunchKernelGGL((nw_align_kernel<R, TB_BAND>), grid, block, c.lds_bytes, s, a); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int band_slots, int wpb) {
+int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int wpb) {
     if (rows_per_lane_for(R * 64) != R) return -1;
-    return shared_lds_bytes(R, La) + wpb * wave_lds_layout(R, La, Lb_max, tb_mode, band_slots).total;
+    return shared_lds_bytes(R, La) + wpb * wave_lds_layout(R, La, Lb_max, tb_mode).total;
 }
 
 int rows_per_lane_for(int La) {

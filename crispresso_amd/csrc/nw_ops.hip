@@ -83,7 +83,7 @@ __global__ __launch_bounds__(1024) void nw_ops_scan(int64_t* blk, int nblk, int6
         if (opsctl[1]) ctl[3] |= 2;   // a kernel found the spill area full
         // the call's reads by path, summed over chunks (nw_batch_path_counts after nw_align_ops)
         long long fb = 0;
-        for (int q = 0; cnt.fallback && q < cnt.passes; ++q) fb += cnt.fallback[4 * q];
+        if (cnt.fallback) fb += cnt.fallback[0];
         // a chunk that skipped its second level (KernelArgs::redo_direct) sent the redo
         // list to the exact kernel
         const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
@@ -91,6 +91,7 @@ __global__ __launch_bounds__(1024) void nw_ops_scan(int64_t* blk, int nblk, int6
         ctl[4] += fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
         if (cnt.band) ctl[6] += *cnt.band;
+        if (cnt.band && cnt.one_level) ctl[7] += *cnt.band;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];
     }

@@ -88,11 +88,18 @@ def concat_ops(parts: Sequence[OpsBatch]) -> OpsBatch:
     return OpsBatch(np.concatenate([p.stats for p in parts]),
                     np.concatenate([p.ops for p in parts]) if parts else np.zeros(0, np.uint32),
                     np.concatenate(offs), np.concatenate([p.read_lens for p in parts]),
-                    parts[0].scale, parts[0].awidth)
+                    parts[0].scale, parts[0].awidth, has_runs=all(getattr(p, "has_runs", True) for p in parts))
 
 
 class MultiGpuAligner:
-    """Aligns one batch on several devices at once (contiguous shards, one thread each)."""
+    """Aligns one batch on several devices at once (contiguous shards, one thread each).
+
+    Drop-in for :class:`~crispresso_amd.aligner.GpuAligner` in ``needle.align_reads``:
+    ``align_ops_packed`` takes the pinned 2-bit batch of the native ingest (each device
+    uploads only its shard's packed bytes), ``align_ops(..., resident=True)`` re-aligns
+    every device's last shard where it lies in HBM (the HDR pass)."""
+
+    ops_native = True
 
     def __init__(self, devices: Sequence[int], factory: Optional[Callable] = None, options=None):
         if factory is None:
@@ -105,6 +112,7 @@ class MultiGpuAligner:
         self.scale = self.aligners[0].scale
         self.reference: Optional[str] = None
         self._pool = cf.ThreadPoolExecutor(max_workers=len(self.devices))
+        self._resident = None   # (n, per-device shard offsets) of the last upload
 
     def set_reference(self, seq: str) -> None:
         for a in self.aligners:
@@ -122,13 +130,47 @@ class MultiGpuAligner:
             jobs.append(self._pool.submit(al.align_packed, b, o, strings))
         return concat_batches([j.result() for j in jobs])
 
-    def align_ops(self, buf: np.ndarray, offsets: np.ndarray) -> OpsBatch:
-        """Records + runs of every read (nw_align_ops per device, shards in parallel)."""
+    def align_ops(self, buf: Optional[np.ndarray], offsets: np.ndarray, resident: bool = False,
+                  records_only: bool = False) -> OpsBatch:
+        """Records + runs of every read (nw_align_ops per device, shards in parallel).
+        ``resident``: every device re-aligns the shard its last call uploaded (against the
+        current amplicon; ``offsets`` must be that batch's)."""
+        from .aligner import NeedleError
+
+        n = len(offsets) - 1
         jobs = []
-        for al, (lo, hi) in zip(self.aligners, self._shards(len(offsets) - 1)):
+        if resident:
+            if self._resident is None or self._resident[0] != n:
+                raise NeedleError(f"no resident batch of these {n} reads on the devices")
+            for al, o in zip(self.aligners, self._resident[1]):
+                jobs.append(self._pool.submit(al.align_ops, None, o, None, True, records_only))
+            return concat_ops([j.result() for j in jobs])
+        shard_offs = []
+        for al, (lo, hi) in zip(self.aligners, self._shards(n)):
             b, o = slice_batch(buf, offsets, lo, hi)
-            jobs.append(self._pool.submit(al.align_ops, b, o))
-        return concat_ops([j.result() for j in jobs])
+            shard_offs.append(o)
+            jobs.append(self._pool.submit(al.align_ops, b, o, None, False, records_only))
+        out = concat_ops([j.result() for j in jobs])
+        self._resident = (n, shard_offs)
+        return out
+
+    def align_ops_packed(self, pr) -> OpsBatch:
+        """The pinned 2-bit batch (aligner.PackedReads) over the devices: device k's call
+        takes reads [lo, hi) -- its slice of the offsets (batch positions unchanged), the
+        same packed bytes (it uploads only its own), the exceptions inside its range."""
+        from .aligner import PackedReads
+
+        n = len(pr.offsets) - 1
+        jobs, shard_offs = [], []
+        for al, (lo, hi) in zip(self.aligners, self._shards(n)):
+            o = pr.offsets[lo:hi + 1]
+            e0, e1 = np.searchsorted(pr.exc_pos, [o[0], o[-1]]) if len(pr.exc_pos) else (0, 0)
+            sub = PackedReads(pr.packed, o, pr.exc_pos[e0:e1], pr.exc_byte[e0:e1])
+            shard_offs.append(o)
+            jobs.append(self._pool.submit(al.align_ops_packed, sub))
+        out = concat_ops([j.result() for j in jobs])
+        self._resident = (n, shard_offs)
+        return out
 
     def align_multi_ops(self, amplicons: Sequence[str], buf: np.ndarray, offsets: np.ndarray,
                         amplicon_of_read: np.ndarray) -> OpsBatch:
@@ -139,7 +181,11 @@ class MultiGpuAligner:
                                                              pooled_costs(amplicons, offsets, which))):
             b, o = slice_batch(buf, offsets, lo, hi)
             jobs.append(self._pool.submit(al.align_multi_ops, list(amplicons), b, o, which[lo:hi]))
-        return concat_ops([j.result() for j in jobs])
+        out = concat_ops([j.result() for j in jobs])
+        # as GpuAligner: every context is left without an amplicon (set_reference before the next pass)
+        self.reference = None
+        self._resident = None
+        return out
 
     def close(self) -> None:
         for a in self.aligners:

@@ -89,6 +89,77 @@ def read_fastq_as_fasta(path: str, min_bp_quality: int = 0,
     return NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), seqs, off
 
 
+class _Owner:
+    """Frees a native ingest handle when the last array viewing its memory is gone."""
+
+    def __init__(self, lib, h):
+        self.lib, self.h = lib, h
+
+    def __del__(self):  # pragma: no cover - runs at garbage collection
+        if self.h:
+            self.lib.nw_fastq_free(self.h)
+            self.h = None
+
+
+class _View:
+    """``np.asarray(_View(...))``: an array over native memory that keeps its owner alive."""
+
+    def __init__(self, owner, addr: int, nbytes: int):
+        self._owner = owner
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "version": 3, "data": (addr or 0, False)}
+
+
+def _native_array(owner, addr, count: int, dtype) -> np.ndarray:
+    dtype = np.dtype(dtype)
+    if count <= 0 or not addr:
+        return np.zeros(0, dtype)
+    return np.asarray(_View(owner, addr, count * dtype.itemsize)).view(dtype)
+
+
+def read_fastq_packed(path: str, pinned: bool = True):
+    """-> (names, text, offsets, packed): the FASTQ's reads as the aligner takes them.
+
+    The native ingest (:func:`read_fastq_as_fasta` semantics, no quality filter: the
+    reference filters the raw reads upstream, ``CORE:1547-1583``) plus ``nw_fastq_pack``:
+    ``packed`` is an :class:`~crispresso_amd.aligner.PackedReads` whose 2-bit bases,
+    exceptions and offsets sit in page-locked memory (``pinned``) ready for
+    ``nw_align_ops_packed``; ``text`` (the bytes, for the alignment rows) and ``offsets``
+    are views of the same native buffers -- nothing is copied into Python-owned memory.
+    The buffers live as long as any of the returned arrays."""
+    import ctypes
+
+    from . import _lib
+    from .aligner import PackedReads
+
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    if lib.nw_fastq_read(os.fsencode(path), ctypes.byref(h)) != _lib.NW_OK:
+        raise OSError(f"cannot read FASTQ {path}")
+    owner = _Owner(lib, h)
+    n = int(lib.nw_fastq_count(h))
+    pk, po, ep, eb = (ctypes.c_void_p() for _ in range(4))
+    ne = ctypes.c_int64()
+    rc = lib.nw_fastq_pack(h, int(bool(pinned)), ctypes.byref(pk), ctypes.byref(po), ctypes.byref(ep),
+                           ctypes.byref(eb), ctypes.byref(ne))
+    if rc != _lib.NW_OK:
+        raise _lib.NativeLibraryError(f"nw_fastq_pack failed (code {rc})")
+    offsets = _native_array(owner, po.value, n + 1, np.int64)
+    if n == 0:
+        offsets = np.zeros(1, np.int64)
+    nb = int(offsets[-1])
+    text = _native_array(owner, lib.nw_fastq_seqs(h), nb, np.uint8)
+    packed = PackedReads(_native_array(owner, pk.value, (nb + 3) // 4 + 16, np.uint8), offsets,
+                         _native_array(owner, ep.value, ne.value, np.int64),
+                         _native_array(owner, eb.value, ne.value, np.uint8))
+    nm = ctypes.c_int64()
+    p = lib.nw_fastq_names(h, ctypes.byref(nm))
+    raw = _native_array(owner, p, nm.value, np.uint8).copy()
+    names_text = raw.tobytes().decode("ascii", "replace") if len(raw) else ""
+    names = names_text.split("\n")[:-1] if n else []
+    return (NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), text, offsets,
+            packed)
+
+
 def read_fastq_as_fasta_py(path: str, min_bp_quality: int = 0,
                            min_single_bp_quality: int = 0) -> Tuple[List[str], np.ndarray, np.ndarray]:
     """The Python restatement (gzip + :func:`fastq_bytes_as_fasta`)."""

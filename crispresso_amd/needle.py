@@ -354,13 +354,17 @@ class PassResult:
 
 def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: np.ndarray,
                 offsets: np.ndarray, amplicon_id: str = "AMPL", outfile: Optional[str] = None,
-                just_score: bool = False) -> PassResult:
+                just_score: bool = False, packed=None, resident: bool = False) -> PassResult:
     """One ``needle -asequence=AMPL -bsequence=/dev/stdin`` run (CRISPRessoCORE.py:1797-1806).
 
     ``outfile`` (``needle_output_*.txt.gz``) is written only when given, as the
     reference keeps it only with --keep_intermediate/--dump (CRISPRessoCORE.py:3694-3697).
     ``just_score``: the caller reads only identities (the repair passes,
     CORE:1740-1741), so the alignment strings stay on the GPU unless a file is written.
+    ``packed``: the same reads 2-bit packed in pinned memory (fastq.read_fastq_packed):
+    the call uploads that (nw_align_ops_packed) instead of the text.  ``resident``: the
+    reads are the batch this aligner's last pass uploaded (still in HBM; the HDR pass,
+    CORE:1808-1828, re-streams the same FASTQ): nothing is uploaded.
     """
     from .aligner import default_output_mode
 
@@ -368,7 +372,15 @@ def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: n
     try:
         if aligner.reference != amplicon:
             aligner.set_reference(amplicon)
-        if use_ops:
+        if use_ops and resident:
+            ob = aligner.align_ops(None, offsets, resident=True, records_only=just_score and not outfile)
+            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
+            batch = ob.expand(amplicon, buf, offsets) if outfile else None
+        elif use_ops and packed is not None:
+            ob = aligner.align_ops_packed(packed)
+            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
+            batch = ob.expand(amplicon, buf, offsets) if outfile else None
+        elif use_ops:
             ob = aligner.align_ops(buf, offsets, records_only=just_score and not outfile)
             res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
             batch = ob.expand(amplicon, buf, offsets) if outfile else None
@@ -396,20 +408,26 @@ class AlignArgs:
     needle_options_string: str = DEFAULT_NEEDLE_OPTIONS
     keep_intermediate: bool = False
     dump: bool = False
-    # --min_average_read_quality / --min_single_bp_quality: the reads the quality filter
-    # keeps (filter_se_fastq_by_qual, CORE:1547-1583) are the ones aligned
-    min_average_read_quality: int = 0
-    min_single_bp_quality: int = 0
+    # (--min_average_read_quality / --min_single_bp_quality act upstream of this step, on
+    # the raw R1 / R2 before trimming and merging, CORE:1547-1583: fastq.filter_se_fastq_by_qual
+    # / filter_pe_fastq_by_qual; processed_output_filename is already filtered)
 
 
 def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Optional[GpuAligner] = None,
                 output_dir: Optional[str] = None, database_id: str = "AMPL",
-                rc_hdr_quirk: str = "reference") -> pd.DataFrame:
+                rc_hdr_quirk: str = "reference", timings: Optional[dict] = None) -> pd.DataFrame:
     """CRISPRessoCORE.py:1788-2000 on the GPU: returns ``df_needle_alignment``.
 
     The result has the reference's columns (``score_ref, length, ref_seq,
     align_str, align_seq`` and, with an HDR amplicon, ``score_repaired,
     score_diff``) and index (read ids, ``_RC`` suffix for reverse-complement hits).
+
+    Data path: the native ingest reads the FASTQ(.gz) and packs the reads 2 bits per base
+    into pinned memory (fastq.read_fastq_packed); the forward pass uploads that batch once
+    (nw_align_ops_packed) and the HDR pass re-aligns it where it lies in HBM
+    (nw_align_ops_resident); records and runs come back into pinned memory, and the
+    DataFrame is built from them and the text (ops_to_dataframe).  ``timings``, when a
+    dict, receives the seconds of each stage (ingest, aligner calls, DataFrame, rest).
     """
     # CRISPRessoCORE.py:1283 and 1350 normalise the amplicons before anything else
     args.amplicon_seq = args.amplicon_seq.upper().strip().rstrip("\n")
@@ -421,15 +439,31 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
         aligner = GpuAligner(0, opts)
     keep_files = bool(output_dir) and (args.keep_intermediate or args.dump)
     _jp = (lambda f: os.path.join(output_dir, f)) if output_dir else (lambda f: f)
+    import time
+
+    tm = timings if timings is not None else {}
+    clock = time.perf_counter
+    t_start = clock()
     try:
-        names, buf, offsets = fastq.read_fastq_as_fasta(processed_output_filename, args.min_average_read_quality,
-                                                        args.min_single_bp_quality)
+        native = getattr(aligner, "ops_native", False) and hasattr(aligner, "align_ops_packed")
+        t0 = clock()
+        if native:
+            names, buf, offsets, packed = fastq.read_fastq_packed(processed_output_filename, pinned=True)
+        else:
+            names, buf, offsets = fastq.read_fastq_as_fasta(processed_output_filename)
+            packed = None
+        tm["ingest_s"] = clock() - t0
+        t0 = clock()
         fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
-                          _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None)
+                          _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None, packed=packed)
+        tm["align_s"] = clock() - t0
         if args.expected_hdr_amplicon_seq:
+            t0 = clock()
             rep = needle_pass(aligner, args.expected_hdr_amplicon_seq, names, buf, offsets, database_id,
                               _jp(f"needle_output_repair_{database_id}.txt.gz") if keep_files else None,
-                              just_score=True)
+                              just_score=True, resident=native)
+            tm["align_hdr_s"] = clock() - t0
+            t0 = clock()
             df_database = fwd.dataframe("ref")
             # same reads, same (non-empty) rows: the repair frame shares the ID index
             df_database_repair = rep.dataframe("repaired", just_score=True, index=df_database.index)
@@ -448,8 +482,11 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
                 df_database_and_repair.score_ref - df_database_and_repair.score_repaired
             )
             df_needle_alignment = df_database_and_repair
+            tm["dataframe_s"] = clock() - t0
         else:
+            t0 = clock()
             df_needle_alignment = fwd.dataframe("ref")
+            tm["dataframe_s"] = clock() - t0
             sr_not_aligned = df_needle_alignment.loc[
                 (df_needle_alignment.score_ref < args.min_identity_score).to_numpy()
             ].align_seq.apply(lambda x: x.replace("_", ""))
@@ -499,6 +536,7 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             df_needle_alignment_rc["align_str"] = df_needle_alignment_rc["align_str"].apply(lambda x: x[::-1])
             df_needle_alignment_rc.index = map(lambda x: "_".join([x, "RC"]), df_needle_alignment_rc.index)
             df_needle_alignment = pd.concat([df_needle_alignment, df_needle_alignment_rc])
+        tm["total_s"] = clock() - t_start
         return df_needle_alignment
     finally:
         if own:

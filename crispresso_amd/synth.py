@@ -18,7 +18,7 @@ bytes over ``ACGTN``.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -165,3 +165,44 @@ def pooled_amplicons(k: int = 96, seed: int = 5) -> list:
 def unpack(buf: np.ndarray, offsets: np.ndarray) -> list:
     b = buf.tobytes()
     return [b[offsets[i]:offsets[i + 1]].decode() for i in range(len(offsets) - 1)]
+
+
+def native_reads(amplicon: str, n: int, seed: int, mix: Mix = C2_MIX, nthreads: int = 0,
+                 buf: Optional[np.ndarray] = None, first: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """n reads of the C2 / C4 mix from the native generator (include/crispr_synth.h):
+    the same mutation kinds and rates as :func:`reads_from` (no N, RC or homopolymer
+    options), a counter-based RNG instead of numpy's PCG64, ~30x faster.  Used for the
+    large sets (C4 shards of 12.5M reads).  ``first``: reads first .. first + n - 1 of
+    the set (any range is generated on its own).  ``buf``: a preallocated uint8 array
+    (e.g. pinned) of at least the range's bytes."""
+    from . import _lib
+
+    if mix.n_rate or mix.rc_frac or mix.homopolymer:
+        raise ValueError("native_reads: the N / RC / homopolymer options are numpy-only (reads_from)")
+    lib = _lib.load()
+    amp = amplicon.encode("ascii")
+    w = np.array([mix.exact, mix.subs, mix.deletion, mix.insertion, mix.noise], dtype=np.float64)
+    off = np.empty(n + 1, np.int64)
+    total = lib.nw_synth_offsets(amp, len(amp), first, n, seed, _lib.ptr(w), _lib.ptr(off), nthreads)
+    if total < 0:
+        raise ValueError("nw_synth_offsets: bad arguments")
+    if buf is None:
+        buf = np.empty(max(int(total), 1), np.uint8)
+    elif len(buf) < total:
+        raise ValueError(f"buffer of {len(buf)} bytes < {total}")
+    if lib.nw_synth_reads(amp, len(amp), first, n, seed, _lib.ptr(w), _lib.ptr(off), _lib.ptr(buf), nthreads) != 0:
+        raise ValueError("nw_synth_reads failed")
+    return buf[: int(total)], off
+
+
+def native_offsets(amplicon: str, n: int, seed: int, mix: Mix = C2_MIX, first: int = 0) -> np.ndarray:
+    """Only the offsets of :func:`native_reads` (lengths without the bytes: cheap)."""
+    from . import _lib
+
+    lib = _lib.load()
+    amp = amplicon.encode("ascii")
+    w = np.array([mix.exact, mix.subs, mix.deletion, mix.insertion, mix.noise], dtype=np.float64)
+    off = np.empty(n + 1, np.int64)
+    if lib.nw_synth_offsets(amp, len(amp), first, n, seed, _lib.ptr(w), _lib.ptr(off), 0) < 0:
+        raise ValueError("nw_synth_offsets: bad arguments")
+    return off

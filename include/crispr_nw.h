@@ -30,7 +30,7 @@ extern "C" {
 #define NW_OK 0
 #define NW_E_INVALID (-1)      /* bad argument (null pointer, empty amplicon, ...) */
 #define NW_E_INEXACT (-2)      /* penalties not exactly representable in integer units */
-#define NW_E_UNSUPPORTED (-3)  /* option the GPU path does not implement (matrix, endweight, size) */
+#define NW_E_UNSUPPORTED (-3)  /* option the GPU path does not implement (matrix other than EDNAFULL, size) */
 #define NW_E_HIP (-4)          /* HIP runtime error or no device */
 #define NW_E_NOMEM (-5)        /* device or host allocation failed */
 #define NW_E_STATE (-6)        /* call out of order (e.g. run before upload) */
@@ -85,9 +85,15 @@ void nw_destroy(nw_ctx* ctx);
 const char* nw_last_error(const nw_ctx* ctx);
 
 /* needle qualifiers (CRISPRessoCORE.py:4226-4231 default
- * "-gapopen=10 -gapextend=0.5 -awidth3=5000").  matrix must be "EDNAFULL";
- * end_weight must be 0 (needle's default, which CRISPResso never changes).
- * Returns NW_E_INEXACT when gap_open/gap_extend are not multiples of 1/16. */
+ * "-gapopen=10 -gapextend=0.5 -awidth3=5000").  matrix must be "EDNAFULL" (or
+ * NULL / empty); tie_policy NW_TIE_EMBOSS.  end_weight != 0 is needle's -endweight
+ * (-endopen end_open, -endextend end_extend; CRISPResso never sets it, but
+ * --needle_options_string forwards it): an end gap of k residues costs
+ * end_open + (k - 1) * end_extend, and every read goes through the
+ * exact int32 kernels (the band certificate assumes free end gaps).  end_open /
+ * end_extend are ignored when end_weight is 0.  Returns NW_E_INEXACT when any
+ * penalty in use is not a multiple of 1/16, NW_E_INVALID when one is negative or
+ * over 1000. */
 int nw_set_params(nw_ctx* ctx, float gap_open, float gap_extend, int end_weight,
                   float end_open, float end_extend, const char* matrix, int tie_policy);
 /* Integer multiplier applied to every score (2 for the defaults). */
@@ -126,20 +132,19 @@ int64_t nw_batch_algo_bytes(nw_ctx* ctx);
 int64_t nw_batch_cells(const nw_ctx* ctx);
 /* Launch geometry of the kernel that aligns the bulk of the batch: rows per
  * lane, waves per block, grid, LDS bytes per block, traceback storage
- * (0 = full in LDS, 1 = full in a global slab, 2 = diagonal band in LDS,
- * 3 = diagonal band in LDS, two reads per wavefront in packed int16,
- * 4 = streaming fill, two reads per wavefront in packed int16, diagonal band
- * in HBM + a separate traceback kernel). */
+ * (0 = exact kernel, full traceback in LDS, 1 = exact kernel, full traceback in a
+ * global slab, 5 = certified diagonal band: two reads per 16-lane row in packed
+ * int16, traceback tiles in HBM). */
 int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
                       int32_t* grid, int32_t* lds_bytes, int32_t* tb_mode);
 /* Reads of the last run aligned by the exact int32 kernel with full traceback
  * storage: what no band level certified, plus a skipped second level's reads
  * (nw_batch_path_counts [3]; synchronises). */
 int64_t nw_batch_fallbacks(nw_ctx* ctx);
-/* Device time of the last run split by kernel (synchronises): the DP fill,
- * the traceback/emit kernel and the rest (fallback kernel, memsets).  With the
- * non-streaming kernels everything is reported as fill.  For batches split
- * into several passes the first two cover the first pass only. */
+/* Device time of the last run split by kernel (synchronises): the first band
+ * level's DP fill, its traceback walk, and the rest (sort, second level, exact
+ * kernel).  With the exact kernel alone everything is reported as fill.  For
+ * batches split into several passes the first two cover the first pass only. */
 int nw_batch_kernel_times(nw_ctx* ctx, float* fill_ms, float* walk_ms, float* rest_ms);
 /* Device-resident output of the last nw_batch_run_async (synchronises): the
  * [n][3][stride] alignment rows and the nw_stat array, valid until the next
@@ -263,6 +268,15 @@ void nw_fastq_free(nw_fastq* q);
 int nw_fastq_read_filtered(const char* path, int32_t min_avg_quality, int32_t min_single_quality, nw_fastq** out);
 int64_t nw_fastq_dropped(const nw_fastq* q);                    /* records the filter removed */
 const uint8_t* nw_fastq_pass(const nw_fastq* q, int64_t* n);    /* every record's verdict (1 = kept), file order */
+/* The handle's reads as nw_align_ops_packed takes them (nw_pack_reads' layout: 2 bits per
+ * base by batch position = the nw_fastq_offsets positions, exceptions ascending) plus a
+ * copy of the offsets, in page-locked host memory (pinned != 0: the upload runs at PCIe
+ * rate; NW_E_NOMEM when the runtime cannot page-lock) or ordinary memory (pinned = 0).
+ * Built once, in parallel, by the first call; the handle owns the buffers; a later call
+ * with the other `pinned` returns NW_E_STATE.  Replaces the reference's FASTA pipe into
+ * needle (CRISPRessoCORE.py:1791-1797) as the aligner's input. */
+int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int64_t** offsets, const int64_t** exc_pos,
+                  const uint8_t** exc_byte, int64_t* n_exc);
 
 /* nw_expand_ops for the reads idx[0 .. m) only: read idx[q]'s rows at aln_out + q*3*stride. */
 int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,

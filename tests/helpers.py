@@ -68,8 +68,12 @@ class OracleAligner:
     def align(self, reads):
         return self.align_packed(*pack_reads(reads))
 
-    def align_ops(self, buf, offsets):
-        return ops_from_batch(self.align_packed(buf, offsets))
+    def align_ops(self, buf, offsets, out=None, resident=False, records_only=False):
+        if resident:
+            buf, offsets = self._resident
+        ob = ops_from_batch(self.align_packed(buf, offsets))
+        self._resident = (buf, offsets)
+        return ob
 
     def align_multi_ops(self, amplicons, buf, offsets, amplicon_of_read):
         return ops_from_batch(self.align_multi(amplicons, buf, offsets, amplicon_of_read))

@@ -8,14 +8,17 @@ from crispresso_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    text = open(os.path.join(ROOT, "include", "crispr_nw.h")).read()
+def declared_symbols(header="crispr_nw.h", prefix="nw_"):
+    text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"\b(nw_[a-z0-9_]+)\s*\(", text))
+    return set(re.findall(r"\b(" + prefix + r"[a-z0-9_]+)\s*\(", text))
 
 
 def test_header_and_binding_agree():
     assert declared_symbols() == set(_lib.EXPORTS)
+    assert declared_symbols("crispr_quant.h", "nwq_") == set(_lib.QUANT_EXPORTS)
+    assert declared_symbols("crispr_flash.h", "nwf_") == set(_lib.FLASH_EXPORTS)
+    assert declared_symbols("crispr_synth.h", "nw_synth_") == set(_lib.SYNTH_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol():

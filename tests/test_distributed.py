@@ -150,3 +150,46 @@ def test_multi_device_ops_and_pooled_equal_single():
     got = multi.align_multi_ops(amps, pbuf, poff, which)
     assert np.array_equal(got.stats, want.stats) and np.array_equal(got.ops, want.ops)
     multi.close()
+
+
+def test_multi_device_pooled_then_single_amplicon_pass():
+    """A pooled call leaves every context without an amplicon; the MultiGpuAligner says
+    so too, so the next single-amplicon pass (needle_pass) sets its amplicon again
+    instead of finding it 'already set' (ADVICE r2)."""
+    from crispresso_amd.needle import needle_pass
+    from tests.helpers import OracleAligner
+
+    multi = MultiGpuAligner([0, 1], factory=lambda d, o: OracleAligner(d, o))
+    amp = synth.random_amplicon(150, 3)
+    buf, off = synth.reads_from(amp, 51, 4)
+    multi.set_reference(amp)
+    amps, pbuf, poff, which = _pooled()
+    multi.align_multi_ops(amps, pbuf, poff, which)
+    assert multi.reference is None
+    for al in multi.aligners:
+        al.reference = None    # what the native contexts are left with
+    res = needle_pass(multi, amp, [f"r{i}" for i in range(51)], buf, off)
+    want = OracleAligner()
+    want.set_reference(amp)
+    assert np.array_equal(res.ops.stats, want.align_ops(buf, off).stats)
+    multi.close()
+
+
+def test_multi_device_resident_second_pass():
+    """align_ops(resident=True) re-aligns each device's last shard (the HDR pass)."""
+    from tests.helpers import OracleAligner
+
+    multi = MultiGpuAligner([0, 1, 2], factory=lambda d, o: OracleAligner(d, o))
+    amp = synth.random_amplicon(150, 3)
+    hdr = synth.hdr_amplicon(amp, 4)
+    buf, off = synth.reads_from(amp, 301, 4)
+    multi.set_reference(amp)
+    multi.align_ops(buf, off)
+    multi.set_reference(hdr)
+    got = multi.align_ops(None, off, resident=True, records_only=True)
+    single = OracleAligner()
+    single.set_reference(hdr)
+    assert np.array_equal(got.stats, single.align_ops(buf, off).stats)
+    with pytest.raises(Exception):
+        multi.align_ops(None, off[:100], resident=True)
+    multi.close()

@@ -229,3 +229,30 @@ def test_host_pool_threads_and_fork(tmp_path, monkeypatch):
     child.join(timeout=60)
     assert child.exitcode == 0
     assert got == (len(ref[0]), int(ref[1].sum()), int(ref[2][-1]))
+
+
+def test_packed_ingest_matches_text_and_pack_reads(tmp_path):
+    """nw_fastq_pack: the aligner's packed input straight from the ingest (pageable here; pinned
+    on a GPU box) equals nw_pack_reads of the text; text and offsets are the same reads the
+    text reader returns (N and IUPAC bytes go to the exception list)."""
+    import gzip
+
+    from crispresso_amd.aligner import pack_2bit
+
+    recs = []
+    rng = np.random.Generator(np.random.PCG64(5))
+    for k in range(3000):
+        L = int(rng.integers(0, 300))
+        seq = "".join(rng.choice(list("ACGTACGTACGTNacgtRY"), L))
+        recs.append(f"@r:{k} x\n{seq}\n+\n{'I' * L}\n")
+    p = tmp_path / "r.fastq.gz"
+    with gzip.open(p, "wt") as f:
+        f.write("".join(recs))
+    names, text, off, pk = fastq.read_fastq_packed(str(p), pinned=False)
+    n2, b2, o2 = fastq.read_fastq_as_fasta(str(p))
+    assert list(names) == list(n2) and np.array_equal(off, o2) and np.array_equal(text, b2)
+    want = pack_2bit(b2, o2)
+    nb = (int(o2[-1]) + 3) // 4
+    assert np.array_equal(pk.packed[:nb], want.packed[:nb])
+    assert np.array_equal(pk.exc_pos, want.exc_pos) and np.array_equal(pk.exc_byte, want.exc_byte)
+    assert len(pk.exc_pos) > 0 and pk.offsets is off

@@ -321,3 +321,118 @@ def test_adaptive_levels_sorted_input(gpu_aligner_factory, monkeypatch):
     # tens of thousands stay on the second level
     assert paths["exact_kernel"] < 0.01 * (len(off) - 1)
 
+
+
+def test_set_params_endweight_through_ctypes(oracle):
+    """The ABI contract of include/crispr_nw.h for -endweight: nw_set_params(end_weight=1,
+    end_open, end_extend) called straight through ctypes returns NW_OK, and an alignment
+    with a leading overhang then pays the end gap as the oracle's restatement
+     says -- not the free-end-gap answer."""
+    import ctypes
+
+    from crispresso_amd import _lib
+
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.nw_create(0, ctypes.byref(h)) == _lib.NW_OK
+    try:
+        assert lib.nw_set_params(h, 10.0, 0.5, 1, 3.0, 1.0, b"EDNAFULL", _lib.NW_TIE_EMBOSS) == _lib.NW_OK
+        assert lib.nw_score_scale(h) == 2
+        # an end penalty not on the 1/16 grid is refused, as the header says
+        assert lib.nw_set_params(h, 10.0, 0.5, 1, 0.03, 1.0, b"EDNAFULL", _lib.NW_TIE_EMBOSS) == _lib.NW_E_INEXACT
+        assert lib.nw_set_params(h, 10.0, 0.5, 1, 3.0, 1.0, b"EDNAFULL", _lib.NW_TIE_EMBOSS) == _lib.NW_OK
+        amp = synth.random_amplicon(200, 808)
+        reads = [amp[40:], amp[:150] + "ACGT", amp]
+        buf, off = pack_reads(reads)
+        assert lib.nw_set_reference(h, amp.encode(), len(amp)) == _lib.NW_OK
+        stride = int(lib.nw_required_stride(h, int(np.diff(off).max())))
+        stats = np.zeros(len(reads), _lib.STAT_DTYPE)
+        aln = np.zeros((len(reads), 3, stride), np.uint8)
+        assert lib.nw_align_batch(h, _lib.ptr(buf), _lib.ptr(off), len(reads), _lib.ptr(aln), stride,
+                                  _lib.ptr(stats)) == _lib.NW_OK
+        p = oracle.params(10.0, 0.5, True, 3.0, 1.0)
+        res, want = oracle.align_batch(amp, buf, off, p, nthreads=1)
+        for f in FIELDS:
+            assert np.array_equal(stats[f], res[f]), f
+        for i in range(len(reads)):
+            L = int(res["aln_len"][i])
+            assert aln[i, :, :L].tobytes() == want[i, :, :L].tobytes()
+        free, _ = oracle.align_batch(amp, buf, off, oracle.params(10.0, 0.5), nthreads=1)
+        assert stats["score"][0] != free["score"][0]   # the overhang's end gap is charged
+    finally:
+        lib.nw_destroy(h)
+
+
+def test_multi_gpu_aligner_c4_and_pooled_vs_oracle(oracle):
+    """MultiGpuAligner with two contexts on device 0 (one host thread each): a batch of the
+    C4 generator (native, seed 10: bench's C4 shards) through the pinned 2-bit path and the
+    resident HDR pass, and a 96-amplicon pooled batch split by DP cells -- every read's
+    record and runs equal to the oracle's."""
+    from crispresso_amd import synth as sy
+    from crispresso_amd.aligner import OpsBatch, PackedReads, pack_2bit
+    from crispresso_amd.distributed import MultiGpuAligner
+
+    amp = sy.random_amplicon(250, 1)
+    buf, off = sy.native_reads(amp, 20001, 10)
+    multi = MultiGpuAligner([0, 0])
+    try:
+        multi.set_reference(amp)
+        pr = pack_2bit(buf, off)
+        got = multi.align_ops_packed(pr)
+        assert_same(oracle, amp, buf, off, got.expand(amp, buf, off), "multi-c4")
+        hdr = sy.hdr_amplicon(amp, 4)
+        multi.set_reference(hdr)
+        rec = multi.align_ops(None, off, resident=True, records_only=True)
+        res, _ = oracle.align_batch(hdr, buf, off, nthreads=8)
+        for f in FIELDS:
+            assert np.array_equal(rec.stats[f], res[f]), f
+        # pooled: 96 amplicons, ~60 reads each from the native generator, grouped by amplicon
+        amps = sy.pooled_amplicons(96, 5)
+        parts = [sy.native_reads(a, 40 + (g % 5) * 10, 100 + g) for g, a in enumerate(amps)]
+        reads = []
+        for b, o in parts:
+            reads += sy.unpack(b, o)
+        which = np.repeat(np.arange(96, dtype=np.int32), [len(o) - 1 for _, o in parts])
+        pbuf, poff = pack_reads(reads)
+        ob = multi.align_multi_ops(amps, pbuf, poff, which)
+        assert multi.reference is None
+        for g, a in enumerate(amps):
+            sel = np.flatnonzero(which == g)
+            gb, go = pack_reads([reads[i] for i in sel])
+            runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in sel]
+            goo = np.zeros(len(sel) + 1, np.int64)
+            goo[1:] = np.cumsum([len(r) for r in runs])
+            sub = OpsBatch(ob.stats[sel], np.concatenate(runs), goo, np.diff(go), ob.scale)
+            assert_same(oracle, a, gb, go, sub.expand(a, gb, go), f"multi-pooled g={g}")
+        # a single-amplicon pass after the pooled call sets its amplicon again
+        multi.set_reference(amp)
+        again = multi.align_ops_packed(pr)
+        assert np.array_equal(again.stats, got.stats) and np.array_equal(again.ops, got.ops)
+    finally:
+        multi.close()
+
+
+def test_pinned_pool_outputs_are_reused_and_kept(gpu_aligner_factory, oracle):
+    """Outputs leased from the pinned pool: a batch the caller keeps is never overwritten by
+    the next call; a dropped one's block is reused."""
+    import gc
+
+    from crispresso_amd import _lib
+
+    amp = synth.random_amplicon(250, 71)
+    buf, off = synth.reads_from(amp, 3000, 72, synth.PARITY_MIX)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    first = a.align_ops(buf, off)
+    keep = (first.stats.copy(), first.ops.copy(), first.ops_off.copy())
+    buf2, off2 = synth.reads_from(amp, 3000, 73, synth.PARITY_MIX)
+    second = a.align_ops(buf2, off2)
+    assert first.stats.ctypes.data != second.stats.ctypes.data
+    assert np.array_equal(first.stats, keep[0]) and np.array_equal(first.ops, keep[1])
+    addr = first.stats.ctypes.data
+    del first
+    gc.collect()
+    third = a.align_ops(buf, off)
+    assert third.stats.ctypes.data == addr      # the dropped batch's block came back
+    assert np.array_equal(third.stats, keep[0]) and np.array_equal(third.ops_off, keep[2])
+    assert_same(oracle, amp, buf2, off2, second.expand(amp, buf2, off2), "pool")

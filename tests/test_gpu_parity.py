@@ -12,21 +12,21 @@ from crispresso_amd.aligner import pack_reads
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["diag", "stream", "stream-profile", "band", "full"]
-BANDED = {"diag": "diag-int16", "stream": "stream-int16"}
+# The kernel families production selects: "diag" = the certified band
+# levels + the exact kernel on what they hand on (the default); "full" = the exact
+# int32 kernel on every read (what runs when the band does not apply: -endweight,
+# penalties outside the band's int16 range).
+KERNELS = ["diag", "full"]
 
 
 @pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")])
 def kernel(request, monkeypatch):
-    """Run a test once per kernel family (CRISPR_NW_KERNEL selects it;
-    stream-profile = the stream kernel without the pair-code score table) and
-    output mode (ops: runs over PCIe + host expansion, the default; rows: the
-    kernels write the three strings)."""
+    """Run a test once per kernel family (CRISPR_NW_KERNEL selects it) and output
+    mode (ops: runs over PCIe + host expansion, the default; rows: the kernels write
+    the three strings)."""
     fam, mode = request.param.split("/")
-    monkeypatch.setenv("CRISPR_NW_KERNEL", fam.split("-")[0])
+    monkeypatch.setenv("CRISPR_NW_KERNEL", fam)
     monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
-    if fam == "stream-profile":
-        monkeypatch.setenv("CRISPR_NW_PAIR_TABLE", "0")
     return request.param
 
 FIELDS = ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j")
@@ -129,11 +129,9 @@ def test_repeated_batches_reuse_context(gpu_aligner_factory, oracle, kernel):
     assert_same(oracle, amp2, buf, off, a.align_packed(buf, off), "switch-ref")
 
 
-@pytest.mark.parametrize("family", sorted(BANDED))
-def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
+def test_band_fallbacks_exact(gpu_aligner_factory, oracle):
     """Reads whose traceback leaves the diagonal band (large indels, shifted
     reads) are re-run with full storage; results stay bit-identical."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", family)
     amp = synth.random_amplicon(250, 1)
     rng = np.random.Generator(np.random.PCG64(33))
     reads = []
@@ -149,7 +147,7 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == BANDED[family]
+    assert a.geometry()["tb_mode"] == "diag-int16"
     assert a.fallbacks() >= 6
     assert_same(oracle, amp, buf, off, batch, "band-fallback")
 
@@ -157,14 +155,12 @@ def test_band_fallbacks_exact(gpu_aligner_factory, oracle, monkeypatch, family):
 @pytest.mark.parametrize("exact", ["multi", "split", "wave"])
 @pytest.mark.parametrize("La", [1, 5, 63, 64, 65, 200, 250, 333, 600, 1000, 1024])
 def test_exact_kernel_work_list(gpu_aligner_factory, oracle, monkeypatch, La, exact):
-    """Every read through the exact int32 kernel's work list (a one-slot band hands
-    nearly all of them on): the multi-wave kernel (nw_exact.hip: one row per lane, up
+    """Every read through the exact int32 kernels (CRISPR_NW_KERNEL=full): the multi-wave kernel (nw_exact.hip: one row per lane, up
     to 16 waves, LDS ring hand-off between waves), the one-wave kernel, and the two
     splitting one list (the multi-wave kernel takes the first grid entries) give the
     oracle's alignments -- IUPAC, '-' and lower-case reads, reads longer and shorter
     than the amplicon, big indels."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "band")
-    monkeypatch.setenv("CRISPR_NW_BAND_SLOTS", "1")
+    monkeypatch.setenv("CRISPR_NW_KERNEL", "full")
     if exact != "wave":
         monkeypatch.setenv("CRISPR_NW_EXACT", "multi")
     if exact == "split":   # 7 reads to the multi-wave kernel, the rest to the one-wave kernel
@@ -184,8 +180,7 @@ def test_exact_kernel_work_list(gpu_aligner_factory, oracle, monkeypatch, La, ex
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
     assert_same(oracle, amp, buf, off, batch, f"exact-{exact} La={La}")
-    # reads whose length differs from the amplicon's cannot fit a one-slot band
-    assert a.fallbacks() >= int((np.diff(off) != La).sum()) - 1
+    assert a.geometry()["tb_mode"] in ("full-lds", "full-global")
 
 
 @pytest.mark.parametrize("mode", ["ops", "rows"])
@@ -238,24 +233,8 @@ def test_endweight(gpu_aligner_factory, oracle, monkeypatch, La, ends, mode):
     assert free["score"] != oracle.align(amp, amp[La // 4:], p)[0]["score"]
 
 
-@pytest.mark.parametrize("slots", ["0", "8", "24"])
-def test_band_width_settings(gpu_aligner_factory, oracle, monkeypatch, slots):
-    """Same answers with the band off (full storage only) or very narrow (mostly fallbacks)."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
-    monkeypatch.setenv("CRISPR_NW_BAND_SLOTS", slots)
-    amp = synth.random_amplicon(250, 1)
-    buf, off = synth.reads_from(amp, 600, 12, synth.PARITY_MIX)
-    a = gpu_aligner_factory()
-    a.set_reference(amp)
-    batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == ("full-lds" if slots == "0" else "stream-int16")
-    assert_same(oracle, amp, buf, off, batch, f"slots={slots}")
-
-
-@pytest.mark.parametrize("family", sorted(BANDED))
-def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle, monkeypatch, family):
-    """Packed kernels: partners of different lengths, empty partners, odd batch size."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", family)
+def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle):
+    """Band pairs: partners of different lengths, empty partners, odd batch size."""
     amp = synth.random_amplicon(230, 41)
     rng = np.random.Generator(np.random.PCG64(41))
     reads = []
@@ -268,12 +247,12 @@ def test_pairs_with_unequal_and_empty_reads(gpu_aligner_factory, oracle, monkeyp
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == BANDED[family]
+    assert a.geometry()["tb_mode"] == "diag-int16"
     assert_same(oracle, amp, buf, off, batch, "pairs")
 
 
 def _mixed_lengths(amp, n, seed):
-    """Reads of every length class: tiny (< the stream's minimum pair span),
+    """Reads of every length class: tiny,
     short, full, longer than the amplicon, empty; exact copies and variants."""
     rng = np.random.Generator(np.random.PCG64(seed))
     La = len(amp)
@@ -294,41 +273,21 @@ def _mixed_lengths(amp, n, seed):
     return reads
 
 
-@pytest.mark.parametrize("grid", ["1", "3"])
-def test_stream_long_streams(gpu_aligner_factory, oracle, monkeypatch, grid):
-    """Stream kernel with a tiny grid: every wavefront streams hundreds of pairs
-    back to back (descriptor ring wrap, column ring wrap, chunk refills, pairs
-    of every length class including those shorter than the minimum span)."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
-    monkeypatch.setenv("CRISPR_NW_STREAM_GRID", grid)
-    amp = synth.random_amplicon(250, 5)
-    reads = _mixed_lengths(amp, 1500, 5)
-    sub, soff = synth.reads_from(amp, 1500, 6, synth.PARITY_MIX)
-    reads += synth.unpack(sub, soff)
-    buf, off = pack_reads(reads)
-    a = gpu_aligner_factory()
-    a.set_reference(amp)
-    batch = a.align_packed(buf, off)
-    assert a.geometry()["tb_mode"] == "stream-int16"
-    assert_same(oracle, amp, buf, off, batch, f"stream grid={grid}")
-
-
 @pytest.mark.parametrize("La", [31, 100, 250, 500])
-def test_stream_mixed_lengths(gpu_aligner_factory, oracle, monkeypatch, La):
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
-    monkeypatch.setenv("CRISPR_NW_STREAM_GRID", "2")
+def test_mixed_lengths(gpu_aligner_factory, oracle, La):
+    """Every length class (tiny, short, full, longer than the amplicon, empty) on the
+    band path: pairs of unequal lengths, reads past the band's length cap."""
     amp = synth.random_amplicon(La, 300 + La)
     reads = _mixed_lengths(amp, 400, La)
     buf, off = pack_reads(reads)
     a = gpu_aligner_factory()
     a.set_reference(amp)
-    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"stream La={La}")
+    assert_same(oracle, amp, buf, off, a.align_packed(buf, off), f"mixed La={La}")
 
 
-def test_stream_pair_table_rare_codes(gpu_aligner_factory, oracle, monkeypatch):
-    """Reads with IUPAC codes outside the pair table (A T G C N, pad) are flagged
-    in the fill kernel and re-aligned by the exact fallback; their partners are not."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
+def test_rare_codes_go_exact(gpu_aligner_factory, oracle):
+    """Reads with IUPAC codes outside A C G T N are flagged by the band fill and
+    re-aligned by the exact kernel; their pair partners are not."""
     amp = synth.random_amplicon(240, 17)
     buf0, off0 = synth.reads_from(amp, 600, 18, synth.PARITY_MIX)
     reads = synth.unpack(buf0, off0)
@@ -350,12 +309,12 @@ def test_stream_pair_table_rare_codes(gpu_aligner_factory, oracle, monkeypatch):
     assert_same(oracle, amp, buf, off, batch, "rare-codes")
 
 
-def test_stream_multiple_passes(gpu_aligner_factory, oracle, monkeypatch):
-    """A region budget smaller than the batch splits it into several fill+walk passes."""
-    monkeypatch.setenv("CRISPR_NW_KERNEL", "stream")
-    monkeypatch.setenv("CRISPR_NW_REGION_MB", "2")      # ~120 pairs per pass at 250 bp
+def test_band_multiple_passes(gpu_aligner_factory, oracle, monkeypatch):
+    """A region budget smaller than the batch splits the band levels into several
+    fill + walk passes."""
+    monkeypatch.setenv("CRISPR_NW_REGION_MB", "2")
     amp = synth.random_amplicon(250, 8)
-    buf, off = synth.reads_from(amp, 1001, 9, synth.PARITY_MIX)
+    buf, off = synth.reads_from(amp, 3001, 9, synth.PARITY_MIX)
     a = gpu_aligner_factory()
     a.set_reference(amp)
     batch = a.align_packed(buf, off, mode="rows")   # kernel_times describe an upload/run pass
