@@ -149,17 +149,6 @@ __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W)
     return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max) * (W / 2) * 4 + 255) & ~(int64_t)255;
 }
 
-// ============================================================================
-// Counting sort of the reads by length (bucket cap + 1 holds longer reads).
-// Block b owns the reads [b * chunk, (b + 1) * chunk): LDS histogram, a
-// bucket-major table of per-block counts, one exclusive scan over it, then each
-// block scatters through its own LDS cursors -- no global atomics.
-// ============================================================================
-__device__ __forceinline__ int len_bucket(const int64_t* offsets, long long r, int cap) {
-    const long long L = offsets[r + 1] - offsets[r];
-    return L <= cap ? (int)L : cap + 1;
-}
-
 // Sort key of every read: its length bucket, or cap + 2 for a read identical to the
 // amplicon (case-insensitive, A C G T only).  Such a read needs no DP: its full
 // diagonal scores S = maxsub * La, every other alignment pairs at most La - 1
@@ -301,83 +290,102 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     }
 }
 
-__device__ __forceinline__ void sort_chunk(const KernelArgs& a, long long* lo, long long* hi) {
-    const long long chunk = (a.n + gridDim.x - 1) / gridDim.x;
-    *lo = (long long)blockIdx.x * chunk;
-    *hi = *lo + chunk < a.n ? *lo + chunk : a.n;
-}
+// ============================================================================
+// Length sort, one launch: segments of kSegReads reads, each sorted by key in LDS
+// (stable: read order within a key), the reads that need the DP (every key but the
+// exact-copy key) placed at the segment's base in the DP list -- an exclusive prefix of
+// the segments' DP counts found by look-back (nw_common.h lookback_excl).  Pairs are
+// consecutive DP-list positions: reads of one length within a segment (most of a
+// CRISPResso segment shares the amplicon's length), so a pair's band holds both reads.
+// Replaces a global counting sort (per-block histograms, two scans, scatter: four
+// launches of ~8 us each per chunk).  The last segment writes the DP count (*band_count).
+// ============================================================================
+constexpr int kSegReads = 4096, kSegThreads = 1024, kSegWaves = kSegThreads / 64;
 
-__global__ __launch_bounds__(256) void nw_band_hist(const KernelArgs a) {
-    extern __shared__ int hist[];
-    const int nb = a.band_lb_cap + 3;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
-    __syncthreads();
-    long long lo, hi;
-    sort_chunk(a, &lo, &hi);
-    for (long long r = lo + threadIdx.x; r < hi; r += blockDim.x) atomicAdd(&hist[a.sort_key[r]], 1);
-    __syncthreads();
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) a.sort_hist[(long long)k * gridDim.x + blockIdx.x] = hist[k];
-}
+__host__ __device__ inline int segsort_lds_bytes(int lb_cap) { return 4 * (kSegWaves + 1) * (lb_cap + 3) + 4 * 32; }
 
-// exclusive scan of each bucket's row of per-block counts (one wavefront per
-// bucket); the row total goes to the base array after the table
-__global__ __launch_bounds__(64) void nw_band_rowscan(const KernelArgs a, int grid) {
-    const int lane = threadIdx.x;
-    int* row = a.sort_hist + (long long)blockIdx.x * grid;
-    const int per = (grid + 63) / 64;
-    const int lo = lane * per, hi = lo + per < grid ? lo + per : grid;
-    int s = 0;
-    for (int k = lo; k < hi; ++k) s += row[k];
-    int incl = s;
+__global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs a, unsigned epoch) {
+    extern __shared__ int seg_sm[];
+    const int NB = a.band_lb_cap + 3, EX = NB - 1;   // key EX: exact copy (no DP)
+    int* cnt = seg_sm;                  // [kSegWaves][NB]: per-wave counts, then prefix over waves
+    int* kbase = seg_sm + kSegWaves * NB;   // [NB]: bucket totals, then their exclusive prefix
+    int* misc = kbase + NB;             // [0] look-back result, [1] DP count, [2] error, [16..31] wave sums
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int k = tid; k < kSegWaves * NB + NB; k += kSegThreads) seg_sm[k] = 0;
+    if (tid < 32) misc[tid] = 0;
+    __syncthreads();
+    const long long r0 = (long long)blockIdx.x * kSegReads + 4 * tid;
+    int key[4], rank[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const long long r = r0 + i;
+        const int k = r < a.n ? a.sort_key[r] : EX;
+        // lanes with the same key this round (11 key bits cover NB <= 2048)
+        unsigned long long m = ~0ull;
+#pragma unroll
+        for (int bit = 0; bit < 11; ++bit) {
+            const unsigned long long bb = __ballot((k >> bit) & 1);
+            m &= ((k >> bit) & 1) ? bb : ~bb;
+        }
+        const unsigned long long below = m & ((1ull << lane) - 1ull);
+        const int old = cnt[wave * NB + k];
+        __builtin_amdgcn_wave_barrier();
+        if (below == 0ull) cnt[wave * NB + k] = old + (int)__builtin_popcountll(m);
+        lds_fence();
+        key[i] = k;
+        rank[i] = old + (int)__builtin_popcountll(below);
+    }
+    __syncthreads();
+    // per key: prefix over the waves (in place) and the key's total
+    for (int k = tid; k < NB; k += kSegThreads) {
+        int run = 0;
+        for (int w = 0; w < kSegWaves; ++w) {
+            const int v = cnt[w * NB + k];
+            cnt[w * NB + k] = run;
+            run += v;
+        }
+        kbase[k] = k == EX ? 0 : run;
+    }
+    __syncthreads();
+    // exclusive prefix of the key totals (thread t: keys [t * per, (t + 1) * per))
+    const int per = (NB + kSegThreads - 1) / kSegThreads;
+    const int k0 = tid * per, k1 = min(NB, k0 + per);
+    int mine = 0;
+    for (int k = k0; k < k1; ++k) mine += kbase[k];
+    int incl = mine;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
     }
-    int run = incl - s;
-    for (int k = lo; k < hi; ++k) {
-        const int c = row[k];
-        row[k] = run;
-        run += c;
-    }
-    if (lane == 63) a.sort_hist[(long long)(a.band_lb_cap + 3) * grid + blockIdx.x] = incl;
-}
-
-// exclusive scan of the bucket totals (one block)
-__global__ __launch_bounds__(1024) void nw_band_scan(const KernelArgs a, int grid) {
-    __shared__ int part[1024];
-    int* base = a.sort_hist + (long long)(a.band_lb_cap + 3) * grid;
-    const int nb = a.band_lb_cap + 3;
-    const int per = (nb + 1023) / 1024;
-    const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
-    int s = 0;
-    for (int k = lo; k < hi; ++k) s += base[k];
-    part[threadIdx.x] = s;
+    if (lane == 63) misc[16 + wave] = incl;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
+    int before = 0, dp = 0;
+#pragma unroll
+    for (int w = 0; w < kSegWaves; ++w) {
+        before += w < wave ? misc[16 + w] : 0;
+        dp += misc[16 + w];
     }
-    int run = part[threadIdx.x] - s;
-    for (int k = lo; k < hi; ++k) {
-        const int c = base[k];
-        base[k] = run;
-        run += c;
+    int run = before + incl - mine;
+    for (int k = k0; k < k1; ++k) {
+        const int v = kbase[k];
+        kbase[k] = run;
+        run += v;
     }
-}
-
-__global__ __launch_bounds__(256) void nw_band_scatter(const KernelArgs a) {
-    extern __shared__ int cur[];
-    const int nb = a.band_lb_cap + 3;
-    const int* base = a.sort_hist + (long long)nb * gridDim.x;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) cur[k] = base[k] + a.sort_hist[(long long)k * gridDim.x + blockIdx.x];
+    if (wave == 0) {
+        const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dp, &misc[2]);
+        if (lane == 0) misc[0] = (int)base;
+    }
     __syncthreads();
+    const long long base = misc[0];
     int32_t* order = const_cast<int32_t*>(a.band_order);
-    long long lo, hi;
-    sort_chunk(a, &lo, &hi);
-    for (long long r = lo + threadIdx.x; r < hi; r += blockDim.x)
-        order[atomicAdd(&cur[a.sort_key[r]], 1)] = (int32_t)r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (key[i] != EX) order[base + kbase[key[i]] + cnt[wave * NB + key[i]] + rank[i]] = (int32_t)(r0 + i);
+    if (tid == 0) {
+        if (misc[2]) a.fallback_count[3] = 1;   // look-back cut off: the call reports an error
+        if (blockIdx.x == gridDim.x - 1) *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dp);
+    }
 }
 
 // ============================================================================
@@ -1299,39 +1307,10 @@ __device__ int block_excl_scan_i32(int v, int* total) {
     return before + incl - v;
 }
 
-__global__ __launch_bounds__(256) void nw_band_redo_blocksum(const KernelArgs a) {
-    const long long n = *a.band_count;
-    const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
-    int s = 0;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) s += k0 + t < n ? a.redo_flags[k0 + t] : 0;
-    int total;
-    block_excl_scan_i32(s, &total);
-    if (threadIdx.x == 0) a.redo_blk[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(1024) void nw_band_redo_scan(const KernelArgs a, int nblk) {
-    __shared__ int part[1024];
-    int carry = 0;
-    for (int t0 = 0; t0 < nblk; t0 += 1024) {
-        const int t = t0 + (int)threadIdx.x;
-        const int v = t < nblk ? a.redo_blk[t] : 0;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const int u = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-            __syncthreads();
-            part[threadIdx.x] += u;
-            __syncthreads();
-        }
-        if (t < nblk) a.redo_blk[t] = carry + part[threadIdx.x] - v;
-        carry += part[1023];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *a.redo_count = carry;
-}
-
-__global__ __launch_bounds__(256) void nw_band_redo_scatter(const KernelArgs a) {
+// One launch: flags of block b's 1024 positions, its exclusive prefix by look-back,
+// scatter; the last block writes the count (*redo_count).
+__global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, unsigned epoch) {
+    __shared__ int sh[2];
     const long long n = *a.band_count;
     const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
     int f[4], s = 0;
@@ -1340,18 +1319,27 @@ __global__ __launch_bounds__(256) void nw_band_redo_scatter(const KernelArgs a) 
         f[t] = k0 + t < n ? a.redo_flags[k0 + t] : 0;
         s += f[t];
     }
+    if (threadIdx.x == 0) sh[1] = 0;
     int total;
-    int pos = a.redo_blk[blockIdx.x] + block_excl_scan_i32(s, &total);
+    const int local = block_excl_scan_i32(s, &total);
+    if (threadIdx.x < 64) {
+        const unsigned e = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)total, &sh[1]);
+        if (threadIdx.x == 0) sh[0] = (int)e;
+    }
+    __syncthreads();
+    int pos = sh[0] + local;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
         if (f[t]) a.redo_list[pos++] = a.band_order[k0 + t];
+    if (threadIdx.x == 0) {
+        if (sh[1]) a.fallback_count[3] = 1;
+        if (blockIdx.x == gridDim.x - 1) *a.redo_count = sh[0] + total;
+    }
 }
 
-hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s) {
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s) {
     const int nblk = (int)std::max<int64_t>(1, (nmax + kRedoBlock - 1) / kRedoBlock);
-    hipLaunchKernelGGL(nw_band_redo_blocksum, dim3(nblk), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(nw_band_redo_scan, dim3(1), dim3(1024), 0, s, a, nblk);
-    hipLaunchKernelGGL(nw_band_redo_scatter, dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nw_band_redo_compact, dim3(nblk), dim3(256), 0, s, a, epoch);
     return hipGetLastError();
 }
 
@@ -1374,19 +1362,17 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
         walk_blocks, W == 16 ? (const void*)nw_band_walk<16> : (const void*)nw_band_walk<32>, 64 * walk_wpb, walk_lds);
 }
 
-// a.sort_hist holds (band_lb_cap + 3) * (grid + 1) ints: the count table, then the bucket
-// bases; a.band_count points at the base of the exact bucket (= reads that need the DP)
-hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s) {
-    const int nb = a.band_lb_cap + 3;
-    const size_t lds = sizeof(int) * (size_t)nb;
+// classify (exact copies, sort keys) then the segment sort; a.band_count receives the
+// DP count, a.lb_status holds ceil(n / kSegReads) look-back words
+hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) {
     hipLaunchKernelGGL(nw_band_classify, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))), dim3(256),
                        (size_t)(8 * ((a.La + 3) / 4)), s, a);
-    hipLaunchKernelGGL(nw_band_hist, dim3(grid), dim3(256), lds, s, a);
-    hipLaunchKernelGGL(nw_band_rowscan, dim3(nb), dim3(64), 0, s, a, grid);
-    hipLaunchKernelGGL(nw_band_scan, dim3(1), dim3(1024), 0, s, a, grid);
-    hipLaunchKernelGGL(nw_band_scatter, dim3(grid), dim3(256), lds, s, a);
+    const int nseg = (int)std::max<int64_t>(1, (a.n + kSegReads - 1) / kSegReads);
+    hipLaunchKernelGGL(nw_band_segsort, dim3(nseg), dim3(kSegThreads), (size_t)segsort_lds_bytes(a.band_lb_cap), s, a,
+                       epoch);
     return hipGetLastError();
 }
+int64_t band_lookback_words(int64_t n) { return std::max<int64_t>(1, (n + 1023) / 1024) + 1; }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {

@@ -67,6 +67,64 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
 
 __device__ __forceinline__ int wave_sum(int v) { return (int)wave_sum_u32((unsigned)v); }
 
+// ---- single-pass block prefix (decoupled look-back) --------------------------------
+// One launch instead of block sums + one scan block + scatter.  Block b publishes an
+// 8-byte status {epoch, flag, value} per block: first its own aggregate (AGG), then its
+// inclusive prefix (INC) once it has it; it finds its exclusive prefix by reading back
+// over its predecessors, 64 at a time (one per lane), summing aggregates down to the
+// nearest inclusive prefix.  The status words are written and read with agent-scope
+// 8-byte atomics (sc1: at the memory side, coherent across the XCDs' L2s, no L2
+// write-back fence -- MI355X_MICROARCH.md, inter-workgroup visibility); nothing else is
+// handed between blocks inside the launch.  `epoch` (30 bits, new per launch) replaces
+// zeroing the array between launches.  Relies on workgroups being dispatched in index
+// order (a predecessor is resident or done when a block waits for it); a wait that never
+// ends is cut off after ~10^7 polls and reported through *bad (the caller's error flag)
+// instead of hanging the device.
+constexpr unsigned kLbAgg = 1u, kLbInc = 2u;
+__device__ __forceinline__ unsigned long long lb_word(unsigned epoch, unsigned flag, unsigned value) {
+    return ((unsigned long long)((epoch << 2) | flag) << 32) | value;
+}
+// Called by every lane of ONE wave of block b (uniform control flow); returns the
+// exclusive prefix of block b's `agg` (the same value in every lane).
+__device__ inline unsigned lookback_excl(unsigned long long* st, long long b, unsigned epoch, unsigned agg,
+                                         int* bad) {
+    const int lane = threadIdx.x & 63;
+    epoch &= 0x3fffffffu;
+    if (b == 0) {
+        if (lane == 0) __hip_atomic_store(st, lb_word(epoch, kLbInc, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0u;
+    }
+    if (lane == 0) __hip_atomic_store(st + b, lb_word(epoch, kLbAgg, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned excl = 0u;
+    long long j = b - 1;   // the newest predecessor not yet summed
+    int polls = 0;
+    for (;;) {
+        const long long idx = j - lane;
+        unsigned long long v = lb_word(epoch, kLbInc, 0u);   // before block 0: an inclusive 0
+        if (idx >= 0) v = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned tag = (unsigned)(v >> 32);
+        const bool ready = (tag >> 2) == epoch && (tag & 3u) != 0u;
+        const unsigned long long inc = __ballot(ready && (tag & 3u) == kLbInc);
+        const unsigned long long notr = __ballot(!ready);
+        const int first = inc ? (int)__builtin_ctzll(inc) : 64;      // nearest inclusive prefix
+        const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+        if (notr & need) {   // a predecessor before it has not published yet: poll again
+            if (++polls > (1 << 23)) {
+                if (lane == 0) *bad = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum_u32(lane <= first ? (unsigned)v : 0u);
+        if (first < 64) break;
+        j -= 64;
+    }
+    if (lane == 0)
+        __hip_atomic_store(st + b, lb_word(epoch, kLbInc, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 // Candidate key for the traceback start cell.  Scan order of the reference
 // walk start (corner, then last column bottom->top, then last row right->left,
 // first strict maximum) becomes "largest (score, priority)".

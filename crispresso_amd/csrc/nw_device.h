@@ -54,14 +54,13 @@ struct KernelArgs {
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
     const uint32_t* band_tab;      // [17 amplicon codes (EDNAFULL, pad)][6][6 read codes] packed int16x2 score + 2 E
     const uint32_t* rowpos;        // [La] codes each amplicon row scores > 0 against (markup ':')
-    int32_t* sort_hist;            // [band_lb_cap + 3][sort grid + 1] per-block bucket counts, bucket bases
     int32_t* sort_key;             // [n] bucket of every read: length, band_lb_cap + 1 (longer), + 2 (exact copy)
     const int32_t* band_count;     // device: entries of band_order to align (sorted reads that need the DP,
                                    // or the previous level's redo count)
+    unsigned long long* lb_status; // look-back words of the single-pass scans (band_lookback_words(n))
     int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
     int32_t* redo_count;
     uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
-    int32_t* redo_blk;             // [ceil(n / 1024)] compaction scratch
     int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
     // > 0: when the first level hands on at most this many reads (*redo_count), the second
     // level's kernels return at once and the exact kernel takes them too (its fallback list,
@@ -138,7 +137,10 @@ int64_t band_region_bytes(int La, int Lb_max, int W);
 bool band_pair_geometry(int La, int Lb, int* dlo);
 hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
                           int* walk_blocks);
-hipError_t launch_band_sort(const KernelArgs& a, int grid, hipStream_t s);
+// classify + the segment sort (a.band_count <- reads that need the DP); `epoch`: a value
+// not used by the previous look-back launch on a.lb_status
+hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
+int64_t band_lookback_words(int64_t n);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
@@ -147,7 +149,7 @@ hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int
                          const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s);
 // the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
 // nmax >= the number of sorted positions (grid size)
-hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, hipStream_t s);
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s);
 
 // exact int32 kernel for work lists (nw_exact.hip): one workgroup of exact_waves(La)
 // wavefronts per read; traceback slots in LDS (tb_lds) or a per-block HBM slab of
@@ -161,25 +163,28 @@ int64_t exact_slab_bytes(int La, int Lb_max);
 hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_lds, int64_t slab_bytes, bool cap,
                         hipStream_t s);
 
-// ops compaction (nw_ops.hip): per-read slots -> one contiguous run array.
-// ctl (int64, kOpsCtl): [0] running base over the chunks of a call (in/out), [1] this chunk's
-// base, [2] this chunk's total, [3] errors (1: staging full, 2: spill area full, from
-// opsctl[1]); running over the call: [4] exact-kernel reads, [5] second band level reads of
-// two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the second
-// level alone (OpsCounts: the device counters of the chunk's kernels).
-// blk: ceil(n / kOpsBlockReads) int64.  opsctl: the kernels' flags.  hctl: pinned host
-// copy of ctl written by the compaction (or null).
+// ops compaction (nw_ops.hip): per-read slots -> one contiguous run array, one launch.
+// ctl (int64, kOpsCtl + 2): [0] running total after this chunk, [1] this chunk's base, [2]
+// this chunk's total, [3] errors (1: staging full, 2: spill area full, from opsctl[1], 4: a
+// look-back cut off); running over the call: [4] exact-kernel reads, [5] second band level
+// reads of two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the
+// second level alone (OpsCounts: the device counters of the chunk's kernels); [8], [9]: the
+// running base, read from [8 + parity] and written to the other (chunk k: parity k & 1).
+// status: band_lookback_words(n) look-back words; epoch: new per launch.  opsctl: the
+// kernels' flags.  hctl: pinned host copy of ctl[0 .. kOpsCtl) written by the launch (or null).
 constexpr int kOpsBlockReads = 1024;
 constexpr int kOpsCtl = 8;
+constexpr int kOpsCtlAll = kOpsCtl + 2;
 struct OpsCounts {
-    const int32_t* fallback;   // [0]: exact-kernel reads of the chunk
+    const int32_t* fallback;   // [0]: exact-kernel reads of the chunk, [3]: look-back error flag
     const int32_t* redo;       // second band level reads (null: one level)
     const int32_t* band;       // reads that needed the DP (null: not the band path)
     int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
     int32_t one_level;         // the chunk ran the 32-diagonal level alone: its DP reads go to ctl[7]
 };
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
-                              int64_t* blk, int64_t* ctl, int64_t* ops_off, uint32_t* staging, int64_t staging_cap,
-                              int32_t* opsctl, const OpsCounts& cnt, hipStream_t s, int64_t* hctl = nullptr);
+                              unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
+                              uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
+                              hipStream_t s, int64_t* hctl = nullptr);
 
 }  // namespace nw

@@ -68,17 +68,16 @@ struct Scratch {
     DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
-    DevBuf<int32_t> d_redo_blk;
-    DevBuf<int32_t> d_order, d_sort_hist, d_sort_key;
+    DevBuf<int32_t> d_order, d_sort_key;
+    DevBuf<unsigned long long> d_lb;   // look-back words of the single-pass scans (sort, redo list, ops)
     DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
     DevBuf<int32_t> d_nops, d_opsctl;
-    DevBuf<int64_t> d_blk;
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_redo.release();
-        d_redo_flags.release(); d_redo_blk.release(); d_order.release(); d_sort_hist.release(); d_sort_key.release();
+        d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
-        d_opsctl.release(); d_blk.release();
+        d_opsctl.release();
     }
 };
 constexpr int kScratchSets = 3;
@@ -138,7 +137,8 @@ struct nw_ctx {
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
-    int diag_words = 0, diag_lb_cap = 0, diag_sort_grid = 1;
+    int diag_words = 0, diag_lb_cap = 0;
+    unsigned epoch = 0;               // look-back launches so far (each launch uses a new value)
     bool ran = false;
     // ops output (nw_align_ops / nw_batch_set_output(NW_OUT_OPS)): per-read run slots,
     // spill area, compaction scratch; the pipelined call's copy streams and events
@@ -171,6 +171,13 @@ int fail(nw_ctx* c, int code, const char* fmt, ...) {
     va_end(ap);
     if (c) c->err = buf;
     return code;
+}
+
+// a look-back launch's epoch: new per launch, never 0 (30 bits, nw_common.h lookback_excl)
+unsigned next_epoch(nw_ctx* c) {
+    c->epoch = (c->epoch + 1) & 0x3fffffffu;
+    if (c->epoch == 0) c->epoch = 1;
+    return c->epoch;
 }
 
 #define HIP_OR_FAIL(ctx, expr)                                                        \
@@ -473,7 +480,6 @@ int configure(nw_ctx* c) {
                            level(16, c->diag16_fill, c->diag16_walk, c->diag16_stride, c->diag16_pass_pairs);
         if (!use16) c->diag16_fill.grid = 0;
         if (level(32, c->diag_fill, c->diag_walk, c->diag_stride, c->diag_pass_pairs)) {
-            c->diag_sort_grid = (int)std::max<int64_t>(1, std::min<int64_t>((c->n + 1023) / 1024, 1024));
             const int64_t rbytes = std::max(std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs) * c->diag_stride,
                                             use16 ? std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag16_pass_pairs) *
                                                         c->diag16_stride : 0);
@@ -481,8 +487,7 @@ int configure(nw_ctx* c) {
             HIP_OR_FAIL(c, c->s->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->s->d_redo_blk.reserve((size_t)std::max<int64_t>((c->n + 1023) / 1024, 1)));
-            HIP_OR_FAIL(c, c->s->d_sort_hist.reserve(((size_t)c->diag_lb_cap + 3) * (c->diag_sort_grid + 1)));
+            HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(c->n)));
             HIP_OR_FAIL(c, c->s->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
             c->use_diag = true;
         }
@@ -736,10 +741,10 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.band_maxsub = 5 * c->scale;
         a.band_tab = c->d_btab.p;
         a.rowpos = c->cur.rowpos;
-        a.sort_hist = c->s->d_sort_hist.p;
         a.sort_key = c->s->d_sort_key.p;
-        a.band_count = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
-        HIP_OR_FAIL(c, nw::launch_band_sort(a, c->diag_sort_grid, c->cs));
+        a.band_count = c->s->d_fallback_count.p + 1;   // the sort writes the DP count here
+        a.lb_status = c->s->d_lb.p;
+        HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
@@ -751,10 +756,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         const bool only16 = two && lv && std::strcmp(lv, "16") == 0;
         a.redo_list = c->s->d_redo.p;
         a.redo_count = c->s->d_fallback_count.p + 2;
-        if (two && !only16) {
-            a.redo_flags = c->s->d_redo_flags.p;
-            a.redo_blk = c->s->d_redo_blk.p;   // flags: the first level's walk writes every position's
-        }
+        if (two && !only16) a.redo_flags = c->s->d_redo_flags.p;   // the first level's walk writes every position's
         // a chunk whose first level hands on at most `direct` reads skips the second level on
         // the device: the exact kernel takes them (CRISPR_NW_DIRECT=0: always both levels)
         int direct = 1024;
@@ -767,7 +769,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             al.redo_direct = lvl == 1 ? direct : 0;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
-                HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, c->cs));
+                HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, next_epoch(c), c->cs));
                 al.band_order = c->s->d_redo.p;
                 al.band_count = a.redo_count;
             }
@@ -820,8 +822,8 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
     HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));
-    HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtl));
-    HIP_OR_FAIL(c, c->s->d_blk.reserve((size_t)((chunk + nw::kOpsBlockReads - 1) / nw::kOpsBlockReads)));
+    HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtlAll));
+    HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(chunk)));
     HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));
     HIP_OR_FAIL(c, c->s->d_staging.reserve((size_t)c->staging_cap));
     return NW_OK;
@@ -831,7 +833,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
 // staging[which]: ops_off of those reads (global: the call's running base in
 // ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
 int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr,
-                     int64_t* hctl = nullptr) {
+                     int64_t* hctl = nullptr, int parity = 0) {
     int rc = launch_range(c, base);
     if (rc) return rc;
     // only the compaction writes the set's staging array: it waits for the copy of the
@@ -842,7 +844,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     nw::OpsCounts cnt{};
     cnt.fallback = c->s->d_fallback_count.p;
     if (c->use_diag && c->n > 0) {
-        cnt.band = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
+        cnt.band = c->s->d_fallback_count.p + 1;
         // second-level reads of a two-level chunk; a chunk run on the 32-diagonal level alone
         // counts its DP reads apart (ctl[7]: the adaptive choice reads two-level chunks only)
         if (c->diag16_fill.grid > 0 && !c->skip16) cnt.redo = c->s->d_fallback_count.p + 2;
@@ -850,9 +852,9 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         cnt.direct = c->skip16 ? 0 : c->redo_direct;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
-    HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n, c->s->d_blk.p,
-                                          c->d_ctl64.p, c->d_opsoff.p + base, c->s->d_staging.p, c->staging_cap,
-                                          c->s->d_opsctl.p, cnt, c->cs, hctl));
+    HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n,
+                                          c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
+                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl));
     return NW_OK;
 }
 
@@ -889,6 +891,7 @@ int ops_events(nw_ctx* c, size_t chunks) {
 }
 
 int ops_error(nw_ctx* c, int64_t err) {
+    if (err & 4) return fail(c, NW_E_HIP, "a device prefix scan waited too long for its predecessor blocks");
     if (err & 2) return fail(c, NW_E_NOMEM, "ops spill area full: reads with more than %d traceback runs need more "
                                             "than CRISPR_NW_SPILL_MB (%lld MB)", c->ops_slot,
                              (long long)(c->spill_cap * 4 >> 20));
@@ -914,7 +917,7 @@ int nw_batch_run_async(nw_ctx* c) {
     if (c->out_mode == NW_OUT_OPS) {
         if (!c->s->d_slots.p || c->s->d_nops.cap < (size_t)std::max<int64_t>(c->n, 1))
             return fail(c, NW_E_STATE, "batch uploaded before nw_batch_set_output(NW_OUT_OPS)");
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
+        HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
         rc = launch_range_ops(c, 0);
     } else {
         rc = launch_range(c, 0);
@@ -943,6 +946,11 @@ int nw_batch_download(nw_ctx* c, char* aln_out, int64_t stride, nw_stat* stats) 
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     if (c->n == 0) return NW_OK;
     if (aln_out && c->out_mode == NW_OUT_OPS) return fail(c, NW_E_STATE, "ops output: use nw_batch_download_ops");
+    if (c->use_diag) {   // the band path's single-pass scans report a cut-off look-back here
+        int32_t fb[4] = {0, 0, 0, 0};
+        HIP_OR_FAIL(c, hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
+        if (fb[3]) return ops_error(c, 4);
+    }
     if (stats)
         HIP_OR_FAIL(c, hipMemcpy(stats, c->d_stats.p, sizeof(nw::Stat) * (size_t)c->n, hipMemcpyDeviceToHost));
     if (aln_out) {
@@ -1230,12 +1238,12 @@ struct HostTimer {
 struct CfgState {
     nw::LaunchCfg cfg, diag_fill, diag_walk, diag16_fill, diag16_walk;
     bool use_diag, exact_tb_lds, exact_full;
-    int exact_grid, exact_lds, diag_words, diag_lb_cap, diag_sort_grid;
+    int exact_grid, exact_lds, diag_words, diag_lb_cap;
     int64_t exact_slab, diag16_pass_pairs, diag16_stride, diag_pass_pairs, diag_stride, stride;
 };
 CfgState save_cfg(const nw_ctx* c) {
     return CfgState{c->cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->use_diag, c->exact_tb_lds,
-                    c->exact_full, c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap, c->diag_sort_grid,
+                    c->exact_full, c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap,
                     c->exact_slab, c->diag16_pass_pairs, c->diag16_stride, c->diag_pass_pairs, c->diag_stride,
                     c->stride};
 }
@@ -1243,7 +1251,7 @@ void load_cfg(nw_ctx* c, const CfgState& st) {
     c->cfg = st.cfg; c->diag_fill = st.diag_fill; c->diag_walk = st.diag_walk; c->diag16_fill = st.diag16_fill;
     c->diag16_walk = st.diag16_walk; c->use_diag = st.use_diag; c->exact_tb_lds = st.exact_tb_lds;
     c->exact_full = st.exact_full; c->exact_grid = st.exact_grid; c->exact_lds = st.exact_lds;
-    c->diag_words = st.diag_words; c->diag_lb_cap = st.diag_lb_cap; c->diag_sort_grid = st.diag_sort_grid;
+    c->diag_words = st.diag_words; c->diag_lb_cap = st.diag_lb_cap;
     c->exact_slab = st.exact_slab; c->diag16_pass_pairs = st.diag16_pass_pairs; c->diag16_stride = st.diag16_stride;
     c->diag_pass_pairs = st.diag_pass_pairs; c->diag_stride = st.diag_stride; c->stride = st.stride;
 }
@@ -1477,7 +1485,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
     ht.lap(2);
     if (upload) c->reads_bias = pk ? (base0 & ~(int64_t)15) : base0;
-    HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtl * sizeof(int64_t), c->stream));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
     // every upload queued up front: the copy engine streams the batch while chunks compute
     HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
     int64_t h2d_bytes = 0;
@@ -1579,7 +1587,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
-                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k)))
+                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k,
+                                   (int)(k & 1))))
             return restore(rc);
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
@@ -1865,9 +1874,8 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
         return NW_OK;
     }
     int32_t fb[4] = {0, 0, 0, 0}, need = 0;
-    const int32_t* band_count = c->s->d_sort_hist.p + (size_t)(c->diag_lb_cap + 3) * c->diag_sort_grid + c->diag_lb_cap + 2;
     HIP_OR_FAIL(c, hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
-    HIP_OR_FAIL(c, hipMemcpy(&need, band_count, sizeof need, hipMemcpyDeviceToHost));
+    need = fb[1];   // the sort's DP count
     const bool two = c->diag16_fill.grid > 0;
     counts4[0] = c->n - need;             // exact copies (no DP)
     counts4[1] = two ? need : 0;          // first level (16 diagonals)
