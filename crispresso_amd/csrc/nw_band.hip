@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
     // here, the first kernel of the chain, instead of by memset launches
-    if (blockIdx.x == 0 && threadIdx.x < 4) a.fallback_count[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 8) a.fallback_count[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 2 && a.ops) a.ops_ctl[threadIdx.x] = 0;
     for (int k = threadIdx.x; k < nd; k += blockDim.x) {
         unsigned w = 0;
@@ -299,6 +299,9 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
 // CRISPResso segment shares the amplicon's length), so a pair's band holds both reads.
 // Replaces a global counting sort (per-block histograms, two scans, scatter: four
 // launches of ~8 us each per chunk).  The last segment writes the DP count (*band_count).
+// With a.order_a (the diagonal pass, ops output): reads of the amplicon's length go to
+// their own list instead (order_a, *count_a; a second look-back): the reads of a
+// substitution-only variant, which nw_band_fill<W, false> aligns without traceback bits.
 // ============================================================================
 constexpr int kSegReads = 4096, kSegThreads = 1024, kSegWaves = kSegThreads / 64;
 
@@ -309,7 +312,8 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
     const int NB = a.band_lb_cap + 3, EX = NB - 1;   // key EX: exact copy (no DP)
     int* cnt = seg_sm;                  // [kSegWaves][NB]: per-wave counts, then prefix over waves
     int* kbase = seg_sm + kSegWaves * NB;   // [NB]: bucket totals, then their exclusive prefix
-    int* misc = kbase + NB;             // [0] look-back result, [1] DP count, [2] error, [16..31] wave sums
+    int* misc = kbase + NB;             // [0], [1] look-back results (lists B, A), [2] error, [16..31] wave sums
+    const int KA = a.order_a ? a.La : -1;   // the key of list A (none without the diagonal pass)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int k = tid; k < kSegWaves * NB + NB; k += kSegThreads) seg_sm[k] = 0;
     if (tid < 32) misc[tid] = 0;
@@ -344,7 +348,8 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
             cnt[w * NB + k] = run;
             run += v;
         }
-        kbase[k] = k == EX ? 0 : run;
+        kbase[k] = (k == EX || k == KA) ? 0 : run;
+        if (k == KA) misc[3] = run;   // list A's reads in this segment
     }
     __syncthreads();
     // exclusive prefix of the key totals (thread t: keys [t * per, (t + 1) * per))
@@ -372,31 +377,181 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
         kbase[k] = run;
         run += v;
     }
+    const int dpA = misc[3];
     if (wave == 0) {
         const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dp, &misc[2]);
         if (lane == 0) misc[0] = (int)base;
+    } else if (wave == 1 && KA >= 0) {   // list A: the look-back words after list B's
+        const unsigned base = lookback_excl(a.lb_status + gridDim.x + 1, blockIdx.x, epoch, (unsigned)dpA, &misc[2]);
+        if (lane == 0) misc[1] = (int)base;
     }
     __syncthreads();
-    const long long base = misc[0];
+    const long long base = misc[0], baseA = misc[1];
     int32_t* order = const_cast<int32_t*>(a.band_order);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (key[i] != EX) order[base + kbase[key[i]] + cnt[wave * NB + key[i]] + rank[i]] = (int32_t)(r0 + i);
+    for (int i = 0; i < 4; ++i) {
+        const int k = key[i];
+        if (k == KA) a.order_a[baseA + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
+        else if (k != EX) order[base + kbase[k] + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
+    }
     if (tid == 0) {
         if (misc[2]) a.fallback_count[3] = 1;   // look-back cut off: the call reports an error
-        if (blockIdx.x == gridDim.x - 1) *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dp);
+        if (blockIdx.x == gridDim.x - 1) {
+            *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dp);
+            if (KA >= 0) *a.count_a = (int32_t)(baseA + dpA);
+        }
     }
 }
 
 // ============================================================================
 // Fill
 // ============================================================================
+// Epilogue of the diagonal pass (nw_band_fill<W, false>): every lane of the wavefront
+// calls it (ballots).  Per read of the lane's pair: the start cell from the captures (the
+// last cell of each band diagonal lies on the last row or column; same keys and scan
+// order as nw_band_walk), the plain certificate (every alignment leaving the band scores
+// <= UB < S), and the single-diagonal test: the start cell's M equals the plain sum of
+// scores down its diagonal (captured beside M), so the traceback is that diagonal plus
+// the end gaps (nw_band_walk's fast path).  A read that passes gets its
+// record and runs here (identical / similar counts along the diagonal from the LDS
+// codes); any other read -- not certified, not diagonal, a code outside A C G T N, a byte
+// EDNAFULL does not score, more runs than a slot -- goes to tile_list, where the
+// traceback pass and the walk take it (and the refined certificate / the next level).
 template <int W>
+__device__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, const uint32_t* tab,
+                                   const unsigned char* pcd, int La, int dlo, int q, int grp, bool valid, bool act,
+                                   long long ra, long long rb, int LbA, int LbB, unsigned badA, unsigned badB,
+                                   unsigned padA, unsigned padB, unsigned cap0, unsigned cap1, unsigned capB0,
+                                   unsigned capB1, unsigned dc0, unsigned dc1, unsigned dcB0, unsigned dcB1,
+                                   unsigned bv0, unsigned bv1, int lane) {
+    using G = BandGeo<W>;
+    constexpr int L = G::L, PR = G::PR;
+    using LdsU = const __attribute__((address_space(3))) unsigned;
+    const int E = a.gap_extend;
+    const unsigned tabbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)tab;
+    bool fail[2] = {false, false};
+    bool use[2] = {valid, valid && rb != ra};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int Lb = h ? LbB : LbA;
+        const long long rd = h ? rb : ra;
+        // start cell: best key over the pair's W diagonals
+        unsigned key = 0u, eqbits = 0u;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int d = dlo + 2 * q + p;
+            const unsigned cm = p ? (h ? capB1 : cap1) : (h ? capB0 : cap0);
+            const unsigned cd = p ? (h ? dcB1 : dc1) : (h ? dcB0 : dc0);
+            const unsigned bv = p ? bv1 : bv0;
+            const int iend = La < Lb - d ? La : Lb - d;
+            const int ilo = 1 - d > 1 ? 1 - d : 1;
+            if (Lb > 0 && iend >= ilo) {
+                const int v = half(cm, h) - kBias16 - E * (2 * iend + d);
+                const int jend = iend + d;
+                const unsigned k = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
+                                   : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
+                key = k > key ? k : key;
+            }
+            // M of the diagonal's last cell == the diagonal's plain sum (both biased alike)
+            eqbits |= (unsigned)(((cm ^ add2(bv, cd)) >> (16 * h) & 0xffffu) == 0u) << p;
+        }
+#pragma unroll
+        for (int o = PR; o < 16; o <<= 1) {
+            const unsigned u = (unsigned)__shfl_xor((int)key, o, 64);
+            key = u > key ? u : key;
+        }
+        int score = 0, ei = 0, ej = 0;
+        decode_end(end_key_widen(key), La, Lb, &score, &ei, &ej);
+        const int dhi = dlo + W - 1;
+        int pmax = -1;
+        if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
+        if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
+        const bool certified = pmax < 0 || score > a.band_maxsub * pmax;
+        // the start diagonal's test bit, from the lane that owns it
+        const int ds = ej - ei - dlo;
+        const int src = (lane & ~15) | (((ds >> 1) & (L - 1)) * PR + (lane & 15) % PR);
+        const unsigned eqs = (unsigned)__shfl((int)eqbits, src, 64);
+        const bool diag = ((eqs >> (ds & 1)) & 1u) != 0u && ds >= 0 && ds < W;
+        const bool codes_ok = !(h ? (badB | padB) : (badA | padA));
+        const int nd = ei < ej ? ei : ej;
+        const bool endg = (ei == La && ej < Lb) || (ej == Lb && ei < La);
+        const int lead = (ei > ej ? ei : ej) - nd;
+        const int nruns = 1 + (int)endg + (lead > 0);
+        const bool ok = use[h] && act && Lb > 0 && certified && diag && codes_ok && nruns <= a.ops_slot;
+        fail[h] = use[h] && !ok;
+        // identical / similar columns down the diagonal (the pair's L lanes stride over it)
+        unsigned cnt = 0u;
+        if (ok) {
+            for (int t = q; t < nd; t += L) {
+                const int i = ei - t, j = ej - t;   // 1-based cell
+                const unsigned ab = acd[kAPad + i];
+                const unsigned pc = pcd[kJPad + j];
+                const int x = (int)((ab - tabbase) / 144u);   // amplicon EDNAFULL code (row of the table)
+                const int y = (int)(h ? (pc >> 2) % 6u : (pc >> 2) / 6u);   // read: A T G C N pad
+                const int s = half(*(LdsU*)(uintptr_t)(ab + pc), h) - 2 * E;
+                const int ycode = y == 0 ? 0 : y == 1 ? 1 : y == 2 ? 2 : y == 3 ? 3 : 14;
+                const bool id = y < 5 && x == ycode;
+                cnt += (unsigned)id | ((unsigned)(id || s > 0) << 16);
+            }
+        }
+#pragma unroll
+        for (int o = PR; o < 16; o <<= 1) cnt += (unsigned)__shfl_xor((int)cnt, o, 64);
+        if (ok && q == 0) {
+            const int endlen = endg ? (ei == La ? Lb - ej : La - ei) : 0;
+            uint32_t* slot = a.ops + rd * a.ops_slot;
+            int w = 0;
+            if (lead > 0) slot[w++] = ((unsigned)(ei > nd ? RUN_Y : RUN_X) << 28) | (unsigned)lead;
+            slot[w++] = ((unsigned)RUN_M << 28) | (unsigned)nd;
+            if (endg) slot[w++] = ((unsigned)(ei == La ? RUN_X : RUN_Y) << 28) | (unsigned)endlen;
+            a.nops[rd] = w;
+            Stat r;
+            r.aln_len = nd + endlen + lead;
+            r.n_ident = (int)(cnt & 0xffffu);
+            r.n_sim = (int)(cnt >> 16);
+            r.n_gaps = endlen + lead;
+            r.score = score;
+            r.end_i = ei;
+            r.end_j = ej;
+            r.flags = 0;
+            a.stats[rd] = r;
+        }
+    }
+    // the reads handed on: one atomic per wavefront
+    const unsigned long long m0 = __ballot(q == 0 && fail[0]), m1 = __ballot(q == 0 && fail[1]);
+    const int n0 = (int)__builtin_popcountll(m0), tot = n0 + (int)__builtin_popcountll(m1);
+    if (tot) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(a.tile_count, tot);
+        base = __builtin_amdgcn_readfirstlane(base);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        if (q == 0 && fail[0]) a.tile_list[base + __builtin_popcountll(m0 & below)] = (int32_t)ra;
+        if (q == 0 && fail[1]) a.tile_list[base + n0 + __builtin_popcountll(m1 & below)] = (int32_t)rb;
+    }
+}
+
+// Virtual DP list of the traceback pass: band_order[0, *band_count) then (diagonal pass
+// on) tile_list[0, *tile_count) -- the list-A reads the diagonal pass handed on.
+__device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
+    return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
+}
+__device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
+    return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
+}
+
+// TB = true: the traceback pass (bits into the pair's region, the walk follows).
+// TB = false: the diagonal pass over list A (ops output only): no traceback bits at all
+// (9 VALU per lane-step instead of 17), the pure-diagonal score of every band diagonal
+// accumulated beside M; the epilogue takes the start cell, the certificate and the
+// single-diagonal test (start cell's M == its diagonal's plain sum: the traceback is the
+// diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
+// passes; the others go to tile_list for the traceback pass.
+template <int W, bool TB>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
+    if (W == kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
@@ -434,8 +589,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    // sorted positions [0, count) hold the reads that need the DP (the rest are exact copies)
-    const long long count = *a.band_count;
+    // list positions [0, count) hold the reads that need the DP (the rest are exact copies)
+    const long long nb = TB ? (long long)*a.band_count : 0ll;
+    const long long count = TB ? band_list_count(a) : (long long)*a.count_a;
     const long long pair_hi = min(a.band_pair_hi, (count + 1) / 2);
     const long long npairs = pair_hi - a.band_pair_lo;
     const long long nwork = npairs > 0 ? (npairs + kBPW - 1) / kBPW : 0;
@@ -447,8 +603,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         long long offA = 0, offB = 0, ra = 0, rb = 0;
         int LbA = 0, LbB = 0;
         if (g < pair_hi) {
-            ra = a.band_order[2 * g];
-            rb = (2 * g + 1 < count) ? a.band_order[2 * g + 1] : ra;
+            if constexpr (TB) {
+                ra = band_list_read(a, 2 * g, nb);
+                rb = (2 * g + 1 < count) ? band_list_read(a, 2 * g + 1, nb) : ra;
+            } else {
+                ra = a.order_a[2 * g];
+                rb = (2 * g + 1 < count) ? a.order_a[2 * g + 1] : ra;
+            }
             offA = a.offsets[ra];
             offB = a.offsets[rb];
             LbA = (int)(a.offsets[ra + 1] - offA);
@@ -467,6 +628,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         for (int k4 = lane; k4 < kBPW * PCS / 4; k4 += 64) ((unsigned*)pcd_wave)[k4] = 0x8c8c8c8cu;   // pad pair
         const int Lw = (int)wave_max_u32((unsigned)Lmax);
         unsigned bad_mask = 0u;   // bit p: pair p has a read A / B code outside A C G T N (bits 0-15 / 16-31)
+        unsigned pad_mask = 0u;   // the same for bytes EDNAFULL does not score ('-', '*', ...: the walk's gap columns)
         constexpr int kSub = kBPW < 4 ? kBPW : 4;   // pairs staged together (loads in flight)
         for (int c0 = 0; c0 < Lw; c0 += 256)
         for (int p0 = 0; p0 < kBPW; p0 += kSub) {
@@ -499,7 +661,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
             for (int pp = 0; pp < kSub; ++pp) {
                 const int p = p0 + pp;
                 const int Lm = max(lenA[pp], lenB[pp]);
-                bool bA = false, bB = false;
+                bool bA = false, bB = false, zA = false, zB = false;
                 if (4 * k4 < Lm) {
                     unsigned packed = 0u;
 #pragma unroll
@@ -510,6 +672,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                         // lut6: 5 = pad / not in EDNAFULL (scores 0, as EMBOSS does); 6 = IUPAC code
                         bA = bA || cA > kPadCode;
                         bB = bB || cB > kPadCode;
+                        zA = zA || (j0 < lenA[pp] && cA == kPadCode);
+                        zB = zB || (j0 < lenB[pp] && cB == kPadCode);
                         cA = min(cA, kPadCode);
                         cB = min(cB, kPadCode);
                         packed |= (unsigned)((cA * 6 + cB) * 4) << (8 * b);
@@ -520,6 +684,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                 // (pair p's header is written by its own q = 0 lane)
                 if (__ballot(bA)) bad_mask |= 1u << p;
                 if (__ballot(bB)) bad_mask |= 1u << (16 + p);
+                if (!TB && __ballot(zA)) pad_mask |= 1u << p;
+                if (!TB && __ballot(zB)) pad_mask |= 1u << (16 + p);
             }
         }
         const int flags = (((bad_mask >> grp) & 1u) ? REGION_BAD_A : 0) | (((bad_mask >> (16 + grp)) & 1u) ? REGION_BAD_B : 0);
@@ -533,15 +699,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         const int tau_end = (int)wave_max_u32(thi);
         const int tau_pro = (int)wave_max_u32(tpro);
         lds_fence();
-        unsigned char* region = a.band_region + (g - a.band_pair_lo) * a.band_stride;
-        if (q == 0 && g < pair_hi) {
+        unsigned char* region = TB ? a.band_region + (g - a.band_pair_lo) * a.band_stride : nullptr;
+        if (TB && q == 0 && g < pair_hi) {
             // everything the walk needs to find the pair's reads: one 48-byte load
             int4* hp = (int4*)region;
             hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive), 0);
             hp[1] = make_int4((int)ra, (int)rb, (int)(a.offsets[ra + 1] - offA), (int)(a.offsets[rb + 1] - offB));
             hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
         }
-        if (tau_end == 0) continue;   // no active group in this wavefront
+        if (tau_end == 0 && TB) continue;   // no active group in this wavefront
 
         const int d0 = dlo + 2 * q;
         int tb[2], te[2], teB[2];
@@ -562,10 +728,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         // or column; blocks before it skip the capture selects
         const int te_lo = (int)wave_min_u32(min(min((unsigned)te[0], (unsigned)te[1]),
                                                 min((unsigned)teB[0], (unsigned)teB[1])));
-        unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q;   // this lane's slot of each tile
+        unsigned* bits = TB ? (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q : nullptr;   // this lane's slot of each tile
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
         unsigned cap0 = NEG2, cap1 = NEG2, capB0 = NEG2, capB1 = NEG2;   // read A's (low) / B's (high half)
+        // diagonal pass: plain sums of the scores (+2E each) down each diagonal, and their captures
+        unsigned ds0 = 0u, ds1 = 0u, dc0 = 0u, dc1 = 0u, dcB0 = 0u, dcB1 = 0u;
         // LDS code cursors of the block starting at tau4: rows i0, i0 + 1; columns j0 .. j0 + 2
         auto ibase = [&](int tau4) { return (tau4 - kBK) / 2 - q; };
         const uint16_t* ap = acd + kAPad + ibase(tau0);
@@ -589,33 +757,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
             constexpr int P = U & 1;
             constexpr bool PRO = decltype(PROc)::value;
             constexpr bool CAP = decltype(CAPc)::value;
-            unsigned X, Y, d1, d2;
+            unsigned X, Y, d1 = 0u, d2 = 0u;
             if constexpr (P == 0) {
                 // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
                 const unsigned Ml = row_shr<G::PR>(MoP), Xl = row_shr<G::PR>(XP);
                 X = max2(Ml, Xl);
-                d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
+                if constexpr (TB) d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
                 Y = max2(MoP, YP);
-                d1 = sub2(YP, MoP);    // sign: Y opens
+                if constexpr (TB) d1 = sub2(YP, MoP);    // sign: Y opens
             } else {
                 // up = lane q+1's d0 one step back; left = own diagonal d0
                 const unsigned Mu = row_shl<G::PR>(MoP), Yu = row_shl<G::PR>(YP);
                 Y = max2(Mu, Yu);
-                d1 = sub2(Yu, Mu);
+                if constexpr (TB) d1 = sub2(Yu, Mu);
                 X = max2(MoP, XP);
-                d2 = sub2(XP, MoP);
+                if constexpr (TB) d2 = sub2(XP, MoP);
             }
             unsigned M = add2(P ? Hp1 : Hp0, scr[U]);
             const unsigned mxy = max2(X, Y);
             unsigned H = max2(M, mxy);
-            const unsigned d3 = sub2(Y, X);     // sign: X > Y
-            const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
+            if constexpr (!TB) {
+                if constexpr (P == 0) ds0 = add2(ds0, scr[U]); else ds1 = add2(ds1, scr[U]);
+            }
             if constexpr (PRO) {
                 if (tau == tb[P]) {   // DP boundary cell (row 0 / column 0): M = 0, X = Y = -inf
                     M = bval[P];
                     H = M;
                     X = NEG2;
                     Y = NEG2;
+                    if constexpr (!TB) {
+                        if constexpr (P == 0) ds0 = 0u; else ds1 = 0u;
+                    }
                 }
             }
             if constexpr (P == 0) Hp0 = H; else Hp1 = H;
@@ -626,15 +798,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                 if constexpr (P == 0) {
                     cap0 = tau == te[0] ? M : cap0;
                     capB0 = tau == teB[0] ? M : capB0;
+                    if constexpr (!TB) {
+                        dc0 = tau == te[0] ? ds0 : dc0;
+                        dcB0 = tau == teB[0] ? ds0 : dcB0;
+                    }
                 } else {
                     cap1 = tau == te[1] ? M : cap1;
                     capB1 = tau == teB[1] ? M : capB1;
+                    if constexpr (!TB) {
+                        dc1 = tau == te[1] ? ds1 : dc1;
+                        dcB1 = tau == teB[1] ? ds1 : dcB1;
+                    }
                 }
             }
-            const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
-            const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
-            acc = and_or(tt, mT[U], acc);
-            acc = and_or(uu, mU[U], acc);
+            if constexpr (TB) {
+                const unsigned d3 = sub2(Y, X);     // sign: X > Y
+                const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
+                const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
+                const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
+                acc = and_or(tt, mT[U], acc);
+                acc = and_or(uu, mU[U], acc);
+            }
         };
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
@@ -655,15 +839,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         // a block pair (8 steps) is half a tile row; its words wait in LDS and the
         // second half stores the row (the phases may split a row: the stage carries it)
         auto flush = [&](int tau4) {
-            asm volatile("" ::: "memory");
-            const int w = ((tau4 - tau0) >> 2) & ~3;
-            if (act && w < NW) *(uint4*)(bits + w * kBL) = *(const uint4*)stage;
+            if constexpr (TB) {
+                asm volatile("" ::: "memory");
+                const int w = ((tau4 - tau0) >> 2) & ~3;
+                if (act && w < NW) *(uint4*)(bits + w * kBL) = *(const uint4*)stage;
+            }
         };
         auto pair8 = [&](int tau4, auto PROc, auto CAPc) {
-            const int h2 = ((tau4 - tau0) >> 2) & 2;
-            stage[h2] = block(tau4, PROc, CAPc, sc, sn);
-            stage[h2 + 1] = block(tau4 + 4, PROc, CAPc, sn, sc);
-            if (h2) flush(tau4);
+            if constexpr (TB) {
+                const int h2 = ((tau4 - tau0) >> 2) & 2;
+                stage[h2] = block(tau4, PROc, CAPc, sc, sn);
+                stage[h2 + 1] = block(tau4 + 4, PROc, CAPc, sn, sc);
+                if (h2) flush(tau4);
+            } else {
+                (void)block(tau4, PROc, CAPc, sc, sn);
+                (void)block(tau4 + 4, PROc, CAPc, sn, sc);
+            }
         };
         // phases in whole block pairs (8 steps) from tau0: prologue (boundary cells,
         // captures of short reads), bulk, capture window to tau_end (may run up to 7
@@ -683,6 +874,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         }
         if (((tau4 - tau0) >> 2) & 2) flush(tau4 - 8);   // a half row left: its other half is past tau_end
 
+        if constexpr (!TB) {
+            band_diag_epilogue<W>(a, acd, tab, pcd, La, dlo, q, grp, g < pair_hi, act, ra, rb, LbA, LbB,
+                                  (bad_mask >> grp) & 1u, (bad_mask >> (16 + grp)) & 1u, (pad_mask >> grp) & 1u,
+                                  (pad_mask >> (16 + grp)) & 1u, cap0, cap1, capB0, capB1, dc0, dc1, dcB0, dcB1,
+                                  bval[0], bval[1], lane);
+            continue;
+        }
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
             caps[2 * q] = (cap0 & 0xffffu) | (capB0 & 0xffff0000u);
@@ -1040,6 +1238,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
+    if (W == kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const int La = a.La, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
     // Reads handed on (next level's redo list, or the exact kernel's list) wait in a
@@ -1100,7 +1299,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     unsigned char* rbuf = wb + kBandRunsCap * 4;
     unsigned char* rows = rbuf + rcap + 256;
 
-    const long long count = *a.band_count;
+    const long long count = band_list_count(a);
     const long long klo = 2 * a.band_pair_lo;
     const long long khi = 2 * a.band_pair_hi < count ? 2 * a.band_pair_hi : count;
     // per read: the pair header (reads, lengths, offsets, geometry) and the 32
@@ -1311,7 +1510,9 @@ __device__ int block_excl_scan_i32(int v, int* total) {
 // scatter; the last block writes the count (*redo_count).
 __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, unsigned epoch) {
     __shared__ int sh[2];
-    const long long n = *a.band_count;
+    if (a.tail_prio) __builtin_amdgcn_s_setprio(3);
+    const long long nb = *a.band_count;
+    const long long n = band_list_count(a);
     const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
     int f[4], s = 0;
 #pragma unroll
@@ -1330,7 +1531,7 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
     int pos = sh[0] + local;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-        if (f[t]) a.redo_list[pos++] = a.band_order[k0 + t];
+        if (f[t]) a.redo_list[pos++] = (int32_t)band_list_read(a, k0 + t, nb);
     if (threadIdx.x == 0) {
         if (sh[1]) a.fallback_count[3] = 1;
         if (blockIdx.x == gridDim.x - 1) *a.redo_count = sh[0] + total;
@@ -1356,7 +1557,8 @@ bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb,
 hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
                           int* walk_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        fill_blocks, W == 16 ? (const void*)nw_band_fill<16> : (const void*)nw_band_fill<32>, 64 * fill_wpb, fill_lds);
+        fill_blocks, W == 16 ? (const void*)nw_band_fill<16, true> : (const void*)nw_band_fill<32, true>, 64 * fill_wpb,
+        fill_lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         walk_blocks, W == 16 ? (const void*)nw_band_walk<16> : (const void*)nw_band_walk<32>, 64 * walk_wpb, walk_lds);
@@ -1377,9 +1579,9 @@ int64_t band_lookback_words(int64_t n) { return std::max<int64_t>(1, (n + 1023) 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {
     if (W == 16)
-        hipLaunchKernelGGL(nw_band_fill<16>, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<16, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else
-        hipLaunchKernelGGL(nw_band_fill<32>, dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<32, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
@@ -1387,6 +1589,19 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
         hipLaunchKernelGGL(nw_band_walk<16>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     else
         hipLaunchKernelGGL(nw_band_walk<32>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+// the diagonal pass over list A (KernelArgs::order_a): one launch, as many blocks as the
+// traceback fill of the same level would use for its pairs
+hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s) {
+    const int ppw = W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pairs + ppw - 1) / ppw + fill.wpb - 1) / fill.wpb,
+                                                                  (int64_t)fill.grid));
+    if (W == 16)
+        hipLaunchKernelGGL((nw_band_fill<16, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL((nw_band_fill<32, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     return hipGetLastError();
 }
 

@@ -61,6 +61,13 @@ struct KernelArgs {
     int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
     int32_t* redo_count;
     uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
+    // the diagonal pass (nw_band_fill<W, false>, ops output): the sort puts the reads of the
+    // amplicon's length in order_a[0, *count_a); the pass hands the reads it does not finish
+    // to tile_list[0, *tile_count), which the traceback pass takes after band_order's
+    int32_t* order_a;              // null: no diagonal pass (every DP read in band_order)
+    int32_t* count_a;
+    int32_t* tile_list;
+    int32_t* tile_count;           // null outside the first level's traceback pass
     int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
     // > 0: when the first level hands on at most this many reads (*redo_count), the second
     // level's kernels return at once and the exact kernel takes them too (its fallback list,
@@ -83,6 +90,10 @@ struct KernelArgs {
     // needle -endweight (the exact kernels only): an end gap of k residues costs
     // end_open + (k - 1) * end_extend (scaled) instead of nothing
     int32_t end_weight, end_open, end_extend;
+    // the latency-bound kernels of a chunk's tail (second band level, exact kernels, the
+    // scans) raise their waves' issue priority (s_setprio): they share the SIMDs with the
+    // other chunk's bulk fill, and a chain waits for its tail (CRISPR_NW_PRIO=0: off)
+    int32_t tail_prio;
 };
 
 // Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and
@@ -143,6 +154,8 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
 int64_t band_lookback_words(int64_t n);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
+// the diagonal pass (nw_band_fill<W, false>) over list A; `pairs`: an upper bound of its pairs
+hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
 // pbyte0, 4-aligned) -> dst[pos - bias] bytes (A C T G), then exceptions [e0, e1)
 hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1, const int64_t* exc_pos,
@@ -179,8 +192,10 @@ struct OpsCounts {
     const int32_t* fallback;   // [0]: exact-kernel reads of the chunk, [3]: look-back error flag
     const int32_t* redo;       // second band level reads (null: one level)
     const int32_t* band;       // reads that needed the DP (null: not the band path)
+    const int32_t* band_a;     // + the diagonal pass's list A (null: none)
     int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
     int32_t one_level;         // the chunk ran the 32-diagonal level alone: its DP reads go to ctl[7]
+    int32_t prio;              // raise the compaction's issue priority (KernelArgs::tail_prio)
 };
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,

@@ -89,6 +89,7 @@ __device__ __forceinline__ unsigned pack_lanes(unsigned v) {
 // wait for all LDS traffic at every store, the ring prefetch included).
 template <int R, bool TBL>
 __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int64_t slab_bytes, int cap) {
+    if (a.tail_prio && a.work_list) __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // work-list entries (null list: every read); cap: [0, min(count, grid)), one per
     // block, the one-wave kernel takes the rest

@@ -57,6 +57,7 @@ struct Profile {
     const uint32_t* rowpos = nullptr;  // band walk: codes each row scores > 0 against
     const uint8_t* amp = nullptr;      // amplicon bytes (+16 pad)
     int R = 0;
+    bool amp_plain = false;            // every amplicon byte is an EDNAFULL letter (the diagonal pass's codes)
 };
 
 // Device buffers of one chunk's kernels.  The pipelined calls alternate two sets on
@@ -69,13 +70,15 @@ struct Scratch {
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
     DevBuf<int32_t> d_order, d_sort_key;
+    DevBuf<int32_t> d_order_a, d_tile;  // the diagonal pass: list A, the reads it hands on
     DevBuf<unsigned long long> d_lb;   // look-back words of the single-pass scans (sort, redo list, ops)
     DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
     DevBuf<int32_t> d_nops, d_opsctl;
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_redo.release();
-        d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release();
+        d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
+        d_tile.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
@@ -139,6 +142,7 @@ struct nw_ctx {
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0;
     unsigned epoch = 0;               // look-back launches so far (each launch uses a new value)
+    int tail_prio = 1;                // KernelArgs::tail_prio (CRISPR_NW_PRIO=0: off)
     bool ran = false;
     // ops output (nw_align_ops / nw_batch_set_output(NW_OUT_OPS)): per-read run slots,
     // spill area, compaction scratch; the pipelined call's copy streams and events
@@ -192,6 +196,7 @@ unsigned next_epoch(nw_ctx* c) {
 // the markup bits of the band walk (codes each row scores > 0 against).
 struct AmpTables {
     int R = 0;
+    bool amp_plain = true;
     std::vector<int8_t> prof;
     std::vector<uint32_t> rowpos;
 };
@@ -208,6 +213,7 @@ bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
         for (int code = 0; code < nw::NCODE; ++code)
             if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
         t->rowpos[(size_t)ai] = m;
+        t->amp_plain = t->amp_plain && ca < 16;
     }
     const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
@@ -318,6 +324,7 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         p.rowpos = (const uint32_t*)(b + o.rowpos);
         p.amp = b + o.amp;
         p.R = tabs[g].R;
+        p.amp_plain = tabs[g].amp_plain;
     }
     c->arena_refs = refs;
     c->arena_profs = *profs;
@@ -367,7 +374,7 @@ int configure_long(nw_ctx* c) {
     c->exact_grid = (int)grid;
     c->exact_full = true;
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
     return NW_OK;
 }
 
@@ -434,7 +441,7 @@ int configure(nw_ctx* c) {
         c->use_diag = false;
         c->diag16_fill.grid = 0;
         HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-        HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
+        HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
         return NW_OK;
     }
     const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" (default) | "full" (tests/diagnostics)
@@ -485,6 +492,8 @@ int configure(nw_ctx* c) {
                                                         c->diag16_stride : 0);
             HIP_OR_FAIL(c, c->s->d_bregion.reserve((size_t)rbytes));
             HIP_OR_FAIL(c, c->s->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_order_a.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            HIP_OR_FAIL(c, c->s->d_tile.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(c->n)));
@@ -493,7 +502,7 @@ int configure(nw_ctx* c) {
         }
     }
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(4));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
     return NW_OK;
 }
 
@@ -687,6 +696,10 @@ hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
 // uploaded arrays (outputs, records and fallback queue at the same index).
 // Everything is queued on c->stream; nothing synchronises.
 int launch_range(nw_ctx* c, int64_t base) {
+    {
+        const char* e = std::getenv("CRISPR_NW_PRIO");
+        c->tail_prio = !(e && std::atoi(e) == 0);
+    }
     nw::KernelArgs a{};
     a.reads = c->d_reads.p - c->reads_bias;
     a.offsets = c->d_offsets.p + base;
@@ -706,6 +719,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.sub16 = c->d_sub16.p;
     a.rowpos = c->cur.rowpos;
     a.end_weight = c->end_weight;
+    a.tail_prio = c->tail_prio;
     a.end_open = c->end_open;
     a.end_extend = c->end_extend;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
@@ -730,7 +744,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
-        if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs) == hipSuccess
+        if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs) == hipSuccess
                                   ? NW_OK : fail(c, NW_E_HIP, "hipMemsetAsync failed");
         a.lut6 = c->d_lut6.p;
         a.band_order = c->s->d_order.p;
@@ -744,6 +758,16 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.sort_key = c->s->d_sort_key.p;
         a.band_count = c->s->d_fallback_count.p + 1;   // the sort writes the DP count here
         a.lb_status = c->s->d_lb.p;
+        // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
+        // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
+        const char* dp_env = std::getenv("CRISPR_NW_DIAGPASS");
+        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !(dp_env && std::atoi(dp_env) == 0);
+        if (diag_pass) {
+            a.order_a = c->s->d_order_a.p;
+            a.count_a = c->s->d_fallback_count.p + 4;
+            a.tile_list = c->s->d_tile.p;
+            a.tile_count = c->s->d_fallback_count.p + 5;
+        }
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
@@ -778,6 +802,13 @@ int launch_range(nw_ctx* c, int64_t base) {
             const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
             const nw::LaunchCfg& wc = lvl == 0 ? c->diag16_walk : c->diag_walk;
             const bool first = lvl == (two ? 0 : 1);
+            if (!first) {   // the second level aligns the redo list only
+                al.order_a = nullptr;
+                al.tile_list = nullptr;
+                al.tile_count = nullptr;
+            } else if (al.order_a) {
+                HIP_OR_FAIL(c, nw::launch_band_diag(W, al, fc, pairs, c->cs));
+            }
             for (int64_t lo = 0; lo < pairs; lo += pp) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
@@ -793,7 +824,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
-    HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 4 * sizeof(int32_t), c->cs));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs));
     if (c->exact_full) {   // long amplicon: every read through the multi-wave kernel
         if (c->n > 0)
             HIP_OR_FAIL(c, nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, false,
@@ -843,8 +874,10 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (prev_done) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, prev_done, 0));
     nw::OpsCounts cnt{};
     cnt.fallback = c->s->d_fallback_count.p;
+    cnt.prio = c->tail_prio;
     if (c->use_diag && c->n > 0) {
         cnt.band = c->s->d_fallback_count.p + 1;
+        cnt.band_a = c->s->d_fallback_count.p + 4;   // list A (0 without the diagonal pass: zeroed by classify)
         // second-level reads of a two-level chunk; a chunk run on the 32-diagonal level alone
         // counts its DP reads apart (ctl[7]: the adaptive choice reads two-level chunks only)
         if (c->diag16_fill.grid > 0 && !c->skip16) cnt.redo = c->s->d_fallback_count.p + 2;
@@ -1873,9 +1906,9 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
         counts4[3] = nw_batch_fallbacks(c);
         return NW_OK;
     }
-    int32_t fb[4] = {0, 0, 0, 0}, need = 0;
+    int32_t fb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, need = 0;
     HIP_OR_FAIL(c, hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
-    need = fb[1];   // the sort's DP count
+    need = fb[1] + fb[4];   // the sort's DP count: list B + list A (the diagonal pass)
     const bool two = c->diag16_fill.grid > 0;
     counts4[0] = c->n - need;             // exact copies (no DP)
     counts4[1] = two ? need : 0;          // first level (16 diagonals)

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wpb = blockDim.x >> 6;
+    if (args.tail_prio && args.work_list) __builtin_amdgcn_s_setprio(3);
     const long long nwork = exact_work_count(args);
     // a work list (or batch) shorter than the grid: blocks past its end leave before any set-up
     if (args.work_lo + (long long)blockIdx.x * wpb >= nwork) return;

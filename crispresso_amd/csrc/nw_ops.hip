@@ -54,9 +54,10 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
                                                               unsigned long long* status, unsigned epoch, int parity,
                                                               int64_t* ctl, int64_t* ops_off, uint32_t* staging,
                                                               int64_t staging_cap, const int32_t* opsctl,
-                                                              OpsCounts cnt, int64_t* hctl) {
+                                                              OpsCounts cnt, int64_t* hctl, int prio) {
     __shared__ int sh_bad;
     __shared__ unsigned sh_excl;
+    if (prio) __builtin_amdgcn_s_setprio(3);
     const long long r0 = (long long)blockIdx.x * kOpsBlockReads + threadIdx.x * kOpsPerThread;
     int c4[kOpsPerThread];
     long long s = 0;
@@ -116,8 +117,9 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         if (direct) fb += *cnt.redo;
         ctl[4] += fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
-        if (cnt.band) ctl[6] += *cnt.band;
-        if (cnt.band && cnt.one_level) ctl[7] += *cnt.band;
+        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0);
+        ctl[6] += dp;
+        if (cnt.one_level) ctl[7] += dp;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];
     }
@@ -131,7 +133,7 @@ hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int sl
                               hipStream_t s, int64_t* hctl) {
     const int nblk = (int)std::max<int64_t>(1, (n + kOpsBlockReads - 1) / kOpsBlockReads);
     hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, spill, n, status, epoch,
-                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl);
+                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio);
     return hipGetLastError();
 }
 
