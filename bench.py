@@ -249,21 +249,25 @@ def kernel_pass(al, buf, offsets, steps, warmup):
 
 
 def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, cpu_sample, no_cpu):
-    """Downstream quantification (process_df_chunk, CORE:428-753) of this rank's
-    aligned reads, straight from the aligner's HBM rows (nwq_run_device).
+    """Downstream quantification (process_df_chunk, CORE:428-753) of this rank's aligned
+    reads, chained on the device: the aligner's resident OPS output (records + runs, the
+    default output; nw_batch_device_ops) goes straight into nwq_run_device_ops, which
+    rebuilds the rows it needs from the runs on the device and quantifies them.
     Settings: one guide cutting mid-amplicon, CRISPResso defaults otherwise
     (window_around_sgrna 1, exclude 15 bp each side)."""
     from crispresso_amd import quantify
+    from crispresso_amd.aligner import OpsBatch
     from crispresso_amd.devmem import DeviceBuffer
 
-    al.set_output("rows")
+    al.set_output("ops")
     al.upload(buf, offsets)
     al.run_async()
     al.sync()
-    d_aln, stride, d_stats = al.device_output()
-    batch = al.download(n_reads, AMPLICON_LEN + 64)
-    lens = batch.stats["aln_len"].astype(np.int64)
-    ident = batch.stats["n_ident"].astype(np.int64)
+    dev = al.device_ops()
+    stride = dev["max_cols"]
+    ob = al.download_ops(n_reads)
+    lens = ob.stats["aln_len"].astype(np.int64)
+    ident = ob.stats["n_ident"].astype(np.int64)
     um = ident == lens
     args = argparse.Namespace(amplicon_seq=amplicon, guide_seq=amplicon[105:125], cleavage_offset=-3,
                               window_around_sgrna=1, exclude_bp_from_left=15, exclude_bp_from_right=15,
@@ -275,11 +279,11 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
     d_pre = DeviceBuffer.from_array(pre, al.device)
     d_out = DeviceBuffer(16 * n_reads, al.device)
     for _ in range(warmup):
-        q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
+        q.run_device_ops(amplicon, dev, d_pre.ptr, n_reads, d_out.ptr)
     kms = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        q.run_device(d_aln, stride, d_stats, 8, d_pre.ptr, n_reads, d_out.ptr)
+        q.run_device_ops(amplicon, dev, d_pre.ptr, n_reads, d_out.ptr)
         kms.append(q.last_kernel_ms)
     elapsed = time.perf_counter() - t0
     algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
@@ -290,7 +294,9 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
         "value": n_reads * steps / elapsed,
         "unit": "reads/s",
         "ms_per_step": elapsed / steps * 1e3,
-        "kernel": "nwq::quant_kernel + nwq::quant_reduce",
+        "input": "the aligner's resident ops output (records + runs + reads in HBM; no rows-mode re-run)",
+        "kernel": "nwq::expand_rows (the rows of the non-UNMODIFIED reads, from their runs) + nwq::quant_kernel "
+                  "+ nwq::quant_reduce",
         "kernel_ms_avg": kavg,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -305,6 +311,9 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
         from oracle import quant_oracle as qo
 
         k = min(cpu_sample, n_reads)
+        sub = OpsBatch(ob.stats[:k], ob.ops[: int(ob.ops_off[k])], ob.ops_off[: k + 1], None, ob.scale,
+                       offsets=offsets[: k + 1])
+        batch = sub.expand(amplicon, buf, offsets[: k + 1])
         rows = [(batch.ref_seq(i), batch.align_str(i), batch.align_seq(i)) for i in range(k)]
         prm = qo.QuantParams(len_amplicon=g.LEN_AMPLICON, include_idxs=frozenset(g.INCLUDE_IDXS),
                              window_around_sgrna=1)

@@ -46,13 +46,13 @@ EXPORTS = (
     "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
-    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat", "nw_fastq_pack",
+    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat", "nw_fastq_pack", "nw_batch_device_ops",
 )
 
 # Every symbol include/crispr_quant.h declares.
 QUANT_EXPORTS = (
     "nwq_create", "nwq_destroy", "nwq_last_error", "nwq_set_params", "nwq_totals_words", "nwq_run",
-    "nwq_run_device",
+    "nwq_run_device", "nwq_run_device_ops",
 )
 
 
@@ -127,6 +127,7 @@ def load() -> ctypes.CDLL:
         "nw_required_stride_multi": (c_int64, [c_void_p, c_int32, c_int32]),
         "nw_batch_device_output": (c_int, [ctx_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)]),
         "nw_batch_set_output": (c_int, [ctx_p, c_int]),
+        "nw_batch_device_ops": (c_int, [ctx_p] + [POINTER(c_void_p)] * 5 + [POINTER(c_int64)] * 2),
         "nw_batch_phase_times": (c_int, [ctx_p, c_void_p]),
         "nw_batch_path_counts": (c_int, [ctx_p, c_void_p]),
         "nw_batch_download_ops": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -175,6 +176,8 @@ def load() -> ctypes.CDLL:
                             POINTER(c_float)]),
         "nwq_run_device": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                    c_void_p, POINTER(c_float)]),
+        "nwq_run_device_ops": (c_int, [ctx_p, c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, POINTER(c_float)]),
         "nw_synth_offsets": (c_int64, [c_char_p, c_int32, c_int64, c_int64, ctypes.c_uint64, c_void_p, c_void_p,
                                         c_int32]),
         "nw_synth_reads": (c_int, [c_char_p, c_int32, c_int64, c_int64, ctypes.c_uint64, c_void_p, c_void_p,

@@ -305,6 +305,17 @@ class GpuAligner:
                                                     ctypes.byref(d_stats)), "nw_batch_device_output")
         return int(d_aln.value), int(stride.value), int(d_stats.value)
 
+    def device_ops(self) -> dict:
+        """Device pointers of the last ops-mode run's resident output (nw_batch_device_ops):
+        runs, run offsets, records, reads (+ their offsets and bias) and max_cols."""
+        p = [ctypes.c_void_p() for _ in range(5)]
+        bias, cols = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.nw_batch_device_ops(self._h, *[ctypes.byref(x) for x in p], ctypes.byref(bias),
+                                                 ctypes.byref(cols)), "nw_batch_device_ops")
+        d = dict(zip(("ops", "ops_off", "stats", "reads", "offsets"), (int(x.value or 0) for x in p)))
+        d["reads_bias"], d["max_cols"] = int(bias.value), int(cols.value)
+        return d
+
     def download(self, n: int, max_len: int) -> AlignmentBatch:
         stride = int(self.lib.nw_required_stride(self._h, max(int(max_len), 1)))
         stats = np.zeros(n, dtype=_lib.STAT_DTYPE)

@@ -1040,6 +1040,27 @@ int nw_batch_device_output(nw_ctx* c, void** d_aln, int64_t* stride, void** d_st
     return NW_OK;
 }
 
+int nw_batch_device_ops(nw_ctx* c, void** d_ops, void** d_ops_off, void** d_stats, void** d_reads, void** d_offsets,
+                        int64_t* reads_bias, int64_t* max_cols) {
+    if (!c) return NW_E_INVALID;
+    if (!c->ran || c->n <= 0 || c->out_mode != NW_OUT_OPS)
+        return fail(c, NW_E_STATE, "no resident ops-mode batch (nw_batch_set_output(NW_OUT_OPS), run first)");
+    (void)hipSetDevice(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    int64_t ctl[nw::kOpsCtl];
+    HIP_OR_FAIL(c, hipMemcpy(ctl, c->d_ctl64.p, sizeof ctl, hipMemcpyDeviceToHost));
+    int rc = ops_error(c, ctl[3]);
+    if (rc) return rc;
+    if (d_ops) *d_ops = c->s->d_staging.p;   // one chunk: the call's runs from offset 0
+    if (d_ops_off) *d_ops_off = c->d_opsoff.p;
+    if (d_stats) *d_stats = c->d_stats.p;
+    if (d_reads) *d_reads = c->d_reads.p;
+    if (d_offsets) *d_offsets = c->d_offsets.p;
+    if (reads_bias) *reads_bias = c->reads_bias;
+    if (max_cols) *max_cols = c->stride;
+    return NW_OK;
+}
+
 int nw_batch_geometry(const nw_ctx* c, int32_t* rows_per_lane, int32_t* waves_per_block, int32_t* grid,
                       int32_t* lds_bytes, int32_t* tb_mode) {
     if (!c) return NW_E_INVALID;

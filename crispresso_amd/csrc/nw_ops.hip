@@ -104,6 +104,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         const long long chunk_total = (long long)sh_excl + total;
         ctl[1] = base;
         ctl[2] = chunk_total;
+        ops_off[n] = base + chunk_total;   // the end of the chunk's last read (the next chunk's first offset)
         ctl[0] = base + chunk_total;
         ctl[8 + (parity ^ 1)] = base + chunk_total;
         if (opsctl[1]) ctl[3] |= 2;   // a kernel found the spill area full

@@ -32,6 +32,7 @@
 #include "../../include/crispr_nw.h"
 #include "../../include/crispr_quant.h"
 #include "nw_common.h"
+#include "nw_edna.h"
 
 namespace nwq {
 
@@ -418,6 +419,70 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
 
 // Sum of the per-block slabs: blockIdx.y takes a contiguous slice of the slabs,
 // adds into the (zeroed) int64 totals.
+// Rows of one read rebuilt from its traceback runs (the aligner's device-resident ops
+// output), exactly as the aligner writes them in NW_OUT_ROWS mode and nw_expand_ops does
+// on the host (nw_expand.cpp): one wave per read, the three rows assembled in LDS (a
+// run's columns spread over the lanes), then copied out as dwords.  Only the reads the
+// quantification loads: not UNMODIFIED on input, unless the amplicon has N (nfix), and
+// not empty.
+__global__ __launch_bounds__(256) void expand_rows(const uint32_t* __restrict__ ops, const int64_t* ops_off,
+                                                   const int32_t* stats, const uint8_t* reads, const int64_t* offsets,
+                                                   int64_t bias, const uint8_t* amp, const uint32_t* rowpos,
+                                                   const uint8_t* lut, int La, const uint8_t* pre, int all, int64_t n,
+                                                   uint8_t* aln, int64_t stride) {
+    extern __shared__ uint8_t ex_sm[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint8_t* rows = ex_sm + (size_t)wave * 3 * stride;
+    for (int64_t r = (int64_t)blockIdx.x * wpb + wave; r < n; r += (int64_t)gridDim.x * wpb) {
+        const int L = __builtin_amdgcn_readfirstlane(stats[r * 8]);   // aln_len
+        const unsigned pf = (unsigned)__builtin_amdgcn_readfirstlane((int)pre[r]);
+        if (L <= 0 || L > stride || (!all && (pf & NWQ_PRE_UNMODIFIED))) continue;
+        const int64_t k0 = ops_off[r], k1 = ops_off[r + 1];
+        const uint8_t* rd = reads + (offsets[r] - bias);
+        int col = 0, ia = 0, jb = 0;
+        for (int64_t k = k0; k < k1; ++k) {
+            const unsigned op = (unsigned)__builtin_amdgcn_readfirstlane((int)ops[k]);
+            const int type = (int)(op >> 28), len = (int)(op & 0x0fffffffu);
+            if (col + len > L) break;   // (not reached: the runs cover aln_len columns)
+            for (int p = lane; p < len; p += 64) {
+                uint8_t c0, c1, c2;
+                if (type == 0) {
+                    const uint8_t ca = amp[ia + p], cb = rd[jb + p];
+                    uint8_t mk = '|';
+                    if (ca != cb || ca == '-') {
+                        const uint8_t ua = (ca >= 'a' && ca <= 'z') ? ca - 32 : ca;
+                        const uint8_t ub = (cb >= 'a' && cb <= 'z') ? cb - 32 : cb;
+                        if (ca == '-' || cb == '-') mk = ' ';
+                        else if (ua == ub) mk = '|';
+                        else mk = ((rowpos[ia + p] >> lut[cb]) & 1u) ? ':' : '.';
+                    }
+                    c0 = ca; c1 = mk; c2 = cb;
+                } else if (type == 1) {
+                    c0 = '-'; c1 = ' '; c2 = rd[jb + p];
+                } else {
+                    c0 = amp[ia + p]; c1 = ' '; c2 = '-';
+                }
+                rows[col + p] = c0;
+                rows[stride + col + p] = c1;
+                rows[2 * stride + col + p] = c2;
+            }
+            col += len;
+            if (type != 1) ia += len;
+            if (type != 2) jb += len;
+        }
+        nw::lds_fence();
+        uint32_t* dst = (uint32_t*)(aln + r * 3 * stride);
+        const uint32_t* src = (const uint32_t*)rows;
+        const int words = (L + 3) >> 2, sw = (int)(stride >> 2);
+        for (int w = lane; w < words; w += 64) {
+            dst[w] = src[w];
+            dst[sw + w] = src[sw + w];
+            dst[2 * sw + w] = src[2 * sw + w];
+        }
+        nw::lds_fence();
+    }
+}
+
 __global__ void quant_reduce(const uint32_t* __restrict__ partial, int nblocks, int nwords, int slice,
                              unsigned long long* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -476,6 +541,10 @@ struct nwq_ctx {
     QBuf<uint8_t> d_aln, d_pre;
     QBuf<int32_t> d_len;
     QBuf<nwq_read> d_out;
+    // nwq_run_device_ops: the amplicon, its positive-code masks, ascii -> EDNAFULL code
+    QBuf<uint8_t> d_amp, d_lut;
+    QBuf<uint32_t> d_rowpos;
+    std::string amp_key;
 };
 
 namespace {
@@ -532,7 +601,8 @@ int geometry(nwq_ctx* c, int64_t stride, int64_t n, QGeom* g) {
 }
 
 int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, int64_t len_stride,
-             const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms) {
+             const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms,
+             bool started = false) {
     if (!c->have_params) return qfail(c, NW_E_STATE, "nwq_set_params not called");
     if (stride <= 0 || (stride & 3) || stride >= 32768)
         return qfail(c, NW_E_INVALID, "stride %lld must be a positive multiple of 4 below 32768", (long long)stride);
@@ -560,7 +630,7 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
     a.wave_words = g.wave_words;
     a.base_words = g.base_words;
     a.flags = c->flags;
-    QHIP(c, hipEventRecord(c->ev0, c->stream));
+    if (!started) QHIP(c, hipEventRecord(c->ev0, c->stream));   // (the row expansion records it first)
     hipLaunchKernelGGL(nwq::quant_kernel, dim3(g.grid), dim3(64 * g.wpb), g.lds, c->stream, a);
     QHIP(c, hipGetLastError());
     const int slices = std::min(g.grid, 32), slice = (g.grid + slices - 1) / slices;
@@ -608,6 +678,9 @@ void nwq_destroy(nwq_ctx* c) {
     c->d_pre.release();
     c->d_len.release();
     c->d_out.release();
+    c->d_amp.release();
+    c->d_lut.release();
+    c->d_rowpos.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -687,6 +760,59 @@ int nwq_run_device(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_
     if (len_stride <= 0) return qfail(c, NW_E_INVALID, "len_stride must be positive");
     QHIP(c, hipSetDevice(c->device));
     return run_impl(c, d_aln, stride, d_aln_len, len_stride, d_pre, n, d_out, totals, kernel_ms);
+}
+
+int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, const uint32_t* d_ops,
+                       const int64_t* d_ops_off, const void* d_stats, const uint8_t* d_reads, const int64_t* d_offsets,
+                       int64_t reads_bias, int64_t stride, const uint8_t* d_pre, int64_t n, nwq_read* d_out,
+                       int64_t* totals, float* kernel_ms) {
+    if (!c) return NW_E_INVALID;
+    if (!c->have_params) return qfail(c, NW_E_STATE, "nwq_set_params not called");
+    if (!amplicon || amplicon_len != c->LEN)
+        return qfail(c, NW_E_INVALID, "amplicon of %d bases for len_amplicon %d", amplicon_len, c->LEN);
+    if (n > 0 && (!d_ops || !d_ops_off || !d_stats || !d_reads || !d_offsets || !d_pre || !d_out))
+        return qfail(c, NW_E_INVALID, "null buffer");
+    if (!totals) return qfail(c, NW_E_INVALID, "null totals");
+    if (stride <= 0 || (stride & 3) || stride >= 32768)
+        return qfail(c, NW_E_INVALID, "stride %lld must be a positive multiple of 4 below 32768", (long long)stride);
+    QHIP(c, hipSetDevice(c->device));
+    const std::string key(amplicon, amplicon + amplicon_len);
+    if (key != c->amp_key) {   // the amplicon's tables (the markup's ':' test), once per amplicon
+        std::vector<uint32_t> rowpos((size_t)amplicon_len);
+        std::vector<uint8_t> lut(256);
+        for (int b = 0; b < 256; ++b) lut[(size_t)b] = nw::code_of((unsigned char)b);
+        for (int i = 0; i < amplicon_len; ++i) {
+            const int ca = nw::code_of((unsigned char)amplicon[i]);
+            uint32_t m = 0;
+            for (int code = 0; code < 16; ++code)
+                if (ca < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
+            rowpos[(size_t)i] = m;
+        }
+        QHIP(c, c->d_amp.reserve((size_t)amplicon_len + 16));
+        QHIP(c, c->d_rowpos.reserve((size_t)amplicon_len));
+        QHIP(c, c->d_lut.reserve(256));
+        QHIP(c, hipMemcpy(c->d_amp.p, amplicon, (size_t)amplicon_len, hipMemcpyHostToDevice));
+        QHIP(c, hipMemcpy(c->d_rowpos.p, rowpos.data(), 4 * rowpos.size(), hipMemcpyHostToDevice));
+        QHIP(c, hipMemcpy(c->d_lut.p, lut.data(), 256, hipMemcpyHostToDevice));
+        c->amp_key = key;
+    }
+    const size_t nn = (size_t)std::max<int64_t>(n, 1);
+    QHIP(c, c->d_aln.reserve(nn * 3 * (size_t)stride));
+    QHIP(c, hipEventRecord(c->ev0, c->stream));   // kernel_ms covers the expansion too
+    if (n > 0) {
+        int wpb = 4;
+        while (wpb > 1 && (int64_t)wpb * 3 * stride > 64 * 1024) wpb >>= 1;
+        const int lds = (int)(wpb * 3 * stride);
+        if (lds > kMaxLds) return qfail(c, NW_E_UNSUPPORTED, "stride %lld too long for the row expansion", (long long)stride);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + wpb - 1) / wpb, (int64_t)c->num_cus * 16));
+        hipLaunchKernelGGL(nwq::expand_rows, dim3(grid), dim3(64 * wpb), lds, c->stream, d_ops, d_ops_off,
+                           (const int32_t*)d_stats, d_reads, d_offsets, reads_bias, c->d_amp.p, c->d_rowpos.p,
+                           c->d_lut.p, amplicon_len, d_pre, (int)((c->flags & nwq::F_NFIX) != 0), n, c->d_aln.p,
+                           stride);
+        QHIP(c, hipGetLastError());
+    }
+    // the records' aln_len, 8 ints apart (nw_stat)
+    return run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms, true);
 }
 
 }  // extern "C"

@@ -220,6 +220,21 @@ class GpuQuantifier:
         self.last_kernel_ms = ms.value
         return totals
 
+    def run_device_ops(self, amplicon: str, dev: dict, d_pre: int, n: int, d_out: int):
+        """On the aligner's device-resident ops output (GpuAligner.device_ops(): runs, run
+        offsets, records, reads): the rows are rebuilt on the device from the runs
+        (nwq_run_device_ops), no rows layout, no host round trip -> totals int64 (host),
+        laid out for ``dev["max_cols"]`` (unpack_totals(totals, dev["max_cols"]))."""
+        stride = int(dev["max_cols"])
+        totals = np.zeros(int(self._lib.nwq_totals_words(self._ctx, stride)), dtype=np.int64)
+        ms = ctypes.c_float()
+        amp = amplicon.encode("ascii")
+        self._check(self._lib.nwq_run_device_ops(self._ctx, amp, len(amp), dev["ops"], dev["ops_off"], dev["stats"],
+                                                 dev["reads"], dev["offsets"], dev["reads_bias"], stride, d_pre, n,
+                                                 d_out, totals.ctypes.data, ctypes.byref(ms)), "nwq_run_device_ops")
+        self.last_kernel_ms = ms.value
+        return totals
+
     def unpack_totals(self, totals: np.ndarray, stride: int) -> Dict:
         L = self._len
         nv = _lib.NWQ_NVEC * L

@@ -152,6 +152,14 @@ int nw_batch_kernel_times(nw_ctx* ctx, float* fill_ms, float* walk_ms, float* re
  * nwq_run_device with aln_len = &stats->aln_len, len_stride = 8) consume the
  * alignments without a round trip through host memory. */
 int nw_batch_device_output(nw_ctx* ctx, void** d_aln, int64_t* stride, void** d_stats);
+/* The same for an NW_OUT_OPS run (synchronises): the runs of every read (uint32), their
+ * offsets (int64 [n + 1]: read r's runs are [d_ops_off[r], d_ops_off[r + 1])), the records
+ * (nw_stat [n]), and the reads as the kernels aligned them (read r at d_reads +
+ * d_offsets[r] - reads_bias, upper case), plus max_cols >= every alignment length (a
+ * multiple of 16).  Valid until the next upload / align call.  The quantification's
+ * nwq_run_device_ops consumes exactly these. */
+int nw_batch_device_ops(nw_ctx* ctx, void** d_ops, void** d_ops_off, void** d_stats, void** d_reads, void** d_offsets,
+                        int64_t* reads_bias, int64_t* max_cols);
 
 /* Pooled batch (replaces one CRISPResso + needle process per amplicon,
  * CRISPRessoPooled.py:882-908): n_refs amplicons packed in `refs` with

@@ -83,6 +83,19 @@ int nwq_run(nwq_ctx* c, uint8_t* aln, int64_t stride, const int32_t* aln_len, co
 int nwq_run_device(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_aln_len, int64_t len_stride,
                    const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms);
 
+/* The same on the aligner's device-resident OPS output (nw_batch_device_ops of an
+ * NW_OUT_OPS run: runs, run offsets [n + 1], nw_stat records, the reads as aligned):
+ * the rows of every read the quantification loads are rebuilt on the device from its
+ * runs, the amplicon and its bytes (the bytes nw_expand_ops writes), then quantified --
+ * align -> quantify without the rows layout or a host round trip.  amplicon /
+ * amplicon_len: the amplicon aligned (len_amplicon of the params); stride: a multiple of
+ * 4 >= every alignment length (nw_batch_device_ops' max_cols).  Synchronous; d_out a
+ * device array, totals a HOST array. */
+int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, const uint32_t* d_ops,
+                       const int64_t* d_ops_off, const void* d_stats, const uint8_t* d_reads, const int64_t* d_offsets,
+                       int64_t reads_bias, int64_t stride, const uint8_t* d_pre, int64_t n, nwq_read* d_out,
+                       int64_t* totals, float* kernel_ms);
+
 #ifdef __cplusplus
 }
 #endif

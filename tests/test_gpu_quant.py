@@ -300,3 +300,52 @@ def test_device_resident_after_aligner(gpu_aligner_factory, gq):
     assert np.array_equal(reads_dev[:, 3], ref["n_deleted"])
     for k in qo.VECTORS:
         assert np.array_equal(tot_dev["vectors"][k], ref["vectors"][k]), k
+
+
+@pytest.mark.parametrize("spec,with_n", [({"guide": True, "window": 10}, False), ({"guide": True, "window": 1}, True),
+                                          ({"guide": True, "coding": True, "window": 5}, False)])
+def test_device_resident_ops_after_aligner(gpu_aligner_factory, gq, spec, with_n):
+    """The aligner's default OPS output consumed in HBM (nw_batch_device_ops ->
+    nwq_run_device_ops: rows rebuilt on the device from the runs) gives what the oracle
+    gives on the rows the host expands from the same runs -- every class, count, vector
+    entry, histogram and counter.  An amplicon with N exercises the N rule (every read's
+    rows expanded)."""
+    amp = synth.random_amplicon(250, 11)
+    if with_n:
+        amp = amp[:60] + "N" + amp[61:180] + "N" + amp[181:]
+    buf, off = synth.reads_from(amp.replace("N", "A"), 12000, 12, synth.PARITY_MIX)
+    al = gpu_aligner_factory()
+    al.set_reference(amp)
+    al.set_output("ops")
+    al.upload(buf, off)
+    al.run_async()
+    al.sync()
+    dev = al.device_ops()
+    n = len(off) - 1
+    ob = al.download_ops(n)
+    rows = ob.expand(amp, buf, off)
+    lens = rows.stats["aln_len"]
+    score = np.array([float("%.1f" % (100.0 * a / b)) if b else 0.0 for a, b in zip(rows.stats["n_ident"], lens)])
+    um = score == 100
+    prm = make_params(amp, spec)
+    gq.set_params(globals_for(prm), args_for(prm, prm.exon_positions is not None), amplicon_has_n=with_n)
+    stride = dev["max_cols"]
+    with DeviceBuffer.from_array(quantify.pre_flags(um)) as d_pre, DeviceBuffer(16 * n) as d_out:
+        tot_dev = gq.unpack_totals(gq.run_device_ops(amp, dev, d_pre.ptr, n, d_out.ptr), stride)
+        reads_dev = d_out.download(np.zeros((n, 4), np.int32))
+    keep = lens > 0
+    R = [rows.aln[i, 0, :lens[i]].tobytes().decode() for i in range(n)]
+    M = [rows.aln[i, 1, :lens[i]].tobytes().decode() for i in range(n)]
+    S = [rows.aln[i, 2, :lens[i]].tobytes().decode() for i in range(n)]
+    if with_n:   # the reference's ignore_n_in_alignment rewrite of align_str (CORE:2031-2046)
+        M = ["".join("|" if r == "N" else m for r, m in zip(Rr, Mm)) for Rr, Mm in zip(R, M)]
+    idx = np.flatnonzero(keep)
+    ref = qo.process_rows([R[i] for i in idx], [M[i] for i in idx], [S[i] for i in idx], um[idx], None, None, prm)
+    assert np.array_equal(reads_dev[idx, 0].astype(np.int8), ref["cls"])
+    for c, k in ((1, "n_mutated"), (2, "n_inserted"), (3, "n_deleted")):
+        assert np.array_equal(reads_dev[idx, c], ref[k]), k
+    for k in qo.VECTORS:
+        assert np.array_equal(tot_dev["vectors"][k], ref["vectors"][k]), k
+    assert tot_dev["counters"] == ref["counters"]
+    assert tot_dev["hist_inframe"] == ref["hist_inframe"]
+    assert tot_dev["hist_frameshift"] == ref["hist_frameshift"]
