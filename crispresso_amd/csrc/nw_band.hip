@@ -26,8 +26,9 @@
 // than N go to the exact int32 kernel's fallback list.
 //
 // Layout / schedule:
-//   * reads are sorted by length on the device (counting sort, nw_band_hist /
-//     _scan / _scatter); sorted positions (2g, 2g+1) form pair g, packed in int16x2
+//   * reads are sorted by length on the device (nw_band_segsort: 4096-read segments
+//     sorted in LDS, placed by look-back); DP-list positions (2g, 2g+1) form pair g,
+//     packed in int16x2
 //     (read A low, B high) on one band that holds both reads' start and end
 //     diagonals; the sort keeps the wavefront's pairs at similar lengths;
 //   * one read pair per 16-lane DPP row, 4 pairs per wavefront; lane q owns
@@ -46,7 +47,10 @@
 //     [words / 4][lanes][4 words]: the fill writes 16 steps of a pair's lanes as one
 //     contiguous dwordx4 row, an M run of the walk reads 16 steps of its diagonal
 //     pair with one dwordx4 per lane;
-//   * nw_band_walk: one wavefront per read: start cell from the 32 captures,
+//   * ops output: a diagonal pass (nw_band_fill<W, false>) first aligns the reads of
+//     the amplicon's length without traceback bits and finishes the single-diagonal
+//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, true>);
+//   * nw_band_walk: one wavefront per read: start cell from the W captures,
 //     certificate, the run-based walk of nw_common.h over the band, strings.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -1574,7 +1578,13 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) 
                        epoch);
     return hipGetLastError();
 }
-int64_t band_lookback_words(int64_t n) { return std::max<int64_t>(1, (n + 1023) / 1024) + 1; }
+// words of the single-pass scans over n reads: the largest of the segment sort's two lists
+// (list A after list B's ceil(n / kSegReads) + 1 words), the redo and ops compactions
+// (1024-read blocks)
+int64_t band_lookback_words(int64_t n) {
+    const int64_t seg = std::max<int64_t>(1, (n + kSegReads - 1) / kSegReads);
+    return std::max<int64_t>(std::max<int64_t>(1, (n + 1023) / 1024) + 1, 2 * seg + 2);
+}
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {
@@ -1598,10 +1608,13 @@ hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, i
     const int ppw = W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pairs + ppw - 1) / ppw + fill.wpb - 1) / fill.wpb,
                                                                   (int64_t)fill.grid));
+    KernelArgs d = a;   // every pair of list A in one launch (no traceback region to bound the pass)
+    d.band_pair_lo = 0;
+    d.band_pair_hi = pairs;
     if (W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<16, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
     else
-        hipLaunchKernelGGL((nw_band_fill<32, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<32, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
     return hipGetLastError();
 }
 

@@ -55,7 +55,7 @@ for i in range(2 * rounds + 4):
     dt = time.perf_counter() - t0
     if i >= 4:
         times[which].append(dt * 1e3)
-    out = (stats.array.tobytes(), ops_off.array.tobytes())
+    out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes())
     if ref is None:
         ref = out
     elif out != ref:
