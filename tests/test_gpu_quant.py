@@ -339,6 +339,8 @@ def test_device_resident_ops_after_aligner(gpu_aligner_factory, gq, spec, with_n
     S = [rows.aln[i, 2, :lens[i]].tobytes().decode() for i in range(n)]
     if with_n:   # the reference's ignore_n_in_alignment rewrite of align_str (CORE:2031-2046)
         M = ["".join("|" if r == "N" else m for r, m in zip(Rr, Mm)) for Rr, Mm in zip(R, M)]
+        # ... and a row whose markup is then one character is UNMODIFIED (CORE:2047-2048)
+        um = um | np.array([len(set(m)) == 1 for m in M])
     idx = np.flatnonzero(keep)
     ref = qo.process_rows([R[i] for i in idx], [M[i] for i in idx], [S[i] for i in idx], um[idx], None, None, prm)
     assert np.array_equal(reads_dev[idx, 0].astype(np.int8), ref["cls"])
