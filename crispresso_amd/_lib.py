@@ -213,9 +213,32 @@ def ptr(a: np.ndarray) -> int:
     return a.ctypes.data if a is not None else 0
 
 
+class _PinnedOwner:
+    """Owns one page-locked block (nw_host_alloc); numpy arrays made from it
+    (``np.asarray``) keep it alive through their ``base``, and the block is freed when
+    the last of them and its :class:`PinnedBuffer` are gone (or at an explicit close)."""
+
+    def __init__(self, lib, p: int, nbytes: int):
+        self._lib, self._p = lib, p
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "version": 3, "data": (p, False)}
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self._lib.nw_host_free(self._p)
+            self._p = None
+
+    def __del__(self):  # pragma: no cover - runs at garbage collection
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class PinnedBuffer:
-    """Page-locked host memory (nw_host_alloc) viewed as a numpy array; freed with
-    the object.  Batches in pinned memory let nw_align_ops copy at PCIe rate."""
+    """Page-locked host memory (nw_host_alloc) viewed as a numpy array.  Batches in
+    pinned memory let nw_align_ops copy at PCIe rate.  The memory lives while this
+    object or any array viewing it does (``PinnedBuffer(n, dt).array`` alone is safe);
+    ``close()`` frees it at once (the caller's promise that no view is used after)."""
 
     def __init__(self, shape, dtype):
         self.lib = load()
@@ -226,20 +249,14 @@ class PinnedBuffer:
         if self.lib.nw_host_alloc(nbytes, ctypes.byref(p)) != NW_OK:
             raise NativeLibraryError(f"nw_host_alloc({nbytes}) failed")
         self._p = p.value
-        raw = (ctypes.c_uint8 * nbytes).from_address(self._p)
-        self.array = np.frombuffer(raw, dtype=np.uint8)[: count * dtype.itemsize].view(dtype).reshape(shape)
+        self._owner = _PinnedOwner(self.lib, self._p, nbytes)
+        self.array = np.asarray(self._owner)[: count * dtype.itemsize].view(dtype).reshape(shape)
 
     def close(self):
         if getattr(self, "_p", None):
             self.array = None
-            self.lib.nw_host_free(self._p)
+            self._owner.free()
             self._p = None
-
-    def __del__(self):  # pragma: no cover - interpreter shutdown ordering
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def pinned_copy(a: np.ndarray) -> PinnedBuffer:

@@ -6,6 +6,9 @@
 // copied once, one kernel aligns the whole batch, results come back as the
 // three alignment strings plus per-read statistics.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -93,6 +96,11 @@ struct nw_ctx {
     Scratch* s = &sc[0];                               // the set launch_range / configure use
     hipStream_t cs = nullptr;                          // the stream launch_range queues on
     hipStream_t cstream[kScratchSets] = {};            // compute stream of each set ([0] = stream)
+    // tail split (ops_call, CRISPR_NW_TAIL): launch_range queues a chunk's first band level on
+    // c->cs, then records split_ev there and moves to split_to for the rest (second level,
+    // exact kernel, compaction)
+    hipStream_t split_to = nullptr;
+    hipEvent_t split_ev = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_fill = nullptr, ev_walk = nullptr;   // after the fill / walk kernels
     hipEvent_t ev_sort = nullptr, ev_l2 = nullptr;     // band path: after the sort, after the second level
@@ -152,7 +160,7 @@ struct nw_ctx {
     int64_t spill_cap = 0, staging_cap = 0;
     int ops_slot = nw::kOpsSlot;       // runs per read slot (CRISPR_NW_OPS_SLOT: tests force spills)
     hipStream_t s_in = nullptr, s_out = nullptr;
-    std::vector<hipEvent_t> ev_in, ev_cs, ev_ce, ev_out;
+    std::vector<hipEvent_t> ev_in, ev_cs, ev_ce, ev_out, ev_bulk;
     hipEvent_t ev_h0 = nullptr;
     hipEvent_t ev_start = nullptr;     // the second compute stream starts after the first's set-up
     int64_t* h_ctl = nullptr;          // pinned: per chunk ctl[0..3] copied back
@@ -506,23 +514,60 @@ int configure(nw_ctx* c) {
     return NW_OK;
 }
 
+// CRISPR_NW_SEGV_TRACE=1 (diagnostics): a host segmentation fault prints the faulting
+// address and the native backtrace (library offsets: addr2line on the same build) before
+// the process dies as it would have.
+void segv_trace(int sig, siginfo_t* si, void*) {
+    char msg[96];
+    const int len = std::snprintf(msg, sizeof msg, "nw: signal %d at address %p\n", sig, si ? si->si_addr : nullptr);
+    if (len > 0) (void)!write(2, msg, (size_t)len);
+    void* frames[64];
+    backtrace_symbols_fd(frames, backtrace(frames, 64), 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+void maybe_install_segv_trace() {
+    static bool done = false;
+    const char* e = std::getenv("CRISPR_NW_SEGV_TRACE");
+    if (done || !e || std::atoi(e) != 1) return;
+    done = true;
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+}
+
 }  // namespace
 
 extern "C" {
 
 int nw_create(int device, nw_ctx** out) {
     if (!out) return NW_E_INVALID;
+    maybe_install_segv_trace();
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NW_E_HIP;
     if (device < 0 || device >= count) return NW_E_INVALID;
     nw_ctx* c = new nw_ctx();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->cstream[1], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->cstream[2], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&c->ev_h0) != hipSuccess ||
+    // Creation order decides which streams share a hardware queue (a process gets
+    // GPU_MAX_HW_QUEUES = 4; the fifth stream shares the first one's queue, and a queue runs
+    // its packets in order, so a cross-stream wait queued there holds back the other
+    // stream too).  Default: s_in first and the third compute stream (the pipelined call's
+    // tail stream) last, so those two share: the uploads of a call are all queued before its
+    // first tail packet.  CRISPR_NW_QORDER=0: the round-2 order (s_out shared the first
+    // compute stream's queue: 2.475 vs 2.423 ms per 1M-read call).
+    const char* qo = std::getenv("CRISPR_NW_QORDER");
+    const bool qorder = !(qo && std::atoi(qo) == 0);
+    hipStream_t* order_old[5] = {&c->stream, &c->s_in, &c->cstream[1], &c->cstream[2], &c->s_out};
+    hipStream_t* order_new[5] = {&c->s_in, &c->stream, &c->cstream[1], &c->s_out, &c->cstream[2]};
+    bool streams_ok = hipSetDevice(device) == hipSuccess;
+    for (hipStream_t* sp : qorder ? order_new : order_old)
+        streams_ok = streams_ok && hipStreamCreateWithFlags(sp, hipStreamNonBlocking) == hipSuccess;
+    if (!streams_ok || hipEventCreate(&c->ev_h0) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess ||
@@ -816,6 +861,11 @@ int launch_range(nw_ctx* c, int64_t base) {
                 HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
                 if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
+            if (first && c->split_to) {   // the latency-bound rest of the chunk on the tail stream
+                HIP_OR_FAIL(c, hipEventRecord(c->split_ev, c->cs));
+                HIP_OR_FAIL(c, hipStreamWaitEvent(c->split_to, c->split_ev, 0));
+                c->cs = c->split_to;
+            }
         }
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
@@ -913,6 +963,7 @@ int ops_events(nw_ctx* c, size_t chunks) {
     HIP_OR_FAIL(c, grow(c->ev_cs, hipEventDefault));
     HIP_OR_FAIL(c, grow(c->ev_ce, hipEventDefault));
     HIP_OR_FAIL(c, grow(c->ev_out, hipEventDisableTiming));
+    HIP_OR_FAIL(c, grow(c->ev_bulk, hipEventDisableTiming));
     if ((int64_t)chunks > c->h_ctl_chunks) {
         if (c->h_ctl) (void)hipHostFree(c->h_ctl);
         c->h_ctl = nullptr;
@@ -1343,37 +1394,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return fail(c, NW_E_STATE, "no resident batch of these %lld reads (nw_align_ops uploads one)", (long long)n);
     if (upload) c->resident_ok = false;
     (void)hipSetDevice(c->device);
-    // longest / shortest read: a vectorisable pass, split over the host pool for large
-    // batches (memory-bound; the exact read is found only on error)
-    int64_t mx = 1, mn = 0;
-    {
-        nw_host::Pool& pool = nw_host::Pool::get();
-        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 17));
-        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
-        pool.run(parts, [&](int q) {
-            int64_t lo, hi, a = 1, b = 0;
-            nw_host::Pool::range(n, parts, q, &lo, &hi);
-            for (int64_t r = lo; r < hi; ++r) {
-                const int64_t len = offsets[r + 1] - offsets[r];
-                a = len > a ? len : a;
-                b = len < b ? len : b;
-            }
-            pmx[(size_t)q] = a;
-            pmn[(size_t)q] = b;
-        });
-        for (int q = 0; q < parts; ++q) {
-            mx = std::max(mx, pmx[(size_t)q]);
-            mn = std::min(mn, pmn[(size_t)q]);
-        }
-    }
-    if (mn < 0 || mx > (1 << 20))
-        for (int64_t r = 0; r < n; ++r) {
-            const int64_t len = offsets[r + 1] - offsets[r];
-            if (len < 0 || len > (1 << 20))
-                return fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len);
-        }
-    const int32_t lb_max = (int32_t)mx;
-    ht.lap(0);
     int64_t chunk = 262144;
     if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
     chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
@@ -1445,6 +1465,104 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
     }
     const int mode_before = c->out_mode;
+    const int64_t base0 = n ? offsets[0] : 0;
+    const int64_t nbytes = n ? offsets[n] - base0 : 0;
+    const int64_t nchunks = (int64_t)chunks.size();
+    auto restore = [&](int code) {
+        c->split_to = nullptr;
+        c->skip16 = false;
+        c->out_mode = mode_before;
+        c->n = 0;
+        c->s = &c->sc[0];
+        c->cs = c->stream;
+        return code;
+    };
+    int rc = NW_OK;
+    // the chunks' edges must be in order before anything is copied (the scan below checks
+    // every read, after the uploads are queued: the copy engine starts streaming at once)
+    for (const Chunk& ch : chunks)
+        if (offsets[ch.lo] > offsets[ch.hi] || offsets[ch.lo] < base0 || offsets[ch.hi] > offsets[n])
+            return fail(c, NW_E_INVALID, "offsets out of order at read %lld", (long long)ch.lo);
+    // packed input: the device copy of the packed stream starts at byte P0 (4-aligned: one
+    // dword = 16 bases), the unpacked bytes at batch position base0 & ~15 (16-B stores)
+    const int64_t P0 = (base0 / 16) * 4;
+    const int64_t pk_hi = n ? (offsets[n] + 3) / 4 : 0;   // end of the caller's packed bytes
+    if (pk && upload &&
+        (c->d_packed.reserve((size_t)std::max<int64_t>(pk_hi - P0, 0) + 64) != hipSuccess ||
+         c->d_exc_pos.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess ||
+         c->d_exc_byte.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess))
+        return restore(fail(c, NW_E_NOMEM, "device allocation failed for the packed batch"));
+    if (c->d_reads.reserve((size_t)nbytes + 512 + 16) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
+        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+        return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
+    if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
+    ht.lap(2);
+    if (upload) c->reads_bias = pk ? (base0 & ~(int64_t)15) : base0;
+    // every upload queued up front: the copy engine streams the batch while chunks compute
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
+    int64_t h2d_bytes = 0;
+    if (pk && upload && pk->n_exc > 0) {
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_pos.p, pk->exc_pos, sizeof(int64_t) * (size_t)pk->n_exc,
+                                      hipMemcpyHostToDevice, c->s_in));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_byte.p, pk->exc_byte, (size_t)pk->n_exc, hipMemcpyHostToDevice, c->s_in));
+        h2d_bytes += 9 * pk->n_exc;
+    }
+    for (int64_t k = 0; upload && k < nchunks; ++k) {
+        const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
+        const int64_t b0 = offsets[lo], b1 = offsets[hi];
+        if (pk) {
+            // the chunk's packed dwords (the caller's bytes only; edge bases are masked)
+            const int64_t q0 = std::max((b0 / 16) * 4, base0 / 4), q1 = std::min((b1 + 15) / 16 * 4, pk_hi);
+            if (b1 > b0 && q1 > q0) {
+                HIP_OR_FAIL(c, hipMemcpyAsync(c->d_packed.p + (q0 - P0), pk->packed + q0, (size_t)(q1 - q0),
+                                              hipMemcpyHostToDevice, c->s_in));
+                h2d_bytes += q1 - q0;
+            }
+        } else if (b1 > b0) {
+            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p + (b0 - base0), reads + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice,
+                                          c->s_in));
+            h2d_bytes += b1 - b0;
+        }
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
+                                      hipMemcpyHostToDevice, c->s_in));
+        h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
+        HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
+    }
+    ht.lap(3);
+    // longest / shortest read: a vectorisable pass, split over the host pool for large
+    // batches (memory-bound; the exact read is found only on error)
+    int64_t mx = 1, mn = 0;
+    {
+        nw_host::Pool& pool = nw_host::Pool::get();
+        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
+        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
+        pool.run(parts, [&](int q) {
+            int64_t lo, hi, a = 1, b = 0;
+            nw_host::Pool::range(n, parts, q, &lo, &hi);
+            for (int64_t r = lo; r < hi; ++r) {
+                const int64_t len = offsets[r + 1] - offsets[r];
+                a = len > a ? len : a;
+                b = len < b ? len : b;
+            }
+            pmx[(size_t)q] = a;
+            pmn[(size_t)q] = b;
+        });
+        for (int q = 0; q < parts; ++q) {
+            mx = std::max(mx, pmx[(size_t)q]);
+            mn = std::min(mn, pmn[(size_t)q]);
+        }
+    }
+    if (mn < 0 || mx > (1 << 20))
+        for (int64_t r = 0; r < n; ++r) {
+            const int64_t len = offsets[r + 1] - offsets[r];
+            if (len < 0 || len > (1 << 20))
+            {
+                (void)hipStreamSynchronize(c->s_in);   // the queued uploads read the caller's arrays
+                return restore(fail(c, NW_E_INVALID, "read %lld has length %lld", (long long)r, (long long)len));
+            }
+        }
+    const int32_t lb_max = (int32_t)mx;
+    ht.lap(0);
     c->out_mode = NW_OUT_OPS;
     c->ran = false;
     c->call_done = false;
@@ -1478,7 +1596,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         configured = r ? -1 : g;
         return r;
     };
-    int rc = NW_OK;
     // configure every group once up front: the buffers reach their largest size before
     // anything is queued (no allocation inside the pipeline)
     // two sets overlap a chunk's tail with the next chunk's bulk; a third measured slower
@@ -1490,6 +1607,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // recorded only once the host has read that chunk's total: one set cannot pipeline
     // several chunks (its wait would come before the record)
     if (several) nsets = std::max(nsets, 2);
+    // tail split (CRISPR_NW_TAIL=1): a chunk's bulk kernels (unpack, classify, sort, first band
+    // level) on compute stream k mod 2, its latency-bound rest (second level, exact kernel,
+    // compaction) on one tail stream in chunk order, three scratch sets: chunk k + 2's bulk no
+    // longer queues behind chunk k's exact kernel
+    // (C5 pooled call 24.7 -> 21.6 ms, C2 unchanged; CRISPR_NW_TAIL=0: off)
+    bool tail_split = several && kScratchSets >= 3;
+    if (const char* e = std::getenv("CRISPR_NW_TAIL")) tail_split = tail_split && std::atoi(e) != 0;
+    if (tail_split) nsets = 3;
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
         configured = -1;
@@ -1508,91 +1633,51 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     ht.lap(1);
     if (ngroups > 1) configured = -1;   // the pipeline restores each group's saved configuration
     c->s = &c->sc[0];
-    const int64_t base0 = n ? offsets[0] : 0;
-    const int64_t nbytes = n ? offsets[n] - base0 : 0;
-    const int64_t nchunks = (int64_t)chunks.size();
     c->skip16 = false;
     const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
     const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
-    auto restore = [&](int code) {
-        c->skip16 = false;
-        c->out_mode = mode_before;
-        c->n = 0;
-        c->s = &c->sc[0];
-        c->cs = c->stream;
-        return code;
-    };
-    if (rc) return restore(rc);
-    // packed input: the device copy of the packed stream starts at byte P0 (4-aligned: one
-    // dword = 16 bases), the unpacked bytes at batch position base0 & ~15 (16-B stores)
-    const int64_t P0 = (base0 / 16) * 4;
-    const int64_t pk_hi = n ? (offsets[n] + 3) / 4 : 0;   // end of the caller's packed bytes
-    if (pk && upload &&
-        (c->d_packed.reserve((size_t)std::max<int64_t>(pk_hi - P0, 0) + 64) != hipSuccess ||
-         c->d_exc_pos.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess ||
-         c->d_exc_byte.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess))
-        return restore(fail(c, NW_E_NOMEM, "device allocation failed for the packed batch"));
-    if (c->d_reads.reserve((size_t)nbytes + 512 + 16) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
-        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
-        return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
-    if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
-    ht.lap(2);
-    if (upload) c->reads_bias = pk ? (base0 & ~(int64_t)15) : base0;
+    if (rc) {
+        (void)hipStreamSynchronize(c->s_in);
+        return restore(rc);
+    }
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
-    // every upload queued up front: the copy engine streams the batch while chunks compute
-    HIP_OR_FAIL(c, hipEventRecord(c->ev_h0, c->s_in));
-    int64_t h2d_bytes = 0;
-    if (pk && upload && pk->n_exc > 0) {
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_pos.p, pk->exc_pos, sizeof(int64_t) * (size_t)pk->n_exc,
-                                      hipMemcpyHostToDevice, c->s_in));
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_byte.p, pk->exc_byte, (size_t)pk->n_exc, hipMemcpyHostToDevice, c->s_in));
-        h2d_bytes += 9 * pk->n_exc;
-    }
-    for (int64_t k = 0; upload && k < nchunks; ++k) {
-        const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
-        const int64_t b0 = offsets[lo], b1 = offsets[hi];
-        if (pk) {
-            // the chunk's packed dwords (the caller's bytes only; edge bases are masked)
-            const int64_t q0 = std::max((b0 / 16) * 4, base0 / 4), q1 = std::min((b1 + 15) / 16 * 4, pk_hi);
-            if (b1 > b0 && q1 > q0) {
-                HIP_OR_FAIL(c, hipMemcpyAsync(c->d_packed.p + (q0 - P0), pk->packed + q0, (size_t)(q1 - q0),
-                                              hipMemcpyHostToDevice, c->s_in));
-                h2d_bytes += q1 - q0;
-            }
-        } else if (b1 > b0) {
-            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p + (b0 - base0), reads + b0, (size_t)(b1 - b0), hipMemcpyHostToDevice,
-                                          c->s_in));
-            h2d_bytes += b1 - b0;
-        }
-        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
-                                      hipMemcpyHostToDevice, c->s_in));
-        h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
-    }
-    ht.lap(3);
     int64_t total = 0, err = 0;
     bool cap_short = false;
-    // chunk k's runs: once its total is known on the host
+    // Chunk k's runs go back in up to two copies.  When its base (the runs of every earlier
+    // chunk) is known as its records are queued, an estimate of its runs is queued with
+    // them (spec[k] words: the runs per read so far, + 25 %, + 1024), so the copy starts
+    // the moment the chunk is done instead of after the host has read its total; copy_runs
+    // adds what the estimate missed.  Words past the call's total may be written (ops_out
+    // holds ops_cap words; the contents past ops_off[n] are unspecified).
+    std::vector<int64_t> spec((size_t)std::max<int64_t>(nchunks, 1), 0), spec_base(spec.size(), 0);
+    int64_t runs_seen = 0, reads_seen = 0;
     auto copy_runs = [&](int64_t k) -> int {
         ht.lap(4);
         HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
         ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
         err |= h[3];
-        const int64_t cb = h[1], tot = h[2];
+        const int64_t cb = h[1], tot = h[2], done = spec[(size_t)k];
+        if (done > 0 && cb != spec_base[(size_t)k])
+            return fail(c, NW_E_HIP, "chunk %lld: runs base %lld, estimate copied to %lld", (long long)k, (long long)cb,
+                        (long long)spec_base[(size_t)k]);
         if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
         } else if (cb + tot > ops_cap) cap_short = true;
-        else if (tot > 0)
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)tot,
-                                          hipMemcpyDeviceToHost, c->s_out));
+        else if (tot > done)
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb + done, c->sc[k % nsets].d_staging.p + done,
+                                          sizeof(uint32_t) * (size_t)(tot - done), hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
         total = cb + tot;
-        if (ops_out) c->ops_d2h_bytes += 4 * tot;
+        runs_seen += tot;
+        reads_seen += chunks[(size_t)k].hi - chunks[(size_t)k].lo;
+        if (ops_out) c->ops_d2h_bytes += 4 * std::max(tot, done);
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
     const int64_t lag = std::max(1, nsets - 1);
+    const char* spec_env = std::getenv("CRISPR_NW_SPEC");   // "0": every runs copy waits for its total
+    const bool spec_on = lag == 1 && !(spec_env && std::atoi(spec_env) == 0);
     bool any_diag = false;
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
@@ -1602,6 +1687,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         c->s = &c->sc[k % nsets];
         c->cs = c->cstream[k % nsets];
+        if (tail_split) {
+            c->cs = c->cstream[k % 2];
+            c->split_to = c->cstream[2];
+            c->split_ev = c->ev_bulk[(size_t)k];
+            // the set's previous chunk (k - 3) must be through its tail
+            if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));
+        }
         if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)k], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
         if (pk && upload) {   // the chunk's bases -> bytes, then its exception bytes
@@ -1655,6 +1747,18 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
+        // the runs estimate: the base of chunk k is `total` once chunks < k are read back
+        if (ops_out && spec_on) {   // (lag 1: copy_runs(k - 1) ran above)
+            const double per = reads_seen > 0 ? (double)runs_seen / (double)reads_seen : 2.0;
+            int64_t w = (int64_t)(per * 1.25 * (double)(hi - lo)) + 1024;
+            w = std::min(w, std::min(ops_cap - total, c->staging_cap));
+            if (w > 0) {
+                HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + total, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)w,
+                                              hipMemcpyDeviceToHost, c->s_out));
+                spec[(size_t)k] = w;
+                spec_base[(size_t)k] = total;
+            }
+        }
     }
     for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k)
         if ((rc = copy_runs(k))) return restore(rc);

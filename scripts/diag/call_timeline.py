@@ -16,8 +16,8 @@ for name, kind in (("kernel_trace", "K"), ("memory_copy_trace", "C")):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind, label[:60],
                              r.get("Stream_Id", r.get("Queue_Id", ""))))
 rows.sort()
-# the last call: from the last H2D burst that precedes the final kernels; print the final 150 events
-tail = rows[-160:]
+# the last call: from the last H2D burst that precedes the final kernels; print the final 200 events
+tail = rows[-200:]
 t0 = tail[0][0]
 for s, e, k, lab, q in tail:
     print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {k} q{q} {lab}")
