@@ -357,12 +357,7 @@ def dual_leg(al, n_reads, steps, warmup):
         al.set_reference(hdr)
         al.align_ops(None, po.array, out=(stats2.array, None, ops_off2.array), resident=True, records_only=True)
 
-    for _ in range(warmup):
-        step()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    dt = (time.perf_counter() - t0) / steps
+    dt = timed_calls(None, step, steps, warmup, LEG_WARM_S) / steps
     hdr_better = int((stats2.array["n_ident"] * stats.array["aln_len"] >
                       stats.array["n_ident"] * stats2.array["aln_len"]).sum())
     out = {"metric": "dual-aligned reads/s (C3: 1M reads x amplicon + HDR amplicon, 1 GPU)",

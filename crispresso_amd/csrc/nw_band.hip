@@ -47,9 +47,10 @@
 //     [words / 4][lanes][4 words]: the fill writes 16 steps of a pair's lanes as one
 //     contiguous dwordx4 row, an M run of the walk reads 16 steps of its diagonal
 //     pair with one dwordx4 per lane;
-//   * ops output: a diagonal pass (nw_band_fill<W, false>) first aligns the reads of
+//   * ops output: a diagonal pass (nw_band_fill<W, 0>) first aligns the reads of
 //     the amplicon's length without traceback bits and finishes the single-diagonal
-//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, true>);
+//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, 1>), or,
+//     when both run in one launch (nw_band_fill<W, 2>), the next level's redo list;
 //   * nw_band_walk: one wavefront per read: start cell from the W captures,
 //     certificate, the run-based walk of nw_common.h over the band, strings.
 #include <hip/hip_runtime.h>
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
 // launches of ~8 us each per chunk).  The last segment writes the DP count (*band_count).
 // With a.order_a (the diagonal pass, ops output): reads of the amplicon's length go to
 // their own list instead (order_a, *count_a; a second look-back): the reads of a
-// substitution-only variant, which nw_band_fill<W, false> aligns without traceback bits.
+// substitution-only variant, which nw_band_fill<W, 0> aligns without traceback bits.
 // ============================================================================
 constexpr int kSegReads = 4096, kSegThreads = 1024, kSegWaves = kSegThreads / 64;
 
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
 // ============================================================================
 // Fill
 // ============================================================================
-// Epilogue of the diagonal pass (nw_band_fill<W, false>): every lane of the wavefront
+// Epilogue of the diagonal pass (nw_band_fill<W, 0 / 2>): every lane of the wavefront
 // calls it (ballots).  Per read of the lane's pair: the start cell from the captures (the
 // last cell of each band diagonal lies on the last row or column; same keys and scan
 // order as nw_band_walk), the plain certificate (every alignment leaving the band scores
@@ -421,8 +422,11 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
 // codes); any other read -- not certified, not diagonal, a code outside A C G T N, a byte
 // EDNAFULL does not score, more runs than a slot -- goes to tile_list, where the
 // traceback pass and the walk take it (and the refined certificate / the next level).
+// Overlap of diagonal d = j - i (pairs of the alignment that stays on it).
+__device__ __forceinline__ int diag_pairs(int La, int Lb, int d) { return d >= 0 ? min(La, Lb - d) : min(Lb, La + d); }
+
 template <int W>
-__device__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, const uint32_t* tab,
+__device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, const uint32_t* tab,
                                    const unsigned char* pcd, int La, int dlo, int q, int grp, bool valid, bool act,
                                    long long ra, long long rb, int LbA, int LbB, unsigned badA, unsigned badB,
                                    unsigned padA, unsigned padB, unsigned cap0, unsigned cap1, unsigned capB0,
@@ -470,13 +474,51 @@ __device__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, con
         int pmax = -1;
         if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
         if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
-        const bool certified = pmax < 0 || score > a.band_maxsub * pmax;
+        bool certified = pmax < 0 || score > a.band_maxsub * pmax;
         // the start diagonal's test bit, from the lane that owns it
         const int ds = ej - ei - dlo;
         const int src = (lane & ~15) | (((ds >> 1) & (L - 1)) * PR + (lane & 15) % PR);
         const unsigned eqs = (unsigned)__shfl((int)eqbits, src, 64);
         const bool diag = ((eqs >> (ds & 1)) & 1u) != 0u && ds >= 0 && ds < W;
         const bool codes_ok = !(h ? (badB | padB) : (badA | padA));
+        // Refined certificate (nw_band_walk's band_single_diagonals_below): when
+        // S <= UB but S > UB - O, an alignment leaving the band with an internal gap scores
+        // below S; one without is a single diagonal beyond the band, summed here down its
+        // whole overlap from the LDS codes (the pair's lanes stride over it) for the diagonals
+        // with maxsub * P(d) >= S.  (The HDR pass: 10 clustered mismatches against the HDR
+        // amplicon leave S below the plain bound of 16 diagonals.)  Control flow stays
+        // uniform over the wavefront: the diagonal counts are wave maxima, the sums reduced
+        // over every lane.
+        {
+            const bool need = use[h] && act && Lb > 0 && !certified && diag && codes_ok &&
+                              score > a.band_maxsub * pmax - a.gap_open;
+            int kn[2] = {0, 0};
+            if (need)
+                for (int side = 0; side < 2; ++side)
+                    for (int k = 1;; ++k) {
+                        const int P = diag_pairs(La, Lb, side == 0 ? dhi + k : dlo - k);
+                        if (P <= 0 || a.band_maxsub * P < score) break;
+                        kn[side] = k;
+                    }
+            bool beaten = false;
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const int km = (int)wave_max_u32((unsigned)kn[side]);
+                for (int k = 1; k <= km; ++k) {
+                    const int d = side == 0 ? dhi + k : dlo - k;
+                    const bool on = k <= kn[side];
+                    const int P = on ? diag_pairs(La, Lb, d) : 0;
+                    const int i0 = d >= 0 ? 1 : 1 - d, j0 = d >= 0 ? 1 + d : 1;   // first cell, 1-based
+                    int sum = 0;
+                    for (int t = q; t < P; t += L)
+                        sum += half(*(LdsU*)(uintptr_t)(acd[kAPad + i0 + t] + pcd[kJPad + j0 + t]), h) - 2 * E;
+#pragma unroll
+                    for (int o = PR; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+                    beaten = beaten || (on && sum >= score);
+                }
+            }
+            if (need && !beaten) certified = true;
+        }
         const int nd = ei < ej ? ei : ej;
         const bool endg = (ei == La && ej < Lb) || (ej == Lb && ei < La);
         const int lead = (ei > ej ? ei : ej) - nd;
@@ -534,9 +576,10 @@ __device__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, con
 }
 
 // Virtual DP list of the traceback pass: band_order[0, *band_count) then (diagonal pass
-// on) tile_list[0, *tile_count) -- the list-A reads the diagonal pass handed on.
+// on, separate launches) tile_list[0, *tile_count) -- the list-A reads the diagonal pass
+// handed on.  (Merged launch, a.tile_to_redo: those go to the next level instead.)
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
-    return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
+    return (long long)*a.band_count + (a.tile_count && !a.tile_to_redo ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
     return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
@@ -549,7 +592,7 @@ __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long lo
 // single-diagonal test (start cell's M == its diagonal's plain sum: the traceback is the
 // diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
 // passes; the others go to tile_list for the traceback pass.
-template <int W, bool TB>
+template <int W, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
@@ -593,15 +636,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    // list positions [0, count) hold the reads that need the DP (the rest are exact copies)
-    const long long nb = TB ? (long long)*a.band_count : 0ll;
-    const long long count = TB ? band_list_count(a) : (long long)*a.count_a;
-    const long long pair_hi = min(a.band_pair_hi, (count + 1) / 2);
-    const long long npairs = pair_hi - a.band_pair_lo;
-    const long long nwork = npairs > 0 ? (npairs + kBPW - 1) / kBPW : 0;
+    // list A (the diagonal pass) and the band list (the traceback fill): wave work items of
+    // kBPW pairs each, list A's first in the merged launch
     const int NW = a.band_words;
-    for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nwork; wv += (long long)gridDim.x * wpb) {
-        const long long g = a.band_pair_lo + wv * kBPW + grp;
+    const long long cntA = MODE != 1 ? (long long)*a.count_a : 0ll;
+    const long long pA = (cntA + 1) / 2;
+    const long long nA = (pA + kBPW - 1) / kBPW;
+    const long long nbB = MODE != 0 ? (long long)*a.band_count : 0ll;
+    const long long cntB = MODE != 0 ? band_list_count(a) : 0ll;
+    const long long pB = MODE != 0 ? min(a.band_pair_hi, (cntB + 1) / 2) : 0ll;
+    const long long npB = pB - (MODE != 0 ? a.band_pair_lo : 0ll);
+    const long long nB = npB > 0 ? (npB + kBPW - 1) / kBPW : 0ll;
+    auto body = [&](auto TBc, long long wv) __attribute__((always_inline)) {
+        constexpr bool TB = decltype(TBc)::value;
+        const long long pair_lo = TB ? a.band_pair_lo : 0ll;
+        const long long pair_hi = TB ? pB : pA;
+        const long long count = TB ? cntB : cntA;
+        const long long nb = nbB;
+        const long long g = pair_lo + wv * kBPW + grp;
         int dlo = 0;
         bool act = false;
         long long offA = 0, offB = 0, ra = 0, rb = 0;
@@ -703,7 +755,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         const int tau_end = (int)wave_max_u32(thi);
         const int tau_pro = (int)wave_max_u32(tpro);
         lds_fence();
-        unsigned char* region = TB ? a.band_region + (g - a.band_pair_lo) * a.band_stride : nullptr;
+        unsigned char* region = TB ? a.band_region + (g - pair_lo) * a.band_stride : nullptr;
         if (TB && q == 0 && g < pair_hi) {
             // everything the walk needs to find the pair's reads: one 48-byte load
             int4* hp = (int4*)region;
@@ -711,7 +763,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
             hp[1] = make_int4((int)ra, (int)rb, (int)(a.offsets[ra + 1] - offA), (int)(a.offsets[rb + 1] - offB));
             hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
         }
-        if (tau_end == 0 && TB) continue;   // no active group in this wavefront
+        if (tau_end == 0 && TB) return;   // no active group in this wavefront
 
         const int d0 = dlo + 2 * q;
         int tb[2], te[2], teB[2];
@@ -883,13 +935,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                                   (bad_mask >> grp) & 1u, (bad_mask >> (16 + grp)) & 1u, (pad_mask >> grp) & 1u,
                                   (pad_mask >> (16 + grp)) & 1u, cap0, cap1, capB0, capB1, dc0, dc1, dcB0, dcB1,
                                   bval[0], bval[1], lane);
-            continue;
+            return;
         }
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
             caps[2 * q] = (cap0 & 0xffffu) | (capB0 & 0xffff0000u);
             caps[2 * q + 1] = (cap1 & 0xffffu) | (capB1 & 0xffff0000u);
         }
+    };
+    for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nA + nB; wv += (long long)gridDim.x * wpb) {
+        if constexpr (MODE == 0) body(std::false_type{}, wv);
+        else if constexpr (MODE == 1) body(std::true_type{}, wv);
+        else if (wv < nA) body(std::false_type{}, wv);
+        else body(std::true_type{}, wv - nA);
     }
 }
 
@@ -1206,8 +1264,6 @@ __device__ void band_emit(const unsigned* runs, int nruns, const unsigned char* 
     }
 }
 
-// Overlap of diagonal d = j - i (pairs of the alignment that stays on it).
-__device__ __forceinline__ int diag_pairs(int La, int Lb, int d) { return d >= 0 ? min(La, Lb - d) : min(Lb, La + d); }
 
 // True when every single-diagonal alignment outside [dlo, dhi] whose overlap could
 // reach `score` (maxsub * P(d) >= score) scores below it.  A score table lookup per
@@ -1517,6 +1573,12 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
     if (a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const long long nb = *a.band_count;
     const long long n = band_list_count(a);
+    // merged first-level fill: the diagonal pass's hand-ons lead the redo list (all of the
+    // amplicon's length: consecutive pairs of equal lengths); block b copies its slice
+    const long long nt = a.tile_to_redo && a.tile_count ? (long long)*a.tile_count : 0ll;
+    for (long long t = (long long)blockIdx.x * kRedoBlock + threadIdx.x; t < nt && t < (long long)(blockIdx.x + 1) * kRedoBlock;
+         t += blockDim.x)
+        a.redo_list[t] = a.tile_list[t];
     const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
     int f[4], s = 0;
 #pragma unroll
@@ -1532,13 +1594,13 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
         if (threadIdx.x == 0) sh[0] = (int)e;
     }
     __syncthreads();
-    int pos = sh[0] + local;
+    long long pos = nt + sh[0] + local;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
         if (f[t]) a.redo_list[pos++] = (int32_t)band_list_read(a, k0 + t, nb);
     if (threadIdx.x == 0) {
         if (sh[1]) a.fallback_count[3] = 1;
-        if (blockIdx.x == gridDim.x - 1) *a.redo_count = sh[0] + total;
+        if (blockIdx.x == gridDim.x - 1) *a.redo_count = (int32_t)(nt + sh[0] + total);
     }
 }
 
@@ -1561,7 +1623,7 @@ bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb,
 hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
                           int* walk_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        fill_blocks, W == 16 ? (const void*)nw_band_fill<16, true> : (const void*)nw_band_fill<32, true>, 64 * fill_wpb,
+        fill_blocks, W == 16 ? (const void*)nw_band_fill<16, 1> : (const void*)nw_band_fill<32, 1>, 64 * fill_wpb,
         fill_lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1587,11 +1649,15 @@ int64_t band_lookback_words(int64_t n) {
 }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill) {
-    if (W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+                       hipEvent_t after_fill, bool merged) {
+    if (merged && W == 16)
+        hipLaunchKernelGGL((nw_band_fill<16, 2>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    else if (merged)
+        hipLaunchKernelGGL((nw_band_fill<32, 2>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    else if (W == 16)
+        hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else
-        hipLaunchKernelGGL((nw_band_fill<32, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<32, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
@@ -1612,9 +1678,9 @@ hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, i
     d.band_pair_lo = 0;
     d.band_pair_hi = pairs;
     if (W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
+        hipLaunchKernelGGL((nw_band_fill<16, 0>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
     else
-        hipLaunchKernelGGL((nw_band_fill<32, false>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
+        hipLaunchKernelGGL((nw_band_fill<32, 0>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
     return hipGetLastError();
 }
 

@@ -68,6 +68,10 @@ struct KernelArgs {
     int32_t* count_a;
     int32_t* tile_list;
     int32_t* tile_count;           // null outside the first level's traceback pass
+    // 1: the merged first-level fill (nw_band_fill<W, 2>: diagonal pass over list A and the
+    // traceback fill over band_order in one launch): the reads the diagonal pass hands on go
+    // to the next level's redo list (first), not to this level's traceback pass
+    int32_t tile_to_redo;
     int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
     // > 0: when the first level hands on at most this many reads (*redo_count), the second
     // level's kernels return at once and the exact kernel takes them too (its fallback list,
@@ -153,7 +157,7 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
 int64_t band_lookback_words(int64_t n);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill);
+                       hipEvent_t after_fill, bool merged = false);
 // the diagonal pass (nw_band_fill<W, false>) over list A; `pairs`: an upper bound of its pairs
 hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
@@ -181,12 +185,14 @@ hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_ld
 // this chunk's total, [3] errors (1: staging full, 2: spill area full, from opsctl[1], 4: a
 // look-back cut off); running over the call: [4] exact-kernel reads, [5] second band level
 // reads of two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the
-// second level alone (OpsCounts: the device counters of the chunk's kernels); [8], [9]: the
-// running base, read from [8 + parity] and written to the other (chunk k: parity k & 1).
+// second level alone, [8] reads of the diagonal passes' lists A, [9] the reads those passes
+// handed to the traceback pass (OpsCounts: the device counters of the chunk's kernels);
+// [kOpsCtl], [kOpsCtl + 1]: the running base, read from [kOpsCtl + parity] and written to
+// the other (chunk k: parity k & 1).
 // status: band_lookback_words(n) look-back words; epoch: new per launch.  opsctl: the
 // kernels' flags.  hctl: pinned host copy of ctl[0 .. kOpsCtl) written by the launch (or null).
 constexpr int kOpsBlockReads = 1024;
-constexpr int kOpsCtl = 8;
+constexpr int kOpsCtl = 10;
 constexpr int kOpsCtlAll = kOpsCtl + 2;
 struct OpsCounts {
     const int32_t* fallback;   // [0]: exact-kernel reads of the chunk, [3]: look-back error flag
@@ -196,6 +202,8 @@ struct OpsCounts {
     int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
     int32_t one_level;         // the chunk ran the 32-diagonal level alone: its DP reads go to ctl[7]
     int32_t prio;              // raise the compaction's issue priority (KernelArgs::tail_prio)
+    const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
+    const int32_t* handed;     // ... and the reads it handed on
 };
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,

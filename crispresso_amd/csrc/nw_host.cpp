@@ -145,6 +145,8 @@ struct nw_ctx {
     bool exact_tb_lds = true;
     bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
     bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
+    bool diag_off = false;            // this chunk: no diagonal pass (ops_call's adaptive choice)
+    bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -741,6 +743,7 @@ hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
 // uploaded arrays (outputs, records and fallback queue at the same index).
 // Everything is queued on c->stream; nothing synchronises.
 int launch_range(nw_ctx* c, int64_t base) {
+    c->diag_ran = false;
     {
         const char* e = std::getenv("CRISPR_NW_PRIO");
         c->tail_prio = !(e && std::atoi(e) == 0);
@@ -806,13 +809,16 @@ int launch_range(nw_ctx* c, int64_t base) {
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
         const char* dp_env = std::getenv("CRISPR_NW_DIAGPASS");
-        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !(dp_env && std::atoi(dp_env) == 0);
+        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off &&
+                               !(dp_env && std::atoi(dp_env) == 0);
+        c->diag_ran = diag_pass;
         if (diag_pass) {
             a.order_a = c->s->d_order_a.p;
             a.count_a = c->s->d_fallback_count.p + 4;
             a.tile_list = c->s->d_tile.p;
             a.tile_count = c->s->d_fallback_count.p + 5;
         }
+        const int64_t pairs0 = (c->n + 1) / 2;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
@@ -832,6 +838,12 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
         if (!two || only16) direct = 0;
         c->redo_direct = direct;
+        // two levels with the diagonal pass: its fill and the first level's traceback fill are
+        // one launch (nw_band_fill<16, 2>), its hand-ons lead the second level's redo list
+        // (CRISPR_NW_MERGE=0: separate launches, hand-ons through the first level's traceback)
+        const char* mg = std::getenv("CRISPR_NW_MERGE");
+        const bool merged = diag_pass && two && !only16 && c->diag16_pass_pairs >= pairs0 && !(mg && std::atoi(mg) == 0);
+        a.tile_to_redo = merged ? 1 : 0;
         for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
             nw::KernelArgs al = a;
             al.band_last = only16;
@@ -851,14 +863,15 @@ int launch_range(nw_ctx* c, int64_t base) {
                 al.order_a = nullptr;
                 al.tile_list = nullptr;
                 al.tile_count = nullptr;
-            } else if (al.order_a) {
+            } else if (al.order_a && !merged) {
                 HIP_OR_FAIL(c, nw::launch_band_diag(W, al, fc, pairs, c->cs));
             }
             for (int64_t lo = 0; lo < pairs; lo += pp) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
                 ap.band_pair_hi = std::min(pairs, lo + pp);
-                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
+                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr,
+                                               first && merged));
                 if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
             if (first && c->split_to) {   // the latency-bound rest of the chunk on the tail stream
@@ -933,6 +946,10 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         if (c->diag16_fill.grid > 0 && !c->skip16) cnt.redo = c->s->d_fallback_count.p + 2;
         cnt.one_level = c->diag16_fill.grid > 0 && c->skip16;
         cnt.direct = c->skip16 ? 0 : c->redo_direct;
+        if (c->diag_ran) {
+            cnt.list_a = c->s->d_fallback_count.p + 4;
+            cnt.handed = c->s->d_fallback_count.p + 5;
+        }
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n,
@@ -1471,6 +1488,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     auto restore = [&](int code) {
         c->split_to = nullptr;
         c->skip16 = false;
+        c->diag_off = false;
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1637,6 +1655,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
     const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
+    std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
+    c->diag_off = false;
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
         return restore(rc);
@@ -1731,11 +1751,28 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
+        // adaptive diagonal pass: when it handed most of a chunk's list A on to the traceback
+        // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
+        // two gaps, not down one diagonal), the next chunks skip it; while skipped, every 4th
+        // chunk runs it again
+        if (adaptive && k >= lag + 1) {
+            const int64_t j = k - lag - 1;
+            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
+            static const int64_t zero[nw::kOpsCtl] = {};
+            const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
+            if (!no_diag[(size_t)j]) {
+                const int64_t la = h[8] - hp[8], ho = h[9] - hp[9];
+                c->diag_off = la >= 2048 && 2 * ho > la;
+            } else {
+                c->diag_off = (k & 3) != 0;
+            }
+        }
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k,
                                    (int)(k & 1))))
             return restore(rc);
+        no_diag[(size_t)k] = !c->diag_ran;
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk

@@ -9,7 +9,7 @@
 // offsets (the call's running base + local offset) and copies their runs into the
 // staging array.  The last block writes the chunk's ctl (base, total, path counts)
 // and its pinned host mirror (no copy launch in the chunk's chain).  The running base
-// alternates between two words (ctl[8 + parity]): chunk k reads one and writes the
+// alternates between two words (ctl[kOpsCtl + parity]): chunk k reads one and writes the
 // other, so no block of a launch can see its own chunk's update.
 // The host copies staging[0, ctl[2]) to ops_out + ctl[1].
 #include <hip/hip_runtime.h>
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         if (threadIdx.x == 0) sh_excl = e;
     }
     __syncthreads();
-    const long long base = ctl[8 + parity];
+    const long long base = ctl[kOpsCtl + parity];
     long long off = (long long)sh_excl + local;
     bool over = false;
 #pragma unroll
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         ctl[2] = chunk_total;
         ops_off[n] = base + chunk_total;   // the end of the chunk's last read (the next chunk's first offset)
         ctl[0] = base + chunk_total;
-        ctl[8 + (parity ^ 1)] = base + chunk_total;
+        ctl[kOpsCtl + (parity ^ 1)] = base + chunk_total;
         if (opsctl[1]) ctl[3] |= 2;   // a kernel found the spill area full
         if (cnt.fallback && cnt.fallback[3]) ctl[3] |= 4;   // an aligner kernel's look-back was cut off
         // the call's reads by path, summed over chunks (nw_batch_path_counts after nw_align_ops)
@@ -121,6 +121,8 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0);
         ctl[6] += dp;
         if (cnt.one_level) ctl[7] += dp;
+        if (cnt.list_a) ctl[8] += *cnt.list_a;
+        if (cnt.handed) ctl[9] += *cnt.handed;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];
     }

@@ -2,7 +2,8 @@
 of env knobs the library reads per call: calls alternate A, B, A, B ... so that box-level
 drift (PCIe, host load) hits both alike.
 Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds] [pooled]   (an empty string = defaults;
-pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads)"""
+pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads; c3: the dual
+alignment step, packed amplicon pass + resident HDR pass records-only)"""
 import os
 import sys
 import time
@@ -22,7 +23,11 @@ def parse(spec):
 A, B = parse(sys.argv[1]), parse(sys.argv[2])
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
-if pooled:
+c3 = len(sys.argv) > 4 and sys.argv[4] == "c3"
+if c3:
+    amplicon, hdr, buf, off = synth.c3_workload(bench.READS_PER_GPU)
+    nr = len(off) - 1
+elif pooled:
     amps, buf, off, which = bench.pooled_workload(96, 100_000)
     pw = _lib.pinned_copy(which)
     nr = len(off) - 1
@@ -37,6 +42,8 @@ ops = _lib.PinnedBuffer(4 * nr + 4096, np.uint32)
 p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
 pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
 al = GpuAligner(0)
+stats2 = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
+ops_off2 = _lib.PinnedBuffer(nr + 1, np.int64)
 if not pooled:
     al.set_reference(amplicon)
 keys = set(A) | set(B)
@@ -50,12 +57,18 @@ for i in range(2 * rounds + 4):
     t0 = time.perf_counter()
     if pooled:
         al.align_multi_ops(amps, pr, None, pw.array, out=(stats.array, ops.array, ops_off.array))
+    elif c3:
+        al.set_reference(amplicon)
+        al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
+        al.set_reference(hdr)
+        al.align_ops(None, po.array, out=(stats2.array, None, ops_off2.array), resident=True, records_only=True)
     else:
         al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
     dt = time.perf_counter() - t0
     if i >= 4:
         times[which].append(dt * 1e3)
-    out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes())
+    out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes(),
+           stats2.array.tobytes() if c3 else b"")
     if ref is None:
         ref = out
     elif out != ref:

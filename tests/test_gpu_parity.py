@@ -19,13 +19,20 @@ pytestmark = pytest.mark.gpu
 KERNELS = ["diag", "full"]
 
 
-@pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")])
+# the band path's ops-mode variants of the first level: the diagonal pass and the traceback
+# fill in separate launches (hand-ons through the traceback pass), and no diagonal pass
+VARIANTS = {"diag-split": {"CRISPR_NW_MERGE": "0"}, "diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
+
+
+@pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")] + [f"{v}/ops" for v in VARIANTS])
 def kernel(request, monkeypatch):
     """Run a test once per kernel family (CRISPR_NW_KERNEL selects it) and output
     mode (ops: runs over PCIe + host expansion, the default; rows: the kernels write
     the three strings)."""
     fam, mode = request.param.split("/")
-    monkeypatch.setenv("CRISPR_NW_KERNEL", fam)
+    for k, v in VARIANTS.get(fam, {}).items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("CRISPR_NW_KERNEL", fam.split("-")[0])
     monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
     return request.param
 
