@@ -59,7 +59,7 @@ READS_PER_GPU = 1_000_000
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
 # VALU instruction count per fill launch (newest first)
 PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
-                 for d in ("r02_v5", "r02_v4", "r02_v3", "r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
+                 for d in ("r03_v1", "r02_v5", "r02_v4", "r02_v3", "r02_pmc", "r01_v24", "r01_v23", "r01_v22", "r01_v21", "r01_v19", "r01_quant")]
 AMPLICON_LEN = 250
 
 
@@ -783,11 +783,12 @@ def main():
 
     traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
                                        "nw::nw_ops_", "nw::(anonymous namespace)::nw_ops_",
-                                       required="nw::nw_band_fill<16>")
-    summ, summ_src = pmc_summary("nw_band_fill<16>")
+                                       required="nw::nw_band_fill<16")
+    summ, summ_src = pmc_summary("nw_band_fill<16")
     fill_valu = None
-    if summ:
-        fill_valu = next((v.get("SQ_INSTS_VALU") for k, v in summ.items() if "nw_band_fill<16>" in k), None)
+    if summ:   # the 16-diagonal fills of one pass: the diagonal pass and the traceback fill
+        vals = [v.get("SQ_INSTS_VALU") for k, v in summ.items() if "nw_band_fill<16" in k and v.get("SQ_INSTS_VALU")]
+        fill_valu = float(sum(vals)) if vals else None
     lens = np.diff(offsets)
     cells = band_cells(counts, AMPLICON_LEN, float(lens.mean()) if n else 0.0)
     pass_gbs = algo_bytes / (kms * 1e-3) / 1e9
@@ -866,7 +867,7 @@ def main():
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",
                 "valu": {
-                    "kernel": "nw_band_fill<16> (the largest phase)",
+                    "kernel": "nw_band_fill<16, *> (the largest phase: the diagonal pass and the traceback fill)",
                     "fill16_ms": fill_ms,
                     "valu_instructions_per_launch": fill_valu,
                     "valu_source": summ_src,

@@ -429,7 +429,8 @@ template <int W>
 __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, const uint32_t* tab,
                                    const unsigned char* pcd, int La, int dlo, int q, int grp, bool valid, bool act,
                                    long long ra, long long rb, int LbA, int LbB, unsigned badA, unsigned badB,
-                                   unsigned padA, unsigned padB, unsigned cap0, unsigned cap1, unsigned capB0,
+                                   unsigned padA, unsigned padB, unsigned nA, unsigned nB, bool amp_n,
+                                   unsigned cap0, unsigned cap1, unsigned capB0,
                                    unsigned capB1, unsigned dc0, unsigned dc1, unsigned dcB0, unsigned dcB1,
                                    unsigned bv0, unsigned bv1, int lane) {
     using G = BandGeo<W>;
@@ -525,9 +526,22 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
         const int nruns = 1 + (int)endg + (lead > 0);
         const bool ok = use[h] && act && Lb > 0 && certified && diag && codes_ok && nruns <= a.ops_slot;
         fail[h] = use[h] && !ok;
-        // identical / similar columns down the diagonal (the pair's L lanes stride over it)
+        // identical / similar columns down the diagonal.  Without N in the amplicon or the read
+        // every pair is A C G T against A C G T: identical scores maxsub, any other -4/5 of it,
+        // so the diagonal's plain sum (captured beside M by the lane owning the start diagonal)
+        // gives the identities, and the similar pairs are the identical ones.  Otherwise the
+        // pair's L lanes stride down the diagonal.
+        const unsigned dsel0 = __shfl((int)(h ? dcB0 : dc0), src, 64), dsel1 = __shfl((int)(h ? dcB1 : dc1), src, 64);
+        int fast_id = -1;
+        if (ok && !amp_n && !(h ? nB : nA)) {
+            const int sc5 = a.band_maxsub / 5;
+            const int sum = half((ds & 1) ? dsel1 : dsel0, h) - 2 * E * nd;   // plain scores down the diagonal
+            const int num = sum + 4 * sc5 * nd;
+            if (a.band_maxsub == 5 * sc5 && num >= 0 && num % (9 * sc5) == 0 && num / (9 * sc5) <= nd)
+                fast_id = num / (9 * sc5);
+        }
         unsigned cnt = 0u;
-        if (ok) {
+        if (ok && fast_id < 0) {
             for (int t = q; t < nd; t += L) {
                 const int i = ei - t, j = ej - t;   // 1-based cell
                 const unsigned ab = acd[kAPad + i];
@@ -552,8 +566,8 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
             a.nops[rd] = w;
             Stat r;
             r.aln_len = nd + endlen + lead;
-            r.n_ident = (int)(cnt & 0xffffu);
-            r.n_sim = (int)(cnt >> 16);
+            r.n_ident = fast_id >= 0 ? fast_id : (int)(cnt & 0xffffu);
+            r.n_sim = fast_id >= 0 ? fast_id : (int)(cnt >> 16);
             r.n_gaps = endlen + lead;
             r.score = score;
             r.end_i = ei;
@@ -616,14 +630,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     unsigned* stage = (unsigned*)(lut6 + 256) + wave * 256 + 4 * lane;
     for (int k = tid; k < kTabRows * 36; k += blockDim.x) tab[k] = a.band_tab[k];
     for (int k = tid; k < 256; k += blockDim.x) lut6[k] = a.lut6[k];
+    int has_n = 0;
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
         const int i = k - kAPad;   // row i = amplicon residue i - 1
         // the amplicon's EDNAFULL code (IUPAC codes included: their row of the table), pad outside
         const int c = (i >= 1 && i <= La) ? a.lut[a.amp[i - 1]] : NCODE_PAD;
         // the score table's LDS address is folded in: a0 + j0 is the entry's LDS address
         acd[k] = (uint16_t)(c * 36 * 4 + (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)tab);
+        has_n = has_n || c == 14;
     }
-    __syncthreads();
+    const bool amp_n = __syncthreads_or(has_n) != 0;   // the amplicon has N (the identity count's shortcut is off)
 
     // byte-plane masks of the sign bits (SGPRs: v_and_or_b32 takes no literal)
     unsigned mT[4], mU[4];
@@ -685,6 +701,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         const int Lw = (int)wave_max_u32((unsigned)Lmax);
         unsigned bad_mask = 0u;   // bit p: pair p has a read A / B code outside A C G T N (bits 0-15 / 16-31)
         unsigned pad_mask = 0u;   // the same for bytes EDNAFULL does not score ('-', '*', ...: the walk's gap columns)
+        unsigned n_mask = 0u;     // the same for N (the diagonal pass's identity count)
         constexpr int kSub = kBPW < 4 ? kBPW : 4;   // pairs staged together (loads in flight)
         for (int c0 = 0; c0 < Lw; c0 += 256)
         for (int p0 = 0; p0 < kBPW; p0 += kSub) {
@@ -717,7 +734,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
             for (int pp = 0; pp < kSub; ++pp) {
                 const int p = p0 + pp;
                 const int Lm = max(lenA[pp], lenB[pp]);
-                bool bA = false, bB = false, zA = false, zB = false;
+                bool bA = false, bB = false, zA = false, zB = false, nnA = false, nnB = false;
                 if (4 * k4 < Lm) {
                     unsigned packed = 0u;
 #pragma unroll
@@ -730,6 +747,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                         bB = bB || cB > kPadCode;
                         zA = zA || (j0 < lenA[pp] && cA == kPadCode);
                         zB = zB || (j0 < lenB[pp] && cB == kPadCode);
+                        nnA = nnA || (j0 < lenA[pp] && cA == 4);   // N
+                        nnB = nnB || (j0 < lenB[pp] && cB == 4);
                         cA = min(cA, kPadCode);
                         cB = min(cB, kPadCode);
                         packed |= (unsigned)((cA * 6 + cB) * 4) << (8 * b);
@@ -742,6 +761,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                 if (__ballot(bB)) bad_mask |= 1u << (16 + p);
                 if (!TB && __ballot(zA)) pad_mask |= 1u << p;
                 if (!TB && __ballot(zB)) pad_mask |= 1u << (16 + p);
+                if (!TB && __ballot(nnA)) n_mask |= 1u << p;
+                if (!TB && __ballot(nnB)) n_mask |= 1u << (16 + p);
             }
         }
         const int flags = (((bad_mask >> grp) & 1u) ? REGION_BAD_A : 0) | (((bad_mask >> (16 + grp)) & 1u) ? REGION_BAD_B : 0);
@@ -933,7 +954,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
         if constexpr (!TB) {
             band_diag_epilogue<W>(a, acd, tab, pcd, La, dlo, q, grp, g < pair_hi, act, ra, rb, LbA, LbB,
                                   (bad_mask >> grp) & 1u, (bad_mask >> (16 + grp)) & 1u, (pad_mask >> grp) & 1u,
-                                  (pad_mask >> (16 + grp)) & 1u, cap0, cap1, capB0, capB1, dc0, dc1, dcB0, dcB1,
+                                  (pad_mask >> (16 + grp)) & 1u, (n_mask >> grp) & 1u, (n_mask >> (16 + grp)) & 1u,
+                                  amp_n, cap0, cap1, capB0, capB1, dc0, dc1, dcB0, dcB1,
                                   bval[0], bval[1], lane);
             return;
         }

@@ -147,6 +147,7 @@ struct nw_ctx {
     bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
     bool diag_off = false;            // this chunk: no diagonal pass (ops_call's adaptive choice)
     bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
+    bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -809,7 +810,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
         const char* dp_env = std::getenv("CRISPR_NW_DIAGPASS");
-        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off &&
+        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
                                !(dp_env && std::atoi(dp_env) == 0);
         c->diag_ran = diag_pass;
         if (diag_pass) {
@@ -838,11 +839,12 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
         if (!two || only16) direct = 0;
         c->redo_direct = direct;
-        // two levels with the diagonal pass: its fill and the first level's traceback fill are
-        // one launch (nw_band_fill<16, 2>), its hand-ons lead the second level's redo list
-        // (CRISPR_NW_MERGE=0: separate launches, hand-ons through the first level's traceback)
+        // CRISPR_NW_MERGE=1: the diagonal pass and the first level's traceback fill as one
+        // launch (nw_band_fill<16, 2>), the hand-ons leading the second level's redo list.
+        // Measured slower (kernel-resident fill 0.578 vs 0.477 ms per 1M reads; call 2.40 vs
+        // 2.45 ms against the separate launches' ... ), so off by default.
         const char* mg = std::getenv("CRISPR_NW_MERGE");
-        const bool merged = diag_pass && two && !only16 && c->diag16_pass_pairs >= pairs0 && !(mg && std::atoi(mg) == 0);
+        const bool merged = diag_pass && two && !only16 && c->diag16_pass_pairs >= pairs0 && mg && std::atoi(mg) == 1;
         a.tile_to_redo = merged ? 1 : 0;
         for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
             nw::KernelArgs al = a;
@@ -1489,6 +1491,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->split_to = nullptr;
         c->skip16 = false;
         c->diag_off = false;
+        c->diag_tail = false;
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1657,6 +1660,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
     std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
     c->diag_off = false;
+    int64_t diag_tail = 2;
+    if (const char* e = std::getenv("CRISPR_NW_DIAG_TAIL")) diag_tail = std::max(0, std::atoi(e));
+    if (nchunks < 2) diag_tail = 0;
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
         return restore(rc);
@@ -1751,6 +1757,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
+        // the last chunks of a call run without the diagonal pass: their chains' latency (not
+        // the GPU's throughput) is what the call waits for at its end, and the pass adds a
+        // launch to the chain (CRISPR_NW_DIAG_TAIL chunks, default 2)
+        c->diag_tail = k >= nchunks - diag_tail;
         // adaptive diagonal pass: when it handed most of a chunk's list A on to the traceback
         // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
         // two gaps, not down one diagonal), the next chunks skip it; while skipped, every 4th

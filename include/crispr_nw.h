@@ -215,6 +215,8 @@ int nw_batch_download_ops(nw_ctx* ctx, uint32_t* ops_out, int64_t ops_cap, int64
  * (an exact copy is one run), nw_expand_ops rebuilds the strings on the host.
  * Host buffers should be pinned (nw_host_alloc / nw_host_register).  Synchronous.
  * Returns NW_E_CAPACITY when ops_cap is short (ops_off filled, ops_off[n] = needed).
+ * ops_out[ops_off[n] .. ops_cap) is scratch: the call may write it (a chunk's runs are
+ * copied back from an estimate of their count before the count is known).
  * ops_out = NULL: records and offsets only (a scores-only pass such as the HDR
  * repair alignment, CRISPRessoCORE.py:1808-1828 with just_score). */
 int nw_align_ops(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out,

@@ -24,7 +24,12 @@ A, B = parse(sys.argv[1]), parse(sys.argv[2])
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
 c3 = len(sys.argv) > 4 and sys.argv[4] == "c3"
-if c3:
+c4 = len(sys.argv) > 4 and sys.argv[4] == "c4"
+if c4:   # the C4 shard: 12.5M reads of the native generator in one call
+    amplicon = synth.random_amplicon(bench.AMPLICON_LEN, 1)
+    buf, off = synth.native_reads(amplicon, bench.C4_CALL_READS, 10)
+    nr = len(off) - 1
+elif c3:
     amplicon, hdr, buf, off = synth.c3_workload(bench.READS_PER_GPU)
     nr = len(off) - 1
 elif pooled:
@@ -38,7 +43,7 @@ else:
 pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
 stats = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
 ops_off = _lib.PinnedBuffer(nr + 1, np.int64)
-ops = _lib.PinnedBuffer(4 * nr + 4096, np.uint32)
+ops = _lib.PinnedBuffer((2 if c4 else 4) * nr + 4096, np.uint32)
 p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
 pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
 al = GpuAligner(0)

@@ -1,0 +1,11 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/r03r; mkdir -p $OUT; export TMPDIR=/tmp
+cd $R
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1 || { echo tests failed; grep -E "^(FAILED|ERROR)" $OUT/tests.log | head -30; tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+timeout -k 10 200 python bench.py --kernel-only --steps 10 --warmup 3 > $OUT/kernel_only.json 2> $OUT/kernel_only.err || { tail -20 $OUT/kernel_only.err; exit 1; }
+cut -c1-420 $OUT/kernel_only.json
+timeout -k 10 300 python scripts/diag/ab_call.py "" "CRISPR_NW_DIAGPASS=0" 5 c4 > $OUT/ab_c4.log 2>&1 || { tail -20 $OUT/ab_c4.log; exit 1; }
+tail -2 $OUT/ab_c4.log
+timeout -k 10 300 python scripts/diag/ab_call.py "" "CRISPR_NW_DIAGPASS=0" 16 > $OUT/ab_c2.log 2>&1 || { tail -20 $OUT/ab_c2.log; exit 1; }
+tail -2 $OUT/ab_c2.log

@@ -20,8 +20,8 @@ KERNELS = ["diag", "full"]
 
 
 # the band path's ops-mode variants of the first level: the diagonal pass and the traceback
-# fill in separate launches (hand-ons through the traceback pass), and no diagonal pass
-VARIANTS = {"diag-split": {"CRISPR_NW_MERGE": "0"}, "diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
+# fill in one launch (hand-ons to the second level), and no diagonal pass
+VARIANTS = {"diag-merged": {"CRISPR_NW_MERGE": "1"}, "diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
 
 
 @pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")] + [f"{v}/ops" for v in VARIANTS])
