@@ -87,6 +87,7 @@ struct Scratch {
     }
 };
 constexpr int kScratchSets = 3;
+constexpr int64_t kDiagMinChunks = 12;   // pipelined calls of fewer chunks run without the diagonal pass
 
 struct nw_ctx {
     int device = 0;
@@ -1660,9 +1661,21 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
     std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
     c->diag_off = false;
+    // The diagonal pass saves GPU time but adds a launch to every chunk's chain.  A short
+    // pipeline (the 1M-read call: 7 chunks) waits on its chains' latency and runs without it
+    // (C2 2.26 vs 2.29 ms per call); a long one (the 12.5M-read C4 shard: 50 chunks) is
+    // throughput-bound (18.1 vs 19.0 ms with it); its last chunks, whose latency the call
+    // waits for at its end, run without it (CRISPR_NW_DIAG_TAIL chunks, default 2).
+    // CRISPR_NW_DIAGPASS=1 / 0: on / off for every chunk.
     int64_t diag_tail = 2;
     if (const char* e = std::getenv("CRISPR_NW_DIAG_TAIL")) diag_tail = std::max(0, std::atoi(e));
     if (nchunks < 2) diag_tail = 0;
+    {
+        const char* e = std::getenv("CRISPR_NW_DIAGPASS");
+        const bool forced_on = e && std::atoi(e) == 1;
+        if (forced_on) diag_tail = 0;
+        else if (nchunks > 1 && nchunks < kDiagMinChunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
+    }
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
         return restore(rc);
