@@ -1715,8 +1715,26 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     };
     c->ops_d2h_bytes = 0;
     const int64_t lag = std::max(1, nsets - 1);
-    const char* spec_env = std::getenv("CRISPR_NW_SPEC");   // "0": every runs copy waits for its total
-    const bool spec_on = lag == 1 && !(spec_env && std::atoi(spec_env) == 0);
+    const char* spec_env = std::getenv("CRISPR_NW_SPEC");   // "1": runs-copy estimates
+    // (measured no gain on the 1M-read call and a loss on the pooled call's 96 small chunks:
+    // CRISPR_NW_SPEC=1 turns it on)
+    const bool spec_on = spec_env && std::atoi(spec_env) == 1;
+    // the runs estimate of chunk j, queued on s_out once its base (`total`, every earlier
+    // chunk read back) is known; s_out has already waited for chunk j's end when j's records
+    // were queued
+    auto spec_copy = [&](int64_t j) -> int {
+        if (!ops_out || !spec_on || j < 0 || j >= nchunks || spec[(size_t)j] > 0) return NW_OK;
+        const double per = reads_seen > 0 ? (double)runs_seen / (double)reads_seen : 2.0;
+        int64_t w = (int64_t)(per * 1.25 * (double)(chunks[(size_t)j].hi - chunks[(size_t)j].lo)) + 1024;
+        w = std::min(w, std::min(ops_cap - total, c->staging_cap));
+        if (w > 0) {
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + total, c->sc[j % nsets].d_staging.p, sizeof(uint32_t) * (size_t)w,
+                                          hipMemcpyDeviceToHost, c->s_out));
+            spec[(size_t)j] = w;
+            spec_base[(size_t)j] = total;
+        }
+        return NW_OK;
+    };
     bool any_diag = false;
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
@@ -1801,27 +1819,21 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
         // k's records and offsets
         if (k >= lag && (rc = copy_runs(k - lag))) return restore(rc);
+        // chunk k - lag + 1's base is known now; below k its records are queued already
+        if (k - lag + 1 < k && (rc = spec_copy(k - lag + 1))) return restore(rc);
         HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
         HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
                                       hipMemcpyDeviceToHost, c->s_out));
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
-        // the runs estimate: the base of chunk k is `total` once chunks < k are read back
-        if (ops_out && spec_on) {   // (lag 1: copy_runs(k - 1) ran above)
-            const double per = reads_seen > 0 ? (double)runs_seen / (double)reads_seen : 2.0;
-            int64_t w = (int64_t)(per * 1.25 * (double)(hi - lo)) + 1024;
-            w = std::min(w, std::min(ops_cap - total, c->staging_cap));
-            if (w > 0) {
-                HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + total, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)w,
-                                              hipMemcpyDeviceToHost, c->s_out));
-                spec[(size_t)k] = w;
-                spec_base[(size_t)k] = total;
-            }
-        }
+        // lag 1: chunk k's own base is known (copy_runs(k - 1) ran above)
+        if (lag == 1 && (rc = spec_copy(k))) return restore(rc);
     }
-    for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k)
+    for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k) {
         if ((rc = copy_runs(k))) return restore(rc);
+        if ((rc = spec_copy(k + 1))) return restore(rc);
+    }
     ht.lap(4);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);
