@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 exact |= 1ull << us[t];
                 if (a.ops) {   // ops output: one M run of La columns, no rows
                     if (lane == 0) {
-                        a.ops[(r0 + us[t]) * a.ops_slot] = ((unsigned)RUN_M << 28) | (unsigned)La;
+                        a.ops[r0 + us[t]] = ((unsigned)RUN_M << 28) | (unsigned)La;   // run 0 of the read's slot
                         a.nops[r0 + us[t]] = 1;
                     }
                     if (lane < 8) {
@@ -558,11 +558,12 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
         for (int o = PR; o < 16; o <<= 1) cnt += (unsigned)__shfl_xor((int)cnt, o, 64);
         if (ok && q == 0) {
             const int endlen = endg ? (ei == La ? Lb - ej : La - ei) : 0;
-            uint32_t* slot = a.ops + rd * a.ops_slot;
+            uint32_t* slot = a.ops + rd;
+            const long long sst = a.ops_stride;
             int w = 0;
-            if (lead > 0) slot[w++] = ((unsigned)(ei > nd ? RUN_Y : RUN_X) << 28) | (unsigned)lead;
-            slot[w++] = ((unsigned)RUN_M << 28) | (unsigned)nd;
-            if (endg) slot[w++] = ((unsigned)(ei == La ? RUN_X : RUN_Y) << 28) | (unsigned)endlen;
+            if (lead > 0) slot[sst * w++] = ((unsigned)(ei > nd ? RUN_Y : RUN_X) << 28) | (unsigned)lead;
+            slot[sst * w++] = ((unsigned)RUN_M << 28) | (unsigned)nd;
+            if (endg) slot[sst * w++] = ((unsigned)(ei == La ? RUN_X : RUN_Y) << 28) | (unsigned)endlen;
             a.nops[rd] = w;
             Stat r;
             r.aln_len = nd + endlen + lead;

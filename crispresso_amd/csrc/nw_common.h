@@ -301,8 +301,8 @@ __device__ int walk_runs_wide(const Nib& nib, int La, int Lb, int ei, int ej, un
 // (bump-allocated, the position in slot[0]).  A full spill area sets ops_ctl[1]
 // (the host reports it).  Rows are not written in this mode.
 __device__ inline void store_ops(const KernelArgs& a, long long rd, const unsigned* runs, int nruns, int lane) {
-    uint32_t* slot = a.ops + rd * a.ops_slot;
-    uint32_t* dst = slot;
+    uint32_t* slot = a.ops + rd;   // word q at slot[q * ops_stride]
+    uint32_t* dst = nullptr;
     if (nruns > a.ops_slot) {
         int pos = 0;
         if (lane == 0) pos = atomicAdd(a.ops_ctl, nruns);
@@ -318,7 +318,10 @@ __device__ inline void store_ops(const KernelArgs& a, long long rd, const unsign
         dst = a.spill + pos;
     }
     if (lane == 0) a.nops[rd] = nruns;
-    for (int q = lane; q < nruns; q += 64) dst[q] = runs[nruns - 1 - q];
+    if (dst)
+        for (int q = lane; q < nruns; q += 64) dst[q] = runs[nruns - 1 - q];
+    else
+        for (int q = lane; q < nruns; q += 64) slot[(long long)q * a.ops_stride] = runs[nruns - 1 - q];
 }
 
 template <class Score>

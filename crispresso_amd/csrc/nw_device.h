@@ -84,6 +84,8 @@ struct KernelArgs {
     // spill area (bump-allocated words, the position in slot[0]).  null ops = rows.
     uint32_t* ops;
     int32_t ops_slot;
+    int64_t ops_stride;            // slot layout: run q of read r at ops[q * ops_stride + r] (the compaction
+                                   // reads the first runs of consecutive reads as whole lines)
     int32_t* nops;                 // [n] runs per read (0: empty read)
     uint32_t* spill;
     int64_t spill_cap;             // words
@@ -205,7 +207,7 @@ struct OpsCounts {
     const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
     const int32_t* handed;     // ... and the reads it handed on
 };
-hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
+hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
                               hipStream_t s, int64_t* hctl = nullptr);

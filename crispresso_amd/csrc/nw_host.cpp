@@ -163,6 +163,7 @@ struct nw_ctx {
     DevBuf<int64_t> d_ctl64, d_opsoff;
     int64_t spill_cap = 0, staging_cap = 0;
     int ops_slot = nw::kOpsSlot;       // runs per read slot (CRISPR_NW_OPS_SLOT: tests force spills)
+    int64_t ops_stride = 1;            // reads per slot row (the chunk capacity: ops_reserve)
     hipStream_t s_in = nullptr, s_out = nullptr;
     std::vector<hipEvent_t> ev_in, ev_cs, ev_ce, ev_out, ev_bulk;
     hipEvent_t ev_h0 = nullptr;
@@ -780,6 +781,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.out = nullptr;
         a.ops = c->s->d_slots.p;
         a.ops_slot = c->ops_slot;
+        a.ops_stride = c->ops_stride;
         a.nops = c->s->d_nops.p;
         a.spill = c->s->d_spill.p;
         a.spill_cap = c->spill_cap;
@@ -915,6 +917,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     c->spill_cap = (spill_mb << 20) / 4;
     if (const char* e = std::getenv("CRISPR_NW_SPILL_WORDS")) c->spill_cap = std::max(1ll, std::atoll(e));   // tests
     c->staging_cap = chunk * c->ops_slot + c->spill_cap;
+    c->ops_stride = chunk;
     HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(chunk * c->ops_slot)));
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
@@ -955,7 +958,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         }
     }
     if (c->n <= 0) cnt.fallback = nullptr;
-    HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->s->d_spill.p, c->n,
+    HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
                                           c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
                                           c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl));
     return NW_OK;
@@ -1722,6 +1725,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // the runs estimate of chunk j, queued on s_out once its base (`total`, every earlier
     // chunk read back) is known; s_out has already waited for chunk j's end when j's records
     // were queued
+    int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
+    const char* er_env = std::getenv("CRISPR_NW_EARLY_RUNS");   // "0": the round-2 order at the call's end
+    const bool early_runs = !(er_env && std::atoi(er_env) == 0);
     auto spec_copy = [&](int64_t j) -> int {
         if (!ops_out || !spec_on || j < 0 || j >= nchunks || spec[(size_t)j] > 0) return NW_OK;
         const double per = reads_seen > 0 ? (double)runs_seen / (double)reads_seen : 2.0;
@@ -1819,6 +1825,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
         // k's records and offsets
         if (k >= lag && (rc = copy_runs(k - lag))) return restore(rc);
+        // the last chunk: every earlier chunk's runs are queued ahead of its records, so they
+        // copy while it computes (otherwise s_out would hold them behind the last chunk's end)
+        if (k == nchunks - 1 && early_runs)
+            for (int64_t j = std::max<int64_t>(0, k - lag + 1); j < k; ++j) {
+                if ((rc = copy_runs(j))) return restore(rc);
+                runs_queued = j + 1;
+            }
         // chunk k - lag + 1's base is known now; below k its records are queued already
         if (k - lag + 1 < k && (rc = spec_copy(k - lag + 1))) return restore(rc);
         HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
@@ -1830,7 +1843,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // lag 1: chunk k's own base is known (copy_runs(k - 1) ran above)
         if (lag == 1 && (rc = spec_copy(k))) return restore(rc);
     }
-    for (int64_t k = std::max<int64_t>(0, nchunks - lag); k < nchunks; ++k) {
+    for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k) {
         if ((rc = copy_runs(k))) return restore(rc);
         if ((rc = spec_copy(k + 1))) return restore(rc);
     }

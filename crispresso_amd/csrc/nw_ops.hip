@@ -50,7 +50,7 @@ __device__ long long block_excl_scan(long long v, long long* total) {
 }
 
 __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nops, const uint32_t* slots, int slot,
-                                                              const uint32_t* spill, int64_t n,
+                                                              int64_t stride, const uint32_t* spill, int64_t n,
                                                               unsigned long long* status, unsigned epoch, int parity,
                                                               int64_t* ctl, int64_t* ops_off, uint32_t* staging,
                                                               int64_t staging_cap, const int32_t* opsctl,
@@ -83,12 +83,17 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         if (r >= n) break;
         ops_off[r] = base + off;
         const int c = c4[k];
-        const uint32_t* src = slots + r * slot;
-        if (c > slot) src = spill + src[0];
+        // run q of read r at slots[q * stride + r]: consecutive reads' first runs share lines
+        const uint32_t* src = slots + r;
+        long long step = stride;
+        if (c > slot) {
+            src = spill + src[0];
+            step = 1;
+        }
         if (off + c > staging_cap) {
             over = true;
         } else {
-            for (int q = 0; q < c; ++q) staging[off + q] = src[q];
+            for (int q = 0; q < c; ++q) staging[off + q] = src[q * step];
         }
         off += c;
     }
@@ -130,12 +135,12 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
 
 }  // namespace
 
-hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, const uint32_t* spill, int64_t n,
+hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
                               hipStream_t s, int64_t* hctl) {
     const int nblk = (int)std::max<int64_t>(1, (n + kOpsBlockReads - 1) / kOpsBlockReads);
-    hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, spill, n, status, epoch,
+    hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, stride, spill, n, status, epoch,
                        parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio);
     return hipGetLastError();
 }
