@@ -22,17 +22,17 @@ def test_pmc_summaries_exist_and_newest_first():
     b = load_bench()
     with open(newest_summary(b)) as f:
         summ = json.load(f)
-    assert any("nw_band_fill<16>" in k for k in summ)
+    assert any("nw_band_fill<16" in k for k in summ)
     assert any("nw_band_walk<16>" in k for k in summ)
 
 
 def test_band_traffic_from_committed_profile():
     b = load_bench()
     traffic, src = b.pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                 required="nw::nw_band_fill<16>")
+                                 required="nw::nw_band_fill<16")
     assert traffic is not None and traffic > 5e8   # ~1-3 GB per 1M C2 reads
     assert src == os.path.relpath(newest_summary(b), ROOT)
-    summ, src2 = b.pmc_summary("nw_band_fill<16>")
+    summ, src2 = b.pmc_summary("nw_band_fill<16")
     assert src2 == src and any("SQ_INSTS_VALU" in v for v in summ.values())
 
 
