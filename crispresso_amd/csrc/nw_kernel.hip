@@ -67,7 +67,7 @@ __host__ __device__ inline WaveLds wave_lds_layout(int R, int La, int Lb_max, in
     int o = 0;
     w.raw = o;     o += align16(Lb_max + 4);
     w.coff = o;    o += align16(2 * (Lb_max + 4));
-    w.lastrow = o; o += align16(4 * (Lb_max + 1));
+    w.lastrow = o; o += align16(4 * (Lb_max + 1 + 64));   // + a dummy slot per lane (branch-free store)
     w.runs = o;    o += align16(4 * (La + Lb_max + 8));
     w.bits = o;
     if (mode == TB_LDS_FULL) o += align16(Lb_max * 64 * es_of(R));
@@ -234,8 +234,9 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
             const int c_nn = coff[min(max(bj + 2, 0), Lb + 3)];
             if (bj >= 0 && bj < Lb && lane < nl) {
                 unsigned acc[NWD];
-#pragma unroll
-                for (int w = 0; w < NWD; ++w) acc[w] = 0;
+                unsigned nib[R];   // each cell's 4 traceback bits, built independently (no serial chain
+                                   // through the whole step: one wave per SIMD runs this kernel, so its
+                                   // dependency depth is its latency)
                 int Hd = Htop, Mou = rMo, Yu = rY;
                 int mlast = 0;
 #pragma unroll
@@ -248,12 +249,11 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     const int Y = max(Mou, Ye);
                     const int mxy = max(X, Y);
                     const int H = max(M, mxy);
-                    unsigned a = acc[k >> 3];
-                    a = push_sign(a, Ye - Mou);       // Y opens (open > extend)
-                    a = push_sign(a, Xe - Mol[k]);    // X opens
-                    a = push_sign(a, Y - X);          // X > Y
-                    a = push_sign(a, M - mxy);        // M < max(X, Y)
-                    acc[k >> 3] = a;
+                    unsigned a = (unsigned)(Ye - Mou) >> 31;   // Y opens (open > extend)
+                    a = push_sign(a, Xe - Mol[k]);            // X opens
+                    a = push_sign(a, Y - X);                  // X > Y
+                    a = push_sign(a, M - mxy);                // M < max(X, Y)
+                    nib[k] = a;
                     mlast = (k == klast) ? M : mlast;
                     Hd = Hold[k];
                     Hold[k] = H;
@@ -263,8 +263,23 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     Yu = Y;
                 }
                 sMo = Mou; sY = Yu; sH = Hold[R - 1];
+                // word w: cells 8w .. 8w + nr - 1, the first cell in the top nibble; pairs of cells
+                // first (a chain over pairs, not over cells)
+#pragma unroll
+                for (int w = 0; w < NWD; ++w) {
+                    constexpr int kNr8 = 8;
+                    const int k0 = kNr8 * w, nr = (R - k0) < kNr8 ? (R - k0) : kNr8;
+                    unsigned v = 0;
+#pragma unroll
+                    for (int k = 0; k < kNr8; k += 2) {
+                        if (k >= nr) break;
+                        if (k + 1 < nr) v = (v << 8) | (nib[k0 + k] << 4) | nib[k0 + k + 1];
+                        else v = (v << 4) | nib[k0 + k];
+                    }
+                    acc[w] = v;
+                }
                 store_bits<R>(tb.at(bj, lane), acc);
-                if (lane == lr) lastrow[bj] = mlast;
+                lastrow[lane == lr ? bj : args.Lb_max + 1 + lane] = mlast;   // the last row's M (other lanes: a dummy slot)
             }
             Htop = rH;
 #pragma unroll

@@ -1,0 +1,11 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/r03w; mkdir -p $OUT; export TMPDIR=/tmp
+cd $R
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1 || { echo tests failed; grep -E "^(FAILED|ERROR)" $OUT/tests.log | head -30; tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/k -o k --output-format csv -- python3 $R/bench.py --kernel-only --steps 5 --warmup 1 > $OUT/k.log 2>&1 || { tail -20 $OUT/k.log; exit 1; }
+grep -h "nw_align_kernel" $OUT/k/k_kernel_stats.csv | cut -c1-110
+cd $R
+timeout -k 10 300 python scripts/diag/ab_call.py "" "CRISPR_NW_EARLY_RUNS=0" 20 > $OUT/ab.log 2>&1 || { tail -20 $OUT/ab.log; exit 1; }
+tail -2 $OUT/ab.log
