@@ -207,9 +207,18 @@ struct OpsCounts {
     const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
     const int32_t* handed;     // ... and the reads it handed on
 };
+// The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
+// straight into the caller's page-locked buffers (no copies and no host round trip after it).
+struct OpsHostOut {
+    const int4* dstats;   // the chunk's records in HBM (2 int4 per nw_stat); null: off
+    int4* hstats;         // the caller's records of the chunk's reads
+    int64_t* hoff;        // the caller's run offsets of the chunk's reads
+    uint32_t* hops;       // the caller's run array (the call's offsets; null: records only)
+    int64_t hcap;         // its words
+};
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl = nullptr);
+                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr);
 
 }  // namespace nw

@@ -933,7 +933,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
 // staging[which]: ops_off of those reads (global: the call's running base in
 // ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
 int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr,
-                     int64_t* hctl = nullptr, int parity = 0) {
+                     int64_t* hctl = nullptr, int parity = 0, const nw::OpsHostOut* host = nullptr) {
     int rc = launch_range(c, base);
     if (rc) return rc;
     // only the compaction writes the set's staging array: it waits for the copy of the
@@ -960,8 +960,20 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
                                           c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
-                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl));
+                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host));
     return NW_OK;
+}
+
+// Page-locked host memory the device addresses with the same pointer (hipHostMalloc /
+// hipHostRegister'd buffers, e.g. nw_host_alloc): kernels may store into it directly.
+bool host_mapped(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost && at.devicePointer == p;
 }
 
 // NW_OUT_ROWS for the scope of a rows-only entry point (nw_align_batch, nw_align_multi)
@@ -1692,6 +1704,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // the moment the chunk is done instead of after the host has read its total; copy_runs
     // adds what the estimate missed.  Words past the call's total may be written (ops_out
     // holds ops_cap words; the contents past ops_off[n] are unspecified).
+    // the last chunk's records, offsets and runs written by its compaction kernel straight into
+    // the caller's buffers when they are page-locked (CRISPR_NW_DIRECT_OUT=0: copies as for the
+    // other chunks): no copies and no host round trip after the call's last kernel
+    const char* do_env = std::getenv("CRISPR_NW_DIRECT_OUT");
+    const bool direct_out = !(do_env && std::atoi(do_env) == 0) && nchunks >= 1 && host_mapped(stats) &&
+                            host_mapped(ops_off) && (!ops_out || host_mapped(ops_out));
+    std::vector<char> direct_done((size_t)std::max<int64_t>(nchunks, 1), 0);
     std::vector<int64_t> spec((size_t)std::max<int64_t>(nchunks, 1), 0), spec_base(spec.size(), 0);
     int64_t runs_seen = 0, reads_seen = 0;
     auto copy_runs = [&](int64_t k) -> int {
@@ -1700,8 +1719,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
         err |= h[3];
-        const int64_t cb = h[1], tot = h[2], done = spec[(size_t)k];
-        if (done > 0 && cb != spec_base[(size_t)k])
+        const int64_t cb = h[1], tot = h[2], done = direct_done[(size_t)k] ? tot : spec[(size_t)k];
+        if (spec[(size_t)k] > 0 && cb != spec_base[(size_t)k])
             return fail(c, NW_E_HIP, "chunk %lld: runs base %lld, estimate copied to %lld", (long long)k, (long long)cb,
                         (long long)spec_base[(size_t)k]);
         if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
@@ -1815,10 +1834,15 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         // the compaction writes the chunk's ctl into h_ctl[k] itself
+        nw::OpsHostOut ho{};
+        const bool direct_k = direct_out && k == nchunks - 1;
+        if (direct_k) ho = nw::OpsHostOut{(const int4*)(c->d_stats.p + lo), (int4*)(stats + lo), ops_off + lo, ops_out,
+                                          ops_out ? ops_cap : 0};
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k,
-                                   (int)(k & 1))))
+                                   (int)(k & 1), direct_k ? &ho : nullptr)))
             return restore(rc);
+        direct_done[(size_t)k] = direct_k;
         no_diag[(size_t)k] = !c->diag_ran;
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
@@ -1834,11 +1858,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         // chunk k - lag + 1's base is known now; below k its records are queued already
         if (k - lag + 1 < k && (rc = spec_copy(k - lag + 1))) return restore(rc);
-        HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
-        HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
-                                      hipMemcpyDeviceToHost, c->s_out));
-        HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
-                                      hipMemcpyDeviceToHost, c->s_out));
+        if (!direct_k) {
+            HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
+            HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
+                                          hipMemcpyDeviceToHost, c->s_out));
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
+                                          hipMemcpyDeviceToHost, c->s_out));
+        }
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
         // lag 1: chunk k's own base is known (copy_runs(k - 1) ran above)
         if (lag == 1 && (rc = spec_copy(k))) return restore(rc);

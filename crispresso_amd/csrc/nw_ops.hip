@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
                                                               unsigned long long* status, unsigned epoch, int parity,
                                                               int64_t* ctl, int64_t* ops_off, uint32_t* staging,
                                                               int64_t staging_cap, const int32_t* opsctl,
-                                                              OpsCounts cnt, int64_t* hctl, int prio) {
+                                                              OpsCounts cnt, int64_t* hctl, int prio, OpsHostOut ho) {
     __shared__ int sh_bad;
     __shared__ unsigned sh_excl;
     if (prio) __builtin_amdgcn_s_setprio(3);
@@ -77,6 +77,18 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
     const long long base = ctl[kOpsCtl + parity];
     long long off = (long long)sh_excl + local;
     bool over = false;
+    if (ho.dstats) {   // the call's last chunk: records and offsets straight to the caller (coalesced rows)
+        long long o = off;
+#pragma unroll
+        for (int k = 0; k < kOpsPerThread; ++k) {
+            const long long r = r0 + k;
+            if (r >= n) break;
+            ho.hstats[2 * r] = ho.dstats[2 * r];
+            ho.hstats[2 * r + 1] = ho.dstats[2 * r + 1];
+            ho.hoff[r] = base + o;
+            o += c4[k];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kOpsPerThread; ++k) {
         const long long r = r0 + k;
@@ -92,6 +104,14 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         }
         if (off + c > staging_cap) {
             over = true;
+        } else if (ho.hops) {
+            uint32_t* h = ho.hops + base + off;
+            const bool fits = base + off + c <= ho.hcap;   // (short: the host reports NW_E_CAPACITY)
+            for (int q = 0; q < c; ++q) {
+                const uint32_t v = src[q * step];
+                staging[off + q] = v;
+                if (fits) h[q] = v;
+            }
         } else {
             for (int q = 0; q < c; ++q) staging[off + q] = src[q * step];
         }
@@ -138,10 +158,11 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl) {
+                              hipStream_t s, int64_t* hctl, const OpsHostOut* host) {
+    const OpsHostOut ho = host ? *host : OpsHostOut{};
     const int nblk = (int)std::max<int64_t>(1, (n + kOpsBlockReads - 1) / kOpsBlockReads);
     hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, stride, spill, n, status, epoch,
-                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio);
+                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio, ho);
     return hipGetLastError();
 }
 
