@@ -301,9 +301,13 @@ __device__ int walk_runs_wide(const Nib& nib, int La, int Lb, int ei, int ej, un
 // (bump-allocated, the position in slot[0]).  A full spill area sets ops_ctl[1]
 // (the host reports it).  Rows are not written in this mode.
 __device__ inline void store_ops(const KernelArgs& a, long long rd, const unsigned* runs, int nruns, int lane) {
-    uint32_t* slot = a.ops + rd;   // word q at slot[q * ops_stride]
-    uint32_t* dst = nullptr;
+    // the walk / exact kernels: one read per wave, its runs contiguous in the row-major area
+    // (one line per read); its slot's first column-major word holds the spill position
+    uint32_t* slot = a.ops + rd;
+    uint32_t* dst = a.ops + a.ops_stride * a.ops_slot + rd * a.ops_slot;
+    int32_t flag = kNopsRows;
     if (nruns > a.ops_slot) {
+        flag = 0;
         int pos = 0;
         if (lane == 0) pos = atomicAdd(a.ops_ctl, nruns);
         pos = __builtin_amdgcn_readfirstlane(pos);
@@ -317,11 +321,8 @@ __device__ inline void store_ops(const KernelArgs& a, long long rd, const unsign
         if (lane == 0) slot[0] = (uint32_t)pos;
         dst = a.spill + pos;
     }
-    if (lane == 0) a.nops[rd] = nruns;
-    if (dst)
-        for (int q = lane; q < nruns; q += 64) dst[q] = runs[nruns - 1 - q];
-    else
-        for (int q = lane; q < nruns; q += 64) slot[(long long)q * a.ops_stride] = runs[nruns - 1 - q];
+    if (lane == 0) a.nops[rd] = nruns | flag;
+    for (int q = lane; q < nruns; q += 64) dst[q] = runs[nruns - 1 - q];
 }
 
 template <class Score>

@@ -12,6 +12,10 @@ constexpr int NCODE_PAD = 16;   // code used for columns past the end of a read
 
 enum : int32_t { FLAG_EMPTY = 1 };
 constexpr int kOpsSlot = 64;    // runs kept per read in its ops slot (more: spill area)
+// nops[r] flag: read r's runs are in the row-major slot area (the walk / exact kernels:
+// run q at ops[ops_stride * ops_slot + r * ops_slot + q]), not the column-major one (the
+// classify / diagonal-pass records: run q at ops[q * ops_stride + r])
+constexpr int32_t kNopsRows = 1 << 30;
 
 // Per-read record written by the kernel; layout matches nw_stat in include/crispr_nw.h.
 struct Stat {
@@ -84,8 +88,9 @@ struct KernelArgs {
     // spill area (bump-allocated words, the position in slot[0]).  null ops = rows.
     uint32_t* ops;
     int32_t ops_slot;
-    int64_t ops_stride;            // slot layout: run q of read r at ops[q * ops_stride + r] (the compaction
-                                   // reads the first runs of consecutive reads as whole lines)
+    int64_t ops_stride;            // slot layouts: column-major run q of read r at ops[q * ops_stride + r] (the
+                                   // compaction reads consecutive reads' first runs as whole lines); row-major
+                                   // (kNopsRows) at ops[ops_stride * ops_slot + r * ops_slot + q]
     int32_t* nops;                 // [n] runs per read (0: empty read)
     uint32_t* spill;
     int64_t spill_cap;             // words

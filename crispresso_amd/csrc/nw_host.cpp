@@ -918,7 +918,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     if (const char* e = std::getenv("CRISPR_NW_SPILL_WORDS")) c->spill_cap = std::max(1ll, std::atoll(e));   // tests
     c->staging_cap = chunk * c->ops_slot + c->spill_cap;
     c->ops_stride = chunk;
-    HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(chunk * c->ops_slot)));
+    HIP_OR_FAIL(c, c->s->d_slots.reserve((size_t)(2 * chunk * c->ops_slot)));   // column-major + row-major areas
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
     HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));

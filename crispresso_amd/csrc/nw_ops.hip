@@ -60,10 +60,13 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
     if (prio) __builtin_amdgcn_s_setprio(3);
     const long long r0 = (long long)blockIdx.x * kOpsBlockReads + threadIdx.x * kOpsPerThread;
     int c4[kOpsPerThread];
+    bool rows4[kOpsPerThread];
     long long s = 0;
 #pragma unroll
     for (int k = 0; k < kOpsPerThread; ++k) {
-        c4[k] = r0 + k < n ? nops[r0 + k] : 0;
+        const int raw = r0 + k < n ? nops[r0 + k] : 0;
+        c4[k] = raw & (kNopsRows - 1);
+        rows4[k] = (raw & kNopsRows) != 0;
         s += c4[k];
     }
     if (threadIdx.x == 0) sh_bad = 0;
@@ -95,11 +98,15 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         if (r >= n) break;
         ops_off[r] = base + off;
         const int c = c4[k];
-        // run q of read r at slots[q * stride + r]: consecutive reads' first runs share lines
+        // column-major: run q of read r at slots[q * stride + r] (consecutive reads' first runs
+        // share lines); row-major (rows4): contiguous at slots[stride * slot + r * slot]
         const uint32_t* src = slots + r;
         long long step = stride;
         if (c > slot) {
             src = spill + src[0];
+            step = 1;
+        } else if (rows4[k]) {
+            src = slots + stride * slot + r * slot;
             step = 1;
         }
         if (off + c > staging_cap) {
