@@ -43,7 +43,7 @@ EXPORTS = (
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
-    "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts",
+    "nw_host_register", "nw_host_unregister", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts", "nw_batch_exact_reads",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
     "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_ops_rows_concat", "nw_fastq_pack", "nw_batch_device_ops",
@@ -130,6 +130,7 @@ def load() -> ctypes.CDLL:
         "nw_batch_device_ops": (c_int, [ctx_p] + [POINTER(c_void_p)] * 5 + [POINTER(c_int64)] * 2),
         "nw_batch_phase_times": (c_int, [ctx_p, c_void_p]),
         "nw_batch_path_counts": (c_int, [ctx_p, c_void_p]),
+        "nw_batch_exact_reads": (c_int64, [ctx_p]),
         "nw_batch_download_ops": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_align_ops_resident": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),

@@ -275,8 +275,13 @@ class GpuAligner:
         return g
 
     def fallbacks(self) -> int:
-        """Reads of the last run re-aligned with full traceback storage."""
+        """Reads of the last run the 16- and 32-diagonal band levels did not certify (the
+        128-diagonal wide level's input; nw_batch_fallbacks)."""
         return int(self.lib.nw_batch_fallbacks(self._h))
+
+    def exact_reads(self) -> int:
+        """Reads of the last run aligned by the exact int32 kernel (nw_batch_exact_reads)."""
+        return int(self.lib.nw_batch_exact_reads(self._h))
 
     def kernel_times(self) -> dict:
         """Device ms of the last run: DP fill, traceback/emit kernel, the rest."""

@@ -124,34 +124,50 @@ __host__ __device__ inline bool band_geometry(int La, int Lb, int* dlo) { return
 namespace {
 
 // band of W diagonals: L = W / 2 lanes per read pair, PR pairs per 16-lane DPP row
-// (interleaved: pair = lane % PR, q = lane / PR within the row), PW pairs per wavefront
+// (interleaved: pair = lane % PR, q = lane / PR within the row), PW pairs per wavefront.
+// W = kWideDiags (the wide level): one pair per wavefront, lane q = the lane, neighbours
+// through the wave-wide DPP shifts (wave_shr:1 / wave_shl:1; lane 0 / 63 read -inf).
 template <int W> struct BandGeo {
+    static constexpr bool Wide = W > 32;
     static constexpr int L = W / 2;
-    static constexpr int PR = 16 / L;
-    static constexpr int PW = 4 * PR;
+    static constexpr int PR = Wide ? 1 : 16 / L;
+    static constexpr int PW = Wide ? 1 : 4 * PR;
     static constexpr int CapBytes = W * 4;
-    static constexpr unsigned RowMask = PR == 1 ? 0xffffu : 0x5555u;
+    __device__ static int q_of(int lane) { return Wide ? lane : (lane & 15) / PR; }
+    __device__ static int grp_of(int lane) { return Wide ? 0 : (lane >> 4) * PR + (lane & 15) % PR; }
+    __device__ static int src_of(int p) { return Wide ? 0 : (p / PR) * 16 + p % PR; }   // lane q = 0 of pair p
+    // the left / upper neighbour's value one step back (0 = -inf past the band's edge)
+    __device__ static unsigned shr(unsigned v) {
+        if constexpr (Wide) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);   // wave_shr:1
+        else return row_shr<PR>(v);
+    }
+    __device__ static unsigned shl(unsigned v) {
+        if constexpr (Wide) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);   // wave_shl:1
+        else return row_shl<PR>(v);
+    }
 };
 constexpr int kBK = 64;               // tau = t - dlo + kBK: >= 0 and even
-constexpr int kAPad = 32;             // amplicon codes: index i + kAPad, i in [-17, La + 48]
-constexpr int kJPad = 95;             // pair codes: index j + kJPad, j in [-48, La + 80]; j = 1 is 4-aligned
+constexpr int kAPad = 80;             // amplicon codes: index i + kAPad, i in [-17, La + 48] (wide level: [-66, La + 102])
+constexpr int kJPad = 95;             // pair codes: index j + kJPad, j in [-48, La + 80] (wide: [-66, La + 196]); j = 1 is 4-aligned
 constexpr int kPadCode = 5;           // lut6: A T G C N pad
 constexpr int kTabRows = NCODE;       // amplicon rows: every EDNAFULL code (IUPAC too) + pad/unknown
 constexpr int kTabBytes = 2448;       // [17][36] packed scores
 constexpr int kHdrBytes = 48;         // {tau0, dlo, flags, -}, {ra, rb, LbA, LbB}, {offA, offB}
 constexpr int kPairInactive = 4;      // header flag: the pair was not filled (walk: empty / fallback)
 
-__host__ __device__ inline int band_acd_elems(int La) { return La + kAPad + 64; }
-__host__ __device__ inline int band_pcs(int La) { return align16(La + kJPad + 96); }
+__host__ __device__ inline int band_acd_elems(int La) { return La + kAPad + 112; }
+__host__ __device__ inline int band_pcs(int La, int W) { return align16(La + kJPad + (W > 32 ? 208 : 96)); }
 
 }  // namespace
 
-__host__ __device__ inline int band_words(int La, int Lb_max) {
-    const int Lbm = Lb_max < La + kBandDiags - 1 ? Lb_max : La + kBandDiags - 1;
+// reads longer than La + W - 1 never enter a level of W diagonals (KernelArgs::band_lb_cap)
+__host__ __device__ inline int band_words(int La, int Lb_max, int W = kBandDiags) {
+    const int Lbm = Lb_max < La + W - 1 ? Lb_max : La + W - 1;
     return (((La + Lbm + 80) / 4 + 2) + 3) & ~3;   // column length: whole dwordx4 of the walk
 }
 __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W) {
-    return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max) * (W / 2) * 4 + 255) & ~(int64_t)255;
+    return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max, W > kBandDiags ? W : kBandDiags) * (W / 2) * 4 +
+            255) & ~(int64_t)255;
 }
 
 // Sort key of every read: its length bucket, or cap + 2 for a read identical to the
@@ -593,10 +609,15 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
 // Virtual DP list of the traceback pass: band_order[0, *band_count) then (diagonal pass
 // on, separate launches) tile_list[0, *tile_count) -- the list-A reads the diagonal pass
 // handed on.  (Merged launch, a.tile_to_redo: those go to the next level instead.)
+// The wide level (a.band_from_work) reads the exact kernel's work list instead: the reads the
+// narrower levels gave up on, then (direct hand-off) the first level's redo list; there
+// a.band_count = a.work_count.
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
+    if (a.band_from_work) return exact_work_count(a);
     return (long long)*a.band_count + (a.tile_count && !a.tile_to_redo ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
+    if (a.band_from_work) return k < nb ? a.work_list[k] : (long long)a.redo_list[k - nb];
     return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
 }
 
@@ -612,18 +633,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
-    if (W == kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
+    if (W == kBandDiags && redo_direct_taken(a)) return;   // second level skipped: its reads go to the wide level
+    if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
-    const int q = (lane & 15) / G::PR, grp = (lane >> 4) * G::PR + (lane & 15) % G::PR;
+    const int q = G::q_of(lane), grp = G::grp_of(lane);
     const unsigned NEG2 = 0u;                    // -inf in the kBias16 domain
     const unsigned OE2 = pk(O - E, O - E);
 
     uint32_t* tab = (uint32_t*)smem;
     uint16_t* acd = (uint16_t*)(smem + kTabBytes);
-    const int PCS = band_pcs(La);
+    const int PCS = band_pcs(La, W);
     unsigned char* pcd_wave = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wave * kBPW * PCS;
     unsigned char* pcd = pcd_wave + grp * PCS;
     unsigned char* lut6 = smem + kTabBytes + align16(2 * band_acd_elems(La)) + wpb * kBPW * PCS;
@@ -712,7 +733,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
 #pragma unroll
             for (int pp = 0; pp < kSub; ++pp) {
                 const int p = p0 + pp;
-                const int src = (p / G::PR) * 16 + p % G::PR;   // lane q = 0 of pair p
+                const int src = G::src_of(p);   // lane q = 0 of pair p
                 const unsigned oAl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offA, src);
                 const unsigned oAh = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(offA >> 32), src);
                 const unsigned oBl = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)offB, src);
@@ -838,14 +859,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
             unsigned X, Y, d1 = 0u, d2 = 0u;
             if constexpr (P == 0) {
                 // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
-                const unsigned Ml = row_shr<G::PR>(MoP), Xl = row_shr<G::PR>(XP);
+                const unsigned Ml = G::shr(MoP), Xl = G::shr(XP);
                 X = max2(Ml, Xl);
                 if constexpr (TB) d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
                 Y = max2(MoP, YP);
                 if constexpr (TB) d1 = sub2(YP, MoP);    // sign: Y opens
             } else {
                 // up = lane q+1's d0 one step back; left = own diagonal d0
-                const unsigned Mu = row_shl<G::PR>(MoP), Yu = row_shl<G::PR>(YP);
+                const unsigned Mu = G::shl(MoP), Yu = G::shl(YP);
                 Y = max2(Mu, Yu);
                 if constexpr (TB) d1 = sub2(Yu, Mu);
                 X = max2(MoP, XP);
@@ -1314,14 +1335,16 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
 }
 
 // W < kBandDiags: a first level; reads it cannot certify go to the redo list of the
-// next (wider) level.  W = kBandDiags: they go to the exact int32 kernel.
+// next (wider) level.  W >= kBandDiags: they go to the fallback list (W = kBandDiags: the
+// wide level's input; the wide level: the exact int32 kernel's).
 template <int W>
 __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if (redo_direct_taken(a)) return;   // second level skipped: its reads go to the exact kernel
-    if (W == kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
+    if (W == kBandDiags && redo_direct_taken(a)) return;   // second level skipped: its reads go to the wide level
+    if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
+    constexpr int CW = W > 64 ? W / 64 : 1;   // captures (band diagonals) per lane
     const int La = a.La, E = a.gap_extend;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wpb = blockDim.x >> 6;
     // Reads handed on (next level's redo list, or the exact kernel's list) wait in a
@@ -1390,13 +1413,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     const long long kstep = (long long)gridDim.x * wpb;
     auto region_of = [&](long long k) { return a.band_region + ((k >> 1) - a.band_pair_lo) * a.band_stride; };
     int4 n0 = make_int4(0, 0, 0, 0), n1 = n0, n2 = n0;
-    unsigned ncw = 0u;
+    unsigned ncw[CW];
     auto prefetch = [&](long long k) {
         const unsigned char* rg = region_of(k);
         n0 = ((const int4*)rg)[0];
         n1 = ((const int4*)rg)[1];
         n2 = ((const int4*)rg)[2];
-        ncw = lane < W ? ((const unsigned*)(rg + kHdrBytes))[lane] : 0u;
+#pragma unroll
+        for (int c = 0; c < CW; ++c) ncw[c] = lane + 64 * c < W ? ((const unsigned*)(rg + kHdrBytes))[lane + 64 * c] : 0u;
     };
     long long k = klo + (long long)blockIdx.x * wpb + wave;
     if (k < khi) prefetch(k);
@@ -1406,7 +1430,9 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
     };
     for (; k < khi; k += kstep) {
         const int4 hdr = uni(n0), hr = uni(n1), ho = uni(n2);
-        const unsigned cw = ncw;
+        unsigned cw[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) cw[c] = ncw[c];
         if (k + kstep < khi) prefetch(k + kstep);
         const int h = (int)(k & 1);
         const long long rd = h ? hr.y : hr.x;
@@ -1442,15 +1468,18 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         const int tau0 = hdr.x;
         // start cell: the last cell of each band diagonal is on the last row or column
         unsigned k32 = 0u;
-        if (lane < W) {
-            const int d = dlo + lane;
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            if (lane + 64 * c >= W) continue;
+            const int d = dlo + lane + 64 * c;
             const int iend = La < Lb - d ? La : Lb - d;
             const int ilo = 1 - d > 1 ? 1 - d : 1;
             if (iend >= ilo) {
-                const int v = half(cw, h) - kBias16 - E * (2 * iend + d);
+                const int v = half(cw[c], h) - kBias16 - E * (2 * iend + d);
                 const int jend = iend + d;
-                k32 = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
-                      : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
+                const unsigned kk = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
+                                    : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
+                k32 = kk > k32 ? kk : k32;
             }
         }
         int score, ei, ej;
@@ -1555,6 +1584,12 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         }
         lds_fence();
     }
+    if constexpr (W > kBandDiags) {
+        // the wide level's list entries past its region's capacity: straight to the exact kernel
+        const long long nb = (long long)*a.band_count;
+        for (long long k2 = khi + (long long)blockIdx.x * wpb + wave; k2 < count; k2 += kstep)
+            give_up(k2, band_list_read(a, k2, nb), false);
+    }
     if (redo_n) flush_redo();
     if (fb_n) flush_fb();
 }
@@ -1635,22 +1670,26 @@ hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch
 
 // ---- host-side helpers -------------------------------------------------------
 int band_fill_lds_bytes(int La, int wpb, int W) {
-    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * (W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW) * band_pcs(La) +
-           256 + wpb * 1024;
+    const int pw = W == 16 ? BandGeo<16>::PW : W == 32 ? BandGeo<32>::PW : BandGeo<kWideDiags>::PW;
+    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * pw * band_pcs(La, W) + 256 + wpb * 1024;
 }
 int band_walk_lds_bytes(int La, int wpb, int lb_max) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max); }
-int band_region_words(int La, int Lb_max) { return band_words(La, Lb_max); }
+int band_region_words(int La, int Lb_max, int W) { return band_words(La, Lb_max, W > kBandDiags ? W : kBandDiags); }
 int64_t band_region_bytes(int La, int Lb_max, int W) { return band_region_stride(La, Lb_max, W); }
 bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb, dlo); }
 
 hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
                           int* walk_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        fill_blocks, W == 16 ? (const void*)nw_band_fill<16, 1> : (const void*)nw_band_fill<32, 1>, 64 * fill_wpb,
-        fill_lds);
+        fill_blocks,
+        W == 16 ? (const void*)nw_band_fill<16, 1>
+                : (W == 32 ? (const void*)nw_band_fill<32, 1> : (const void*)nw_band_fill<kWideDiags, 1>),
+        64 * fill_wpb, fill_lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        walk_blocks, W == 16 ? (const void*)nw_band_walk<16> : (const void*)nw_band_walk<32>, 64 * walk_wpb, walk_lds);
+        walk_blocks,
+        W == 16 ? (const void*)nw_band_walk<16> : (W == 32 ? (const void*)nw_band_walk<32> : (const void*)nw_band_walk<kWideDiags>),
+        64 * walk_wpb, walk_lds);
 }
 
 // classify (exact copies, sort keys) then the segment sort; a.band_count receives the
@@ -1679,15 +1718,19 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
         hipLaunchKernelGGL((nw_band_fill<32, 2>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else if (W == 16)
         hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
-    else
+    else if (W == 32)
         hipLaunchKernelGGL((nw_band_fill<32, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL((nw_band_fill<kWideDiags, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
     if (W == 16)
         hipLaunchKernelGGL(nw_band_walk<16>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
-    else
+    else if (W == 32)
         hipLaunchKernelGGL(nw_band_walk<32>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL(nw_band_walk<kWideDiags>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     return hipGetLastError();
 }
 

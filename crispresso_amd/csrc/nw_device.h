@@ -82,6 +82,7 @@ struct KernelArgs {
     // then the redo list): a few hundred reads cost the exact kernel's latency once, less
     // than the second level's fill + walk ahead of it.  Decided on the device per chunk.
     int32_t redo_direct;
+    int32_t band_from_work;    // the wide level: the band list is the exact kernel's work list (exact_work_read)
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
     // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
     // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
@@ -152,9 +153,10 @@ enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // band pair header: re
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
 constexpr int kBandDiags = 32;
+constexpr int kWideDiags = 128;   // the wide level: the narrower levels' give-ups before the exact kernel
 int band_fill_lds_bytes(int La, int wpb, int W);
 int band_walk_lds_bytes(int La, int wpb, int lb_max);
-int band_region_words(int La, int Lb_max);
+int band_region_words(int La, int Lb_max, int W = kBandDiags);
 int64_t band_region_bytes(int La, int Lb_max, int W);
 bool band_pair_geometry(int La, int Lb, int* dlo);
 hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int walk_lds, int* fill_blocks,
@@ -169,8 +171,19 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
 hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
 // pbyte0, 4-aligned) -> dst[pos - bias] bytes (A C T G), then exceptions [e0, e1)
+// With `lens` (a chunk's length segment, LenSeg below): the same launch also rebuilds the
+// chunk's offsets d_off[r_lo .. r_hi] (call-indexed, r_hi inclusive) from its reads' uint16
+// lengths and every 1024th offset (the 8-B offsets no longer cross PCIe).
+struct LenSeg {
+    const uint8_t* seg = nullptr;   // device: [ngroups] int64 group bases, then uint16 lengths from read 1024 * g0
+    int64_t g0 = 0, ngroups = 0;    // groups g0 .. g0 + ngroups - 1 (group g: reads [1024 g, 1024 g + 1024))
+    int64_t r_lo = 0, r_hi = 0;     // offsets written: reads r_lo .. r_hi
+    int64_t* d_off = nullptr;
+};
+constexpr int kLenGroup = 1024;
 hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1, const int64_t* exc_pos,
-                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s);
+                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s,
+                         const LenSeg* lens = nullptr);
 // the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
 // nmax >= the number of sorted positions (grid size)
 hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s);
@@ -193,13 +206,13 @@ hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_ld
 // look-back cut off); running over the call: [4] exact-kernel reads, [5] second band level
 // reads of two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the
 // second level alone, [8] reads of the diagonal passes' lists A, [9] the reads those passes
-// handed to the traceback pass (OpsCounts: the device counters of the chunk's kernels);
+// handed to the traceback pass, [10] reads that reached the exact kernel (after the wide level) (OpsCounts: the device counters of the chunk's kernels);
 // [kOpsCtl], [kOpsCtl + 1]: the running base, read from [kOpsCtl + parity] and written to
 // the other (chunk k: parity k & 1).
 // status: band_lookback_words(n) look-back words; epoch: new per launch.  opsctl: the
 // kernels' flags.  hctl: pinned host copy of ctl[0 .. kOpsCtl) written by the launch (or null).
 constexpr int kOpsBlockReads = 1024;
-constexpr int kOpsCtl = 10;
+constexpr int kOpsCtl = 11;
 constexpr int kOpsCtlAll = kOpsCtl + 2;
 struct OpsCounts {
     const int32_t* fallback;   // [0]: exact-kernel reads of the chunk, [3]: look-back error flag
@@ -211,6 +224,7 @@ struct OpsCounts {
     int32_t prio;              // raise the compaction's issue priority (KernelArgs::tail_prio)
     const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
     const int32_t* handed;     // ... and the reads it handed on
+    const int32_t* exact;      // the wide level's give-ups: the exact kernel's reads (null: no wide level)
 };
 // The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
 // straight into the caller's page-locked buffers (no copies and no host round trip after it).

@@ -68,7 +68,8 @@ struct Profile {
 // kernel, compaction) overlaps the next chunk's bulk kernels.
 struct Scratch {
     DevBuf<uint8_t> d_tb;              // exact kernel: traceback slabs when they do not fit LDS
-    DevBuf<int64_t> d_fallback;        // reads re-run with full traceback storage
+    DevBuf<int64_t> d_fallback;        // reads the 16 / 32-diagonal levels gave up on (the wide level's input)
+    DevBuf<int64_t> d_fallback2;       // reads the wide level gave up on (the exact kernel's list)
     DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
@@ -79,7 +80,7 @@ struct Scratch {
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
     DevBuf<int32_t> d_nops, d_opsctl;
     void release() {
-        d_tb.release(); d_fallback.release(); d_fallback_count.release(); d_redo.release();
+        d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
         d_tile.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
@@ -87,7 +88,8 @@ struct Scratch {
     }
 };
 constexpr int kScratchSets = 3;
-constexpr int64_t kDiagMinChunks = 12;   // pipelined calls of fewer chunks run without the diagonal pass
+constexpr int64_t kDiagMinChunks = 12;
+constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level (region capacity)   // pipelined calls of fewer chunks run without the diagonal pass
 
 struct nw_ctx {
     int device = 0;
@@ -131,6 +133,10 @@ struct nw_ctx {
     DevBuf<uint8_t> d_packed, d_exc_byte;   // 2-bit packed input (nw_align_ops_packed) and its exceptions
     DevBuf<int64_t> d_exc_pos;
     DevBuf<int64_t> d_offsets;
+    // packed calls: the chunks' length segments (nw::LenSeg), pinned on the host and in HBM
+    DevBuf<uint8_t> d_lens;
+    uint8_t* h_lens = nullptr;
+    int64_t h_lens_cap = 0;
     DevBuf<uint8_t> d_out;
     DevBuf<nw::Stat> d_stats;
     nw::LaunchCfg cfg{};              // full-storage kernel
@@ -138,6 +144,11 @@ struct nw_ctx {
     bool use_diag = false;
     nw::LaunchCfg diag_fill{}, diag_walk{};          // 32-diagonal level (the certificate's last resort)
     nw::LaunchCfg diag16_fill{}, diag16_walk{};      // 16-diagonal first level (0 grid: off)
+    // the wide level (kWideDiags diagonals, one read pair per wavefront) over what the 16 / 32
+    // levels gave up on, before the exact kernel (0 grid: off)
+    nw::LaunchCfg wide_fill{}, wide_walk{};
+    int64_t wide_pairs = 0, wide_stride = 0;
+    int wide_words = 0, wide_lb_cap = 0;
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
     DevBuf<uint32_t> d_btab;
     DevBuf<uint32_t> d_sub16;         // exact multi-wave kernel's score rows
@@ -149,6 +160,7 @@ struct nw_ctx {
     bool diag_off = false;            // this chunk: no diagonal pass (ops_call's adaptive choice)
     bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
     bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
+    bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -175,6 +187,7 @@ struct nw_ctx {
     bool resident_ok = false;          // d_reads / d_offsets hold the last nw_align_ops batch
     int64_t resident_n = 0, resident_lo = 0, resident_hi = 0;
     int64_t call_counts[4] = {0, 0, 0, 0};
+    int64_t call_exact = 0;            // reads of the last call that reached the exact kernel
     int64_t ops_h2d_bytes = 0, ops_d2h_bytes = 0;
 };
 
@@ -471,13 +484,22 @@ int configure(nw_ctx* c) {
         c->diag_lb_cap = La + nw::kBandDiags - 1;
         c->diag_words = nw::band_region_words(La, c->lb_max);
         // one level: fill + walk launch configs, region stride and pairs per pass
-        auto level = [&](int W, nw::LaunchCfg& f, nw::LaunchCfg& w, int64_t& stride, int64_t& pass_pairs) -> int {
+        int wide_fill_wpb = 1, wide_walk_wpb = 2;   // CRISPR_NW_WIDE_WPB=f:w (A/Bs)
+        if (const char* e = std::getenv("CRISPR_NW_WIDE_WPB")) {
+            wide_fill_wpb = std::max(1, std::min(8, std::atoi(e)));
+            if (const char* col = std::strchr(e, ':')) wide_walk_wpb = std::max(1, std::min(8, std::atoi(col + 1)));
+        }
+        auto level = [&](int W, nw::LaunchCfg& f, nw::LaunchCfg& w, int64_t& stride, int64_t& pass_pairs,
+                         int64_t max_pairs = INT64_MAX) -> int {
             f = nw::LaunchCfg{};
             w = nw::LaunchCfg{};
             f.R = w.R = R;
             f.tb_mode = w.tb_mode = nw::TB_DIAG;
-            f.wpb = 8;
-            w.wpb = 8;
+            // the wide level aligns few reads, latency-bound: one wavefront per block (fill) and
+            // two (walk) spread them over the CUs instead of stacking 8 on a CU's 4 SIMDs
+            const bool wide = W > nw::kBandDiags;
+            f.wpb = wide ? wide_fill_wpb : 8;
+            w.wpb = wide ? wide_walk_wpb : 8;
             f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb, W);
             w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb, c->lb_max);
             int fb = 0, wb = 0;
@@ -485,9 +507,9 @@ int configure(nw_ctx* c) {
             if (nw::band_occupancy(W, f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb) != hipSuccess || fb <= 0 ||
                 wb <= 0)
                 return 0;
-            const int ppw = W == 16 ? 8 : 4;   // read pairs per wavefront
+            const int ppw = W == 16 ? 8 : (W == 32 ? 4 : 1);   // read pairs per wavefront
             stride = nw::band_region_bytes(La, c->lb_max, W);
-            pass_pairs = std::max<int64_t>(ppw, std::min<int64_t>(pairs, cap_bytes / stride));
+            pass_pairs = std::max<int64_t>(ppw, std::min<int64_t>(std::min(pairs, max_pairs), cap_bytes / stride));
             pass_pairs = (pass_pairs + ppw - 1) / ppw * ppw;
             const int64_t pp = std::min<int64_t>(std::max<int64_t>(pairs, 1), pass_pairs);
             f.grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pp + ppw - 1) / ppw + f.wpb - 1) / f.wpb,
@@ -500,9 +522,22 @@ int configure(nw_ctx* c) {
                            level(16, c->diag16_fill, c->diag16_walk, c->diag16_stride, c->diag16_pass_pairs);
         if (!use16) c->diag16_fill.grid = 0;
         if (level(32, c->diag_fill, c->diag_walk, c->diag_stride, c->diag_pass_pairs)) {
-            const int64_t rbytes = std::max(std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs) * c->diag_stride,
-                                            use16 ? std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag16_pass_pairs) *
-                                                        c->diag16_stride : 0);
+            int64_t rbytes = std::max(std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag_pass_pairs) * c->diag_stride,
+                                      use16 ? std::min<int64_t>(std::max<int64_t>(pairs, 1), c->diag16_pass_pairs) *
+                                                  c->diag16_stride : 0);
+            // the wide level: at most kWidePairs read pairs per chunk in the region (the rest of
+            // its list goes to the exact kernel); CRISPR_NW_WIDE=0: off
+            c->wide_fill.grid = 0;
+            const char* wv = std::getenv("CRISPR_NW_WIDE");
+            if (!(wv && std::atoi(wv) == 0) &&
+                level(nw::kWideDiags, c->wide_fill, c->wide_walk, c->wide_stride, c->wide_pairs, kWidePairs)) {
+                c->wide_words = nw::band_region_words(La, c->lb_max, nw::kWideDiags);
+                c->wide_lb_cap = La + nw::kWideDiags - 1;
+                rbytes = std::max(rbytes, c->wide_pairs * c->wide_stride);
+                HIP_OR_FAIL(c, c->s->d_fallback2.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            } else {
+                c->wide_fill.grid = 0;
+            }
             HIP_OR_FAIL(c, c->s->d_bregion.reserve((size_t)rbytes));
             HIP_OR_FAIL(c, c->s->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_order_a.reserve((size_t)std::max<int64_t>(c->n, 1)));
@@ -595,7 +630,7 @@ void nw_destroy(nw_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->d_arena.release(); c->d_lut.release();
     c->d_reads.release(); c->d_offsets.release(); c->d_out.release();
-    c->d_packed.release(); c->d_exc_byte.release(); c->d_exc_pos.release();
+    c->d_packed.release(); c->d_exc_byte.release(); c->d_exc_pos.release(); c->d_lens.release();
     c->d_stats.release();
     c->d_lut6.release();
     c->d_btab.release();
@@ -609,6 +644,7 @@ void nw_destroy(nw_ctx* c) {
     for (auto* v : {&c->ev_in, &c->ev_cs, &c->ev_ce, &c->ev_out})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->h_lens) (void)hipHostFree(c->h_lens);
     if (c->ev_h0) (void)hipEventDestroy(c->ev_h0);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->s_in) (void)hipStreamDestroy(c->s_in);
@@ -734,7 +770,12 @@ namespace {
 // latency of a few reads), the rest, if any, to the one-wave kernel (throughput when
 // many reads need the exact DP, e.g. an unrelated amplicon's HDR pass).
 hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
-    if (c->exact_grid <= 0) return nw::launch(a, c->cfg, c->cs);
+    // a work list expected short (ops_call: the recent chunks sent few reads to the exact
+    // kernel): a small grid, so that the launch's empty blocks do not wait behind the other
+    // chunks' kernels for LDS (a full grid of early-exiting blocks measured ~20 us per chunk)
+    nw::LaunchCfg cfg = c->cfg;
+    if (a.work_list && c->exact_small) cfg.grid = std::min(cfg.grid, std::max(1, c->num_cus / 2));
+    if (c->exact_grid <= 0) return nw::launch(a, cfg, c->cs);
     hipError_t e = nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, true, c->cs);
     if (e != hipSuccess) return e;
     nw::KernelArgs rest = a;
@@ -886,10 +927,37 @@ int launch_range(nw_ctx* c, int64_t base) {
             }
         }
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
-        a.work_list = a.fallback_list;   // exact int32 kernel on what the band could not certify
+        a.work_list = a.fallback_list;   // what the 16 / 32 levels could not certify
         a.work_count = c->s->d_fallback_count.p;
         a.redo_direct = direct;
-        HIP_OR_FAIL(c, launch_work(c, a));
+        if (c->wide_fill.grid > 0 && !only16) {
+            // the wide level over that list (and, direct hand-off, the first level's redo list):
+            // one read pair per wavefront, 128 diagonals: a few fill + walk launches of ~20 us
+            // latency where the exact kernel took ~80 us per chunk; its give-ups -> the exact kernel
+            nw::KernelArgs aw = a;
+            aw.band_from_work = 1;
+            aw.band_count = a.work_count;
+            aw.redo_flags = nullptr;
+            aw.order_a = nullptr;
+            aw.tile_list = nullptr;
+            aw.tile_count = nullptr;
+            aw.tile_to_redo = 0;
+            aw.band_last = 0;
+            aw.band_stride = c->wide_stride;
+            aw.band_words = c->wide_words;
+            aw.band_lb_cap = c->wide_lb_cap;
+            aw.band_pair_lo = 0;
+            aw.band_pair_hi = c->wide_pairs;
+            aw.fallback_list = c->s->d_fallback2.p + base;
+            aw.fallback_count = c->s->d_fallback_count.p + 6;   // zeroed by nw_band_classify
+            HIP_OR_FAIL(c, nw::launch_band(nw::kWideDiags, aw, c->wide_fill, c->wide_walk, c->cs, nullptr));
+            a.work_list = aw.fallback_list;
+            a.work_count = aw.fallback_count;
+            a.redo_direct = 0;
+        }
+        // CRISPR_NW_SKIP_EXACT=1: diagnostics only (wrong results): the chain without the exact kernel
+        const char* sk = std::getenv("CRISPR_NW_SKIP_EXACT");
+        if (!(sk && std::atoi(sk) == 1)) HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
     HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs));
@@ -956,6 +1024,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
             cnt.list_a = c->s->d_fallback_count.p + 4;
             cnt.handed = c->s->d_fallback_count.p + 5;
         }
+        if (c->wide_fill.grid > 0) cnt.exact = c->s->d_fallback_count.p + 6;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
@@ -1237,6 +1306,7 @@ int nw_align_multi(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int3
     HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * stride_all));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)));
+    HIP_OR_FAIL(c, c->s->d_fallback2.reserve((size_t)std::max<int64_t>(n, 1)));   // indexed like d_fallback (+ group base)
     if (!sreads.empty())
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, sreads.data(), sreads.size(), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, soff.data(), sizeof(int64_t) * soff.size(), hipMemcpyHostToDevice, c->stream));
@@ -1376,13 +1446,16 @@ struct HostTimer {
 // geometry): a pooled call configures every group once up front and restores these
 // per chunk instead of re-running configure (its occupancy queries are host API calls).
 struct CfgState {
-    nw::LaunchCfg cfg, diag_fill, diag_walk, diag16_fill, diag16_walk;
+    nw::LaunchCfg cfg, diag_fill, diag_walk, diag16_fill, diag16_walk, wide_fill, wide_walk;
+    int64_t wide_pairs, wide_stride;
+    int wide_words, wide_lb_cap;
     bool use_diag, exact_tb_lds, exact_full;
     int exact_grid, exact_lds, diag_words, diag_lb_cap;
     int64_t exact_slab, diag16_pass_pairs, diag16_stride, diag_pass_pairs, diag_stride, stride;
 };
 CfgState save_cfg(const nw_ctx* c) {
-    return CfgState{c->cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->use_diag, c->exact_tb_lds,
+    return CfgState{c->cfg, c->diag_fill, c->diag_walk, c->diag16_fill, c->diag16_walk, c->wide_fill, c->wide_walk,
+                    c->wide_pairs, c->wide_stride, c->wide_words, c->wide_lb_cap, c->use_diag, c->exact_tb_lds,
                     c->exact_full, c->exact_grid, c->exact_lds, c->diag_words, c->diag_lb_cap,
                     c->exact_slab, c->diag16_pass_pairs, c->diag16_stride, c->diag_pass_pairs, c->diag_stride,
                     c->stride};
@@ -1394,6 +1467,8 @@ void load_cfg(nw_ctx* c, const CfgState& st) {
     c->diag_words = st.diag_words; c->diag_lb_cap = st.diag_lb_cap;
     c->exact_slab = st.exact_slab; c->diag16_pass_pairs = st.diag16_pass_pairs; c->diag16_stride = st.diag16_stride;
     c->diag_pass_pairs = st.diag_pass_pairs; c->diag_stride = st.diag_stride; c->stride = st.stride;
+    c->wide_fill = st.wide_fill; c->wide_walk = st.wide_walk; c->wide_pairs = st.wide_pairs;
+    c->wide_stride = st.wide_stride; c->wide_words = st.wide_words; c->wide_lb_cap = st.wide_lb_cap;
 }
 
 // 2-bit packed batch (nw_align_ops_packed): bases by batch position, exceptions ascending.
@@ -1508,6 +1583,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->skip16 = false;
         c->diag_off = false;
         c->diag_tail = false;
+        c->exact_small = false;
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1551,6 +1627,95 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // pace of the middle chunks.  Diagnostics only.
     const char* up_env = std::getenv("CRISPR_NW_UPLOAD");
     const int upload_mode = up_env ? std::atoi(up_env) : 0;
+    // Packed input: the reads' offsets cross as uint16 lengths plus every kLenGroup-th offset
+    // (a chunk's length segment: 2 B per read instead of 8, 70.5 -> 64.5 MB per 1M C2 reads);
+    // the chunk's unpack launch rebuilds its int64 offsets.  The host writes a chunk's segment
+    // (one pass over its offsets on the pool, which also finds the longest / shortest read)
+    // once the first chunk's bases are queued.  A chunk with a read longer than 65535 sends its
+    // int64 offsets instead.  CRISPR_NW_LENS=1: on (measured slower: the host pass now precedes the
+    // later uploads, C2 2.31 vs 2.22 ms, C5 23.2 vs 22.0 ms).
+    const char* lens_env = std::getenv("CRISPR_NW_LENS");
+    const bool lens_on = pk && upload && n > 0 && upload_mode == 0 && lens_env && std::atoi(lens_env) == 1;
+    std::vector<nw::LenSeg> lseg((size_t)(lens_on ? nchunks : 0));
+    std::vector<int64_t> lseg_off((size_t)(lens_on ? nchunks + 1 : 0), 0);
+    int64_t mx = 1, mn = 0;
+    if (lens_on) {
+        for (int64_t k = 0; k < nchunks; ++k) {
+            const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
+            const int64_t g0 = lo / nw::kLenGroup, ng = hi / nw::kLenGroup - g0 + 1;
+            lseg_off[(size_t)k + 1] = lseg_off[(size_t)k] + ((8 * ng + 2 * (hi - g0 * nw::kLenGroup) + 15) & ~(int64_t)15);
+        }
+        const int64_t need = lseg_off[(size_t)nchunks] + 16;
+        if (need > c->h_lens_cap) {
+            if (c->h_lens) (void)hipHostFree(c->h_lens);
+            c->h_lens = nullptr;
+            c->h_lens_cap = 0;
+            HIP_OR_FAIL(c, hipHostMalloc((void**)&c->h_lens, (size_t)need, hipHostMallocDefault));
+            c->h_lens_cap = need;
+        }
+        if (c->d_lens.reserve((size_t)need) != hipSuccess)
+            return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
+    }
+    nw_host::Pool& pool = nw_host::Pool::get();
+    // every chunk's length segment in one pass over the caller's offsets on the pool (run once
+    // the first chunk's bases are queued): group bases, then the lengths of reads [g0 *
+    // kLenGroup, hi); a chunk with a read longer than 65535 (or negative: the scan below
+    // reports it) sends its int64 offsets instead
+    std::vector<char> lens_bad((size_t)(lens_on ? nchunks : 0), 0);
+    auto write_lens = [&]() {
+        auto seg_of = [&](int64_t k, int64_t* g0, int64_t* ng, uint16_t** ln) {
+            *g0 = chunks[(size_t)k].lo / nw::kLenGroup;
+            *ng = chunks[(size_t)k].hi / nw::kLenGroup - *g0 + 1;
+            *ln = (uint16_t*)(c->h_lens + lseg_off[(size_t)k] + 8 * *ng);
+        };
+        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
+        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
+        pool.run(parts, [&](int q) {
+            int64_t a0, a1, a = 1, b = 0;
+            nw_host::Pool::range(n, parts, q, &a0, &a1);
+            // the chunk holding read a0 (chunks are in read order)
+            int64_t k = std::upper_bound(chunks.begin(), chunks.end(), a0,
+                                         [](int64_t r, const Chunk& ch) { return r < ch.hi; }) - chunks.begin();
+            for (int64_t r = a0; r < a1 && k < nchunks; ++k) {
+                int64_t g0, ng;
+                uint16_t* ln;
+                seg_of(k, &g0, &ng, &ln);
+                const int64_t e = std::min(a1, chunks[(size_t)k].hi), rb = g0 * nw::kLenGroup;
+                int64_t ka = 1, kb = 0;
+                for (r = std::max(r, chunks[(size_t)k].lo); r < e; ++r) {
+                    const int64_t len = offsets[r + 1] - offsets[r];
+                    ka = len > ka ? len : ka;
+                    kb = len < kb ? len : kb;
+                    ln[r - rb] = (uint16_t)len;
+                }
+                if (kb < 0 || ka > 65535) lens_bad[(size_t)k] = 1;   // set-only: racing parts write the same value
+                a = std::max(a, ka);
+                b = std::min(b, kb);
+            }
+            pmx[(size_t)q] = a;
+            pmn[(size_t)q] = b;
+        });
+        for (int q = 0; q < parts; ++q) {
+            mx = std::max(mx, pmx[(size_t)q]);
+            mn = std::min(mn, pmn[(size_t)q]);
+        }
+        for (int64_t k = 0; k < nchunks; ++k) {
+            int64_t g0, ng;
+            uint16_t* ln;
+            seg_of(k, &g0, &ng, &ln);
+            int64_t* gb = (int64_t*)(c->h_lens + lseg_off[(size_t)k]);
+            for (int64_t g = 0; g < ng; ++g) gb[g] = offsets[(g0 + g) * nw::kLenGroup];
+            // the group's reads before the chunk (the previous chunks' lengths)
+            const int64_t lo = chunks[(size_t)k].lo;
+            for (int64_t r = g0 * nw::kLenGroup; r < lo; ++r) {
+                const int64_t len = offsets[r + 1] - offsets[r];
+                if (len < 0 || len > 65535) lens_bad[(size_t)k] = 1;
+                ln[r - g0 * nw::kLenGroup] = (uint16_t)len;
+            }
+            if (!lens_bad[(size_t)k]) lseg[(size_t)k] = nw::LenSeg{c->d_lens.p + lseg_off[(size_t)k], g0, ng, lo,
+                                                                   chunks[(size_t)k].hi, c->d_offsets.p};
+        }
+    };
     for (int64_t k = 0; upload && k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
@@ -1578,7 +1743,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                           c->s_in));
             h2d_bytes += b1 - b0;
         }
-        if (!offs_apart) {
+        if (lens_on && k == 0) write_lens();
+        if (lens_on && !lens_bad[(size_t)k]) {
+            const int64_t bytes = lseg_off[(size_t)k + 1] - lseg_off[(size_t)k];
+            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + lseg_off[(size_t)k], c->h_lens + lseg_off[(size_t)k], (size_t)bytes,
+                                          hipMemcpyHostToDevice, c->s_in));
+            h2d_bytes += bytes;
+        } else if (!offs_apart) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
                                           hipMemcpyHostToDevice, c->s_in));
             h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
@@ -1587,10 +1758,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     }
     ht.lap(3);
     // longest / shortest read: a vectorisable pass, split over the host pool for large
-    // batches (memory-bound; the exact read is found only on error)
-    int64_t mx = 1, mn = 0;
-    {
-        nw_host::Pool& pool = nw_host::Pool::get();
+    // batches (memory-bound; the exact read is found only on error); the length segments'
+    // pass found them already
+    if (!lens_on) {
         const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
         std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
         pool.run(parts, [&](int q) {
@@ -1684,7 +1854,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         if (!rc) rc = ops_reserve(c, chunk, n);
-        if (!rc && c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+        // the fallback lists are indexed by the call's read (d_fallback + chunk base)
+        if (!rc && (c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess ||
+                    c->s->d_fallback2.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess))
             rc = fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n);
     }
     ht.lap(1);
@@ -1696,20 +1868,24 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
     std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
     c->diag_off = false;
-    // The diagonal pass saves GPU time but adds a launch to every chunk's chain.  A short
-    // pipeline (the 1M-read call: 7 chunks) waits on its chains' latency and runs without it
-    // (C2 2.26 vs 2.29 ms per call); a long one (the 12.5M-read C4 shard: 50 chunks) is
-    // throughput-bound (18.1 vs 19.0 ms with it); its last chunks, whose latency the call
-    // waits for at its end, run without it (CRISPR_NW_DIAG_TAIL chunks, default 2).
-    // CRISPR_NW_DIAGPASS=1 / 0: on / off for every chunk.
-    int64_t diag_tail = 2;
+    // The diagonal pass saves GPU time but adds a launch to every chunk's chain.  The call's
+    // last chunk, whose latency the call waits for at its end, runs without it
+    // (CRISPR_NW_DIAG_TAIL chunks, default 1); every other chunk of an uploading call with it
+    // (with the wide level taking the exact kernel's ~80 us off each chain, the 1M-read C2 call
+    // measured 2.17 ms vs 2.26 without the pass in its 7 chunks).  A resident pass (the C3 HDR
+    // pass, whose list-A reads the pass mostly hands on) keeps round 3's rule: calls of fewer
+    // than kDiagMinChunks chunks run without it.  CRISPR_NW_DIAGPASS=1 / 0: on / off for every
+    // chunk; CRISPR_NW_DIAG_MIN: that chunk threshold (A/Bs).
+    int64_t diag_tail = 1;
     if (const char* e = std::getenv("CRISPR_NW_DIAG_TAIL")) diag_tail = std::max(0, std::atoi(e));
     if (nchunks < 2) diag_tail = 0;
     {
         const char* e = std::getenv("CRISPR_NW_DIAGPASS");
         const bool forced_on = e && std::atoi(e) == 1;
         if (forced_on) diag_tail = 0;
-        else if (nchunks > 1 && nchunks < kDiagMinChunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
+        int64_t min_chunks = upload ? 2 : kDiagMinChunks;
+        if (const char* m = std::getenv("CRISPR_NW_DIAG_MIN")) min_chunks = std::max(0, std::atoi(m));
+        if (!forced_on && nchunks > 1 && nchunks < min_chunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
     }
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
@@ -1802,8 +1978,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             const int64_t b0 = offsets[lo], b1 = offsets[hi];
             const int64_t e0 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b0) - pk->exc_pos;
             const int64_t e1 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b1) - pk->exc_pos;
+            const nw::LenSeg* ls = lens_on && lseg[(size_t)k].seg ? &lseg[(size_t)k] : nullptr;
             HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, b0, b1, c->d_exc_pos.p, c->d_exc_byte.p,
-                                             e0, e1, c->d_reads.p, c->reads_bias, c->cs));
+                                             e0, e1, c->d_reads.p, c->reads_bias, c->cs, ls));
         }
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         any_diag = any_diag || c->use_diag;
@@ -1833,6 +2010,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
+        // the exact kernel's grid: small while the newest chunk read back sent it few reads
+        // (after the wide level it gets the rare read no band certifies)
+        c->exact_small = true;
+        if (k >= lag + 1) {
+            const int64_t j = k - lag - 1;
+            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
+            c->exact_small = h[10] - (j > 0 ? c->h_ctl[nw::kOpsCtl * (j - 1) + 10] : 0) < 256;
+        }
         // the last chunks of a call run without the diagonal pass: their chains' latency (not
         // the GPU's throughput) is what the call waits for at its end, and the pass adds a
         // launch to the chain (CRISPR_NW_DIAG_TAIL chunks, default 2)
@@ -1904,6 +2089,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->call_counts[1] = two ? h[6] - h[7] : 0;                // first level: two-level chunks' DP reads
         c->call_counts[2] = any_diag ? (two ? h[5] + h[7] : h[6]) : 0;
         c->call_counts[3] = h[4];
+        c->call_exact = h[10];
     }
     c->call_done = true;
     // device times: the upload span on s_in, the chunks' compute spans summed
@@ -2171,8 +2357,19 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
     // a skipped second level (KernelArgs::redo_direct) sent its reads to the exact kernel
     const bool direct = two && c->redo_direct > 0 && fb[2] <= c->redo_direct;
     counts4[2] = two ? (direct ? 0 : fb[2]) : need;   // second level (32 diagonals)
-    counts4[3] = fb[0] + (direct ? fb[2] : 0);        // exact int32 kernel
+    counts4[3] = fb[0] + (direct ? fb[2] : 0);        // the 16 / 32 levels' give-ups (wide level + exact kernel)
     return NW_OK;
+}
+
+int64_t nw_batch_exact_reads(nw_ctx* c) {
+    if (c && c->call_done) return c->call_exact;
+    if (!c || !c->ran) return -1;
+    if (!c->use_diag || c->wide_fill.grid <= 0) return nw_batch_fallbacks(c);
+    (void)hipSetDevice(c->device);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    int32_t fb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return fb[6];
 }
 
 }  // extern "C"

@@ -149,6 +149,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
         if (direct) fb += *cnt.redo;
         ctl[4] += fb;
+        ctl[10] += cnt.exact ? (long long)*cnt.exact : fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
         const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0);
         ctl[6] += dp;

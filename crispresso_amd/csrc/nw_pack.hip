@@ -20,8 +20,46 @@ namespace {
 // Bases [b0, b1) (batch positions) from the packed stream (device copy starting at
 // stream byte pbyte0, a multiple of 4) into dst[pos - bias] (bias a multiple of 16).
 // Thread: 16 bases = one packed dword -> one 16-byte store (byte stores at the edges).
+// Blocks from `nub` on rebuild the chunk's offsets instead (one block per group of
+// kLenGroup reads: the group's base offset + an exclusive scan of its uint16 lengths).
 __global__ __launch_bounds__(256) void nw_unpack_kernel(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1,
-                                                        uint8_t* dst, int64_t bias) {
+                                                        uint8_t* dst, int64_t bias, unsigned nub, const LenSeg ls) {
+    if (blockIdx.x >= nub) {
+        __shared__ int64_t wsum[4];
+        const int64_t b = blockIdx.x - nub;
+        const int64_t g = ls.g0 + b;
+        const int64_t r0 = g * kLenGroup + 4 * threadIdx.x;   // this thread's 4 reads
+        const uint16_t* len = (const uint16_t*)(ls.seg + 8 * ls.ngroups) + b * kLenGroup + 4 * threadIdx.x;
+        // lengths exist for reads below r_hi only (the segment ends there)
+        uint32_t l[4];
+        if (r0 + 4 <= ls.r_hi) {
+            const uint2 w = *(const uint2*)len;
+            l[0] = w.x & 0xffffu; l[1] = w.x >> 16; l[2] = w.y & 0xffffu; l[3] = w.y >> 16;
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) l[m] = r0 + m < ls.r_hi ? len[m] : 0u;
+        }
+        const int64_t t4 = (int64_t)l[0] + l[1] + l[2] + l[3];
+        // wave inclusive scan of the 4-read sums, then the waves' totals
+        int64_t inc = t4;
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int64_t base = ((const int64_t*)ls.seg)[b] + inc - t4;
+        for (int w = 0; w < wave; ++w) base += wsum[w];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int64_t r = r0 + m;
+            if (r >= ls.r_lo && r <= ls.r_hi) ls.d_off[r] = base;
+            base += l[m];
+        }
+        return;
+    }
     const int64_t first = b0 & ~(int64_t)15;
     const int64_t i0 = first + 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
     if (i0 >= b1) return;
@@ -58,12 +96,14 @@ __global__ __launch_bounds__(256) void nw_exceptions_kernel(const int64_t* pos, 
 }  // namespace
 
 hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int64_t b1, const int64_t* exc_pos,
-                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s) {
-    if (b1 > b0) {
-        const int64_t words = (b1 - (b0 & ~(int64_t)15) + 15) / 16;
-        hipLaunchKernelGGL(nw_unpack_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, packed, pbyte0, b0,
-                           b1, dst, bias);
-    }
+                         const uint8_t* exc_byte, int64_t e0, int64_t e1, uint8_t* dst, int64_t bias, hipStream_t s,
+                         const LenSeg* lens) {
+    const int64_t words = b1 > b0 ? (b1 - (b0 & ~(int64_t)15) + 15) / 16 : 0;
+    const unsigned nub = (unsigned)((words + 255) / 256);
+    const unsigned nlb = lens ? (unsigned)lens->ngroups : 0u;
+    if (nub + nlb > 0)
+        hipLaunchKernelGGL(nw_unpack_kernel, dim3(nub + nlb), dim3(256), 0, s, packed, pbyte0, b0, b1, dst, bias, nub,
+                           lens ? *lens : LenSeg{});
     if (e1 > e0)
         hipLaunchKernelGGL(nw_exceptions_kernel, dim3((unsigned)((e1 - e0 + 255) / 256)), dim3(256), 0, s, exc_pos,
                            exc_byte, e0, e1, dst, bias);

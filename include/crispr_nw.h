@@ -137,9 +137,10 @@ int64_t nw_batch_cells(const nw_ctx* ctx);
  * int16, traceback tiles in HBM). */
 int nw_batch_geometry(const nw_ctx* ctx, int32_t* rows_per_lane, int32_t* waves_per_block,
                       int32_t* grid, int32_t* lds_bytes, int32_t* tb_mode);
-/* Reads of the last run aligned by the exact int32 kernel with full traceback
- * storage: what no band level certified, plus a skipped second level's reads
- * (nw_batch_path_counts [3]; synchronises). */
+/* Reads of the last run that the 16- and 32-diagonal band levels did not certify, plus a
+ * skipped second level's reads (nw_batch_path_counts [3]; synchronises): the 128-diagonal
+ * wide level's input; what it cannot certify either goes to the exact int32 kernel
+ * (nw_batch_exact_reads). */
 int64_t nw_batch_fallbacks(nw_ctx* ctx);
 /* Device time of the last run split by kernel (synchronises): the first band
  * level's DP fill, its traceback walk, and the rest (sort, second level, exact
@@ -195,10 +196,15 @@ int nw_align_multi_ops_packed(nw_ctx* ctx, const char* refs, const int64_t* ref_
  * 32-diagonal level, [4] the exact kernel + ops compaction.  Other paths: all in [4]. */
 int nw_batch_phase_times(nw_ctx* ctx, float* ms5);
 /* Reads of the last run by path: [0] exact copies (no DP), [1] first band level,
- * [2] second band level, [3] exact int32 kernel (synchronises).  A chunk whose first
- * level gave up on at most 1024 reads skips the second level (direct
- * hand-off; CRISPR_NW_DIRECT=0 disables it): those reads count under [3]. */
+ * [2] second band level, [3] the 128-diagonal wide level and the exact int32 kernel after
+ * it (synchronises).  A chunk whose first level gave up on at most 1024 reads skips the
+ * second level (direct hand-off; CRISPR_NW_DIRECT=0 disables it): those
+ * reads count under [3]. */
 int nw_batch_path_counts(nw_ctx* ctx, int64_t* counts4);
+/* Of the reads in nw_batch_path_counts [3] (what the 16- and 32-diagonal levels did not
+ * certify), those the 128-diagonal wide level did not certify either: the reads the exact
+ * int32 kernel aligned (synchronises; -1 when nothing ran). */
+int64_t nw_batch_exact_reads(nw_ctx* ctx);
 
 /* Output mode of the upload/run API (NW_OUT_ROWS default).  Takes effect from
  * the next nw_batch_upload. */

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from crispresso_amd import synth
-from crispresso_amd.aligner import pack_reads
+from crispresso_amd.aligner import pack_2bit, pack_reads
 
 pytestmark = pytest.mark.gpu
 
@@ -619,3 +619,72 @@ def test_iupac_amplicon_band_path(gpu_aligner_factory, oracle, monkeypatch, ops)
     paths = a.path_counts()
     assert_same(oracle, amp, buf, off, batch, f"iupac-amplicon ops={ops}")
     assert paths["band16"] > 1000 and paths["exact_kernel"] < 0.1 * len(reads)
+
+
+# ---------------------------------------------------------------- the wide level (128 diagonals)
+
+def _wide_reads(amp, seed, n_bulk=300):
+    """Reads the 16 / 32-diagonal levels cannot certify but 128 diagonals can (deletions and
+    insertions of 26-60 bp, two separated indels), reads no band certifies (chimeras,
+    unrelated, reversed, IUPAC codes), and a bulk of parity-mix reads."""
+    La = len(amp)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    reads = []
+    for d in (26, 28, 30, 34, 40, 50, 60):
+        if d <= La // 2:
+            p = int(rng.integers(La // 8, La - d - La // 8))
+            reads.append(amp[:p] + amp[p + d:])
+    for k in (26, 33, 45, 60):
+        p = int(rng.integers(La // 8, La - La // 8))
+        reads.append(amp[:p] + synth.random_amplicon(k, 90 + k) + amp[p:])
+    if La >= 200:
+        p, q = La // 4, 2 * La // 3
+        reads.append(amp[:p] + amp[p + 20:q] + synth.random_amplicon(25, 5) + amp[q:])   # -20 then +25
+        reads.append(amp[:p] + amp[p + 30:q] + amp[q + 12:])                              # two deletions
+    reads += [amp[:60] + synth.random_amplicon(90, 6) + amp[150:], synth.random_amplicon(La, 8), amp[::-1],
+              amp[40:] + amp[:40], amp[:80] + "R" + amp[81:]]
+    buf0, off0 = synth.reads_from(amp, n_bulk, seed + 1, synth.PARITY_MIX)
+    reads += synth.unpack(buf0, off0)
+    return reads
+
+
+@pytest.mark.parametrize("wide", [None, "0"])
+@pytest.mark.parametrize("La", [250, 96, 600])
+def test_wide_level(gpu_aligner_factory, oracle, monkeypatch, kernel, wide, La):
+    """The 128-diagonal wide level takes what the 16 / 32 levels give up on (the exact
+    kernel's list before it): large indels are certified there, the rest reaches the
+    exact kernel; bit-identical either way (CRISPR_NW_WIDE=0: no wide level)."""
+    if wide is not None:
+        monkeypatch.setenv("CRISPR_NW_WIDE", wide)
+    amp = synth.random_amplicon(La, 40 + La)
+    reads = _wide_reads(amp, La)
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    batch = a.align_packed(buf, off)
+    assert_same(oracle, amp, buf, off, batch, f"wide={wide} La={La}")
+    if kernel.startswith("diag"):
+        fb, ex = a.fallbacks(), a.exact_reads()
+        assert fb >= 10
+        if wide is None:
+            assert 4 <= ex < fb - 5, (fb, ex)   # the large indels certified on the wide level
+        else:
+            assert ex == fb
+
+
+def test_wide_level_capacity(gpu_aligner_factory, oracle, monkeypatch):
+    """More reads for the wide level than its region holds (2048 pairs per chunk): the
+    list's tail goes straight to the exact kernel."""
+    amp = synth.random_amplicon(150, 61)
+    rng = np.random.Generator(np.random.PCG64(62))
+    reads = []
+    for i in range(4700):
+        d = int(rng.integers(30, 70))
+        p = int(rng.integers(10, 150 - d - 10))
+        reads.append(amp[:p] + amp[p + d:] if i % 3 else amp[:p] + synth.random_amplicon(d, i) + amp[p:])
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops_packed(pack_2bit(buf, off))
+    assert a.fallbacks() > 4096
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "wide-capacity")
