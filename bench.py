@@ -349,7 +349,8 @@ def dual_leg(al, n_reads, steps, warmup):
     ops_off2 = _lib.PinnedBuffer(n + 1, np.int64)
     ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
-    pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
+    p_lens = _lib.PinnedBuffer(max(n, 1), np.uint16)
+    pr = pack_2bit(pb.array, po.array, packed=p_packed.array, lens=p_lens.array)
 
     def step():
         al.set_reference(amp)
@@ -399,8 +400,9 @@ def pack_pinned(buf, offsets, threads):
 
     po = _lib.pinned_copy(offsets)
     pp = _lib.PinnedBuffer((int(offsets[-1]) + 3) // 4 + 16, np.uint8)
-    pr = pack_2bit(buf, po.array, nthreads=threads, packed=pp.array)
-    return PackedReads(pr.packed, po.array, pr.exc_pos, pr.exc_byte), (po, pp)
+    pl = _lib.PinnedBuffer(max(len(offsets) - 1, 1), np.uint16)
+    pr = pack_2bit(buf, po.array, nthreads=threads, packed=pp.array, lens=pl.array)
+    return PackedReads(pr.packed, po.array, pr.exc_pos, pr.exc_byte, pr.lens), (po, pp, pl)
 
 
 def c4_leg(al, amplicon, rank, world, dist, threads, steps, warmup, sample_every):
@@ -637,9 +639,11 @@ def merge_leg(device, n_pairs):
 
 def band_cells(counts, La, mean_len):
     """DP cells the band path computes per pass: W diagonals x (La + Lb) / 2 anti-diagonal steps per read
-    and level (16 and 32), the full La x Lb matrix for the exact kernel, none for exact copies."""
+    and level (16, 32 and the 128-diagonal wide level), the full La x Lb matrix for the exact kernel, none
+    for exact copies."""
     steps = (La + mean_len) / 2.0
-    return (counts["band16"] * 16 * steps + counts["band32"] * 32 * steps + counts["exact_kernel"] * La * mean_len)
+    return (counts["band16"] * 16 * steps + counts["band32"] * 32 * steps + counts["band_fallback"] * 128 * steps +
+            counts["exact_kernel"] * La * mean_len)
 
 
 def main():
@@ -690,6 +694,7 @@ def main():
     # aligner exactly such a batch: the e2e leg)
     pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(offsets)
     p_packed = _lib.PinnedBuffer((int(offsets[-1]) + 3) // 4 + 16, np.uint8)
+    p_lens = _lib.PinnedBuffer(max(n, 1), np.uint16)
     p_stats = _lib.PinnedBuffer(n, _lib.STAT_DTYPE)
     p_off = _lib.PinnedBuffer(n + 1, np.int64)
     p_ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
@@ -705,7 +710,7 @@ def main():
     from crispresso_amd.aligner import pack_2bit
 
     t1 = time.perf_counter()
-    pr = pack_2bit(pb.array, po.array, nthreads=threads, packed=p_packed.array)
+    pr = pack_2bit(pb.array, po.array, nthreads=threads, packed=p_packed.array, lens=p_lens.array)
     pack_s = time.perf_counter() - t1
     state = {}
 
@@ -740,7 +745,8 @@ def main():
     expand_s = time.perf_counter() - t1
 
     kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
-    geo["fallback_reads"] = counts["exact_kernel"]
+    geo["fallback_reads"] = counts["band_fallback"]
+    geo["exact_kernel_reads"] = counts["exact_kernel"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

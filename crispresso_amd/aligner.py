@@ -151,12 +151,29 @@ class PackedReads:
     offsets: np.ndarray      # int64 [n + 1], the text's offsets
     exc_pos: np.ndarray      # int64, ascending
     exc_byte: np.ndarray     # uint8
+    lens: Optional[np.ndarray] = None   # uint16 [n] read lengths: they cross PCIe instead of the offsets
+
+
+def read_lengths16(offsets: np.ndarray, out: Optional[np.ndarray] = None) -> Optional[np.ndarray]:
+    """uint16 read lengths for nw_align_ops_packed_lens (nw_read_lengths16), or None when a
+    read is longer than 65535.  ``out``: a preallocated (e.g. pinned) uint16 array of n."""
+    lib = _lib.load()
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    n = len(offsets) - 1
+    lens = out if out is not None else np.empty(max(n, 1), np.uint16)
+    rc = lib.nw_read_lengths16(_lib.ptr(offsets), n, _lib.ptr(lens), 0)
+    if rc == _lib.NW_E_UNSUPPORTED:
+        return None
+    if rc != _lib.NW_OK:
+        raise NeedleError(f"nw_read_lengths16 failed (code {rc})")
+    return lens[:n]
 
 
 def pack_2bit(buf: np.ndarray, offsets: np.ndarray, nthreads: int = 0, packed: Optional[np.ndarray] = None,
-              exc_cap: int = 0) -> PackedReads:
+              exc_cap: int = 0, lens: Optional[np.ndarray] = None) -> PackedReads:
     """2-bit pack a text batch (host C++, ``nthreads`` threads; 0 = all cores).  ``packed``
-    may be a preallocated (e.g. pinned) uint8 array of (offsets[-1] + 3) // 4 bytes."""
+    may be a preallocated (e.g. pinned) uint8 array of (offsets[-1] + 3) // 4 bytes; the
+    read lengths go into ``lens`` (uint16 [n], e.g. pinned) or a new array."""
     lib = _lib.load()
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     n = len(offsets) - 1
@@ -175,7 +192,7 @@ def pack_2bit(buf: np.ndarray, offsets: np.ndarray, nthreads: int = 0, packed: O
             continue
         if rc != _lib.NW_OK:
             raise NeedleError(f"nw_pack_reads failed (code {rc})")
-        return PackedReads(packed, offsets, pos[: cnt.value], byt[: cnt.value])
+        return PackedReads(packed, offsets, pos[: cnt.value], byt[: cnt.value], read_lengths16(offsets, lens))
     raise NeedleError("nw_pack_reads: exception list kept growing")
 
 
@@ -300,7 +317,11 @@ class GpuAligner:
         """Reads of the last run by path (nw_batch_path_counts)."""
         v = np.zeros(4, np.int64)
         self._check(self.lib.nw_batch_path_counts(self._h, _lib.ptr(v)), "nw_batch_path_counts")
-        return dict(zip(("exact_copies", "band16", "band32", "exact_kernel"), map(int, v)))
+        d = dict(zip(("exact_copies", "band16", "band32", "band_fallback"), map(int, v)))
+        ex = self.exact_reads()   # of the 16 / 32 levels' give-ups: the wide level certified the rest
+        d["wide128"] = d["band_fallback"] - ex
+        d["exact_kernel"] = ex
+        return d
 
     def device_output(self):
         """(d_aln, stride, d_stats) device pointers of the last run's resident output
@@ -398,10 +419,15 @@ class GpuAligner:
         else:
             stats, ops, ops_off = out
 
+        exc = (_lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,
+               len(pr.exc_pos))
+
         def call(o):
-            return self.lib.nw_align_ops_packed(self._h, _lib.ptr(pr.packed), _lib.ptr(offsets), n,
-                                                _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None,
-                                                _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None, len(pr.exc_pos),
+            if pr.lens is not None:   # the lengths cross PCIe instead of the offsets
+                return self.lib.nw_align_ops_packed_lens(self._h, _lib.ptr(pr.packed), _lib.ptr(offsets),
+                                                         _lib.ptr(pr.lens), n, *exc, _lib.ptr(o), len(o),
+                                                         _lib.ptr(ops_off), _lib.ptr(stats))
+            return self.lib.nw_align_ops_packed(self._h, _lib.ptr(pr.packed), _lib.ptr(offsets), n, *exc,
                                                 _lib.ptr(o), len(o), _lib.ptr(ops_off), _lib.ptr(stats))
 
         rc = call(ops)
@@ -478,6 +504,12 @@ class GpuAligner:
             stats, ops, ops_off = out
 
         def call(o):
+            if packed and buf.lens is not None:
+                return self.lib.nw_align_multi_ops_packed_lens(
+                    self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf.packed), _lib.ptr(offsets),
+                    _lib.ptr(buf.lens), _lib.ptr(idx), n, _lib.ptr(buf.exc_pos) if len(buf.exc_pos) else None,
+                    _lib.ptr(buf.exc_byte) if len(buf.exc_byte) else None, len(buf.exc_pos), _lib.ptr(o), len(o),
+                    _lib.ptr(ops_off), _lib.ptr(stats))
             if packed:
                 return self.lib.nw_align_multi_ops_packed(
                     self._h, refs, _lib.ptr(roff), len(amps), _lib.ptr(buf.packed), _lib.ptr(offsets),

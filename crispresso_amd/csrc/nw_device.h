@@ -171,13 +171,14 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
 hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
 // pbyte0, 4-aligned) -> dst[pos - bias] bytes (A C T G), then exceptions [e0, e1)
-// With `lens` (a chunk's length segment, LenSeg below): the same launch also rebuilds the
-// chunk's offsets d_off[r_lo .. r_hi] (call-indexed, r_hi inclusive) from its reads' uint16
-// lengths and every 1024th offset (the 8-B offsets no longer cross PCIe).
+// With `lens`: the same launch also rebuilds the chunk's offsets d_off[r_lo .. r_hi]
+// (call-indexed, r_hi inclusive) from the reads' uint16 lengths and every kLenGroup-th
+// offset (nw_align_ops_packed_lens: the 8-B offsets do not cross PCIe).
 struct LenSeg {
-    const uint8_t* seg = nullptr;   // device: [ngroups] int64 group bases, then uint16 lengths from read 1024 * g0
-    int64_t g0 = 0, ngroups = 0;    // groups g0 .. g0 + ngroups - 1 (group g: reads [1024 g, 1024 g + 1024))
-    int64_t r_lo = 0, r_hi = 0;     // offsets written: reads r_lo .. r_hi
+    const uint16_t* len = nullptr;   // device: the call's read lengths (read r at len[r])
+    const int64_t* gbase = nullptr;  // device: offset of read g * kLenGroup, per group g
+    int64_t g0 = 0, ngroups = 0;     // the chunk's groups g0 .. g0 + ngroups - 1 (group g: reads [1024 g, 1024 g + 1024))
+    int64_t r_lo = 0, r_hi = 0;      // offsets written: reads r_lo .. r_hi
     int64_t* d_off = nullptr;
 };
 constexpr int kLenGroup = 1024;

@@ -66,7 +66,8 @@ struct nw_fastq {
     int64_t* exc_pos = nullptr;
     uint8_t* exc_byte = nullptr;
     int64_t n_exc = 0;
-    void* blocks[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint16_t* lens = nullptr;   // nw_fastq_lens (null: a read longer than 65535)
+    void* blocks[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     ~nw_fastq() {
         for (void* b : blocks)
             if (b) {
@@ -556,6 +557,10 @@ int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int
             std::memcpy(q->exc_byte, byt.data(), (size_t)got);
         }
         q->n_exc = got;
+        // the lengths (nw_align_ops_packed_lens: they cross PCIe instead of the offsets)
+        q->lens = (uint16_t*)get(sizeof(uint16_t) * (size_t)std::max<int64_t>(n, 1), 4);
+        if (!q->lens) return NW_E_NOMEM;
+        if (nw_read_lengths16(q->offsets.data(), n, q->lens, nt) != NW_OK) q->lens = nullptr;
         q->packed_done = true;
     }
     if (packed) *packed = q->pk;
@@ -564,6 +569,13 @@ int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int
     if (exc_byte) *exc_byte = q->exc_byte;
     if (n_exc) *n_exc = q->n_exc;
     return NW_OK;
+}
+
+int nw_fastq_lens(nw_fastq* q, const uint16_t** lens) {
+    if (!q || !lens) return NW_E_INVALID;
+    if (!q->packed_done) return NW_E_STATE;   // nw_fastq_pack first
+    *lens = q->lens;
+    return q->lens ? NW_OK : NW_E_UNSUPPORTED;
 }
 
 }  // extern "C"

@@ -1477,6 +1477,7 @@ struct PackedInput {
     const int64_t* exc_pos;
     const uint8_t* exc_byte;
     int64_t n_exc;
+    const uint16_t* lens = nullptr;   // the reads' lengths (nw_align_ops_packed_lens): they cross instead of the offsets
 };
 
 // Amplicon groups of a pooled call: reads [first[g], first[g + 1]) align against
@@ -1627,25 +1628,18 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // pace of the middle chunks.  Diagnostics only.
     const char* up_env = std::getenv("CRISPR_NW_UPLOAD");
     const int upload_mode = up_env ? std::atoi(up_env) : 0;
-    // Packed input: the reads' offsets cross as uint16 lengths plus every kLenGroup-th offset
-    // (a chunk's length segment: 2 B per read instead of 8, 70.5 -> 64.5 MB per 1M C2 reads);
-    // the chunk's unpack launch rebuilds its int64 offsets.  The host writes a chunk's segment
-    // (one pass over its offsets on the pool, which also finds the longest / shortest read)
-    // once the first chunk's bases are queued.  A chunk with a read longer than 65535 sends its
-    // int64 offsets instead.  CRISPR_NW_LENS=1: on (measured slower: the host pass now precedes the
-    // later uploads, C2 2.31 vs 2.22 ms, C5 23.2 vs 22.0 ms).
+    // Packed input with the reads' lengths (nw_align_ops_packed_lens): per read its uint16
+    // length crosses PCIe instead of its int64 offset (plus every kLenGroup-th offset, once):
+    // 2 B instead of 8, 70.5 -> 64.5 MB per 1M C2 reads.  The call is PCIe-bound at the
+    // margin (8 MB more upload measured +0.15 ms).  Each chunk's unpack launch rebuilds its
+    // offsets (nw::LenSeg); the scan below checks the lengths against the group offsets
+    // before any kernel runs.  CRISPR_NW_LENS=0: the offsets cross instead.
     const char* lens_env = std::getenv("CRISPR_NW_LENS");
-    const bool lens_on = pk && upload && n > 0 && upload_mode == 0 && lens_env && std::atoi(lens_env) == 1;
-    std::vector<nw::LenSeg> lseg((size_t)(lens_on ? nchunks : 0));
-    std::vector<int64_t> lseg_off((size_t)(lens_on ? nchunks + 1 : 0), 0);
+    const bool lens_on = pk && pk->lens && upload && n > 0 && upload_mode == 0 && !(lens_env && std::atoi(lens_env) == 0);
+    const int64_t ngroups_len = lens_on ? n / nw::kLenGroup + 1 : 0;
     int64_t mx = 1, mn = 0;
     if (lens_on) {
-        for (int64_t k = 0; k < nchunks; ++k) {
-            const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
-            const int64_t g0 = lo / nw::kLenGroup, ng = hi / nw::kLenGroup - g0 + 1;
-            lseg_off[(size_t)k + 1] = lseg_off[(size_t)k] + ((8 * ng + 2 * (hi - g0 * nw::kLenGroup) + 15) & ~(int64_t)15);
-        }
-        const int64_t need = lseg_off[(size_t)nchunks] + 16;
+        const int64_t need = 8 * ngroups_len;
         if (need > c->h_lens_cap) {
             if (c->h_lens) (void)hipHostFree(c->h_lens);
             c->h_lens = nullptr;
@@ -1653,69 +1647,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             HIP_OR_FAIL(c, hipHostMalloc((void**)&c->h_lens, (size_t)need, hipHostMallocDefault));
             c->h_lens_cap = need;
         }
-        if (c->d_lens.reserve((size_t)need) != hipSuccess)
+        if (c->d_lens.reserve((size_t)(need + 2 * n + 64)) != hipSuccess)
             return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
+        int64_t* gb = (int64_t*)c->h_lens;
+        for (int64_t g = 0; g < ngroups_len; ++g) gb[g] = offsets[g * nw::kLenGroup];
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p, c->h_lens, (size_t)need, hipMemcpyHostToDevice, c->s_in));
+        h2d_bytes += need;
     }
     nw_host::Pool& pool = nw_host::Pool::get();
-    // every chunk's length segment in one pass over the caller's offsets on the pool (run once
-    // the first chunk's bases are queued): group bases, then the lengths of reads [g0 *
-    // kLenGroup, hi); a chunk with a read longer than 65535 (or negative: the scan below
-    // reports it) sends its int64 offsets instead
-    std::vector<char> lens_bad((size_t)(lens_on ? nchunks : 0), 0);
-    auto write_lens = [&]() {
-        auto seg_of = [&](int64_t k, int64_t* g0, int64_t* ng, uint16_t** ln) {
-            *g0 = chunks[(size_t)k].lo / nw::kLenGroup;
-            *ng = chunks[(size_t)k].hi / nw::kLenGroup - *g0 + 1;
-            *ln = (uint16_t*)(c->h_lens + lseg_off[(size_t)k] + 8 * *ng);
-        };
-        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
-        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
-        pool.run(parts, [&](int q) {
-            int64_t a0, a1, a = 1, b = 0;
-            nw_host::Pool::range(n, parts, q, &a0, &a1);
-            // the chunk holding read a0 (chunks are in read order)
-            int64_t k = std::upper_bound(chunks.begin(), chunks.end(), a0,
-                                         [](int64_t r, const Chunk& ch) { return r < ch.hi; }) - chunks.begin();
-            for (int64_t r = a0; r < a1 && k < nchunks; ++k) {
-                int64_t g0, ng;
-                uint16_t* ln;
-                seg_of(k, &g0, &ng, &ln);
-                const int64_t e = std::min(a1, chunks[(size_t)k].hi), rb = g0 * nw::kLenGroup;
-                int64_t ka = 1, kb = 0;
-                for (r = std::max(r, chunks[(size_t)k].lo); r < e; ++r) {
-                    const int64_t len = offsets[r + 1] - offsets[r];
-                    ka = len > ka ? len : ka;
-                    kb = len < kb ? len : kb;
-                    ln[r - rb] = (uint16_t)len;
-                }
-                if (kb < 0 || ka > 65535) lens_bad[(size_t)k] = 1;   // set-only: racing parts write the same value
-                a = std::max(a, ka);
-                b = std::min(b, kb);
-            }
-            pmx[(size_t)q] = a;
-            pmn[(size_t)q] = b;
-        });
-        for (int q = 0; q < parts; ++q) {
-            mx = std::max(mx, pmx[(size_t)q]);
-            mn = std::min(mn, pmn[(size_t)q]);
-        }
-        for (int64_t k = 0; k < nchunks; ++k) {
-            int64_t g0, ng;
-            uint16_t* ln;
-            seg_of(k, &g0, &ng, &ln);
-            int64_t* gb = (int64_t*)(c->h_lens + lseg_off[(size_t)k]);
-            for (int64_t g = 0; g < ng; ++g) gb[g] = offsets[(g0 + g) * nw::kLenGroup];
-            // the group's reads before the chunk (the previous chunks' lengths)
-            const int64_t lo = chunks[(size_t)k].lo;
-            for (int64_t r = g0 * nw::kLenGroup; r < lo; ++r) {
-                const int64_t len = offsets[r + 1] - offsets[r];
-                if (len < 0 || len > 65535) lens_bad[(size_t)k] = 1;
-                ln[r - g0 * nw::kLenGroup] = (uint16_t)len;
-            }
-            if (!lens_bad[(size_t)k]) lseg[(size_t)k] = nw::LenSeg{c->d_lens.p + lseg_off[(size_t)k], g0, ng, lo,
-                                                                   chunks[(size_t)k].hi, c->d_offsets.p};
-        }
-    };
     for (int64_t k = 0; upload && k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
@@ -1743,12 +1682,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                           c->s_in));
             h2d_bytes += b1 - b0;
         }
-        if (lens_on && k == 0) write_lens();
-        if (lens_on && !lens_bad[(size_t)k]) {
-            const int64_t bytes = lseg_off[(size_t)k + 1] - lseg_off[(size_t)k];
-            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + lseg_off[(size_t)k], c->h_lens + lseg_off[(size_t)k], (size_t)bytes,
+        if (lens_on) {
+            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(hi - lo),
                                           hipMemcpyHostToDevice, c->s_in));
-            h2d_bytes += bytes;
+            h2d_bytes += 2 * (hi - lo);
         } else if (!offs_apart) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
                                           hipMemcpyHostToDevice, c->s_in));
@@ -1757,9 +1694,38 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
     }
     ht.lap(3);
+    // lengths given: the longest read, and each group's lengths must add up to its offsets
+    // (the device rebuilds the offsets from them: a mismatch would misplace reads)
+    if (lens_on) {
+        const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 16));
+        std::vector<int64_t> pmx((size_t)parts, 1), pbad((size_t)parts, -1);
+        pool.run(parts, [&](int q) {
+            int64_t g0, g1;
+            nw_host::Pool::range(ngroups_len, parts, q, &g0, &g1);
+            unsigned a = 1;
+            for (int64_t g = g0; g < g1 && pbad[(size_t)q] < 0; ++g) {
+                const int64_t r0 = g * nw::kLenGroup, r1 = std::min(n, r0 + nw::kLenGroup);
+                int64_t sum = 0;
+                for (int64_t r = r0; r < r1; ++r) {
+                    const unsigned l = pk->lens[r];
+                    a = l > a ? l : a;
+                    sum += l;
+                }
+                if (sum != offsets[r1] - offsets[r0]) pbad[(size_t)q] = g;
+            }
+            pmx[(size_t)q] = a;
+        });
+        for (int q = 0; q < parts; ++q) {
+            mx = std::max(mx, pmx[(size_t)q]);
+            if (pbad[(size_t)q] >= 0) {
+                (void)hipStreamSynchronize(c->s_in);   // the queued uploads read the caller's arrays
+                return restore(fail(c, NW_E_INVALID, "lens do not add up to the offsets of reads %lld ..",
+                                    (long long)(pbad[(size_t)q] * nw::kLenGroup)));
+            }
+        }
+    }
     // longest / shortest read: a vectorisable pass, split over the host pool for large
-    // batches (memory-bound; the exact read is found only on error); the length segments'
-    // pass found them already
+    // batches (memory-bound; the exact read is found only on error)
     if (!lens_on) {
         const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
         std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
@@ -1978,7 +1944,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             const int64_t b0 = offsets[lo], b1 = offsets[hi];
             const int64_t e0 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b0) - pk->exc_pos;
             const int64_t e1 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b1) - pk->exc_pos;
-            const nw::LenSeg* ls = lens_on && lseg[(size_t)k].seg ? &lseg[(size_t)k] : nullptr;
+            nw::LenSeg lsk{};
+            if (lens_on)
+                lsk = nw::LenSeg{(const uint16_t*)(c->d_lens.p + 8 * ngroups_len), (const int64_t*)c->d_lens.p,
+                                 lo / nw::kLenGroup, hi / nw::kLenGroup - lo / nw::kLenGroup + 1, lo, hi, c->d_offsets.p};
+            const nw::LenSeg* ls = lens_on ? &lsk : nullptr;
             HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, b0, b1, c->d_exc_pos.p, c->d_exc_byte.p,
                                              e0, e1, c->d_reads.p, c->reads_bias, c->cs, ls));
         }
@@ -2141,6 +2111,16 @@ int nw_align_ops_packed(nw_ctx* c, const uint8_t* packed, const int64_t* offsets
     return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, true, nullptr, &pk);
 }
 
+int nw_align_ops_packed_lens(nw_ctx* c, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
+                             const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out,
+                             int64_t ops_cap, int64_t* ops_off, nw_stat* stats) {
+    if (n_exc < 0) return fail(c, NW_E_INVALID, "bad exception count");
+    if (n > 0 && !lens) return fail(c, NW_E_INVALID, "no lengths");
+    PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    pk.lens = lens;
+    return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, true, nullptr, &pk);
+}
+
 int nw_align_ops_resident(nw_ctx* c, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
                           int64_t* ops_off, nw_stat* stats) {
     return ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, false);
@@ -2278,6 +2258,18 @@ int nw_align_multi_ops_packed(nw_ctx* c, const char* refs, const int64_t* ref_of
     if (!c) return NW_E_INVALID;
     if (n_exc < 0 || (n > 0 && !packed)) return fail(c, NW_E_INVALID, "bad packed batch");
     const PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    return multi_ops(c, refs, ref_offsets, n_refs, nullptr, offsets, ref_of_read, n, ops_out, ops_cap, ops_off, stats,
+                     &pk);
+}
+
+int nw_align_multi_ops_packed_lens(nw_ctx* c, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
+                                   const uint8_t* packed, const int64_t* offsets, const uint16_t* lens,
+                                   const int32_t* ref_of_read, int64_t n, const int64_t* exc_pos, const uint8_t* exc_byte,
+                                   int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off, nw_stat* stats) {
+    if (!c) return NW_E_INVALID;
+    if (n_exc < 0 || (n > 0 && (!packed || !lens))) return fail(c, NW_E_INVALID, "bad packed batch");
+    PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    pk.lens = lens;
     return multi_ops(c, refs, ref_offsets, n_refs, nullptr, offsets, ref_of_read, n, ops_out, ops_cap, ops_off, stats,
                      &pk);
 }

@@ -26,11 +26,10 @@ __global__ __launch_bounds__(256) void nw_unpack_kernel(const uint32_t* packed, 
                                                         uint8_t* dst, int64_t bias, unsigned nub, const LenSeg ls) {
     if (blockIdx.x >= nub) {
         __shared__ int64_t wsum[4];
-        const int64_t b = blockIdx.x - nub;
-        const int64_t g = ls.g0 + b;
+        const int64_t g = ls.g0 + (blockIdx.x - nub);
         const int64_t r0 = g * kLenGroup + 4 * threadIdx.x;   // this thread's 4 reads
-        const uint16_t* len = (const uint16_t*)(ls.seg + 8 * ls.ngroups) + b * kLenGroup + 4 * threadIdx.x;
-        // lengths exist for reads below r_hi only (the segment ends there)
+        const uint16_t* len = ls.len + r0;
+        // lengths of the reads below r_hi only (the chunk's own and the group's earlier ones)
         uint32_t l[4];
         if (r0 + 4 <= ls.r_hi) {
             const uint2 w = *(const uint2*)len;
@@ -50,7 +49,7 @@ __global__ __launch_bounds__(256) void nw_unpack_kernel(const uint32_t* packed, 
         }
         if (lane == 63) wsum[wave] = inc;
         __syncthreads();
-        int64_t base = ((const int64_t*)ls.seg)[b] + inc - t4;
+        int64_t base = ls.gbase[g] + inc - t4;
         for (int w = 0; w < wave; ++w) base += wsum[w];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {

@@ -165,7 +165,8 @@ class MultiGpuAligner:
         for al, (lo, hi) in zip(self.aligners, self._shards(n)):
             o = pr.offsets[lo:hi + 1]
             e0, e1 = np.searchsorted(pr.exc_pos, [o[0], o[-1]]) if len(pr.exc_pos) else (0, 0)
-            sub = PackedReads(pr.packed, o, pr.exc_pos[e0:e1], pr.exc_byte[e0:e1])
+            sub = PackedReads(pr.packed, o, pr.exc_pos[e0:e1], pr.exc_byte[e0:e1],
+                              pr.lens[lo:hi] if pr.lens is not None else None)
             shard_offs.append(o)
             jobs.append(self._pool.submit(al.align_ops_packed, sub))
         out = concat_ops([j.result() for j in jobs])

@@ -148,9 +148,12 @@ def read_fastq_packed(path: str, pinned: bool = True):
         offsets = np.zeros(1, np.int64)
     nb = int(offsets[-1])
     text = _native_array(owner, lib.nw_fastq_seqs(h), nb, np.uint8)
+    pl = ctypes.c_void_p()   # the read lengths (they cross PCIe instead of the offsets); None past 65535 bases
+    lens = (_native_array(owner, pl.value, n, np.uint16)
+            if n and lib.nw_fastq_lens(h, ctypes.byref(pl)) == _lib.NW_OK else None)
     packed = PackedReads(_native_array(owner, pk.value, (nb + 3) // 4 + 16, np.uint8), offsets,
                          _native_array(owner, ep.value, ne.value, np.int64),
-                         _native_array(owner, eb.value, ne.value, np.uint8))
+                         _native_array(owner, eb.value, ne.value, np.uint8), lens)
     nm = ctypes.c_int64()
     p = lib.nw_fastq_names(h, ctypes.byref(nm))
     raw = _native_array(owner, p, nm.value, np.uint8).copy()

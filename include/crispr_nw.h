@@ -236,6 +236,22 @@ int nw_align_ops(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t
 int nw_align_ops_packed(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, int64_t n, const int64_t* exc_pos,
                         const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off,
                         nw_stat* stats);
+/* nw_align_ops_packed with every read's length as well (lens[r] = offsets[r + 1] -
+ * offsets[r], at most 65535; nw_fastq_lens / nw_read_lengths16 produce them): the lengths
+ * cross PCIe instead of the offsets (2 B per read instead of 8; the device rebuilds the
+ * offsets from them and every 1024th offset).  NW_E_INVALID when the lengths of a group of
+ * 1024 reads do not add up to its offsets (checked before any kernel runs). */
+int nw_align_ops_packed_lens(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
+                             const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out,
+                             int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* The same for the pooled call (nw_align_multi_ops_packed). */
+int nw_align_multi_ops_packed_lens(nw_ctx* ctx, const char* refs, const int64_t* ref_offsets, int32_t n_refs,
+                                   const uint8_t* packed, const int64_t* offsets, const uint16_t* lens,
+                                   const int32_t* ref_of_read, int64_t n, const int64_t* exc_pos, const uint8_t* exc_byte,
+                                   int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
+/* lens[r] = offsets[r + 1] - offsets[r] as uint16 (host, nthreads; <= 0: the host pool):
+ * NW_E_UNSUPPORTED when a read is longer than 65535 (or offsets decrease). */
+int nw_read_lengths16(const int64_t* offsets, int64_t n, uint16_t* lens, int32_t nthreads);
 /* Pack reads[offsets[0] .. offsets[n]) for nw_align_ops_packed (host, nthreads; <= 0:
  * all cores): packed must hold bytes offsets[0] / 4 .. (offsets[n] + 3) / 4 (indexed by
  * batch position).  NW_E_CAPACITY when more than exc_cap exceptions (*n_exc = count). */
@@ -293,6 +309,9 @@ const uint8_t* nw_fastq_pass(const nw_fastq* q, int64_t* n);    /* every record'
  * needle (CRISPRessoCORE.py:1791-1797) as the aligner's input. */
 int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int64_t** offsets, const int64_t** exc_pos,
                   const uint8_t** exc_byte, int64_t* n_exc);
+/* After nw_fastq_pack: the reads' lengths as nw_align_ops_packed_lens takes them, in the
+ * same kind of memory; NW_E_UNSUPPORTED (null) when a read is longer than 65535. */
+int nw_fastq_lens(nw_fastq* q, const uint16_t** lens);
 
 /* nw_expand_ops for the reads idx[0 .. m) only: read idx[q]'s rows at aln_out + q*3*stride. */
 int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,

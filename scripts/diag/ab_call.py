@@ -45,7 +45,8 @@ stats = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
 ops_off = _lib.PinnedBuffer(nr + 1, np.int64)
 ops = _lib.PinnedBuffer((2 if c4 else 4) * nr + 4096, np.uint32)
 p_packed = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 1, np.uint8)
-pr = pack_2bit(pb.array, po.array, packed=p_packed.array)
+p_lens = _lib.PinnedBuffer(max(nr, 1), np.uint16)
+pr = pack_2bit(pb.array, po.array, packed=p_packed.array, lens=p_lens.array)
 al = GpuAligner(0)
 stats2 = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
 ops_off2 = _lib.PinnedBuffer(nr + 1, np.int64)

@@ -256,3 +256,4 @@ def test_packed_ingest_matches_text_and_pack_reads(tmp_path):
     assert np.array_equal(pk.packed[:nb], want.packed[:nb])
     assert np.array_equal(pk.exc_pos, want.exc_pos) and np.array_equal(pk.exc_byte, want.exc_byte)
     assert len(pk.exc_pos) > 0 and pk.offsets is off
+    assert pk.lens is not None and np.array_equal(pk.lens, np.diff(o2))   # nw_fastq_lens

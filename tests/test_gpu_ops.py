@@ -246,11 +246,14 @@ def test_multi_gpu_aligner_threads_on_one_device(oracle):
     multi.close()
 
 
-@pytest.mark.parametrize("chunk", ["97", "100000"])
-def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk):
+@pytest.mark.parametrize("lens", [True, False])
+@pytest.mark.parametrize("chunk", ["97", "1500", "100000"])
+def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk, lens):
     """nw_align_ops_packed: 2-bit bases + exceptions (N, IUPAC, U, '-', lower case) give
     the same records and runs as the text path and the oracle; a batch whose offsets
-    start mid-buffer; chunk edges inside packed bytes; the resident second pass after it."""
+    start mid-buffer; chunk edges inside packed bytes and inside 1024-read length groups
+    (lens: nw_align_ops_packed_lens, the offsets rebuilt on the device); the resident
+    second pass after it."""
     from crispresso_amd.aligner import pack_2bit
 
     monkeypatch.setenv("CRISPR_NW_CHUNK", chunk)
@@ -263,6 +266,9 @@ def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk):
     a = gpu_aligner_factory()
     a.set_reference(amp)
     pr = pack_2bit(full, off)
+    assert pr.lens is not None and np.array_equal(pr.lens, np.diff(off))
+    if not lens:
+        pr.lens = None
     ob = a.align_ops_packed(pr)
     assert a.ops_times()["h2d_bytes"] < (int(off[-1]) - int(off[0])) // 2
     assert_same(oracle, amp, buf, off0, ob.expand(amp, full, off), f"packed chunk={chunk}")
@@ -276,6 +282,24 @@ def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk):
     a.set_reference(hdr)
     again = a.align_ops(None, off, resident=True)
     assert_same(oracle, hdr, buf, off0, again.expand(hdr, full, off), "packed-resident")
+
+
+def test_packed_lens_must_match_offsets(gpu_aligner_factory, oracle):
+    """nw_align_ops_packed_lens checks the lengths against the offsets (per 1024-read
+    group) before any kernel runs: a mismatch is NW_E_INVALID, and the context still works."""
+    from crispresso_amd.aligner import NeedleError, pack_2bit
+
+    amp = synth.random_amplicon(200, 71)
+    buf, off = synth.reads_from(amp, 5000, 72)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    pr = pack_2bit(buf, off)
+    pr.lens = pr.lens.copy()
+    pr.lens[3000] += 1
+    with pytest.raises(NeedleError, match="lens do not add up"):
+        a.align_ops_packed(pr)
+    pr.lens[3000] -= 1
+    assert_same(oracle, amp, buf, off, a.align_ops_packed(pr).expand(amp, buf, off), "lens-after-error")
 
 
 def test_adaptive_first_level_hdr_pass(gpu_aligner_factory, oracle, monkeypatch):

@@ -402,7 +402,7 @@ def test_diag_is_default_and_certifies_c2(gpu_aligner_factory, oracle, monkeypat
         assert a.fallbacks() <= 4 and paths["band32"] > 0
     else:
         assert paths["band32"] == 0 and 0 < a.fallbacks() <= 0.01 * (len(off) - 1)
-    assert a.fallbacks() == paths["exact_kernel"]
+    assert a.fallbacks() == paths["band_fallback"] and paths["exact_kernel"] <= paths["band_fallback"]
     assert_same(oracle, amp, buf, off, batch, "diag-c2")
 
 
@@ -536,7 +536,7 @@ def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
     assert a.geometry()["tb_mode"] == "diag-int16"
     paths = a.path_counts()
     if levels == "16+32 direct":
-        assert paths["band32"] == 0 and paths["exact_kernel"] > 1
+        assert paths["band32"] == 0 and paths["band_fallback"] > 1
     elif levels.startswith("16+32"):
         assert paths["band32"] > 1
     assert_same(oracle, amp, buf, off, batch, f"levels={levels}")
