@@ -254,17 +254,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             for (int t = 0; t < kCand; ++t) {
                 if (us[t] < 0 || __ballot(diff[t] != 0u) != 0ull) continue;
                 exact |= 1ull << us[t];
-                if (a.ops) {   // ops output: one M run of La columns, no rows
-                    if (lane == 0) {
-                        a.ops[r0 + us[t]] = ((unsigned)RUN_M << 28) | (unsigned)La;   // run 0 of the read's slot
-                        a.nops[r0 + us[t]] = 1;
-                    }
-                    if (lane < 8) {
-                        const int v = lane == 3 || lane == 7 ? 0 : (lane == 4 ? a.band_maxsub * La : La);
-                        ((int*)(a.stats + r0 + us[t]))[lane] = v;
-                    }
-                    continue;
-                }
+                if (a.ops) continue;   // ops output: the wave's exact copies are written together below
                 if (!one_chunk) {
                     emit_later |= 1ull << us[t];
                     continue;
@@ -284,6 +274,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         }
         if (r < a.n)
             a.sort_key[r] = ((exact >> lane) & 1ull) ? a.band_lb_cap + 2 : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+        // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
+        // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
+        // coalesced stores instead of three partial-line stores per copy
+        if (a.ops && r < a.n && ((exact >> lane) & 1ull)) {
+            a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
+            a.nops[r] = 1;
+            int4* st = (int4*)(a.stats + r);
+            st[0] = make_int4(La, La, La, 0);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * La, La, La, 0);   // score, end_i, end_j, flags
+        }
         // the diagonal of every exact copy longer than one chunk: amplicon, '|' markup,
         // read; rows as dwords up to round4(La) (within the row stride)
         while (emit_later) {

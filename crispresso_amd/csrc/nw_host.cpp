@@ -878,8 +878,13 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.redo_count = c->s->d_fallback_count.p + 2;
         if (two && !only16) a.redo_flags = c->s->d_redo_flags.p;   // the first level's walk writes every position's
         // a chunk whose first level hands on at most `direct` reads skips the second level on
-        // the device: the exact kernel takes them (CRISPR_NW_DIRECT=0: always both levels)
-        int direct = 1024;
+        // the device: the wide level takes them (up to 1/16 of the chunk, as many as its region
+        // holds), or without it the exact kernel (1024).  A chunk where more reads need more than
+        // 16 diagonals (the HDR pass) keeps the second level, 4 read pairs per wavefront, and the
+        // adaptive first-level choice sees them.  CRISPR_NW_DIRECT=0: always both levels.
+        int direct = c->wide_fill.grid > 0
+                         ? (int)std::max<int64_t>(1024, std::min<int64_t>(c->n / 16, 2 * c->wide_pairs))
+                         : 1024;
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
         if (!two || only16) direct = 0;
         c->redo_direct = direct;
