@@ -182,6 +182,22 @@ __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const uns
 
 constexpr int kCand = 8;   // exact-copy candidates compared together (2 dword loads each in flight)
 
+// Reads of the amplicon's length with ONE substitution (A C G T against A C G T; ops output,
+// an A C G T amplicon of at most 256 bp) need no DP either.  With k mismatches on the main
+// diagonal its sum is D = m (La - 1) - x for k = 1 (m = maxsub, x = -mismatch = 4 m / 5).  Any
+// alignment with an internal gap pairs at most La - 1 residues and pays at least the gap
+// open O: <= m (La - 1) - O < D when O > x (EMBOSS's 10 vs 4, scaled).  One without is a
+// single diagonal d with free end gaps: |d| >= 2 pairs at most La - 2 residues (m (La - 2) <
+// D as m > x); d = +1 / -1 score m p - x (La - 1 - p) for p matches of their La - 1 pairs,
+// below D exactly when p <= La - 2: each needs one mismatch (shifted byte compares, ballots).
+// So the diagonal is the unique optimum; along it M(i, i) = D_i >= m i - m - x >= X(i, i),
+// Y(i, i) (<= m (i - 1) - O), so M wins every traceback tie: the record is the diagonal's,
+// as the exact copy's.  ~8 % of C2's reads (a third of the 1-3 substitution
+// class and of the 1 % noise class) leave the DP this way.
+__device__ __forceinline__ unsigned zero_bytes(unsigned x) {   // 0x80 in each zero byte of x
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+
 __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     const int La = a.La, nd = (La + 3) / 4;
@@ -199,7 +215,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         amp_sh[k] = w;
         amp_sh[nd + k] = ld_dw(a.amp + 4 * k);
     }
-    __syncthreads();
+    int acgt_amp = 1;   // every amplicon byte A C G T (either case)
+    for (int q = threadIdx.x; q < La; q += blockDim.x) {
+        const unsigned char c = upcase(a.amp[q]);
+        acgt_amp &= (c == 'A' || c == 'C' || c == 'G' || c == 'T');
+    }
+    const int sc5 = a.band_maxsub / 5;
+    // the one-substitution certificate (above): ops output, one 256-byte chunk, EDNAFULL's
+    // 5 / -4 scaled, a gap open above the mismatch cost
+    const bool sub1_ok = __syncthreads_and(acgt_amp) && a.ops && nd <= 64 && a.band_maxsub == 5 * sc5 &&
+                         a.gap_open > 4 * sc5 && a.gap_extend >= 0;
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
@@ -210,7 +235,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         const long long my_off = r < a.n ? a.offsets[r] : 0;
         const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
         unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
-        unsigned long long exact = 0ull;
+        unsigned long long exact = 0ull, sub1 = 0ull;
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
         // away from the words already in registers
@@ -252,7 +277,34 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             }
 #pragma unroll
             for (int t = 0; t < kCand; ++t) {
-                if (us[t] < 0 || __ballot(diff[t] != 0u) != 0ull) continue;
+                if (us[t] < 0) continue;
+                const unsigned long long anyd = __ballot(diff[t] != 0u);
+                if (anyd != 0ull) {
+                    // one substitution: a single lane with a single mismatching byte, A C G T in the read
+                    if (!sub1_ok || __builtin_popcountll(anyd) != 1) continue;
+                    const unsigned zd = ~zero_bytes(diff[t]) & 0x80808080u;   // the mismatching bytes
+                    const unsigned rf = raw[t] | 0x20202020u;
+                    const int pb = zd ? (int)__builtin_ctz(zd) - 7 : 0;
+                    const unsigned cb = (rf >> pb) & 0xffu;
+                    const bool bad = zd && (__builtin_popcount(zd) != 1 ||
+                                            !(cb == 'a' || cb == 'c' || cb == 'g' || cb == 't'));
+                    if (__ballot(bad)) continue;
+                    // the diagonals d = +1 (read byte q + 1 vs amplicon byte q) and -1, q <= La - 2
+                    const int k4 = lane, kc = k4 < nd ? k4 : nd - 1;   // one chunk (sub1_ok)
+                    const unsigned rn = (unsigned)__shfl_down((int)raw[t], 1, 64);
+                    const unsigned an = k4 + 1 < nd ? amp_sh[k4 + 1] : 0u;
+                    const unsigned am0 = k4 < nd ? amp_sh[kc] : 0u;
+                    const unsigned x1 = (__builtin_amdgcn_alignbyte(rn, raw[t], 1) | 0x20202020u) ^ am0;
+                    const unsigned x2 = rf ^ __builtin_amdgcn_alignbyte(an, am0, 1);
+                    const int q0 = 4 * k4;   // the lane's first byte
+                    const unsigned vm = q0 + 3 <= La - 2 ? 0x80808080u
+                                        : (q0 > La - 2 ? 0u : (0x80808080u >> (8 * (q0 + 3 - (La - 2)))));
+                    // S_d = m p - x (La - 1 - p) with p matches of La - 1 pairs is below D exactly when
+                    // p <= La - 2: one mismatch on each shifted diagonal (two ballots, no sums)
+                    if (__ballot((~zero_bytes(x1) & vm) != 0u) != 0ull && __ballot((~zero_bytes(x2) & vm) != 0u) != 0ull)
+                        sub1 |= 1ull << us[t];
+                    continue;
+                }
                 exact |= 1ull << us[t];
                 if (a.ops) continue;   // ops output: the wave's exact copies are written together below
                 if (!one_chunk) {
@@ -273,16 +325,18 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             }
         }
         if (r < a.n)
-            a.sort_key[r] = ((exact >> lane) & 1ull) ? a.band_lb_cap + 2 : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+            a.sort_key[r] = (((exact | sub1) >> lane) & 1ull) ? a.band_lb_cap + 2
+                                                               : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
-        if (a.ops && r < a.n && ((exact >> lane) & 1ull)) {
+        if (a.ops && r < a.n && (((exact | sub1) >> lane) & 1ull)) {
+            const int k = (int)((sub1 >> lane) & 1ull);   // substitutions (0 or 1; a mismatch scores -4 / 5 maxsub)
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
             a.nops[r] = 1;
             int4* st = (int4*)(a.stats + r);
-            st[0] = make_int4(La, La, La, 0);   // aln_len, n_ident, n_sim, n_gaps
-            st[1] = make_int4(a.band_maxsub * La, La, La, 0);   // score, end_i, end_j, flags
+            st[0] = make_int4(La, La - k, La - k, 0);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * (La - k) - k * 4 * sc5, La, La, 0);   // score, end_i, end_j, flags
         }
         // the diagonal of every exact copy longer than one chunk: amplicon, '|' markup,
         // read; rows as dwords up to round4(La) (within the row stride)

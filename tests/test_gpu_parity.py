@@ -688,3 +688,36 @@ def test_wide_level_capacity(gpu_aligner_factory, oracle, monkeypatch):
     ob = a.align_ops_packed(pack_2bit(buf, off))
     assert a.fallbacks() > 4096
     assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), "wide-capacity")
+
+
+@pytest.mark.parametrize("kind", ["random", "homopolymer", "all-A", "dinucleotide", "La256", "La257"])
+def test_one_substitution_certificate(gpu_aligner_factory, oracle, kind):
+    """Reads of the amplicon's length with one A C G T substitution are finished by the
+    classify kernel (no DP) when the shifted diagonals score below the main one; repeats,
+    N, two substitutions and amplicons over 256 bp go through the band.  Bit-identical."""
+    La = {"La256": 256, "La257": 257}.get(kind, 250)
+    rng = np.random.Generator(np.random.PCG64(91))
+    if kind == "homopolymer":
+        amp = "".join(b * int(rng.integers(1, 9)) for b in rng.choice(list("ACGT"), 80))[:La]
+    elif kind == "all-A":
+        amp = "A" * La
+    elif kind == "dinucleotide":
+        amp = ("AC" * La)[:La]
+    else:
+        amp = synth.random_amplicon(La, 92)
+    La = len(amp)
+    sub = {"A": "C", "C": "G", "G": "T", "T": "A"}
+    reads = []
+    for p in sorted({0, 1, 2, La // 3, La // 2, La - 3, La - 2, La - 1} | set(rng.integers(0, La, 40).tolist())):
+        reads.append(amp[:p] + sub[amp[p]] + amp[p + 1:])
+    reads.append(amp[:10].lower() + sub[amp[10]].lower() + amp[11:])
+    reads.append(amp[:50] + "N" + amp[51:])
+    reads.append(amp[:50] + sub[amp[50]] + amp[51:90] + sub[amp[90]] + amp[91:])
+    reads += [amp] * 3
+    buf, off = pack_reads(reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops_packed(pack_2bit(buf, off))
+    assert_same(oracle, amp, buf, off, ob.expand(amp, buf, off), f"sub1 {kind}")
+    if kind in ("random", "La256"):
+        assert a.path_counts()["exact_copies"] >= len(reads) - 3   # no DP but for N and the double substitution
