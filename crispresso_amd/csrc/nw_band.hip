@@ -225,6 +225,14 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // 5 / -4 scaled, a gap open above the mismatch cost
     const bool sub1_ok = __syncthreads_and(acgt_amp) && a.ops && nd <= 64 && a.band_maxsub == 5 * sc5 &&
                          a.gap_open > 4 * sc5 && a.gap_extend >= 0;
+    // two substitutions (x = 9/5 maxsub: a mismatch's loss against a match, D = m La - 2 x): with an
+    // internal gap and <= La - 2 pairs O > 2 x - 2 m; La - 1 pairs and two gaps 2 O > 2 x - m, one gap
+    // and a mismatch O > x - m; |d| >= 4 m (La - 4) < D: x < 2 m; d = +-1 / +-2 / +-3 need 2 / 1 / 1
+    // mismatches (EDNAFULL); one gap, one end gap, no mismatch: excluded per read (below)
+    const int mt2 = a.band_maxsub, xl = 9 * sc5;
+    const bool sub2_ok = sub1_ok && 2 * a.gap_open > 2 * xl - mt2 && a.gap_open > 2 * xl - 2 * mt2 &&
+                         a.gap_open > xl - mt2 && xl < 2 * mt2 && (2 * xl - mt2) / xl + 1 == 2 &&
+                         (2 * xl - 2 * mt2) / xl + 1 == 1 && (2 * xl - 3 * mt2) / xl + 1 == 1;
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
@@ -235,7 +243,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         const long long my_off = r < a.n ? a.offsets[r] : 0;
         const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
         unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
-        unsigned long long exact = 0ull, sub1 = 0ull;
+        unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull;
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
         // away from the words already in registers
@@ -280,29 +288,64 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 if (us[t] < 0) continue;
                 const unsigned long long anyd = __ballot(diff[t] != 0u);
                 if (anyd != 0ull) {
-                    // one substitution: a single lane with a single mismatching byte, A C G T in the read
-                    if (!sub1_ok || __builtin_popcountll(anyd) != 1) continue;
-                    const unsigned zd = ~zero_bytes(diff[t]) & 0x80808080u;   // the mismatching bytes
+                    // one or two substitutions (A C G T in the read): the certificates above
+                    if (!sub1_ok) continue;
+                    const unsigned zd = ~zero_bytes(diff[t]) & 0x80808080u;   // the lane's mismatching bytes
+                    const int nzl = __builtin_popcount(zd);
+                    const unsigned long long l2 = __ballot(nzl >= 2);
+                    if (__ballot(nzl >= 3) || (l2 && __builtin_popcountll(anyd) > 1) || __builtin_popcountll(anyd) > 2)
+                        continue;
+                    const int ksub = l2 ? 2 : (int)__builtin_popcountll(anyd);
+                    if (ksub == 2 && !sub2_ok) continue;
                     const unsigned rf = raw[t] | 0x20202020u;
-                    const int pb = zd ? (int)__builtin_ctz(zd) - 7 : 0;
-                    const unsigned cb = (rf >> pb) & 0xffu;
-                    const bool bad = zd && (__builtin_popcount(zd) != 1 ||
-                                            !(cb == 'a' || cb == 'c' || cb == 'g' || cb == 't'));
+                    bool bad = false;
+                    for (unsigned z = zd; z; z &= z - 1) {
+                        const unsigned cb = (rf >> ((int)__builtin_ctz(z) - 7)) & 0xffu;
+                        bad = bad || !(cb == 'a' || cb == 'c' || cb == 'g' || cb == 't');
+                    }
                     if (__ballot(bad)) continue;
-                    // the diagonals d = +1 (read byte q + 1 vs amplicon byte q) and -1, q <= La - 2
+                    // the shifted diagonals: d = +s pairs read byte q + s with amplicon byte q, d = -s
+                    // read byte q with amplicon byte q + s (q <= La - 1 - s); mismatching bytes 0x80
                     const int k4 = lane, kc = k4 < nd ? k4 : nd - 1;   // one chunk (sub1_ok)
                     const unsigned rn = (unsigned)__shfl_down((int)raw[t], 1, 64);
                     const unsigned an = k4 + 1 < nd ? amp_sh[k4 + 1] : 0u;
                     const unsigned am0 = k4 < nd ? amp_sh[kc] : 0u;
-                    const unsigned x1 = (__builtin_amdgcn_alignbyte(rn, raw[t], 1) | 0x20202020u) ^ am0;
-                    const unsigned x2 = rf ^ __builtin_amdgcn_alignbyte(an, am0, 1);
                     const int q0 = 4 * k4;   // the lane's first byte
-                    const unsigned vm = q0 + 3 <= La - 2 ? 0x80808080u
-                                        : (q0 > La - 2 ? 0u : (0x80808080u >> (8 * (q0 + 3 - (La - 2)))));
-                    // S_d = m p - x (La - 1 - p) with p matches of La - 1 pairs is below D exactly when
-                    // p <= La - 2: one mismatch on each shifted diagonal (two ballots, no sums)
-                    if (__ballot((~zero_bytes(x1) & vm) != 0u) != 0ull && __ballot((~zero_bytes(x2) & vm) != 0u) != 0ull)
-                        sub1 |= 1ull << us[t];
+                    auto upto = [&](int qmax) -> unsigned {   // bytes q <= qmax of the lane
+                        return qmax >= q0 + 3 ? 0x80808080u : (qmax < q0 ? 0u : (0x80808080u >> (8 * (q0 + 3 - qmax))));
+                    };
+                    auto mis = [&](int sgn, int sh) -> unsigned {
+                        const unsigned x = sgn > 0 ? (__builtin_amdgcn_alignbyte(rn, raw[t], sh) | 0x20202020u) ^ am0
+                                                   : rf ^ __builtin_amdgcn_alignbyte(an, am0, sh);
+                        return ~zero_bytes(x) & upto(La - 1 - sh);
+                    };
+                    const unsigned p1m = mis(1, 1), m1m = mis(-1, 1);
+                    if (ksub == 1) {
+                        // S_+-1 = m p - x (La - 1 - p) is below D exactly when p <= La - 2: one
+                        // mismatch on each shifted diagonal (two ballots, no sums)
+                        if (__ballot(p1m != 0u) != 0ull && __ballot(m1m != 0u) != 0ull) sub1 |= 1ull << us[t];
+                        continue;
+                    }
+                    // two substitutions at read bytes f < l: d = +-1 need two mismatches each, one at
+                    // a read byte > f (no diagonal-0 prefix + one gap + shifted suffix scores above D)
+                    // and one at a read byte < l (no shifted prefix + diagonal-0 suffix); d = +-2, +-3
+                    // need one (S_d < D); |d| >= 4 and two or more gaps score below D by the checks in sub2_ok
+                    const unsigned long long lz = __ballot(zd != 0u);
+                    const int lf = (int)__builtin_ctzll(lz), ll = 63 - (int)__builtin_clzll(lz);
+                    const int zf = __builtin_amdgcn_readlane((int)zd, lf), zl = __builtin_amdgcn_readlane((int)zd, ll);
+                    const int f = 4 * lf + (__builtin_ctz((unsigned)zf) >> 3), l = 4 * ll + ((31 - __builtin_clz((unsigned)zl)) >> 3);
+                    auto from = [&](int qmin) -> unsigned { return 0x80808080u & ~upto(qmin - 1); };   // bytes q >= qmin
+                    auto two = [&](unsigned m) {   // at least two mismatching bytes over the wave
+                        const unsigned long long b1 = __ballot(m != 0u);
+                        return __ballot(__builtin_popcount(m) >= 2) != 0ull || __builtin_popcountll(b1) >= 2;
+                    };
+                    bool ok = two(p1m) && two(m1m);
+                    // d = +1: read byte j = q + 1; d = -1: j = q
+                    ok = ok && __ballot((p1m & from(f)) != 0u) && __ballot((p1m & upto(l - 2)) != 0u);
+                    ok = ok && __ballot((m1m & from(f + 1)) != 0u) && __ballot((m1m & upto(l - 1)) != 0u);
+                    ok = ok && __ballot(mis(1, 2) != 0u) && __ballot(mis(-1, 2) != 0u) && __ballot(mis(1, 3) != 0u) &&
+                         __ballot(mis(-1, 3) != 0u);
+                    if (ok) sub2 |= 1ull << us[t];
                     continue;
                 }
                 exact |= 1ull << us[t];
@@ -325,13 +368,14 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             }
         }
         if (r < a.n)
-            a.sort_key[r] = (((exact | sub1) >> lane) & 1ull) ? a.band_lb_cap + 2
+            a.sort_key[r] = (((exact | sub1 | sub2) >> lane) & 1ull) ? a.band_lb_cap + 2
                                                                : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
-        if (a.ops && r < a.n && (((exact | sub1) >> lane) & 1ull)) {
-            const int k = (int)((sub1 >> lane) & 1ull);   // substitutions (0 or 1; a mismatch scores -4 / 5 maxsub)
+        if (a.ops && r < a.n && (((exact | sub1 | sub2) >> lane) & 1ull)) {
+            // substitutions (0, 1 or 2; a mismatch scores -4 / 5 maxsub)
+            const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull);
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
             a.nops[r] = 1;
             int4* st = (int4*)(a.stats + r);
