@@ -879,13 +879,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
                 // (pair p's header is written by its own q = 0 lane)
                 if (__ballot(bA)) bad_mask |= 1u << p;
                 if (__ballot(bB)) bad_mask |= 1u << (16 + p);
-                if (!TB && __ballot(zA)) pad_mask |= 1u << p;
-                if (!TB && __ballot(zB)) pad_mask |= 1u << (16 + p);
-                if (!TB && __ballot(nnA)) n_mask |= 1u << p;
-                if (!TB && __ballot(nnB)) n_mask |= 1u << (16 + p);
+                if (__ballot(zA)) pad_mask |= 1u << p;
+                if (__ballot(zB)) pad_mask |= 1u << (16 + p);
+                if (__ballot(nnA)) n_mask |= 1u << p;
+                if (__ballot(nnB)) n_mask |= 1u << (16 + p);
             }
         }
-        const int flags = (((bad_mask >> grp) & 1u) ? REGION_BAD_A : 0) | (((bad_mask >> (16 + grp)) & 1u) ? REGION_BAD_B : 0);
+        const unsigned npm = n_mask | pad_mask;   // N, or a byte EDNAFULL does not score (the walk's plain reads have neither)
+        const int flags = (((bad_mask >> grp) & 1u) ? REGION_BAD_A : 0) | (((bad_mask >> (16 + grp)) & 1u) ? REGION_BAD_B : 0) |
+                          (((npm >> grp) & 1u) ? REGION_NP_A : 0) | (((npm >> (16 + grp)) & 1u) ? REGION_NP_B : 0);
 
         // wave-uniform tau range; per lane: boundary and capture steps
         const unsigned tlo = act ? (unsigned)(kBK - dlo) : 0xffffffffu;
@@ -1096,91 +1098,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void n
 // ============================================================================
 // Walk + emit: one wavefront per read (sorted order), latency-bound.
 // ============================================================================
-// The run-based traceback of nw_common.h (walk_runs_wide), written for a
-// wave-uniform state machine: state, i, j live in SGPRs, every lane tests CPL
-// cells of the current run with branch-free lookups, one ballot per round.
-// Same results (runs in end->start order; -1 when the walk leaves the band or
-// needs more than `cap` runs).
-template <int CPL, class Code>
-__device__ int band_walk_runs(const Code& code_at, int La, int Lb, int ei, int ej, unsigned* runs, int cap, int lane) {
-    int nruns = 0, last_type = -1;
-    bool full = false;
-    auto push = [&](int type, int n) {
-        if (n <= 0) return;
-        if (type == last_type) {
-            if (lane == 0) runs[nruns - 1] += (unsigned)n;
-        } else if (nruns < cap) {
-            if (lane == 0) runs[nruns] = ((unsigned)type << 28) | (unsigned)n;
-            ++nruns;
-            last_type = type;
-        } else {
-            full = true;
-        }
-    };
-    if (ei == La && ej < Lb) push(RUN_X, Lb - ej);
-    else if (ej == Lb && ei < La) push(RUN_Y, La - ei);
-    constexpr int W = 64 * CPL;
-    int i = __builtin_amdgcn_readfirstlane(ei), j = __builtin_amdgcn_readfirstlane(ej), state = RUN_M;
-    while (i > 0 && j > 0) {
-        // cells tested: M: (i-1-k, j-1-k); X: (i, j-k); Y: (i-k, j)   (1-based, k = 0..W-1)
-        const int off = state == RUN_M ? 1 : 0;
-        const int dI = state == RUN_X ? 0 : 1, dJ = state == RUN_Y ? 0 : 1;
-        const unsigned gobit = state == RUN_X ? 4u : 8u;
-        int first = CPL, first_best = RUN_M, first_oob = 0;
-        unsigned c[CPL];
-#pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int kk = lane * CPL + u;
-            c[u] = code_at(i - off - dI * kk - 1, j - off - dJ * kk - 1);
-        }
-#pragma unroll
-        for (int u = CPL - 1; u >= 0; --u) {
-            const int kk = lane * CPL + u;
-            const bool valid = i - off - dI * kk >= 1 && j - off - dJ * kk >= 1;
-            const int best = (c[u] & 1u) ? ((c[u] & 2u) ? RUN_X : RUN_Y) : RUN_M;
-            const bool go = state == RUN_M ? best == RUN_M : (c[u] & gobit) == 0u;
-            const bool oob = (c[u] & 16u) != 0u;
-            if (!valid || oob || !go) {
-                first = u;
-                first_oob = valid && oob;
-                first_best = best;
-            }
-        }
-        const unsigned long long m = __ballot(first < CPL);
-        if (m == 0) {
-            push(state, W);
-            if (state != RUN_Y) j -= W;
-            if (state != RUN_X) i -= W;
-            continue;
-        }
-        const int L = (int)__builtin_ctzll(m);
-        const int k0 = L * CPL + __builtin_amdgcn_readlane(first, L);
-        const int nb = __builtin_amdgcn_readlane(first_best, L);
-        if (__builtin_amdgcn_readlane(first_oob, L) || full) return -1;
-        push(state, k0 + 1);
-        if (state != RUN_Y) j -= k0 + 1;
-        if (state != RUN_X) i -= k0 + 1;
-        state = (state == RUN_M) ? nb : RUN_M;
-    }
-    if (i > 0) push(RUN_Y, i);
-    if (j > 0) push(RUN_X, j);
-    return full ? -1 : nruns;
-}
-
-// band_walk_runs specialised per run type (the state is wave-uniform, so each round
-// takes one scalar branch): an M run follows one diagonal (its band membership is
-// uniform, tau falls by 2 per cell); X / Y runs move along a row / column.  Each
+// The run-based traceback (nw_common.h walk_runs_wide) specialised per run type (the state
+// is wave-uniform, so each round takes one scalar branch): an M run follows one diagonal
+// (its band membership is uniform, tau falls by 2 per cell); X / Y runs move along a
+// row / column.  Each
 // lane tests CPL cells; the round's first stop is found with one ballot.  `word(tau,
 // kd)` returns the band dword of anti-diagonal step tau (relative to the stored
 // range) and band diagonal kd; bit positions of read h at sub-step s: Y opens hb,
 // X > Y hb + 4, X opens 16 + hb, M < max(X, Y) 20 + hb, with hb = 8 h + s.
+// tot (optional): [0] M columns, [1] gap columns, [2] the paid gaps' cost (runs opened inside the
+// matrix: O + (k - 1) E; the end overhangs are free) -- a plain read's record without band_emit.
 template <int CPL, int W>
 __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int ei, int ej, int dlo, int tb0, int h,
-                               unsigned* runs, int cap, int lane) {
+                               unsigned* runs, int cap, int lane, int gO = 0, int gE = 0, int* tot = nullptr) {
     int nruns = 0, last_type = -1;
     bool full = false;
-    auto push = [&](int type, int n) {
+    int tm = 0, tg = 0, tp = 0;
+    auto push = [&](int type, int n, bool paid = false) {
         if (n <= 0) return;
+        if (type == RUN_M) tm += n; else tg += n;
+        if (paid) tp += (type == last_type ? 0 : gO - gE) + n * gE;
         if (type == last_type) {
             if (lane == 0) runs[nruns - 1] += (unsigned)n;
         } else if (nruns < cap) {
@@ -1279,7 +1216,7 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
             }
             const unsigned long long m = __ballot(stop != 0u);
             if (m == 0) {
-                push(state, WR);
+                push(state, WR, true);
                 if (isX) j -= WR; else i -= WR;
                 continue;
             }
@@ -1288,7 +1225,7 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
             const int u0 = (int)__builtin_ctz(sL);
             if (((unsigned)__builtin_amdgcn_readlane((int)oob, L) >> u0) & 1u) return -1;
             k0 = L * CPL + u0;
-            push(state, k0 + 1);
+            push(state, k0 + 1, true);
             if (isX) j -= k0 + 1; else i -= k0 + 1;
             state = RUN_M;
         }
@@ -1296,6 +1233,11 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
     }
     if (i > 0) push(RUN_Y, i);
     if (j > 0) push(RUN_X, j);
+    if (tot) {
+        tot[0] = tm;
+        tot[1] = tg;
+        tot[2] = tp;
+    }
     return full ? -1 : nruns;
 }
 
@@ -1490,7 +1432,15 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         rowpos[k] = a.rowpos[k];
     }
     for (int k = tid; k < 17 * 4; k += blockDim.x) sub_lds[k] = a.sub16[k];
-    __syncthreads();
+    int acgt = 1;
+    for (int k = tid; k < La; k += blockDim.x) {
+        const unsigned char c = upcase(a.amp[k]);
+        acgt &= c == 'A' || c == 'C' || c == 'G' || c == 'T';
+    }
+    // a plain read (A C G T against an A C G T amplicon, EDNAFULL): every pair scores +m or -x
+    // (x = 4 m / 5), so a diagonal's sum, and an alignment's identities, follow from its score
+    const int sc5 = a.band_maxsub / 5;
+    const bool amp_acgt = __syncthreads_and(acgt) && a.band_maxsub == 5 * sc5;
     // substitution score of amplicon byte x against read byte y (0 for codes outside EDNAFULL)
     auto sub_of = [&](unsigned char x, unsigned char y) {
         const int cx = lut_lds[x], cy = lut_lds[y];
@@ -1615,9 +1565,14 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         int nruns;
         const int nd = min(ei, ej);
+        const bool plain = amp_acgt && !(hdr.z & (h ? (REGION_BAD_B | REGION_NP_B) : (REGION_BAD_A | REGION_NP_A)));
+        // a plain read's diagonal sums to m nd - (m + x) k for its k mismatches: a score not of that
+        // form cannot be the diagonal's (reads with an indel: the test's loop is skipped)
+        const int dres = a.band_maxsub * nd - score;
+        const bool maybe_diag = !plain || (dres >= 0 && dres % (9 * sc5) == 0);
         int dsum = 0;
         unsigned cnt = 0u;   // identical | similar << 10 | gap columns << 20 of the diagonal (band_emit's counts)
-        for (int t = lane; t < nd; t += 64) {
+        for (int t = lane; maybe_diag && t < nd; t += 64) {
             const unsigned char ca = amp_lds[ei - 1 - t], cb = rbuf[mis + ej - 1 - t];
             const int sc = sub_of(ca, cb);
             dsum += sc;
@@ -1626,7 +1581,7 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
             const bool sim = !gapc && (id || sc > 0);
             cnt += (unsigned)id | ((unsigned)sim << 10) | ((unsigned)gapc << 20);
         }
-        const bool diag = wave_sum(dsum) == score;
+        const bool diag = maybe_diag && wave_sum(dsum) == score;
         if (diag) {
             const bool endg = (ei == La && ej < Lb) || (ej == Lb && ei < La);
             const int lead = max(ei, ej) - nd;   // leading gap run (Y when ei > nd, X when ej > nd)
@@ -1663,8 +1618,30 @@ __global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
         } else {
             const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
             const int tb0 = kBK - dlo + 2 - tau0;
+            int tot[3];
             nruns = band_walk_runs2<NW_BAND_WALK_CPL, W>(bits, a.band_words, La, Lb, ei, ej, dlo, tb0, h, runs,
-                                                         kBandRunsCap, lane);
+                                                         kBandRunsCap, lane, a.gap_open, a.gap_extend, tot);
+            // ops output, plain read: the record from the runs and the score (score = m id - x (M - id) -
+            // paid gaps), no emit pass; similar pairs are the identical ones
+            const int idn = score + tot[2] + 4 * sc5 * tot[0];
+            if (a.ops && plain && nruns >= 0 && idn >= 0 && idn % (9 * sc5) == 0) {
+                lds_fence();
+                store_ops(a, rd, runs, nruns, lane);
+                if (lane == 0) {
+                    Stat r;
+                    r.aln_len = tot[0] + tot[1];
+                    r.n_ident = idn / (9 * sc5);
+                    r.n_sim = r.n_ident;
+                    r.n_gaps = tot[1];
+                    r.score = score;
+                    r.end_i = ei;
+                    r.end_j = ej;
+                    r.flags = 0;
+                    a.stats[rd] = r;
+                }
+                lds_fence();
+                continue;
+            }
         }
         if (nruns < 0) {
             give_up(k, rd, true);

@@ -148,7 +148,9 @@ int lds_bytes_for(int R, int La, int Lb_max, int tb_mode, int wpb);
 int tb_bytes_per_wave(int R, int Lb_max);
 hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
-enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2 };   // band pair header: read has a code outside A C G T N
+// band pair header flags: read A / B has a code outside A C G T N (BAD), or an N or a byte EDNAFULL
+// does not score (NP: not a plain read for the walk's shortcuts)
+enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2, REGION_NP_A = 8, REGION_NP_B = 16 };
 
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
