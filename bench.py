@@ -54,6 +54,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md "Wave scheduling")
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
+VOP3P_ISSUE_CEILING = 1024 * 2.4e9 * 0.22   # measured: packed 16-bit VALU, 8 waves per SIMD
 READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
@@ -879,6 +880,12 @@ def main():
                     "valu_source": summ_src,
                     "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
                     "issue_peak_per_s": VALU_ISSUE_PEAK,
+                    # the measured issue ceiling of the fills' packed (VOP3P) instructions: ~0.22 wave64
+                    # instructions per SIMD per cycle at the ~2.4 GHz GRBM_GUI_ACTIVE shows
+                    "vop3p_ceiling_per_s": VOP3P_ISSUE_CEILING,
+                    "ceiling_frac": (fill_valu / (fill_ms * 1e-3) / VOP3P_ISSUE_CEILING) if fill_valu and fill_ms else None,
+                    "ceiling_source": "profiles/r02_ubench/ubench_issue_rate.txt (v_pk_* at 0.21-0.23 per SIMD-cycle), "
+                                      "clock from profiles/r03s2_v3 GRBM_GUI_ACTIVE / kernel time",
                     "band_cells_per_pass": cells,
                     "band_gcups": cells / (kms * 1e-3) / 1e9,
                     "note": "issue_frac = SQ_INSTS_VALU of one fill<16> launch (PMC, chip total) / its live HIP-event "

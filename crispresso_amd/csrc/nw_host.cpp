@@ -1645,8 +1645,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const char* lu_env = std::getenv("CRISPR_NW_LENS_UP");
     const int lens_up = lu_env ? std::atoi(lu_env) : 1;
     int64_t mx = 1, mn = 0;
+    const char* ba = std::getenv("CRISPR_NW_BASES_APART");   // "1": the group bases in a copy of their own (A/Bs)
+    bool bases_apart = false;
     if (lens_on) {
-        const int64_t need = 8 * ngroups_len;
+        // the group bases and chunk 0's lengths in one copy (the device layout is [bases][lengths])
+        bases_apart = ba && std::atoi(ba) == 1;
+        const int64_t n0 = nchunks > 0 && !bases_apart ? chunks[0].hi - chunks[0].lo : 0;
+        const int64_t need = 8 * ngroups_len + 2 * n0;
         if (need > c->h_lens_cap) {
             if (c->h_lens) (void)hipHostFree(c->h_lens);
             c->h_lens = nullptr;
@@ -1654,10 +1659,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             HIP_OR_FAIL(c, hipHostMalloc((void**)&c->h_lens, (size_t)need, hipHostMallocDefault));
             c->h_lens_cap = need;
         }
-        if (c->d_lens.reserve((size_t)(need + 2 * n + 64)) != hipSuccess)
+        if (c->d_lens.reserve((size_t)(8 * ngroups_len + 2 * n + 64)) != hipSuccess)
             return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
         int64_t* gb = (int64_t*)c->h_lens;
         for (int64_t g = 0; g < ngroups_len; ++g) gb[g] = offsets[g * nw::kLenGroup];
+        std::memcpy(c->h_lens + 8 * ngroups_len, pk->lens + chunks[0].lo, 2 * (size_t)n0);
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p, c->h_lens, (size_t)need, hipMemcpyHostToDevice, c->s_in));
         h2d_bytes += need;
     }
@@ -1699,7 +1705,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             // fewer copies, fewer gaps on the engine (C4 16.9 -> 16.4 ms, C5 17.2 -> 17.0 ms;
             // CRISPR_NW_LENS_UP=0: one lengths copy per chunk)
             const bool lens_apart = lens_up == 1 && nchunks > 1;
-            if (!lens_apart || k == 0) {
+            if ((k > 0 || bases_apart) && (!lens_apart || k == 0)) {   // chunk 0's went with the group bases
                 HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(hi - lo),
                                               hipMemcpyHostToDevice, c->s_in));
                 h2d_bytes += 2 * (hi - lo);
