@@ -61,6 +61,9 @@
 
 #include "nw_common.h"
 
+#ifndef NW_CAND   // classify: exact-copy candidates compared together
+#define NW_CAND 8
+#endif
 #ifndef NW_BAND_WALK_CPL   // gap-run cells per lane and round (a gap run inside the band is < W <= 64 cells)
 #define NW_BAND_WALK_CPL 1
 #endif
@@ -180,7 +183,7 @@ __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W)
 // (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
 __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
 
-constexpr int kCand = 8;   // exact-copy candidates compared together (2 dword loads each in flight)
+constexpr int kCand = NW_CAND; // exact-copy candidates compared together (2 dword loads each in flight)
 
 // Reads of the amplicon's length with ONE substitution (A C G T against A C G T; ops output,
 // an A C G T amplicon of at most 256 bp) need no DP either.  With k mismatches on the main

@@ -189,10 +189,13 @@ def test_multi_ops_96_amplicons(gpu_aligner_factory, oracle, grouped):
         from crispresso_amd.aligner import pack_2bit
         pr = pack_2bit(buf, off)
         if grouped:
-            pk = a.align_multi_ops(amps, pr, None, which)
-            for f in FIELDS + ("flags",):
-                assert np.array_equal(pk.stats[f], ob.stats[f])
-            assert np.array_equal(pk.ops, ob.ops) and np.array_equal(pk.ops_off, ob.ops_off)
+            assert pr.lens is not None
+            for lens in (pr.lens, None):   # nw_align_multi_ops_packed_lens, then nw_align_multi_ops_packed
+                pr.lens = lens
+                pk = a.align_multi_ops(amps, pr, None, which)
+                for f in FIELDS + ("flags",):
+                    assert np.array_equal(pk.stats[f], ob.stats[f])
+                assert np.array_equal(pk.ops, ob.ops) and np.array_equal(pk.ops_off, ob.ops_off)
         else:
             with pytest.raises(NeedleError):
                 a.align_multi_ops(amps, pr, None, which)
