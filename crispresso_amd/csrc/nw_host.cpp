@@ -960,9 +960,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.work_count = aw.fallback_count;
             a.redo_direct = 0;
         }
-        // CRISPR_NW_SKIP_EXACT=1: diagnostics only (wrong results): the chain without the exact kernel
-        const char* sk = std::getenv("CRISPR_NW_SKIP_EXACT");
-        if (!(sk && std::atoi(sk) == 1)) HIP_OR_FAIL(c, launch_work(c, a));
+        HIP_OR_FAIL(c, launch_work(c, a));
         return NW_OK;
     }
     HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs));
@@ -1645,12 +1643,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const char* lu_env = std::getenv("CRISPR_NW_LENS_UP");
     const int lens_up = lu_env ? std::atoi(lu_env) : 1;
     int64_t mx = 1, mn = 0;
-    const char* ba = std::getenv("CRISPR_NW_BASES_APART");   // "1": the group bases in a copy of their own (A/Bs)
-    bool bases_apart = false;
     if (lens_on) {
         // the group bases and chunk 0's lengths in one copy (the device layout is [bases][lengths])
-        bases_apart = ba && std::atoi(ba) == 1;
-        const int64_t n0 = nchunks > 0 && !bases_apart ? chunks[0].hi - chunks[0].lo : 0;
+        const int64_t n0 = nchunks > 0 ? chunks[0].hi - chunks[0].lo : 0;
         const int64_t need = 8 * ngroups_len + 2 * n0;
         if (need > c->h_lens_cap) {
             if (c->h_lens) (void)hipHostFree(c->h_lens);
@@ -1705,7 +1700,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             // fewer copies, fewer gaps on the engine (C4 16.9 -> 16.4 ms, C5 17.2 -> 17.0 ms;
             // CRISPR_NW_LENS_UP=0: one lengths copy per chunk)
             const bool lens_apart = lens_up == 1 && nchunks > 1;
-            if ((k > 0 || bases_apart) && (!lens_apart || k == 0)) {   // chunk 0's went with the group bases
+            if (k > 0 && !lens_apart) {   // chunk 0's went with the group bases
                 HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(hi - lo),
                                               hipMemcpyHostToDevice, c->s_in));
                 h2d_bytes += 2 * (hi - lo);
