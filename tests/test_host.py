@@ -176,3 +176,25 @@ def test_ops_to_dataframe_equals_rows_dataframe():
         got = ops_to_dataframe(ob, amp, buf, off, NameList(names, raw), "ref")
         pd.testing.assert_frame_equal(got, want)
         assert got.index.tolist()[:2] == ["@r:0", "@r:1"]
+
+
+def test_read_lengths16():
+    """nw_read_lengths16 (the lengths nw_align_ops_packed_lens uploads instead of the offsets):
+    np.diff of the offsets as uint16, threads over contiguous ranges; None past 65535 bases."""
+    from crispresso_amd.aligner import pack_2bit, read_lengths16
+
+    rng = np.random.Generator(np.random.PCG64(3))
+    lens = rng.integers(0, 700, 300_000)
+    off = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    off += 123   # a batch that starts mid-buffer
+    got = read_lengths16(off)
+    assert got.dtype == np.uint16 and np.array_equal(got, lens)
+    out = np.empty(len(lens), np.uint16)
+    assert read_lengths16(off, out) is not None and np.array_equal(out, lens)
+    big = off.copy()
+    big[1000:] += 70_000   # read 999 is 70k bases long
+    assert read_lengths16(big) is None
+    assert len(read_lengths16(np.zeros(1, np.int64))) == 0
+    buf, o2 = synth.reads_from(synth.random_amplicon(120, 4), 50, 5)
+    assert np.array_equal(pack_2bit(buf, o2).lens, np.diff(o2))
