@@ -730,7 +730,10 @@ __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long lo
 // diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
 // passes; the others go to tile_list for the traceback pass.
 template <int W, int MODE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void nw_band_fill(const KernelArgs a) {
+#ifndef NW_FILL_WPE
+#define NW_FILL_WPE 6
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1381,7 +1384,10 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
 // next (wider) level.  W >= kBandDiags: they go to the fallback list (W = kBandDiags: the
 // wide level's input; the wide level: the exact int32 kernel's).
 template <int W>
-__global__ __launch_bounds__(512, 8) void nw_band_walk(const KernelArgs a) {
+#ifndef NW_WALK_WPE
+#define NW_WALK_WPE 8
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
