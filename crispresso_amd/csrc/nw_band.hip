@@ -1385,7 +1385,7 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
 // wide level's input; the wide level: the exact int32 kernel's).
 template <int W>
 #ifndef NW_WALK_WPE
-#define NW_WALK_WPE 8
+#define NW_WALK_WPE 6
 #endif
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
