@@ -127,6 +127,35 @@ def dist_setup():
     return rank, local, world, dist
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): start the N ranks as a
+    torch.distributed.run child (one process per GPU, rank r on device r) and relay its exit
+    status.  This process never touches the GPU (nothing GPU-related is imported before this
+    point), so the ranks start from a clean runtime; rank 0 writes the JSON line straight to
+    the inherited stdout."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n} without a launcher: starting {n} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.run(cmd, env=dict(os.environ, CRISPR_BENCH_LAUNCHED="1")).returncode
+
+
+def ranks_seen(dist):
+    """Ranks that reached this point (a sum over the process group), 1 without one."""
+    if dist is None:
+        return 1
+    import torch
+
+    t = torch.ones(1, dtype=torch.float64)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
 def barrier(dist):
     if dist is not None:
         dist.barrier()
@@ -173,40 +202,61 @@ def pmc_traffic(*prefixes, required=None):
     return None, None
 
 
-def sample_reads(buf, offsets, idx):
-    """Packed sub-batch of reads `idx`."""
-    lens = (offsets[idx + 1] - offsets[idx]).astype(np.int64)
-    off = np.zeros(len(idx) + 1, np.int64)
-    np.cumsum(lens, out=off[1:])
-    parts = [buf[offsets[i]:offsets[i + 1]] for i in idx]
-    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), off
-
-
 def sample_check(amplicon, buf, offsets, ob, every, threads):
     """Every `every`-th read of the timed batch: its record and the rows expanded from its
     runs against the CPU oracle (outside the timed region)."""
-    from crispresso_amd.aligner import OpsBatch
-    from oracle import oracle_py
+    from tests.every_read import check_subset
 
-    n = len(offsets) - 1
-    idx = np.arange(0, n, every, dtype=np.int64)
-    sbuf, soff = sample_reads(buf, offsets, idx)
-    runs = [ob.ops[ob.ops_off[i]:ob.ops_off[i + 1]] for i in idx]
-    sops_off = np.zeros(len(idx) + 1, np.int64)
-    np.cumsum([len(r) for r in runs], out=sops_off[1:])
-    sub = OpsBatch(ob.stats[idx], np.concatenate(runs) if runs else np.zeros(0, np.uint32), sops_off,
-                   np.diff(soff), ob.scale)
-    got = sub.expand(amplicon, sbuf, soff)
-    res, aln = oracle_py.align_batch(amplicon, sbuf, soff, nthreads=threads)
-    bad = np.zeros(len(idx), bool)
-    for f in ("aln_len", "n_ident", "n_sim", "n_gaps", "score", "end_i", "end_j"):
-        bad |= got.stats[f] != res[f]
-    for i in np.flatnonzero(~bad):
-        L = int(res["aln_len"][i])
-        bad[i] = got.aln[i, :, :L].tobytes() != aln[i, :, :L].tobytes()
+    offsets = np.asarray(offsets, dtype=np.int64)
+    idx = np.arange(0, len(offsets) - 1, every, dtype=np.int64)
+    bad = check_subset(amplicon, buf, offsets, ob, idx, threads)
     return {"reads_checked": int(len(idx)), "every": every, "sample_mismatches": int(bad.sum()),
             "what": "record (length, identity, similarity, gaps, score, start cell) and the three rows expanded "
                     "from the runs, vs oracle/nw_oracle.c on the same reads"}
+
+
+def sample_check_multi(amplicons, buf, offsets, which, ob, every, threads):
+    """sample_check of a pooled batch (reads grouped by amplicon): every `every`-th read, each
+    against its own amplicon."""
+    from crispresso_amd.aligner import OpsBatch
+    from tests.every_read import check_subset
+
+    offsets = np.asarray(offsets, dtype=np.int64)
+    idx = np.arange(0, len(offsets) - 1, every, dtype=np.int64)
+    bounds = np.searchsorted(which, np.arange(len(amplicons) + 1))
+    bad = 0
+    for g, amp in enumerate(amplicons):
+        lo, hi = int(bounds[g]), int(bounds[g + 1])
+        sel = idx[(idx >= lo) & (idx < hi)]
+        if not len(sel):
+            continue
+        sub_off = offsets[lo:hi + 1] - offsets[lo]
+        r0, r1 = int(ob.ops_off[lo]), int(ob.ops_off[hi])
+        sub = OpsBatch(ob.stats[lo:hi], ob.ops[r0:r1], ob.ops_off[lo:hi + 1] - r0, np.diff(sub_off), ob.scale)
+        bad += int(check_subset(amp, buf[offsets[lo]:offsets[hi]], sub_off, sub, sel - lo, threads).sum())
+    return {"reads_checked": int(len(idx)), "every": every, "sample_mismatches": bad,
+            "what": "record and the three rows expanded from the runs, each read against its own amplicon, vs "
+                    "oracle/nw_oracle.c"}
+
+
+def sample_check_records(amplicon, buf, offsets, stats, every, threads):
+    """Records of every `every`-th read of a records-only pass (the HDR pass) vs the oracle."""
+    from oracle import oracle_py
+    from tests.every_read import FIELDS
+
+    offsets = np.asarray(offsets, dtype=np.int64)
+    idx = np.arange(0, len(offsets) - 1, every, dtype=np.int64)
+    lens = offsets[idx + 1] - offsets[idx]
+    soff = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(lens, out=soff[1:])
+    sbuf = np.concatenate([buf[offsets[r]:offsets[r + 1]] for r in idx.tolist()]) if len(idx) else np.zeros(1, np.uint8)
+    res, _ = oracle_py.align_batch(amplicon, sbuf, soff, nthreads=threads)
+    bad = np.zeros(len(idx), bool)
+    for f in FIELDS:
+        bad |= stats[f][idx] != res[f]
+    return {"reads_checked": int(len(idx)), "every": every, "sample_mismatches": int(bad.sum()),
+            "what": "records (length, identity, similarity, gaps, score, start cell) of the records-only pass vs "
+                    "oracle/nw_oracle.c"}
 
 
 def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t, share_detail):
@@ -330,7 +380,7 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
     return out
 
 
-def dual_leg(al, n_reads, steps, warmup):
+def dual_leg(al, n_reads, steps, warmup, threads, sample_every):
     """C3: every read against the amplicon (records + runs) and against the HDR
     amplicon (records only: the repair pass reads scores, CORE:1808-1828 with just_score).
     One context: the reads cross PCIe once, 2-bit packed as in the headline
@@ -353,18 +403,24 @@ def dual_leg(al, n_reads, steps, warmup):
     p_lens = _lib.PinnedBuffer(max(n, 1), np.uint16)
     pr = pack_2bit(pb.array, po.array, packed=p_packed.array, lens=p_lens.array)
 
+    state = {}
+
     def step():
         al.set_reference(amp)
-        al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
+        state["ob"] = al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
         al.set_reference(hdr)
         al.align_ops(None, po.array, out=(stats2.array, None, ops_off2.array), resident=True, records_only=True)
 
     dt = timed_calls(None, step, steps, warmup, LEG_WARM_S) / steps
+    checks = None
+    if sample_every:   # the last timed step's outputs, both passes
+        checks = {"amplicon_pass": sample_check(amp, buf, off, state["ob"], sample_every, threads),
+                  "hdr_pass": sample_check_records(hdr, buf, off, stats2.array, sample_every, threads)}
     hdr_better = int((stats2.array["n_ident"] * stats.array["aln_len"] >
                       stats.array["n_ident"] * stats2.array["aln_len"]).sum())
     out = {"metric": "dual-aligned reads/s (C3: 1M reads x amplicon + HDR amplicon, 1 GPU)",
            "value": n / dt, "unit": "reads/s", "ms_per_step": dt * 1e3, "reads": n,
-           "reads_closer_to_hdr": hdr_better,
+           "reads_closer_to_hdr": hdr_better, "sample_check": checks,
            "note": "per step: set the amplicon, nw_align_ops_packed (pinned 2-bit reads in, records + runs out), "
                    "set the HDR amplicon, nw_align_ops_resident on the same reads still in HBM (records out); "
                    "synchronous; packing outside the timed region, as in the headline"}
@@ -487,7 +543,8 @@ def pooled_workload(n_amplicons, reads_per_amplicon, lo=None, hi=None):
     return amps, buf, off, which
 
 
-def pooled_leg(al, rank, world, dist, n_amplicons, reads_per_amplicon, steps, warmup, threads, text_too):
+def pooled_leg(al, rank, world, dist, n_amplicons, reads_per_amplicon, steps, warmup, threads, text_too,
+               sample_every):
     """BASELINE configs[4] (C5: CRISPRessoPooled, 96 amplicons x 100k reads, 150-300 bp, over the
     N GPUs): the reads are split by DP cells (distributed.cell_partition, the same split
     align_pooled_sharded makes; CRISPRessoPooled.py:882-908 ran one CRISPResso per amplicon,
@@ -534,6 +591,8 @@ def pooled_leg(al, rank, world, dist, n_amplicons, reads_per_amplicon, steps, wa
            "mean_read_len": float(lens.mean()), "path_counts": al.path_counts(), "pcie": al.ops_times(),
            "runs_per_read": int(ob.ops_off[n]) / max(n, 1), "input_prep_s": gen_s,
            "algo_bytes_this_rank": int((off[-1] - off[0]) + 3 * outs[0]["aln_len"].astype(np.int64).sum() + 16 * n),
+           "sample_check": (sample_check_multi(amps, buf, off, which, ob, sample_every, threads)
+                            if sample_every else None),
            "note": "step = one nw_align_multi_ops_packed call per rank on its cell_partition range (2-bit reads + "
                    "exceptions in, pinned; every amplicon's tables uploaded once; chunks of one amplicon each); "
                    "barrier + max over ranks"}
@@ -647,6 +706,39 @@ def band_cells(counts, La, mean_len):
             counts["exact_kernel"] * La * mean_len)
 
 
+def dry_run(args, rank, local, world, dist, seen):
+    """--dry-run: the N-rank plumbing without a GPU (CPU tests).  Each rank derives its share of
+    the C2 / C4 / pooled work exactly as a measured run would and reports it; rank 0 prints
+    them all in one line."""
+    from crispresso_amd import synth
+    from crispresso_amd.distributed import cell_partition, pooled_costs
+
+    per_rank_c4 = C4_CALL_READS if world == 1 else C4_TOTAL_READS // world
+    amps = synth.pooled_amplicons(args.pooled_amplicons, 5)
+    lens = np.concatenate([np.diff(synth.native_offsets(a, args.pooled_reads, 100 + g)) for g, a in enumerate(amps)])
+    off_all = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=off_all[1:])
+    which_all = np.repeat(np.arange(len(amps), dtype=np.int32), args.pooled_reads)
+    parts = cell_partition(pooled_costs(amps, off_all, which_all), world)
+    mine = {"rank": rank, "device": local, "c2_reads": args.reads, "c2_seed": 2 if world == 1 else 10 + rank,
+            "c4_reads": per_rank_c4, "pooled_range": list(map(int, parts[rank]))}
+    import torch
+
+    t = torch.tensor([rank, local, mine["c4_reads"], *mine["pooled_range"]], dtype=torch.int64)
+    gathered = [torch.zeros_like(t) for _ in range(world)] if dist is not None else [t]
+    if dist is not None:
+        dist.all_gather(gathered, t)
+    barrier(dist)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": seen,
+                          "ranks": [{"rank": int(g[0]), "device": int(g[1]), "c4_reads": int(g[2]),
+                                     "pooled_range": [int(g[3]), int(g[4])]} for g in gathered],
+                          "c4_reads_total": int(sum(int(g[2]) for g in gathered)),
+                          "pooled_reads_total": int(len(lens))}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -674,14 +766,31 @@ def main():
                     help="tracing: stop after the timed packed calls (no text call, kernel-resident pass or legs)")
     ap.add_argument("--pooled-amplicons", type=int, default=96)
     ap.add_argument("--pooled-reads", type=int, default=100_000, help="C5 reads per amplicon")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check without a GPU: form the world, partition the C4 / pooled work over the ranks, "
+                         "print rank 0's line with \"dry_run\": true; no alignment, no value")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:   # checked before joining the process group
+        log(f"[bench] --gpus {args.gpus} but the launcher formed a world of {world_env} ranks")
+        sys.exit(2)
     rank, local, world, dist = dist_setup()
+    seen = ranks_seen(dist)
+    if seen != world:
+        log(f"[rank {rank}] {seen} of {world} ranks reached the start")
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, local, world, dist, seen)
+        return
     from crispresso_amd import _lib, synth
     from crispresso_amd.aligner import GpuAligner
 
     share, share_detail = cpu_share()
-    threads = args.cpu_threads or share
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    threads = args.cpu_threads or max(1, share // max(1, local_world))   # the ranks of a node share its CPUs
     amplicon = synth.random_amplicon(AMPLICON_LEN, 1)
     seed = 2 if world == 1 else 10 + rank
     t0 = time.perf_counter()
@@ -770,7 +879,8 @@ def main():
                                          0 if args.no_check else 1250)
                 else:
                     multi[name] = pooled_leg(al, rank, world, dist, args.pooled_amplicons, args.pooled_reads,
-                                             args.multi_steps, 1, threads, text_too=world == 1)
+                                             args.multi_steps, 1, threads, text_too=world == 1,
+                                             sample_every=0 if args.no_check else 1000)
             except Exception as exc:
                 multi[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
@@ -782,7 +892,8 @@ def main():
                     al.set_reference(amplicon)
                     legs[name] = e2e_leg(al, amplicon, buf, offsets, threads)
                 elif name == "dual":
-                    legs[name] = dual_leg(al, args.reads, args.steps, args.warmup)
+                    legs[name] = dual_leg(al, args.reads, args.steps, args.warmup, threads,
+                                          0 if args.no_check else args.sample_every)
                 else:
                     legs[name] = merge_leg(local, args.merge_pairs)
             except Exception as exc:
@@ -809,6 +920,7 @@ def main():
             "value": value,
             "unit": "aligned reads/s",
             "n_gpus": world,
+            "ranks_seen": seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,

@@ -302,17 +302,22 @@ class PinnedPool:
     lifetime, up to ``keep_bytes`` of free blocks."""
 
     def __init__(self, keep_bytes: int = 2 << 30):
+        import collections
         import threading
 
         self._free: list = []
         self._keep = keep_bytes
         self._mu = threading.Lock()
+        # blocks handed back by _Lease.__del__: a lock-free hand-off, since a lease can be
+        # finalised by the cyclic GC inside array() while this thread holds _mu
+        self._returned = collections.deque()
 
     def array(self, shape, dtype) -> np.ndarray:
         dtype = np.dtype(dtype)
         count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
         nbytes = max(count * dtype.itemsize, 1)
         with self._mu:
+            self._drain()
             fits = [b for b in self._free if b.nbytes >= nbytes]
             block = min(fits, key=lambda b: b.nbytes) if fits else None
             if block is not None:
@@ -327,17 +332,22 @@ class PinnedPool:
         return raw[: count * dtype.itemsize].view(dtype).reshape(shape)
 
     def _release(self, block: "PinnedBuffer") -> None:
-        with self._mu:
-            self._free.append(block)
-            total = sum(b.nbytes for b in self._free)
-            while total > self._keep and self._free:
-                big = max(self._free, key=lambda b: b.nbytes)
-                self._free.remove(big)
-                total -= big.nbytes
-                big.close()
+        self._returned.append(block)   # no lock (deque.append is atomic); taken in by _drain
+
+    def _drain(self) -> None:
+        """Move returned blocks to the free list, trimmed to keep_bytes (caller holds _mu)."""
+        while self._returned:
+            self._free.append(self._returned.popleft())
+        total = sum(b.nbytes for b in self._free)
+        while total > self._keep and self._free:
+            big = max(self._free, key=lambda b: b.nbytes)
+            self._free.remove(big)
+            total -= big.nbytes
+            big.close()
 
     def free_bytes(self) -> int:
         with self._mu:
+            self._drain()
             return sum(b.nbytes for b in self._free)
 
 

@@ -1713,8 +1713,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
     }
     ht.lap(3);
-    // lengths given: the longest read, and each group's lengths must add up to its offsets
-    // (the device rebuilds the offsets from them: a mismatch would misplace reads)
+    // lengths given: the longest read, and every length must equal its offsets' difference
+    // (the device rebuilds the offsets from the lengths and the group bases, the host expands
+    // the rows from the offsets: a mismatch would make them refer to different bytes)
     if (lens_on) {
         const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 16));
         std::vector<int64_t> pmx((size_t)parts, 1), pbad((size_t)parts, -1);
@@ -1724,13 +1725,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             unsigned a = 1;
             for (int64_t g = g0; g < g1 && pbad[(size_t)q] < 0; ++g) {
                 const int64_t r0 = g * nw::kLenGroup, r1 = std::min(n, r0 + nw::kLenGroup);
-                int64_t sum = 0;
+                int64_t diff = 0;
                 for (int64_t r = r0; r < r1; ++r) {
                     const unsigned l = pk->lens[r];
                     a = l > a ? l : a;
-                    sum += l;
+                    diff |= (int64_t)l ^ (offsets[r + 1] - offsets[r]);
                 }
-                if (sum != offsets[r1] - offsets[r0]) pbad[(size_t)q] = g;
+                if (diff) pbad[(size_t)q] = g;
             }
             pmx[(size_t)q] = a;
         });
@@ -1738,7 +1739,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             mx = std::max(mx, pmx[(size_t)q]);
             if (pbad[(size_t)q] >= 0) {
                 (void)hipStreamSynchronize(c->s_in);   // the queued uploads read the caller's arrays
-                return restore(fail(c, NW_E_INVALID, "lens do not add up to the offsets of reads %lld ..",
+                return restore(fail(c, NW_E_INVALID, "lens differ from the offsets in reads %lld ..",
                                     (long long)(pbad[(size_t)q] * nw::kLenGroup)));
             }
         }

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/crispr_nw.h"
+#include "host_pool.h"
 
 namespace {
 
@@ -88,15 +89,18 @@ extern "C" int nw_pack_reads(const char* reads, const int64_t* offsets, int64_t 
     return NW_OK;
 }
 
-// uint16 read lengths for nw_align_ops_packed_lens: one pass over the offsets, threads on
-// contiguous ranges; NW_E_UNSUPPORTED when a length does not fit (or is negative).
+// uint16 read lengths for nw_align_ops_packed_lens: one pass over the offsets on the host
+// pool (nthreads <= 0: all of its threads; > 0: at most that many parts), contiguous ranges;
+// NW_E_UNSUPPORTED when a length does not fit (or is negative).
 extern "C" int nw_read_lengths16(const int64_t* offsets, int64_t n, uint16_t* lens, int32_t nthreads) {
     if (n < 0 || (n > 0 && (!offsets || !lens))) return NW_E_INVALID;
-    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    nw_host::Pool& pool = nw_host::Pool::get();
+    int nt = nthreads > 0 ? std::min(nthreads, pool.threads()) : pool.threads();
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n >> 16));
     std::vector<char> bad((size_t)nt, 0);
-    auto part = [&](int t) {
-        const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    pool.run(nt, [&](int t) {
+        int64_t lo, hi;
+        nw_host::Pool::range(n, nt, t, &lo, &hi);
         bool b = false;
         for (int64_t r = lo; r < hi; ++r) {
             const int64_t l = offsets[r + 1] - offsets[r];
@@ -104,11 +108,7 @@ extern "C" int nw_read_lengths16(const int64_t* offsets, int64_t n, uint16_t* le
             lens[r] = (uint16_t)l;
         }
         bad[(size_t)t] = b;
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
-    part(0);
-    for (auto& t : th) t.join();
+    });
     for (char b : bad)
         if (b) return NW_E_UNSUPPORTED;
     return NW_OK;

@@ -413,6 +413,16 @@ class AlignArgs:
     # / filter_pe_fastq_by_qual; processed_output_filename is already filtered)
 
 
+def _dtypes_for_concat(df: pd.DataFrame, like: pd.DataFrame) -> pd.DataFrame:
+    """`df` with its all-NA columns cast to `like`'s dtypes, so that pd.concat([like, df])
+    (CRISPRessoCORE.py:1998) gives the dtypes it gives today -- pandas excludes all-NA
+    columns when it picks a concatenation's dtypes (the RC-HDR quirk's NaN repair scores)
+    and has deprecated that -- without depending on the pandas version."""
+    cast = {c: like[c].dtype for c in df.columns
+            if c in like.columns and df[c].dtype != like[c].dtype and df[c].isna().all()}
+    return df.astype(cast) if cast else df
+
+
 def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Optional[GpuAligner] = None,
                 output_dir: Optional[str] = None, database_id: str = "AMPL",
                 rc_hdr_quirk: str = "reference", timings: Optional[dict] = None) -> pd.DataFrame:
@@ -535,7 +545,8 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             df_needle_alignment_rc["align_seq"] = df_needle_alignment_rc["align_seq"].apply(reverse_complement)
             df_needle_alignment_rc["align_str"] = df_needle_alignment_rc["align_str"].apply(lambda x: x[::-1])
             df_needle_alignment_rc.index = map(lambda x: "_".join([x, "RC"]), df_needle_alignment_rc.index)
-            df_needle_alignment = pd.concat([df_needle_alignment, df_needle_alignment_rc])
+            df_needle_alignment = pd.concat([df_needle_alignment, _dtypes_for_concat(df_needle_alignment_rc,
+                                                                                    df_needle_alignment)])
         tm["total_s"] = clock() - t_start
         return df_needle_alignment
     finally:

@@ -239,8 +239,8 @@ int nw_align_ops_packed(nw_ctx* ctx, const uint8_t* packed, const int64_t* offse
 /* nw_align_ops_packed with every read's length as well (lens[r] = offsets[r + 1] -
  * offsets[r], at most 65535; nw_fastq_lens / nw_read_lengths16 produce them): the lengths
  * cross PCIe instead of the offsets (2 B per read instead of 8; the device rebuilds the
- * offsets from them and every 1024th offset).  NW_E_INVALID when the lengths of a group of
- * 1024 reads do not add up to its offsets (checked before any kernel runs). */
+ * offsets from them and every 1024th offset).  NW_E_INVALID when a length differs from its
+ * offsets' difference (checked for every read before any kernel runs). */
 int nw_align_ops_packed_lens(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
                              const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out,
                              int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
@@ -249,7 +249,7 @@ int nw_align_multi_ops_packed_lens(nw_ctx* ctx, const char* refs, const int64_t*
                                    const uint8_t* packed, const int64_t* offsets, const uint16_t* lens,
                                    const int32_t* ref_of_read, int64_t n, const int64_t* exc_pos, const uint8_t* exc_byte,
                                    int64_t n_exc, uint32_t* ops_out, int64_t ops_cap, int64_t* ops_off, nw_stat* stats);
-/* lens[r] = offsets[r + 1] - offsets[r] as uint16 (host, nthreads; <= 0: the host pool):
+/* lens[r] = offsets[r + 1] - offsets[r] as uint16 (host pool; nthreads > 0 caps its parts):
  * NW_E_UNSUPPORTED when a read is longer than 65535 (or offsets decrease). */
 int nw_read_lengths16(const int64_t* offsets, int64_t n, uint16_t* lens, int32_t nthreads);
 /* Pack reads[offsets[0] .. offsets[n]) for nw_align_ops_packed (host, nthreads; <= 0:

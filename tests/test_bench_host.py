@@ -71,3 +71,35 @@ def test_bench_multi_rank_path_is_torch_cuda_free(tmp_path):
         port = s.getsockname()[1]
     mp.start_processes(_bench_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="fork")
     assert (tmp_path / "ok0").read_text() == "2.0" and (tmp_path / "ok1").read_text() == "2.0"
+
+
+def _run_bench(*args, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_launches_n_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher forms a 2-rank world (one process per GPU),
+    every rank takes its share of the C4 / pooled work, and one line comes back."""
+    p = _run_bench("--gpus", "2", "--dry-run", "--pooled-reads", "1000", env_extra={"CRISPR_BENCH_DEVICES": "1"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2
+    assert [r["rank"] for r in d["ranks"]] == [0, 1] and all(r["device"] == 0 for r in d["ranks"])
+    assert d["c4_reads_total"] == 100_000_000 and all(r["c4_reads"] == 50_000_000 for r in d["ranks"])
+    rng = [r["pooled_range"] for r in d["ranks"]]
+    assert rng[0][0] == 0 and rng[0][1] == rng[1][0] and rng[1][1] == d["pooled_reads_total"] == 96_000
+
+
+def test_bench_refuses_a_world_that_is_not_gpus():
+    p = _run_bench("--gpus", "1", "--dry-run", "--pooled-reads", "100",
+                   env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                              "MASTER_PORT": "1"}, timeout=60)
+    assert p.returncode == 2 and "formed a world of 2" in p.stderr

@@ -145,3 +145,25 @@ def test_flash_restatement_reproduces_fixture(fixture, tmp_path):
     assert st["pairs"] == 8906 and st["combined"] == len(fixture["merged_reads"])
     got = [(n, s) for n, s, _ in flash_oracle.read_fastq(str(tmp_path / "out.extendedFrags.fastq.gz"))]
     assert [tuple(x) for x in fixture["merged_reads"]] == [(n, s.decode()) for n, s in got]
+
+
+@pytest.mark.gpu
+def test_e2e_pin_gpu_from_raw_pairs(fixture, tmp_path, gpu_aligner_factory):
+    """The reference's pinned paired-end run (tests/crispresso_tests.py:131-195) from the raw
+    reads, every stage on the GPU: the FLASH merge (CORE:1655-1677) of
+    tests/golden/test_L001_R{1,2}_001.fastq.gz (the reference's own test data) with
+    CRISPResso's options, the alignment of the merged reads (CORE:1788-2000), the
+    quantification (CORE:2014-2067, 428-753) and the summary: the 14 asserted values."""
+    from crispresso_amd.flash import FlashOptions, run_flash
+
+    st = run_flash(os.path.join(HERE, "test_L001_R1_001.fastq.gz"), os.path.join(HERE, "test_L001_R2_001.fastq.gz"),
+                   str(tmp_path), options=FlashOptions(min_overlap=4, max_overlap=100, allow_outies=True))
+    assert st["pairs"] == 8906 and st["combined"] == len(fixture["merged_reads"]) == 8092
+    merged = str(tmp_path / "out.extendedFrags.fastq.gz")
+    args = quant_args(fixture)
+    df = align_reads(AlignArgs(amplicon_seq=fixture["amplicon_seq"]), merged, aligner=gpu_aligner_factory())
+    check_rows(df, fixture)
+    g = quantify.globals_from_args(args)
+    quantify.quantify_alignments(df, args, globals_=g)
+    cuts = quantify.compute_cut_points(args.amplicon_seq, args.guide_seq)
+    assert summary_values(quantify.run_summary(df, g.LEN_AMPLICON, cuts)) == expected(fixture)

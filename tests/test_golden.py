@@ -53,6 +53,11 @@ def check(case, aligner):
     if "score_repaired" in rows[0]:
         cols += ["score_repaired", "score_diff"]
     assert list(df.columns) == cols
+    # the dtypes CORE:1998's pd.concat gives the reference (pandas 2.x: all-NA repair scores
+    # of the RC-HDR quirk do not turn the column into object)
+    for c in ("score_ref", "score_repaired", "score_diff"):
+        if c in cols:
+            assert str(df[c].dtype) == "float64", (case, c, df[c].dtype)
     for (idx, got), want in zip(df.iterrows(), rows):
         for c in cols:
             assert same(got[c], want[c]), (case, idx, c, got[c], want[c])

@@ -1,0 +1,126 @@
+"""Every read of the benchmark workloads against the CPU oracle, through the exact paths
+bench.py times (not a sample): the alignment of CRISPRessoCORE.py:1797-1806 (forward
+pass) and 1812-1828 (HDR pass).
+
+* C2: the headline's 1M-read batch (seed 2) through nw_align_ops_packed_lens (2-bit
+  reads + lengths in, records + runs out);
+* C3: the C3 reads against the amplicon (the same packed call) and, still resident in
+  HBM, against the HDR amplicon (nw_align_ops_resident, with runs and records-only);
+* C5: 96 amplicons x 10k reads in one nw_align_multi_ops_packed_lens call;
+* C4: a 1M-read slice of the C4 generator (native, seed 10: rank 0's shard).
+
+Every read's record (length, identity, similarity, gaps, score, start cell, flags) and
+the three rows expanded from its runs equal the oracle's (tests/every_read.py: the
+oracle runs once per distinct read; duplicates must carry the same GPU output).  These
+cover round 3's certificate paths (one- and two-substitution reads finished in
+classify, the diagonal pass's single-diagonal reads, the walk's plain-read records, the
+128-diagonal wide level) on the workloads that exercise them.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from crispresso_amd import _lib, synth
+from crispresso_amd.aligner import GpuAligner, pack_2bit
+from tests.every_read import every_read, every_read_multi, every_read_records
+
+pytestmark = pytest.mark.gpu
+
+AMPLICON_LEN = 250          # bench.AMPLICON_LEN
+READS = 1_000_000           # bench.READS_PER_GPU
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _pinned_out(n):
+    bufs = (_lib.PinnedBuffer(n, _lib.STAT_DTYPE), _lib.PinnedBuffer(4 * n + 4096, np.uint32),
+            _lib.PinnedBuffer(n + 1, np.int64))
+    return bufs, tuple(b.array for b in bufs)
+
+
+def _packed(buf, off):
+    pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(off)
+    pp = _lib.PinnedBuffer((int(off[-1]) + 3) // 4 + 16, np.uint8)
+    pl = _lib.PinnedBuffer(max(len(off) - 1, 1), np.uint16)
+    pr = pack_2bit(pb.array, po.array, packed=pp.array, lens=pl.array)
+    assert pr.lens is not None   # the lengths path (nw_align_ops_packed_lens), as in the bench
+    return pr, (pb, po, pp, pl)
+
+
+def _close(*groups):
+    for g in groups:
+        for b in g:
+            b.close()
+
+
+@pytest.fixture(scope="module")
+def al():
+    a = GpuAligner(0)
+    yield a
+    a.close()
+
+
+def _assert_clean(res, what):
+    assert res["mismatches"] == 0, f"{what}: {res}"
+    assert res["reads"] > 0
+
+
+def test_c2_every_read(al):
+    amp = synth.random_amplicon(AMPLICON_LEN, 1)
+    buf, off = synth.reads_from(amp, READS, 2)
+    pr, keep = _packed(buf, off)
+    outs, out = _pinned_out(len(off) - 1)
+    al.set_reference(amp)
+    ob = al.align_ops_packed(pr, out=out)
+    counts = al.path_counts()
+    res = every_read(amp, buf, off, ob, THREADS)
+    _assert_clean(res, "C2")
+    # the batch exercises the certificate paths this test is for
+    assert counts["exact_copies"] > 700_000 and counts["band16"] > 0 and counts["band_fallback"] > 0
+    _close(keep, outs)
+
+
+def test_c3_both_passes_every_read(al):
+    amp, hdr, buf, off = synth.c3_workload(READS)
+    pr, keep = _packed(buf, off)
+    n = len(off) - 1
+    outs1, out1 = _pinned_out(n)
+    outs2, out2 = _pinned_out(n)
+    outs3, out3 = _pinned_out(n)
+    al.set_reference(amp)
+    ob1 = al.align_ops_packed(pr, out=out1)
+    _assert_clean(every_read(amp, buf, off, ob1, THREADS), "C3 amplicon pass")
+    al.set_reference(hdr)
+    ob2 = al.align_ops(None, pr.offsets, out=out2, resident=True)
+    _assert_clean(every_read(hdr, buf, off, ob2, THREADS), "C3 HDR pass (resident, runs)")
+    # the bench's form of the HDR pass: records only, resident (right after the packed call)
+    al.set_reference(amp)
+    al.align_ops_packed(pr, out=out1)
+    al.set_reference(hdr)
+    ob3 = al.align_ops(None, pr.offsets, out=(out3[0], None, out3[2]), resident=True, records_only=True)
+    assert every_read_records(ob3.stats, ob2.stats) == 0
+    _close(keep, outs1, outs2, outs3)
+
+
+def test_c5_pooled_every_read(al):
+    from bench import pooled_workload
+
+    amps, buf, off, which = pooled_workload(96, 10_000)
+    pr, keep = _packed(buf, off)
+    pw = _lib.pinned_copy(which)
+    outs, out = _pinned_out(len(off) - 1)
+    ob = al.align_multi_ops(amps, pr, None, pw.array, out=out)
+    res = every_read_multi(amps, buf, off, which, ob, THREADS)
+    _assert_clean(res, "C5")
+    _close(keep, outs, (pw,))
+
+
+def test_c4_slice_every_read(al):
+    amp = synth.random_amplicon(AMPLICON_LEN, 1)
+    buf, off = synth.native_reads(amp, READS, 10)
+    pr, keep = _packed(buf, off)
+    outs, out = _pinned_out(len(off) - 1)
+    al.set_reference(amp)
+    ob = al.align_ops_packed(pr, out=out)
+    _assert_clean(every_read(amp, buf, off, ob, THREADS), "C4 slice (seed 10)")
+    _close(keep, outs)

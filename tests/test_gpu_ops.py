@@ -288,8 +288,9 @@ def test_packed_input_parity(gpu_aligner_factory, oracle, monkeypatch, chunk, le
 
 
 def test_packed_lens_must_match_offsets(gpu_aligner_factory, oracle):
-    """nw_align_ops_packed_lens checks the lengths against the offsets (per 1024-read
-    group) before any kernel runs: a mismatch is NW_E_INVALID, and the context still works."""
+    """nw_align_ops_packed_lens checks every length against its offsets before any kernel
+    runs: a mismatch is NW_E_INVALID (also one that keeps its 1024-read group's sum), and the
+    context still works."""
     from crispresso_amd.aligner import NeedleError, pack_2bit
 
     amp = synth.random_amplicon(200, 71)
@@ -299,9 +300,13 @@ def test_packed_lens_must_match_offsets(gpu_aligner_factory, oracle):
     pr = pack_2bit(buf, off)
     pr.lens = pr.lens.copy()
     pr.lens[3000] += 1
-    with pytest.raises(NeedleError, match="lens do not add up"):
+    with pytest.raises(NeedleError, match="lens differ from the offsets"):
+        a.align_ops_packed(pr)
+    pr.lens[3001] -= 1   # same group sum, two wrong lengths
+    with pytest.raises(NeedleError, match="lens differ from the offsets"):
         a.align_ops_packed(pr)
     pr.lens[3000] -= 1
+    pr.lens[3001] += 1
     assert_same(oracle, amp, buf, off, a.align_ops_packed(pr).expand(amp, buf, off), "lens-after-error")
 
 
@@ -466,3 +471,42 @@ def test_pinned_pool_outputs_are_reused_and_kept(gpu_aligner_factory, oracle):
     assert pool.free_bytes() <= free0 + freed - freed // 2   # ... and the next call leased from it
     assert np.array_equal(third.stats, keep[0]) and np.array_equal(third.ops_off, keep[2])
     assert_same(oracle, amp, buf2, off2, second.expand(amp, buf2, off2), "pool")
+
+
+def test_outputs_fully_written_over_stale_memory(gpu_aligner_factory):
+    """The pinned pool hands out blocks without zeroing them (aligner._outputs): every call
+    must write every record and run offset itself (empty reads included).  Outputs filled
+    with junk first give the same results as zeroed ones, for the text, packed, resident
+    and records-only calls."""
+    from crispresso_amd.aligner import pack_2bit
+
+    amp = synth.random_amplicon(250, 81)
+    buf, off = pack_reads(_reads(amp, 82))
+    n = len(off) - 1
+
+    def outs(fill):
+        st = np.zeros(n, _lib.STAT_DTYPE)
+        ops = np.zeros(4 * n + 4096, np.uint32)
+        oo = np.zeros(n + 1, np.int64)
+        for x in (st, ops, oo):
+            x.view(np.uint8)[...] = fill
+        return st, ops, oo
+
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    pr = pack_2bit(buf, off)
+    for call in ("text", "packed", "resident", "records"):
+        res = []
+        for fill in (0, 0x5A):
+            st, ops, oo = outs(fill)
+            if call == "text":
+                ob = a.align_ops(buf, off, out=(st, ops, oo))
+            elif call == "packed":
+                ob = a.align_ops_packed(pr, out=(st, ops, oo))
+            else:
+                a.align_ops(buf, off)
+                ob = a.align_ops(None, off, out=(st, None if call == "records" else ops, oo), resident=True,
+                                 records_only=call == "records")
+            res.append((ob.stats.copy(), ob.ops_off.copy(), ob.ops.copy()))
+        (s0, o0, r0), (s1, o1, r1) = res
+        assert np.array_equal(s0, s1) and np.array_equal(o0, o1) and np.array_equal(r0, r1), call
