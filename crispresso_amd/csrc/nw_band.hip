@@ -709,13 +709,13 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
 
 // Virtual DP list of the traceback pass: band_order[0, *band_count) then (diagonal pass
 // on, separate launches) tile_list[0, *tile_count) -- the list-A reads the diagonal pass
-// handed on.  (Merged launch, a.tile_to_redo: those go to the next level instead.)
+// handed on.
 // The wide level (a.band_from_work) reads the exact kernel's work list instead: the reads the
 // narrower levels gave up on, then (direct hand-off) the first level's redo list; there
 // a.band_count = a.work_count.
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
     if (a.band_from_work) return exact_work_count(a);
-    return (long long)*a.band_count + (a.tile_count && !a.tile_to_redo ? (long long)*a.tile_count : 0ll);
+    return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
     if (a.band_from_work) return k < nb ? a.work_list[k] : (long long)a.redo_list[k - nb];
@@ -778,8 +778,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    // list A (the diagonal pass) and the band list (the traceback fill): wave work items of
-    // kBPW pairs each, list A's first in the merged launch
+    // list A (the diagonal pass, MODE 0) or the band list (the traceback fill, MODE 1): wave
+    // work items of kBPW pairs each
     const int NW = a.band_words;
     const long long cntA = MODE != 1 ? (long long)*a.count_a : 0ll;
     const long long pA = (cntA + 1) / 2;
@@ -1095,9 +1095,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     };
     for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nA + nB; wv += (long long)gridDim.x * wpb) {
         if constexpr (MODE == 0) body(std::false_type{}, wv);
-        else if constexpr (MODE == 1) body(std::true_type{}, wv);
-        else if (wv < nA) body(std::false_type{}, wv);
-        else body(std::true_type{}, wv - nA);
+        else body(std::true_type{}, wv);
     }
 }
 
@@ -1418,7 +1416,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
         fb_n = 0;
     };
     auto give_up = [&](long long k, long long rd, bool retry) {
-        if (a.band_last) retry = false;
         if (W < kBandDiags && retry && a.redo_flags) {
             // the next level's list keeps the sorted order (nw_band_redo_* compaction):
             // its pairs are reads of similar length, as on this level
@@ -1715,12 +1712,6 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
     if (a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const long long nb = *a.band_count;
     const long long n = band_list_count(a);
-    // merged first-level fill: the diagonal pass's hand-ons lead the redo list (all of the
-    // amplicon's length: consecutive pairs of equal lengths); block b copies its slice
-    const long long nt = a.tile_to_redo && a.tile_count ? (long long)*a.tile_count : 0ll;
-    for (long long t = (long long)blockIdx.x * kRedoBlock + threadIdx.x; t < nt && t < (long long)(blockIdx.x + 1) * kRedoBlock;
-         t += blockDim.x)
-        a.redo_list[t] = a.tile_list[t];
     const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
     int f[4], s = 0;
 #pragma unroll
@@ -1736,13 +1727,13 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
         if (threadIdx.x == 0) sh[0] = (int)e;
     }
     __syncthreads();
-    long long pos = nt + sh[0] + local;
+    long long pos = sh[0] + local;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
         if (f[t]) a.redo_list[pos++] = (int32_t)band_list_read(a, k0 + t, nb);
     if (threadIdx.x == 0) {
         if (sh[1]) a.fallback_count[3] = 1;
-        if (blockIdx.x == gridDim.x - 1) *a.redo_count = (int32_t)(nt + sh[0] + total);
+        if (blockIdx.x == gridDim.x - 1) *a.redo_count = (int32_t)(sh[0] + total);
     }
 }
 
@@ -1795,12 +1786,8 @@ int64_t band_lookback_words(int64_t n) {
 }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill, bool merged) {
-    if (merged && W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, 2>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
-    else if (merged)
-        hipLaunchKernelGGL((nw_band_fill<32, 2>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
-    else if (W == 16)
+                       hipEvent_t after_fill) {
+    if (W == 16)
         hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else if (W == 32)
         hipLaunchKernelGGL((nw_band_fill<32, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);

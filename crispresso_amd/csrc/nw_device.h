@@ -37,8 +37,6 @@ struct KernelArgs {
     Stat* stats;               // [n]
     uint8_t* tb_global;        // traceback slabs when they do not fit LDS
     int64_t tb_wave_bytes;
-    int32_t debug_mode;        // 0 = normal; diagnostic builds of the phases: 1 = stop after
-                               // the start-cell search, 2 = stop after the traceback walk
     // exact kernel: reads whose walk failed are appended here (never with full storage)
     int64_t* fallback_list;
     int32_t* fallback_count;
@@ -75,8 +73,6 @@ struct KernelArgs {
     // 1: the merged first-level fill (nw_band_fill<W, 2>: diagonal pass over list A and the
     // traceback fill over band_order in one launch): the reads the diagonal pass hands on go
     // to the next level's redo list (first), not to this level's traceback pass
-    int32_t tile_to_redo;
-    int32_t band_last;             // this level is the last: what it cannot certify goes to the exact kernel
     // > 0: when the first level hands on at most this many reads (*redo_count), the second
     // level's kernels return at once and the exact kernel takes them too (its fallback list,
     // then the redo list): a few hundred reads cost the exact kernel's latency once, less
@@ -104,7 +100,7 @@ struct KernelArgs {
     int32_t end_weight, end_open, end_extend;
     // the latency-bound kernels of a chunk's tail (second band level, exact kernels, the
     // scans) raise their waves' issue priority (s_setprio): they share the SIMDs with the
-    // other chunk's bulk fill, and a chain waits for its tail (CRISPR_NW_PRIO=0: off)
+    // other chunk's bulk fill, and a chain waits for its tail
     int32_t tail_prio;
 };
 
@@ -168,7 +164,7 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
 int64_t band_lookback_words(int64_t n);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill, bool merged = false);
+                       hipEvent_t after_fill);
 // the diagonal pass (nw_band_fill<W, false>) over list A; `pairs`: an upper bound of its pairs
 hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte

@@ -6,8 +6,6 @@
 // copied once, one kernel aligns the whole batch, results come back as the
 // three alignment strings plus per-read statistics.
 #include <hip/hip_runtime.h>
-#include <execinfo.h>
-#include <signal.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -89,7 +87,25 @@ struct Scratch {
 };
 constexpr int kScratchSets = 3;
 constexpr int64_t kDiagMinChunks = 12;
-constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level (region capacity)   // pipelined calls of fewer chunks run without the diagonal pass
+constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level (region capacity)
+
+// Test switches (environment, read per call).  Each forces a path the defaults reach only on
+// particular inputs, so the tests can hold every path to the oracle:
+//   CRISPR_NW_KERNEL     "full": every read through the exact int32 kernel; "diag32": the band
+//                        path without its 16-diagonal level
+//   CRISPR_NW_EXACT      "multi[:grid]": the exact work lists through the multi-wave kernel (the
+//                        first `grid` entries, the rest through the one-wave kernel)
+//   CRISPR_NW_DIAGPASS   "0" / "1": the diagonal pass off / on in every chunk
+//   CRISPR_NW_WIDE       "0": no 128-diagonal level
+//   CRISPR_NW_DIRECT     reads up to which a chunk's first level hands straight to the wide level
+//   CRISPR_NW_ADAPT      "0": no adaptive level choice across chunks
+//   CRISPR_NW_CHUNK, CRISPR_NW_OPS_SLOT, CRISPR_NW_SPILL_WORDS, CRISPR_NW_REGION_MB: sizes
+//                        (chunk reads, runs per slot, spill words, band region MB)
+// and CRISPR_NW_HOST_TIMING=1 (diagnostics: the host's phase split of a call on stderr).
+int diag_pass_env() {   // -1: default, 0 / 1: forced off / on
+    const char* e = std::getenv("CRISPR_NW_DIAGPASS");
+    return e ? (std::atoi(e) != 0) : -1;
+}
 
 struct nw_ctx {
     int device = 0;
@@ -99,7 +115,7 @@ struct nw_ctx {
     Scratch* s = &sc[0];                               // the set launch_range / configure use
     hipStream_t cs = nullptr;                          // the stream launch_range queues on
     hipStream_t cstream[kScratchSets] = {};            // compute stream of each set ([0] = stream)
-    // tail split (ops_call, CRISPR_NW_TAIL): launch_range queues a chunk's first band level on
+    // tail split (ops_call): launch_range queues a chunk's first band level on
     // c->cs, then records split_ev there and moves to split_to for the rest (second level,
     // exact kernel, compaction)
     hipStream_t split_to = nullptr;
@@ -166,7 +182,7 @@ struct nw_ctx {
     int64_t diag_pass_pairs = 0, diag_stride = 0;
     int diag_words = 0, diag_lb_cap = 0;
     unsigned epoch = 0;               // look-back launches so far (each launch uses a new value)
-    int tail_prio = 1;                // KernelArgs::tail_prio (CRISPR_NW_PRIO=0: off)
+    int tail_prio = 1;                // KernelArgs::tail_prio
     bool ran = false;
     // ops output (nw_align_ops / nw_batch_set_output(NW_OUT_OPS)): per-read run slots,
     // spill area, compaction scratch; the pipelined call's copy streams and events
@@ -423,13 +439,8 @@ int configure(nw_ctx* c) {
             break;
         }
     }
-    // traceback in HBM instead of LDS (more wavefronts per CU for a bulk exact list) measured
-    // no faster on the HDR pass (the kernel is VALU-issue bound there): diagnostics only
-    const char* tbe = std::getenv("CRISPR_NW_EXACT_TB");   // "global"
-    if (cfg.tb_mode == nw::TB_LDS_FULL && tbe && std::strcmp(tbe, "global") == 0) {
-        cfg.tb_mode = nw::TB_GLOBAL_FULL;
-        cfg.wpb = 4;
-    }
+    // (traceback in HBM instead of LDS, for more wavefronts per CU on a bulk exact list,
+    // measured no faster on the HDR pass: the kernel is VALU-issue bound there)
     if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, cfg.wpb);
     if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
         return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel", c->lb_max);
@@ -444,8 +455,8 @@ int configure(nw_ctx* c) {
     c->exact_grid = 0;
     // Off by default: at the ~15 reads per 1M C2 reads it is not faster than the one-wave
     // kernel (both are VALU-issue bound), so it serves the long amplicons
-    const char* ex = std::getenv("CRISPR_NW_EXACT");   // "multi": fallbacks through it (tests/diagnostics)
-    if (nw::exact_rows_per_lane(La) > 0 && ex && std::strcmp(ex, "multi") == 0) {
+    const char* ex = std::getenv("CRISPR_NW_EXACT");   // "multi[:grid]": fallbacks through it (tests)
+    if (nw::exact_rows_per_lane(La) > 0 && ex && std::strncmp(ex, "multi", 5) == 0) {
         c->exact_tb_lds = true;
         c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, true);
         c->exact_slab = 0;
@@ -457,8 +468,7 @@ int configure(nw_ctx* c) {
             grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (1ll << 30) / std::max<int64_t>(c->exact_slab, 1)));
             HIP_OR_FAIL(c, c->s->d_tb.reserve((size_t)(c->exact_slab * grid)));
         }
-        if (const char* eg = std::getenv("CRISPR_NW_EXACT_GRID"))   // tests: split the list between the kernels
-            grid = std::max(1, std::min(grid, std::atoi(eg)));
+        if (ex[5] == ':') grid = std::max(1, std::min(grid, std::atoi(ex + 6)));   // split the list between the kernels
         if (c->exact_lds > 0 && c->exact_lds <= kMaxLds) c->exact_grid = grid;
     }
     // -endweight: the band certificate assumes free end gaps; every read goes through
@@ -470,11 +480,11 @@ int configure(nw_ctx* c) {
         HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
         return NW_OK;
     }
-    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" (default) | "full" (tests/diagnostics)
+    const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" (default) | "diag32" | "full" (tests)
     // certified diagonal band (default): scores and biases within int16, amplicon
     // within the band table's alphabet, non-negative gap costs (the certificate)
     c->use_diag = false;
-    const bool want_diag = !kern || std::strcmp(kern, "diag") == 0;
+    const bool want_diag = !kern || std::strncmp(kern, "diag", 4) == 0;
     const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
     if (want_diag && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
         c->gap_open >= c->gap_extend) {
@@ -484,11 +494,8 @@ int configure(nw_ctx* c) {
         c->diag_lb_cap = La + nw::kBandDiags - 1;
         c->diag_words = nw::band_region_words(La, c->lb_max);
         // one level: fill + walk launch configs, region stride and pairs per pass
-        int wide_fill_wpb = 1, wide_walk_wpb = 2;   // CRISPR_NW_WIDE_WPB=f:w (A/Bs)
-        if (const char* e = std::getenv("CRISPR_NW_WIDE_WPB")) {
-            wide_fill_wpb = std::max(1, std::min(8, std::atoi(e)));
-            if (const char* col = std::strchr(e, ':')) wide_walk_wpb = std::max(1, std::min(8, std::atoi(col + 1)));
-        }
+        // (the wide level at 8, 2 or 4 wavefronts per fill block measured slower or no faster)
+        const int wide_fill_wpb = 1, wide_walk_wpb = 2;
         auto level = [&](int W, nw::LaunchCfg& f, nw::LaunchCfg& w, int64_t& stride, int64_t& pass_pairs,
                          int64_t max_pairs = INT64_MAX) -> int {
             f = nw::LaunchCfg{};
@@ -517,8 +524,7 @@ int configure(nw_ctx* c) {
             w.grid = (int)std::max<int64_t>(1, std::min<int64_t>((2 * pp + w.wpb - 1) / w.wpb, (int64_t)c->num_cus * wb));
             return 1;
         };
-        const char* w16 = std::getenv("CRISPR_NW_DIAG16");   // "0": 32-diagonal level only
-        const bool use16 = !(w16 && std::strcmp(w16, "0") == 0) &&
+        const bool use16 = !(kern && std::strcmp(kern, "diag32") == 0) &&
                            level(16, c->diag16_fill, c->diag16_walk, c->diag16_stride, c->diag16_pass_pairs);
         if (!use16) c->diag16_fill.grid = 0;
         if (level(32, c->diag_fill, c->diag_walk, c->diag_stride, c->diag_pass_pairs)) {
@@ -554,39 +560,12 @@ int configure(nw_ctx* c) {
     return NW_OK;
 }
 
-// CRISPR_NW_SEGV_TRACE=1 (diagnostics): a host segmentation fault prints the faulting
-// address and the native backtrace (library offsets: addr2line on the same build) before
-// the process dies as it would have.
-void segv_trace(int sig, siginfo_t* si, void*) {
-    char msg[96];
-    const int len = std::snprintf(msg, sizeof msg, "nw: signal %d at address %p\n", sig, si ? si->si_addr : nullptr);
-    if (len > 0) (void)!write(2, msg, (size_t)len);
-    void* frames[64];
-    backtrace_symbols_fd(frames, backtrace(frames, 64), 2);
-    signal(sig, SIG_DFL);
-    raise(sig);
-}
-
-void maybe_install_segv_trace() {
-    static bool done = false;
-    const char* e = std::getenv("CRISPR_NW_SEGV_TRACE");
-    if (done || !e || std::atoi(e) != 1) return;
-    done = true;
-    struct sigaction sa;
-    std::memset(&sa, 0, sizeof sa);
-    sa.sa_sigaction = segv_trace;
-    sa.sa_flags = SA_SIGINFO;
-    sigaction(SIGSEGV, &sa, nullptr);
-    sigaction(SIGBUS, &sa, nullptr);
-}
-
 }  // namespace
 
 extern "C" {
 
 int nw_create(int device, nw_ctx** out) {
     if (!out) return NW_E_INVALID;
-    maybe_install_segv_trace();
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NW_E_HIP;
@@ -598,14 +577,11 @@ int nw_create(int device, nw_ctx** out) {
     // its packets in order, so a cross-stream wait queued there holds back the other
     // stream too).  Default: s_in first and the third compute stream (the pipelined call's
     // tail stream) last, so those two share: the uploads of a call are all queued before its
-    // first tail packet.  CRISPR_NW_QORDER=0: the round-2 order (s_out shared the first
-    // compute stream's queue: 2.475 vs 2.423 ms per 1M-read call).
-    const char* qo = std::getenv("CRISPR_NW_QORDER");
-    const bool qorder = !(qo && std::atoi(qo) == 0);
-    hipStream_t* order_old[5] = {&c->stream, &c->s_in, &c->cstream[1], &c->cstream[2], &c->s_out};
-    hipStream_t* order_new[5] = {&c->s_in, &c->stream, &c->cstream[1], &c->s_out, &c->cstream[2]};
+    // first tail packet.  (Round 2's order, where s_out shared the first compute stream's
+    // queue: 2.475 vs 2.423 ms per 1M-read call.)
+    hipStream_t* order[5] = {&c->s_in, &c->stream, &c->cstream[1], &c->s_out, &c->cstream[2]};
     bool streams_ok = hipSetDevice(device) == hipSuccess;
-    for (hipStream_t* sp : qorder ? order_new : order_old)
+    for (hipStream_t* sp : order)
         streams_ok = streams_ok && hipStreamCreateWithFlags(sp, hipStreamNonBlocking) == hipSuccess;
     if (!streams_ok || hipEventCreate(&c->ev_h0) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
@@ -788,10 +764,7 @@ hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
 // Everything is queued on c->stream; nothing synchronises.
 int launch_range(nw_ctx* c, int64_t base) {
     c->diag_ran = false;
-    {
-        const char* e = std::getenv("CRISPR_NW_PRIO");
-        c->tail_prio = !(e && std::atoi(e) == 0);
-    }
+    c->tail_prio = true;   // the latency-bound kernels of a chunk's chain at raised issue priority (-1.1 %)
     nw::KernelArgs a{};
     a.reads = c->d_reads.p - c->reads_bias;
     a.offsets = c->d_offsets.p + base;
@@ -834,7 +807,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_opsctl.p, 0, 2 * sizeof(int32_t), c->cs));
         }
     }
-    if (const char* dm = std::getenv("CRISPR_NW_DEBUG_MODE")) a.debug_mode = std::atoi(dm);
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
         if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs) == hipSuccess
@@ -853,9 +825,8 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.lb_status = c->s->d_lb.p;
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
-        const char* dp_env = std::getenv("CRISPR_NW_DIAGPASS");
         const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
-                               !(dp_env && std::atoi(dp_env) == 0);
+                               diag_pass_env() != 0;
         c->diag_ran = diag_pass;
         if (diag_pass) {
             a.order_a = c->s->d_order_a.p;
@@ -863,7 +834,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.tile_list = c->s->d_tile.p;
             a.tile_count = c->s->d_fallback_count.p + 5;
         }
-        const int64_t pairs0 = (c->n + 1) / 2;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
@@ -871,12 +841,9 @@ int launch_range(nw_ctx* c, int64_t base) {
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
         // ranges to the device-side counts.
         const bool two = c->diag16_fill.grid > 0 && !c->skip16;
-        // CRISPR_NW_LEVELS=16: the first level's give-ups go straight to the exact kernel
-        const char* lv = std::getenv("CRISPR_NW_LEVELS");
-        const bool only16 = two && lv && std::strcmp(lv, "16") == 0;
         a.redo_list = c->s->d_redo.p;
         a.redo_count = c->s->d_fallback_count.p + 2;
-        if (two && !only16) a.redo_flags = c->s->d_redo_flags.p;   // the first level's walk writes every position's
+        if (two) a.redo_flags = c->s->d_redo_flags.p;   // the first level's walk writes every position's
         // a chunk whose first level hands on at most `direct` reads skips the second level on
         // the device: the wide level takes them (up to 1/16 of the chunk, as many as its region
         // holds), or without it the exact kernel (1024).  A chunk where more reads need more than
@@ -886,18 +853,12 @@ int launch_range(nw_ctx* c, int64_t base) {
                          ? (int)std::max<int64_t>(1024, std::min<int64_t>(c->n / 16, 2 * c->wide_pairs))
                          : 1024;
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
-        if (!two || only16) direct = 0;
+        if (!two) direct = 0;
         c->redo_direct = direct;
-        // CRISPR_NW_MERGE=1: the diagonal pass and the first level's traceback fill as one
-        // launch (nw_band_fill<16, 2>), the hand-ons leading the second level's redo list.
-        // Measured slower (kernel-resident fill 0.578 vs 0.477 ms per 1M reads; call 2.40 vs
-        // 2.45 ms against the separate launches' ... ), so off by default.
-        const char* mg = std::getenv("CRISPR_NW_MERGE");
-        const bool merged = diag_pass && two && !only16 && c->diag16_pass_pairs >= pairs0 && mg && std::atoi(mg) == 1;
-        a.tile_to_redo = merged ? 1 : 0;
-        for (int lvl = two ? 0 : 1; lvl < (only16 ? 1 : 2); ++lvl) {
+        // (the diagonal pass and the traceback fill as one launch measured slower: kernel-resident
+        // fill 0.578 vs 0.477 ms per 1M reads)
+        for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
-            al.band_last = only16;
             al.redo_direct = lvl == 1 ? direct : 0;
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
@@ -914,15 +875,14 @@ int launch_range(nw_ctx* c, int64_t base) {
                 al.order_a = nullptr;
                 al.tile_list = nullptr;
                 al.tile_count = nullptr;
-            } else if (al.order_a && !merged) {
+            } else if (al.order_a) {
                 HIP_OR_FAIL(c, nw::launch_band_diag(W, al, fc, pairs, c->cs));
             }
             for (int64_t lo = 0; lo < pairs; lo += pp) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
                 ap.band_pair_hi = std::min(pairs, lo + pp);
-                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr,
-                                               first && merged));
+                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
                 if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
             if (first && c->split_to) {   // the latency-bound rest of the chunk on the tail stream
@@ -935,7 +895,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.work_list = a.fallback_list;   // what the 16 / 32 levels could not certify
         a.work_count = c->s->d_fallback_count.p;
         a.redo_direct = direct;
-        if (c->wide_fill.grid > 0 && !only16) {
+        if (c->wide_fill.grid > 0) {
             // the wide level over that list (and, direct hand-off, the first level's redo list):
             // one read pair per wavefront, 128 diagonals: a few fill + walk launches of ~20 us
             // latency where the exact kernel took ~80 us per chunk; its give-ups -> the exact kernel
@@ -946,8 +906,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             aw.order_a = nullptr;
             aw.tile_list = nullptr;
             aw.tile_count = nullptr;
-            aw.tile_to_redo = 0;
-            aw.band_last = 0;
             aw.band_stride = c->wide_stride;
             aw.band_words = c->wide_words;
             aw.band_lb_cap = c->wide_lb_cap;
@@ -981,8 +939,7 @@ int launch_range(nw_ctx* c, int64_t base) {
 // staging[c % 2] while the copy of chunk c - 1's runs may still be in flight).
 int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     chunk = std::max<int64_t>(chunk, 1);
-    int64_t spill_mb = 64;
-    if (const char* e = std::getenv("CRISPR_NW_SPILL_MB")) spill_mb = std::max(1ll, std::atoll(e));
+    const int64_t spill_mb = 64;
     c->ops_slot = nw::kOpsSlot;
     if (const char* e = std::getenv("CRISPR_NW_OPS_SLOT")) c->ops_slot = std::max(1, std::atoi(e));
     c->spill_cap = (spill_mb << 20) / 4;
@@ -1084,7 +1041,7 @@ int ops_events(nw_ctx* c, size_t chunks) {
 int ops_error(nw_ctx* c, int64_t err) {
     if (err & 4) return fail(c, NW_E_HIP, "a device prefix scan waited too long for its predecessor blocks");
     if (err & 2) return fail(c, NW_E_NOMEM, "ops spill area full: reads with more than %d traceback runs need more "
-                                            "than CRISPR_NW_SPILL_MB (%lld MB)", c->ops_slot,
+                                            "than the spill area (%lld MB)", c->ops_slot,
                              (long long)(c->spill_cap * 4 >> 20));
     if (err & 1) return fail(c, NW_E_NOMEM, "ops staging array full");
     return NW_OK;
@@ -1518,21 +1475,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // sizes ramp up and down at both ends of the call (chunk / 4, chunk / 2, ...): the
     // first chunk's upload and the last chunk's records are the pipeline's serial head
     // and tail; every chunk in between is a full chunk
-    // ramp parts as divisors of the chunk, in call order (diagnostics: CRISPR_NW_RAMP_HEAD / _TAIL, e.g. "8:4:2")
-    auto ramp = [&](const char* var, std::vector<int> dflt) {
-        const char* e = std::getenv(var);
-        if (!e) return dflt;
-        std::vector<int> v;
-        for (const char* p = e; *p;) {
-            const int d = std::atoi(p);
-            if (d > 0) v.push_back(d);
-            while (*p >= '0' && *p <= '9') ++p;
-            while (*p && (*p < '0' || *p > '9')) ++p;   // any separator (',' or ':')
-        }
-        return v;
-    };
-    const std::vector<int> ramp_head = ramp("CRISPR_NW_RAMP_HEAD", {4, 2}), ramp_tail = ramp("CRISPR_NW_RAMP_TAIL", {2, 4});
-    const bool tuned_ramp = std::getenv("CRISPR_NW_RAMP_HEAD") || std::getenv("CRISPR_NW_RAMP_TAIL");
+    // (8:4:2 ramps and other chunk sizes measured no faster)
     auto sizes = [&](int64_t len) {
         std::vector<int64_t> v;
         if (len <= chunk) {
@@ -1541,26 +1484,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         std::vector<int64_t> head, tail;
         int64_t left = len;
-        if (!tuned_ramp)   // ramp parts in pairs (one at each end)
-            for (int64_t part : {chunk / 4, chunk / 2}) {
-                if (part >= 1024 && left > 2 * (part + chunk)) {
-                    head.push_back(part);
-                    tail.push_back(part);
-                    left -= 2 * part;
-                }
-            }
-        for (int d : tuned_ramp ? ramp_head : std::vector<int>{}) {
-            const int64_t part = chunk / d;
-            if (part >= 1024 && left > part + 2 * chunk) {
+        for (int64_t part : {chunk / 4, chunk / 2}) {   // ramp parts in pairs (one at each end)
+            if (part >= 1024 && left > 2 * (part + chunk)) {
                 head.push_back(part);
-                left -= part;
-            }
-        }
-        for (auto it = ramp_tail.rbegin(); tuned_ramp && it != ramp_tail.rend(); ++it) {
-            const int64_t part = chunk / *it;
-            if (part >= 1024 && left > part + 2 * chunk) {
                 tail.push_back(part);
-                left -= part;
+                left -= 2 * part;
             }
         }
         for (int64_t x : head) v.push_back(x);
@@ -1624,24 +1552,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_byte.p, pk->exc_byte, (size_t)pk->n_exc, hipMemcpyHostToDevice, c->s_in));
         h2d_bytes += 9 * pk->n_exc;
     }
-    // CRISPR_NW_UPLOAD=1: the first chunk's offsets, then its bases, then every other chunk's
-    // offsets in one copy, then one copy of bases per chunk (half the copies: each copy costs
-    // the engine a gap).  The uploads end ~50 us sooner, but the chunks' compute starts later
-    // and the call ends later (2.38 vs 2.27 ms): the pipeline's compute, not PCIe, sets the
-    // pace of the middle chunks.  Diagnostics only.
-    const char* up_env = std::getenv("CRISPR_NW_UPLOAD");
-    const int upload_mode = up_env ? std::atoi(up_env) : 0;
     // Packed input with the reads' lengths (nw_align_ops_packed_lens): per read its uint16
     // length crosses PCIe instead of its int64 offset (plus every kLenGroup-th offset, once):
     // 2 B instead of 8, 70.5 -> 64.5 MB per 1M C2 reads.  The call is PCIe-bound at the
     // margin (8 MB more upload measured +0.15 ms).  Each chunk's unpack launch rebuilds its
     // offsets (nw::LenSeg); the scan below checks the lengths against the group offsets
-    // before any kernel runs.  CRISPR_NW_LENS=0: the offsets cross instead.
-    const char* lens_env = std::getenv("CRISPR_NW_LENS");
-    const bool lens_on = pk && pk->lens && upload && n > 0 && upload_mode == 0 && !(lens_env && std::atoi(lens_env) == 0);
+    // before any kernel runs.
+    const bool lens_on = pk && pk->lens && upload && n > 0;
     const int64_t ngroups_len = lens_on ? n / nw::kLenGroup + 1 : 0;
-    const char* lu_env = std::getenv("CRISPR_NW_LENS_UP");
-    const int lens_up = lu_env ? std::atoi(lu_env) : 1;
     int64_t mx = 1, mn = 0;
     if (lens_on) {
         // the group bases and chunk 0's lengths in one copy (the device layout is [bases][lengths])
@@ -1666,18 +1584,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     for (int64_t k = 0; upload && k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
-        const bool offs_apart = upload_mode == 1 && nchunks > 1;
-        if (offs_apart && k == 0) {
-            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
-                                          hipMemcpyHostToDevice, c->s_in));
-            h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
-        }
-        if (offs_apart && k == 1) {   // every later chunk's offsets at once
-            HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(n - lo + 1),
-                                          hipMemcpyHostToDevice, c->s_in));
-            h2d_bytes += (int64_t)sizeof(int64_t) * (n - lo + 1);
-        }
-        if (lens_on && lens_up == 1 && k == 1) {   // every later chunk's lengths at once
+        // chunk 0's lengths went with the group bases; every later chunk's in one copy queued
+        // ahead of chunk 1's bases: fewer copies, fewer gaps on the engine (C4 16.9 -> 16.4 ms,
+        // C5 17.2 -> 17.0 ms against one lengths copy per chunk)
+        if (lens_on && k == 1) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(n - lo),
                                           hipMemcpyHostToDevice, c->s_in));
             h2d_bytes += 2 * (n - lo);
@@ -1695,17 +1605,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                           c->s_in));
             h2d_bytes += b1 - b0;
         }
-        if (lens_on) {
-            // chunk 0's lengths, then every later chunk's in one copy queued ahead of chunk 1's bases:
-            // fewer copies, fewer gaps on the engine (C4 16.9 -> 16.4 ms, C5 17.2 -> 17.0 ms;
-            // CRISPR_NW_LENS_UP=0: one lengths copy per chunk)
-            const bool lens_apart = lens_up == 1 && nchunks > 1;
-            if (k > 0 && !lens_apart) {   // chunk 0's went with the group bases
-                HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(hi - lo),
-                                              hipMemcpyHostToDevice, c->s_in));
-                h2d_bytes += 2 * (hi - lo);
-            }
-        } else if (!offs_apart) {
+        if (!lens_on) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p + lo, offsets + lo, sizeof(int64_t) * (size_t)(hi - lo + 1),
                                           hipMemcpyHostToDevice, c->s_in));
             h2d_bytes += (int64_t)sizeof(int64_t) * (hi - lo + 1);
@@ -1814,20 +1714,15 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // two sets overlap a chunk's tail with the next chunk's bulk; a third measured slower
     // (328M vs 306M reads/s at 262144-read chunks, scripts/gpu_sets_sweep.sh)
     const bool several = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1;
-    int nsets = several ? 2 : 1;
-    if (const char* e = std::getenv("CRISPR_NW_SETS")) nsets = std::max(1, std::min(kScratchSets, std::atoi(e)));
-    // chunk k's compaction waits for the copy of the runs two sets back (ev_out[k - nsets]),
-    // recorded only once the host has read that chunk's total: one set cannot pipeline
-    // several chunks (its wait would come before the record)
-    if (several) nsets = std::max(nsets, 2);
-    // tail split (CRISPR_NW_TAIL=1): a chunk's bulk kernels (unpack, classify, sort, first band
-    // level) on compute stream k mod 2, its latency-bound rest (second level, exact kernel,
+    // tail split: a chunk's bulk kernels (unpack, classify, sort, first band level) on compute
+    // stream k mod 2, its latency-bound rest (second level, wide level, exact kernel,
     // compaction) on one tail stream in chunk order, three scratch sets: chunk k + 2's bulk no
-    // longer queues behind chunk k's exact kernel
-    // (C5 pooled call 24.7 -> 21.6 ms, C2 unchanged; CRISPR_NW_TAIL=0: off)
-    bool tail_split = several && kScratchSets >= 3;
-    if (const char* e = std::getenv("CRISPR_NW_TAIL")) tail_split = tail_split && std::atoi(e) != 0;
-    if (tail_split) nsets = 3;
+    // longer queues behind chunk k's tail (C5 pooled call 24.7 -> 21.6 ms, C2 unchanged).
+    // (Chunk k's compaction waits for the copy of the runs a set back, ev_out[k - nsets],
+    // recorded once the host has read that chunk's total: one set cannot pipeline chunks.)
+    static_assert(kScratchSets >= 3, "the tail split needs three scratch sets");
+    const bool tail_split = several;
+    const int nsets = several ? 3 : 1;
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
         configured = -1;
@@ -1855,23 +1750,18 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
     c->diag_off = false;
     // The diagonal pass saves GPU time but adds a launch to every chunk's chain.  The call's
-    // last chunk, whose latency the call waits for at its end, runs without it
-    // (CRISPR_NW_DIAG_TAIL chunks, default 1); every other chunk of an uploading call with it
-    // (with the wide level taking the exact kernel's ~80 us off each chain, the 1M-read C2 call
-    // measured 2.17 ms vs 2.26 without the pass in its 7 chunks).  A resident pass (the C3 HDR
-    // pass, whose list-A reads the pass mostly hands on) keeps round 3's rule: calls of fewer
-    // than kDiagMinChunks chunks run without it.  CRISPR_NW_DIAGPASS=1 / 0: on / off for every
-    // chunk; CRISPR_NW_DIAG_MIN: that chunk threshold (A/Bs).
-    int64_t diag_tail = 1;
-    if (const char* e = std::getenv("CRISPR_NW_DIAG_TAIL")) diag_tail = std::max(0, std::atoi(e));
-    if (nchunks < 2) diag_tail = 0;
+    // last chunk, whose latency the call waits for at its end, runs without it; every other
+    // chunk of an uploading call with it (with the wide level taking the exact kernel's ~80 us
+    // off each chain, the 1M-read C2 call measured 2.17 ms vs 2.26 without the pass in its 7
+    // chunks).  A resident pass (the C3 HDR pass, whose list-A reads the pass mostly hands on)
+    // keeps round 3's rule: calls of fewer than kDiagMinChunks chunks run without it.
+    // CRISPR_NW_DIAGPASS=1 / 0: on / off for every chunk (tests).
+    int64_t diag_tail = nchunks < 2 ? 0 : 1;
     {
-        const char* e = std::getenv("CRISPR_NW_DIAGPASS");
-        const bool forced_on = e && std::atoi(e) == 1;
-        if (forced_on) diag_tail = 0;
-        int64_t min_chunks = upload ? 2 : kDiagMinChunks;
-        if (const char* m = std::getenv("CRISPR_NW_DIAG_MIN")) min_chunks = std::max(0, std::atoi(m));
-        if (!forced_on && nchunks > 1 && nchunks < min_chunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
+        const int forced = diag_pass_env();
+        if (forced == 1) diag_tail = 0;
+        const int64_t min_chunks = upload ? 2 : kDiagMinChunks;
+        if (forced != 1 && nchunks > 1 && nchunks < min_chunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
     }
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
@@ -1880,68 +1770,35 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
     int64_t total = 0, err = 0;
     bool cap_short = false;
-    // Chunk k's runs go back in up to two copies.  When its base (the runs of every earlier
-    // chunk) is known as its records are queued, an estimate of its runs is queued with
-    // them (spec[k] words: the runs per read so far, + 25 %, + 1024), so the copy starts
-    // the moment the chunk is done instead of after the host has read its total; copy_runs
-    // adds what the estimate missed.  Words past the call's total may be written (ops_out
-    // holds ops_cap words; the contents past ops_off[n] are unspecified).
-    // the last chunk's records, offsets and runs written by its compaction kernel straight into
-    // the caller's buffers when they are page-locked (CRISPR_NW_DIRECT_OUT=0: copies as for the
-    // other chunks): no copies and no host round trip after the call's last kernel
-    const char* do_env = std::getenv("CRISPR_NW_DIRECT_OUT");
-    const bool direct_out = !(do_env && std::atoi(do_env) == 0) && nchunks >= 1 && host_mapped(stats) &&
-                            host_mapped(ops_off) && (!ops_out || host_mapped(ops_out));
+    // Chunk k's runs go back once the host has read its total (copy_runs).  (Copying an
+    // estimate of them as soon as the chunk is done measured no gain on the 1M-read call and a
+    // loss on the pooled call's 96 small chunks: not kept.)
+    // The last chunk's records, offsets and runs are written by its compaction kernel straight
+    // into the caller's buffers when they are page-locked: no copies and no host round trip
+    // after the call's last kernel (2.31 -> 2.27 ms per 1M-read call)
+    const bool direct_out = nchunks >= 1 && host_mapped(stats) && host_mapped(ops_off) &&
+                            (!ops_out || host_mapped(ops_out));
     std::vector<char> direct_done((size_t)std::max<int64_t>(nchunks, 1), 0);
-    std::vector<int64_t> spec((size_t)std::max<int64_t>(nchunks, 1), 0), spec_base(spec.size(), 0);
-    int64_t runs_seen = 0, reads_seen = 0;
     auto copy_runs = [&](int64_t k) -> int {
         ht.lap(4);
         HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
         ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
         err |= h[3];
-        const int64_t cb = h[1], tot = h[2], done = direct_done[(size_t)k] ? tot : spec[(size_t)k];
-        if (spec[(size_t)k] > 0 && cb != spec_base[(size_t)k])
-            return fail(c, NW_E_HIP, "chunk %lld: runs base %lld, estimate copied to %lld", (long long)k, (long long)cb,
-                        (long long)spec_base[(size_t)k]);
+        const int64_t cb = h[1], tot = h[2];
         if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
         } else if (cb + tot > ops_cap) cap_short = true;
-        else if (tot > done)
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb + done, c->sc[k % nsets].d_staging.p + done,
-                                          sizeof(uint32_t) * (size_t)(tot - done), hipMemcpyDeviceToHost, c->s_out));
+        else if (tot > 0 && !direct_done[(size_t)k])
+            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)tot,
+                                          hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
         total = cb + tot;
-        runs_seen += tot;
-        reads_seen += chunks[(size_t)k].hi - chunks[(size_t)k].lo;
-        if (ops_out) c->ops_d2h_bytes += 4 * std::max(tot, done);
+        if (ops_out) c->ops_d2h_bytes += 4 * tot;
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
     const int64_t lag = std::max(1, nsets - 1);
-    const char* spec_env = std::getenv("CRISPR_NW_SPEC");   // "1": runs-copy estimates
-    // (measured no gain on the 1M-read call and a loss on the pooled call's 96 small chunks:
-    // CRISPR_NW_SPEC=1 turns it on)
-    const bool spec_on = spec_env && std::atoi(spec_env) == 1;
-    // the runs estimate of chunk j, queued on s_out once its base (`total`, every earlier
-    // chunk read back) is known; s_out has already waited for chunk j's end when j's records
-    // were queued
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
-    const char* er_env = std::getenv("CRISPR_NW_EARLY_RUNS");   // "0": the round-2 order at the call's end
-    const bool early_runs = !(er_env && std::atoi(er_env) == 0);
-    auto spec_copy = [&](int64_t j) -> int {
-        if (!ops_out || !spec_on || j < 0 || j >= nchunks || spec[(size_t)j] > 0) return NW_OK;
-        const double per = reads_seen > 0 ? (double)runs_seen / (double)reads_seen : 2.0;
-        int64_t w = (int64_t)(per * 1.25 * (double)(chunks[(size_t)j].hi - chunks[(size_t)j].lo)) + 1024;
-        w = std::min(w, std::min(ops_cap - total, c->staging_cap));
-        if (w > 0) {
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + total, c->sc[j % nsets].d_staging.p, sizeof(uint32_t) * (size_t)w,
-                                          hipMemcpyDeviceToHost, c->s_out));
-            spec[(size_t)j] = w;
-            spec_base[(size_t)j] = total;
-        }
-        return NW_OK;
-    };
     bool any_diag = false;
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
@@ -2010,7 +1867,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         // the last chunks of a call run without the diagonal pass: their chains' latency (not
         // the GPU's throughput) is what the call waits for at its end, and the pass adds a
-        // launch to the chain (CRISPR_NW_DIAG_TAIL chunks, default 2)
+        // launch to the chain
         c->diag_tail = k >= nchunks - diag_tail;
         // adaptive diagonal pass: when it handed most of a chunk's list A on to the traceback
         // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
@@ -2046,13 +1903,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (k >= lag && (rc = copy_runs(k - lag))) return restore(rc);
         // the last chunk: every earlier chunk's runs are queued ahead of its records, so they
         // copy while it computes (otherwise s_out would hold them behind the last chunk's end)
-        if (k == nchunks - 1 && early_runs)
+        if (k == nchunks - 1)
             for (int64_t j = std::max<int64_t>(0, k - lag + 1); j < k; ++j) {
                 if ((rc = copy_runs(j))) return restore(rc);
                 runs_queued = j + 1;
             }
-        // chunk k - lag + 1's base is known now; below k its records are queued already
-        if (k - lag + 1 < k && (rc = spec_copy(k - lag + 1))) return restore(rc);
         if (!direct_k) {
             HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
             HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
@@ -2061,13 +1916,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                           hipMemcpyDeviceToHost, c->s_out));
         }
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
-        // lag 1: chunk k's own base is known (copy_runs(k - 1) ran above)
-        if (lag == 1 && (rc = spec_copy(k))) return restore(rc);
     }
-    for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k) {
+    for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k)
         if ((rc = copy_runs(k))) return restore(rc);
-        if ((rc = spec_copy(k + 1))) return restore(rc);
-    }
     ht.lap(4);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);

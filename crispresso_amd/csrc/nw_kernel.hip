@@ -309,10 +309,6 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
         int score, ei, ej;   // 1-based start cell
         decode_end(key, La, Lb, &score, &ei, &ej);
 
-        if (args.debug_mode == 1) {
-            if (lane == 0) { Stat z = {}; z.score = score; z.end_i = ei; z.end_j = ej; *st = z; }
-            continue;
-        }
         // ---- traceback in runs ----
         auto nib = [&](int ai, int bj, bool* oob) { return tb.nibble(ai, bj, oob); };
         const int nruns = walk_runs(nib, La, Lb, ei, ej, runs, La + Lb + 8, lane);
@@ -321,10 +317,6 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
             continue;
         }
         lds_fence();
-        if (args.debug_mode == 2) {
-            if (lane == 0) { Stat z = {}; z.score = score; z.aln_len = nruns; *st = z; }
-            continue;
-        }
         // ---- emit strings, forward order ----
         auto sim = [&](int ai, int code) {
             return (int)(signed char)prof_lds[code * 64 * RP + (ai / R) * RP + (ai % R)];

@@ -19,9 +19,8 @@ pytestmark = pytest.mark.gpu
 KERNELS = ["diag", "full"]
 
 
-# the band path's ops-mode variants of the first level: the diagonal pass and the traceback
-# fill in one launch (hand-ons to the second level), and no diagonal pass
-VARIANTS = {"diag-merged": {"CRISPR_NW_MERGE": "1"}, "diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
+# the band path's ops-mode variant without the diagonal pass (what every call's last chunk runs)
+VARIANTS = {"diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
 
 
 @pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")] + [f"{v}/ops" for v in VARIANTS])
@@ -169,9 +168,8 @@ def test_exact_kernel_work_list(gpu_aligner_factory, oracle, monkeypatch, La, ex
     than the amplicon, big indels."""
     monkeypatch.setenv("CRISPR_NW_KERNEL", "full")
     if exact != "wave":
-        monkeypatch.setenv("CRISPR_NW_EXACT", "multi")
-    if exact == "split":   # 7 reads to the multi-wave kernel, the rest to the one-wave kernel
-        monkeypatch.setenv("CRISPR_NW_EXACT_GRID", "7")
+        # split: 7 reads to the multi-wave kernel, the rest to the one-wave kernel
+        monkeypatch.setenv("CRISPR_NW_EXACT", "multi:7" if exact == "split" else "multi")
     amp = synth.random_amplicon(La, 500 + La)
     rng = np.random.Generator(np.random.PCG64(La))
     reads = [amp, amp.lower(), amp[: max(1, La // 2)], "ACGTRYKMSWBDHVNU", "T-C-A" * 3, "N" * 9]
@@ -520,7 +518,7 @@ def test_diag_band_levels(gpu_aligner_factory, oracle, monkeypatch, levels):
     the first level's give-ups after its own list (threshold above / below the batch's
     give-ups: both branches of KernelArgs::redo_direct)."""
     if levels == "32":
-        monkeypatch.setenv("CRISPR_NW_DIAG16", "0")
+        monkeypatch.setenv("CRISPR_NW_KERNEL", "diag32")
     monkeypatch.setenv("CRISPR_NW_DIRECT", {"16+32 direct": "100000", "16+32 direct-small": "1"}.get(levels, "0"))
     amp = synth.random_amplicon(250, 44)
     rng = np.random.Generator(np.random.PCG64(45))
@@ -552,7 +550,7 @@ def test_diag_iupac_in_every_pair_slot(gpu_aligner_factory, oracle, monkeypatch,
     slot of the fill's wavefronts: each must leave the band for the exact kernel
     (the per-pair flag is taken by a ballot that every lane must see)."""
     if levels == "32":
-        monkeypatch.setenv("CRISPR_NW_DIAG16", "0")
+        monkeypatch.setenv("CRISPR_NW_KERNEL", "diag32")
     amp = synth.random_amplicon(250, 7)
     rng = np.random.Generator(np.random.PCG64(71))
     reads = []
