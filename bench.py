@@ -283,10 +283,10 @@ def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t, share_d
     }
 
 
-def kernel_pass(al, buf, offsets, steps, warmup):
-    """The call's kernels + ops compaction on the batch resident in HBM (upload once)."""
-    al.set_output("ops")
-    al.upload(buf, offsets)
+def kernel_pass(al, pr, steps, warmup):
+    """The packed call's kernels + ops compaction on the batch resident in HBM (upload once, in
+    nw_align_ops_packed_lens' layout: classify decodes the 2-bit reads as in the call)."""
+    al.upload_packed(pr)
     for _ in range(warmup):
         al.run_async()
         al.sync()
@@ -427,6 +427,39 @@ def dual_leg(al, n_reads, steps, warmup, threads, sample_every):
     for b in (pb, po, stats, stats2, ops_off, ops_off2, ops, p_packed):
         b.close()
     return out
+
+
+def c1_shape_leg(al, n_reads, steps, warmup, threads, sample_every):
+    """The reference's own read shape at volume (tests/crispresso_tests.py:145-155: 151 bp reads
+    against the 280 bp amplicon; CORE:1791-1806): 1M 151 bp windows of a 280 bp amplicon (seed 6)
+    at uniform offsets with the C2 edit mix (synth.c1_shape_workload), one nw_align_ops_packed
+    call per step as in the headline."""
+    from crispresso_amd import _lib, synth
+
+    t0 = time.perf_counter()
+    amp, buf, off = synth.c1_shape_workload(n_reads)
+    pr, bufs = pack_pinned(buf, off, threads)
+    n = len(off) - 1
+    out = (_lib.PinnedBuffer(n, _lib.STAT_DTYPE), _lib.PinnedBuffer(4 * n + 4096, np.uint32),
+           _lib.PinnedBuffer(n + 1, np.int64))
+    outs = tuple(b.array for b in out)
+    gen_s = time.perf_counter() - t0
+    al.set_reference(amp)
+    state = {}
+
+    def call():
+        state["ob"] = al.align_ops_packed(pr, out=outs)
+
+    dt = timed_calls(None, call, steps, warmup, LEG_WARM_S) / steps
+    res = {"metric": "aligned reads/s (C1 shape: 151 bp reads x 280 bp amplicon, 1 GPU)", "value": n / dt,
+           "unit": "aligned reads/s", "ms_per_step": dt * 1e3, "reads": n, "amplicon_len": len(amp),
+           "path_counts": al.path_counts(), "pcie": al.ops_times(), "input_prep_s": gen_s,
+           "sample_check": sample_check(amp, buf, off, state["ob"], sample_every, threads) if sample_every else None,
+           "note": "reads at uniform offsets 0..129 of the amplicon (La - Lb = -129), C2 edit mix within each "
+                   "window; same call and buffers as the headline (pinned 2-bit reads in, records + runs out)"}
+    for b in bufs + out:
+        b.close()
+    return res
 
 
 LEG_WARM_S = 0.5   # untimed seconds of calls before a leg's timed steps (steady GPU clocks)
@@ -810,7 +843,10 @@ def main():
     p_ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     out = (p_stats.array, p_ops.array, p_off.array)
     if args.kernel_only:
-        kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
+        from crispresso_amd.aligner import pack_2bit
+
+        pr = pack_2bit(pb.array, po.array, nthreads=threads, packed=p_packed.array, lens=p_lens.array)
+        kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup)
         if rank == 0:
             print(json.dumps({"metric": "kernel-resident aligned reads/s (profiling run, not the bench metric)",
                               "value": n / (kms * 1e-3), "kernel_ms": kms, "phases_ms": phases,
@@ -854,7 +890,7 @@ def main():
     ob.expand(amplicon, pb.array, po.array, nthreads=threads)
     expand_s = time.perf_counter() - t1
 
-    kms, phases, counts, algo_bytes, geo = kernel_pass(al, buf, offsets, args.steps, args.warmup)
+    kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup)
     geo["fallback_reads"] = counts["band_fallback"]
     geo["exact_kernel_reads"] = counts["exact_kernel"]
 
@@ -884,13 +920,16 @@ def main():
             except Exception as exc:
                 multi[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
-    legs = {"e2e": None, "dual": None, "merge": None}
+    legs = {"e2e": None, "dual": None, "c1": None, "merge": None}
     if rank == 0 and world == 1 and not args.no_legs:
         for name in legs:
             try:   # informational legs: never cost the bench line
                 if name == "e2e":
                     al.set_reference(amplicon)
                     legs[name] = e2e_leg(al, amplicon, buf, offsets, threads)
+                elif name == "c1":
+                    legs[name] = c1_shape_leg(al, args.reads, args.steps, args.warmup, threads,
+                                              0 if args.no_check else args.sample_every)
                 elif name == "dual":
                     legs[name] = dual_leg(al, args.reads, args.steps, args.warmup, threads,
                                           0 if args.no_check else args.sample_every)
@@ -1011,6 +1050,7 @@ def main():
             "pooled": multi["pooled"],
             "e2e": legs["e2e"],
             "dual_alignment": legs["dual"],
+            "c1_shape": legs["c1"],
             "downstream_quantification": quant,
             "upstream_merge": legs["merge"],
         }

@@ -38,7 +38,7 @@ STAT_DTYPE = np.dtype([(f, "<i4") for f in STAT_FIELDS])
 # Every symbol include/crispr_nw.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "nw_create", "nw_destroy", "nw_last_error", "nw_set_params", "nw_score_scale",
-    "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload",
+    "nw_set_reference", "nw_required_stride", "nw_align_batch", "nw_batch_upload", "nw_batch_upload_packed",
     "nw_batch_run_async", "nw_batch_sync", "nw_batch_download", "nw_batch_algo_bytes",
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
@@ -115,6 +115,7 @@ def load() -> ctypes.CDLL:
         "nw_required_stride": (c_int64, [ctx_p, c_int32]),
         "nw_align_batch": (c_int, [ctx_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
         "nw_batch_upload": (c_int, [ctx_p, c_void_p, c_void_p, c_int64]),
+        "nw_batch_upload_packed": (c_int, [ctx_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64]),
         "nw_batch_run_async": (c_int, [ctx_p]),
         "nw_batch_sync": (c_int, [ctx_p, POINTER(c_float)]),
         "nw_batch_download": (c_int, [ctx_p, c_void_p, c_int64, c_void_p]),

@@ -270,6 +270,18 @@ class GpuAligner:
         self._check(self.lib.nw_batch_upload(self._h, _lib.ptr(buf), _lib.ptr(offsets), len(offsets) - 1),
                     "nw_batch_upload")
 
+    def upload_packed(self, pr: "PackedReads") -> None:
+        """Resident batch in the packed call's layout (nw_batch_upload_packed, ops output):
+        run_async then times the kernels nw_align_ops_packed_lens runs."""
+        if pr.lens is None:
+            raise NeedleError("upload_packed needs the reads' lengths (PackedReads.lens)")
+        self.set_output("ops")
+        n = len(pr.offsets) - 1
+        self._check(self.lib.nw_batch_upload_packed(
+            self._h, _lib.ptr(pr.packed), _lib.ptr(pr.offsets), _lib.ptr(pr.lens), n,
+            _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,
+            len(pr.exc_pos)), "nw_batch_upload_packed")
+
     def run_async(self) -> None:
         self._check(self.lib.nw_batch_run_async(self._h), "nw_batch_run_async")
 

@@ -49,8 +49,7 @@
 //     pair with one dwordx4 per lane;
 //   * ops output: a diagonal pass (nw_band_fill<W, 0>) first aligns the reads of
 //     the amplicon's length without traceback bits and finishes the single-diagonal
-//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, 1>), or,
-//     when both run in one launch (nw_band_fill<W, 2>), the next level's redo list;
+//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, 1>);
 //   * nw_band_walk: one wavefront per read: start cell from the W captures,
 //     certificate, the run-based walk of nw_common.h over the band, strings.
 #include <hip/hip_runtime.h>
@@ -201,7 +200,45 @@ __device__ __forceinline__ unsigned zero_bytes(unsigned x) {   // 0x80 in each z
     return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
 }
 
-__global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
+// Packed input (KernelArgs::pk_words): the 4 bases at batch position p as bytes A C T G (an
+// exception's place reads as A: its read is flagged).  The stream's dword k holds positions
+// pk_pos0 + 16 k .. + 15, 2 bits each; the device copy has a spare dword past its end.
+__device__ __forceinline__ unsigned pk_decode4(const KernelArgs& a, long long p) {
+    const long long q = p - a.pk_pos0;
+    const unsigned* w = a.pk_words + (q >> 4);
+    const unsigned x = __builtin_amdgcn_alignbit(w[1], w[0], (unsigned)(2 * (q & 15))) & 0xffu;
+    const unsigned sel = (x | (x << 6) | (x << 12) | (x << 18)) & 0x03030303u;   // one code per byte
+    return __builtin_amdgcn_perm(0u, 0x47544341u, sel);   // 0 1 2 3 -> 'A' 'C' 'T' 'G'
+}
+
+// pk_decode4 at a 4-aligned position (the four bases sit in one stream dword: one load)
+__device__ __forceinline__ unsigned pk_decode4_al(const KernelArgs& a, long long p) {
+    const long long q = p - a.pk_pos0;
+    const unsigned x = (a.pk_words[q >> 4] >> (unsigned)(2 * (q & 15))) & 0xffu;
+    const unsigned sel = (x | (x << 6) | (x << 12) | (x << 18)) & 0x03030303u;
+    return __builtin_amdgcn_perm(0u, 0x47544341u, sel);
+}
+
+// First exception at or after batch position `pos` in [pk_e0, pk_e1): a 64-ary search by one
+// wavefront (every lane samples a pivot; ~3 dependent loads for a million exceptions).
+__device__ inline long long exc_lower_bound(const KernelArgs& a, long long pos, int lane) {
+    long long lo = a.pk_e0, hi = a.pk_e1;
+    while (hi - lo > 64) {
+        const long long step = (hi - lo + 63) / 64;
+        const long long idx = lo + lane * step;
+        const bool below = idx < hi && a.pk_exc_pos[idx] < pos;
+        const int k = (int)__builtin_popcountll(__ballot(below));   // pivots below pos: lanes 0 .. k - 1
+        const long long nlo = k == 0 ? lo : lo + (long long)(k - 1) * step + 1;
+        hi = min(hi, lo + (long long)k * step);
+        lo = nlo;
+    }
+    const long long idx = lo + lane;
+    const bool below = idx < hi && a.pk_exc_pos[idx] < pos;
+    return lo + (long long)__builtin_popcountll(__ballot(below));
+}
+
+template <bool PK>
+__global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
@@ -239,13 +276,11 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
-    // wavefront batches of 64 reads: lane u holds read r0 + u's offset and length
-    for (long long r0 = ((long long)blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; r0 < a.n;
-         r0 += (long long)gridDim.x * wpb * 64) {
+    // a wavefront batch of the 64 reads r0 .. r0 + 63 (below r_end): lane u holds read r0 + u's
+    // offset and length; exc: the reads holding an exception byte (packed input)
+    auto batch = [&](long long r0, long long r_end, long long my_off, int my_len, bool exc) {
         const long long r = r0 + lane;
-        const long long my_off = r < a.n ? a.offsets[r] : 0;
-        const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
-        unsigned long long cand = __ballot(my_len == La);   // reads of the amplicon's length
+        unsigned long long cand = __ballot(my_len == La && !exc);   // reads of the amplicon's length
         unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull;
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
@@ -275,14 +310,18 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
                     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
                     const long long off = (long long)(((unsigned long long)hi << 32) | lo);
-                    w[t] = *(const uint2*)(a.reads + (off & ~3ll) + 4 * kc);   // 4-aligned dwordx2
-                    sh[t] = (int)(off & 3);
+                    if constexpr (PK) {   // the read's bytes 4 kc .. 4 kc + 3 from the 2-bit stream
+                        raw[t] = pk_decode4(a, off + 4 * kc);
+                    } else {
+                        w[t] = *(const uint2*)(a.reads + (off & ~3ll) + 4 * kc);   // 4-aligned dwordx2
+                        sh[t] = (int)(off & 3);
+                    }
                 }
                 const unsigned am = k4 < nd ? amp_sh[kc] : 0u;
                 const unsigned msk = k4 < nd ? (k4 == nd - 1 ? tail_mask : 0xffffffffu) : 0u;
 #pragma unroll
                 for (int t = 0; t < kCand; ++t) {
-                    raw[t] = __builtin_amdgcn_alignbyte(w[t].y, w[t].x, sh[t]);
+                    if constexpr (!PK) raw[t] = __builtin_amdgcn_alignbyte(w[t].y, w[t].x, sh[t]);
                     diff[t] |= ((raw[t] | 0x20202020u) ^ am) & msk;
                 }
             }
@@ -370,13 +409,13 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 }
             }
         }
-        if (r < a.n)
+        if (r < r_end)
             a.sort_key[r] = (((exact | sub1 | sub2) >> lane) & 1ull) ? a.band_lb_cap + 2
                                                                : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
-        if (a.ops && r < a.n && (((exact | sub1 | sub2) >> lane) & 1ull)) {
+        if (a.ops && r < r_end && (((exact | sub1 | sub2) >> lane) & 1ull)) {
             // substitutions (0, 1 or 2; a mismatch scores -4 / 5 maxsub)
             const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull);
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
@@ -408,6 +447,143 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 for (int t = 0; t < 8; ++t) x = lane == t ? v[t] : x;
                 ((int*)(a.stats + r0 + u))[lane] = x;
             }
+        }
+        // packed input: the bytes of every read that needs the DP (the only reads a later kernel
+        // reads), exactly its own bytes (neighbouring reads' bytes are never written by another
+        // read's wave: no races between blocks); exception bytes follow (below)
+        if constexpr (PK) {
+            // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
+            // before any store (one read per round trip measured 2.7x the byte-input classify)
+            constexpr int kWr = 8;
+            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2) >> lane) & 1ull));
+            uint8_t* dst = const_cast<uint8_t*>(a.reads);
+            while (dp) {
+                long long o[kWr], e[kWr];
+                int rounds = 0;
+#pragma unroll
+                for (int t = 0; t < kWr; ++t) {
+                    o[t] = e[t] = 0;
+                    if (dp) {
+                        const int u = (int)__builtin_ctzll(dp);
+                        dp &= dp - 1;
+                        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+                        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
+                        o[t] = (long long)(((unsigned long long)hi << 32) | lo);
+                        e[t] = o[t] + __builtin_amdgcn_readlane(my_len, u);
+                        const int span = (int)(e[t] - (o[t] & ~3ll));
+                        rounds = max(rounds, (span + 255) >> 8);
+                    }
+                }
+                for (int rd2 = 0; rd2 < rounds; ++rd2) {
+                    unsigned v[kWr];
+#pragma unroll
+                    for (int t = 0; t < kWr; ++t) {
+                        const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
+                        v[t] = p < e[t] ? pk_decode4_al(a, p) : 0u;
+                    }
+#pragma unroll
+                    for (int t = 0; t < kWr; ++t) {
+                        const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
+                        if (p >= e[t]) continue;
+                        if (p >= o[t] && p + 4 <= e[t]) {
+                            *(unsigned*)(dst + p) = v[t];
+                        } else {
+                            for (int b = 0; b < 4; ++b)
+                                if (p + b >= o[t] && p + b < e[t]) dst[p + b] = (uint8_t)(v[t] >> (8 * b));
+                        }
+                    }
+                }
+            }
+        }
+    };
+    if constexpr (!PK) {
+        // wavefront batches of 64 reads, grid-strided
+        for (long long r0 = ((long long)blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; r0 < a.n;
+             r0 += (long long)gridDim.x * wpb * 64) {
+            const long long r = r0 + lane;
+            const long long my_off = r < a.n ? a.offsets[r] : 0;
+            const int my_len = r < a.n ? (int)(a.offsets[r + 1] - my_off) : -1;
+            batch(r0, a.n, my_off, my_len, false);
+        }
+    } else {
+        // block b: the chunk's reads of call group G = call_lo / kLenGroup + b, [bl, bh)
+        __shared__ long long s_off[kLenGroup + 1];
+        __shared__ unsigned char s_exc[kLenGroup];
+        __shared__ long long s_wsum[16];
+        __shared__ long long s_x[2];
+        const long long G = a.pk_call_lo / kLenGroup + blockIdx.x;
+        const long long bl = max(0ll, G * kLenGroup - a.pk_call_lo), bh = min(a.n, (G + 1) * kLenGroup - a.pk_call_lo);
+        const int cnt = (int)(bh - bl), tid = threadIdx.x, wave = tid >> 6;
+        int64_t* offs = const_cast<int64_t*>(a.offsets);
+        if (a.pk_len) {
+            // the offsets from the lengths (nw_align_ops_packed_lens): the group's base offset + an
+            // exclusive scan of the lengths of its reads up to the chunk's end (reads of earlier
+            // chunks in the group included: they are uploaded with the call's first lengths copy)
+            const long long rr = G * kLenGroup + tid - a.pk_call_lo;   // chunk-relative
+            const long long l = rr < bh ? (long long)a.pk_len[G * kLenGroup + tid] : 0ll;
+            long long inc = l;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const long long o = __shfl_up(inc, d, 64);
+                if (lane >= d) inc += o;
+            }
+            if (lane == 63) s_wsum[wave] = inc;
+            __syncthreads();
+            long long o = a.pk_gbase[G] + inc - l;
+            for (int w2 = 0; w2 < wave; ++w2) o += s_wsum[w2];
+            if (rr >= bl && rr < bh) {
+                s_off[rr - bl] = o;
+                offs[rr] = o;
+            }
+            if (rr == bh - 1) {   // the end of the block's last read (the chunk's last: offsets[n])
+                s_off[cnt] = o + l;
+                offs[bh] = o + l;
+            }
+        } else {
+            for (int i = tid; i <= cnt; i += blockDim.x) s_off[i] = a.offsets[bl + i];
+        }
+        // reads holding exception bytes (not certifiable here; every one of them needs the DP)
+        const bool any_exc = a.pk_e1 > a.pk_e0;
+        for (int i = tid; i < kLenGroup; i += blockDim.x) s_exc[i] = 0;
+        __syncthreads();
+        long long x0 = 0, x1 = 0;
+        if (any_exc) {
+            if (wave == 0) {
+                const long long lo_b = exc_lower_bound(a, s_off[0], lane);
+                const long long hi_b = exc_lower_bound(a, s_off[cnt], lane);
+                if (lane == 0) {
+                    s_x[0] = lo_b;
+                    s_x[1] = hi_b;
+                }
+            }
+            __syncthreads();
+            x0 = s_x[0];
+            x1 = s_x[1];
+            for (long long t = x0 + tid; t < x1; t += blockDim.x) {
+                const long long p = a.pk_exc_pos[t];
+                int lo_i = 0, hi_i = cnt - 1;   // the last read starting at or before p
+                while (lo_i < hi_i) {
+                    const int mid = (lo_i + hi_i + 1) >> 1;
+                    if (s_off[mid] <= p) lo_i = mid;
+                    else hi_i = mid - 1;
+                }
+                s_exc[lo_i] = 1;
+            }
+            __syncthreads();
+        }
+        const long long r0 = bl + 64 * wave;
+        if (r0 < bh) {
+            const long long r = r0 + lane;
+            const long long my_off = r < bh ? s_off[r - bl] : 0;
+            const int my_len = r < bh ? (int)(s_off[r - bl + 1] - my_off) : -1;
+            batch(r0, bh, my_off, my_len, r < bh && s_exc[r - bl] != 0);
+        }
+        if (any_exc && x1 > x0) {
+            // after every wave's byte stores (completed: workgroup-scope release), the exception bytes
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            uint8_t* dst = const_cast<uint8_t*>(a.reads);
+            for (long long t = x0 + tid; t < x1; t += blockDim.x) dst[a.pk_exc_pos[t]] = a.pk_exc_byte[t];
         }
     }
 }
@@ -1770,8 +1946,14 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 // classify (exact copies, sort keys) then the segment sort; a.band_count receives the
 // DP count, a.lb_status holds ceil(n / kSegReads) look-back words
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) {
-    hipLaunchKernelGGL(nw_band_classify, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))), dim3(256),
-                       (size_t)(8 * ((a.La + 3) / 4)), s, a);
+    if (a.pk_words) {   // one block per call group of kLenGroup reads the chunk touches
+        const int64_t g0 = a.pk_call_lo / kLenGroup, g1 = (a.pk_call_lo + a.n - 1) / kLenGroup;
+        hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(kLenGroup),
+                           (size_t)(8 * ((a.La + 3) / 4)), s, a);
+    } else {
+        hipLaunchKernelGGL(nw_band_classify<false>, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))),
+                           dim3(256), (size_t)(8 * ((a.La + 3) / 4)), s, a);
+    }
     const int nseg = (int)std::max<int64_t>(1, (a.n + kSegReads - 1) / kSegReads);
     hipLaunchKernelGGL(nw_band_segsort, dim3(nseg), dim3(kSegThreads), (size_t)segsort_lds_bytes(a.band_lb_cap), s, a,
                        epoch);

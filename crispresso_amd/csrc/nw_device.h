@@ -102,6 +102,18 @@ struct KernelArgs {
     // scans) raise their waves' issue priority (s_setprio): they share the SIMDs with the
     // other chunk's bulk fill, and a chain waits for its tail
     int32_t tail_prio;
+    // packed input (nw_align_ops_packed; band path): nw_band_classify decodes the chunk's reads
+    // from the 2-bit stream, rebuilds their offsets from the lengths (pk_len), and writes the
+    // bytes of the reads that need the DP -- the only bytes any later kernel reads -- with their
+    // exception bytes.  Null pk_words: byte input (reads / offsets as uploaded).
+    const uint32_t* pk_words;      // the stream's device copy: dword k = batch positions pk_pos0 + 16 k ..
+    int64_t pk_pos0;               // a multiple of 16
+    const int64_t* pk_exc_pos;     // the call's exceptions (positions ascending, bytes) ...
+    const uint8_t* pk_exc_byte;
+    int64_t pk_e0, pk_e1;          // ... searched in [pk_e0, pk_e1)
+    const uint16_t* pk_len;        // call-indexed read lengths (null: the offsets are in place)
+    const int64_t* pk_gbase;       // offset of read g * kLenGroup
+    int64_t pk_call_lo;            // call index of the chunk's read 0
 };
 
 // Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and

@@ -201,6 +201,14 @@ struct nw_ctx {
     float ops_h2d_ms = 0.0f, ops_compute_ms = 0.0f;
     bool call_done = false;            // the last operation was nw_align_ops: the getters report its counts
     bool resident_ok = false;          // d_reads / d_offsets hold the last nw_align_ops batch
+    // ... or d_packed / d_exc_* / d_offsets (a packed call: classify decodes the reads again)
+    bool resident_packed = false;
+    int64_t resident_n_exc = 0;
+    nw::KernelArgs pkc{};              // the packed-input fields (pk_*) of the chunk launch_range queues next
+    // nw_batch_upload_packed: the batch is the 2-bit stream (classify decodes it, writing only
+    // the DP reads' bytes); the bytes of every read exist once bytes_full (nw_batch_device_ops)
+    bool batch_packed = false, bytes_full = true;
+    int64_t batch_pos0 = 0, batch_base0 = 0, batch_nbytes = 0, batch_n_exc = 0;
     int64_t resident_n = 0, resident_lo = 0, resident_hi = 0;
     int64_t call_counts[4] = {0, 0, 0, 0};
     int64_t call_exact = 0;            // reads of the last call that reached the exact kernel
@@ -724,6 +732,9 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     if (c->out_mode == NW_OUT_ROWS) HIP_OR_FAIL(c, c->d_out.reserve((size_t)std::max<int64_t>(n, 1) * 3 * c->stride));
     HIP_OR_FAIL(c, c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)));
     c->resident_ok = false;
+    c->batch_packed = false;
+    c->bytes_full = true;
+    c->pkc = nw::KernelArgs{};
     if (nbytes) HIP_OR_FAIL(c, hipMemcpyAsync(c->d_reads.p, reads + base, (size_t)nbytes, hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->d_offsets.p, rel.data(), sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, c->stream));
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
@@ -731,6 +742,86 @@ int nw_batch_upload(nw_ctx* c, const char* reads, const int64_t* offsets, int64_
     int rc = configure(c);
     if (rc) return rc;
     if (c->out_mode == NW_OUT_OPS && (rc = ops_reserve(c, n, n))) return rc;
+    c->ran = false;
+    c->call_done = false;
+    return NW_OK;
+}
+
+int nw_batch_upload_packed(nw_ctx* c, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
+                           const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
+    if (c->out_mode != NW_OUT_OPS) return fail(c, NW_E_STATE, "a packed batch needs nw_batch_set_output(NW_OUT_OPS)");
+    if (n <= 0 || !offsets || !packed || !lens || (n_exc > 0 && (!exc_pos || !exc_byte)) || n_exc < 0)
+        return fail(c, NW_E_INVALID, "bad batch");
+    (void)hipSetDevice(c->device);
+    const int La = (int)c->ref.size();
+    int32_t lb_max = 1;
+    int64_t cells = 0;
+    c->read_lens.resize((size_t)n);
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t len = offsets[r + 1] - offsets[r];
+        if (len < 0 || len > 65535 || len != lens[r])
+            return fail(c, NW_E_INVALID, "read %lld: length %lld, lens %u", (long long)r, (long long)len, (unsigned)lens[r]);
+        c->read_lens[(size_t)r] = (int32_t)len;
+        lb_max = std::max<int32_t>(lb_max, (int32_t)len);
+        cells += (int64_t)La * len;
+    }
+    const int64_t base0 = offsets[0], nbytes = offsets[n] - base0;
+    const int64_t P0 = (base0 / 16) * 4, pk_hi = (offsets[n] + 3) / 4, q0 = base0 / 4;
+    const int64_t ngroups = n / nw::kLenGroup + 1;
+    c->n = n;
+    c->lb_max = lb_max;
+    c->cells = cells;
+    c->stride = stride_for(La, lb_max);
+    HIP_OR_FAIL(c, c->d_reads.reserve((size_t)nbytes + 512 + 16));
+    HIP_OR_FAIL(c, c->d_offsets.reserve((size_t)n + 1));
+    HIP_OR_FAIL(c, c->d_stats.reserve((size_t)n));
+    HIP_OR_FAIL(c, c->d_packed.reserve((size_t)(pk_hi - P0) + 64));
+    HIP_OR_FAIL(c, c->d_exc_pos.reserve((size_t)std::max<int64_t>(n_exc, 1)));
+    HIP_OR_FAIL(c, c->d_exc_byte.reserve((size_t)std::max<int64_t>(n_exc, 1)));
+    HIP_OR_FAIL(c, c->d_lens.reserve((size_t)(8 * ngroups + 2 * n + 64)));
+    std::vector<int64_t> gb((size_t)ngroups);
+    for (int64_t g = 0; g < ngroups; ++g) gb[(size_t)g] = offsets[g * nw::kLenGroup];
+    c->resident_ok = false;
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_packed.p + (q0 - P0), packed + q0, (size_t)(pk_hi - q0), hipMemcpyHostToDevice,
+                                  c->stream));
+    if (n_exc) {
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_pos.p, exc_pos, 8 * (size_t)n_exc, hipMemcpyHostToDevice, c->stream));
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->d_exc_byte.p, exc_byte, (size_t)n_exc, hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p, gb.data(), 8 * (size_t)ngroups, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups, lens, 2 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->reads_bias = base0 & ~(int64_t)15;
+    int rc = configure(c);
+    if (rc) return rc;
+    if ((rc = ops_reserve(c, n, n))) return rc;
+    c->batch_packed = true;
+    c->batch_pos0 = 4 * P0;
+    c->batch_base0 = base0;
+    c->batch_nbytes = nbytes;
+    c->batch_n_exc = n_exc;
+    c->pkc = nw::KernelArgs{};
+    nw::LenSeg ls{(const uint16_t*)(c->d_lens.p + 8 * ngroups), (const int64_t*)c->d_lens.p, 0, ngroups, 0, n,
+                  c->d_offsets.p};
+    if (c->use_diag) {   // classify decodes the batch on every run (KernelArgs::pk_*)
+        c->pkc.pk_words = (const uint32_t*)c->d_packed.p;
+        c->pkc.pk_pos0 = 4 * P0;
+        c->pkc.pk_exc_pos = c->d_exc_pos.p;
+        c->pkc.pk_exc_byte = c->d_exc_byte.p;
+        c->pkc.pk_e0 = 0;
+        c->pkc.pk_e1 = n_exc;
+        c->pkc.pk_len = ls.len;
+        c->pkc.pk_gbase = ls.gbase;
+        c->pkc.pk_call_lo = 0;
+        c->bytes_full = false;
+    } else {   // the exact kernels read bytes: unpack once
+        HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, base0, offsets[n], c->d_exc_pos.p,
+                                         c->d_exc_byte.p, 0, n_exc, c->d_reads.p, c->reads_bias, c->stream, &ls));
+        HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+        c->bytes_full = true;
+    }
     c->ran = false;
     c->call_done = false;
     return NW_OK;
@@ -823,6 +914,16 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.sort_key = c->s->d_sort_key.p;
         a.band_count = c->s->d_fallback_count.p + 1;   // the sort writes the DP count here
         a.lb_status = c->s->d_lb.p;
+        // packed input (ops_call): classify decodes the chunk (KernelArgs::pk_*)
+        a.pk_words = c->pkc.pk_words;
+        a.pk_pos0 = c->pkc.pk_pos0;
+        a.pk_exc_pos = c->pkc.pk_exc_pos;
+        a.pk_exc_byte = c->pkc.pk_exc_byte;
+        a.pk_e0 = c->pkc.pk_e0;
+        a.pk_e1 = c->pkc.pk_e1;
+        a.pk_len = c->pkc.pk_len;
+        a.pk_gbase = c->pkc.pk_gbase;
+        a.pk_call_lo = c->pkc.pk_call_lo;
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
         const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
@@ -1166,6 +1267,13 @@ int nw_batch_device_ops(nw_ctx* c, void** d_ops, void** d_ops_off, void** d_stat
     HIP_OR_FAIL(c, hipMemcpy(ctl, c->d_ctl64.p, sizeof ctl, hipMemcpyDeviceToHost));
     int rc = ops_error(c, ctl[3]);
     if (rc) return rc;
+    if (!c->bytes_full) {   // a packed batch: classify wrote the DP reads' bytes only; now every read's
+        HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, c->batch_pos0 / 4, c->batch_base0,
+                                         c->batch_base0 + c->batch_nbytes, c->d_exc_pos.p, c->d_exc_byte.p, 0,
+                                         c->batch_n_exc, c->d_reads.p, c->reads_bias, c->stream));
+        HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+        c->bytes_full = true;
+    }
     if (d_ops) *d_ops = c->s->d_staging.p;   // one chunk: the call's runs from offset 0
     if (d_ops_off) *d_ops_off = c->d_opsoff.p;
     if (d_stats) *d_stats = c->d_stats.p;
@@ -1516,6 +1624,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->diag_off = false;
         c->diag_tail = false;
         c->exact_small = false;
+        c->pkc = nw::KernelArgs{};
         c->out_mode = mode_before;
         c->n = 0;
         c->s = &c->sc[0];
@@ -1800,6 +1909,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const int64_t lag = std::max(1, nsets - 1);
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
+    // a resident packed batch (nw_align_ops_resident after nw_align_ops_packed): the band path's
+    // classify decodes it again; the exact kernels alone (-endweight, amplicons over 1024 bp)
+    // need its bytes, unpacked once here before any chunk
+    const bool packed_resident = !upload && c->resident_packed && c->use_diag;
+    if (!upload && c->resident_packed && !c->use_diag && n > 0)
+        HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, base0, base0 + nbytes, c->d_exc_pos.p,
+                                         c->d_exc_byte.p, 0, c->resident_n_exc, c->d_reads.p, c->reads_bias, c->stream));
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
     HIP_OR_FAIL(c, hipEventRecord(c->ev_start, c->stream));
@@ -1817,7 +1933,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)k], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
-        if (pk && upload) {   // the chunk's bases -> bytes, then its exception bytes
+        if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
+        c->pkc = nw::KernelArgs{};
+        if (pk && upload && !c->use_diag) {   // the exact kernels read bytes: the chunk's bases -> bytes + exceptions
             const int64_t b0 = offsets[lo], b1 = offsets[hi];
             const int64_t e0 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b0) - pk->exc_pos;
             const int64_t e1 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, b1) - pk->exc_pos;
@@ -1828,8 +1946,27 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             const nw::LenSeg* ls = lens_on ? &lsk : nullptr;
             HIP_OR_FAIL(c, nw::launch_unpack((const uint32_t*)c->d_packed.p, P0, b0, b1, c->d_exc_pos.p, c->d_exc_byte.p,
                                              e0, e1, c->d_reads.p, c->reads_bias, c->cs, ls));
+        } else if ((pk && upload) || packed_resident) {
+            // band path: classify decodes the chunk from the 2-bit stream itself (rebuilding its
+            // offsets from the lengths) and writes only the bytes of the reads that need the DP --
+            // no unpack launch, and 2 bits per base read instead of a byte written and re-read
+            c->pkc.pk_words = (const uint32_t*)c->d_packed.p;
+            c->pkc.pk_pos0 = 4 * P0;
+            c->pkc.pk_exc_pos = c->d_exc_pos.p;
+            c->pkc.pk_exc_byte = c->d_exc_byte.p;
+            if (upload) {
+                c->pkc.pk_e0 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, offsets[lo]) - pk->exc_pos;
+                c->pkc.pk_e1 = std::lower_bound(pk->exc_pos, pk->exc_pos + pk->n_exc, offsets[hi]) - pk->exc_pos;
+            } else {
+                c->pkc.pk_e0 = 0;
+                c->pkc.pk_e1 = c->resident_n_exc;
+            }
+            if (lens_on) {
+                c->pkc.pk_len = (const uint16_t*)(c->d_lens.p + 8 * ngroups_len);
+                c->pkc.pk_gbase = (const int64_t*)c->d_lens.p;
+            }
+            c->pkc.pk_call_lo = lo;
         }
-        if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         any_diag = any_diag || c->use_diag;
         // adaptive first level: when most of the DP reads of the chunks done so far needed the
         // 32-diagonal level (e.g. the HDR pass: a 10-bp block substitution costs two 10-bp gaps
@@ -1955,6 +2092,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
     }
     c->resident_ok = true;   // the batch stays in HBM for nw_align_ops_resident
+    if (upload) {
+        c->resident_packed = pk != nullptr;
+        c->resident_n_exc = pk ? pk->n_exc : 0;
+    }
     c->resident_n = n;
     c->resident_lo = base0;
     c->resident_hi = base0 + nbytes;

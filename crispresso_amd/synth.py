@@ -156,6 +156,42 @@ def c3_workload(n: int = 1_000_000, seed: int = 2) -> Tuple[str, str, np.ndarray
     return amp, hdr, buf, off
 
 
+def window_reads(amplicon: str, n: int, seed: int, read_len: int = 151, mix: Mix = C2_MIX
+                 ) -> Tuple[np.ndarray, np.ndarray]:
+    """Reads shorter than the amplicon (the reference's own test shape: 151 bp reads against the
+    280 bp amplicon, tests/crispresso_tests.py:145-155): read r covers amplicon[s : s + read_len]
+    for an offset s drawn uniformly from 0 .. La - read_len, with the `mix` edits applied to that
+    window (indels at its centre).  Reads of all offsets interleaved (seeded permutation)."""
+    La = len(amplicon)
+    span = La - read_len + 1
+    if span < 1:
+        raise ValueError("read_len exceeds the amplicon")
+    rng = np.random.Generator(np.random.PCG64(seed))
+    s_of = rng.integers(0, span, size=n)
+    counts = np.bincount(s_of, minlength=span)
+    parts = []
+    for s_off in range(span):
+        if counts[s_off]:
+            parts.append(reads_from(amplicon[s_off:s_off + read_len], int(counts[s_off]), seed * 1000 + s_off, mix))
+    lens = np.concatenate([np.diff(o) for _, o in parts])
+    starts = np.concatenate([o[:-1] + base for (_, o), base in
+                             zip(parts, np.cumsum([0] + [len(b) for b, _ in parts[:-1]]))])
+    allbuf = np.concatenate([b for b, _ in parts])
+    perm = rng.permutation(n)
+    lens_p = lens[perm]
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(lens_p, out=off[1:])
+    src = np.repeat(starts[perm], lens_p) + (np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1], lens_p))
+    return np.ascontiguousarray(allbuf[src]), off
+
+
+def c1_shape_workload(n: int = 1_000_000, seed: int = 6) -> Tuple[str, np.ndarray, np.ndarray]:
+    """C1 at volume: 151 bp windows of a 280 bp amplicon (seed 6) with the C2 edit mix."""
+    amp = random_amplicon(280, seed)
+    buf, off = window_reads(amp, n, seed + 1)
+    return amp, buf, off
+
+
 def pooled_amplicons(k: int = 96, seed: int = 5) -> list:
     rng = np.random.Generator(np.random.PCG64(seed))
     lens = rng.integers(150, 301, size=k)

@@ -121,6 +121,14 @@ int nw_align_batch(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64
  * waits and returns the kernel time of the last run measured with HIP events
  * on that stream, download copies results to the host. */
 int nw_batch_upload(nw_ctx* ctx, const char* reads, const int64_t* offsets, int64_t n);
+/* nw_batch_upload for a batch in nw_align_ops_packed_lens' layout (2 bits per base by batch
+ * position + exceptions + uint16 lengths; NW_OUT_OPS only): runs then execute the kernels of
+ * the packed call on the resident batch (classify decodes the reads, rebuilds their offsets
+ * from the lengths and writes the bytes of the reads that need the DP only), so
+ * nw_batch_run_async times exactly the pipelined call's kernels.  nw_batch_device_ops unpacks
+ * every read's bytes first. */
+int nw_batch_upload_packed(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
+                           const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc);
 int nw_batch_run_async(nw_ctx* ctx);
 int nw_batch_sync(nw_ctx* ctx, float* kernel_ms);
 int nw_batch_download(nw_ctx* ctx, char* aln_out, int64_t stride, nw_stat* stats);

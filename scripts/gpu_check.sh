@@ -14,9 +14,10 @@ python3 - "$OUT/bench.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("value", d["value"], "ms", d["ms_per_step"])
-for k in ("c4_shard", "pooled", "dual_alignment", "e2e", "downstream_quantification", "upstream_merge"):
+for k in ("c4_shard", "pooled", "dual_alignment", "c1_shape", "e2e", "downstream_quantification", "upstream_merge"):
     v = d.get(k) or {}
-    print(k, {x: v.get(x) for x in ("value", "ms_per_step") if x in v})
+    print(k, {x: v.get(x) for x in ("value", "ms_per_step", "error") if x in v},
+          (v.get("sample_check") or {}).get("sample_mismatches") if isinstance(v.get("sample_check"), dict) else "")
 print("roofline", {k: d["roofline"].get(k) for k in ("achieved", "frac", "call_frac", "traffic")})
 print("kernel_rate", d.get("kernel_rate", {}).get("kernel_ms"), d.get("sample_check", {}).get("sample_mismatches"))
 PY

@@ -62,7 +62,7 @@ int main() {
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, 0) == hipSuccess) cus = prop.multiProcessorCount;
-    const int iters = 1 << 14, blocks = cus * 4;   // 8 waves per SIMD
+    const int iters = 1 << 18, blocks = cus * 4;   // 8 waves per SIMD; >= 10 ms per launch (the DVFS clock settles)
     unsigned* out;
     (void)hipMalloc(&out, sizeof(unsigned) * 512 * blocks);
     (void)hipMalloc(&g_clk, sizeof(unsigned long long));

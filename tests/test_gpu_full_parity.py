@@ -124,3 +124,15 @@ def test_c4_slice_every_read(al):
     ob = al.align_ops_packed(pr, out=out)
     _assert_clean(every_read(amp, buf, off, ob, THREADS), "C4 slice (seed 10)")
     _close(keep, outs)
+
+
+def test_c1_shape_every_read(al):
+    """The reference's own read shape (151 bp reads, 280 bp amplicon: tests/crispresso_tests.py:145-155)
+    at the offsets bench.py's c1_shape leg uses (synth.c1_shape_workload), 200k reads."""
+    amp, buf, off = synth.c1_shape_workload(200_000)
+    pr, keep = _packed(buf, off)
+    outs, out = _pinned_out(len(off) - 1)
+    al.set_reference(amp)
+    ob = al.align_ops_packed(pr, out=out)
+    _assert_clean(every_read(amp, buf, off, ob, THREADS), "C1 shape")
+    _close(keep, outs)

@@ -510,3 +510,35 @@ def test_outputs_fully_written_over_stale_memory(gpu_aligner_factory):
             res.append((ob.stats.copy(), ob.ops_off.copy(), ob.ops.copy()))
         (s0, o0, r0), (s1, o1, r1) = res
         assert np.array_equal(s0, s1) and np.array_equal(o0, o1) and np.array_equal(r0, r1), call
+
+
+def test_packed_batch_upload_runs_the_call_kernels(gpu_aligner_factory, oracle):
+    """nw_batch_upload_packed: the resident pass over a packed batch (classify decodes the
+    2-bit reads, rebuilds the offsets from the lengths, writes only the DP reads' bytes) gives
+    the oracle's records and runs, run after run; nw_batch_device_ops then holds every read's
+    bytes (the quantification reads them)."""
+    from crispresso_amd.aligner import pack_2bit
+
+    amp = synth.random_amplicon(250, 91)
+    reads = _reads(amp, 92) + ["N" * 250, amp[:100] + "NNN" + amp[103:]]
+    buf, off = pack_reads(reads)
+    n = len(off) - 1
+    # the batch mid-buffer (offsets not starting at 0 or a multiple of 16)
+    full = np.concatenate([np.frombuffer(b"ACGTACG", np.uint8), buf])
+    off7 = off + 7
+    pr = pack_2bit(full, off7)
+    assert len(pr.exc_pos) > 0 and pr.lens is not None
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    a.upload_packed(pr)
+    for _ in range(2):
+        a.run_async()
+        a.sync()
+        ob = a.download_ops(n)
+        assert_same(oracle, amp, buf, off, ob.expand(amp, full, off7), "packed batch upload")
+    from crispresso_amd.devmem import _D2H, hip
+
+    dev = a.device_ops()
+    got = np.zeros(int(off7[-1] - off7[0]), np.uint8)
+    assert hip().hipMemcpy(got.ctypes.data, dev["reads"] + int(off7[0]) - dev["reads_bias"], got.nbytes, _D2H) == 0
+    assert got.tobytes() == bytes(buf).upper()   # the kernels' bytes: upper case, every read
