@@ -277,6 +277,7 @@ class GpuAligner:
             raise NeedleError("upload_packed needs the reads' lengths (PackedReads.lens)")
         self.set_output("ops")
         n = len(pr.offsets) - 1
+        self._buf, self._off = None, pr.offsets
         self._check(self.lib.nw_batch_upload_packed(
             self._h, _lib.ptr(pr.packed), _lib.ptr(pr.offsets), _lib.ptr(pr.lens), n,
             _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,

@@ -263,8 +263,9 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
     const int sc5 = a.band_maxsub / 5;
     // the one-substitution certificate (above): ops output, one 256-byte chunk, EDNAFULL's
     // 5 / -4 scaled, a gap open above the mismatch cost
-    const bool sub1_ok = __syncthreads_and(acgt_amp) && a.ops && nd <= 64 && a.band_maxsub == 5 * sc5 &&
-                         a.gap_open > 4 * sc5 && a.gap_extend >= 0;
+    const bool amp_acgt_all = __syncthreads_and(acgt_amp) != 0;
+    const bool sub1_ok = amp_acgt_all && a.ops && nd <= 64 && a.band_maxsub == 5 * sc5 && a.gap_open > 4 * sc5 &&
+                         a.gap_extend >= 0;
     // two substitutions (x = 9/5 maxsub: a mismatch's loss against a match, D = m La - 2 x): with an
     // internal gap and <= La - 2 pairs O > 2 x - 2 m; La - 1 pairs and two gaps 2 O > 2 x - m, one gap
     // and a mismatch O > x - m; |d| >= 4 m (La - 4) < D: x < 2 m; d = +-1 / +-2 / +-3 need 2 / 1 / 1
@@ -276,6 +277,51 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
+    // Window reads (packed input, ops output): a read shorter than the amplicon that equals one of its
+    // windows amplicon[s, s + Lb) (A C G T, case-insensitive) scores m Lb, the most any alignment can
+    // (pairs <= Lb, each <= m; a gap costs > 0), and every alignment that does is such a window: the
+    // start-cell scan (last column bottom -> top) takes the largest such s, and along its diagonal M =
+    // m j beats X, Y <= m j - O, so the traceback is the diagonal with free end gaps: s amplicon
+    // residues before, La - s - Lb after.  One substitution (D = m (Lb - 1) - x): an alignment with an
+    // internal gap pairs <= Lb residues and pays >= O, <= m Lb - O < D when O > m + x; a single
+    // diagonal pairs its overlap P(d): P <= Lb - 2 scores <= m (Lb - 2) < D (m > x), P = Lb - 1 needs one
+    // mismatch and P = Lb two (checked for every such diagonal, below) -- D is then the unique optimum
+    // and M wins every tie along it (X, Y <= m j - O < m j - m - x <= M).  The window's offset comes from
+    // the read's first (or, for a substitution there, last) 16 bases looked up among the amplicon's
+    // sorted 16-mers (Profile::seed_key).
+    unsigned* amp2s = amp_sh + 2 * nd;
+    const int n2 = (La + 15) / 16 + 2, nseed = a.n_seed;
+    unsigned* skey = amp2s + n2;
+    uint16_t* spos = (uint16_t*)(skey + nseed);
+    const bool win_ok = PK && amp_acgt_all && a.ops && a.band_maxsub == 5 * sc5 && a.gap_extend >= 0 && a.amp2 &&
+                        a.gap_open > xl && nseed > 0 && La <= 1024;
+    if (win_ok) {
+        for (int k = threadIdx.x; k < n2; k += blockDim.x) amp2s[k] = a.amp2[k];
+        for (int k = threadIdx.x; k < nseed; k += blockDim.x) {
+            skey[k] = a.seed_key[k];
+            spos[k] = a.seed_pos[k];
+        }
+        __syncthreads();
+    }
+    // 16 bases of the packed stream from batch position p, and of the amplicon from position p (LDS)
+    auto rword = [&](long long p) -> unsigned {
+        const long long q = p - a.pk_pos0;
+        const unsigned* w = a.pk_words + (q >> 4);
+        return __builtin_amdgcn_alignbit(w[1], w[0], (unsigned)(2 * (q & 15)));
+    };
+    auto aword = [&](int p) -> unsigned {
+        return __builtin_amdgcn_alignbit(amp2s[(p >> 4) + 1], amp2s[p >> 4], (unsigned)(2 * (p & 15)));
+    };
+    // mismatches of read bases [roff + j0, + len) against amplicon [s, s + len), counted up to cap + 1
+    auto mism = [&](long long roff, int j0, int s, int len, int cap) -> int {
+        int cnt = 0;
+        for (int w = 0; w < len && cnt <= cap; w += 16) {
+            unsigned x = rword(roff + j0 + w) ^ aword(s + w);
+            if (len - w < 16) x &= (1u << (2 * (len - w))) - 1u;
+            cnt += __builtin_popcount((x | (x >> 1)) & 0x55555555u);
+        }
+        return cnt;
+    };
     // a wavefront batch of the 64 reads r0 .. r0 + 63 (below r_end): lane u holds read r0 + u's
     // offset and length; exc: the reads holding an exception byte (packed input)
     auto batch = [&](long long r0, long long r_end, long long my_off, int my_len, bool exc) {
@@ -409,9 +455,92 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
                 }
             }
         }
+        // window reads (above): an exact window at the largest offset, else one substitution
+        unsigned long long win = 0ull;
+        int win_s = 0, win_k = 0;
+        if constexpr (PK) {
+            if (win_ok) {
+                bool cand_w = r < r_end && !exc && my_len >= 16 && my_len < La;
+                int best1 = -1;   // an offset with one mismatch
+                if (cand_w) {
+                    const unsigned key0 = rword(my_off);
+                    int lo = 0, hi = nseed;   // first index with key > key0
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (skey[mid] <= key0) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    int tries = 0;
+                    for (int i = lo - 1; i >= 0 && skey[i] == key0 && tries < 8; --i, ++tries) {   // offsets descending
+                        const int s = spos[i];
+                        if (s + my_len > La) continue;
+                        const int mm = mism(my_off, 16, s + 16, my_len - 16, 1);
+                        if (mm == 0) {
+                            win_s = s;
+                            win_k = 0;
+                            best1 = -2;
+                            break;
+                        }
+                        if (mm == 1 && best1 == -1) best1 = s;
+                    }
+                    if (best1 == -1) {   // the substitution among the first 16 bases: the last 16 as the seed
+                        const unsigned key1 = rword(my_off + my_len - 16);
+                        lo = 0;
+                        hi = nseed;
+                        while (lo < hi) {
+                            const int mid = (lo + hi) >> 1;
+                            if (skey[mid] <= key1) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        tries = 0;
+                        for (int i = lo - 1; i >= 0 && skey[i] == key1 && tries < 8; --i, ++tries) {
+                            const int s = (int)spos[i] - (my_len - 16);
+                            if (s < 0) continue;
+                            if (mism(my_off, 0, s, my_len - 16, 1) == 1) {
+                                best1 = s;
+                                break;
+                            }
+                        }
+                    }
+                    if (best1 >= 0) {
+                        win_s = best1;
+                        win_k = 1;
+                    }
+                    cand_w = best1 != -1;
+                }
+                win = __ballot(cand_w);
+                // one substitution: every other full-overlap diagonal needs two mismatches, the two
+                // diagonals pairing Lb - 1 residues one (the whole wave on each such read)
+                for (unsigned long long need = __ballot(cand_w && win_k == 1); need; need &= need - 1) {
+                    const int u = (int)__builtin_ctzll(need);
+                    const int s1 = __builtin_amdgcn_readlane(win_s, u), Lb = __builtin_amdgcn_readlane(my_len, u);
+                    const unsigned lo32 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+                    const unsigned hi32 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
+                    const long long ro = (long long)(((unsigned long long)hi32 << 32) | lo32);
+                    bool bad = false;
+                    for (int s2 = lane; s2 <= La - Lb; s2 += 64)
+                        if (s2 != s1) bad = bad || mism(ro, 0, s2, Lb, 1) < 2;
+                    if (lane == 0) bad = bad || mism(ro, 1, 0, Lb - 1, 0) < 1;            // d = +1
+                    if (lane == 1) bad = bad || mism(ro, 0, La - Lb + 1, Lb - 1, 0) < 1;   // d = Lb - La - 1
+                    if (__ballot(bad)) win &= ~(1ull << u);
+                }
+            }
+        }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2) >> lane) & 1ull) ? a.band_lb_cap + 2
-                                                               : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+            a.sort_key[r] = (((exact | sub1 | sub2 | win) >> lane) & 1ull) ? a.band_lb_cap + 2
+                                                                     : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+        if (a.ops && r < r_end && ((win >> lane) & 1ull)) {
+            // runs: s amplicon residues (Y), the window (M), the rest of the amplicon (Y)
+            int q = 0;
+            const long long sst = a.ops_stride;
+            if (win_s > 0) a.ops[sst * q++ + r] = ((unsigned)RUN_Y << 28) | (unsigned)win_s;
+            a.ops[sst * q++ + r] = ((unsigned)RUN_M << 28) | (unsigned)my_len;
+            if (La - win_s - my_len > 0) a.ops[sst * q++ + r] = ((unsigned)RUN_Y << 28) | (unsigned)(La - win_s - my_len);
+            a.nops[r] = q;
+            int4* st = (int4*)(a.stats + r);
+            st[0] = make_int4(La, my_len - win_k, my_len - win_k, La - my_len);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * (my_len - win_k) - win_k * 4 * sc5, win_s + my_len, my_len, 0);
+        }
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
@@ -455,7 +584,7 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
             // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
             // before any store (one read per round trip measured 2.7x the byte-input classify)
             constexpr int kWr = 8;
-            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2) >> lane) & 1ull));
+            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win) >> lane) & 1ull));
             uint8_t* dst = const_cast<uint8_t*>(a.reads);
             while (dp) {
                 long long o[kWr], e[kWr];
@@ -1948,8 +2077,9 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) {
     if (a.pk_words) {   // one block per call group of kLenGroup reads the chunk touches
         const int64_t g0 = a.pk_call_lo / kLenGroup, g1 = (a.pk_call_lo + a.n - 1) / kLenGroup;
-        hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(kLenGroup),
-                           (size_t)(8 * ((a.La + 3) / 4)), s, a);
+        const size_t lds = (size_t)(8 * ((a.La + 3) / 4)) +
+                           (a.amp2 ? (size_t)(4 * ((a.La + 15) / 16 + 2) + 6 * a.n_seed + 16) : 0);
+        hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(kLenGroup), lds, s, a);
     } else {
         hipLaunchKernelGGL(nw_band_classify<false>, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))),
                            dim3(256), (size_t)(8 * ((a.La + 3) / 4)), s, a);

@@ -114,6 +114,13 @@ struct KernelArgs {
     const uint16_t* pk_len;        // call-indexed read lengths (null: the offsets are in place)
     const int64_t* pk_gbase;       // offset of read g * kLenGroup
     int64_t pk_call_lo;            // call index of the chunk's read 0
+    // window seeds (packed classify): the amplicon's 2-bit stream and its A C G T 16-mers sorted by
+    // (key, position) -- reads shorter than the amplicon that are an exact copy of one of its windows,
+    // or one substitution from one, leave the DP (null amp2: off)
+    const uint32_t* amp2;
+    const uint32_t* seed_key;
+    const uint16_t* seed_pos;
+    int32_t n_seed;
 };
 
 // Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and

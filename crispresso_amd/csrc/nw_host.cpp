@@ -59,6 +59,12 @@ struct Profile {
     const uint8_t* amp = nullptr;      // amplicon bytes (+16 pad)
     int R = 0;
     bool amp_plain = false;            // every amplicon byte is an EDNAFULL letter (the diagonal pass's codes)
+    // window seeds (classify, packed input): the amplicon 2 bits per base (the reads' packing) and
+    // its A C G T 16-mers sorted by (key, position); null for amplicons over 1024 bp
+    const uint32_t* amp2 = nullptr;
+    const uint32_t* seed_key = nullptr;
+    const uint16_t* seed_pos = nullptr;
+    int32_t n_seed = 0;
 };
 
 // Device buffers of one chunk's kernels.  The pipelined calls alternate two sets on
@@ -94,7 +100,8 @@ constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level
 //   CRISPR_NW_KERNEL     "full": every read through the exact int32 kernel; "diag32": the band
 //                        path without its 16-diagonal level
 //   CRISPR_NW_EXACT      "multi[:grid]": the exact work lists through the multi-wave kernel (the
-//                        first `grid` entries, the rest through the one-wave kernel)
+//                        first `grid` entries, the rest through the one-wave kernel); "lds": the
+//                        one-wave kernel keeps its traceback in LDS however few waves fit
 //   CRISPR_NW_DIAGPASS   "0" / "1": the diagonal pass off / on in every chunk
 //   CRISPR_NW_WIDE       "0": no 128-diagonal level
 //   CRISPR_NW_DIRECT     reads up to which a chunk's first level hands straight to the wide level
@@ -249,7 +256,39 @@ struct AmpTables {
     bool amp_plain = true;
     std::vector<int8_t> prof;
     std::vector<uint32_t> rowpos;
+    std::vector<uint32_t> amp2, seed_key;   // window seeds (Profile::amp2 / seed_key / seed_pos)
+    std::vector<uint16_t> seed_pos;
 };
+
+// The amplicon's 2-bit stream (A C T G = 0 1 2 3 = (byte >> 1) & 3, base p in bits 2 (p % 16)
+// of dword p / 16, as nw_pack_reads packs reads; two spare dwords) and its 16-mers of A C G T
+// bases only, sorted by (key, position): classify's window seeds.
+void seed_tables(const std::string& ref, AmpTables* t) {
+    const int La = (int)ref.size();
+    if (La < 16 || La > 1024) return;
+    t->amp2.assign((size_t)(La + 15) / 16 + 2, 0u);
+    std::vector<uint8_t> ok((size_t)La);
+    for (int p = 0; p < La; ++p) {
+        const unsigned char u = (unsigned char)ref[p] & 0xDF;
+        ok[(size_t)p] = u == 'A' || u == 'C' || u == 'G' || u == 'T';
+        t->amp2[(size_t)p / 16] |= (uint32_t)(((unsigned char)ref[p] >> 1) & 3u) << (2 * (p % 16));
+    }
+    std::vector<std::pair<uint32_t, uint16_t>> kp;
+    for (int p = 0; p + 16 <= La; ++p) {
+        bool all = true;
+        uint32_t key = 0;
+        for (int b = 0; b < 16; ++b) {
+            all = all && ok[(size_t)(p + b)];
+            key |= (uint32_t)(((unsigned char)ref[p + b] >> 1) & 3u) << (2 * b);
+        }
+        if (all) kp.emplace_back(key, (uint16_t)p);
+    }
+    std::sort(kp.begin(), kp.end());
+    for (auto& e : kp) {
+        t->seed_key.push_back(e.first);
+        t->seed_pos.push_back(e.second);
+    }
+}
 
 bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
     const int La = (int)ref.size();
@@ -267,6 +306,7 @@ bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
     }
     const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
+    seed_tables(ref, t);
     if (R <= 0) return true;
     const int RP = nw::profile_rp(R);
     t->prof.assign((size_t)nw::NCODE * 64 * RP, 0);
@@ -345,14 +385,15 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         total += (bytes + 255) & ~(size_t)255;
         return at;
     };
-    struct Off { size_t prof, rowpos, amp; };
+    struct Off { size_t prof, rowpos, amp, amp2, skey, spos; };
     std::vector<Off> offs(refs.size());
     for (size_t g = 0; g < refs.size(); ++g) {
         if (!amp_tables(refs[g], c->scale, &tabs[g]))
             return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", (int)refs[g].size(), kMaxRef);
         const AmpTables& t = tabs[g];
         const size_t o1 = sec(t.prof.size()), o5 = sec(t.rowpos.size() * 4), o6 = sec(refs[g].size() + 16);
-        offs[g] = {o1, o5, o6};
+        const size_t o7 = sec(t.amp2.size() * 4), o8 = sec(t.seed_key.size() * 4), o9 = sec(t.seed_pos.size() * 2);
+        offs[g] = {o1, o5, o6, o7, o8, o9};
     }
     std::vector<uint8_t> host(std::max<size_t>(total, 256), 0);
     for (size_t g = 0; g < refs.size(); ++g) {
@@ -361,6 +402,9 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         std::memcpy(host.data() + o.prof, t.prof.data(), t.prof.size());
         std::memcpy(host.data() + o.rowpos, t.rowpos.data(), t.rowpos.size() * 4);
         std::memcpy(host.data() + o.amp, refs[g].data(), refs[g].size());
+        std::memcpy(host.data() + o.amp2, t.amp2.data(), t.amp2.size() * 4);
+        std::memcpy(host.data() + o.skey, t.seed_key.data(), t.seed_key.size() * 4);
+        std::memcpy(host.data() + o.spos, t.seed_pos.data(), t.seed_pos.size() * 2);
     }
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));   // no kernel may still read the old arena
     HIP_OR_FAIL(c, c->d_arena.reserve(host.size()));
@@ -375,6 +419,12 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         p.amp = b + o.amp;
         p.R = tabs[g].R;
         p.amp_plain = tabs[g].amp_plain;
+        if (!tabs[g].amp2.empty()) {
+            p.amp2 = (const uint32_t*)(b + o.amp2);
+            p.seed_key = (const uint32_t*)(b + o.skey);
+            p.seed_pos = (const uint16_t*)(b + o.spos);
+            p.n_seed = (int32_t)tabs[g].seed_key.size();
+        }
     }
     c->arena_refs = refs;
     c->arena_profs = *profs;
@@ -447,8 +497,16 @@ int configure(nw_ctx* c) {
             break;
         }
     }
-    // (traceback in HBM instead of LDS, for more wavefronts per CU on a bulk exact list,
-    // measured no faster on the HDR pass: the kernel is VALU-issue bound there)
+    // Traceback in HBM instead of LDS when the LDS traceback leaves a SIMD without a second
+    // wavefront (a read's whole matrix at 4 bits per cell: 151 x 280 C1-shape reads take 41 KB per
+    // wavefront, three per CU): a lone wavefront issues a VALU instruction per ~4 cycles and
+    // waits out its own latencies.  CRISPR_NW_EXACT=lds keeps the LDS traceback (A/Bs).
+    const char* ex_env = std::getenv("CRISPR_NW_EXACT");   // "multi[:grid]" | "lds" (tests, A/Bs)
+    if (cfg.tb_mode == nw::TB_LDS_FULL && !(ex_env && std::strcmp(ex_env, "lds") == 0) &&
+        cfg.wpb * std::min(8, kMaxLds / cfg.lds_bytes) < 8) {
+        cfg.tb_mode = nw::TB_GLOBAL_FULL;
+        cfg.wpb = 4;
+    }
     if (cfg.tb_mode == nw::TB_GLOBAL_FULL) cfg.lds_bytes = nw::lds_bytes_for(R, La, c->lb_max, nw::TB_GLOBAL_FULL, cfg.wpb);
     if (cfg.lds_bytes <= 0 || cfg.lds_bytes > kMaxLds)
         return fail(c, NW_E_UNSUPPORTED, "reads of %d bases do not fit the kernel", c->lb_max);
@@ -463,7 +521,7 @@ int configure(nw_ctx* c) {
     c->exact_grid = 0;
     // Off by default: at the ~15 reads per 1M C2 reads it is not faster than the one-wave
     // kernel (both are VALU-issue bound), so it serves the long amplicons
-    const char* ex = std::getenv("CRISPR_NW_EXACT");   // "multi[:grid]": fallbacks through it (tests)
+    const char* ex = ex_env;   // "multi[:grid]": fallbacks through it (tests)
     if (nw::exact_rows_per_lane(La) > 0 && ex && std::strncmp(ex, "multi", 5) == 0) {
         c->exact_tb_lds = true;
         c->exact_lds = nw::exact_lds_bytes(La, c->lb_max, true);
@@ -913,6 +971,10 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.rowpos = c->cur.rowpos;
         a.sort_key = c->s->d_sort_key.p;
         a.band_count = c->s->d_fallback_count.p + 1;   // the sort writes the DP count here
+        a.amp2 = c->cur.amp2;
+        a.seed_key = c->cur.seed_key;
+        a.seed_pos = c->cur.seed_pos;
+        a.n_seed = c->cur.n_seed;
         a.lb_status = c->s->d_lb.p;
         // packed input (ops_call): classify decodes the chunk (KernelArgs::pk_*)
         a.pk_words = c->pkc.pk_words;
