@@ -238,7 +238,7 @@ __device__ inline long long exc_lower_bound(const KernelArgs& a, long long pos, 
 }
 
 template <bool PK>
-__global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const KernelArgs a) {
+__global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
@@ -312,15 +312,38 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
     auto aword = [&](int p) -> unsigned {
         return __builtin_amdgcn_alignbit(amp2s[(p >> 4) + 1], amp2s[p >> 4], (unsigned)(2 * (p & 15)));
     };
-    // mismatches of read bases [roff + j0, + len) against amplicon [s, s + len), counted up to cap + 1
+    // mismatches of read bases [roff + j0, + len) against amplicon [s, s + len), counted up to cap + 1:
+    // 16 words (256 bases) per round with every load in flight before any compare
     auto mism = [&](long long roff, int j0, int s, int len, int cap) -> int {
         int cnt = 0;
-        for (int w = 0; w < len && cnt <= cap; w += 16) {
-            unsigned x = rword(roff + j0 + w) ^ aword(s + w);
-            if (len - w < 16) x &= (1u << (2 * (len - w))) - 1u;
-            cnt += __builtin_popcount((x | (x >> 1)) & 0x55555555u);
+        for (int w0 = 0; w0 < len && cnt <= cap; w0 += 256) {
+            unsigned x[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) x[t] = w0 + 16 * t < len ? rword(roff + j0 + w0 + 16 * t) : 0u;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int w = w0 + 16 * t;
+                if (w >= len) continue;
+                unsigned y = x[t] ^ aword(s + w);
+                if (len - w < 16) y &= (1u << (2 * (len - w))) - 1u;
+                cnt += __builtin_popcount((y | (y >> 1)) & 0x55555555u);
+            }
         }
         return cnt;
+    };
+    auto ham16 = [&](unsigned x, unsigned y) { const unsigned z = x ^ y; return __builtin_popcount((z | (z >> 1)) & 0x55555555u); };
+    // positions of a 16-mer key among the amplicon's (sorted): [lo, hi)
+    auto seed_range = [&](unsigned key, int* first) -> int {
+        int lo = 0, hi = nseed;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (skey[mid] <= key) lo = mid + 1;
+            else hi = mid;
+        }
+        int f = lo;
+        while (f > 0 && skey[f - 1] == key && lo - f < 8) --f;   // at most 8 offsets (repeats: the DP)
+        *first = f;
+        return lo;
     };
     // a wavefront batch of the 64 reads r0 .. r0 + 63 (below r_end): lane u holds read r0 + u's
     // offset and length; exc: the reads holding an exception byte (packed input)
@@ -460,52 +483,39 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
         int win_s = 0, win_k = 0;
         if constexpr (PK) {
             if (win_ok) {
-                bool cand_w = r < r_end && !exc && my_len >= 16 && my_len < La;
-                int best1 = -1;   // an offset with one mismatch
+                bool cand_w = r < r_end && !exc && my_len >= 32 && my_len < La;
+                int best1 = -1;   // -2: an exact window at win_s; >= 0: an offset with one mismatch
                 if (cand_w) {
-                    const unsigned key0 = rword(my_off);
-                    int lo = 0, hi = nseed;   // first index with key > key0
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (skey[mid] <= key0) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    int tries = 0;
-                    for (int i = lo - 1; i >= 0 && skey[i] == key0 && tries < 8; --i, ++tries) {   // offsets descending
+                    // a window at s has the read's first 16 bases at s or its last 16 at s + Lb - 16 (one
+                    // substitution cannot hit both); the other end word must then be within one mismatch
+                    // -- one word compare rejects most offsets (reads with an indel) before the middle
+                    const unsigned key0 = rword(my_off), key1 = rword(my_off + my_len - 16);
+                    int f0, f1;
+                    const int l0 = seed_range(key0, &f0), l1 = seed_range(key1, &f1);
+                    for (int i = l0 - 1; i >= f0; --i) {   // offsets descending: the largest exact window first
                         const int s = spos[i];
                         if (s + my_len > La) continue;
-                        const int mm = mism(my_off, 16, s + 16, my_len - 16, 1);
+                        const int he = ham16(key1, aword(s + my_len - 16));
+                        if (he > 1) continue;
+                        const int mm = he + mism(my_off, 16, s + 16, my_len - 32, 1 - he);
                         if (mm == 0) {
-                            win_s = s;
-                            win_k = 0;
                             best1 = -2;
+                            win_s = s;
                             break;
                         }
                         if (mm == 1 && best1 == -1) best1 = s;
                     }
-                    if (best1 == -1) {   // the substitution among the first 16 bases: the last 16 as the seed
-                        const unsigned key1 = rword(my_off + my_len - 16);
-                        lo = 0;
-                        hi = nseed;
-                        while (lo < hi) {
-                            const int mid = (lo + hi) >> 1;
-                            if (skey[mid] <= key1) lo = mid + 1;
-                            else hi = mid;
-                        }
-                        tries = 0;
-                        for (int i = lo - 1; i >= 0 && skey[i] == key1 && tries < 8; --i, ++tries) {
+                    if (best1 == -1)   // the substitution among the first 16 bases
+                        for (int i = l1 - 1; i >= f1; --i) {
                             const int s = (int)spos[i] - (my_len - 16);
-                            if (s < 0) continue;
-                            if (mism(my_off, 0, s, my_len - 16, 1) == 1) {
+                            if (s < 0 || ham16(key0, aword(s)) != 1) continue;
+                            if (mism(my_off, 16, s + 16, my_len - 32, 0) == 0) {
                                 best1 = s;
                                 break;
                             }
                         }
-                    }
-                    if (best1 >= 0) {
-                        win_s = best1;
-                        win_k = 1;
-                    }
+                    if (best1 >= 0) win_s = best1;
+                    win_k = best1 >= 0 ? 1 : 0;
                     cand_w = best1 != -1;
                 }
                 win = __ballot(cand_w);
@@ -635,30 +645,39 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
             batch(r0, a.n, my_off, my_len, false);
         }
     } else {
-        // block b: the chunk's reads of call group G = call_lo / kLenGroup + b, [bl, bh)
-        __shared__ long long s_off[kLenGroup + 1];
-        __shared__ unsigned char s_exc[kLenGroup];
-        __shared__ long long s_wsum[16];
+        // block b: the chunk's reads of call block B = call_lo / kPkBlock + b, [bl, bh) (kPkBlock reads,
+        // one per thread; four blocks per group of kLenGroup lengths)
+        constexpr int kPkBlock = 256;
+        static_assert(kLenGroup % kPkBlock == 0, "blocks tile the length groups");
+        __shared__ long long s_off[kPkBlock + 1];
+        __shared__ unsigned char s_exc[kPkBlock];
+        __shared__ long long s_wsum[8];
         __shared__ long long s_x[2];
-        const long long G = a.pk_call_lo / kLenGroup + blockIdx.x;
-        const long long bl = max(0ll, G * kLenGroup - a.pk_call_lo), bh = min(a.n, (G + 1) * kLenGroup - a.pk_call_lo);
+        const long long B = a.pk_call_lo / kPkBlock + blockIdx.x;
+        const long long bl = max(0ll, B * kPkBlock - a.pk_call_lo), bh = min(a.n, (B + 1) * kPkBlock - a.pk_call_lo);
         const int cnt = (int)(bh - bl), tid = threadIdx.x, wave = tid >> 6;
         int64_t* offs = const_cast<int64_t*>(a.offsets);
         if (a.pk_len) {
-            // the offsets from the lengths (nw_align_ops_packed_lens): the group's base offset + an
-            // exclusive scan of the lengths of its reads up to the chunk's end (reads of earlier
-            // chunks in the group included: they are uploaded with the call's first lengths copy)
-            const long long rr = G * kLenGroup + tid - a.pk_call_lo;   // chunk-relative
-            const long long l = rr < bh ? (long long)a.pk_len[G * kLenGroup + tid] : 0ll;
+            // the offsets from the lengths (nw_align_ops_packed_lens): the group's base offset, the
+            // lengths of the group's reads before this block (earlier chunks' included: they are uploaded
+            // with the call's first lengths copy), an exclusive scan of the block's own
+            const long long G = B * kPkBlock / kLenGroup, g0 = G * kLenGroup;
+            const long long rr = B * kPkBlock + tid - a.pk_call_lo;   // chunk-relative
+            const long long l = rr < bh ? (long long)a.pk_len[B * kPkBlock + tid] : 0ll;
+            long long pre = 0;   // the group's reads [g0, B * kPkBlock): at most three per thread
+            for (long long q = g0 + tid; q < B * kPkBlock; q += kPkBlock) pre += a.pk_len[q];
             long long inc = l;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const long long o = __shfl_up(inc, d, 64);
+                const long long op = __shfl_xor(pre, d, 64);
                 if (lane >= d) inc += o;
+                pre += op;
             }
             if (lane == 63) s_wsum[wave] = inc;
+            if (lane == 0) s_wsum[4 + wave] = pre;
             __syncthreads();
-            long long o = a.pk_gbase[G] + inc - l;
+            long long o = a.pk_gbase[G] + inc - l + s_wsum[4] + s_wsum[5] + s_wsum[6] + s_wsum[7];
             for (int w2 = 0; w2 < wave; ++w2) o += s_wsum[w2];
             if (rr >= bl && rr < bh) {
                 s_off[rr - bl] = o;
@@ -673,7 +692,7 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
         }
         // reads holding exception bytes (not certifiable here; every one of them needs the DP)
         const bool any_exc = a.pk_e1 > a.pk_e0;
-        for (int i = tid; i < kLenGroup; i += blockDim.x) s_exc[i] = 0;
+        for (int i = tid; i < kPkBlock; i += blockDim.x) s_exc[i] = 0;
         __syncthreads();
         long long x0 = 0, x1 = 0;
         if (any_exc) {
@@ -700,7 +719,7 @@ __global__ __launch_bounds__(PK ? 1024 : 256) void nw_band_classify(const Kernel
             }
             __syncthreads();
         }
-        const long long r0 = bl + 64 * wave;
+        const long long r0 = bl + 64 * wave;   // one batch per wavefront
         if (r0 < bh) {
             const long long r = r0 + lane;
             const long long my_off = r < bh ? s_off[r - bl] : 0;
@@ -2075,11 +2094,11 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 // classify (exact copies, sort keys) then the segment sort; a.band_count receives the
 // DP count, a.lb_status holds ceil(n / kSegReads) look-back words
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) {
-    if (a.pk_words) {   // one block per call group of kLenGroup reads the chunk touches
-        const int64_t g0 = a.pk_call_lo / kLenGroup, g1 = (a.pk_call_lo + a.n - 1) / kLenGroup;
+    if (a.pk_words) {   // one block per call block of 256 reads the chunk touches
+        const int64_t g0 = a.pk_call_lo / 256, g1 = (a.pk_call_lo + a.n - 1) / 256;
         const size_t lds = (size_t)(8 * ((a.La + 3) / 4)) +
                            (a.amp2 ? (size_t)(4 * ((a.La + 15) / 16 + 2) + 6 * a.n_seed + 16) : 0);
-        hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(kLenGroup), lds, s, a);
+        hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(256), lds, s, a);
     } else {
         hipLaunchKernelGGL(nw_band_classify<false>, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))),
                            dim3(256), (size_t)(8 * ((a.La + 3) / 4)), s, a);
