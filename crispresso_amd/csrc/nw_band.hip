@@ -211,6 +211,12 @@ __device__ __forceinline__ unsigned pk_decode4(const KernelArgs& a, long long p)
     return __builtin_amdgcn_perm(0u, 0x47544341u, sel);   // 0 1 2 3 -> 'A' 'C' 'T' 'G'
 }
 
+// the low 8 bits of x (4 bases) as bytes A C T G
+__device__ __forceinline__ unsigned pk_expand(unsigned x) {
+    x &= 0xffu;
+    return __builtin_amdgcn_perm(0u, 0x47544341u, (x | (x << 6) | (x << 12) | (x << 18)) & 0x03030303u);
+}
+
 // pk_decode4 at a 4-aligned position (the four bases sit in one stream dword: one load)
 __device__ __forceinline__ unsigned pk_decode4_al(const KernelArgs& a, long long p) {
     const long long q = p - a.pk_pos0;
@@ -293,8 +299,12 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const int n2 = (La + 15) / 16 + 2, nseed = a.n_seed;
     unsigned* skey = amp2s + n2;
     uint16_t* spos = (uint16_t*)(skey + nseed);
+#ifdef NW_NO_WIN
+    const bool win_ok = false;
+#else
     const bool win_ok = PK && amp_acgt_all && a.ops && a.band_maxsub == 5 * sc5 && a.gap_extend >= 0 && a.amp2 &&
                         a.gap_open > xl && nseed > 0 && La <= 1024;
+#endif
     if (win_ok) {
         for (int k = threadIdx.x; k < n2; k += blockDim.x) amp2s[k] = a.amp2[k];
         for (int k = threadIdx.x; k < nseed; k += blockDim.x) {
@@ -380,7 +390,10 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
                     const long long off = (long long)(((unsigned long long)hi << 32) | lo);
                     if constexpr (PK) {   // the read's bytes 4 kc .. 4 kc + 3 from the 2-bit stream
-                        raw[t] = pk_decode4(a, off + 4 * kc);
+                        const long long q0 = off - a.pk_pos0;   // wave-uniform: 64-bit math in SGPRs
+                        const unsigned tq = (unsigned)(q0 & 15) + 4u * (unsigned)kc;
+                        w[t] = *(const uint2*)(a.pk_words + (q0 >> 4) + (tq >> 4));
+                        sh[t] = (int)(2 * (tq & 15));
                     } else {
                         w[t] = *(const uint2*)(a.reads + (off & ~3ll) + 4 * kc);   // 4-aligned dwordx2
                         sh[t] = (int)(off & 3);
@@ -390,7 +403,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 const unsigned msk = k4 < nd ? (k4 == nd - 1 ? tail_mask : 0xffffffffu) : 0u;
 #pragma unroll
                 for (int t = 0; t < kCand; ++t) {
-                    if constexpr (!PK) raw[t] = __builtin_amdgcn_alignbyte(w[t].y, w[t].x, sh[t]);
+                    if constexpr (PK) raw[t] = pk_expand(__builtin_amdgcn_alignbit(w[t].y, w[t].x, (unsigned)sh[t]));
+                    else raw[t] = __builtin_amdgcn_alignbyte(w[t].y, w[t].x, sh[t]);
                     diff[t] |= ((raw[t] | 0x20202020u) ^ am) & msk;
                 }
             }

@@ -256,6 +256,11 @@ struct OpsHostOut {
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr);
+                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr,
+                              int64_t* dchunk = nullptr);
+// The chunk's runs staging[0, dchunk[1]) -> hops + dchunk[0] (the caller's page-locked run array) by
+// kernel stores, skipped when that passes hcap; max_words bounds the grid.
+hipError_t launch_ops_runs_out(const int64_t* dchunk, const uint32_t* staging, uint32_t* hops, int64_t hcap, int64_t max_words,
+                               hipStream_t s);
 
 }  // namespace nw
