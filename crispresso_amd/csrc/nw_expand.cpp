@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/crispr_nw.h"
+#include "host_pool.h"
 #include "nw_edna.h"
 
 namespace {
@@ -205,6 +206,83 @@ extern "C" int64_t nw_reads_equal_ref(const char* ref, int32_t ref_len, const ch
         count += c;
     });
     return count.load();
+}
+
+namespace {
+
+uint64_t read_hash(const unsigned char* p, int64_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    int64_t k = 0;
+    for (; k + 8 <= n; k += 8) {
+        uint64_t w;
+        std::memcpy(&w, p + k, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 32;
+    }
+    uint64_t w = 0;
+    std::memcpy(&w, p + k, (size_t)(n - k));
+    h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+    return h ^ (h >> 29);
+}
+
+}  // namespace
+
+// rep[q] = the first q' with read idx[q']'s bytes equal to read idx[q]'s (idx null: the reads
+// 0 .. m).  Hashes in parallel, then one open-addressing
+// table per hash partition (each thread owns the reads whose hash falls in its partition,
+// visited in read order, so the first occurrence is the one kept); equal hashes are
+// confirmed by comparing the bytes.  Returns the number of distinct reads.
+extern "C" int64_t nw_reads_first_copy(const char* reads, const int64_t* offsets, const int64_t* idx, int64_t n,
+                                       int64_t* rep, int32_t nthreads) {
+    if (n < 0 || (n > 0 && (!reads || !offsets || !rep))) return NW_E_INVALID;
+    auto rd = [&](int64_t q) { return idx ? idx[q] : q; };
+    if (n == 0) return 0;
+    nw_host::Pool& pool = nw_host::Pool::get();
+    int P = nthreads > 0 ? std::min(nthreads, pool.threads()) : pool.threads();
+    P = (int)std::max<int64_t>(1, std::min<int64_t>(P, n / 8192 + 1));
+    std::vector<uint64_t> h((size_t)n);
+    pool.run(P, [&](int k) {
+        int64_t lo, hi;
+        nw_host::Pool::range(n, P, k, &lo, &hi);
+        for (int64_t q = lo; q < hi; ++q) {
+            const int64_t r = rd(q);
+            h[(size_t)q] = read_hash((const unsigned char*)reads + offsets[r], offsets[r + 1] - offsets[r]);
+        }
+    });
+    std::vector<int64_t> distinct((size_t)P, 0);
+    pool.run(P, [&](int part) {
+        // this partition's reads: hash % P == part (the slot comes from the high bits)
+        int64_t cnt = 0;
+        for (int64_t r = 0; r < n; ++r) cnt += (int)(h[(size_t)r] % (uint64_t)P) == part;
+        size_t cap = 16;
+        while (cap < (size_t)(2 * cnt + 16)) cap <<= 1;
+        std::vector<int64_t> slot(cap, -1);
+        int64_t d = 0;
+        for (int64_t r = 0; r < n; ++r) {
+            const uint64_t hr = h[(size_t)r];
+            if ((int)(hr % (uint64_t)P) != part) continue;
+            const int64_t a = rd(r), Lr = offsets[a + 1] - offsets[a];
+            for (size_t s = (size_t)(hr >> 24) & (cap - 1);; s = (s + 1) & (cap - 1)) {
+                const int64_t q = slot[s];
+                if (q < 0) {
+                    slot[s] = r;
+                    rep[r] = r;
+                    ++d;
+                    break;
+                }
+                const int64_t b = rd(q);
+                if (h[(size_t)q] == hr && offsets[b + 1] - offsets[b] == Lr &&
+                    std::memcmp(reads + offsets[b], reads + offsets[a], (size_t)Lr) == 0) {
+                    rep[r] = q;
+                    break;
+                }
+            }
+        }
+        distinct[(size_t)part] = d;
+    });
+    int64_t tot = 0;
+    for (int64_t d : distinct) tot += d;
+    return tot;
 }
 
 extern "C" int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,

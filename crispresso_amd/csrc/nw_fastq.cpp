@@ -52,10 +52,31 @@
 #include "../../include/crispr_nw.h"
 #include "host_pool.h"
 
+// std::vector storage that resize() leaves uninitialised: the ingest's buffers are written
+// in full right after they grow (a zero-fill of the 1M-read text alone was ~0.1 s).
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInit<U>;
+    };
+    NoInit() = default;
+    template <class U>
+    NoInit(const NoInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+
 struct nw_fastq {
-    std::vector<char> seqs;
-    std::vector<int64_t> offsets{0};
-    std::vector<char> names;   // record names joined by '\n'
+    std::vector<char, NoInit<char>> seqs;
+    std::vector<int64_t, NoInit<int64_t>> offsets{0};
+    std::vector<char, NoInit<char>> names;   // record names joined by '\n'
     std::vector<uint8_t> pass; // quality verdict of every record read (filtered reads only)
     int64_t dropped = 0;
     std::string err;
@@ -162,7 +183,7 @@ struct Parser {
                 q->names.push_back(ch == ':' ? '_' : (char)ch);
             }
         } else if (k == 1) {   // the bytes EMBOSS keeps (':' became '_', which it drops)
-            std::vector<char>& v = q->seqs;
+            auto& v = q->seqs;
             const size_t at = v.size();
             if (v.capacity() < at + (size_t)(e - p)) v.reserve(std::max(2 * v.capacity(), at + (size_t)(e - p)));
             v.resize(at + (size_t)(e - p));
@@ -341,6 +362,11 @@ void parse_parallel(Parser& ps, const unsigned char* b, size_t len, bool* pendin
     std::vector<Parser> pp;
     pp.reserve((size_t)P);
     for (int k = 0; k < P; ++k) {
+        // capacity for the part's worst case (untouched pages cost nothing): no regrowth copies
+        const size_t bytes = cut[(size_t)k + 1] - cut[(size_t)k];
+        parts[(size_t)k].seqs.reserve(bytes);
+        parts[(size_t)k].names.reserve(bytes);
+        parts[(size_t)k].offsets.reserve(bytes / 6 + 2);
         pp.push_back(Parser{&parts[(size_t)k]});
         pp.back().filter = ps.filter;
         pp.back().min_avg = ps.min_avg;
@@ -409,6 +435,7 @@ int read_whole(const char* path, Parser& ps, bool* pending) {
     const size_t isize = (size_t)in.p[in.n - 4] | (size_t)in.p[in.n - 3] << 8 | (size_t)in.p[in.n - 2] << 16 |
                          (size_t)in.p[in.n - 1] << 24;
     size_t pos = 0, cap = std::max(isize, 4 * in.n) + 4096;
+    nw_host::Pool& pool = nw_host::Pool::get();
     int rc = 1;
     bool first = true;
     while (pos + 18 <= in.n && in.p[pos] == 0x1f && in.p[pos + 1] == 0x8b) {
@@ -417,6 +444,15 @@ int read_whole(const char* path, Parser& ps, bool* pending) {
         int r = 3;
         for (;;) {   // LIBDEFLATE_INSUFFICIENT_SPACE (3): a bigger buffer, same member
             if (!outb.make(cap)) break;
+            if (cap >= kParallelMin) {   // the page faults of the output, taken in parallel before the serial inflate
+                const int P = pool.threads();
+                const size_t touch = std::min(cap, isize + 4096);
+                pool.run(P, [&](int k) {
+                    int64_t lo, hi;
+                    nw_host::Pool::range((int64_t)touch, P, k, &lo, &hi);
+                    for (int64_t b = lo & ~(int64_t)4095; b < hi; b += 4096) outb.p[b] = 0;
+                });
+            }
             r = D.gzip_ex(dec, in.p + pos, in.n - pos, outb.p, outb.n, &ain, &aout);
             if (r != 3 || cap >= kWholeMax) break;
             outb.release();
@@ -568,6 +604,49 @@ int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int
     if (exc_pos) *exc_pos = q->exc_pos;
     if (exc_byte) *exc_byte = q->exc_byte;
     if (n_exc) *n_exc = q->n_exc;
+    return NW_OK;
+}
+
+// The ID column of parse_needle_output (CRISPRessoCORE.py:1725: the name line's last word with
+// '_' back to ':') from names joined by '\n' (nw_fastq_names): ids = the bytes without the
+// newlines, '_' -> ':'; off[i] .. off[i + 1] = name i.  NW_E_UNSUPPORTED when a name holds
+// whitespace or a non-ASCII byte (then split() decides, in Python) or the newlines are not n.
+int nw_names_to_ids(const uint8_t* raw, int64_t nbytes, int64_t n, uint8_t* ids, int64_t* off) {
+    if (nbytes < 0 || n < 0 || (nbytes > 0 && (!raw || !ids)) || !off) return NW_E_INVALID;
+    off[0] = 0;
+    if (nbytes == 0) return n == 0 ? NW_OK : NW_E_UNSUPPORTED;
+    nw_host::Pool& pool = nw_host::Pool::get();
+    const int P = (int)std::max<int64_t>(1, std::min<int64_t>(pool.threads(), nbytes >> 20));
+    std::vector<int64_t> nl((size_t)P + 1, 0);
+    pool.run(P, [&](int k) {
+        int64_t lo, hi, c = 0;
+        nw_host::Pool::range(nbytes, P, k, &lo, &hi);
+        for (int64_t p = lo; p < hi; ++p) c += raw[p] == '\n';
+        nl[(size_t)k + 1] = c;
+    });
+    for (int k = 0; k < P; ++k) nl[(size_t)k + 1] += nl[(size_t)k];
+    if (nl[(size_t)P] != n || raw[nbytes - 1] != '\n') return NW_E_UNSUPPORTED;
+    std::vector<char> bad((size_t)P, 0);
+    pool.run(P, [&](int k) {
+        int64_t lo, hi, i = nl[(size_t)k];
+        nw_host::Pool::range(nbytes, P, k, &lo, &hi);
+        unsigned char acc = 0;
+        bool ws = false;
+        for (int64_t p = lo; p < hi; ++p) {
+            const unsigned char ch = raw[p];
+            if (ch == '\n') {
+                off[i + 1] = p - i;   // name i ends here (i newlines before it)
+                ++i;
+                continue;
+            }
+            acc |= ch;
+            ws |= ch == ' ' || ch == '\t' || ch == '\r' || ch == '\f' || ch == '\v' || (ch >= 0x1c && ch <= 0x1f);
+            ids[p - i] = ch == '_' ? ':' : ch;
+        }
+        bad[(size_t)k] = (acc & 0x80) || ws;
+    });
+    for (char b : bad)
+        if (b) return NW_E_UNSUPPORTED;
     return NW_OK;
 }
 

@@ -17,7 +17,8 @@ import gzip
 import io
 import os
 import re
-from typing import List, Tuple
+from collections.abc import Sequence
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -42,16 +43,43 @@ def fasta_name(header_line: bytes) -> str:
     return tok[0].decode("ascii", "replace") if tok else ""
 
 
-class NameList(list):
-    """The record names (a list of str) plus ``raw``: the same names as one uint8
+class NameList(Sequence):
+    """The record names (a sequence of str) plus ``raw``: the same names as one uint8
     block, each followed by '\\n' -- what the native reader produced, kept so the
-    DataFrame's ID column is built from it in bulk (needle._ids_of)."""
+    DataFrame's ID column is built from it in bulk (needle._ids_of).  The str objects are
+    made on first use (a 1M-read ingest does not pay for 1M of them when only the IDs are
+    read); ``raw`` is empty when a name holds a byte outside ASCII."""
 
-    raw: np.ndarray
-
-    def __init__(self, names, raw: np.ndarray):
-        super().__init__(names)
+    def __init__(self, names: Optional[List[str]], raw: np.ndarray, n: Optional[int] = None,
+                 text: Optional[np.ndarray] = None):
+        self._list = names
+        self._n = len(names) if names is not None else int(n)
+        self._text = text
         self.raw = raw
+
+    def _names(self) -> List[str]:
+        if self._list is None:
+            t = self._text if self._text is not None else self.raw
+            self._list = t.tobytes().decode("ascii", "replace").split("\n")[:-1] if self._n else []
+            self._text = None
+        return self._list
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        return self._names()[i]
+
+    def __iter__(self):
+        return iter(self._names())
+
+    def __eq__(self, other):
+        if isinstance(other, (list, tuple, NameList)):
+            return self._names() == list(other)
+        return NotImplemented
+
+    def __repr__(self):
+        return f"NameList({self._names()!r})"
 
 
 def read_fastq_as_fasta(path: str, min_bp_quality: int = 0,
@@ -84,9 +112,8 @@ def read_fastq_as_fasta(path: str, min_bp_quality: int = 0,
                else np.zeros(0, np.uint8))
     finally:
         lib.nw_fastq_free(h)
-    text = raw.tobytes().decode("ascii", "replace") if len(raw) else ""
-    names = text.split("\n")[:-1] if n else []
-    return NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), seqs, off
+    ascii_ok = len(raw) and int(raw.max()) < 128
+    return NameList(None, raw if ascii_ok else np.zeros(0, np.uint8), n, raw), seqs, off
 
 
 class _Owner:
@@ -157,10 +184,8 @@ def read_fastq_packed(path: str, pinned: bool = True):
     nm = ctypes.c_int64()
     p = lib.nw_fastq_names(h, ctypes.byref(nm))
     raw = _native_array(owner, p, nm.value, np.uint8).copy()
-    names_text = raw.tobytes().decode("ascii", "replace") if len(raw) else ""
-    names = names_text.split("\n")[:-1] if n else []
-    return (NameList(names, raw if len(raw) and int(raw.max()) < 128 else np.zeros(0, np.uint8)), text, offsets,
-            packed)
+    ascii_ok = len(raw) and int(raw.max()) < 128
+    return NameList(None, raw if ascii_ok else np.zeros(0, np.uint8), n, raw), text, offsets, packed
 
 
 def read_fastq_as_fasta_py(path: str, min_bp_quality: int = 0,

@@ -124,12 +124,12 @@ def _ids_of(names: Sequence[str], keep: np.ndarray) -> np.ndarray:
     as an object array.  Names read natively (:class:`fastq.NameList`) are converted
     from their byte block without a per-name Python step."""
     raw = getattr(names, "raw", None)
-    if raw is not None and len(raw) and not _WS_BYTES[raw].any():
-        nl = np.flatnonzero(raw == 10)
-        if len(nl) == len(names):
-            ids = np.where(raw == ord("_"), np.uint8(ord(":")), raw)[raw != 10]
-            off = np.zeros(len(nl) + 1, np.int64)
-            off[1:] = nl - np.arange(len(nl))
+    if raw is not None and len(raw):
+        lib = _lib.load()
+        raw = np.ascontiguousarray(raw, dtype=np.uint8)
+        ids = np.empty(len(raw), np.uint8)
+        off = np.empty(len(names) + 1, np.int64)
+        if lib.nw_names_to_ids(_lib.ptr(raw), len(raw), len(names), _lib.ptr(ids), _lib.ptr(off)) == _lib.NW_OK:
             allids = _strings(ids, off, ascii_checked=True)
             return allids if len(keep) == len(names) else allids[keep]
     sel = [names[i] for i in keep] if len(keep) != len(names) else list(names)
@@ -144,9 +144,6 @@ def _ids_of(names: Sequence[str], keep: np.ndarray) -> np.ndarray:
 
 
 _WS = __import__("re").compile(r"[ \t\r\f\v\x0b\x1c-\x1f\x85\xa0]")
-_WS_BYTES = np.zeros(256, dtype=bool)
-for _b in b" \t\r\f\v\x0b\x1c\x1d\x1e\x1f\x85\xa0":
-    _WS_BYTES[_b] = True
 
 
 def _strings(data: np.ndarray, off: np.ndarray, take: Optional[np.ndarray] = None,
@@ -192,10 +189,22 @@ def _rows_to_str(mat: np.ndarray, lens: np.ndarray) -> np.ndarray:
 
 
 def _printed_percents(num: np.ndarray, den: np.ndarray) -> np.ndarray:
-    """printed_percent over arrays: formatted once per distinct (num, den)."""
+    """printed_percent over arrays: formatted once per distinct (num, den) -- found through a
+    dense (den, num) table when the values are small (alignment lengths), else by sorting."""
     if len(num) == 0:
         return np.zeros(0, dtype=np.float64)
-    key = (den.astype(np.int64) << 32) | (num.astype(np.int64) & 0xFFFFFFFF)
+    num = num.astype(np.int64)
+    den = den.astype(np.int64)
+    hi_n, hi_d = int(num.max()) + 1, int(den.max()) + 1
+    if int(num.min()) >= 0 and int(den.min()) >= 0 and hi_n * hi_d <= (1 << 24):
+        key = den * hi_n + num
+        seen = np.zeros(hi_n * hi_d, dtype=bool)
+        seen[key] = True
+        uniq = np.flatnonzero(seen)
+        lut = np.zeros(hi_n * hi_d, dtype=np.float64)
+        lut[uniq] = [printed_percent(int(k % hi_n), int(k // hi_n)) for k in uniq.tolist()]
+        return lut[key]
+    key = (den << 32) | (num & 0xFFFFFFFF)
     uniq, inv = np.unique(key, return_inverse=True)
     vals = np.array([printed_percent(int(k & 0xFFFFFFFF), int(k >> 32)) for k in uniq.tolist()], dtype=np.float64)
     return vals[inv.reshape(-1)]
@@ -267,18 +276,21 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
     eq = np.zeros(len(offsets) - 1, np.uint8)
     if La <= ob.awidth:
         lib.nw_reads_equal_ref(ref, La, _lib.ptr(buf), _lib.ptr(offsets), len(eq), _lib.ptr(eq), nthreads)
-    same = eq[keep].astype(bool)
-    other = np.flatnonzero(~same)
-    ref_col = np.empty(len(keep), dtype=object)
-    str_col = np.empty(len(keep), dtype=object)
-    seq_col = np.empty(len(keep), dtype=object)
-    ends = np.full(len(keep), La, dtype=np.int64)
-    if same.any():
-        ref_col[same] = amplicon
-        str_col[same] = "|" * La
-        seq_col[same] = amplicon
+    other = np.flatnonzero(eq[keep] == 0)
+    # row q's strings are entry which[q] of each column's table: 0 = the amplicon's rows,
+    # 1 + p = distinct read p's (identical reads have identical rows: built once)
+    which = np.zeros(len(keep), np.int64)
+    ref_t, str_t, seq_t = [np.array([s], dtype=object) for s in (amplicon, "|" * La, amplicon)]
+    end_t = np.array([La], np.int64)
     if len(other):
-        rd = np.ascontiguousarray(keep[other], dtype=np.int64)
+        rk = np.ascontiguousarray(keep[other], dtype=np.int64)
+        rep = np.empty(len(rk), np.int64)
+        lib.nw_reads_first_copy(_lib.ptr(buf), _lib.ptr(offsets), _lib.ptr(rk), len(rk), _lib.ptr(rep), nthreads)
+        first = np.flatnonzero(rep == np.arange(len(rk)))
+        rd = rk[first]
+        slot = np.empty(len(rk), np.int64)
+        slot[first] = np.arange(1, len(first) + 1)
+        which[other] = slot[rep]
         cols = np.minimum(st["aln_len"][rd], ob.awidth).astype(np.int64)
         row_off = np.zeros(len(rd) + 1, np.int64)
         np.cumsum(cols, out=row_off[1:])
@@ -294,20 +306,25 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
         if rc != _lib.NW_OK:
             raise NeedleException("Failed to build the alignment rows (runs inconsistent with the reads, "
                                   "or a byte outside ASCII in a read)")
-        amp_row = is_amp.astype(bool)
-        refs = np.empty(len(rd), dtype=object)
-        refs[amp_row] = amplicon
-        if not amp_row.all():   # the gapped amplicon rows
-            sub = np.flatnonzero(~amp_row)
-            refs[sub] = _strings(r0, row_off, take=sub, ascii_checked=True)
-        ref_col[other] = refs
-        str_col[other] = _strings(r1, row_off, ascii_checked=True)
-        seq_col[other] = _strings(r2, row_off, ascii_checked=True)
-        ends[other] = nchar
-    len_col = _int_strings(ends)
-    data = {"score_" + name: ident, "length": len_col, "ref_seq": ref_col, "align_str": str_col,
-            "align_seq": seq_col}
-    return pd.DataFrame(data, index=index, columns=["score_" + name, "length", "ref_seq", "align_str", "align_seq"])
+        refs = np.empty(len(rd) + 1, dtype=object)
+        refs[0] = amplicon
+        amp_row = np.flatnonzero(is_amp)
+        refs[1 + amp_row] = amplicon
+        if len(amp_row) < len(rd):   # the gapped amplicon rows
+            sub = np.flatnonzero(is_amp == 0)
+            refs[1 + sub] = _strings(r0, row_off, take=sub, ascii_checked=True)
+        ref_t = refs
+        str_t = np.concatenate([str_t, _strings(r1, row_off, ascii_checked=True)])
+        seq_t = np.concatenate([seq_t, _strings(r2, row_off, ascii_checked=True)])
+        end_t = np.concatenate([end_t, nchar.astype(np.int64)])
+    # the four str columns as one object block (pandas keeps a 2-D array as its block)
+    block = np.empty((4, len(keep)), dtype=object)
+    block[0] = _int_strings(end_t[which])
+    for k, t in enumerate((ref_t, str_t, seq_t)):
+        np.take(t, which, out=block[k + 1])
+    df = pd.DataFrame(block.T, index=index, columns=["length", "ref_seq", "align_str", "align_seq"], copy=False)
+    df.insert(0, "score_" + name, ident)
+    return df
 
 
 _INT_OBJ = np.array(_INT_STR, dtype=object)
@@ -334,7 +351,7 @@ SRSPAIR_TRAILER = "#---------------------------------------\n#------------------
 
 @dataclass
 class PassResult:
-    names: List[str]
+    names: Sequence[str]
     batch: Optional[AlignmentBatch]
     ops: Optional[OpsBatch] = None          # the ops path: runs + the inputs to build rows from
     amplicon: str = ""
@@ -374,19 +391,19 @@ def needle_pass(aligner: GpuAligner, amplicon: str, names: Sequence[str], buf: n
             aligner.set_reference(amplicon)
         if use_ops and resident:
             ob = aligner.align_ops(None, offsets, resident=True, records_only=just_score and not outfile)
-            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
+            res = PassResult(names if isinstance(names, (list, fastq.NameList)) else list(names), None, ob, amplicon, buf, offsets)
             batch = ob.expand(amplicon, buf, offsets) if outfile else None
         elif use_ops and packed is not None:
             ob = aligner.align_ops_packed(packed)
-            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
+            res = PassResult(names if isinstance(names, (list, fastq.NameList)) else list(names), None, ob, amplicon, buf, offsets)
             batch = ob.expand(amplicon, buf, offsets) if outfile else None
         elif use_ops:
             ob = aligner.align_ops(buf, offsets, records_only=just_score and not outfile)
-            res = PassResult(names if isinstance(names, list) else list(names), None, ob, amplicon, buf, offsets)
+            res = PassResult(names if isinstance(names, (list, fastq.NameList)) else list(names), None, ob, amplicon, buf, offsets)
             batch = ob.expand(amplicon, buf, offsets) if outfile else None
         else:
             batch = aligner.align_packed(buf, offsets, strings=not just_score or bool(outfile))
-            res = PassResult(names if isinstance(names, list) else list(names), batch)
+            res = PassResult(names if isinstance(names, (list, fastq.NameList)) else list(names), batch)
     except (NeedleError, UnsupportedNeedleOption) as exc:
         raise NeedleException("Needle failed to run, please check the log file.") from exc
     if outfile:

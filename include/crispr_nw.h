@@ -320,6 +320,11 @@ int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int
 /* After nw_fastq_pack: the reads' lengths as nw_align_ops_packed_lens takes them, in the
  * same kind of memory; NW_E_UNSUPPORTED (null) when a read is longer than 65535. */
 int nw_fastq_lens(nw_fastq* q, const uint16_t** lens);
+/* The DataFrame's ID column (CRISPRessoCORE.py:1725) from nw_fastq_names' block (n names,
+ * each followed by '\n'): ids = the names' bytes without the newlines, '_' -> ':'; name i
+ * at [off[i], off[i + 1]) (off: n + 1 entries).  NW_E_UNSUPPORTED when a name holds
+ * whitespace or a non-ASCII byte, or the block does not hold n names. */
+int nw_names_to_ids(const uint8_t* raw, int64_t nbytes, int64_t n, uint8_t* ids, int64_t* off);
 
 /* nw_expand_ops for the reads idx[0 .. m) only: read idx[q]'s rows at aln_out + q*3*stride. */
 int nw_expand_ops_subset(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets,
@@ -339,6 +344,13 @@ int nw_ops_rows_concat(const char* ref, int32_t ref_len, const char* reads, cons
  * count. */
 int64_t nw_reads_equal_ref(const char* ref, int32_t ref_len, const char* reads, const int64_t* offsets, int64_t n,
                            uint8_t* equal, int32_t nthreads);
+
+/* Over the reads idx[0 .. m) (idx null: reads 0 .. m): rep[q] = the first q' whose read has
+ * read idx[q]'s bytes (rep[q] == q for the first of each); returns the number of distinct
+ * reads.  The alignment is a function of the read's bytes, so the DataFrame hand-off builds
+ * the row strings of each distinct read once and shares them. */
+int64_t nw_reads_first_copy(const char* reads, const int64_t* offsets, const int64_t* idx, int64_t m, int64_t* rep,
+                            int32_t nthreads);
 
 /* srspair text of n alignments (the blocks parse_needle_output consumes,
  * CRISPRessoCORE.py:1715-1765).  aname = amplicon id; bnames = n NUL-separated

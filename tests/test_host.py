@@ -198,3 +198,48 @@ def test_read_lengths16():
     assert len(read_lengths16(np.zeros(1, np.int64))) == 0
     buf, o2 = synth.reads_from(synth.random_amplicon(120, 4), 50, 5)
     assert np.array_equal(pack_2bit(buf, o2).lens, np.diff(o2))
+
+
+def test_reads_first_copy():
+    """nw_reads_first_copy (the DataFrame hand-off builds each distinct read's strings once):
+    the first index with the same bytes, over all reads and over an index subset; reads that
+    differ only in length or case are distinct."""
+    from crispresso_amd import _lib
+
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(11))
+    pool = ["".join(rng.choice(list("ACGT"), int(rng.integers(0, 40)))) for _ in range(300)]
+    pool += ["ACGT", "ACG", "acgt", ""]
+    reads = [pool[int(k)] for k in rng.integers(0, len(pool), 50_000)]
+    buf, off = pack_reads(reads)
+    for idx in (None, np.sort(rng.choice(len(reads), 20_000, replace=False)).astype(np.int64)):
+        sel = list(range(len(reads))) if idx is None else idx.tolist()
+        seen, want = {}, []
+        for q, r in enumerate(sel):
+            want.append(seen.setdefault(reads[r], q))
+        rep = np.empty(len(sel), np.int64)
+        nd = lib.nw_reads_first_copy(_lib.ptr(buf), _lib.ptr(off), None if idx is None else _lib.ptr(idx), len(sel),
+                                     _lib.ptr(rep), 0)
+        assert nd == len(seen) and rep.tolist() == want
+
+
+def test_names_to_ids():
+    """nw_names_to_ids: CORE:1725's split()[-1].replace('_', ':') of each name, for names
+    without whitespace (the reader keeps the header's first word); a name with whitespace,
+    a non-ASCII byte or a count mismatch is left to Python."""
+    from crispresso_amd import _lib
+
+    lib = _lib.load()
+    rng = np.random.Generator(np.random.PCG64(12))
+    names = [f"@M0_{k}_{'x' * int(rng.integers(0, 30))}_1" if k % 7 else "" for k in range(200_000)]
+    raw = np.frombuffer(("\n".join(names) + "\n").encode(), np.uint8).copy()   # > 1 MB: the parallel path
+    ids = np.empty(len(raw), np.uint8)
+    off = np.empty(len(names) + 1, np.int64)
+    assert lib.nw_names_to_ids(_lib.ptr(raw), len(raw), len(names), _lib.ptr(ids), _lib.ptr(off)) == _lib.NW_OK
+    got = [ids[off[i]:off[i + 1]].tobytes().decode() for i in range(len(names))]
+    assert got == [nm.replace("_", ":") for nm in names]
+    for bad in (b"@a b\n@c\n", "@é\n@c\n".encode()):
+        r = np.frombuffer(bad, np.uint8).copy()
+        assert lib.nw_names_to_ids(_lib.ptr(r), len(r), 2, _lib.ptr(ids), _lib.ptr(off)) == _lib.NW_E_UNSUPPORTED
+    r = np.frombuffer(b"@a\n@c\n", np.uint8).copy()
+    assert lib.nw_names_to_ids(_lib.ptr(r), len(r), 3, _lib.ptr(ids), _lib.ptr(off)) == _lib.NW_E_UNSUPPORTED
