@@ -47,7 +47,7 @@ EXPORTS = (
     "nw_align_ops_packed_lens", "nw_align_multi_ops_packed_lens", "nw_read_lengths16", "nw_fastq_lens",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
-    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_reads_first_copy", "nw_names_to_ids", "nw_ops_rows_concat", "nw_fastq_pack", "nw_batch_device_ops",
+    "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_reads_first_copy", "nw_names_to_ids", "nw_gunzip_parallel", "nw_ops_rows_concat", "nw_fastq_pack", "nw_batch_device_ops",
 )
 
 # Every symbol include/crispr_quant.h declares.
@@ -147,6 +147,7 @@ def load() -> ctypes.CDLL:
         "nw_reads_equal_ref": (c_int64, [c_char_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int32]),
         "nw_reads_first_copy": (c_int64, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32]),
         "nw_names_to_ids": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+        "nw_gunzip_parallel": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p]),
         "nw_fastq_count": (c_int64, [c_void_p]),
         "nw_fastq_seqs": (c_void_p, [c_void_p]),
         "nw_fastq_offsets": (c_void_p, [c_void_p]),

@@ -50,6 +50,7 @@
 #include <vector>
 
 #include "../../include/crispr_nw.h"
+#include "gz_inflate.h"
 #include "host_pool.h"
 
 // std::vector storage that resize() leaves uninitialised: the ingest's buffers are written
@@ -228,6 +229,7 @@ struct Deflate {
     void* (*alloc)() = nullptr;
     int (*gzip_ex)(void*, const void*, size_t, void*, size_t, size_t*, size_t*) = nullptr;
     void (*release)(void*) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void*, size_t) = nullptr;   // optional (folding CRC)
     Deflate() {
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
@@ -235,6 +237,7 @@ struct Deflate {
         gzip_ex = (int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*))dlsym(
             h, "libdeflate_gzip_decompress_ex");
         release = (void (*)(void*))dlsym(h, "libdeflate_free_decompressor");
+        crc32 = (uint32_t(*)(uint32_t, const void*, size_t))dlsym(h, "libdeflate_crc32");
         if (!alloc || !gzip_ex || !release) alloc = nullptr;
     }
     bool ok() const { return alloc != nullptr; }
@@ -428,6 +431,14 @@ int read_whole(const char* path, Parser& ps, bool* pending) {
         return 1;
     }
     const Deflate& D = deflate_lib();
+    {   // one member decoded by all the pool's threads (gz_inflate.h); else one thread below
+        nw_gz::Buffer whole;
+        if (nw_gz::inflate_parallel(in.p, in.n, nw_host::Pool::get().threads(), D.crc32, &whole)) {
+            parse_parallel(ps, whole.p, whole.n, pending);
+            whole.release();
+            return 1;
+        }
+    }
     if (!D.ok()) return 0;
     void* dec = D.alloc();
     if (!dec) return 0;
@@ -648,6 +659,20 @@ int nw_names_to_ids(const uint8_t* raw, int64_t nbytes, int64_t n, uint8_t* ids,
     for (char b : bad)
         if (b) return NW_E_UNSUPPORTED;
     return NW_OK;
+}
+
+// The ingest's parallel decompressor on its own (gz_inflate.h): the bytes of a one-member
+// gzip image into out[0 .. cap).  NW_E_UNSUPPORTED when it does not take the image (the
+// ingest then decodes on one thread), NW_E_CAPACITY when cap is short (*out_n = the size).
+int nw_gunzip_parallel(const uint8_t* gz, int64_t n, int32_t threads, uint8_t* out, int64_t cap, int64_t* out_n) {
+    if (!gz || n < 0 || !out_n || (cap > 0 && !out)) return NW_E_INVALID;
+    nw_gz::Buffer b;
+    if (!nw_gz::inflate_parallel(gz, (size_t)n, threads, deflate_lib().crc32, &b)) return NW_E_UNSUPPORTED;
+    *out_n = (int64_t)b.n;
+    const int rc = (int64_t)b.n > cap ? NW_E_CAPACITY : NW_OK;
+    if (rc == NW_OK) std::memcpy(out, b.p, b.n);
+    b.release();
+    return rc;
 }
 
 int nw_fastq_lens(nw_fastq* q, const uint16_t** lens) {

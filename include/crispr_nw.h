@@ -320,6 +320,12 @@ int nw_fastq_pack(nw_fastq* q, int32_t pinned, const uint8_t** packed, const int
 /* After nw_fastq_pack: the reads' lengths as nw_align_ops_packed_lens takes them, in the
  * same kind of memory; NW_E_UNSUPPORTED (null) when a read is longer than 65535. */
 int nw_fastq_lens(nw_fastq* q, const uint16_t** lens);
+/* The FASTQ ingest's decompressor: a one-member gzip image decoded by `threads` threads
+ * (ranges of the compressed bits decoded from block starts found in them, chained and
+ * checked against the member's CRC-32 and size) into out[0 .. cap); *out_n = its size.
+ * NW_E_UNSUPPORTED: not taken (several members, too small, no block starts found, damaged
+ * data) -- nw_fastq_read then decodes on one thread; NW_E_CAPACITY: cap < *out_n. */
+int nw_gunzip_parallel(const uint8_t* gz, int64_t n, int32_t threads, uint8_t* out, int64_t cap, int64_t* out_n);
 /* The DataFrame's ID column (CRISPRessoCORE.py:1725) from nw_fastq_names' block (n names,
  * each followed by '\n'): ids = the names' bytes without the newlines, '_' -> ':'; name i
  * at [off[i], off[i + 1]) (off: n + 1 entries).  NW_E_UNSUPPORTED when a name holds
