@@ -22,11 +22,12 @@ namespace nw_host {
 
 class Pool {
 public:
-    // The process-wide pool: CRISPR_NW_HOST_THREADS (default min(8, cores)) threads in
+    // The process-wide pool: CRISPR_NW_HOST_THREADS (default min(16, cores): a GPU box gives a
+    // process 16 CPUs; the FASTQ ingest parses and inflates on all of them) threads in
     // all, the caller included.  Never destroyed: parked threads end with the process.
     static Pool& get() {
         static Pool* p = [] {
-            int nt = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+            int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
             if (const char* e = std::getenv("CRISPR_NW_HOST_THREADS")) nt = std::max(1, std::min(64, std::atoi(e)));
             return new Pool(nt);
         }();

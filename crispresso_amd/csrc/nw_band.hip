@@ -251,25 +251,29 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // here, the first kernel of the chain, instead of by memset launches
     if (blockIdx.x == 0 && threadIdx.x < 8) a.fallback_count[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 2 && a.ops) a.ops_ctl[threadIdx.x] = 0;
-    for (int k = threadIdx.x; k < nd; k += blockDim.x) {
-        unsigned w = 0;
-        for (int b = 0; b < 4; ++b) {
-            const int q = 4 * k + b;
-            const unsigned char c = q < La ? upcase(a.amp[q]) : 0;
-            w |= (unsigned)((c == 'A' || c == 'C' || c == 'G' || c == 'T') ? (c | 0x20) : 0) << (8 * b);
-        }
-        amp_sh[k] = w;
-        amp_sh[nd + k] = ld_dw(a.amp + 4 * k);
+    // packed input, block b: the chunk's reads of call block B = call_lo / kPkBlock + b, [bl, bh)
+    // (kPkBlock reads, one per thread; four blocks per group of kLenGroup lengths).  Its lengths'
+    // loads go out before the image copy's barrier.
+    constexpr int kPkBlock = 256;
+    static_assert(kLenGroup % kPkBlock == 0, "blocks tile the length groups");
+    const long long pB = a.pk_call_lo / kPkBlock + blockIdx.x;
+    const long long pbl = max(0ll, pB * kPkBlock - a.pk_call_lo), pbh = min(a.n, (pB + 1) * kPkBlock - a.pk_call_lo);
+    const long long pG = pB * kPkBlock / kLenGroup, pg0 = pG * kLenGroup;
+    const long long prr = pB * kPkBlock + threadIdx.x - a.pk_call_lo;   // chunk-relative
+    long long pk_l = 0, pk_pre = 0;   // this thread's read length; the group's lengths before the block (<= 3 per thread)
+    if (PK && a.pk_len) {
+        pk_l = prr < pbh ? (long long)a.pk_len[pB * kPkBlock + threadIdx.x] : 0ll;
+        for (long long q = pg0 + threadIdx.x; q < pB * kPkBlock; q += kPkBlock) pk_pre += a.pk_len[q];
     }
-    int acgt_amp = 1;   // every amplicon byte A C G T (either case)
-    for (int q = threadIdx.x; q < La; q += blockDim.x) {
-        const unsigned char c = upcase(a.amp[q]);
-        acgt_amp &= (c == 'A' || c == 'C' || c == 'G' || c == 'T');
-    }
+    // the amplicon's folded and raw dwords and the window seeds: the host-built image, one copy
+    // (the byte-input launch sizes LDS for the amplicon dwords only: no window seeds there)
+    const int img_words = PK ? a.cls_words : 2 * nd;
+    for (int k = threadIdx.x; k < img_words; k += blockDim.x) amp_sh[k] = a.cls_img[k];
+    __syncthreads();
     const int sc5 = a.band_maxsub / 5;
     // the one-substitution certificate (above): ops output, one 256-byte chunk, EDNAFULL's
     // 5 / -4 scaled, a gap open above the mismatch cost
-    const bool amp_acgt_all = __syncthreads_and(acgt_amp) != 0;
+    const bool amp_acgt_all = a.amp_acgt != 0;
     const bool sub1_ok = amp_acgt_all && a.ops && nd <= 64 && a.band_maxsub == 5 * sc5 && a.gap_open > 4 * sc5 &&
                          a.gap_extend >= 0;
     // two substitutions (x = 9/5 maxsub: a mismatch's loss against a match, D = m La - 2 x): with an
@@ -305,14 +309,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const bool win_ok = PK && amp_acgt_all && a.ops && a.band_maxsub == 5 * sc5 && a.gap_extend >= 0 && a.amp2 &&
                         a.gap_open > xl && nseed > 0 && La <= 1024;
 #endif
-    if (win_ok) {
-        for (int k = threadIdx.x; k < n2; k += blockDim.x) amp2s[k] = a.amp2[k];
-        for (int k = threadIdx.x; k < nseed; k += blockDim.x) {
-            skey[k] = a.seed_key[k];
-            spos[k] = a.seed_pos[k];
-        }
-        __syncthreads();
-    }
     // 16 bases of the packed stream from batch position p, and of the amplicon from position p (LDS)
     auto rword = [&](long long p) -> unsigned {
         const long long q = p - a.pk_pos0;
@@ -659,27 +655,19 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             batch(r0, a.n, my_off, my_len, false);
         }
     } else {
-        // block b: the chunk's reads of call block B = call_lo / kPkBlock + b, [bl, bh) (kPkBlock reads,
-        // one per thread; four blocks per group of kLenGroup lengths)
-        constexpr int kPkBlock = 256;
-        static_assert(kLenGroup % kPkBlock == 0, "blocks tile the length groups");
         __shared__ long long s_off[kPkBlock + 1];
         __shared__ unsigned char s_exc[kPkBlock];
         __shared__ long long s_wsum[8];
         __shared__ long long s_x[2];
-        const long long B = a.pk_call_lo / kPkBlock + blockIdx.x;
-        const long long bl = max(0ll, B * kPkBlock - a.pk_call_lo), bh = min(a.n, (B + 1) * kPkBlock - a.pk_call_lo);
+        const long long bl = pbl, bh = pbh;
         const int cnt = (int)(bh - bl), tid = threadIdx.x, wave = tid >> 6;
         int64_t* offs = const_cast<int64_t*>(a.offsets);
         if (a.pk_len) {
             // the offsets from the lengths (nw_align_ops_packed_lens): the group's base offset, the
             // lengths of the group's reads before this block (earlier chunks' included: they are uploaded
             // with the call's first lengths copy), an exclusive scan of the block's own
-            const long long G = B * kPkBlock / kLenGroup, g0 = G * kLenGroup;
-            const long long rr = B * kPkBlock + tid - a.pk_call_lo;   // chunk-relative
-            const long long l = rr < bh ? (long long)a.pk_len[B * kPkBlock + tid] : 0ll;
-            long long pre = 0;   // the group's reads [g0, B * kPkBlock): at most three per thread
-            for (long long q = g0 + tid; q < B * kPkBlock; q += kPkBlock) pre += a.pk_len[q];
+            const long long G = pG, rr = prr, l = pk_l;
+            long long pre = pk_pre;
             long long inc = l;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {

@@ -121,6 +121,9 @@ struct KernelArgs {
     const uint32_t* seed_key;
     const uint16_t* seed_pos;
     int32_t n_seed;
+    const uint32_t* cls_img;       // classify's LDS image of the amplicon (nw_host.cpp cls_image)
+    int32_t cls_words;
+    int32_t amp_acgt;              // every amplicon byte A C G T (either case)
 };
 
 // Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and
@@ -256,11 +259,6 @@ struct OpsHostOut {
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr,
-                              int64_t* dchunk = nullptr);
-// The chunk's runs staging[0, dchunk[1]) -> hops + dchunk[0] (the caller's page-locked run array) by
-// kernel stores, skipped when that passes hcap; max_words bounds the grid.
-hipError_t launch_ops_runs_out(const int64_t* dchunk, const uint32_t* staging, uint32_t* hops, int64_t hcap, int64_t max_words,
-                               hipStream_t s);
+                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr);
 
 }  // namespace nw

@@ -65,6 +65,10 @@ struct Profile {
     const uint32_t* seed_key = nullptr;
     const uint16_t* seed_pos = nullptr;
     int32_t n_seed = 0;
+    // classify's LDS image of the amplicon (cls_image): copied as it is by every block
+    const uint32_t* cls_img = nullptr;
+    int32_t cls_words = 0;
+    bool amp_acgt = false;             // every amplicon byte A C G T (either case)
 };
 
 // Device buffers of one chunk's kernels.  The pipelined calls alternate two sets on
@@ -196,7 +200,6 @@ struct nw_ctx {
     int out_mode = NW_OUT_ROWS;
     int64_t reads_bias = 0;            // kernels index reads with the caller's offsets minus this
     DevBuf<int64_t> d_ctl64, d_opsoff;
-    DevBuf<int64_t> d_chunkctl;        // per chunk of a call: its runs' base and total (the runs copy kernel)
     int64_t spill_cap = 0, staging_cap = 0;
     int ops_slot = nw::kOpsSlot;       // runs per read slot (CRISPR_NW_OPS_SLOT: tests force spills)
     int64_t ops_stride = 1;            // reads per slot row (the chunk capacity: ops_reserve)
@@ -259,7 +262,31 @@ struct AmpTables {
     std::vector<uint32_t> rowpos;
     std::vector<uint32_t> amp2, seed_key;   // window seeds (Profile::amp2 / seed_key / seed_pos)
     std::vector<uint16_t> seed_pos;
+    std::vector<uint32_t> cls;              // classify's LDS image (cls_image)
+    bool amp_acgt = false;
 };
+
+// classify's LDS image of the amplicon, in the kernel's LDS order: [nd] dwords of the folded
+// amplicon (lower-case A C G T, 0 at any other byte and past La), [nd] of its raw bytes (0
+// past La), then, with window seeds, amp2, the seed keys and the seed positions (uint16, two
+// per word) -- one coalesced copy per block instead of per-byte folding and three table loads.
+void cls_image(const std::string& ref, AmpTables* t) {
+    const int La = (int)ref.size(), nd = (La + 3) / 4;
+    t->cls.assign((size_t)(2 * nd), 0u);
+    t->amp_acgt = La > 0;
+    for (int q = 0; q < La; ++q) {
+        const unsigned char c = (unsigned char)ref[(size_t)q], u = c & 0xDF;
+        const bool acgt = u == 'A' || u == 'C' || u == 'G' || u == 'T';
+        t->amp_acgt = t->amp_acgt && acgt;
+        t->cls[(size_t)(q / 4)] |= (uint32_t)(acgt ? (u | 0x20) : 0) << (8 * (q % 4));
+        t->cls[(size_t)(nd + q / 4)] |= (uint32_t)c << (8 * (q % 4));
+    }
+    if (t->amp2.empty()) return;
+    t->cls.insert(t->cls.end(), t->amp2.begin(), t->amp2.end());
+    t->cls.insert(t->cls.end(), t->seed_key.begin(), t->seed_key.end());
+    for (size_t i = 0; i < t->seed_pos.size(); i += 2)
+        t->cls.push_back((uint32_t)t->seed_pos[i] | (i + 1 < t->seed_pos.size() ? (uint32_t)t->seed_pos[i + 1] << 16 : 0u));
+}
 
 // The amplicon's 2-bit stream (A C T G = 0 1 2 3 = (byte >> 1) & 3, base p in bits 2 (p % 16)
 // of dword p / 16, as nw_pack_reads packs reads; two spare dwords) and its 16-mers of A C G T
@@ -308,6 +335,7 @@ bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
     const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
     seed_tables(ref, t);
+    cls_image(ref, t);
     if (R <= 0) return true;
     const int RP = nw::profile_rp(R);
     t->prof.assign((size_t)nw::NCODE * 64 * RP, 0);
@@ -386,7 +414,7 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         total += (bytes + 255) & ~(size_t)255;
         return at;
     };
-    struct Off { size_t prof, rowpos, amp, amp2, skey, spos; };
+    struct Off { size_t prof, rowpos, amp, amp2, skey, spos, cls; };
     std::vector<Off> offs(refs.size());
     for (size_t g = 0; g < refs.size(); ++g) {
         if (!amp_tables(refs[g], c->scale, &tabs[g]))
@@ -394,7 +422,8 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         const AmpTables& t = tabs[g];
         const size_t o1 = sec(t.prof.size()), o5 = sec(t.rowpos.size() * 4), o6 = sec(refs[g].size() + 16);
         const size_t o7 = sec(t.amp2.size() * 4), o8 = sec(t.seed_key.size() * 4), o9 = sec(t.seed_pos.size() * 2);
-        offs[g] = {o1, o5, o6, o7, o8, o9};
+        const size_t o10 = sec(t.cls.size() * 4);
+        offs[g] = {o1, o5, o6, o7, o8, o9, o10};
     }
     std::vector<uint8_t> host(std::max<size_t>(total, 256), 0);
     for (size_t g = 0; g < refs.size(); ++g) {
@@ -406,6 +435,7 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         std::memcpy(host.data() + o.amp2, t.amp2.data(), t.amp2.size() * 4);
         std::memcpy(host.data() + o.skey, t.seed_key.data(), t.seed_key.size() * 4);
         std::memcpy(host.data() + o.spos, t.seed_pos.data(), t.seed_pos.size() * 2);
+        std::memcpy(host.data() + o.cls, t.cls.data(), t.cls.size() * 4);
     }
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));   // no kernel may still read the old arena
     HIP_OR_FAIL(c, c->d_arena.reserve(host.size()));
@@ -420,6 +450,9 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         p.amp = b + o.amp;
         p.R = tabs[g].R;
         p.amp_plain = tabs[g].amp_plain;
+        p.cls_img = (const uint32_t*)(b + o.cls);
+        p.cls_words = (int32_t)tabs[g].cls.size();
+        p.amp_acgt = tabs[g].amp_acgt;
         if (!tabs[g].amp2.empty()) {
             p.amp2 = (const uint32_t*)(b + o.amp2);
             p.seed_key = (const uint32_t*)(b + o.skey);
@@ -976,6 +1009,9 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.seed_key = c->cur.seed_key;
         a.seed_pos = c->cur.seed_pos;
         a.n_seed = c->cur.n_seed;
+        a.cls_img = c->cur.cls_img;
+        a.cls_words = c->cur.cls_words;
+        a.amp_acgt = c->cur.amp_acgt ? 1 : 0;
         a.lb_status = c->s->d_lb.p;
         // packed input (ops_call): classify decodes the chunk (KernelArgs::pk_*)
         a.pk_words = c->pkc.pk_words;
@@ -1125,8 +1161,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
 // staging[which]: ops_off of those reads (global: the call's running base in
 // ctl[0]) and ctl[1..3] = chunk base, chunk total, error.
 int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr, hipEvent_t prev_done = nullptr,
-                     int64_t* hctl = nullptr, int parity = 0, const nw::OpsHostOut* host = nullptr,
-                     int64_t* dchunk = nullptr) {
+                     int64_t* hctl = nullptr, int parity = 0, const nw::OpsHostOut* host = nullptr) {
     int rc = launch_range(c, base);
     if (rc) return rc;
     // only the compaction writes the set's staging array: it waits for the copy of the
@@ -1154,8 +1189,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
                                           c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
-                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host,
-                                          dchunk));
+                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host));
     return NW_OK;
 }
 
@@ -1971,21 +2005,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
-    // Free-running calls (uploads, every output page-locked): a chunk's runs go back by a copy
-    // kernel on s_out that reads its base and total on the device (nw_ops_runs_out), records and
-    // offsets by copies of known size -- the host waits for nothing inside the loop, so every
-    // chunk's launches are queued while the uploads stream, and the last chunk's kernels wait for
-    // its upload, not for the host (which had waited for chunk k - 2 before queueing chunk k).
-    // The adaptive choices read the newest chunk already finished (hipEventQuery), if any.
-    const bool free_run = upload && direct_out;
-    if (free_run) HIP_OR_FAIL(c, c->d_chunkctl.reserve((size_t)(2 * std::max<int64_t>(nchunks, 1))));
-    int64_t newest_done = -1;   // free-running: the newest chunk known finished
-    auto done_upto = [&](int64_t j) {   // chunk j finished (the compactions run in chunk order)
-        if (j <= newest_done) return true;
-        if (hipEventQuery(c->ev_ce[(size_t)j]) != hipSuccess) return false;
-        newest_done = j;
-        return true;
-    };
     const int64_t lag = std::max(1, nsets - 1);
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
@@ -2061,15 +2080,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // The newest chunk the host has read back (k - lag - 1, synchronised in copy_runs)
         // decides from its own counts when it ran both levels; while the level is skipped
         // every 4th chunk runs both again, so input that changes back is noticed.
-        // free-running: the newest finished chunk at or before k - lag - 1 (none: keep the choice)
-        int64_t jn = k - lag - 1;
-        if (free_run) {   // two event queries at most: the candidate, else the one after the newest known
-            if (jn >= 0 && !done_upto(jn) && newest_done + 1 < jn) (void)done_upto(newest_done + 1);
-            jn = std::min<int64_t>(newest_done, jn);
-        }
-        const bool have_j = free_run ? jn >= 0 : k >= lag + 1;
-        if (adaptive && have_j) {   // pooled calls too: one library's amplicons, one read source
-            const int64_t j = jn;
+        if (adaptive && k >= lag + 1) {   // pooled calls too: one library's amplicons, one read source
+            const int64_t j = k - lag - 1;
             const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
             static const int64_t zero[nw::kOpsCtl] = {};
             const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
@@ -2084,8 +2096,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // the exact kernel's grid: small while the newest chunk read back sent it few reads
         // (after the wide level it gets the rare read no band certifies)
         c->exact_small = true;
-        if (have_j) {
-            const int64_t j = jn;
+        if (k >= lag + 1) {
+            const int64_t j = k - lag - 1;
             const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
             c->exact_small = h[10] - (j > 0 ? c->h_ctl[nw::kOpsCtl * (j - 1) + 10] : 0) < 256;
         }
@@ -2097,8 +2109,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
         // two gaps, not down one diagonal), the next chunks skip it; while skipped, every 4th
         // chunk runs it again
-        if (adaptive && have_j) {
-            const int64_t j = jn;
+        if (adaptive && k >= lag + 1) {
+            const int64_t j = k - lag - 1;
             const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
             static const int64_t zero[nw::kOpsCtl] = {};
             const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
@@ -2116,27 +2128,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                           ops_out ? ops_cap : 0};
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
                                    k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k,
-                                   (int)(k & 1), direct_k ? &ho : nullptr,
-                                   free_run ? c->d_chunkctl.p + 2 * k : nullptr)))
+                                   (int)(k & 1), direct_k ? &ho : nullptr)))
             return restore(rc);
         direct_done[(size_t)k] = direct_k;
         no_diag[(size_t)k] = !c->diag_ran;
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
-        if (free_run) {   // s_out: the chunk's records, offsets and runs (device-sized), then its staging is free
-            HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
-            if (!direct_k) {
-                HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
-                                              hipMemcpyDeviceToHost, c->s_out));
-                HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
-                                              hipMemcpyDeviceToHost, c->s_out));
-                if (ops_out)
-                    HIP_OR_FAIL(c, nw::launch_ops_runs_out(c->d_chunkctl.p + 2 * k, c->s->d_staging.p, ops_out, ops_cap,
-                                                           3 * (hi - lo), c->s_out));
-            }
-            HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
-            c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
-            continue;
-        }
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
         // k's records and offsets
@@ -2157,20 +2153,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
     }
-    if (!free_run)
-        for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k)
-            if ((rc = copy_runs(k))) return restore(rc);
+    for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k)
+        if ((rc = copy_runs(k))) return restore(rc);
     ht.lap(4);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);
-    if (free_run)   // every chunk's ctl is in h_ctl now (s_out waited for every chunk's end)
-        for (int64_t k = 0; k < nchunks; ++k) {
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
-            err |= h[3];
-            total = h[1] + h[2];
-            if (ops_out && total > ops_cap) cap_short = true;
-            if (ops_out) c->ops_d2h_bytes += 4 * h[2];
-        }
     ops_off[n] = total;
     if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)
         const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);

@@ -54,8 +54,7 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
                                                               unsigned long long* status, unsigned epoch, int parity,
                                                               int64_t* ctl, int64_t* ops_off, uint32_t* staging,
                                                               int64_t staging_cap, const int32_t* opsctl,
-                                                              OpsCounts cnt, int64_t* hctl, int prio, OpsHostOut ho,
-                                                              int64_t* dchunk) {
+                                                              OpsCounts cnt, int64_t* hctl, int prio, OpsHostOut ho) {
     __shared__ int sh_bad;
     __shared__ unsigned sh_excl;
     if (prio) __builtin_amdgcn_s_setprio(3);
@@ -137,10 +136,6 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         const long long chunk_total = (long long)sh_excl + total;
         ctl[1] = base;
         ctl[2] = chunk_total;
-        if (dchunk) {   // this chunk's base and total, kept for its runs copy (nw_ops_runs_out)
-            dchunk[0] = base;
-            dchunk[1] = chunk_total;
-        }
         ops_off[n] = base + chunk_total;   // the end of the chunk's last read (the next chunk's first offset)
         ctl[0] = base + chunk_total;
         ctl[kOpsCtl + (parity ^ 1)] = base + chunk_total;
@@ -166,35 +161,16 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
     }
 }
 
-// The chunk's runs (staging[0, total)) to the caller's page-locked run array at its base, by
-// kernel stores: the base and total come from the chunk's compaction (dchunk), so no host round
-// trip sizes the copy.  A copy that would pass hcap is skipped (the host reports NW_E_CAPACITY).
-__global__ __launch_bounds__(256) void nw_ops_runs_out(const int64_t* dchunk, const uint32_t* staging, uint32_t* hops,
-                                                       int64_t hcap) {
-    const long long base = dchunk[0], tot = dchunk[1];
-    if (base + tot > hcap) return;
-    uint32_t* dst = hops + base;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long long)gridDim.x * blockDim.x)
-        dst[i] = staging[i];
-}
-
 }  // namespace
-
-hipError_t launch_ops_runs_out(const int64_t* dchunk, const uint32_t* staging, uint32_t* hops, int64_t hcap, int64_t max_words,
-                               hipStream_t s) {
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(256, (max_words + 4095) / 4096));
-    hipLaunchKernelGGL(nw_ops_runs_out, dim3(grid), dim3(256), 0, s, dchunk, staging, hops, hcap);
-    return hipGetLastError();
-}
 
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl, const OpsHostOut* host, int64_t* dchunk) {
+                              hipStream_t s, int64_t* hctl, const OpsHostOut* host) {
     const OpsHostOut ho = host ? *host : OpsHostOut{};
     const int nblk = (int)std::max<int64_t>(1, (n + kOpsBlockReads - 1) / kOpsBlockReads);
     hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, stride, spill, n, status, epoch,
-                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio, ho, dchunk);
+                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio, ho);
     return hipGetLastError();
 }
 

@@ -310,11 +310,12 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
         refs[0] = amplicon
         amp_row = np.flatnonzero(is_amp)
         refs[1 + amp_row] = amplicon
-        if len(amp_row) < len(rd):   # the gapped amplicon rows
+        if len(amp_row) < len(rd):   # the gapped amplicon rows (a few hundred distinct ones)
             sub = np.flatnonzero(is_amp == 0)
-            refs[1 + sub] = _strings(r0, row_off, take=sub, ascii_checked=True)
+            refs[1 + sub] = _distinct_strings(lib, r0, row_off, sub, nthreads)
         ref_t = refs
-        str_t = np.concatenate([str_t, _strings(r1, row_off, ascii_checked=True)])
+        # markup rows repeat across reads (the same substitution positions): one str per distinct row
+        str_t = np.concatenate([str_t, _distinct_strings(lib, r1, row_off, None, nthreads)])
         seq_t = np.concatenate([seq_t, _strings(r2, row_off, ascii_checked=True)])
         end_t = np.concatenate([end_t, nchar.astype(np.int64)])
     # the four str columns as one object block (pandas keeps a 2-D array as its block)
@@ -325,6 +326,23 @@ def ops_to_dataframe(ob: OpsBatch, amplicon: str, buf: np.ndarray, offsets: np.n
     df = pd.DataFrame(block.T, index=index, columns=["length", "ref_seq", "align_str", "align_seq"], copy=False)
     df.insert(0, "score_" + name, ident)
     return df
+
+
+def _distinct_strings(lib, data: np.ndarray, off: np.ndarray, take: Optional[np.ndarray], nthreads: int) -> np.ndarray:
+    """_strings(data, off, take) with one str object per distinct byte string (equal rows
+    share it; nw_reads_first_copy finds the first of each)."""
+    idx = np.arange(len(off) - 1, dtype=np.int64) if take is None else np.ascontiguousarray(take, dtype=np.int64)
+    if len(idx) == 0:
+        return np.empty(0, dtype=object)
+    rep = np.empty(len(idx), np.int64)
+    lib.nw_reads_first_copy(_lib.ptr(data), _lib.ptr(off), _lib.ptr(idx), len(idx), _lib.ptr(rep), nthreads)
+    first = np.flatnonzero(rep == np.arange(len(idx)))
+    uniq = _strings(data, off, take=idx[first], ascii_checked=True)
+    if len(first) == len(idx):
+        return uniq
+    slot = np.empty(len(idx), np.int64)
+    slot[first] = np.arange(len(first))
+    return uniq[slot[rep]]
 
 
 _INT_OBJ = np.array(_INT_STR, dtype=object)
