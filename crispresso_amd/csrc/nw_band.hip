@@ -546,9 +546,40 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 }
             }
         }
+        // Seeded band: a read the 16-diagonal band cannot hold (La - Lb >= 16, the
+        // reference's own 151 bp reads on a 280 bp amplicon) and no window certificate took: the
+        // diagonals of every exact hit of its disjoint 16-base blocks among the amplicon's 16-mers.
+        // The wide level then centres its band on them and certifies it (nw_band_walk).  A block
+        // with more than 8 hits (a repeat) leaves the read to the exact kernel.
+        int32_t sinfo = 0;
+        if constexpr (PK) {
+            if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
+                !(((exact | sub1 | sub2 | win) >> lane) & 1ull)) {
+                int dmin = 1 << 20, dmax = -(1 << 20);
+                bool ok = true;
+                const int nb = my_len >> 4;
+                for (int b = 0; b < nb && ok; ++b) {
+                    const unsigned key = rword(my_off + 16 * b);
+                    int f;
+                    const int l = seed_range(key, &f);
+                    if (f > 0 && skey[f - 1] == key) ok = false;   // more occurrences than seed_range returns
+                    for (int i = f; ok && i < l; ++i) {
+                        const int d = 16 * b - (int)spos[i];
+                        dmin = min(dmin, d);
+                        dmax = max(dmax, d);
+                    }
+                }
+                if (ok && dmax >= dmin && dmax - dmin <= kWideDiags / 2 && nb < 128)
+                    sinfo = seed_pack(dmin, dmax, nb);
+            }
+            if (a.seed_info && r < r_end) a.seed_info[r] = sinfo;
+        }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2 | win) >> lane) & 1ull) ? a.band_lb_cap + 2
-                                                                     : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1);
+            a.sort_key[r] = (((exact | sub1 | sub2 | win) >> lane) & 1ull)
+                                ? a.band_lb_cap + 2
+                                : (sinfo ? a.band_lb_cap + 3 +
+                                               min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
+                                         : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1));
         if (a.ops && r < r_end && ((win >> lane) & 1ull)) {
             // runs: s amplicon residues (Y), the window (M), the rest of the amplicon (Y)
             int q = 0;
@@ -757,11 +788,14 @@ __host__ __device__ inline int segsort_lds_bytes(int lb_cap) { return 4 * (kSegW
 
 __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs a, unsigned epoch) {
     extern __shared__ int seg_sm[];
-    const int NB = a.band_lb_cap + 3, EX = NB - 1;   // key EX: exact copy (no DP)
+    // keys: lengths 0 .. cap, cap + 1 (too long for the band), EX = cap + 2 (exact copy, no DP),
+    // then the seeded reads' diagonal keys
+    const int NB = a.band_lb_cap + 3 + a.seed_keys, EX = a.band_lb_cap + 2;
     int* cnt = seg_sm;                  // [kSegWaves][NB]: per-wave counts, then prefix over waves
     int* kbase = seg_sm + kSegWaves * NB;   // [NB]: bucket totals, then their exclusive prefix
     int* misc = kbase + NB;             // [0], [1] look-back results (lists B, A), [2] error, [16..31] wave sums
     const int KA = a.order_a ? a.La : -1;   // the key of list A (none without the diagonal pass)
+    const int KS = a.seed_list ? a.band_lb_cap + 3 : NB;   // keys >= KS: seeded reads (their own list)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int k = tid; k < kSegWaves * NB + NB; k += kSegThreads) seg_sm[k] = 0;
     if (tid < 32) misc[tid] = 0;
@@ -825,28 +859,37 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
         kbase[k] = run;
         run += v;
     }
+    __syncthreads();
+    // the seeded keys are the tail of the key range: their prefix past the band list's total is
+    // their place in the seeded list
+    const int dpB = KS < NB ? kbase[KS] : dp, dpS = dp - dpB;
     const int dpA = misc[3];
     if (wave == 0) {
-        const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dp, &misc[2]);
+        const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dpB, &misc[2]);
         if (lane == 0) misc[0] = (int)base;
     } else if (wave == 1 && KA >= 0) {   // list A: the look-back words after list B's
         const unsigned base = lookback_excl(a.lb_status + gridDim.x + 1, blockIdx.x, epoch, (unsigned)dpA, &misc[2]);
         if (lane == 0) misc[1] = (int)base;
+    } else if (wave == 2 && a.seed_list) {   // the seeded list: after list A's words
+        const unsigned base = lookback_excl(a.lb_status + 2 * (gridDim.x + 1), blockIdx.x, epoch, (unsigned)dpS, &misc[2]);
+        if (lane == 0) misc[4] = (int)base;
     }
     __syncthreads();
-    const long long base = misc[0], baseA = misc[1];
+    const long long base = misc[0], baseA = misc[1], baseS = misc[4];
     int32_t* order = const_cast<int32_t*>(a.band_order);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = key[i];
         if (k == KA) a.order_a[baseA + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
+        else if (k >= KS) a.seed_list[baseS + (kbase[k] - dpB) + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
         else if (k != EX) order[base + kbase[k] + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
     }
     if (tid == 0) {
         if (misc[2]) a.fallback_count[3] = 1;   // look-back cut off: the call reports an error
         if (blockIdx.x == gridDim.x - 1) {
-            *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dp);
+            *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dpB);
             if (KA >= 0) *a.count_a = (int32_t)(baseA + dpA);
+            if (a.seed_list) *a.seed_count = (int32_t)(baseS + dpS);
         }
     }
 }
@@ -1039,12 +1082,18 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
 // The wide level (a.band_from_work) reads the exact kernel's work list instead: the reads the
 // narrower levels gave up on, then (direct hand-off) the first level's redo list; there
 // a.band_count = a.work_count.
+// The wide level's list ends with the seeded reads (the segment sort's seeded list, sorted by
+// their hits' diagonals, so a pair's two reads share a band).
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
-    if (a.band_from_work) return exact_work_count(a);
+    if (a.band_from_work) return exact_work_count(a) + (a.seed_list ? (long long)*a.seed_count : 0ll);
     return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
-    if (a.band_from_work) return k < nb ? a.work_list[k] : (long long)a.redo_list[k - nb];
+    if (a.band_from_work) {
+        if (k < nb) return a.work_list[k];
+        const long long nr = redo_direct_taken(a) ? (long long)*a.redo_count : 0ll;
+        return k < nb + nr ? (long long)a.redo_list[k - nb] : (long long)a.seed_list[k - nb - nr];
+    }
     return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
 }
 
@@ -1126,6 +1175,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         bool act = false;
         long long offA = 0, offB = 0, ra = 0, rb = 0;
         int LbA = 0, LbB = 0;
+        bool seeded = false;
         if (g < pair_hi) {
             if constexpr (TB) {
                 ra = band_list_read(a, 2 * g, nb);
@@ -1139,6 +1189,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
             act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo, W);
+            if constexpr (TB && W > kBandDiags) {
+                // seeded reads (both of the pair): the band centred on their hits' diagonals
+                if (a.seed_info) {
+                    const int32_t sa = a.seed_info[ra], sb = a.seed_info[rb];
+                    const int lo = min(seed_dmin(sa), seed_dmin(sb)), hi = max(seed_dmax(sa), seed_dmax(sb));
+                    const int sdlo = lo - (W - (hi - lo + 1)) / 2;
+                    if (seed_valid(sa) && seed_valid(sb) && hi - lo + 1 <= W - 2 && LbA <= a.band_lb_cap &&
+                        LbB <= a.band_lb_cap && sdlo <= kBK && sdlo + W - 1 >= 1 - La) {
+                        dlo = sdlo;   // (tau = t - dlo + kBK stays >= 0)
+                        act = true;
+                        seeded = true;
+                    }
+                }
+            }
         }
         if (!act) {   // neutral geometry, nothing stored
             band_geometry2(La, La, La, &dlo, W);
@@ -1234,7 +1298,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         if (TB && q == 0 && g < pair_hi) {
             // everything the walk needs to find the pair's reads: one 48-byte load
             int4* hp = (int4*)region;
-            hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive), 0);
+            hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive) | (seeded ? REGION_SEEDED : 0), 0);
             hp[1] = make_int4((int)ra, (int)rb, (int)(a.offsets[ra + 1] - offA), (int)(a.offsets[rb + 1] - offB));
             hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
         }
@@ -1578,9 +1642,12 @@ __host__ __device__ inline int band_walk_shared_bytes(int La) { return 256 + ali
 constexpr int kBandRunsCap = 256;     // traceback runs per read (more: the read goes to the next level)
 __host__ __device__ inline int band_walk_row(int La, int lb_max) { return (La + lb_max + 15) & ~15; }   // = stride_for()
 __host__ __device__ inline int band_walk_rcap(int lb_max) { return min(kBandReadCap, (lb_max + 255) & ~255); }
-// per wave: runs, the read's bytes, the three output rows
-__host__ __device__ inline int band_walk_wave_bytes(int La, int lb_max) {
-    return kBandRunsCap * 4 + band_walk_rcap(lb_max) + 256 + 3 * band_walk_row(La, lb_max);
+// a pair's header and W captures, whole 64-dword DMA loads
+__host__ __device__ constexpr int band_walk_hdr_slot(int W) { return 64 * ((kHdrBytes / 4 + W + 63) / 64); }
+// per wave: runs, two read-byte buffers and two header slots (one read ahead), the three output rows
+__host__ __device__ inline int band_walk_wave_bytes(int La, int lb_max, int W) {
+    return kBandRunsCap * 4 + 2 * (band_walk_rcap(lb_max) + 256) + 2 * 4 * band_walk_hdr_slot(W) +
+           3 * band_walk_row(La, lb_max);
 }
 
 // emit_alignment (nw_common.h) with the three rows built in LDS (byte writes) and
@@ -1780,45 +1847,84 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
     };
     const int row = band_walk_row(La, a.Lb_max);   // columns <= La + Lb
     const int rcap = band_walk_rcap(a.Lb_max);
-    unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes(La, a.Lb_max);
+    constexpr int kSlot = band_walk_hdr_slot(W);   // dwords of a pair header + captures slot
+    unsigned char* wb = smem + band_walk_shared_bytes(La) + wave * band_walk_wave_bytes(La, a.Lb_max, W);
     unsigned* runs = (unsigned*)wb;
-    unsigned char* rbuf = wb + kBandRunsCap * 4;
-    unsigned char* rows = rbuf + rcap + 256;
+    unsigned char* rbufs = wb + kBandRunsCap * 4;               // [2][rcap + 256]: read bytes (DMA)
+    unsigned* hbufs = (unsigned*)(rbufs + 2 * (rcap + 256));    // [2][kSlot]: pair header + captures (DMA)
+    unsigned char* rows = (unsigned char*)(hbufs + 2 * kSlot);
 
     const long long count = band_list_count(a);
     const long long klo = 2 * a.band_pair_lo;
     const long long khi = 2 * a.band_pair_hi < count ? 2 * a.band_pair_hi : count;
-    // per read: the pair header (reads, lengths, offsets, geometry) and the 32
-    // captures come in one round trip; the next read's are loaded during this one
+    // Per read, everything it needs from memory before its walk -- the pair header (reads,
+    // lengths, offsets, geometry), the W captures and the read's bytes -- lands in LDS by DMA
+    // ahead of it: read k's bytes (and read k + kstep's header) go out right after read
+    // k - kstep's wait, so they travel during that read's walk; read k's own wait (vmcnt 0)
+    // then finds them landed, and only the walk's rounds wait on memory.
     const long long kstep = (long long)gridDim.x * wpb;
     auto region_of = [&](long long k) { return a.band_region + ((k >> 1) - a.band_pair_lo) * a.band_stride; };
-    int4 n0 = make_int4(0, 0, 0, 0), n1 = n0, n2 = n0;
-    unsigned ncw[CW];
-    auto prefetch = [&](long long k) {
-        const unsigned char* rg = region_of(k);
-        n0 = ((const int4*)rg)[0];
-        n1 = ((const int4*)rg)[1];
-        n2 = ((const int4*)rg)[2];
+    auto load_hdr = [&](long long kk, unsigned* dst) {   // header and captures: the region's first kSlot dwords
+        const unsigned char* rg = region_of(kk);
 #pragma unroll
-        for (int c = 0; c < CW; ++c) ncw[c] = lane + 64 * c < W ? ((const unsigned*)(rg + kHdrBytes))[lane + 64 * c] : 0u;
+        for (int m = 0; m < kSlot; m += 64)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(rg + 4 * (m + lane)),
+                                             (__attribute__((address_space(3))) void*)(dst + m), 4, 0, 0);
     };
-    long long k = klo + (long long)blockIdx.x * wpb + wave;
-    if (k < khi) prefetch(k);
-    auto uni = [](int4 v) {   // the prefetched header is wave-uniform: SGPRs, scalar branches
+    auto uni = [](int4 v) {   // the header is wave-uniform: SGPRs, scalar branches
         return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
                          __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
     };
-    for (; k < khi; k += kstep) {
-        const int4 hdr = uni(n0), hr = uni(n1), ho = uni(n2);
+    // read kk's length and byte offset from its header slot (kk & 1: read B of the pair)
+    auto read_of = [&](const unsigned* hb, long long kk, int* Lb, long long* off) {
+        const int4 hr = uni(*(const int4*)(hb + 4)), ho = uni(*(const int4*)(hb + 8));
+        const bool hB = (kk & 1) != 0;
+        *Lb = hB ? hr.w : hr.z;
+        *off = hB ? (long long)(((unsigned long long)(unsigned)ho.w << 32) | (unsigned)ho.z)
+                  : (long long)(((unsigned long long)(unsigned)ho.y << 32) | (unsigned)ho.x);
+    };
+    auto load_bytes = [&](long long off, int Lb, unsigned char* dst) {   // Lb <= rcap
+        const unsigned char* raw = a.reads + off;
+        const int ms = (int)((uintptr_t)raw & 3);
+        for (int m = 0; m < Lb + ms; m += 256)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(raw - ms + m + 4 * lane),
+                                             (__attribute__((address_space(3))) void*)(dst + m), 4, 0, 0);
+    };
+    long long k = klo + (long long)blockIdx.x * wpb + wave;
+    int it = 0;   // parity of the slots holding read k's header and bytes
+    if (k < khi) {   // the pipeline's start: read k's header, then its bytes and the next header
+        load_hdr(k, hbufs);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int Lb0;
+        long long off0;
+        read_of(hbufs, k, &Lb0, &off0);
+        if (Lb0 > 0 && Lb0 <= rcap) load_bytes(off0, Lb0, rbufs);
+        if (k + kstep < khi) load_hdr(k + kstep, hbufs + kSlot);
+    }
+    for (; k < khi; k += kstep, it ^= 1) {
+        const unsigned* hb = hbufs + it * kSlot;   // landed: the previous read's wait
+        unsigned char* rbuf = rbufs + it * (rcap + 256);
+        const int4 hdr = uni(*(const int4*)hb), hr = uni(*(const int4*)(hb + 4));
         unsigned cw[CW];
 #pragma unroll
-        for (int c = 0; c < CW; ++c) cw[c] = ncw[c];
-        if (k + kstep < khi) prefetch(k + kstep);
+        for (int c = 0; c < CW; ++c) cw[c] = lane + 64 * c < W ? hb[kHdrBytes / 4 + lane + 64 * c] : 0u;
         const int h = (int)(k & 1);
         const long long rd = h ? hr.y : hr.x;
-        const int Lb = h ? hr.w : hr.z;
-        const long long off = h ? (long long)(((unsigned long long)(unsigned)ho.w << 32) | (unsigned)ho.z)
-                                : (long long)(((unsigned long long)(unsigned)ho.y << 32) | (unsigned)ho.x);
+        int Lb;
+        long long off;
+        read_of(hb, k, &Lb, &off);
+        // every load issued for this read has landed (its bytes, the next read's header), and the
+        // header reads above are done (lgkmcnt); the next read's bytes and the header after it go
+        // out now, into the slots the previous read used and this read's header slot
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (k + kstep < khi) {
+            unsigned* hn = hbufs + (it ^ 1) * kSlot;
+            int Lbn;
+            long long offn;
+            read_of(hn, k + kstep, &Lbn, &offn);
+            if (Lbn > 0 && Lbn <= rcap) load_bytes(offn, Lbn, rbufs + (it ^ 1) * (rcap + 256));
+            if (k + 2 * kstep < khi) load_hdr(k + 2 * kstep, hbufs + it * kSlot);   // this read's header is in registers
+        }
         if (W < kBandDiags && a.redo_flags && lane == 0) a.redo_flags[k] = 0;   // give_up may set it
         if (Lb <= 0) {
             if (lane == 0) {
@@ -1835,16 +1941,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
         }
         const int dlo = hdr.y;
         const unsigned char* region = region_of(k);
-        const unsigned char* raw = a.reads + off;
-        // the read's bytes -> LDS (DMA, one dword per lane) for the emit
         if (Lb > rcap) {   // not reached: rcap covers the band length cap
             give_up(k, rd, false);
             continue;
         }
-        const int mis = (int)((uintptr_t)raw & 3);
-        for (int m = 0; m < Lb + mis; m += 256)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(raw - mis + m + 4 * lane),
-                                             (__attribute__((address_space(3))) void*)(rbuf + m), 4, 0, 0);
+        const int mis = (int)((uintptr_t)(a.reads + off) & 3);
         const int tau0 = hdr.x;
         // start cell: the last cell of each band diagonal is on the last row or column
         unsigned k32 = 0u;
@@ -1874,6 +1975,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
         if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
         bool certified = pmax < 0 || score > a.band_maxsub * pmax;
         const bool bad_code = (hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) != 0;
+        if (W > kBandDiags && (hdr.z & REGION_SEEDED) && !certified) {
+            // Seeded band: every exact hit of the read's nb disjoint 16-base blocks
+            // lies on diagonals [smin, smax] inside the band.  An alignment with a cell outside the
+            // band either has a block paired as an exact match -- on one of those diagonals, so its
+            // gaps shift it by >= dexit diagonals: it scores <= m Lb - O - (dexit - 1) E -- or has
+            // none: each block then loses >= m (an unpaired base, a mismatch, or a gap opened
+            // inside it, O >= m), <= m (Lb - nb).  Plain reads and amplicon, EDNAFULL 5 / -4.
+            const int32_t si = a.seed_info[rd];
+            const int smin = seed_dmin(si), smax = seed_dmax(si), nb = seed_blocks(si);
+            const int dexit = min(smin - dlo + 1, dhi - smax + 1);
+            const int m = a.band_maxsub;
+            const bool plainr = amp_acgt && !(hdr.z & (h ? (REGION_BAD_B | REGION_NP_B) : (REGION_BAD_A | REGION_NP_A)));
+            certified = plainr && seed_valid(si) && dexit >= 1 && a.gap_open >= m && a.gap_open >= a.gap_extend &&
+                        a.gap_extend >= 0 && score > m * (Lb - nb) &&
+                        score > m * Lb - a.gap_open - (dexit - 1) * a.gap_extend;
+        }
         if (!certified && !bad_code && score > a.band_maxsub * pmax - a.gap_open) {
             // Refined bound: an alignment leaving the band with an internal gap pays at
             // least the gap open, so it scores <= maxsub * pmax - O < score; one without
@@ -1881,12 +1998,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
             // overlap P(d): its score S_d is computed exactly, for the few diagonals beyond
             // the band with maxsub * P(d) >= score (P falls by one per diagonal: at most
             // about two per side, as score > maxsub * (pmax - 2)).
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the read's bytes are in LDS
             certified = band_single_diagonals_below(a, amp_lds, rbuf + mis, La, Lb, dlo, dhi, score, lane);
         }
         if (bad_code || !certified) {
             give_up(k, rd, !bad_code);   // IUPAC codes: no band helps
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             continue;
         }
         // Single-diagonal fast path: when the start cell's score equals the plain sum of
@@ -1894,7 +2009,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
         // traceback is that diagonal (M(i, j) >= D(i, j) everywhere, so H = M = D on
         // each of its cells, and M wins ties), with the end gaps around it: no band bits
         // are read.  Reads with substitutions only (most non-identical reads) take it.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read bytes landed in LDS
         int nruns;
         const int nd = min(ei, ej);
         const bool plain = amp_acgt && !(hdr.z & (h ? (REGION_BAD_B | REGION_NP_B) : (REGION_BAD_A | REGION_NP_A)));
@@ -2074,7 +2188,9 @@ int band_fill_lds_bytes(int La, int wpb, int W) {
     const int pw = W == 16 ? BandGeo<16>::PW : W == 32 ? BandGeo<32>::PW : BandGeo<kWideDiags>::PW;
     return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * pw * band_pcs(La, W) + 256 + wpb * 1024;
 }
-int band_walk_lds_bytes(int La, int wpb, int lb_max) { return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max); }
+int band_walk_lds_bytes(int La, int wpb, int lb_max, int W) {
+    return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max, W);
+}
 int band_region_words(int La, int Lb_max, int W) { return band_words(La, Lb_max, W > kBandDiags ? W : kBandDiags); }
 int64_t band_region_bytes(int La, int Lb_max, int W) { return band_region_stride(La, Lb_max, W); }
 bool band_pair_geometry(int La, int Lb, int* dlo) { return band_geometry(La, Lb, dlo); }
@@ -2106,7 +2222,7 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) 
                            dim3(256), (size_t)(8 * ((a.La + 3) / 4)), s, a);
     }
     const int nseg = (int)std::max<int64_t>(1, (a.n + kSegReads - 1) / kSegReads);
-    hipLaunchKernelGGL(nw_band_segsort, dim3(nseg), dim3(kSegThreads), (size_t)segsort_lds_bytes(a.band_lb_cap), s, a,
+    hipLaunchKernelGGL(nw_band_segsort, dim3(nseg), dim3(kSegThreads), (size_t)segsort_lds_bytes(a.band_lb_cap + a.seed_keys), s, a,
                        epoch);
     return hipGetLastError();
 }
@@ -2115,7 +2231,7 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) 
 // (1024-read blocks)
 int64_t band_lookback_words(int64_t n) {
     const int64_t seg = std::max<int64_t>(1, (n + kSegReads - 1) / kSegReads);
-    return std::max<int64_t>(std::max<int64_t>(1, (n + 1023) / 1024) + 1, 2 * seg + 2);
+    return std::max<int64_t>(std::max<int64_t>(1, (n + 1023) / 1024) + 1, 3 * seg + 3);   // lists B, A, seeded
 }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,

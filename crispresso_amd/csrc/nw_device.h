@@ -121,6 +121,13 @@ struct KernelArgs {
     const uint32_t* seed_key;
     const uint16_t* seed_pos;
     int32_t n_seed;
+    // seeded band: per read, the diagonals of its 16-mer blocks' exact hits
+    // (seed_pack), written by the packed classify; null: off.  seed_keys: sort keys past the
+    // length keys that order seeded reads by their hits' centre (the segment sort's key range)
+    int32_t* seed_info;
+    int32_t seed_keys;
+    int32_t* seed_list;            // the segment sort's seeded reads (sorted), the wide level's list tail
+    int32_t* seed_count;
     const uint32_t* cls_img;       // classify's LDS image of the amplicon (nw_host.cpp cls_image)
     int32_t cls_words;
     int32_t amp_acgt;              // every amplicon byte A C G T (either case)
@@ -168,14 +175,23 @@ hipError_t launch(const KernelArgs& a, const LaunchCfg& c, hipStream_t s);
 
 // band pair header flags: read A / B has a code outside A C G T N (BAD), or an N or a byte EDNAFULL
 // does not score (NP: not a plain read for the walk's shortcuts)
-enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2, REGION_NP_A = 8, REGION_NP_B = 16 };
+enum : int32_t { REGION_BAD_A = 1, REGION_BAD_B = 2, REGION_NP_A = 8, REGION_NP_B = 16, REGION_SEEDED = 32 };
+// seed_info word: bit 31 valid; the lowest and highest hit diagonal (d = j - i, + 1024, 11 bits
+// each) and the number of 16-base blocks (7 bits)
+__host__ __device__ inline int32_t seed_pack(int dmin, int dmax, int nb) {
+    return (int32_t)(0x80000000u | (unsigned)(dmin + 1024) | ((unsigned)(dmax + 1024) << 11) | ((unsigned)nb << 22));
+}
+__host__ __device__ inline bool seed_valid(int32_t s) { return ((unsigned)s >> 31) != 0u; }
+__host__ __device__ inline int seed_dmin(int32_t s) { return (int)((unsigned)s & 0x7ffu) - 1024; }
+__host__ __device__ inline int seed_dmax(int32_t s) { return (int)(((unsigned)s >> 11) & 0x7ffu) - 1024; }
+__host__ __device__ inline int seed_blocks(int32_t s) { return (int)(((unsigned)s >> 22) & 0x7fu); }
 
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.
 constexpr int kBandDiags = 32;
 constexpr int kWideDiags = 128;   // the wide level: the narrower levels' give-ups before the exact kernel
 int band_fill_lds_bytes(int La, int wpb, int W);
-int band_walk_lds_bytes(int La, int wpb, int lb_max);
+int band_walk_lds_bytes(int La, int wpb, int lb_max, int W);
 int band_region_words(int La, int Lb_max, int W = kBandDiags);
 int64_t band_region_bytes(int La, int Lb_max, int W);
 bool band_pair_geometry(int La, int Lb, int* dlo);
@@ -246,6 +262,7 @@ struct OpsCounts {
     const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
     const int32_t* handed;     // ... and the reads it handed on
     const int32_t* exact;      // the wide level's give-ups: the exact kernel's reads (null: no wide level)
+    const int32_t* seeded;     // the seeded reads (straight to the wide level; null: none)
 };
 // The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
 // straight into the caller's page-locked buffers (no copies and no host round trip after it).

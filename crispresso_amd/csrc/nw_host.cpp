@@ -77,6 +77,8 @@ struct Profile {
 struct Scratch {
     DevBuf<uint8_t> d_tb;              // exact kernel: traceback slabs when they do not fit LDS
     DevBuf<int64_t> d_fallback;        // reads the 16 / 32-diagonal levels gave up on (the wide level's input)
+    DevBuf<int32_t> d_seed;            // seeded band: per read of the chunk, its hits' diagonals (seed_pack)
+    DevBuf<int32_t> d_seed_list;       // seeded band: the chunk's seeded reads (the segment sort's third list)
     DevBuf<int64_t> d_fallback2;       // reads the wide level gave up on (the exact kernel's list)
     DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
@@ -90,7 +92,7 @@ struct Scratch {
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
-        d_tile.release();
+        d_tile.release(); d_seed.release(); d_seed_list.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
@@ -176,6 +178,12 @@ struct nw_ctx {
     nw::LaunchCfg wide_fill{}, wide_walk{};
     int64_t wide_pairs = 0, wide_stride = 0;
     int wide_words = 0, wide_lb_cap = 0;
+    // seeded band of the current call: reads the 16-diagonal band cannot hold
+    // (La - Lb >= 16) go to the wide level centred on their 16-mer hits; seed_pairs widens the
+    // wide level's region for them, seed_keys their sort keys
+    bool seed_on = false, seed_chunk = false;
+    int64_t seed_pairs = 0;
+    int32_t seed_keys = 0;
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
     DevBuf<uint32_t> d_btab;
     DevBuf<uint32_t> d_sub16;         // exact multi-wave kernel's score rows
@@ -608,7 +616,7 @@ int configure(nw_ctx* c) {
             f.wpb = wide ? wide_fill_wpb : 8;
             w.wpb = wide ? wide_walk_wpb : 8;
             f.lds_bytes = nw::band_fill_lds_bytes(La, f.wpb, W);
-            w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb, c->lb_max);
+            w.lds_bytes = nw::band_walk_lds_bytes(La, w.wpb, c->lb_max, W);
             int fb = 0, wb = 0;
             if (f.lds_bytes > kMaxLds || w.lds_bytes > kMaxLds) return 0;
             if (nw::band_occupancy(W, f.wpb, w.wpb, f.lds_bytes, w.lds_bytes, &fb, &wb) != hipSuccess || fb <= 0 ||
@@ -636,7 +644,8 @@ int configure(nw_ctx* c) {
             c->wide_fill.grid = 0;
             const char* wv = std::getenv("CRISPR_NW_WIDE");
             if (!(wv && std::atoi(wv) == 0) &&
-                level(nw::kWideDiags, c->wide_fill, c->wide_walk, c->wide_stride, c->wide_pairs, kWidePairs)) {
+                level(nw::kWideDiags, c->wide_fill, c->wide_walk, c->wide_stride, c->wide_pairs,
+                      kWidePairs + c->seed_pairs)) {
                 c->wide_words = nw::band_region_words(La, c->lb_max, nw::kWideDiags);
                 c->wide_lb_cap = La + nw::kWideDiags - 1;
                 rbytes = std::max(rbytes, c->wide_pairs * c->wide_stride);
@@ -652,6 +661,10 @@ int configure(nw_ctx* c) {
             HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(c->n)));
             HIP_OR_FAIL(c, c->s->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            if (c->seed_on) {
+                HIP_OR_FAIL(c, c->s->d_seed.reserve((size_t)std::max<int64_t>(c->n, 1)));
+                HIP_OR_FAIL(c, c->s->d_seed_list.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            }
             c->use_diag = true;
         }
     }
@@ -1012,6 +1025,15 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.cls_img = c->cur.cls_img;
         a.cls_words = c->cur.cls_words;
         a.amp_acgt = c->cur.amp_acgt ? 1 : 0;
+        // seeded band: the packed classify marks the reads, the segment sort lists them apart
+        // (sorted by their hits' diagonals), the wide level takes that list after its own
+        c->seed_chunk = c->seed_on && c->pkc.pk_words && c->wide_fill.grid > 0 && c->cur.n_seed > 0;
+        if (c->seed_chunk) {
+            a.seed_info = c->s->d_seed.p;
+            a.seed_keys = c->seed_keys;
+            a.seed_list = c->s->d_seed_list.p;
+            a.seed_count = c->s->d_fallback_count.p + 7;   // zeroed by nw_band_classify
+        }
         a.lb_status = c->s->d_lb.p;
         // packed input (ops_call): classify decodes the chunk (KernelArgs::pk_*)
         a.pk_words = c->pkc.pk_words;
@@ -1185,6 +1207,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
             cnt.handed = c->s->d_fallback_count.p + 5;
         }
         if (c->wide_fill.grid > 0) cnt.exact = c->s->d_fallback_count.p + 6;
+        if (c->seed_chunk) cnt.seeded = c->s->d_fallback_count.p + 7;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
@@ -1691,6 +1714,18 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         std::vector<int64_t> head, tail;
         int64_t left = len;
+        if (const char* e = std::getenv("CRISPR_NW_RAMP")) {   // A/B: "h1,h2,...;t1,t2,..." (tail in call order)
+            std::vector<int64_t>* dst = &head;
+            for (const char* q = e; *q;) {
+                if (*q == ';') { dst = &tail; ++q; continue; }
+                char* end = nullptr;
+                const long long x = std::strtoll(q, &end, 10);
+                if (end == q) { ++q; continue; }
+                if (x > 0 && left > x + chunk) { dst->push_back(x); left -= x; }
+                q = end;
+            }
+            std::reverse(tail.begin(), tail.end());
+        } else
         for (int64_t part : {chunk / 4, chunk / 2}) {   // ramp parts in pairs (one at each end)
             if (part >= 1024 && left > 2 * (part + chunk)) {
                 head.push_back(part);
@@ -1718,6 +1753,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
     const int64_t nchunks = (int64_t)chunks.size();
     auto restore = [&](int code) {
+        c->seed_on = false;
+        c->seed_chunk = false;
+        c->seed_pairs = 0;
         c->split_to = nullptr;
         c->skip16 = false;
         c->diag_off = false;
@@ -1769,6 +1807,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const bool lens_on = pk && pk->lens && upload && n > 0;
     const int64_t ngroups_len = lens_on ? n / nw::kLenGroup + 1 : 0;
     int64_t mx = 1, mn = 0;
+    int64_t n_short = 0;   // reads the 16-diagonal band cannot hold (Lb <= La - 16): the seeded band's
+    const int64_t short_la = ngroups == 1 ? (int64_t)c->ref.size() : 0;
     if (lens_on) {
         // the group bases and chunk 0's lengths in one copy (the device layout is [bases][lengths])
         const int64_t n0 = nchunks > 0 ? chunks[0].hi - chunks[0].lo : 0;
@@ -1826,25 +1866,29 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // the rows from the offsets: a mismatch would make them refer to different bytes)
     if (lens_on) {
         const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 16));
-        std::vector<int64_t> pmx((size_t)parts, 1), pbad((size_t)parts, -1);
+        std::vector<int64_t> pmx((size_t)parts, 1), pbad((size_t)parts, -1), psh((size_t)parts, 0);
         pool.run(parts, [&](int q) {
             int64_t g0, g1;
             nw_host::Pool::range(ngroups_len, parts, q, &g0, &g1);
             unsigned a = 1;
+            int64_t sh = 0;
             for (int64_t g = g0; g < g1 && pbad[(size_t)q] < 0; ++g) {
                 const int64_t r0 = g * nw::kLenGroup, r1 = std::min(n, r0 + nw::kLenGroup);
                 int64_t diff = 0;
                 for (int64_t r = r0; r < r1; ++r) {
                     const unsigned l = pk->lens[r];
                     a = l > a ? l : a;
+                    sh += (int64_t)l + 16 <= short_la;
                     diff |= (int64_t)l ^ (offsets[r + 1] - offsets[r]);
                 }
                 if (diff) pbad[(size_t)q] = g;
             }
             pmx[(size_t)q] = a;
+            psh[(size_t)q] = sh;
         });
         for (int q = 0; q < parts; ++q) {
             mx = std::max(mx, pmx[(size_t)q]);
+            n_short += psh[(size_t)q];
             if (pbad[(size_t)q] >= 0) {
                 (void)hipStreamSynchronize(c->s_in);   // the queued uploads read the caller's arrays
                 return restore(fail(c, NW_E_INVALID, "lens differ from the offsets in reads %lld ..",
@@ -1856,21 +1900,24 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // batches (memory-bound; the exact read is found only on error)
     if (!lens_on) {
         const int parts = (int)std::min<int64_t>(pool.threads(), std::max<int64_t>(1, n >> 15));
-        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0);
+        std::vector<int64_t> pmx((size_t)parts, 1), pmn((size_t)parts, 0), psh((size_t)parts, 0);
         pool.run(parts, [&](int q) {
-            int64_t lo, hi, a = 1, b = 0;
+            int64_t lo, hi, a = 1, b = 0, sh = 0;
             nw_host::Pool::range(n, parts, q, &lo, &hi);
             for (int64_t r = lo; r < hi; ++r) {
                 const int64_t len = offsets[r + 1] - offsets[r];
                 a = len > a ? len : a;
                 b = len < b ? len : b;
+                sh += len + 16 <= short_la;
             }
             pmx[(size_t)q] = a;
             pmn[(size_t)q] = b;
+            psh[(size_t)q] = sh;
         });
         for (int q = 0; q < parts; ++q) {
             mx = std::max(mx, pmx[(size_t)q]);
             mn = std::min(mn, pmn[(size_t)q]);
+            n_short += psh[(size_t)q];
         }
     }
     if (mn < 0 || mx > (1 << 20))
@@ -1883,6 +1930,19 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
     const int32_t lb_max = (int32_t)mx;
+    // the seeded band: a one-amplicon call whose classify decodes a packed batch
+    // (an upload, or the resident batch of one), with reads the 16-diagonal band cannot hold; its
+    // sort keys must fit the segment sort (11 key bits, LDS)
+    {
+        const int La = (int)c->ref.size();
+        const int keys = La / 2 + 2, cap = La + nw::kBandDiags - 1;
+        // (a few such reads -- C2's long deletions -- the 32-diagonal level holds: not worth the keys)
+        c->seed_on = ngroups == 1 && n_short > 0 && 64 * n_short >= n && (pk != nullptr || (!upload && c->resident_packed)) &&
+                     !c->end_weight && La <= 1024 && cap + 3 + keys <= 2048 &&
+                     4 * 17 * (cap + keys + 3) + 128 <= 64 * 1024;   // segsort_lds_bytes (default LDS limit)
+        c->seed_keys = c->seed_on ? keys : 0;
+        c->seed_pairs = c->seed_on ? std::min<int64_t>(chunk, n_short) / 2 + 1 : 0;
+    }
     ht.lap(0);
     c->out_mode = NW_OUT_OPS;
     c->ran = false;

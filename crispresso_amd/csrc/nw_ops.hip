@@ -148,10 +148,11 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         // list to the exact kernel
         const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
         if (direct) fb += *cnt.redo;
-        ctl[4] += fb;
+        const long long ns = cnt.seeded ? (long long)*cnt.seeded : 0ll;   // seeded: DP reads the wide level takes first
+        ctl[4] += fb + ns;
         ctl[10] += cnt.exact ? (long long)*cnt.exact : fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
-        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0);
+        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0) + ns;
         ctl[6] += dp;
         if (cnt.one_level) ctl[7] += dp;
         if (cnt.list_a) ctl[8] += *cnt.list_a;

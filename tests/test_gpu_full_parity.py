@@ -128,11 +128,18 @@ def test_c4_slice_every_read(al):
 
 def test_c1_shape_every_read(al):
     """The reference's own read shape (151 bp reads, 280 bp amplicon: tests/crispresso_tests.py:145-155)
-    at the offsets bench.py's c1_shape leg uses (synth.c1_shape_workload), 200k reads."""
+    at the offsets bench.py's c1_shape leg uses (synth.c1_shape_workload), 200k reads: the window
+    certificates and the seeded band (its reads through the wide level's band centred on their 16-mer
+    hits, certified per read) against the oracle on every read."""
     amp, buf, off = synth.c1_shape_workload(200_000)
     pr, keep = _packed(buf, off)
     outs, out = _pinned_out(len(off) - 1)
     al.set_reference(amp)
     ob = al.align_ops_packed(pr, out=out)
+    counts = al.path_counts()
     _assert_clean(every_read(amp, buf, off, ob, THREADS), "C1 shape")
+    # the seeded band (DESIGN.md 4a) takes most reads no window certificate took: the wide level
+    # certifies them, few reach the exact kernel
+    dp = len(off) - 1 - counts["exact_copies"]
+    assert counts["wide128"] > 0.8 * dp and counts["exact_kernel"] < 0.15 * dp, counts
     _close(keep, outs)
