@@ -246,6 +246,8 @@ __device__ inline long long exc_lower_bound(const KernelArgs& a, long long pos, 
 template <bool PK>
 __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
+    constexpr int kRbw = 66;               // a window read's 16-base words (Lb < La <= 1024) + a zero word
+    __shared__ unsigned s_rbw[4][kRbw];
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
     // here, the first kernel of the chain, instead of by memset launches
@@ -531,18 +533,41 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 win = __ballot(cand_w);
                 // one substitution: every other full-overlap diagonal needs two mismatches, the two
                 // diagonals pairing Lb - 1 residues one (the whole wave on each such read)
+#ifdef NW_NO_SUB1WIN
+                if (true) win &= ~__ballot(cand_w && win_k == 1);
+                else
+#endif
+                // (the read's 16-base words go to LDS once per candidate: the offsets' compares read them
+                // there, with no global round trip per offset)
+                unsigned* rbw = s_rbw[threadIdx.x >> 6];
                 for (unsigned long long need = __ballot(cand_w && win_k == 1); need; need &= need - 1) {
                     const int u = (int)__builtin_ctzll(need);
                     const int s1 = __builtin_amdgcn_readlane(win_s, u), Lb = __builtin_amdgcn_readlane(my_len, u);
                     const unsigned lo32 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
                     const unsigned hi32 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
                     const long long ro = (long long)(((unsigned long long)hi32 << 32) | lo32);
+                    const int nwd = (Lb + 15) / 16 + 1;   // <= kRbw
+                    for (int k = lane; k < nwd; k += 64) rbw[k] = 16 * k < Lb ? rword(ro + 16 * k) : 0u;
+                    lds_fence();
+                    // mismatches of read bases [j0, j0 + len) against amplicon [s, s + len), up to cap + 1
+                    auto mism_l = [&](int j0, int s, int len, int cap) -> int {
+                        int cnt = 0;
+                        for (int w = 0; w < len && cnt <= cap; w += 16) {
+                            const int p = j0 + w;
+                            unsigned y = __builtin_amdgcn_alignbit(rbw[(p >> 4) + 1], rbw[p >> 4], (unsigned)(2 * (p & 15))) ^
+                                         aword(s + w);
+                            if (len - w < 16) y &= (1u << (2 * (len - w))) - 1u;
+                            cnt += __builtin_popcount((y | (y >> 1)) & 0x55555555u);
+                        }
+                        return cnt;
+                    };
                     bool bad = false;
                     for (int s2 = lane; s2 <= La - Lb; s2 += 64)
-                        if (s2 != s1) bad = bad || mism(ro, 0, s2, Lb, 1) < 2;
-                    if (lane == 0) bad = bad || mism(ro, 1, 0, Lb - 1, 0) < 1;            // d = +1
-                    if (lane == 1) bad = bad || mism(ro, 0, La - Lb + 1, Lb - 1, 0) < 1;   // d = Lb - La - 1
+                        if (s2 != s1) bad = bad || mism_l(0, s2, Lb, 1) < 2;
+                    if (lane == 0) bad = bad || mism_l(1, 0, Lb - 1, 0) < 1;            // d = +1
+                    if (lane == 1) bad = bad || mism_l(0, La - Lb + 1, Lb - 1, 0) < 1;   // d = Lb - La - 1
                     if (__ballot(bad)) win &= ~(1ull << u);
+                    lds_fence();   // every lane's reads of rbw before the next candidate's writes
                 }
             }
         }
@@ -553,20 +578,31 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // with more than 8 hits (a repeat) leaves the read to the exact kernel.
         int32_t sinfo = 0;
         if constexpr (PK) {
+#ifdef NW_NO_SEED
+            if (false) {
+#else
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
                 !(((exact | sub1 | sub2 | win) >> lane) & 1ull)) {
+#endif
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
-                for (int b = 0; b < nb && ok; ++b) {
-                    const unsigned key = rword(my_off + 16 * b);
-                    int f;
-                    const int l = seed_range(key, &f);
-                    if (f > 0 && skey[f - 1] == key) ok = false;   // more occurrences than seed_range returns
-                    for (int i = f; ok && i < l; ++i) {
-                        const int d = 16 * b - (int)spos[i];
-                        dmin = min(dmin, d);
-                        dmax = max(dmax, d);
+                for (int b0 = 0; b0 < nb && ok; b0 += 8) {   // eight blocks' words in flight together
+                    unsigned keys[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) keys[t] = b0 + t < nb ? rword(my_off + 16 * (b0 + t)) : 0u;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int b = b0 + t;
+                        if (b >= nb || !ok) continue;
+                        int f;
+                        const int l = seed_range(keys[t], &f);
+                        if (f > 0 && skey[f - 1] == keys[t]) ok = false;   // more occurrences than seed_range returns
+                        for (int i = f; ok && i < l; ++i) {
+                            const int d = 16 * b - (int)spos[i];
+                            dmin = min(dmin, d);
+                            dmax = max(dmax, d);
+                        }
                     }
                 }
                 if (ok && dmax >= dmin && dmax - dmin <= kWideDiags / 2 && nb < 128)

@@ -1714,18 +1714,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         std::vector<int64_t> head, tail;
         int64_t left = len;
-        if (const char* e = std::getenv("CRISPR_NW_RAMP")) {   // A/B: "h1,h2,...;t1,t2,..." (tail in call order)
-            std::vector<int64_t>* dst = &head;
-            for (const char* q = e; *q;) {
-                if (*q == ';') { dst = &tail; ++q; continue; }
-                char* end = nullptr;
-                const long long x = std::strtoll(q, &end, 10);
-                if (end == q) { ++q; continue; }
-                if (x > 0 && left > x + chunk) { dst->push_back(x); left -= x; }
-                q = end;
-            }
-            std::reverse(tail.begin(), tail.end());
-        } else
         for (int64_t part : {chunk / 4, chunk / 2}) {   // ramp parts in pairs (one at each end)
             if (part >= 1024 && left > 2 * (part + chunk)) {
                 head.push_back(part);

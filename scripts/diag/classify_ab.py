@@ -1,6 +1,6 @@
 """Kernel-resident pass of the C2 batch: text upload (byte classify) vs packed upload (packed
 classify), alternating; prints the phase times (classify + sort, fills, walk, rest).
-Usage: classify_ab.py [rounds]"""
+Usage: classify_ab.py [rounds] [c1]"""
 import os
 import sys
 
@@ -12,8 +12,11 @@ from crispresso_amd import synth  # noqa: E402
 from crispresso_amd.aligner import GpuAligner, pack_2bit  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-amp = synth.random_amplicon(bench.AMPLICON_LEN, 1)
-buf, off = synth.reads_from(amp, bench.READS_PER_GPU, 2)
+if len(sys.argv) > 2 and sys.argv[2] == "c1":   # the C1-shape leg's reads (151 bp windows of 280 bp)
+    amp, buf, off = synth.c1_shape_workload(1_000_000)
+else:
+    amp = synth.random_amplicon(bench.AMPLICON_LEN, 1)
+    buf, off = synth.reads_from(amp, bench.READS_PER_GPU, 2)
 pr = pack_2bit(buf, off)
 al = GpuAligner(0)
 al.set_reference(amp)
