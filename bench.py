@@ -869,7 +869,11 @@ def main():
     n_runs = int(ob.ops_off[n])
     call_counts = al.path_counts()
 
-    if args.skip_kernel_pass:
+    if args.skip_kernel_pass:   # tracing / call A/B: the timed calls only
+        if rank == 0:
+            print(json.dumps({"metric": "aligned reads/s (timed calls only, --skip-kernel-pass)",
+                              "value": n * world * args.steps / elapsed, "ms_per_step": elapsed / args.steps * 1e3,
+                              "n_gpus": world, "pcie": pcie, "path_counts": call_counts}), flush=True)
         al.close()
         return
     # the timed call's own outputs against the oracle (before anything reuses the buffers)
