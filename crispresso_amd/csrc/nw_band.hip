@@ -364,6 +364,89 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // away from the words already in registers
         const bool one_chunk = nd <= 64;
         unsigned long long emit_later = 0ull;
+#ifndef NW_WAVE_CMP
+        if constexpr (PK) {
+            // Packed input, ops output, an A C G T amplicon of at most 256 bp: one read per lane.  Its
+            // 2-bit words (one shift of the stream's dwords) against the amplicon's give the
+            // mismatches of the main diagonal; a read with one or two takes the certificates above
+            // from the shifted diagonals' masks (the wave-per-candidate loop below decides the same
+            // from byte compares).  Mismatch masks: one bit per base (bit 2 i of word t: base 16 t + i).
+            if (a.ops && one_chunk && amp_acgt_all && a.amp2 && cand) {
+                const bool c = ((cand >> lane) & 1ull) != 0ull;
+                cand = 0ull;
+                const int nw = (La + 15) >> 4;   // <= 16
+                auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
+                    const int b = len - 16 * t;
+                    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
+                };
+                unsigned rw[17];
+                {
+                    const long long q0 = my_off - a.pk_pos0;
+                    const unsigned* src = a.pk_words + (q0 >> 4);
+                    const unsigned s2 = (unsigned)(2 * (q0 & 15));
+                    unsigned wd[17];
+#pragma unroll
+                    for (int t = 0; t < 17; ++t) wd[t] = c && t <= nw ? src[t] : 0u;   // <= the read's last dword + 1
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
+                    rw[16] = 0u;   // bases past the read: masked below
+                }
+                int k = 0, f = -1, l = -1;   // mismatches of the main diagonal, first and last base
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    if (t >= nw) continue;
+                    const unsigned x = rw[t] ^ amp2s[t];
+                    const unsigned m = (x | (x >> 1)) & vmask(t, La);
+                    k += __builtin_popcount(m);
+                    if (m != 0u && f < 0) f = 16 * t + (__builtin_ctz(m) >> 1);
+                    if (m != 0u) l = 16 * t + ((31 - __builtin_clz(m)) >> 1);
+                }
+                exact = __ballot(c && k == 0);
+                const bool s1 = c && sub1_ok && k == 1, s2 = c && sub2_ok && k == 2;
+                // diagonal d = sgn * sh (q <= La - 1 - sh): mismatches (counted up to 2), any at q >= qa, any at q <= qb
+                auto shifted = [&](int sgn, int sh, int qa, int qb, int* tot, bool* ge, bool* le) {
+                    int n = 0;
+                    unsigned g = 0u, e = 0u;
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) {
+                        if (t >= nw) continue;
+                        const unsigned am = sgn > 0 ? amp2s[t]
+                                                    : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
+                        const unsigned rd = sgn > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
+                        const unsigned x = rd ^ am;
+                        const unsigned m = (x | (x >> 1)) & vmask(t, La - sh);
+                        n += __builtin_popcount(m);
+                        g |= m & ~vmask(t, qa);      // bases >= qa
+                        e |= m & vmask(t, qb + 1);   // bases <= qb
+                    }
+                    *tot = n;
+                    *ge = g != 0u;
+                    *le = e != 0u;
+                };
+                if (__ballot(s1 || s2)) {
+                    // S_+-1 below D: one mismatch on each (k = 1); two substitutions at bases f < l: two on
+                    // each, d = +1 one at q >= f and one at q <= l - 2, d = -1 at q >= f + 1 and q <= l - 1
+                    int tp, tm;
+                    bool gp, lp, gm, lm;
+                    shifted(1, 1, f, l - 2, &tp, &gp, &lp);
+                    shifted(-1, 1, f + 1, l - 1, &tm, &gm, &lm);
+                    sub1 = __ballot(s1 && tp >= 1 && tm >= 1);
+                    bool ok2 = s2 && tp >= 2 && tm >= 2 && gp && lp && gm && lm;
+                    if (__ballot(ok2)) {   // d = +-2, +-3: one mismatch each
+#pragma unroll
+                        for (int sh = 2; sh <= 3; ++sh) {
+                            int t2, t3;
+                            bool x0, x1;
+                            shifted(1, sh, 0, La, &t2, &x0, &x1);
+                            shifted(-1, sh, 0, La, &t3, &x0, &x1);
+                            ok2 = ok2 && t2 >= 1 && t3 >= 1;
+                        }
+                    }
+                    sub2 = __ballot(ok2);
+                }
+            }
+        }
+#endif
         while (cand) {
             int us[kCand];
             unsigned diff[kCand], raw[kCand];
@@ -1807,14 +1890,366 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
     return true;
 }
 
+// The first level's walk, one read per lane (ops output): 64 consecutive list positions per
+// wavefront, each lane its own read's header, start cell, certificate and traceback
+// (band_walk_runs2's rules cell for cell, the state machine in VGPRs: the wave-per-read walk
+// spends ~430 scalar instructions per read on it), its record from the runs and the score
+// (plain reads), its runs into its slot.  What a lane cannot finish -- the refined certificate
+// (sums over the band's neighbour diagonals), reads with codes outside A C G T, more than
+// kLaneRuns runs -- goes to `defer(k)`, the wave-per-read body, one read at a time.
+constexpr int kLaneRuns = 8;   // runs per lane in LDS ([kLaneRuns][64] dwords at the wave's area)
+#ifndef NW_LANE_MROWS
+#define NW_LANE_MROWS 2
+#endif
+constexpr int kMRows = NW_LANE_MROWS;   // tile rows per M round of the lane walk (<= 4: 32 cells)
+// The lane walk's wavefront waits for its slowest lane (~20 dependent rounds of tile loads for a
+// read with an indel): it pays on one long list (the kernel-resident pass: walk<16> 0.189 -> 0.165
+// ms) and not in a pipelined call, whose chunks' chains then ran longer (calls 1.94-1.97 vs
+// 1.92-1.93 ms with it on chunks of 196k reads and more) -- launches of fewer than kLaneWalkReads
+// reads (every chunk of a call: at most 262144) keep the wave-per-read walk at 6 wavefronts per SIMD.
+#ifndef NW_LANE_READS
+#define NW_LANE_READS 300000
+#endif
+constexpr long long kLaneWalkReads = NW_LANE_READS;
+template <int W, class Defer>
+__device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, unsigned char* wb,
+                           const unsigned char* amp_lds, bool amp_acgt, int sc5, const Defer& defer) {
+    constexpr int kCapBytes = BandGeo<W>::CapBytes;
+    const int La = a.La, E = a.gap_extend, O = a.gap_open, m = a.band_maxsub, NW = a.band_words;
+    const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
+    const int rcap = band_walk_rcap(a.Lb_max);
+    unsigned* lruns = (unsigned*)wb;   // [kLaneRuns][64]: lane's run q at lruns[64 q + lane]
+    const long long ng = (khi - klo + 63) >> 6;
+    for (long long g = (long long)blockIdx.x * wpb + wave; g < ng; g += (long long)gridDim.x * wpb) {
+        const long long k = klo + 64 * g + lane;
+        const bool live = k < khi;
+        // 0: done, 1: the wave path, 2: redo list (retry), 3: fallback list
+        int fate = 0;
+        long long rd = 0;
+        if (live) {
+            const unsigned char* region = a.band_region + ((k >> 1) - a.band_pair_lo) * a.band_stride;
+            const int4 hdr = *(const int4*)region, hr = *(const int4*)(region + 16), ho = *(const int4*)(region + 32);
+            const int h = (int)(k & 1);
+            rd = h ? hr.y : hr.x;
+            const int Lb = h ? hr.w : hr.z;
+            if (a.redo_flags) a.redo_flags[k] = 0;
+            if (Lb <= 0) {
+                Stat z = {};
+                z.flags = FLAG_EMPTY;
+                a.stats[rd] = z;
+                a.nops[rd] = 0;
+            } else if (hdr.z & kPairInactive) {
+                fate = 2;
+            } else if (Lb > rcap) {
+                fate = 3;
+            } else {
+                const int dlo = hdr.y, tau0 = hdr.x;
+                // start cell: the largest end key over the band's diagonals (their last cells)
+                const uint4* capw = (const uint4*)(region + kHdrBytes);
+                unsigned k32 = 0u;
+#pragma unroll
+                for (int c4 = 0; c4 < W / 4; ++c4) {
+                    const uint4 q4 = capw[c4];
+                    const unsigned cv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int d = dlo + 4 * c4 + e;
+                        const int iend = La < Lb - d ? La : Lb - d;
+                        const int ilo = 1 - d > 1 ? 1 - d : 1;
+                        if (iend >= ilo) {
+                            const int v = half(cv[e], h) - kBias16 - E * (2 * iend + d);
+                            const int jend = iend + d;
+                            const unsigned kk = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
+                                                : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
+                            k32 = kk > k32 ? kk : k32;
+                        }
+                    }
+                }
+                int score, ei, ej;
+                decode_end(end_key_widen(k32), La, Lb, &score, &ei, &ej);
+                const int dhi = dlo + W - 1;
+                int pmax = -1;
+                if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
+                if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
+                const bool certified = pmax < 0 || score > m * pmax;
+                const bool bad_code = (hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) != 0;
+                const bool plain = amp_acgt && !(hdr.z & (h ? (REGION_BAD_B | REGION_NP_B) : (REGION_BAD_A | REGION_NP_A)));
+                const int nd = min(ei, ej);
+                const long long off = h ? (long long)(((unsigned long long)(unsigned)ho.w << 32) | (unsigned)ho.z)
+                                        : (long long)(((unsigned long long)(unsigned)ho.y << 32) | (unsigned)ho.x);
+                // mismatches of amplicon bytes [ia, ia + n) against read bytes [jb, jb + n) (plain: A C G T,
+                // case folded), dword compares
+                auto count_mis = [&](int ia, int jb, int n) -> int {
+                    int c = 0;
+                    const unsigned char* rp = a.reads + off + jb;
+                    const int ra = (int)((uintptr_t)rp & 3), aa = ia & 3;
+                    const unsigned* rw = (const unsigned*)(rp - ra);
+                    const unsigned* aw = (const unsigned*)(amp_lds + (ia - aa));
+                    unsigned rlo = rw[0], alo = aw[0];
+#pragma unroll 4
+                    for (int t = 0; t < n; t += 4) {
+                        const unsigned rhi = rw[(t >> 2) + 1], ahi = aw[(t >> 2) + 1];
+                        unsigned x = (__builtin_amdgcn_alignbyte(rhi, rlo, ra) ^ __builtin_amdgcn_alignbyte(ahi, alo, aa)) &
+                                     0xdfdfdfdfu;
+                        if (n - t < 4) x &= 0xffffffffu >> (8 * (4 - (n - t)));
+                        c += 4 - __builtin_popcount(zero_bytes(x));
+                        rlo = rhi;
+                        alo = ahi;
+                    }
+                    return c;
+                };
+                bool cert = certified;
+                if (!certified && !bad_code && score > m * pmax - O) {
+                    // the refined certificate (band_single_diagonals_below): every single diagonal beyond the
+                    // band whose overlap could reach the score sums below it -- a plain read's diagonal d
+                    // sums to m P - 9 sc5 mis_d; other reads: the wave path
+                    if (!plain) {
+                        fate = 1;
+                    } else {
+                        cert = true;
+                        for (int side = 0; side < 2 && cert; ++side) {
+                            for (int kq = 1;; ++kq) {
+                                const int d = side == 0 ? dhi + kq : dlo - kq;
+                                const int P = diag_pairs(La, Lb, d);
+                                if (P <= 0 || m * P < score) break;
+                                const int i0 = d >= 0 ? 0 : -d, j0 = d >= 0 ? d : 0;
+                                if (m * P - 9 * sc5 * count_mis(i0, j0, P) >= score) {
+                                    cert = false;
+                                    break;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (fate != 0) {
+                } else if (bad_code || !cert) {
+                    fate = bad_code ? 3 : 2;
+                } else if (!plain || nd >= 1024) {
+                    fate = 1;
+                } else {
+                    // (no single-diagonal fast path here: when the start cell's diagonal sums to the score the
+                    // walk's M rounds follow that diagonal to the edge -- M wins every tie on it -- and the record
+                    // from the runs equals the diagonal's; a compare of every pair would cost as many rounds)
+                    int nr = 0, tm = 0, tg = 0, tp = 0, last = -1;
+                    bool over = false;
+                    auto push = [&](int type, int n, bool paid) {
+                        if (n <= 0) return;
+                        if (type == RUN_M) tm += n; else tg += n;
+                        if (paid) tp += (type == last ? 0 : O - E) + n * E;
+                        if (type == last) {
+                            lruns[64 * (nr - 1) + lane] += (unsigned)n;
+                        } else if (nr < kLaneRuns) {
+                            lruns[64 * nr + lane] = ((unsigned)type << 28) | (unsigned)n;
+                            ++nr;
+                            last = type;
+                        } else {
+                            over = true;
+                        }
+                    };
+                    if (ei == La && ej < Lb) push(RUN_X, Lb - ej, false);
+                    else if (ej == Lb && ei < La) push(RUN_Y, La - ei, false);
+                    Stat r;
+                    r.score = score;
+                    r.end_i = ei;
+                    r.end_j = ej;
+                    r.flags = 0;
+                    {
+                        // band_walk_runs2, one lane: M runs scan kMRows tile rows (8 cells of their diagonal
+                        // each) per round, X / Y runs 8 cells per round; the same stop rules
+                        const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
+                        const int tb0 = kBK - dlo + 2 - tau0, hb = 8 * h;
+                        int i = ei, j = ej, state = RUN_M, kc = 0;   // kc: cells of the current run so far
+                        bool fail = false;
+                        for (int guard = 0; i > 0 && j > 0 && !over && !fail; ++guard) {
+                            if (guard > 4 * (La + Lb + 64)) {
+                                fate = 1;
+                                break;
+                            }
+                            if (state == RUN_M) {
+                                const int kd = j - i - dlo;
+                                if ((unsigned)kd >= (unsigned)W) {
+                                    fail = true;
+                                    break;
+                                }
+                                const int lim = min(i, j) - 1;
+                                const int tc = i + j - 4 + tb0 - 2 * kc;   // tau of the next cell to test
+                                // kMRows tile rows per round (8 cells of the diagonal each), their loads together
+                                const int r0 = tc >> 4, NR = NW >> 2;
+                                uint4 v[kMRows];
+#pragma unroll
+                                for (int q = 0; q < kMRows; ++q)
+                                    v[q] = r0 - q >= 0 && r0 - q < NR ? *(const uint4*)(bits + (r0 - q) * (2 * W) + 4 * (kd >> 1))
+                                                                      : make_uint4(0u, 0u, 0u, 0u);
+                                // the rows' cells of this diagonal in decreasing tau, from the "M < max" bits of its
+                                // parity (s = p: bit sh, s = p + 2: bit sh + 2 of each word)
+                                const int p = tc & 1;
+                                const unsigned sh = 20 + hb + p;
+                                unsigned long long all = 0ull, oddr = 0ull;
+#pragma unroll
+                                for (int q = 0; q < kMRows; ++q) {
+                                    const unsigned w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+                                    unsigned mm = 0u;
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e) {
+                                        const unsigned t = w[e] >> sh;
+                                        mm |= (((t >> 2) & 1u) | ((t & 1u) << 1)) << (2 * (3 - e));
+                                    }
+                                    all |= (unsigned long long)mm << (8 * q);
+                                    // a cell of the matrix outside the stored steps: the wave path's clamps decide
+                                    if (r0 - q < 0 || r0 - q >= NR) oddr |= 0xffull << (8 * q);
+                                }
+                                constexpr int kCells = 8 * kMRows;
+                                const int c0 = (16 * r0 + 14 + p - tc) >> 1;   // cell tc's place in row r0 (0 .. 7)
+                                const int ncell = kCells - c0;
+                                const unsigned cells = (unsigned)((1ull << ncell) - 1ull);
+                                const unsigned nm = (unsigned)(all >> c0) & cells;
+                                const int L = lim - kc;   // cells u < L are inside the matrix
+                                const unsigned inm = L <= 0 ? 0u : (L >= ncell ? cells : (1u << L) - 1u);
+                                const unsigned stop = nm | (cells & ~inm);
+                                const unsigned odd = (unsigned)(oddr >> c0) & inm;
+                                const unsigned upto = stop ? (unsigned)((2ull << __builtin_ctz(stop)) - 1ull) : 0xffffffffu;
+                                if (odd & upto) {
+                                    fate = 1;
+                                    break;
+                                }
+                                if (stop) {
+                                    const int u0 = __builtin_ctz(stop);
+                                    const int run = kc + u0 + 1;
+                                    push(RUN_M, run, false);
+                                    i -= run;
+                                    j -= run;
+                                    const int ts = tc - 2 * u0;   // the stop cell: "X > Y" picks the gap it continues in
+                                    uint4 vs = v[0];
+#pragma unroll
+                                    for (int q = 1; q < kMRows; ++q) vs = (ts >> 4) == r0 - q ? v[q] : vs;
+                                    const int qs = (ts >> 2) & 3;
+                                    const unsigned ws = qs == 0 ? vs.x : (qs == 1 ? vs.y : (qs == 2 ? vs.z : vs.w));
+                                    state = ((ws >> (4 + hb + (ts & 3))) & 1u) ? RUN_X : RUN_Y;
+                                    kc = 0;
+                                } else {
+                                    kc += ncell;
+                                }
+                            } else {
+                                const bool isX = state == RUN_X;
+                                const int lim = isX ? j : i;
+                                const int kd0 = j - i - dlo;
+                                const int t0 = i + j - 2 + tb0;
+                                const int bit = isX ? 16 : 0;
+                                unsigned stop = 0u, oob = 0u;
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) {
+                                    const int kk = kc + u;
+                                    const int kd = isX ? kd0 - kk : kd0 + kk;
+                                    const int tau = t0 - kk;
+                                    const bool out = (unsigned)kd >= (unsigned)W;
+                                    const int wd = min(max(tau, 0) >> 2, NW - 1);
+                                    const bool valid = kk < lim;
+                                    const unsigned w = (valid && !out)
+                                                           ? bits[(wd >> 2) * (2 * W) + 4 * ((kd & (W - 1)) >> 1) + (wd & 3)]
+                                                           : 0u;
+                                    const bool opens = ((w >> (bit + hb + (tau & 3))) & 1u) != 0u;
+                                    stop |= (unsigned)(!valid || out || opens) << u;
+                                    oob |= (unsigned)(valid && out) << u;
+                                }
+                                if (stop) {
+                                    const int u0 = __builtin_ctz(stop);
+                                    if ((oob >> u0) & 1u) {
+                                        fail = true;
+                                        break;
+                                    }
+                                    const int run = kc + u0 + 1;
+                                    push(state, run, true);
+                                    if (isX) j -= run; else i -= run;
+                                    state = RUN_M;
+                                    kc = 0;
+                                } else {
+                                    kc += 8;
+                                }
+                            }
+                        }
+                        if (fate == 0) {
+                            if (fail) {
+                                fate = 2;
+                            } else {
+                                if (i > 0) push(RUN_Y, i, false);
+                                if (j > 0) push(RUN_X, j, false);
+                                // a plain read's record from its runs and score: m id - x (M - id) - paid gaps
+                                const int idn = score + tp + 4 * sc5 * tm;
+                                if (over || idn < 0 || idn % (9 * sc5) != 0) {
+                                    fate = 1;
+                                } else {
+                                    r.aln_len = tm + tg;
+                                    r.n_ident = idn / (9 * sc5);
+                                    r.n_sim = r.n_ident;
+                                    r.n_gaps = tg;
+                                }
+                            }
+                        }
+                    }
+                    if (fate == 0 && over) fate = 1;
+                    if (fate == 0) {
+                        // store_ops for one lane: its runs start -> end into its slot (or the spill area)
+                        uint32_t* dst = a.ops + a.ops_stride * a.ops_slot + rd * a.ops_slot;
+                        int32_t flag = kNopsRows;
+                        bool lost = false;
+                        if (nr > a.ops_slot) {
+                            flag = 0;
+                            const int pos = atomicAdd(a.ops_ctl, nr);
+                            if ((long long)pos + nr > a.spill_cap) {
+                                atomicOr(a.ops_ctl + 1, 1);
+                                a.nops[rd] = 0;
+                                lost = true;
+                            } else {
+                                a.ops[rd] = (uint32_t)pos;
+                                dst = a.spill + pos;
+                            }
+                        }
+                        if (!lost) {
+                            a.nops[rd] = nr | flag;
+                            for (int q = 0; q < nr; ++q) dst[q] = lruns[64 * (nr - 1 - q) + lane];
+                        }
+                        a.stats[rd] = r;
+                    }
+                }
+            }
+        }
+        // the lists: one atomic per list and wavefront (redo flags instead when the level keeps them)
+        const unsigned long long to_redo = __ballot(fate == 2 && !a.redo_flags), to_fb = __ballot(fate == 3);
+        if (fate == 2 && a.redo_flags) a.redo_flags[k] = 1;
+        if (to_redo) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(a.redo_count, (int)__builtin_popcountll(to_redo));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if ((to_redo >> lane) & 1ull) a.redo_list[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(to_redo >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)to_redo, 0u))] = (int)rd;
+        }
+        if (to_fb) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(a.fallback_count, (int)__builtin_popcountll(to_fb));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if ((to_fb >> lane) & 1ull) a.fallback_list[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(to_fb >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)to_fb, 0u))] = rd;
+        }
+        // the wave path for the rest, one read at a time (its LDS buffers overlay lruns: read above)
+        lds_fence();
+        for (unsigned long long dq = __ballot(fate == 1); dq; dq &= dq - 1) {
+            const int u = (int)__builtin_ctzll(dq);
+            const long long ku = klo + 64 * g + u;
+            defer(ku);
+            lds_fence();
+        }
+    }
+}
+
 // W < kBandDiags: a first level; reads it cannot certify go to the redo list of the
 // next (wider) level.  W >= kBandDiags: they go to the fallback list (W = kBandDiags: the
 // wide level's input; the wide level: the exact int32 kernel's).
-template <int W>
+template <int W, bool LN = false>   // LN: the lane walk (walk_lanes) first, W < kBandDiags, ops output
 #ifndef NW_WALK_WPE
 #define NW_WALK_WPE 6
 #endif
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
+#ifndef NW_WALK_LANE_WPE
+#define NW_WALK_LANE_WPE 5   // the first level's lane walk holds ~100 VGPRs
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WALK_LANE_WPE : NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1926,41 +2361,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(raw - ms + m + 4 * lane),
                                              (__attribute__((address_space(3))) void*)(dst + m), 4, 0, 0);
     };
-    long long k = klo + (long long)blockIdx.x * wpb + wave;
-    int it = 0;   // parity of the slots holding read k's header and bytes
-    if (k < khi) {   // the pipeline's start: read k's header, then its bytes and the next header
-        load_hdr(k, hbufs);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int Lb0;
-        long long off0;
-        read_of(hbufs, k, &Lb0, &off0);
-        if (Lb0 > 0 && Lb0 <= rcap) load_bytes(off0, Lb0, rbufs);
-        if (k + kstep < khi) load_hdr(k + kstep, hbufs + kSlot);
-    }
-    for (; k < khi; k += kstep, it ^= 1) {
-        const unsigned* hb = hbufs + it * kSlot;   // landed: the previous read's wait
-        unsigned char* rbuf = rbufs + it * (rcap + 256);
-        const int4 hdr = uni(*(const int4*)hb), hr = uni(*(const int4*)(hb + 4));
-        unsigned cw[CW];
-#pragma unroll
-        for (int c = 0; c < CW; ++c) cw[c] = lane + 64 * c < W ? hb[kHdrBytes / 4 + lane + 64 * c] : 0u;
-        const int h = (int)(k & 1);
-        const long long rd = h ? hr.y : hr.x;
-        int Lb;
-        long long off;
-        read_of(hb, k, &Lb, &off);
-        // every load issued for this read has landed (its bytes, the next read's header), and the
-        // header reads above are done (lgkmcnt); the next read's bytes and the header after it go
-        // out now, into the slots the previous read used and this read's header slot
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (k + kstep < khi) {
-            unsigned* hn = hbufs + (it ^ 1) * kSlot;
-            int Lbn;
-            long long offn;
-            read_of(hn, k + kstep, &Lbn, &offn);
-            if (Lbn > 0 && Lbn <= rcap) load_bytes(offn, Lbn, rbufs + (it ^ 1) * (rcap + 256));
-            if (k + 2 * kstep < khi) load_hdr(k + 2 * kstep, hbufs + it * kSlot);   // this read's header is in registers
-        }
+    // read k once its header (hb: pair header + captures) and bytes (rbuf) are in LDS and have landed
+    auto process = [&](long long k, const int4 hdr, const int4 hr, const unsigned* cw, int h, long long rd, int Lb,
+                       long long off, unsigned char* rbuf) {
         if (W < kBandDiags && a.redo_flags && lane == 0) a.redo_flags[k] = 0;   // give_up may set it
         if (Lb <= 0) {
             if (lane == 0) {
@@ -1969,17 +2372,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
                 a.stats[rd] = z;
                 if (a.ops) a.nops[rd] = 0;
             }
-            continue;
+            return;
         }
         if (hdr.z & kPairInactive) {   // too long, or the pair's lengths do not fit the band
             give_up(k, rd, true);
-            continue;
+            return;
         }
         const int dlo = hdr.y;
         const unsigned char* region = region_of(k);
         if (Lb > rcap) {   // not reached: rcap covers the band length cap
             give_up(k, rd, false);
-            continue;
+            return;
         }
         const int mis = (int)((uintptr_t)(a.reads + off) & 3);
         const int tau0 = hdr.x;
@@ -2038,7 +2441,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
         }
         if (bad_code || !certified) {
             give_up(k, rd, !bad_code);   // IUPAC codes: no band helps
-            continue;
+            return;
         }
         // Single-diagonal fast path: when the start cell's score equals the plain sum of
         // substitution scores down its diagonal to the matrix edge, D(ei, ej), the
@@ -2095,7 +2498,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
                     a.stats[rd] = r;
                 }
                 lds_fence();
-                continue;
+                return;
             }
         } else {
             const unsigned* bits = (const unsigned*)(region + kHdrBytes + kCapBytes);
@@ -2122,12 +2525,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
                     a.stats[rd] = r;
                 }
                 lds_fence();
-                continue;
+                return;
             }
         }
         if (nruns < 0) {
             give_up(k, rd, true);
-            continue;
+            return;
         }
         lds_fence();
         auto sim = [&](int ai, int code) { return (int)((rowpos[ai] >> code) & 1u); };
@@ -2140,6 +2543,70 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_WALK_WPE
                             score, ei, ej, a.stats + rd, lane);
         }
         lds_fence();
+    };
+#ifndef NW_WALK_WAVE
+    if constexpr (LN && W < kBandDiags) {
+        if (a.ops) {
+            walk_lanes<W>(a, klo, khi, wb, amp_lds, amp_acgt, sc5, [&](long long kq) {
+                // a read the lane walk leaves to the wave path: its header, captures and bytes into
+                // LDS, then the per-read body
+                load_hdr(kq, hbufs);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int4 hdr = uni(*(const int4*)hbufs), hr = uni(*(const int4*)(hbufs + 4));
+                unsigned cw[CW];
+#pragma unroll
+                for (int c = 0; c < CW; ++c) cw[c] = lane + 64 * c < W ? hbufs[kHdrBytes / 4 + lane + 64 * c] : 0u;
+                const int h = (int)(kq & 1);
+                const long long rd = h ? hr.y : hr.x;
+                int Lb;
+                long long off;
+                read_of(hbufs, kq, &Lb, &off);
+                if (Lb > 0 && Lb <= rcap) load_bytes(off, Lb, rbufs);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                process(kq, hdr, hr, cw, h, rd, Lb, off, rbufs);
+            });
+            if (redo_n) flush_redo();
+            if (fb_n) flush_fb();
+            return;
+        }
+    }
+#endif
+    long long k = klo + (long long)blockIdx.x * wpb + wave;
+    int it = 0;   // parity of the slots holding read k's header and bytes
+    if (k < khi) {   // the pipeline's start: read k's header, then its bytes and the next header
+        load_hdr(k, hbufs);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int Lb0;
+        long long off0;
+        read_of(hbufs, k, &Lb0, &off0);
+        if (Lb0 > 0 && Lb0 <= rcap) load_bytes(off0, Lb0, rbufs);
+        if (k + kstep < khi) load_hdr(k + kstep, hbufs + kSlot);
+    }
+    for (; k < khi; k += kstep, it ^= 1) {
+        const unsigned* hb = hbufs + it * kSlot;   // landed: the previous read's wait
+        unsigned char* rbuf = rbufs + it * (rcap + 256);
+        const int4 hdr = uni(*(const int4*)hb), hr = uni(*(const int4*)(hb + 4));
+        unsigned cw[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) cw[c] = lane + 64 * c < W ? hb[kHdrBytes / 4 + lane + 64 * c] : 0u;
+        const int h = (int)(k & 1);
+        const long long rd = h ? hr.y : hr.x;
+        int Lb;
+        long long off;
+        read_of(hb, k, &Lb, &off);
+        // every load issued for this read has landed (its bytes, the next read's header), and the
+        // header reads above are done (lgkmcnt); the next read's bytes and the header after it go
+        // out now, into the slots the previous read used and this read's header slot
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (k + kstep < khi) {
+            unsigned* hn = hbufs + (it ^ 1) * kSlot;
+            int Lbn;
+            long long offn;
+            read_of(hn, k + kstep, &Lbn, &offn);
+            if (Lbn > 0 && Lbn <= rcap) load_bytes(offn, Lbn, rbufs + (it ^ 1) * (rcap + 256));
+            if (k + 2 * kstep < khi) load_hdr(k + 2 * kstep, hbufs + it * kSlot);   // this read's header is in registers
+        }
+        process(k, hdr, hr, cw, h, rd, Lb, off, rbuf);
     }
     if constexpr (W > kBandDiags) {
         // the wide level's list entries past its region's capacity: straight to the exact kernel
@@ -2281,7 +2748,9 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
-    if (W == 16)
+    if (W == 16 && a.ops && a.n >= kLaneWalkReads)
+        hipLaunchKernelGGL((nw_band_walk<16, true>), dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    else if (W == 16)
         hipLaunchKernelGGL(nw_band_walk<16>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     else if (W == 32)
         hipLaunchKernelGGL(nw_band_walk<32>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);

@@ -23,7 +23,7 @@ def test_pmc_summaries_exist_and_newest_first():
     with open(newest_summary(b)) as f:
         summ = json.load(f)
     assert any("nw_band_fill<16" in k for k in summ)
-    assert any("nw_band_walk<16>" in k for k in summ)
+    assert any("nw_band_walk<16" in k for k in summ)   # <16> or <16, true> (the lane walk)
 
 
 def test_band_traffic_from_committed_profile():
