@@ -542,3 +542,37 @@ def test_packed_batch_upload_runs_the_call_kernels(gpu_aligner_factory, oracle):
     got = np.zeros(int(off7[-1] - off7[0]), np.uint8)
     assert hip().hipMemcpy(got.ctypes.data, dev["reads"] + int(off7[0]) - dev["reads_bias"], got.nbytes, _D2H) == 0
     assert got.tobytes() == bytes(buf).upper()   # the kernels' bytes: upper case, every read
+
+
+def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, oracle):
+    """A resident pass of 400k reads (one launch of >= 300k reads: the first level's lane walk,
+    nw_band_walk<16, true>, and the lane-per-read classify compare) gives the same records and
+    runs as the pipelined call over the same batch (chunks of <= 262144 reads: the wave-per-read
+    walk), every read; and a sample of both against the oracle."""
+    from crispresso_amd.aligner import pack_2bit
+
+    amp = synth.random_amplicon(250, 1)
+    buf, off = synth.reads_from(amp, 400_000, 7)
+    n = len(off) - 1
+    pr = pack_2bit(buf, off)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    call = a.align_ops_packed(pr)
+    c_stats, c_off = call.stats.copy(), call.ops_off.copy()
+    c_ops = call.ops[:int(c_off[n])].copy()
+    a.upload_packed(pr)
+    a.run_async()
+    a.sync()
+    res = a.download_ops(n)
+    assert int(res.ops_off[n]) == int(c_off[n])
+    np.testing.assert_array_equal(res.ops_off, c_off)
+    for f in FIELDS:
+        np.testing.assert_array_equal(res.stats[f], c_stats[f], err_msg=f)
+    np.testing.assert_array_equal(res.ops[:int(c_off[n])], c_ops)
+    idx = np.arange(0, n, 997)
+    sub_buf, sub_off = pack_reads([bytes(buf[off[i]:off[i + 1]]).decode() for i in idx])
+    ob = a.align_ops(sub_buf, sub_off)
+    assert_same(oracle, amp, sub_buf, sub_off, ob.expand(amp, sub_buf, sub_off), "lane walk sample")
+    for j, i in enumerate(idx):   # the sample's records are the resident pass's
+        for f in FIELDS:
+            assert ob.stats[f][j] == res.stats[f][i], (f, int(i))
