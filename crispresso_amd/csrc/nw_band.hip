@@ -167,9 +167,16 @@ __host__ __device__ inline int band_words(int La, int Lb_max, int W = kBandDiags
     const int Lbm = Lb_max < La + W - 1 ? Lb_max : La + W - 1;
     return (((La + Lbm + 80) / 4 + 2) + 3) & ~3;   // column length: whole dwordx4 of the walk
 }
+// Stop summary (the first level, KernelArgs::band_summ): after a pair's tiles, per lane (diagonal
+// pair q) one byte per 16 words (64 steps, four tile rows) -- the OR of the block's "M < max"
+// bits, read A's four sub-steps in the low nibble, read B's in the high -- padded to 16 bytes
+// per lane.  A lane walk's M run skips the blocks whose bits for its read and diagonal are clear.
+__host__ __device__ inline int band_summ_bytes(int NW) { return ((((NW + 15) >> 4) + 15) & ~15); }
+
 __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W) {
-    return ((int64_t)kHdrBytes + 4 * W + (int64_t)band_words(La, Lb_max, W > kBandDiags ? W : kBandDiags) * (W / 2) * 4 +
-            255) & ~(int64_t)255;
+    const int NW = band_words(La, Lb_max, W > kBandDiags ? W : kBandDiags);
+    return ((int64_t)kHdrBytes + 4 * W + (int64_t)NW * (W / 2) * 4 + (int64_t)(W / 2) * band_summ_bytes(NW) + 255) &
+           ~(int64_t)255;
 }
 
 // Sort key of every read: its length bucket, or cap + 2 for a read identical to the
@@ -1223,7 +1230,7 @@ __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long lo
 // single-diagonal test (start cell's M == its diagonal's plain sum: the traceback is the
 // diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
 // passes; the others go to tile_list for the traceback pass.
-template <int W, int MODE>
+template <int W, int MODE, bool SUMM = false>   // SUMM: the traceback fill also writes the stop summary (lane walk)
 #ifndef NW_FILL_WPE
 #define NW_FILL_WPE 6
 #endif
@@ -1443,6 +1450,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         const int te_lo = (int)wave_min_u32(min(min((unsigned)te[0], (unsigned)te[1]),
                                                 min((unsigned)teB[0], (unsigned)teB[1])));
         unsigned* bits = TB ? (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q : nullptr;   // this lane's slot of each tile
+        // the stop summary (band_summ): the OR of a 16-word block's words (accumulated in LDS at each
+        // row's store, next to the row's stage), one byte per block
+        constexpr bool summ_on = TB && SUMM;
+        unsigned* sum_lds = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 64 + lane;
+        if (summ_on) *sum_lds = 0u;
+        auto summ_store = [&](int b, unsigned x) {   // this lane's byte of block b (addressed from its tile slot)
+            unsigned char* sp = (unsigned char*)(bits - 4 * q) + (size_t)NW * (W / 2) * 4 + q * band_summ_bytes(NW) + b;
+            *sp = (unsigned char)(((x >> 20) & 0xfu) | (((x >> 28) & 0xfu) << 4));
+        };
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
         unsigned cap0 = NEG2, cap1 = NEG2, capB0 = NEG2, capB1 = NEG2;   // read A's (low) / B's (high half)
@@ -1556,7 +1572,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
             if constexpr (TB) {
                 asm volatile("" ::: "memory");
                 const int w = ((tau4 - tau0) >> 2) & ~3;
-                if (act && w < NW) *(uint4*)(bits + w * kBL) = *(const uint4*)stage;
+                const uint4 row = *(const uint4*)stage;
+                if (act && w < NW) *(uint4*)(bits + w * kBL) = row;
+                if (summ_on) {
+                    const unsigned x = *sum_lds | row.x | row.y | row.z | row.w;
+                    const bool last = ((w >> 2) & 3) == 3;   // the block's fourth row: its summary byte
+                    if (last && act && (w >> 4) <= ((NW - 1) >> 4)) summ_store(w >> 4, x);   // a block with stored words
+                    *sum_lds = last ? 0u : x;
+                }
             }
         };
         auto pair8 = [&](int tau4, auto PROc, auto CAPc) {
@@ -1587,6 +1610,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
             pair8(tau4, std::false_type{}, std::true_type{});
         }
         if (((tau4 - tau0) >> 2) & 2) flush(tau4 - 8);   // a half row left: its other half is past tau_end
+        if (summ_on) {   // the last block, unless its fourth row stored it (every block up to the last word is written)
+            const int wl = ((tau4 - tau0) >> 2) - 1;
+            if (act && wl >= 0 && (wl >> 4) <= ((NW - 1) >> 4) && ((wl >> 2) & 3) != 3) summ_store(wl >> 4, *sum_lds);
+        }
 
         if constexpr (!TB) {
             band_diag_epilogue<W>(a, acd, tab, pcd, La, dlo, q, grp, g < pair_hi, act, ra, rb, LbA, LbB,
@@ -1902,11 +1929,11 @@ constexpr int kLaneRuns = 8;   // runs per lane in LDS ([kLaneRuns][64] dwords a
 #define NW_LANE_MROWS 2
 #endif
 constexpr int kMRows = NW_LANE_MROWS;   // tile rows per M round of the lane walk (<= 4: 32 cells)
-// The lane walk's wavefront waits for its slowest lane (~20 dependent rounds of tile loads for a
-// read with an indel): it pays on one long list (the kernel-resident pass: walk<16> 0.189 -> 0.165
-// ms) and not in a pipelined call, whose chunks' chains then ran longer (calls 1.94-1.97 vs
-// 1.92-1.93 ms with it on chunks of 196k reads and more) -- launches of fewer than kLaneWalkReads
-// reads (every chunk of a call: at most 262144) keep the wave-per-read walk at 6 wavefronts per SIMD.
+// The lane walk (with the stop summary its fill writes) pays on one long list: the kernel-resident
+// pass, walk<16> 0.189 -> 0.092 ms (fill<16> +13 us for the summary).  In a pipelined call it does
+// not (C2 1.962 vs 1.964 ms, the pooled C5 call 17.65 vs 16.98 ms with it on every chunk, in-process
+// A/Bs): launches of fewer than kLaneWalkReads reads (every chunk of a call: at most 262144) keep
+// the wave-per-read walk at 6 wavefronts per SIMD and the fill without the summary.
 #ifndef NW_LANE_READS
 #define NW_LANE_READS 300000
 #endif
@@ -2060,6 +2087,12 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                         const int tb0 = kBK - dlo + 2 - tau0, hb = 8 * h;
                         int i = ei, j = ej, state = RUN_M, kc = 0;   // kc: cells of the current run so far
                         bool fail = false;
+                        // the stop summary (band_summ_bytes): 16 blocks' bytes of one diagonal pair per load,
+                        // kept while the M runs stay on that pair and chunk
+                        const unsigned char* summ = (const unsigned char*)bits + (size_t)NW * (W / 2) * 4;
+                        const int NBp = band_summ_bytes(NW);
+                        int skey = -1;
+                        uint4 sv = make_uint4(0u, 0u, 0u, 0u);
                         for (int guard = 0; i > 0 && j > 0 && !over && !fail; ++guard) {
                             if (guard > 4 * (La + Lb + 64)) {
                                 fate = 1;
@@ -2073,8 +2106,48 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                                 }
                                 const int lim = min(i, j) - 1;
                                 const int tc = i + j - 4 + tb0 - 2 * kc;   // tau of the next cell to test
-                                // kMRows tile rows per round (8 cells of the diagonal each), their loads together
                                 const int r0 = tc >> 4, NR = NW >> 2;
+                                if (tc >= 0 && r0 < NR) {
+                                    // the first block at or below tc's with an "M < max" bit of this read on this
+                                    // diagonal (tau parity p: sub-steps p, p + 2); the cells above it are clear
+                                    const int b = tc >> 6, pq = kd >> 1;
+                                    const unsigned shb = 4 * h + (tc & 1);
+                                    int bf = -1;
+                                    for (int ch = b >> 4; ch >= 0 && bf < 0; --ch) {
+                                        if (skey != pq * 64 + ch) {
+                                            sv = *(const uint4*)(summ + pq * NBp + 16 * ch);
+                                            skey = pq * 64 + ch;
+                                        }
+                                        const unsigned sw[4] = {sv.x, sv.y, sv.z, sv.w};
+                                        unsigned m16 = 0u;
+#pragma unroll
+                                        for (int e = 0; e < 4; ++e) {
+                                            const unsigned t = (sw[e] >> shb) & 0x05050505u;
+                                            const unsigned nz = (t + 0x7f7f7f7fu) & 0x80808080u;   // bytes with a bit
+                                            m16 |= (((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) | ((nz >> 28) & 8u))
+                                                   << (4 * e);
+                                        }
+                                        const int top = ch == (b >> 4) ? (b & 15) : 15;
+                                        const unsigned cand = m16 & ((2u << top) - 1u);
+                                        if (cand) bf = 16 * ch + 31 - __builtin_clz(cand);
+                                    }
+                                    if (bf < b) {   // skip the clear blocks (to the matrix edge when none is flagged)
+                                        const int tstop = bf < 0 ? -1 : 64 * bf + 63;
+                                        const int cnt = (tc - tstop + 1) >> 1;   // cells with tau > tstop
+                                        const int L = lim - kc;
+                                        if (cnt > L) {   // the run reaches the matrix edge first
+                                            const int run = kc + max(L, 0) + 1;
+                                            push(RUN_M, run, false);
+                                            i -= run;
+                                            j -= run;
+                                            kc = 0;
+                                        } else {
+                                            kc += cnt;
+                                        }
+                                        continue;
+                                    }
+                                }
+                                // kMRows tile rows per round (8 cells of the diagonal each), their loads together
                                 uint4 v[kMRows];
 #pragma unroll
                                 for (int q = 0; q < kMRows; ++q)
@@ -2689,7 +2762,8 @@ hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch
 // ---- host-side helpers -------------------------------------------------------
 int band_fill_lds_bytes(int La, int wpb, int W) {
     const int pw = W == 16 ? BandGeo<16>::PW : W == 32 ? BandGeo<32>::PW : BandGeo<kWideDiags>::PW;
-    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * pw * band_pcs(La, W) + 256 + wpb * 1024;
+    return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * pw * band_pcs(La, W) + 256 + wpb * 1024 +
+           (W == 16 ? wpb * 256 : 0);   // + the stop summary's per-lane accumulators
 }
 int band_walk_lds_bytes(int La, int wpb, int lb_max, int W) {
     return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max, W);
@@ -2739,7 +2813,12 @@ int64_t band_lookback_words(int64_t n) {
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {
-    if (W == 16)
+    // the lane walk (and the stop summary its fill writes for it) on launches of kLaneWalkReads reads
+    KernelArgs al = a;
+    al.band_summ = W == 16 && a.ops && a.n >= kLaneWalkReads;
+    if (al.band_summ)
+        hipLaunchKernelGGL((nw_band_fill<16, 1, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, al);
+    else if (W == 16)
         hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else if (W == 32)
         hipLaunchKernelGGL((nw_band_fill<32, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
@@ -2748,8 +2827,8 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
-    if (W == 16 && a.ops && a.n >= kLaneWalkReads)
-        hipLaunchKernelGGL((nw_band_walk<16, true>), dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
+    if (al.band_summ)
+        hipLaunchKernelGGL((nw_band_walk<16, true>), dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, al);
     else if (W == 16)
         hipLaunchKernelGGL(nw_band_walk<16>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     else if (W == 32)
