@@ -1451,13 +1451,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                                                 min((unsigned)teB[0], (unsigned)teB[1])));
         unsigned* bits = TB ? (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q : nullptr;   // this lane's slot of each tile
         // the stop summary (band_summ): the OR of a 16-word block's words (accumulated in LDS at each
-        // row's store, next to the row's stage), one byte per block
+        // row's store, next to the row's stage), one byte per block, gathered in LDS 16 blocks at a
+        // time and stored as one 16-byte line piece per lane (byte stores spread over the pass had
+        // cost +0.12 GB of partial-line writes)
         constexpr bool summ_on = TB && SUMM;
-        unsigned* sum_lds = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 64 + lane;
-        if (summ_on) *sum_lds = 0u;
-        auto summ_store = [&](int b, unsigned x) {   // this lane's byte of block b (addressed from its tile slot)
-            unsigned char* sp = (unsigned char*)(bits - 4 * q) + (size_t)NW * (W / 2) * 4 + q * band_summ_bytes(NW) + b;
-            *sp = (unsigned char)(((x >> 20) & 0xfu) | (((x >> 28) & 0xfu) << 4));
+        unsigned* sum_lds = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 320 + lane;   // the block's OR
+        unsigned* sum_chunk = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 320 + 64 + 4 * lane;   // 16 blocks' bytes
+        if (summ_on) {
+            *sum_lds = 0u;
+            *(uint4*)sum_chunk = make_uint4(0u, 0u, 0u, 0u);
+        }
+        auto summ_flush = [&](int b) {   // the chunk holding block b, to the pair's summary
+            unsigned char* sp = (unsigned char*)(bits - 4 * q) + (size_t)NW * (W / 2) * 4 + q * band_summ_bytes(NW);
+            *(uint4*)(sp + (b & ~15)) = *(const uint4*)sum_chunk;
+            *(uint4*)sum_chunk = make_uint4(0u, 0u, 0u, 0u);
+        };
+        auto summ_put = [&](int b, unsigned x) {   // block b's byte; the chunk goes out with its last block
+            ((unsigned char*)sum_chunk)[b & 15] = (unsigned char)(((x >> 20) & 0xfu) | (((x >> 28) & 0xfu) << 4));
+            if ((b & 15) == 15) summ_flush(b);
         };
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
@@ -1577,7 +1588,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                 if (summ_on) {
                     const unsigned x = *sum_lds | row.x | row.y | row.z | row.w;
                     const bool last = ((w >> 2) & 3) == 3;   // the block's fourth row: its summary byte
-                    if (last && act && (w >> 4) <= ((NW - 1) >> 4)) summ_store(w >> 4, x);   // a block with stored words
+                    if (last && act && (w >> 4) <= ((NW - 1) >> 4)) summ_put(w >> 4, x);   // a block with stored words
                     *sum_lds = last ? 0u : x;
                 }
             }
@@ -1612,7 +1623,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         if (((tau4 - tau0) >> 2) & 2) flush(tau4 - 8);   // a half row left: its other half is past tau_end
         if (summ_on) {   // the last block, unless its fourth row stored it (every block up to the last word is written)
             const int wl = ((tau4 - tau0) >> 2) - 1;
-            if (act && wl >= 0 && (wl >> 4) <= ((NW - 1) >> 4) && ((wl >> 2) & 3) != 3) summ_store(wl >> 4, *sum_lds);
+            const int bl = min(wl >> 4, (NW - 1) >> 4);   // the last block with stored words
+            if (act && wl >= 0) {
+                // its byte unless its fourth row put it (the block ends past the computed words), then its chunk
+                const bool open = (wl >> 4) <= bl && ((wl >> 2) & 3) != 3;
+                if (open) ((unsigned char*)sum_chunk)[bl & 15] =
+                    (unsigned char)(((*sum_lds >> 20) & 0xfu) | (((*sum_lds >> 28) & 0xfu) << 4));
+                if (open || (bl & 15) != 15) summ_flush(bl);
+            }
         }
 
         if constexpr (!TB) {
@@ -2763,7 +2781,7 @@ hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch
 int band_fill_lds_bytes(int La, int wpb, int W) {
     const int pw = W == 16 ? BandGeo<16>::PW : W == 32 ? BandGeo<32>::PW : BandGeo<kWideDiags>::PW;
     return kTabBytes + align16(2 * band_acd_elems(La)) + wpb * pw * band_pcs(La, W) + 256 + wpb * 1024 +
-           (W == 16 ? wpb * 256 : 0);   // + the stop summary's per-lane accumulators
+           (W == 16 ? wpb * 1280 : 0);   // + the stop summary's per-lane accumulators and 16-block chunks
 }
 int band_walk_lds_bytes(int La, int wpb, int lb_max, int W) {
     return band_walk_shared_bytes(La) + wpb * band_walk_wave_bytes(La, lb_max, W);
