@@ -60,7 +60,7 @@ READS_PER_GPU = 1_000_000
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
 # VALU instruction count per fill launch (newest first)
 PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
-                 for d in ("r04_pmc_v16", "r04_pmc_v15", "r04_pmc_v14", "r04_pmc", "r03s2_v4", "r03s2_v3", "r03s2_v2", "r03_v3", "r02_v5", "r01_quant")]
+                 for d in ("r04_pmc_v16", "r04_pmc", "r03s2_v4", "r03s2_v3", "r03s2_v2", "r03_v3", "r02_v5", "r01_quant")]
 AMPLICON_LEN = 250
 
 
