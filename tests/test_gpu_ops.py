@@ -544,15 +544,24 @@ def test_packed_batch_upload_runs_the_call_kernels(gpu_aligner_factory, oracle):
     assert got.tobytes() == bytes(buf).upper()   # the kernels' bytes: upper case, every read
 
 
-def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, oracle):
+@pytest.mark.parametrize("kind", ["c2", "repeats"])
+def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, oracle, kind):
     """A resident pass of 400k reads (one launch of >= 300k reads: the first level's lane walk,
-    nw_band_walk<16, true>, and the lane-per-read classify compare) gives the same records and
-    runs as the pipelined call over the same batch (chunks of <= 262144 reads: the wave-per-read
-    walk), every read; and a sample of both against the oracle."""
+    nw_band_walk<16, true>, its fill's stop summary, and the lane-per-read classify compare) gives
+    the same records and runs as the pipelined call over the same batch (chunks of <= 262144
+    reads: the wave-per-read walk), every read; and a sample of both against the oracle.
+    "repeats": homopolymer and tandem-repeat runs in the amplicon (gap placement among equal
+    scores, "M < max" bits off the path) and the parity mix (more indels, N codes)."""
     from crispresso_amd.aligner import pack_2bit
 
-    amp = synth.random_amplicon(250, 1)
-    buf, off = synth.reads_from(amp, 400_000, 7)
+    if kind == "c2":
+        amp = synth.random_amplicon(250, 1)
+        buf, off = synth.reads_from(amp, 400_000, 7)
+    else:
+        rnd = synth.random_amplicon(250, 3)
+        amp = (rnd[:40] + "AAAAAAAA" + rnd[40:70] + "CAGCAGCAGCAGCAG" + rnd[70:120] + "TTTTTTGGGGGG" +
+               rnd[120:160] + "ATATATATAT" + rnd[160:])[:250]
+        buf, off = synth.reads_from(amp, 400_000, 8, synth.PARITY_MIX)
     n = len(off) - 1
     pr = pack_2bit(buf, off)
     a = gpu_aligner_factory()
