@@ -2338,7 +2338,7 @@ template <int W, bool LN = false>   // LN: the lane walk (walk_lanes) first, W <
 #define NW_WALK_WPE 6
 #endif
 #ifndef NW_WALK_LANE_WPE
-#define NW_WALK_LANE_WPE 5   // the first level's lane walk holds ~100 VGPRs
+#define NW_WALK_LANE_WPE 4   // the lane walk: 116 VGPRs, no spills (5: 96 with 11 spilled, walk 0.091 vs 0.085 ms); a resident pass runs ~9 of its wavefronts per CU
 #endif
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WALK_LANE_WPE : NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
