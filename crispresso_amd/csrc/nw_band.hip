@@ -1943,6 +1943,9 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
 // (sums over the band's neighbour diagonals), reads with codes outside A C G T, more than
 // kLaneRuns runs -- goes to `defer(k)`, the wave-per-read body, one read at a time.
 constexpr int kLaneRuns = 8;   // runs per lane in LDS ([kLaneRuns][64] dwords at the wave's area)
+#ifndef NW_MIS_UNROLL
+#define NW_MIS_UNROLL 8   // dword compares in flight per lane in count_mis (4: walk 0.086 ms, 8: 0.079, 16: 0.081)
+#endif
 #ifndef NW_LANE_MROWS
 #define NW_LANE_MROWS 2
 #endif
@@ -2031,7 +2034,7 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                     const unsigned* rw = (const unsigned*)(rp - ra);
                     const unsigned* aw = (const unsigned*)(amp_lds + (ia - aa));
                     unsigned rlo = rw[0], alo = aw[0];
-#pragma unroll 4
+#pragma unroll NW_MIS_UNROLL
                     for (int t = 0; t < n; t += 4) {
                         const unsigned rhi = rw[(t >> 2) + 1], ahi = aw[(t >> 2) + 1];
                         unsigned x = (__builtin_amdgcn_alignbyte(rhi, rlo, ra) ^ __builtin_amdgcn_alignbyte(ahi, alo, aa)) &
