@@ -54,7 +54,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md "Wave scheduling")
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
-VOP3P_ISSUE_CEILING = 1024 * 2.4e9 * 0.22   # measured: packed 16-bit VALU, 8 waves per SIMD
+# a micro-benchmark's rate, not a validated hardware ceiling: packed 16-bit / VOP3 / DPP VALU ops issued at 0.228
+# wave-instructions per SIMD-cycle (8 independent chains, 8 waves per SIMD; v_add_u32 reached only 0.39-0.41 of the
+# nominal 0.5 in the same benchmark), profiles/r04_ubench/ubench_issue_rate.txt
+UBENCH_VOP3P_RATE = 1024 * 2.4e9 * 0.228
 READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
 # 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
@@ -739,11 +742,11 @@ def band_cells(counts, La, mean_len):
             counts["exact_kernel"] * La * mean_len)
 
 
-def dry_run(args, rank, local, world, dist, seen):
+def dry_run(args, rank, local, world, dist, seen, place):
     """--dry-run: the N-rank plumbing without a GPU (CPU tests).  Each rank derives its share of
-    the C2 / C4 / pooled work exactly as a measured run would and reports it; rank 0 prints
-    them all in one line."""
-    from crispresso_amd import synth
+    the C2 / C4 / pooled work exactly as a measured run would and reports it, with its host
+    placement (CPU slice, native pool threads); rank 0 prints them all in one line."""
+    from crispresso_amd import _lib, synth
     from crispresso_amd.distributed import cell_partition, pooled_costs
 
     per_rank_c4 = C4_CALL_READS if world == 1 else C4_TOTAL_READS // world
@@ -761,11 +764,18 @@ def dry_run(args, rank, local, world, dist, seen):
     gathered = [torch.zeros_like(t) for _ in range(world)] if dist is not None else [t]
     if dist is not None:
         dist.all_gather(gathered, t)
+    place = dict(place, pool_threads=int(_lib.load().nw_host_threads()))
+    places = [None] * world
+    if dist is not None:
+        dist.all_gather_object(places, place)
+    else:
+        places = [place]
     barrier(dist)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": seen,
                           "ranks": [{"rank": int(g[0]), "device": int(g[1]), "c4_reads": int(g[2]),
                                      "pooled_range": [int(g[3]), int(g[4])]} for g in gathered],
+                          "host_placement": places,
                           "c4_reads_total": int(sum(int(g[2]) for g in gathered)),
                           "pooled_reads_total": int(len(lens))}), flush=True)
     if dist is not None:
@@ -815,15 +825,26 @@ def main():
     if seen != world:
         log(f"[rank {rank}] {seen} of {world} ranks reached the start")
         sys.exit(2)
+    # host placement before anything is allocated or the library's pool exists (one
+    # host thread set per GPU): at N > 1 every rank is bound to its slice of the CPU share on its
+    # GPU's NUMA node and its native pool sized to that slice; at N = 1 nothing changes
+    from crispresso_amd import placement
+
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    local_rank = int(os.environ.get("LOCAL_RANK", local))
+    ndev = int(os.environ.get("CRISPR_BENCH_DEVICES", "0"))   # the rehearsal's shared devices
+    place = placement.bind_rank(local_rank, local_world, apply=local_world > 1,
+                                device_of=(lambda r: r % ndev) if ndev > 0 else None)
     if args.dry_run:
-        dry_run(args, rank, local, world, dist, seen)
+        dry_run(args, rank, local, world, dist, seen, place)
         return
     from crispresso_amd import _lib, synth
     from crispresso_amd.aligner import GpuAligner
 
     share, share_detail = cpu_share()
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-    threads = args.cpu_threads or max(1, share // max(1, local_world))   # the ranks of a node share its CPUs
+    place["pool_threads"] = int(_lib.load().nw_host_threads())
+    # the ranks of a node share its CPUs: a bound rank uses its slice
+    threads = args.cpu_threads or (place["threads"] if local_world > 1 else max(1, share // max(1, local_world)))
     amplicon = synth.random_amplicon(AMPLICON_LEN, 1)
     seed = 2 if world == 1 else 10 + rank
     t0 = time.perf_counter()
@@ -833,6 +854,8 @@ def main():
 
     al = GpuAligner(local)
     al.set_reference(amplicon)
+    place["device_pci"] = placement.device_pci(local)   # the device HIP opened: does it match the KFD order?
+    place["pci_match"] = place["device_pci"] == place["gpu_pci"] if place["gpu_pci"] else None
     # the host batch and the outputs in pinned memory (the native FASTQ ingest, nw_fastq_pack, hands the
     # aligner exactly such a batch: the e2e leg)
     pb, po = _lib.pinned_copy(buf), _lib.pinned_copy(offsets)
@@ -983,6 +1006,7 @@ def main():
                 "kernel_geometry": geo,
             },
             "path_counts": call_counts,
+            "host_placement": place,
             "ingest_pack": {"ms": pack_s * 1e3, "bases_per_s": (int(offsets[-1]) - int(offsets[0])) / pack_s,
                             "threads": threads, "exceptions": int(len(pr.exc_pos)),
                             "note": "nw_pack_reads: the text batch -> 2 bits per base + exception list (host; the "
@@ -1035,12 +1059,13 @@ def main():
                     "valu_source": summ_src,
                     "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
                     "issue_peak_per_s": VALU_ISSUE_PEAK,
-                    # the measured issue ceiling of the fills' packed (VOP3P) instructions: ~0.22 wave64
-                    # instructions per SIMD per cycle at the ~2.4 GHz GRBM_GUI_ACTIVE shows
-                    "vop3p_ceiling_per_s": VOP3P_ISSUE_CEILING,
-                    "ceiling_frac": (fill_valu / (fill_ms * 1e-3) / VOP3P_ISSUE_CEILING) if fill_valu and fill_ms else None,
-                    "ceiling_source": "profiles/r02_ubench/ubench_issue_rate.txt (v_pk_* at 0.21-0.23 per SIMD-cycle), "
-                                      "clock from profiles/r03s2_v3 GRBM_GUI_ACTIVE / kernel time",
+                    # the rate the fills' packed (VOP3P) instructions reached in a micro-benchmark: a
+                    # measured rate, NOT a validated hardware ceiling
+                    "ubench_vop3p_rate_per_s": UBENCH_VOP3P_RATE,
+                    "ubench_rate_frac": (fill_valu / (fill_ms * 1e-3) / UBENCH_VOP3P_RATE) if fill_valu and fill_ms else None,
+                    "ubench_source": "profiles/r04_ubench/ubench_issue_rate.txt: v_pk_* / v_perm / v_and_or / DPP moves at "
+                                     "0.228 wave-instructions per SIMD-cycle with 8 independent chains and 8 waves per "
+                                     "SIMD; unvalidated as a ceiling (v_add_u32 reached 0.39, not the nominal 0.5)",
                     "band_cells_per_pass": cells,
                     "band_gcups": cells / (kms * 1e-3) / 1e9,
                     "note": "issue_frac = SQ_INSTS_VALU of one fill<16> launch (PMC, chip total) / its live HIP-event "

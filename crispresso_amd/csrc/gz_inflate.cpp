@@ -563,7 +563,9 @@ bool inflate_parallel(const unsigned char* file, size_t n, int threads, Crc32Fn 
         uint64_t e = 0;
         if (decode_range(b, o, stop, &e) != kOk || !o.finish()) return;
         const unsigned char* d = buf.p + off[(size_t)k];
-        crcs[(size_t)k] = crc ? crc(0, d, len[(size_t)k]) : (uint32_t)crc32(0, d, (uInt)len[(size_t)k]);
+        // zlib's crc32 takes a 32-bit length: a range over 4 GiB (few block starts found in a
+        // large member) goes through crc32_z's size_t length instead of being truncated
+        crcs[(size_t)k] = crc ? crc(0, d, len[(size_t)k]) : (uint32_t)crc32_z(0, d, (z_size_t)len[(size_t)k]);
         ok2[(size_t)k] = 1;
     });
     uint32_t all = crcs[0];

@@ -10,27 +10,62 @@
 #include <algorithm>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
 
+#include <sched.h>
 #include <unistd.h>
 
 namespace nw_host {
 
+// The host threads this process may use: CRISPR_NW_HOST_THREADS when set (the rank binder,
+// crispresso_amd/placement.py, sets it to the size of the rank's CPU slice), else the CPUs of
+// the process's affinity mask capped by the cgroup CPU quota (a GPU box shows the whole
+// machine -- 256 CPUs -- to sched_getaffinity and hardware_concurrency but gives a job 16 of
+// them), divided among the node's ranks (LOCAL_WORLD_SIZE: 8 processes of one node must not
+// each start a pool sized for all of it), at most 64.
+inline int default_threads() {
+    if (const char* e = std::getenv("CRISPR_NW_HOST_THREADS")) return std::max(1, std::min(64, std::atoi(e)));
+    int cpus = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
+    if (cpus <= 0) cpus = (int)std::max(1u, std::thread::hardware_concurrency());
+    double quota = 0;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {   // cgroup v2: "<quota|max> <period>"
+        char q[32] = {0};
+        long per = 0;
+        if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
+            quota = std::atof(q) / (double)per;
+        std::fclose(f);
+    } else if (FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {   // cgroup v1
+        long q = -1, per = 0;
+        if (std::fscanf(g, "%ld", &q) != 1) q = -1;
+        std::fclose(g);
+        if (FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(h, "%ld", &per) != 1) per = 0;
+            std::fclose(h);
+        }
+        if (q > 0 && per > 0) quota = (double)q / (double)per;
+    }
+    if (quota >= 1.0) cpus = std::min(cpus, (int)quota);
+    int ranks = 1;
+    if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, std::atoi(e));
+    return std::max(1, std::min(64, cpus / ranks));
+}
+
 class Pool {
 public:
-    // The process-wide pool: CRISPR_NW_HOST_THREADS (default min(16, cores): a GPU box gives a
-    // process 16 CPUs; the FASTQ ingest parses and inflates on all of them) threads in
-    // all, the caller included.  Never destroyed: parked threads end with the process.
+    // The process-wide pool: default_threads() threads in all, the caller included (the FASTQ
+    // ingest parses and inflates on all of them).  Never destroyed: parked threads end with
+    // the process.
     static Pool& get() {
-        static Pool* p = [] {
-            int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-            if (const char* e = std::getenv("CRISPR_NW_HOST_THREADS")) nt = std::max(1, std::min(64, std::atoi(e)));
-            return new Pool(nt);
-        }();
+        static Pool* p = new Pool(default_threads());
         return *p;
     }
 

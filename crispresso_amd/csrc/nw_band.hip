@@ -60,12 +60,8 @@
 
 #include "nw_common.h"
 
-#ifndef NW_CAND   // classify: exact-copy candidates compared together
-#define NW_CAND 8
-#endif
-#ifndef NW_BAND_WALK_CPL   // gap-run cells per lane and round (a gap run inside the band is < W <= 64 cells)
-#define NW_BAND_WALK_CPL 1
-#endif
+#define NW_CAND 8            // classify: exact-copy candidates compared together
+#define NW_BAND_WALK_CPL 1   // gap-run cells per lane and round (a gap run inside the band is < W <= 64 cells)
 
 namespace nw {
 
@@ -312,12 +308,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const int n2 = (La + 15) / 16 + 2, nseed = a.n_seed;
     unsigned* skey = amp2s + n2;
     uint16_t* spos = (uint16_t*)(skey + nseed);
-#ifdef NW_NO_WIN
-    const bool win_ok = false;
-#else
     const bool win_ok = PK && amp_acgt_all && a.ops && a.band_maxsub == 5 * sc5 && a.gap_extend >= 0 && a.amp2 &&
                         a.gap_open > xl && nseed > 0 && La <= 1024;
-#endif
     // 16 bases of the packed stream from batch position p, and of the amplicon from position p (LDS)
     auto rword = [&](long long p) -> unsigned {
         const long long q = p - a.pk_pos0;
@@ -371,7 +363,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // away from the words already in registers
         const bool one_chunk = nd <= 64;
         unsigned long long emit_later = 0ull;
-#ifndef NW_WAVE_CMP
         if constexpr (PK) {
             // Packed input, ops output, an A C G T amplicon of at most 256 bp: one read per lane.  Its
             // 2-bit words (one shift of the stream's dwords) against the amplicon's give the
@@ -453,7 +444,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 }
             }
         }
-#endif
         while (cand) {
             int us[kCand];
             unsigned diff[kCand], raw[kCand];
@@ -623,10 +613,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 win = __ballot(cand_w);
                 // one substitution: every other full-overlap diagonal needs two mismatches, the two
                 // diagonals pairing Lb - 1 residues one (the whole wave on each such read)
-#ifdef NW_NO_SUB1WIN
-                if (true) win &= ~__ballot(cand_w && win_k == 1);
-                else
-#endif
                 // (the read's 16-base words go to LDS once per candidate: the offsets' compares read them
                 // there, with no global round trip per offset)
                 unsigned* rbw = s_rbw[threadIdx.x >> 6];
@@ -668,12 +654,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // with more than 8 hits (a repeat) leaves the read to the exact kernel.
         int32_t sinfo = 0;
         if constexpr (PK) {
-#ifdef NW_NO_SEED
-            if (false) {
-#else
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
                 !(((exact | sub1 | sub2 | win) >> lane) & 1ull)) {
-#endif
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
@@ -1231,9 +1213,7 @@ __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long lo
 // diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
 // passes; the others go to tile_list for the traceback pass.
 template <int W, int MODE, bool SUMM = false>   // SUMM: the traceback fill also writes the stop summary (lane walk)
-#ifndef NW_FILL_WPE
-#define NW_FILL_WPE 6
-#endif
+#define NW_FILL_WPE 6   // 5: no spills in the traceback fill but slower
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
@@ -1943,22 +1923,14 @@ __device__ bool band_single_diagonals_below(const KernelArgs& a, const unsigned 
 // (sums over the band's neighbour diagonals), reads with codes outside A C G T, more than
 // kLaneRuns runs -- goes to `defer(k)`, the wave-per-read body, one read at a time.
 constexpr int kLaneRuns = 8;   // runs per lane in LDS ([kLaneRuns][64] dwords at the wave's area)
-#ifndef NW_MIS_UNROLL
 #define NW_MIS_UNROLL 8   // dword compares in flight per lane in count_mis (4: walk 0.086 ms, 8: 0.079, 16: 0.081)
-#endif
-#ifndef NW_LANE_MROWS
-#define NW_LANE_MROWS 2
-#endif
-constexpr int kMRows = NW_LANE_MROWS;   // tile rows per M round of the lane walk (<= 4: 32 cells)
+constexpr int kMRows = 2;   // tile rows per M round of the lane walk (<= 4: 32 cells)
 // The lane walk (with the stop summary its fill writes) pays on one long list: the kernel-resident
 // pass, walk<16> 0.189 -> 0.092 ms (fill<16> +13 us for the summary).  In a pipelined call it does
 // not (C2 1.962 vs 1.964 ms, the pooled C5 call 17.65 vs 16.98 ms with it on every chunk, in-process
 // A/Bs): launches of fewer than kLaneWalkReads reads (every chunk of a call: at most 262144) keep
 // the wave-per-read walk at 6 wavefronts per SIMD and the fill without the summary.
-#ifndef NW_LANE_READS
-#define NW_LANE_READS 300000
-#endif
-constexpr long long kLaneWalkReads = NW_LANE_READS;
+constexpr long long kLaneWalkReads = 300000;
 template <int W, class Defer>
 __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, unsigned char* wb,
                            const unsigned char* amp_lds, bool amp_acgt, int sc5, const Defer& defer) {
@@ -2337,12 +2309,8 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
 // next (wider) level.  W >= kBandDiags: they go to the fallback list (W = kBandDiags: the
 // wide level's input; the wide level: the exact int32 kernel's).
 template <int W, bool LN = false>   // LN: the lane walk (walk_lanes) first, W < kBandDiags, ops output
-#ifndef NW_WALK_WPE
 #define NW_WALK_WPE 6
-#endif
-#ifndef NW_WALK_LANE_WPE
 #define NW_WALK_LANE_WPE 4   // the lane walk: 116 VGPRs, no spills (5: 96 with 11 spilled, walk 0.091 vs 0.085 ms); a resident pass runs ~9 of its wavefronts per CU
-#endif
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WALK_LANE_WPE : NW_WALK_WPE))) void nw_band_walk(const KernelArgs a) {
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
@@ -2638,7 +2606,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
         }
         lds_fence();
     };
-#ifndef NW_WALK_WAVE
     if constexpr (LN && W < kBandDiags) {
         if (a.ops) {
             walk_lanes<W>(a, klo, khi, wb, amp_lds, amp_acgt, sc5, [&](long long kq) {
@@ -2664,7 +2631,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
             return;
         }
     }
-#endif
     long long k = klo + (long long)blockIdx.x * wpb + wave;
     int it = 0;   // parity of the slots holding read k's header and bytes
     if (k < khi) {   // the pipeline's start: read k's header, then its bytes and the next header

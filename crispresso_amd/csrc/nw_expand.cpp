@@ -90,7 +90,7 @@ bool expand_one(const Tables& T, const unsigned char* ref, int64_t La, const uin
 
 template <class F>
 void parallel_for(int64_t n, int32_t nthreads, const F& f) {
-    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nt = nthreads > 0 ? nthreads : nw_host::default_threads();
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
     if (nt == 1) {
         f(0, n);
@@ -292,7 +292,7 @@ extern "C" int nw_expand_ops(const char* ref, int32_t ref_len, const char* reads
     const Tables& T = tables();
     std::vector<uint8_t> acode((size_t)ref_len);
     for (int32_t i = 0; i < ref_len; ++i) acode[(size_t)i] = T.code[(unsigned char)ref[i]];
-    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nt = nthreads > 0 ? nthreads : nw_host::default_threads();
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
     std::atomic<int> bad{0};
     auto work = [&](int64_t lo, int64_t hi) {

@@ -2442,6 +2442,8 @@ int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d
     return NW_OK;
 }
 
+int nw_host_threads(void) { return nw_host::Pool::get().threads(); }
+
 int nw_host_alloc(int64_t bytes, void** out) {
     if (!out || bytes < 0) return NW_E_INVALID;
     *out = nullptr;

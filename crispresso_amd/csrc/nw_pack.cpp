@@ -63,7 +63,7 @@ extern "C" int nw_pack_reads(const char* reads, const int64_t* offsets, int64_t 
     const int64_t b0 = offsets[0], b1 = offsets[n];
     if (b1 < b0) return NW_E_INVALID;
     const int64_t q0 = b0 / 4, q1 = (b1 + 3) / 4;
-    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nt = nthreads > 0 ? nthreads : nw_host::default_threads();
     nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, (q1 - q0) / (1 << 16) + 1));
     std::vector<std::vector<std::pair<int64_t, uint8_t>>> exc((size_t)nt);
     const int64_t per = ((q1 - q0 + nt - 1) / nt + 3) & ~(int64_t)3;

@@ -280,6 +280,11 @@ int nw_host_alloc(int64_t bytes, void** out);
 void nw_host_free(void* p);
 int nw_host_register(void* p, int64_t bytes);
 int nw_host_unregister(void* p);
+/* Threads of the library's host pool (the call's length scan, FASTQ ingest, packing, the
+ * DataFrame helpers): CRISPR_NW_HOST_THREADS when set, else the process's CPU affinity capped
+ * by the cgroup quota and divided by LOCAL_WORLD_SIZE (crispresso_amd/placement.py binds a
+ * rank and sets the variable).  Creates the pool on first use. */
+int nw_host_threads(void);
 
 /* The three alignment rows of n reads from their runs (host, nthreads threads;
  * <= 0: all cores): for read r at aln_out + r*3*stride the aligned amplicon, the
