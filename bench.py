@@ -59,11 +59,12 @@ VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2
 # nominal 0.5 in the same benchmark), profiles/r04_ubench/ubench_issue_rate.txt
 UBENCH_VOP3P_RATE = 1024 * 2.4e9 * 0.228
 READS_PER_GPU = 1_000_000
-# rocprofv3 --pmc summaries of this build's kernels on this workload (scripts/gpu_pmc.sh + pmc_summary.py:
-# 2 x FETCH_SIZE + WRITE_SIZE per launch, the guide's gfx950 correction); source of roofline.traffic and of the
-# VALU instruction count per fill launch (newest first)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", d, "pmc_summary.json")
-                 for d in ("r04_pmc_v16", "r04_pmc", "r03s2_v4", "r03s2_v3", "r03s2_v2", "r03_v3", "r02_v5", "r01_quant")]
+# rocprofv3 --pmc summaries (scripts/gpu_pmc_call.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the guide's
+# gfx950 correction) of the TIMED CALL's kernels (every launch of warmup + steps calls, per call) and of the
+# quantification leg's kernels; each records the sha1 of the library it profiled (checked against the one loaded)
+CALL_PMC = os.path.join(ROOT, "profiles", "r05_pmc", "summary_call.json")
+QUANT_PMC = os.path.join(ROOT, "profiles", "r05_pmc", "summary_quant.json")
+LIB_SO = os.path.join(ROOT, "crispresso_amd", "lib", "libcrispr_nw.so")
 AMPLICON_LEN = 250
 
 
@@ -174,35 +175,34 @@ def max_over_ranks(dist, value):
     return float(t.item())
 
 
-def pmc_summary(required):
-    """(summary dict, path) of the newest PMC summary holding a kernel whose name contains `required`."""
-    for path in PMC_SUMMARIES:
-        try:
-            with open(path) as f:
-                summ = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if any(required in k for k in summ):
-            return summ, os.path.relpath(path, ROOT)
-    return None, None
+def lib_sha1():
+    import hashlib
+
+    try:
+        with open(LIB_SO, "rb") as f:
+            return hashlib.sha1(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
-def pmc_traffic(*prefixes, required=None):
-    """(HBM bytes per launch of the kernels whose names start with `prefixes`, source file), from the
-    first summary in PMC_SUMMARIES that holds them (and a kernel containing `required`)."""
-    for path in PMC_SUMMARIES:
-        try:
-            with open(path) as f:
-                summ = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if required and not any(required in k for k in summ):
-            continue
-        vals = [v["hbm_bytes_per_launch"] for k, v in summ.items()
-                if any(k.startswith(p) for p in prefixes) and "hbm_bytes_per_launch" in v]
-        if vals:
-            return float(sum(vals)), os.path.relpath(path, ROOT)
-    return None, None
+def pmc_per_call(path, select):
+    """(HBM bytes per call, VALU per call of the fill<16> kernels, kernels, source note) summed over the
+    kernels of a per-call PMC summary whose names satisfy `select`; None when the summary is absent."""
+    try:
+        with open(path) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None
+    meta = summ.pop("_meta", {})
+    names = sorted(k for k in summ if select(k) and "hbm_bytes_per_call" in summ[k])
+    if not names:
+        return None
+    traffic = float(sum(summ[k]["hbm_bytes_per_call"] for k in names))
+    valu16 = sum(summ[k].get("valu_per_call", 0.0) for k in names if "nw_band_fill<16" in k) or None
+    here = lib_sha1()
+    return {"traffic": traffic, "valu_fill16": valu16, "kernels": names,
+            "source": os.path.relpath(path, ROOT), "calls_profiled": meta.get("calls"),
+            "lib_sha1": meta.get("lib_sha1"), "lib_matches_loaded": (meta.get("lib_sha1") == here) if here else None}
 
 
 def sample_check(amplicon, buf, offsets, ob, every, threads):
@@ -286,10 +286,13 @@ def cpu_baseline(amplicon, buf, offsets, n_sample, threads, n_sample_1t, share_d
     }
 
 
-def kernel_pass(al, pr, steps, warmup):
+def kernel_pass(al, pr, steps, warmup, lane_walk=False):
     """The packed call's kernels + ops compaction on the batch resident in HBM (upload once, in
-    nw_align_ops_packed_lens' layout: classify decodes the 2-bit reads as in the call)."""
+    nw_align_ops_packed_lens' layout: classify decodes the 2-bit reads as in the call), one
+    launch of each over the whole batch.  lane_walk: the first level's lane walk + stop summary
+    instead of the call's wave-per-read walk (no pipelined call runs it)."""
     al.upload_packed(pr)
+    al.set_lane_walk(lane_walk)
     for _ in range(warmup):
         al.run_async()
         al.sync()
@@ -299,6 +302,7 @@ def kernel_pass(al, pr, steps, warmup):
         kms.append(al.sync())
         phases.append(al.phase_times())
     ph = {k: float(np.mean([d[k] for d in phases])) for k in phases[0]}
+    al.set_lane_walk(False)
     return float(np.mean(kms)), ph, al.path_counts(), al.algo_bytes(), al.geometry()
 
 
@@ -342,7 +346,7 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
     elapsed = time.perf_counter() - t0
     algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
     kavg = float(np.mean(kms))
-    q_traffic, q_src = pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce")
+    qp = pmc_per_call(QUANT_PMC, lambda k: "nwq::" in k)
     out = {
         "metric": "quantified reads/s (process_df_chunk on the aligned C2 batch, device-resident)",
         "value": n_reads * steps / elapsed,
@@ -354,8 +358,11 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
         "kernel_ms_avg": kavg,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": q_traffic,
-                     "traffic_source": q_src,
+                     "traffic": qp["traffic"] if qp else None,
+                     "traffic_source": (f"{qp['source']} (rocprofv3 --pmc of bench.py --quant-only, per run, "
+                                        f"library sha1 {qp['lib_sha1']}, matches the loaded one: "
+                                        f"{qp['lib_matches_loaded']})") if qp else None,
+                     "traffic_kernels": qp["kernels"] if qp else None,
                      "algo_bytes_per_launch": algo,
                      "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 16 (result); + 3*aln_len for rows not "
                                        "UNMODIFIED on input (the three alignment rows)"},
@@ -805,6 +812,8 @@ def main():
     ap.add_argument("--kernel-only", action="store_true",
                     help="profiling: only the kernel-resident pass (one launch of each kernel per step over the whole "
                          "batch, so rocprofv3 per-dispatch figures are per-pass figures); value = the kernel rate")
+    ap.add_argument("--quant-only", action="store_true",
+                    help="profiling: only the downstream quantification leg (its kernels on the resident batch)")
     ap.add_argument("--skip-kernel-pass", action="store_true",
                     help="tracing: stop after the timed packed calls (no text call, kernel-resident pass or legs)")
     ap.add_argument("--pooled-amplicons", type=int, default=96)
@@ -865,6 +874,12 @@ def main():
     p_off = _lib.PinnedBuffer(n + 1, np.int64)
     p_ops = _lib.PinnedBuffer(4 * n + 4096, np.uint32)
     out = (p_stats.array, p_ops.array, p_off.array)
+    if args.quant_only:
+        q = quant_leg(al, amplicon, buf, offsets, n, args.steps, args.warmup, rank, world, args.quant_cpu_sample, True)
+        if rank == 0:
+            print(json.dumps(q), flush=True)
+        al.close()
+        return
     if args.kernel_only:
         from crispresso_amd.aligner import pack_2bit
 
@@ -918,6 +933,7 @@ def main():
     expand_s = time.perf_counter() - t1
 
     kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup)
+    kms_lw, phases_lw, _, _, _ = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
     geo["fallback_reads"] = counts["band_fallback"]
     geo["exact_kernel_reads"] = counts["exact_kernel"]
 
@@ -965,14 +981,10 @@ def main():
             except Exception as exc:
                 legs[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
-    traffic, traffic_src = pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                       "nw::nw_ops_", "nw::(anonymous namespace)::nw_ops_",
-                                       required="nw::nw_band_fill<16")
-    summ, summ_src = pmc_summary("nw_band_fill<16")
-    fill_valu = None
-    if summ:   # the 16-diagonal fills of one pass: the diagonal pass and the traceback fill
-        vals = [v.get("SQ_INSTS_VALU") for k, v in summ.items() if "nw_band_fill<16" in k and v.get("SQ_INSTS_VALU")]
-        fill_valu = float(sum(vals)) if vals else None
+    # the call's own kernels: HBM traffic and the fill<16> VALU count per call (PMC of the timed call)
+    cp = pmc_per_call(CALL_PMC, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
+    traffic = cp["traffic"] if cp else None
+    fill_valu = cp["valu_fill16"] if cp else None
     lens = np.diff(offsets)
     cells = band_cells(counts, AMPLICON_LEN, float(lens.mean()) if n else 0.0)
     pass_gbs = algo_bytes / (kms * 1e-3) / 1e9
@@ -1025,8 +1037,14 @@ def main():
             "kernel_rate": {
                 "value": n / (kms * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms, "phases_ms": phases,
                 "path_counts": counts,
-                "note": "the call's kernels + ops compaction on the batch resident in HBM, outputs left in HBM "
-                        "(HIP events on the aligner's stream)",
+                "note": "the call's own kernels (the wave-per-read walk) + ops compaction on the batch resident in "
+                        "HBM, one launch of each over the batch, outputs left in HBM (HIP events on the aligner's "
+                        "stream)",
+            },
+            "kernel_rate_lane_walk": {
+                "value": n / (kms_lw * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms_lw, "phases_ms": phases_lw,
+                "note": "the same resident pass with the first level's lane walk + stop summary "
+                        "(nw_batch_set_lane_walk): faster on one long list, no pipelined call runs it (DESIGN.md 4a)",
             },
             "expand": {"ms": expand_s * 1e3, "reads_per_s": n / expand_s, "threads": threads,
                        "note": "nw_expand_ops: the three rows of every read rebuilt from its runs on the host "
@@ -1041,11 +1059,16 @@ def main():
                 "call_achieved": call_gbs,
                 "call_frac": call_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "traffic_source": f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the bench "
-                                  "command, per pass of the band kernels + exact kernel + compaction)",
-                "kernel": "one aligner pass: nw_band_classify + length sort + nw_band_fill<16> + nw_band_walk<16> "
-                          "+ the 32-diagonal level on its redo list + nw_align_kernel on what neither band "
-                          "certifies + nw_ops compaction",
+                "traffic_source": (f"{cp['source']} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py "
+                                   f"--skip-kernel-pass: every launch of {cp['calls_profiled']} timed calls, summed "
+                                   f"per call; library sha1 {cp['lib_sha1']}, matches the loaded one: "
+                                   f"{cp['lib_matches_loaded']})") if cp else None,
+                "traffic_kernels": cp["kernels"] if cp else None,
+                "kernel": "the call's kernels over the 1M reads: nw_band_classify<true> + nw_band_segsort + "
+                          "nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1> + nw_band_walk<16> (wave per "
+                          "read) + redo compaction + nw_band_fill/walk<128> (wide level) + nw_align_kernel + "
+                          "nw_ops_compact; achieved = their resident pass (one launch each), the call itself: "
+                          "call_achieved",
                 "kernel_ms_avg": kms,
                 "achieved_def": "algorithmic bytes of the pass / its device time (HIP events on the aligner's "
                                 "stream, batch resident in HBM); call_achieved: the same bytes / ms_per_step (the "
@@ -1056,7 +1079,7 @@ def main():
                     "kernel": "nw_band_fill<16, *> (the largest phase: the diagonal pass and the traceback fill)",
                     "fill16_ms": fill_ms,
                     "valu_instructions_per_launch": fill_valu,
-                    "valu_source": summ_src,
+                    "valu_source": cp["source"] if cp else None,
                     "issue_frac": (fill_valu / (fill_ms * 1e-3) / VALU_ISSUE_PEAK) if fill_valu and fill_ms else None,
                     "issue_peak_per_s": VALU_ISSUE_PEAK,
                     # the rate the fills' packed (VOP3P) instructions reached in a micro-benchmark: a

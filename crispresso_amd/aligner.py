@@ -272,7 +272,8 @@ class GpuAligner:
 
     def upload_packed(self, pr: "PackedReads") -> None:
         """Resident batch in the packed call's layout (nw_batch_upload_packed, ops output):
-        run_async then times the kernels nw_align_ops_packed_lens runs."""
+        run_async then times the kernels nw_align_ops_packed_lens runs (in one launch each over
+        the whole batch; set_lane_walk(True) swaps the first level's walk for the lane walk)."""
         if pr.lens is None:
             raise NeedleError("upload_packed needs the reads' lengths (PackedReads.lens)")
         self.set_output("ops")
@@ -282,6 +283,11 @@ class GpuAligner:
             self._h, _lib.ptr(pr.packed), _lib.ptr(pr.offsets), _lib.ptr(pr.lens), n,
             _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,
             len(pr.exc_pos)), "nw_batch_upload_packed")
+
+    def set_lane_walk(self, on: bool) -> None:
+        """Resident passes only: the first band level's lane walk + stop summary
+        (nw_batch_set_lane_walk; no pipelined call runs it)."""
+        self._check(self.lib.nw_batch_set_lane_walk(self._h, 1 if on else 0), "nw_batch_set_lane_walk")
 
     def run_async(self) -> None:
         self._check(self.lib.nw_batch_run_async(self._h), "nw_batch_run_async")

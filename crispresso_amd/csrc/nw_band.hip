@@ -1928,9 +1928,8 @@ constexpr int kMRows = 2;   // tile rows per M round of the lane walk (<= 4: 32 
 // The lane walk (with the stop summary its fill writes) pays on one long list: the kernel-resident
 // pass, walk<16> 0.189 -> 0.092 ms (fill<16> +13 us for the summary).  In a pipelined call it does
 // not (C2 1.962 vs 1.964 ms, the pooled C5 call 17.65 vs 16.98 ms with it on every chunk, in-process
-// A/Bs): launches of fewer than kLaneWalkReads reads (every chunk of a call: at most 262144) keep
-// the wave-per-read walk at 6 wavefronts per SIMD and the fill without the summary.
-constexpr long long kLaneWalkReads = 300000;
+// A/Bs), so no call uses it: only a resident pass that asks for it (nw_batch_set_lane_walk;
+// KernelArgs::band_summ) runs it -- the bench reports that pass beside the call's kernels.
 template <int W, class Defer>
 __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, unsigned char* wb,
                            const unsigned char* amp_lds, bool amp_acgt, int sc5, const Defer& defer) {
@@ -2800,9 +2799,9 @@ int64_t band_lookback_words(int64_t n) {
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill) {
-    // the lane walk (and the stop summary its fill writes for it) on launches of kLaneWalkReads reads
+    // the lane walk (and the stop summary its fill writes for it) when the context asked for it
     KernelArgs al = a;
-    al.band_summ = W == 16 && a.ops && a.n >= kLaneWalkReads;
+    al.band_summ = W == 16 && a.ops && a.band_summ;
     if (al.band_summ)
         hipLaunchKernelGGL((nw_band_fill<16, 1, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, al);
     else if (W == 16)

@@ -52,7 +52,7 @@ struct KernelArgs {
     uint8_t* band_region;          // per-pair regions of the pass (band_stride bytes each)
     int64_t band_stride;
     int32_t band_words;            // traceback words per lane and pair
-    int32_t band_summ;             // the first level's fill writes the stop summary the lane walk reads
+    int32_t band_summ;             // the first level's fill writes the stop summary the lane walk reads (nw_batch_set_lane_walk)
     int32_t band_lb_cap;           // longest read the band kernels take; longer ones sort last
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
     const uint32_t* band_tab;      // [17 amplicon codes (EDNAFULL, pad)][6][6 read codes] packed int16x2 score + 2 E

@@ -196,6 +196,8 @@ struct nw_ctx {
     bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
     bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
+    bool l2_skip = false;             // this chunk: no second-level launches, the wide level takes the redo list
+    bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -232,9 +234,28 @@ struct nw_ctx {
     int64_t call_counts[4] = {0, 0, 0, 0};
     int64_t call_exact = 0;            // reads of the last call that reached the exact kernel
     int64_t ops_h2d_bytes = 0, ops_d2h_bytes = 0;
+    // CRISPR_NW_TRACE=1 (diagnostics): an event after every launch of the call's last chunks,
+    // printed (us from the first upload) at the end of the call
+    bool trace_on = false;
+    int trace_chunk = 0;
+    std::vector<std::pair<std::string, hipEvent_t>> trace_ev;
+    size_t trace_used = 0;
 };
 
 namespace {
+
+// diagnostics: an event after the launch just queued on c->cs (CRISPR_NW_TRACE)
+void tmark(nw_ctx* c, const char* what) {
+    if (!c->trace_on) return;
+    if (c->trace_used == c->trace_ev.size()) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->trace_ev.push_back({std::string(), e});
+    }
+    auto& slot = c->trace_ev[c->trace_used++];
+    slot.first = std::to_string(c->trace_chunk) + " " + what;
+    (void)hipEventRecord(slot.second, c->cs);
+}
 
 int fail(nw_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
@@ -981,6 +1002,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.rowpos = c->cur.rowpos;
     a.end_weight = c->end_weight;
     a.tail_prio = c->tail_prio;
+    a.band_summ = c->lane_walk && c->phases ? 1 : 0;   // resident passes only (nw_batch_run_async)
     a.end_open = c->end_open;
     a.end_extend = c->end_extend;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
@@ -1057,6 +1079,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.tile_count = c->s->d_fallback_count.p + 5;
         }
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
+        tmark(c, "classify+sort");
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 1) / 2;
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
@@ -1075,6 +1098,7 @@ int launch_range(nw_ctx* c, int64_t base) {
                          ? (int)std::max<int64_t>(1024, std::min<int64_t>(c->n / 16, 2 * c->wide_pairs))
                          : 1024;
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
+        if (c->l2_skip && two && c->wide_fill.grid > 0) direct = 1 << 30;   // every redo read to the wide level
         if (!two) direct = 0;
         c->redo_direct = direct;
         // (the diagonal pass and the traceback fill as one launch measured slower: kernel-resident
@@ -1085,6 +1109,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             const int W = lvl == 0 ? 16 : 32;
             if (lvl == 1 && two) {
                 HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, next_epoch(c), c->cs));
+                tmark(c, "redo");
                 al.band_order = c->s->d_redo.p;
                 al.band_count = a.redo_count;
             }
@@ -1093,18 +1118,21 @@ int launch_range(nw_ctx* c, int64_t base) {
             const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
             const nw::LaunchCfg& wc = lvl == 0 ? c->diag16_walk : c->diag_walk;
             const bool first = lvl == (two ? 0 : 1);
+            if (!first && c->l2_skip && direct == (1 << 30)) break;   // no second-level launches at all
             if (!first) {   // the second level aligns the redo list only
                 al.order_a = nullptr;
                 al.tile_list = nullptr;
                 al.tile_count = nullptr;
             } else if (al.order_a) {
                 HIP_OR_FAIL(c, nw::launch_band_diag(W, al, fc, pairs, c->cs));
+                tmark(c, "diag");
             }
             for (int64_t lo = 0; lo < pairs; lo += pp) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
                 ap.band_pair_hi = std::min(pairs, lo + pp);
                 HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
+                tmark(c, W == 16 ? "fill16+walk16" : "fill32+walk32");
                 if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
             if (first && c->split_to) {   // the latency-bound rest of the chunk on the tail stream
@@ -1136,11 +1164,13 @@ int launch_range(nw_ctx* c, int64_t base) {
             aw.fallback_list = c->s->d_fallback2.p + base;
             aw.fallback_count = c->s->d_fallback_count.p + 6;   // zeroed by nw_band_classify
             HIP_OR_FAIL(c, nw::launch_band(nw::kWideDiags, aw, c->wide_fill, c->wide_walk, c->cs, nullptr));
+            tmark(c, "wide");
             a.work_list = aw.fallback_list;
             a.work_count = aw.fallback_count;
             a.redo_direct = 0;
         }
         HIP_OR_FAIL(c, launch_work(c, a));
+        tmark(c, "exact");
         return NW_OK;
     }
     HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs));
@@ -1213,6 +1243,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
                                           c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
                                           c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host));
+    tmark(c, "compact");
     return NW_OK;
 }
 
@@ -1727,10 +1758,31 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         for (auto it = tail.rbegin(); it != tail.rend(); ++it) v.push_back(*it);
         return v;
     };
+    std::vector<int64_t> ramp;   // CRISPR_NW_RAMP=a,b,c (diagnostics): explicit chunk sizes of a one-group call
+    if (const char* e = std::getenv("CRISPR_NW_RAMP")) {
+        for (const char* p = e; *p;) {
+            char* q = nullptr;
+            const long long v = std::strtoll(p, &q, 10);
+            if (q == p) break;
+            if (v > 0) ramp.push_back(v);
+            p = *q ? q + 1 : q;
+        }
+    }
     for (int g = 0; g < ngroups; ++g) {
         const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
         int64_t lo = g0;
-        for (int64_t len : sizes(g1 - g0)) {
+        std::vector<int64_t> sz = sizes(g1 - g0);
+        if (!groups && !ramp.empty()) {
+            sz.clear();
+            int64_t left = g1 - g0;
+            for (size_t i = 0; left > 0; ++i) {
+                const int64_t v = i < ramp.size() ? std::min(ramp[i], left) : std::min(chunk, left);
+                sz.push_back(v);
+                left -= v;
+            }
+            chunk = std::max(chunk, *std::max_element(sz.begin(), sz.end()));
+        }
+        for (int64_t len : sz) {
             if (len <= 0) continue;
             chunks.push_back({lo, lo + len, g});
             lo += len;
@@ -1749,6 +1801,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->diag_off = false;
         c->diag_tail = false;
         c->exact_small = false;
+        c->l2_skip = false;
+        c->trace_on = false;
         c->pkc = nw::KernelArgs{};
         c->out_mode = mode_before;
         c->n = 0;
@@ -2034,9 +2088,22 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // after the call's last kernel (2.31 -> 2.27 ms per 1M-read call)
     const bool direct_out = nchunks >= 1 && host_mapped(stats) && host_mapped(ops_off) &&
                             (!ops_out || host_mapped(ops_out));
+    // diagnostics / A-B knobs of the call (CRISPR_NW_L2SKIP, CRISPR_NW_SPIN)
+    const char* l2e = std::getenv("CRISPR_NW_L2SKIP");
+    const bool l2_skip_on = l2e && std::strcmp(l2e, "1") == 0;
+    int nosplit_last = 0;
+    if (const char* e = std::getenv("CRISPR_NW_NOSPLIT_LAST")) nosplit_last = std::atoi(e);
+    const char* spe = std::getenv("CRISPR_NW_SPIN");
+    const bool spin = spe && std::strcmp(spe, "1") == 0;
     std::vector<char> direct_done((size_t)std::max<int64_t>(nchunks, 1), 0);
     auto copy_runs = [&](int64_t k) -> int {
         ht.lap(4);
+        if (spin) {
+            hipError_t q;
+            while ((q = hipEventQuery(c->ev_ce[(size_t)k])) == hipErrorNotReady) {
+            }
+            HIP_OR_FAIL(c, q);
+        }
         HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
         ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
@@ -2053,6 +2120,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
+    int trace_chunks = 0;
+    if (const char* e = std::getenv("CRISPR_NW_TRACE")) trace_chunks = std::atoi(e);
+    c->trace_used = 0;
     const int64_t lag = std::max(1, nsets - 1);
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
@@ -2073,7 +2143,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->cs = c->cstream[k % nsets];
         if (tail_split) {
             c->cs = c->cstream[k % 2];
-            c->split_to = c->cstream[2];
+            // the last chunks keep their tail on their own compute stream (no later chunk's bulk
+            // queues behind it there): their tails overlap instead of queueing on the tail stream
+            c->split_to = k >= nchunks - nosplit_last ? nullptr : c->cstream[2];
             c->split_ev = c->ev_bulk[(size_t)k];
             // the set's previous chunk (k - 3) must be through its tail
             if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));
@@ -2141,6 +2213,16 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
+        // no second-level launches while the newest chunk read back needed none (its redo list
+        // went to the wide level: direct hand-off); the wide level then takes the whole redo
+        // list (what its region cannot hold goes on to the exact kernel)
+        c->l2_skip = false;
+        if (l2_skip_on && k >= lag + 1) {
+            const int64_t j = k - lag - 1;
+            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
+            const int64_t l2 = h[5] - (j > 0 ? c->h_ctl[nw::kOpsCtl * (j - 1) + 5] : 0);
+            c->l2_skip = !one_level[(size_t)j] && !c->skip16 && l2 == 0;
+        }
         // the exact kernel's grid: small while the newest chunk read back sent it few reads
         // (after the wide level it gets the rare read no band certifies)
         c->exact_small = true;
@@ -2169,6 +2251,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                 c->diag_off = (k & 3) != 0;
             }
         }
+        // diagnostics: the last chunks' launches
+        c->trace_on = trace_chunks > 0 && k >= nchunks - trace_chunks;
+        c->trace_chunk = (int)k;
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         nw::OpsHostOut ho{};
         const bool direct_k = direct_out && k == nchunks - 1;
@@ -2204,6 +2289,12 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k)
         if ((rc = copy_runs(k))) return restore(rc);
     ht.lap(4);
+    if (spin) {
+        hipError_t q;
+        while ((q = hipEventQuery(c->ev_out[(size_t)(nchunks - 1)])) == hipErrorNotReady) {
+        }
+        HIP_OR_FAIL(c, q);
+    }
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);
     ops_off[n] = total;
@@ -2228,6 +2319,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
             c->ops_compute_ms += ms;
         }
+        for (size_t i = 0; i < c->trace_used; ++i) {
+            float t = 0;
+            (void)hipEventElapsedTime(&t, c->ev_h0, c->trace_ev[i].second);
+            std::fprintf(stderr, "  trace chunk %s: %.1f us\n", c->trace_ev[i].first.c_str(), 1e3 * t);
+        }
+        c->trace_on = false;
+        c->trace_used = 0;
         if (ht.on)   // per chunk (ms from the first upload): upload done, compute start, compute end
             for (int64_t k = 0; k < nchunks; ++k) {
                 float a = 0, b = 0, e = 0;
@@ -2443,6 +2541,12 @@ int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d
 }
 
 int nw_host_threads(void) { return nw_host::Pool::get().threads(); }
+
+int nw_batch_set_lane_walk(nw_ctx* c, int on) {
+    if (!c) return NW_E_INVALID;
+    c->lane_walk = on != 0;
+    return NW_OK;
+}
 
 int nw_host_alloc(int64_t bytes, void** out) {
     if (!out || bytes < 0) return NW_E_INVALID;

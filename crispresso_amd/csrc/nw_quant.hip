@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +57,8 @@ struct QArgs {
     int4* out;
     uint32_t* partial;       // [gridDim.x][nwords]
     const int32_t* prefix;   // [3][LEN + 1] prefix counts of INC / EXON / SPL, then [LEN] table bytes
+    const int32_t* list;     // reads to process (quant_lanes' fallback list), or null: reads [0, n)
+    const int32_t* list_count;
     int32_t LEN, H, run_cap, window, nwords, wave_words, base_words;
     uint32_t flags;
 };
@@ -128,11 +131,14 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
     // Reads go to waves in groups of 64: one coalesced load of the flags and
     // lengths, one coalesced store of the results; rows of the next read to
     // process are loaded while the current one is worked on.
-    const int64_t ngroups = (a.n + 63) >> 6;
+    const int64_t n_eff = a.list ? (int64_t)*a.list_count : a.n;
+    const int64_t ngroups = (n_eff + 63) >> 6;
     const int64_t tw = (int64_t)gridDim.x * wpb;
     for (int64_t grp = (int64_t)blockIdx.x * wpb + wave; grp < ngroups; grp += tw) {
-        const int64_t idx = (grp << 6) + lane;
-        const bool valid = idx < a.n;
+        const int64_t pos = (grp << 6) + lane;
+        const bool valid = pos < n_eff;
+        const int32_t ridx = valid ? (a.list ? a.list[pos] : (int32_t)pos) : 0;
+        const int64_t idx = ridx;
         const unsigned mypre = valid ? (unsigned)a.pre[idx] : (unsigned)NWQ_PRE_UNMODIFIED;
         const int mylen = valid ? a.len[idx * a.len_stride] : 1;
         const bool skip = (mypre & NWQ_PRE_UNMODIFIED) && !nfix;
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
         int4 myout = make_int4((!skip && badlen) ? -1 : 0, 0, 0, 0);
         unsigned long long todo = ballot(!skip && !badlen);
 
-        auto row_ptr = [&](int k) { return a.aln + ((grp << 6) + k) * 3 * stride; };
+        auto row_ptr = [&](int k) { return a.aln + (int64_t)__builtin_amdgcn_readlane(ridx, k) * 3 * stride; };
         auto load3 = [&](int k, int L, int c0, uint32_t& dr, uint32_t& dm, uint32_t& ds) {
             dr = dm = ds = 0;
             if (c0 < L) {
@@ -429,11 +435,14 @@ __global__ __launch_bounds__(256) void expand_rows(const uint32_t* __restrict__ 
                                                    const int32_t* stats, const uint8_t* reads, const int64_t* offsets,
                                                    int64_t bias, const uint8_t* amp, const uint32_t* rowpos,
                                                    const uint8_t* lut, int La, const uint8_t* pre, int all, int64_t n,
-                                                   uint8_t* aln, int64_t stride) {
+                                                   uint8_t* aln, int64_t stride, const int32_t* list,
+                                                   const int32_t* list_count) {
     extern __shared__ uint8_t ex_sm[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     uint8_t* rows = ex_sm + (size_t)wave * 3 * stride;
-    for (int64_t r = (int64_t)blockIdx.x * wpb + wave; r < n; r += (int64_t)gridDim.x * wpb) {
+    const int64_t n_eff = list ? (int64_t)*list_count : n;   // list: quant_lanes' fallback reads
+    for (int64_t i = (int64_t)blockIdx.x * wpb + wave; i < n_eff; i += (int64_t)gridDim.x * wpb) {
+        const int64_t r = list ? (int64_t)list[i] : i;
         const int L = __builtin_amdgcn_readfirstlane(stats[r * 8]);   // aln_len
         const unsigned pf = (unsigned)__builtin_amdgcn_readfirstlane((int)pre[r]);
         if (L <= 0 || L > stride || (!all && (pf & NWQ_PRE_UNMODIFIED))) continue;
@@ -481,6 +490,366 @@ __global__ __launch_bounds__(256) void expand_rows(const uint32_t* __restrict__ 
         }
         nw::lds_fence();
     }
+}
+
+// ---------------------------------------------------------------------------
+// quant_lanes: process_df_chunk straight from the aligner's traceback runs, one LANE per read.
+//
+// The row kernels above rebuild three rows per read (3 * aln_len bytes written to HBM and read
+// back) and then find the '.' / '-' runs of the rows with a wave per read.  The runs already
+// are those features: a Y run is a run of '-' in align_seq (a deletion, CORE:496-502), an X run
+// a run of '-' in ref_seq (an insertion, CORE:509-526), and the '.' columns of align_str (the
+// substitutions, CORE:486-492) are the non-identical, non-positive pairs of the M runs -- of
+// which the record says how many there are: M columns - n_ident (M = La + Lb - aln_len), so an
+// M run is scanned (4 columns per step against the amplicon in LDS) only while some are left.
+// compute_ref_positions (CORE:2055-2067) of an amplicon made of A C G T is the amplicon index
+// of every M / Y column; an insertion's flanks are the columns either side (CORE:520-526, with
+// its -1 / -idx at the ends).  Each lane then classifies its read and applies the window and
+// frameshift rules exactly as quant_kernel does (same flags, same quirks), and adds its
+// positions to the block's vectors once per distinct position (numpy's buffered
+// `vec[idx] += 1`): substitution and deletion positions are distinct amplicon bases, insertion
+// flanks are deduplicated against them and each other.
+//
+// Scope: an amplicon of A C G T only, no N rule (amplicon_has_n); everything else of the read
+// is handled except a '-' byte in the read (RC-retry input, CORE:1846: it makes a '-' column
+// of align_seq inside an M or X run) and more than kQS / kQD / kQI substitutions / deletions /
+// insertions: such a read goes to the fallback list, which expand_rows + quant_kernel process
+// after this kernel (the same results, by the row path).
+constexpr int kQS = 16, kQD = 4, kQI = 4;   // per-lane list capacities (LDS, [cap][64] per wave)
+constexpr int kQWaveWords = kQS * 64 / 2 + (kQD + kQI) * 64 * 2;
+
+struct LArgs {
+    const uint32_t* ops;
+    const int64_t* ops_off;
+    const int32_t* stats;     // nw_stat records (8 ints): aln_len, n_ident, ...
+    const uint8_t* reads;
+    const int64_t* offsets;
+    int64_t bias;
+    const uint8_t* amp;       // the amplicon (global; staged into LDS)
+    const uint32_t* rowpos;   // per amplicon position: EDNAFULL codes scoring > 0 against it (':' test)
+    const uint8_t* lut;       // ascii -> EDNAFULL code
+    const uint8_t* pre;
+    int64_t n;
+    int64_t stride;           // the rows' stride of the row path (aln_len above it: cls -1, as there)
+    int4* out;
+    uint32_t* partial;        // [gridDim.x][nwords]
+    const int32_t* prefix;
+    int32_t* fb_list;         // reads this kernel leaves to the row path
+    int32_t* fb_count;
+    int32_t LEN, H, window, nwords, base_words, amp_words;
+    uint32_t flags;
+};
+
+__global__ __launch_bounds__(256) void quant_lanes(const LArgs a) {
+    extern __shared__ uint32_t smem[];
+    const int LEN = a.LEN;
+    uint32_t* blk = smem;
+    int32_t* incp = (int32_t*)(blk + a.nwords);
+    int32_t* exop = incp + (LEN + 1);
+    int32_t* splp = exop + (LEN + 1);
+    uint8_t* tbl = (uint8_t*)(splp + (LEN + 1));
+    uint32_t* amp32 = smem + a.base_words;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wpb = blockDim.x >> 6;
+    uint16_t* subl = (uint16_t*)(amp32 + a.amp_words + wave * kQWaveWords);   // [kQS][64]
+    uint2* dell = (uint2*)(subl + kQS * 64);                                    // [kQD][64]
+    uint2* insl = dell + kQD * 64;                                              // [kQI][64]
+
+    for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) blk[i] = 0;
+    const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
+    for (int i = threadIdx.x; i < pref_words; i += blockDim.x) incp[i] = a.prefix[i];
+    for (int i = threadIdx.x; i < a.amp_words; i += blockDim.x) {
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b)
+            if (4 * i + b < LEN) w |= (uint32_t)a.amp[4 * i + b] << (8 * b);
+        amp32[i] = w;
+    }
+    __syncthreads();
+
+    const unsigned flags = a.flags;
+    const bool hide = flags & F_HIDE;
+    const bool ign_sub = flags & F_IGN_SUB, ign_ins = flags & F_IGN_INS, ign_del = flags & F_IGN_DEL;
+    uint32_t* ctr = blk + NV * LEN;
+    uint32_t* hin = ctr + 4;
+    uint32_t* hfs = hin + a.H;
+
+    const int64_t ngroups = (a.n + 63) >> 6;
+    const int64_t tw = (int64_t)gridDim.x * wpb;
+    for (int64_t grp = (int64_t)blockIdx.x * wpb + wave; grp < ngroups; grp += tw) {
+        const int64_t r = (grp << 6) + lane;
+        const bool valid = r < a.n;
+        const unsigned pre = valid ? (unsigned)a.pre[r] : (unsigned)NWQ_PRE_UNMODIFIED;
+        const int L = valid ? a.stats[r * 8] : 1;
+        const bool skip = pre & NWQ_PRE_UNMODIFIED;
+        const bool badlen = L <= 0 || L > a.stride;
+        int4 res = make_int4((!skip && badlen) ? -1 : 0, 0, 0, 0);
+        const bool act = valid && !skip && !badlen;
+        bool fb = false, bad = false;
+        int nsub = 0, nsubi = 0, nd = 0, ni = 0;
+        unsigned subbits = 0;   // 1 exon, 2 splice, 4 exon & include, 8 splice & include
+        if (act) {
+            const int nid = a.stats[r * 8 + 1];
+            const int64_t k0 = a.ops_off[r], k1 = a.ops_off[r + 1];
+            const int64_t o0 = a.offsets[r];
+            const int Lb = (int)(a.offsets[r + 1] - o0);
+            const uint8_t* R = a.reads + (o0 - a.bias);
+            int left = LEN + Lb - L - nid;   // non-identical M columns
+            fb = left < 0;
+            int col = 0, ia = 0, jb = 0, ctype = -1, clen = 0;
+            for (int64_t k = k0; k <= k1 && !fb && !bad; ++k) {
+                int t = -2, l = 0;
+                if (k < k1) {
+                    const uint32_t op = a.ops[k];
+                    t = (int)(op >> 28);
+                    l = (int)(op & 0x0fffffffu);
+                }
+                if (t == ctype) {   // consecutive runs of one type: one column run
+                    clen += l;
+                    continue;
+                }
+                if (ctype == 0) {   // M: the '.' columns among the non-identical ones
+                    if (ia + clen > LEN) {
+                        bad = true;
+                    } else if (left > 0) {
+                        const uintptr_t ra = (uintptr_t)(R + jb);
+                        const uint32_t* rw = (const uint32_t*)(ra & ~(uintptr_t)3);
+                        const int rsh = (int)(ra & 3), ash = ia & 3;
+                        const uint32_t* aw = amp32 + (ia >> 2);
+                        uint32_t rlo = rw[0], alo = aw[0];
+                        for (int p = 0, q = 0; p < clen && left > 0; p += 4, ++q) {
+                            const uint32_t rhi = rw[q + 1], ahi = aw[q + 1];
+                            const uint32_t rv = __builtin_amdgcn_alignbyte(rhi, rlo, rsh);
+                            const uint32_t av = __builtin_amdgcn_alignbyte(ahi, alo, ash);
+                            rlo = rhi;
+                            alo = ahi;
+                            uint32_t x = rv ^ av;
+                            if (clen - p < 4) x &= (1u << (8 * (clen - p))) - 1u;
+                            while (x) {
+                                const int b = __builtin_ctz(x) >> 3;
+                                x &= ~(255u << (8 * b));
+                                const unsigned cb = (rv >> (8 * b)) & 255u, ca = (av >> (8 * b)) & 255u;
+                                if (cb == '-') {   // a '-' byte of the read: a deletion column of align_seq
+                                    fb = true;
+                                    break;
+                                }
+                                if ((cb ^ ca) == 0x20u && cb >= 'a' && cb <= 'z') continue;   // '|' (case)
+                                --left;
+                                const int qp = ia + p + b;
+                                if ((a.rowpos[qp] >> a.lut[cb]) & 1u) continue;   // ':'
+                                if (ign_sub) continue;
+                                if (nsub >= kQS) {
+                                    fb = true;
+                                    break;
+                                }
+                                subl[nsub * 64 + lane] = (uint16_t)qp;
+                                ++nsub;
+                                const unsigned tb = tbl[qp];
+                                nsubi += tb & T_INC;
+                                subbits |= ((tb & T_EXON) ? 1u : 0u) | ((tb & T_SPL) ? 2u : 0u);
+                                if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
+                            }
+                            if (fb) break;
+                        }
+                    }
+                    col += clen;
+                    ia += clen;
+                    jb += clen;
+                } else if (ctype == 2) {   // Y: a deletion (its amplicon positions)
+                    if (ia + clen > LEN) {
+                        bad = true;
+                    } else if (!ign_del) {
+                        if (nd >= kQD) {
+                            fb = true;
+                        } else {
+                            const int e = ia + clen;
+                            const unsigned f = (incp[e] - incp[ia] > 0 ? R_INC : 0) | (splp[e] - splp[ia] > 0 ? R_SPL : 0);
+                            dell[nd * 64 + lane] = make_uint2((unsigned)ia | ((unsigned)clen << 16),
+                                                              f | ((unsigned)(exop[e] - exop[ia]) << 16));
+                            ++nd;
+                        }
+                    }
+                    col += clen;
+                    ia += clen;
+                } else if (ctype == 1) {   // X: an insertion (its flanking reference positions)
+                    for (int p = 0; p < clen && !fb; ++p) fb = R[jb + p] == '-';
+                    if (!ign_ins && !fb) {
+                        if (ni >= kQI) {
+                            fb = true;
+                        } else {
+                            const int fa = col > 0 ? ia - 1 : -1;
+                            const int fbk = col + clen < L ? ia : (ia > 0 ? -ia : -1);
+                            unsigned f = 0;   // T_* and R_INC / R_EXON / R_SPL share bit positions
+                            if (fa >= 0 && fa < LEN) f |= tbl[fa];
+                            if (fbk >= 0 && fbk < LEN) f |= tbl[fbk];
+                            insl[ni * 64 + lane] = make_uint2(((unsigned)fa & 0xffffu) | ((unsigned)fbk << 16),
+                                                              (unsigned)clen | (f << 24));
+                            ++ni;
+                        }
+                    }
+                    col += clen;
+                    jb += clen;
+                } else if (ctype >= 3) {
+                    fb = true;
+                }
+                ctype = t;
+                clen = l;
+            }
+            if (!fb && !bad && (col != L || jb != Lb)) fb = true;
+            if (!fb && !bad && ia != LEN) bad = true;
+            if (bad) res = make_int4(-1, 0, 0, 0);
+        }
+        // the reads left to the row path: one atomic per wave
+        {
+            const unsigned long long fbm = ballot(fb);
+            if (fbm) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(a.fb_count, __popcll(fbm));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (fb) a.fb_list[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fbm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)fbm, 0u))] = (int32_t)r;
+            }
+        }
+        if (act && !fb && !bad) {
+            // classification (CORE:530-575)
+            bool hit = nsubi > 0;
+            for (int j = 0; j < nd; ++j) hit |= (dell[j * 64 + lane].y & R_INC) != 0;
+            for (int j = 0; j < ni; ++j) hit |= ((insl[j * 64 + lane].y >> 24) & R_INC) != 0;
+            const int cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
+            const bool windowed = cls == 1 && a.window != 0;
+            // NHEJ window filter (CORE:611-641): deletion_positions_flat is recomputed only when
+            // a deletion survives the filter
+            bool anykept = false;
+            for (int j = 0; j < nd; ++j) anykept |= !windowed || (dell[j * 64 + lane].y & R_INC);
+            const bool post_sel = windowed && anykept;
+            int ndel = 0, exdel = 0;
+            bool spldel = false;
+            for (int j = 0; j < nd; ++j) {
+                uint2 d = dell[j * 64 + lane];
+                const bool kept = !windowed || (d.y & R_INC);
+                const bool post = post_sel ? kept : true;
+                d.y |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
+                dell[j * 64 + lane] = d;
+                ndel += kept ? (int)(d.x >> 16) : 0;
+                exdel += post ? (int)(d.y >> 16) : 0;
+                spldel |= post && (d.y & R_SPL);
+            }
+            int nins = 0, insex_len = 0;
+            bool insex = false, insspl = false;
+            for (int j = 0; j < ni; ++j) {
+                const uint2 e = insl[j * 64 + lane];
+                const int fa = (int)(short)(e.x & 0xffffu), fbk = (int)(short)(e.x >> 16);
+                const int sz = (int)(e.y & 0xffffffu);
+                const unsigned f = e.y >> 24;
+                const bool kept = !windowed || (f & R_INC);
+                insspl |= (f & R_SPL) != 0;
+                if (kept) {
+                    nins += sz;
+                    if (f & R_EXON) {
+                        insex = true;
+                        insex_len += sz;
+                    }
+                    if (cls != 0) {
+                        const int wa = fa < 0 ? fa + LEN : fa, wb = fbk < 0 ? fbk + LEN : fbk;
+                        atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)sz);
+                        if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)sz);
+                    }
+                }
+            }
+            const int n_mut = windowed ? nsubi : nsub;
+            bool noncoding = false;
+            if ((flags & F_FRAMESHIFT) && cls != 0) {   // CORE:653-725
+                const bool sub_exon = windowed ? (subbits & 4u) : (subbits & 1u);
+                const bool sub_spl = windowed ? (subbits & 8u) : (subbits & 2u);
+                const int eff = insex_len - exdel;
+                const bool exon_mod = insex || exdel > 0 || sub_exon;
+                const bool has_lens = insex || exdel > 0;
+                if (sub_spl || spldel || insspl) atomicAdd(ctr + C_SPLICE, 1u);
+                if (exon_mod) {
+                    if (!has_lens) {
+                        atomicAdd(ctr + C_NONFS, 1u);
+                        atomicAdd(hin + LEN, 1u);
+                    } else if (eff % 3 == 0) {
+                        atomicAdd(ctr + C_NONFS, 1u);
+                        atomicAdd(hin + LEN + eff, 1u);
+                    } else {
+                        atomicAdd(ctr + C_FS, 1u);
+                        atomicAdd(hfs + LEN + eff, 1u);
+                    }
+                } else {
+                    atomicAdd(ctr + C_NONMOD, 1u);
+                }
+                noncoding = !exon_mod;
+            }
+            res = cls ? make_int4(cls, n_mut, nins, ndel) : make_int4(0, 0, 0, 0);
+
+            // the read's vector increments, once per distinct position
+            auto is_flank = [&](int p) {
+                for (int j = 0; j < ni; ++j) {
+                    const unsigned x = insl[j * 64 + lane].x;
+                    const int fa = (int)(short)(x & 0xffffu), fbk = (int)(short)(x >> 16);
+                    if ((fa < 0 ? fa + LEN : fa) == p || (fbk < 0 ? fbk + LEN : fbk) == p) return true;
+                }
+                return false;
+            };
+            auto incr = [&](int p, unsigned sub, unsigned del, unsigned ins, unsigned sub_post, unsigned del_post,
+                            unsigned dsz, bool kept) {
+                uint32_t* h = blk + p;
+                if (cls == 3) {
+                    vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
+                } else if (cls == 2) {
+                    vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
+                } else if (cls == 1) {
+                    vadd(h, V_MUT, LEN, hide ? sub_post : sub);
+                    vadd(h, V_DEL, LEN, hide ? del_post : del);
+                    vadd(h, V_INS, LEN, ins);
+                }
+                vadd(h, V_ANY, LEN, 1u);
+                if (noncoding) {
+                    vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
+                }
+                if (cls != 0 && del && kept) vadd(h, V_AVG_DEL, LEN, dsz);
+            };
+            for (int j = 0; j < nsub; ++j) {
+                const int p = subl[j * 64 + lane];
+                const unsigned sp = (!windowed || (tbl[p] & T_INC)) ? 1u : 0u;
+                incr(p, 1u, 0u, is_flank(p) ? 1u : 0u, sp, 0u, 0u, false);
+            }
+            for (int j = 0; j < nd; ++j) {
+                const uint2 d = dell[j * 64 + lane];
+                const int s = (int)(d.x & 0xffffu), sz = (int)(d.x >> 16);
+                const unsigned dp = (d.y & R_POST) ? 1u : 0u;
+                const bool kept = d.y & R_KEPT;
+                for (int p = s; p < s + sz; ++p) incr(p, 0u, 1u, (ni && is_flank(p)) ? 1u : 0u, 0u, dp, (unsigned)sz, kept);
+            }
+            for (int j = 0; j < ni; ++j) {
+                const unsigned x = insl[j * 64 + lane].x;
+                const int fa = (int)(short)(x & 0xffffu), fbk = (int)(short)(x >> 16);
+                const int w2[2] = {fa < 0 ? fa + LEN : fa, fbk < 0 ? fbk + LEN : fbk};
+                for (int h = 0; h < 2; ++h) {
+                    const int w = w2[h];
+                    if (h == 1 && w == w2[0]) continue;
+                    bool seen = false;
+                    for (int jj = 0; jj < j && !seen; ++jj) {
+                        const unsigned xx = insl[jj * 64 + lane].x;
+                        const int ga = (int)(short)(xx & 0xffffu), gb = (int)(short)(xx >> 16);
+                        seen = (ga < 0 ? ga + LEN : ga) == w || (gb < 0 ? gb + LEN : gb) == w;
+                    }
+                    for (int q = 0; q < nsub && !seen; ++q) seen = subl[q * 64 + lane] == w;
+                    for (int q = 0; q < nd && !seen; ++q) {
+                        const unsigned dx = dell[q * 64 + lane].x;
+                        seen = w >= (int)(dx & 0xffffu) && w < (int)(dx & 0xffffu) + (int)(dx >> 16);
+                    }
+                    if (!seen) incr(w, 0u, 0u, 1u, 0u, 0u, 0u, false);
+                }
+            }
+        }
+        if (valid && !fb) a.out[r] = res;
+    }
+
+    __syncthreads();
+    uint32_t* dst = a.partial + (int64_t)blockIdx.x * a.nwords;
+    for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) dst[i] = blk[i];
 }
 
 __global__ void quant_reduce(const uint32_t* __restrict__ partial, int nblocks, int nwords, int slice,
@@ -545,6 +914,8 @@ struct nwq_ctx {
     QBuf<uint8_t> d_amp, d_lut;
     QBuf<uint32_t> d_rowpos;
     std::string amp_key;
+    QBuf<int32_t> d_fb;      // quant_lanes' fallback list [n] + its count
+    bool rows_only = false;  // CRISPR_NWQ_ROWS=1: every read through the rows (A/B, tests)
 };
 
 namespace {
@@ -600,9 +971,13 @@ int geometry(nwq_ctx* c, int64_t stride, int64_t n, QGeom* g) {
     return NW_OK;
 }
 
+// The row kernel (quant_kernel) over reads [0, n), or over a device work list (list /
+// list_count: quant_lanes' fallback reads, `slabs0` block slabs of that kernel already at the
+// start of d_partial), then the slabs' sum into the totals.
 int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, int64_t len_stride,
              const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms,
-             bool started = false) {
+             bool started = false, const int32_t* list = nullptr, const int32_t* list_count = nullptr,
+             int slabs0 = 0) {
     if (!c->have_params) return qfail(c, NW_E_STATE, "nwq_set_params not called");
     if (stride <= 0 || (stride & 3) || stride >= 32768)
         return qfail(c, NW_E_INVALID, "stride %lld must be a positive multiple of 4 below 32768", (long long)stride);
@@ -610,7 +985,8 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
     QGeom g;
     int rc = geometry(c, stride, n, &g);
     if (rc) return rc;
-    QHIP(c, c->d_partial.reserve((size_t)g.grid * g.nwords));
+    if (list) g.grid = std::min(g.grid, c->num_cus);   // a short list (usually empty): a small grid
+    QHIP(c, c->d_partial.reserve((size_t)(slabs0 + g.grid) * g.nwords));
     QHIP(c, c->d_totals.reserve((size_t)g.nwords));
     nwq::QArgs a;
     a.aln = d_aln;
@@ -620,8 +996,10 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
     a.pre = d_pre;
     a.n = n;
     a.out = reinterpret_cast<int4*>(d_out);
-    a.partial = c->d_partial.p;
+    a.partial = c->d_partial.p + (size_t)slabs0 * g.nwords;
     a.prefix = c->d_prefix.p;
+    a.list = list;
+    a.list_count = list_count;
     a.LEN = c->LEN;
     a.H = (int)hist_size(c->LEN, stride);
     a.run_cap = g.run_cap;
@@ -633,10 +1011,11 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
     if (!started) QHIP(c, hipEventRecord(c->ev0, c->stream));   // (the row expansion records it first)
     hipLaunchKernelGGL(nwq::quant_kernel, dim3(g.grid), dim3(64 * g.wpb), g.lds, c->stream, a);
     QHIP(c, hipGetLastError());
-    const int slices = std::min(g.grid, 32), slice = (g.grid + slices - 1) / slices;
+    const int nslabs = slabs0 + g.grid;
+    const int slices = std::min(nslabs, 32), slice = (nslabs + slices - 1) / slices;
     QHIP(c, hipMemsetAsync(c->d_totals.p, 0, sizeof(int64_t) * (size_t)g.nwords, c->stream));
     hipLaunchKernelGGL(nwq::quant_reduce, dim3((g.nwords + 255) / 256, slices), dim3(256), 0, c->stream,
-                       c->d_partial.p, g.grid, g.nwords, slice, reinterpret_cast<unsigned long long*>(c->d_totals.p));
+                       c->d_partial.p, nslabs, g.nwords, slice, reinterpret_cast<unsigned long long*>(c->d_totals.p));
     QHIP(c, hipGetLastError());
     QHIP(c, hipEventRecord(c->ev1, c->stream));
     QHIP(c, hipMemcpyAsync(totals, c->d_totals.p, sizeof(int64_t) * (size_t)g.nwords, hipMemcpyDeviceToHost,
@@ -664,6 +1043,7 @@ int nwq_create(int device, nwq_ctx** out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (const char* e = std::getenv("CRISPR_NWQ_ROWS")) c->rows_only = std::strcmp(e, "1") == 0;
     *out = c;
     return NW_OK;
 }
@@ -681,6 +1061,7 @@ void nwq_destroy(nwq_ctx* c) {
     c->d_amp.release();
     c->d_lut.release();
     c->d_rowpos.release();
+    c->d_fb.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -798,7 +1179,73 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
     }
     const size_t nn = (size_t)std::max<int64_t>(n, 1);
     QHIP(c, c->d_aln.reserve(nn * 3 * (size_t)stride));
+    // the lane path (quant_lanes: features straight from the runs) for an amplicon of A C G T
+    // without the N rule, when its LDS fits; its fallback reads (and every read otherwise) go
+    // through the rows rebuilt on the device
+    bool acgt = true;
+    for (int i = 0; i < amplicon_len && acgt; ++i)
+        acgt = amplicon[i] == 'A' || amplicon[i] == 'C' || amplicon[i] == 'G' || amplicon[i] == 'T';
+    const int LEN = c->LEN;
+    const int nwords = (int)words_for(LEN, stride);
+    const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
+    const int base_words = nwords + pref_words;
+    const int amp_words = (LEN + 3) / 4 + 2;
+    int lane_wpb = 4;
+    while (lane_wpb > 1 && 4 * (base_words + amp_words + lane_wpb * nwq::kQWaveWords) > kMaxLds / 2) lane_wpb >>= 1;
+    const int lane_lds = 4 * (base_words + amp_words + lane_wpb * nwq::kQWaveWords);
+    const bool lanes = acgt && !(c->flags & nwq::F_NFIX) && lane_lds <= kMaxLds && n > 0 && !c->rows_only;
     QHIP(c, hipEventRecord(c->ev0, c->stream));   // kernel_ms covers the expansion too
+    if (lanes) {
+        int per_cu = 0;
+        QHIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwq::quant_lanes, 64 * lane_wpb, lane_lds));
+        per_cu = std::max(per_cu, 1);
+        const int64_t groups = (n + 63) / 64;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((groups + lane_wpb - 1) / lane_wpb,
+                                                                     (int64_t)c->num_cus * per_cu));
+        QHIP(c, c->d_fb.reserve(nn + 1));
+        // every slab up front: the row kernel's list grid is at most num_cus (run_impl), and a
+        // reserve there would move the slabs this kernel is about to write
+        QHIP(c, c->d_partial.reserve((size_t)(grid + c->num_cus) * nwords));
+        QHIP(c, hipMemsetAsync(c->d_fb.p + nn, 0, sizeof(int32_t), c->stream));
+        nwq::LArgs la;
+        la.ops = d_ops;
+        la.ops_off = d_ops_off;
+        la.stats = (const int32_t*)d_stats;
+        la.reads = d_reads;
+        la.offsets = d_offsets;
+        la.bias = reads_bias;
+        la.amp = c->d_amp.p;
+        la.rowpos = c->d_rowpos.p;
+        la.lut = c->d_lut.p;
+        la.pre = d_pre;
+        la.n = n;
+        la.stride = stride;
+        la.out = reinterpret_cast<int4*>(d_out);
+        la.partial = c->d_partial.p;
+        la.prefix = c->d_prefix.p;
+        la.fb_list = c->d_fb.p;
+        la.fb_count = c->d_fb.p + nn;
+        la.LEN = LEN;
+        la.H = (int)hist_size(LEN, stride);
+        la.window = c->window;
+        la.nwords = nwords;
+        la.base_words = base_words;
+        la.amp_words = amp_words;
+        la.flags = c->flags;
+        hipLaunchKernelGGL(nwq::quant_lanes, dim3(grid), dim3(64 * lane_wpb), lane_lds, c->stream, la);
+        QHIP(c, hipGetLastError());
+        // the fallback reads: their rows, then the row kernel over the list
+        int wpb = 4;
+        while (wpb > 1 && (int64_t)wpb * 3 * stride > 64 * 1024) wpb >>= 1;
+        const int lds = (int)(wpb * 3 * stride);
+        if (lds > kMaxLds) return qfail(c, NW_E_UNSUPPORTED, "stride %lld too long for the row expansion", (long long)stride);
+        hipLaunchKernelGGL(nwq::expand_rows, dim3(c->num_cus), dim3(64 * wpb), lds, c->stream, d_ops, d_ops_off,
+                           (const int32_t*)d_stats, d_reads, d_offsets, reads_bias, c->d_amp.p, c->d_rowpos.p,
+                           c->d_lut.p, amplicon_len, d_pre, 0, n, c->d_aln.p, stride, c->d_fb.p, c->d_fb.p + nn);
+        QHIP(c, hipGetLastError());
+        return run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms, true,
+                        c->d_fb.p, c->d_fb.p + nn, grid);
+    }
     if (n > 0) {
         int wpb = 4;
         while (wpb > 1 && (int64_t)wpb * 3 * stride > 64 * 1024) wpb >>= 1;
@@ -808,7 +1255,7 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
         hipLaunchKernelGGL(nwq::expand_rows, dim3(grid), dim3(64 * wpb), lds, c->stream, d_ops, d_ops_off,
                            (const int32_t*)d_stats, d_reads, d_offsets, reads_bias, c->d_amp.p, c->d_rowpos.p,
                            c->d_lut.p, amplicon_len, d_pre, (int)((c->flags & nwq::F_NFIX) != 0), n, c->d_aln.p,
-                           stride);
+                           stride, nullptr, nullptr);
         QHIP(c, hipGetLastError());
     }
     // the records' aln_len, 8 ints apart (nw_stat)

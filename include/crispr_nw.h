@@ -285,6 +285,10 @@ int nw_host_unregister(void* p);
  * by the cgroup quota and divided by LOCAL_WORLD_SIZE (crispresso_amd/placement.py binds a
  * rank and sets the variable).  Creates the pool on first use. */
 int nw_host_threads(void);
+/* Resident passes (nw_batch_run_async) only: the first band level's lane walk and the stop
+ * summary its fill writes (on != 0), instead of the wave-per-read walk every pipelined call
+ * runs.  The bench times both; off by default. */
+int nw_batch_set_lane_walk(nw_ctx* ctx, int on);
 
 /* The three alignment rows of n reads from their runs (host, nthreads threads;
  * <= 0: all cores): for read r at aln_out + r*3*stride the aligned amplicon, the

@@ -1,5 +1,6 @@
-"""bench.py's host-side pieces (no GPU): the PMC traffic it reports comes from the
-newest committed rocprofv3 summary under profiles/ and covers the band path's kernels."""
+"""bench.py's host-side pieces (no GPU): the PMC traffic it reports comes from the committed
+rocprofv3 summaries of the TIMED CALL's kernels and of the quantification leg (per call), and
+records which library build they profiled."""
 import importlib.util
 import json
 import os
@@ -14,32 +15,35 @@ def load_bench():
     return mod
 
 
-def newest_summary(b):
-    return next(p for p in b.PMC_SUMMARIES if os.path.exists(p))
-
-
-def test_pmc_summaries_exist_and_newest_first():
+def test_call_pmc_summary_covers_the_calls_kernels():
     b = load_bench()
-    with open(newest_summary(b)) as f:
+    with open(b.CALL_PMC) as f:
         summ = json.load(f)
-    assert any("nw_band_fill<16" in k for k in summ)
-    assert any("nw_band_walk<16" in k for k in summ)   # <16> or <16, true> (the lane walk)
+    assert summ["_meta"]["calls"] and summ["_meta"]["lib_sha1"]
+    for k in ("nw_band_classify", "nw_band_segsort", "nw_band_fill<16, 1", "nw_band_walk<16", "nw_ops_compact"):
+        assert any(k in name for name in summ), k
+    cp = b.pmc_per_call(b.CALL_PMC, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
+    assert cp["traffic"] > 5e7 and cp["valu_fill16"] > 0   # ~0.1-1.5 GB per 1M C2 reads
 
 
-def test_band_traffic_from_committed_profile():
+def test_quant_pmc_summary():
     b = load_bench()
-    traffic, src = b.pmc_traffic("void nw::nw_band_", "nw::nw_band_", "void nw::nw_align_kernel",
-                                 required="nw::nw_band_fill<16")
-    assert traffic is not None and traffic > 5e8   # ~1-3 GB per 1M C2 reads
-    assert src == os.path.relpath(newest_summary(b), ROOT)
-    summ, src2 = b.pmc_summary("nw_band_fill<16")
-    assert src2 == src and any("SQ_INSTS_VALU" in v for v in summ.values())
+    qp = b.pmc_per_call(b.QUANT_PMC, lambda k: "nwq::" in k)
+    assert qp is not None and qp["traffic"] > 0
+    assert any("quant_lanes" in k for k in qp["kernels"])
 
 
-def test_quant_traffic_available():
+def test_pmc_per_call_sums_kernels(tmp_path):
     b = load_bench()
-    traffic, _ = b.pmc_traffic("nwq::quant_kernel", "nwq::quant_reduce")
-    assert traffic is not None and traffic > 0
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps({"_meta": {"calls": 4, "lib_sha1": "x"},
+                             "void nw::nw_band_fill<16, 1, false>(nw::KernelArgs)": {"hbm_bytes_per_call": 10.0,
+                                                                                    "valu_per_call": 7.0},
+                             "nw::nw_band_segsort(nw::KernelArgs, unsigned int)": {"hbm_bytes_per_call": 5.0},
+                             "nwq::quant_lanes(nwq::LArgs)": {"hbm_bytes_per_call": 100.0}}))
+    cp = b.pmc_per_call(str(p), lambda k: "nwq::" not in k)
+    assert cp["traffic"] == 15.0 and cp["valu_fill16"] == 7.0 and cp["calls_profiled"] == 4
+    assert cp["lib_matches_loaded"] in (False, None)
 
 
 def _bench_rank(rank, world, port, out_dir):

@@ -546,10 +546,11 @@ def test_packed_batch_upload_runs_the_call_kernels(gpu_aligner_factory, oracle):
 
 @pytest.mark.parametrize("kind", ["c2", "repeats"])
 def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, oracle, kind):
-    """A resident pass of 400k reads (one launch of >= 300k reads: the first level's lane walk,
-    nw_band_walk<16, true>, its fill's stop summary, and the lane-per-read classify compare) gives
-    the same records and runs as the pipelined call over the same batch (chunks of <= 262144
-    reads: the wave-per-read walk), every read; and a sample of both against the oracle.
+    """A resident pass of 400k reads with the lane walk on (nw_batch_set_lane_walk: the first
+    level's nw_band_walk<16, true> and its fill's stop summary), and one without (the call's own
+    kernels in one launch each), give the same records and runs as the pipelined call over the
+    same batch (the wave-per-read walk), every read; and every read of the lane-walk pass against
+    the oracle.
     "repeats": homopolymer and tandem-repeat runs in the amplicon (gap placement among equal
     scores, "M < max" bits off the path) and the parity mix (more indels, N codes)."""
     from crispresso_amd.aligner import pack_2bit
@@ -570,18 +571,20 @@ def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, or
     c_stats, c_off = call.stats.copy(), call.ops_off.copy()
     c_ops = call.ops[:int(c_off[n])].copy()
     a.upload_packed(pr)
-    a.run_async()
-    a.sync()
-    res = a.download_ops(n)
-    assert int(res.ops_off[n]) == int(c_off[n])
-    np.testing.assert_array_equal(res.ops_off, c_off)
-    for f in FIELDS:
-        np.testing.assert_array_equal(res.stats[f], c_stats[f], err_msg=f)
-    np.testing.assert_array_equal(res.ops[:int(c_off[n])], c_ops)
-    idx = np.arange(0, n, 997)
-    sub_buf, sub_off = pack_reads([bytes(buf[off[i]:off[i + 1]]).decode() for i in idx])
-    ob = a.align_ops(sub_buf, sub_off)
-    assert_same(oracle, amp, sub_buf, sub_off, ob.expand(amp, sub_buf, sub_off), "lane walk sample")
-    for j, i in enumerate(idx):   # the sample's records are the resident pass's
+    for lane_walk in (False, True):
+        a.set_lane_walk(lane_walk)
+        a.run_async()
+        a.sync()
+        res = a.download_ops(n)
+        assert int(res.ops_off[n]) == int(c_off[n])
+        np.testing.assert_array_equal(res.ops_off, c_off)
         for f in FIELDS:
-            assert ob.stats[f][j] == res.stats[f][i], (f, int(i))
+            np.testing.assert_array_equal(res.stats[f], c_stats[f], err_msg=f)
+        np.testing.assert_array_equal(res.ops[:int(c_off[n])], c_ops)
+    a.set_lane_walk(False)
+    # every read of the resident pass (the one the bench's roofline is quoted on) against the
+    # oracle: once per distinct read, duplicates against their first copy (tests/every_read.py)
+    from tests.every_read import every_read
+
+    chk = every_read(amp, buf, off, res, threads=16)
+    assert chk["mismatches"] == 0, chk
