@@ -417,8 +417,10 @@ def dual_leg(al, n_reads, steps, warmup, threads, sample_every):
 
     def step():
         al.set_reference(amp)
+        al.set_known(hdr)   # the HDR amplicon's copies: one alignment (needle.align_reads does the same)
         state["ob"] = al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
-        al.set_reference(hdr)
+        al.set_known(None)
+        al.set_reference(hdr)   # the resident pass: the reference amplicon's copies from one alignment
         al.align_ops(None, po.array, out=(stats2.array, None, ops_off2.array), resident=True, records_only=True)
 
     dt = timed_calls(None, step, steps, warmup, LEG_WARM_S) / steps

@@ -284,6 +284,12 @@ class GpuAligner:
             _lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,
             len(pr.exc_pos)), "nw_batch_upload_packed")
 
+    def set_known(self, seq: Optional[str]) -> None:
+        """nw_set_known: reads equal to `seq` take one alignment of it (the HDR amplicon during the
+        amplicon pass of the dual alignment); None clears it."""
+        b = (seq or "").encode("ascii")
+        self._check(self.lib.nw_set_known(self._h, b, len(b)), "nw_set_known")
+
     def set_lane_walk(self, on: bool) -> None:
         """Resident passes only: the first band level's lane walk + stop summary
         (nw_batch_set_lane_walk; no pipelined call runs it)."""

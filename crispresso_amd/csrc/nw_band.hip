@@ -251,6 +251,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     constexpr int kRbw = 66;               // a window read's 16-base words (Lb < La <= 1024) + a zero word
     __shared__ unsigned s_rbw[4][kRbw];
+    __shared__ unsigned s_known[18];       // the known sequence's 2-bit words (KernelArgs::known2; La <= 256)
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
     // here, the first kernel of the chain, instead of by memset launches
@@ -274,6 +275,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // (the byte-input launch sizes LDS for the amplicon dwords only: no window seeds there)
     const int img_words = PK ? a.cls_words : 2 * nd;
     for (int k = threadIdx.x; k < img_words; k += blockDim.x) amp_sh[k] = a.cls_img[k];
+    if (PK && a.known2 && threadIdx.x < 18) s_known[threadIdx.x] = threadIdx.x < (La + 15) / 16 ? a.known2[threadIdx.x] : 0u;
     __syncthreads();
     const int sc5 = a.band_maxsub / 5;
     // the one-substitution certificate (above): ops output, one 256-byte chunk, EDNAFULL's
@@ -358,6 +360,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         const long long r = r0 + lane;
         unsigned long long cand = __ballot(my_len == La && !exc);   // reads of the amplicon's length
         unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull;
+        unsigned long long known = 0ull;   // copies of the known sequence (KernelArgs::known2)
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
         // away from the words already in registers
@@ -441,6 +444,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         }
                     }
                     sub2 = __ballot(ok2);
+                }
+                if (a.known2) {   // a copy of the known sequence that no certificate above took
+                    int k2 = 0;
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) {
+                        if (t >= nw) continue;
+                        const unsigned x = rw[t] ^ s_known[t];
+                        k2 += __builtin_popcount((x | (x >> 1)) & vmask(t, La));
+                    }
+                    known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2);
                 }
             }
         }
@@ -655,7 +668,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         int32_t sinfo = 0;
         if constexpr (PK) {
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
-                !(((exact | sub1 | sub2 | win) >> lane) & 1ull)) {
+                !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull)) {
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
@@ -683,7 +696,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             if (a.seed_info && r < r_end) a.seed_info[r] = sinfo;
         }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2 | win) >> lane) & 1ull)
+            a.sort_key[r] = (((exact | sub1 | sub2 | win | known) >> lane) & 1ull)
                                 ? a.band_lb_cap + 2
                                 : (sinfo ? a.band_lb_cap + 3 +
                                                min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
@@ -700,6 +713,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             st[0] = make_int4(La, my_len - win_k, my_len - win_k, La - my_len);   // aln_len, n_ident, n_sim, n_gaps
             st[1] = make_int4(a.band_maxsub * (my_len - win_k) - win_k * 4 * sc5, win_s + my_len, my_len, 0);
         }
+        // a known copy: record and runs from the known alignment, by the compaction
+        if (a.ops && r < r_end && ((known >> lane) & 1ull)) a.nops[r] = kNopsKnown;
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
@@ -743,7 +758,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
             // before any store (one read per round trip measured 2.7x the byte-input classify)
             constexpr int kWr = 8;
-            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win) >> lane) & 1ull));
+            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull));
             uint8_t* dst = const_cast<uint8_t*>(a.reads);
             while (dp) {
                 long long o[kWr], e[kWr];

@@ -16,6 +16,9 @@ constexpr int kOpsSlot = 64;    // runs kept per read in its ops slot (more: spi
 // run q at ops[ops_stride * ops_slot + r * ops_slot + q]), not the column-major one (the
 // classify / diagonal-pass records: run q at ops[q * ops_stride + r])
 constexpr int32_t kNopsRows = 1 << 30;
+// nops[r] flag: read r is a copy of the known sequence (KernelArgs::known2): its record and runs
+// are the known alignment's (OpsKnown), filled in by the compaction
+constexpr int32_t kNopsKnown = 1 << 29;
 
 // Per-read record written by the kernel; layout matches nw_stat in include/crispr_nw.h.
 struct Stat {
@@ -132,6 +135,11 @@ struct KernelArgs {
     const uint32_t* cls_img;       // classify's LDS image of the amplicon (nw_host.cpp cls_image)
     int32_t cls_words;
     int32_t amp_acgt;              // every amplicon byte A C G T (either case)
+    // known copies: the 2-bit words of a sequence of the amplicon's length whose
+    // alignment against the amplicon is computed once (the previous amplicon of a resident batch:
+    // the HDR pass's reads that are copies of the reference amplicon); classify flags the reads equal
+    // to it (nops kNopsKnown) and the compaction gives them that alignment.  Null: off.
+    const uint32_t* known2;
 };
 
 // Boundary value of a leading end gap of k residues (0: free end gaps, or k = 0) and
@@ -267,6 +275,15 @@ struct OpsCounts {
 };
 // The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
 // straight into the caller's page-locked buffers (no copies and no host round trip after it).
+// The known alignment (KernelArgs::known2): its record, run count (nops flags) and runs, as the
+// exact kernel left them for one read in a 1-read layout (ops_stride 1).
+struct OpsKnown {
+    const Stat* stat;     // null: off
+    const int32_t* nops;
+    const uint32_t* slots;
+    const uint32_t* spill;
+    int32_t slot;
+};
 struct OpsHostOut {
     const int4* dstats;   // the chunk's records in HBM (2 int4 per nw_stat); null: off
     int4* hstats;         // the caller's records of the chunk's reads
@@ -277,6 +294,7 @@ struct OpsHostOut {
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr);
+                              hipStream_t s, int64_t* hctl = nullptr, const OpsHostOut* host = nullptr,
+                              Stat* stats = nullptr, const OpsKnown* known = nullptr);
 
 }  // namespace nw

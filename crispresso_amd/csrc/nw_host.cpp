@@ -238,6 +238,20 @@ struct nw_ctx {
     // printed (us from the first upload) at the end of the call
     bool trace_on = false;
     int trace_chunk = 0;
+    // known copies: a resident pass against a new amplicon takes the reads equal to
+    // the amplicon the batch was last aligned against (resident_ref: the HDR pass's copies of the
+    // reference amplicon) from ONE alignment of that sequence, computed by the exact kernel on the
+    // upload stream while the chunks start (d_k*: its bytes, offsets, 2-bit words, record, runs,
+    // scratch); KernelArgs::known2 / nw::OpsKnown
+    std::string resident_ref;
+    std::string known_seq;     // nw_set_known: a sequence whose copies take one alignment in every call
+    bool known_on = false;
+    DevBuf<uint8_t> d_kbytes, d_ktb;
+    DevBuf<int64_t> d_koff, d_kfb;
+    DevBuf<uint32_t> d_k2, d_kslots;
+    DevBuf<nw::Stat> d_kstat;
+    DevBuf<int32_t> d_kmisc;   // [0] nops, [1..2] ops_ctl, [8..16) fallback counts
+    hipEvent_t ev_known = nullptr;
     std::vector<std::pair<std::string, hipEvent_t>> trace_ev;
     size_t trace_used = 0;
 };
@@ -748,6 +762,11 @@ void nw_destroy(nw_ctx* c) {
     for (Scratch& S : c->sc) S.release();
     c->d_ctl64.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
+    c->d_kbytes.release(); c->d_ktb.release(); c->d_koff.release(); c->d_kfb.release(); c->d_k2.release();
+    c->d_kslots.release(); c->d_kstat.release(); c->d_kmisc.release();
+    if (c->ev_known) (void)hipEventDestroy(c->ev_known);
+    for (auto& t : c->trace_ev) (void)hipEventDestroy(t.second);
+    for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
     for (int k = 1; k < kScratchSets; ++k)
         if (c->cstream[k]) (void)hipStreamSynchronize(c->cstream[k]);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out);
@@ -1067,6 +1086,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.pk_len = c->pkc.pk_len;
         a.pk_gbase = c->pkc.pk_gbase;
         a.pk_call_lo = c->pkc.pk_call_lo;
+        a.known2 = c->known_on ? c->d_k2.p : nullptr;
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
         const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
@@ -1240,9 +1260,15 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         if (c->seed_chunk) cnt.seeded = c->s->d_fallback_count.p + 7;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
+    nw::OpsKnown kn{};
+    if (c->known_on) {   // the known alignment (computed on the upload stream) before any copy takes it
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_known, 0));
+        kn = nw::OpsKnown{c->d_kstat.p, c->d_kmisc.p, c->d_kslots.p, c->d_kslots.p + 2 * nw::kOpsSlot, nw::kOpsSlot};
+    }
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
                                           c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
-                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host));
+                                          c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host,
+                                          c->d_stats.p + base, c->known_on ? &kn : nullptr));
     tmark(c, "compact");
     return NW_OK;
 }
@@ -1709,6 +1735,71 @@ struct Groups {
     const std::vector<int64_t>* first;
 };
 
+// Known copies (nw_ctx::resident_ref): the resident batch was aligned against amplicon A and is
+// now aligned against H (the HDR pass, CORE:1808-1828): reads equal to A all have A's alignment
+// against H.  A goes through the exact kernel once, as a one-read batch with its own buffers, on
+// the upload stream (idle in a resident pass) while the chunks start; classify flags A's copies
+// (KernelArgs::known2) and every chunk's compaction waits for the alignment and gives it to them.
+// Off unless both sequences are A C G T, of one length <= 256 (classify's lane-per-read compare)
+// and at most the batch's longest read (the exact kernel's LDS sizing).
+int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks) {
+    c->known_on = false;
+    const int La = (int)c->ref.size();
+    if ((int)A.size() != La || La > 256 || La > c->lb_max || A == c->ref || !c->cur.amp_acgt || !c->cur.amp2 ||
+        c->cfg.R <= 0 || c->end_weight)
+        return NW_OK;
+    for (char ch : A) {
+        const char u = (char)(ch & 0xDF);
+        if (u != 'A' && u != 'C' && u != 'G' && u != 'T') return NW_OK;
+    }
+    std::vector<uint32_t> w2((size_t)(La + 15) / 16 + 2, 0u);
+    for (int p = 0; p < La; ++p) w2[(size_t)p / 16] |= (uint32_t)(((unsigned char)A[p] >> 1) & 3u) << (2 * (p % 16));
+    const int64_t tbw = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cfg.R, c->lb_max) : 0;
+    HIP_OR_FAIL(c, c->d_kbytes.reserve((size_t)La + 64));
+    HIP_OR_FAIL(c, c->d_koff.reserve(2));
+    HIP_OR_FAIL(c, c->d_k2.reserve(w2.size()));
+    HIP_OR_FAIL(c, c->d_kslots.reserve(2 * nw::kOpsSlot + 4096));   // column-major + row-major slot, spill
+    HIP_OR_FAIL(c, c->d_kstat.reserve(1));
+    HIP_OR_FAIL(c, c->d_kmisc.reserve(16));
+    HIP_OR_FAIL(c, c->d_kfb.reserve(1));
+    HIP_OR_FAIL(c, c->d_ktb.reserve((size_t)std::max<int64_t>(tbw * c->cfg.wpb, 16)));
+    if (!c->ev_known) HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_known, hipEventDisableTiming));
+    const int64_t off[2] = {0, La};
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_kbytes.p, A.data(), (size_t)La, hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_koff.p, off, sizeof off, hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_k2.p, w2.data(), 4 * w2.size(), hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_kmisc.p, 0, 16 * sizeof(int32_t), ks));
+    nw::KernelArgs ka{};
+    ka.reads = c->d_kbytes.p;
+    ka.offsets = c->d_koff.p;
+    ka.n = 1;
+    ka.prof = c->cur.prof;
+    ka.lut = c->d_lut.p;
+    ka.amp = c->cur.amp;
+    ka.La = La;
+    ka.gap_open = c->gap_open;
+    ka.gap_extend = c->gap_extend;
+    ka.Lb_max = c->lb_max;
+    ka.stats = c->d_kstat.p;
+    ka.tb_global = c->d_ktb.p;
+    ka.tb_wave_bytes = tbw;
+    ka.fallback_list = c->d_kfb.p;
+    ka.fallback_count = c->d_kmisc.p + 8;
+    ka.ops = c->d_kslots.p;
+    ka.ops_slot = nw::kOpsSlot;
+    ka.ops_stride = 1;
+    ka.nops = c->d_kmisc.p;
+    ka.spill = c->d_kslots.p + 2 * nw::kOpsSlot;
+    ka.spill_cap = 4096;
+    ka.ops_ctl = c->d_kmisc.p + 1;
+    nw::LaunchCfg one = c->cfg;
+    one.grid = 1;
+    HIP_OR_FAIL(c, nw::launch(ka, one, ks));
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_known, ks));
+    c->known_on = true;
+    return NW_OK;
+}
+
 // nw_align_ops (upload = true), nw_align_ops_resident (the batch the last call
 // uploaded, still in HBM: no upload) and nw_align_multi_ops (groups: chunks never
 // straddle two amplicons; each chunk's kernels use its amplicon's tables).
@@ -1803,6 +1894,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->exact_small = false;
         c->l2_skip = false;
         c->trace_on = false;
+        c->known_on = false;
         c->pkc = nw::KernelArgs{};
         c->out_mode = mode_before;
         c->n = 0;
@@ -2078,6 +2170,20 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         return restore(rc);
     }
     HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
+    // copies of a known sequence from one alignment (packed classify): the caller's (nw_set_known),
+    // or in a resident pass against a new amplicon the one the batch was last aligned against.  The
+    // alignment runs on the upload stream of a resident pass (idle), else on the tail stream (its
+    // first tail packet comes a chunk's chain later); every compaction waits for it
+    c->known_on = false;
+    {
+        const std::string& K = (!c->known_seq.empty() && c->known_seq != c->ref) ? c->known_seq
+                               : (!upload && c->resident_ref != c->ref) ? c->resident_ref : c->known_seq;
+        const bool packed_classify = (pk != nullptr && upload) || (!upload && c->resident_packed);
+        if (!groups && packed_classify && c->use_diag && n > 0 && !K.empty() && K != c->ref) {
+            if ((rc = use_group(0, std::min(chunk, n))) || (rc = known_prepare(c, K, upload ? c->cstream[2] : c->s_in)))
+                return restore(rc);
+        }
+    }
     int64_t total = 0, err = 0;
     bool cap_short = false;
     // Chunk k's runs go back once the host has read its total (copy_runs).  (Copying an
@@ -2344,6 +2450,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->resident_n = n;
     c->resident_lo = base0;
     c->resident_hi = base0 + nbytes;
+    c->resident_ref = groups ? std::string() : c->ref;   // a later resident pass's known sequence
     if ((rc = ops_error(c, err))) return restore(rc);
     if (cap_short)
         return restore(fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs (ops_off holds the offsets)", (long long)ops_cap,
@@ -2541,6 +2648,12 @@ int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d
 }
 
 int nw_host_threads(void) { return nw_host::Pool::get().threads(); }
+
+int nw_set_known(nw_ctx* c, const char* seq, int32_t len) {
+    if (!c || len < 0 || (len > 0 && !seq)) return NW_E_INVALID;
+    c->known_seq.assign(seq ? seq : "", (size_t)len);
+    return NW_OK;
+}
 
 int nw_batch_set_lane_walk(nw_ctx* c, int on) {
     if (!c) return NW_E_INVALID;

@@ -54,20 +54,31 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
                                                               unsigned long long* status, unsigned epoch, int parity,
                                                               int64_t* ctl, int64_t* ops_off, uint32_t* staging,
                                                               int64_t staging_cap, const int32_t* opsctl,
-                                                              OpsCounts cnt, int64_t* hctl, int prio, OpsHostOut ho) {
+                                                              OpsCounts cnt, int64_t* hctl, int prio, OpsHostOut ho,
+                                                              Stat* stats, OpsKnown kn) {
     __shared__ int sh_bad;
     __shared__ unsigned sh_excl;
     if (prio) __builtin_amdgcn_s_setprio(3);
     const long long r0 = (long long)blockIdx.x * kOpsBlockReads + threadIdx.x * kOpsPerThread;
     int c4[kOpsPerThread];
-    bool rows4[kOpsPerThread];
+    bool rows4[kOpsPerThread], known4[kOpsPerThread];
+    // the known alignment (a copy of the known sequence takes its record and runs)
+    const int kraw = kn.stat ? *kn.nops : 0;
+    const int kc = kraw & (kNopsKnown - 1);
     long long s = 0;
 #pragma unroll
     for (int k = 0; k < kOpsPerThread; ++k) {
         const int raw = r0 + k < n ? nops[r0 + k] : 0;
-        c4[k] = raw & (kNopsRows - 1);
+        known4[k] = kn.stat && (raw & kNopsKnown);
+        c4[k] = known4[k] ? kc : raw & (kNopsKnown - 1);
         rows4[k] = (raw & kNopsRows) != 0;
         s += c4[k];
+    }
+    if (kn.stat) {   // the known copies' records, before the host copy below reads them
+        const Stat ks = *kn.stat;
+#pragma unroll
+        for (int k = 0; k < kOpsPerThread; ++k)
+            if (known4[k]) stats[r0 + k] = ks;
     }
     if (threadIdx.x == 0) sh_bad = 0;
     long long total;
@@ -102,7 +113,10 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         // share lines); row-major (rows4): contiguous at slots[stride * slot + r * slot]
         const uint32_t* src = slots + r;
         long long step = stride;
-        if (c > slot) {
+        if (known4[k]) {   // the known alignment's 1-read layout (ops_stride 1)
+            step = 1;
+            src = c > kn.slot ? kn.spill + kn.slots[0] : ((kraw & kNopsRows) ? kn.slots + kn.slot : kn.slots);
+        } else if (c > slot) {
             src = spill + src[0];
             step = 1;
         } else if (rows4[k]) {
@@ -167,11 +181,12 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
 hipError_t launch_ops_compact(const int32_t* nops, const uint32_t* slots, int slot, int64_t stride, const uint32_t* spill, int64_t n,
                               unsigned long long* status, unsigned epoch, int parity, int64_t* ctl, int64_t* ops_off,
                               uint32_t* staging, int64_t staging_cap, int32_t* opsctl, const OpsCounts& cnt,
-                              hipStream_t s, int64_t* hctl, const OpsHostOut* host) {
+                              hipStream_t s, int64_t* hctl, const OpsHostOut* host, Stat* stats, const OpsKnown* known) {
     const OpsHostOut ho = host ? *host : OpsHostOut{};
+    const OpsKnown kn = known && stats ? *known : OpsKnown{};
     const int nblk = (int)std::max<int64_t>(1, (n + kOpsBlockReads - 1) / kOpsBlockReads);
     hipLaunchKernelGGL(nw_ops_compact, dim3(nblk), dim3(kOpsThreads), 0, s, nops, slots, slot, stride, spill, n, status, epoch,
-                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio, ho);
+                       parity, ctl, ops_off, staging, staging_cap, opsctl, cnt, hctl, cnt.prio, ho, stats, kn);
     return hipGetLastError();
 }
 

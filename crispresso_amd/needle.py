@@ -499,8 +499,17 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
             packed = None
         tm["ingest_s"] = clock() - t0
         t0 = clock()
-        fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
-                          _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None, packed=packed)
+        # the HDR amplicon's copies among the reads take one alignment of it in the forward pass
+        # (nw_set_known), the reference amplicon's copies in the resident HDR pass (automatic)
+        known = args.expected_hdr_amplicon_seq if native and hasattr(aligner, "set_known") else None
+        if known:
+            aligner.set_known(known)
+        try:
+            fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
+                              _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None, packed=packed)
+        finally:
+            if known:
+                aligner.set_known(None)
         tm["align_s"] = clock() - t0
         if args.expected_hdr_amplicon_seq:
             t0 = clock()

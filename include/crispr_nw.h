@@ -285,6 +285,14 @@ int nw_host_unregister(void* p);
  * by the cgroup quota and divided by LOCAL_WORLD_SIZE (crispresso_amd/placement.py binds a
  * rank and sets the variable).  Creates the pool on first use. */
 int nw_host_threads(void);
+/* A sequence whose exact copies among the reads (case-insensitive A C G T) take ONE alignment of
+ * it against the amplicon, computed by the exact kernel during the call, instead of a DP each:
+ * the HDR amplicon during the reference-amplicon pass of CRISPResso's dual alignment
+ * (CRISPRessoCORE.py:1788-1828; len 0 clears it).  A resident pass against a new amplicon
+ * (nw_align_ops_resident) uses the amplicon the batch was last aligned against the same way when
+ * none is set.  Results are those of aligning every read; used when both sequences are A C G T,
+ * of one length <= 256, and the input is packed. */
+int nw_set_known(nw_ctx* ctx, const char* seq, int32_t len);
 /* Resident passes (nw_batch_run_async) only: the first band level's lane walk and the stop
  * summary its fill writes (on != 0), instead of the wave-per-read walk every pipelined call
  * runs.  The bench times both; off by default. */

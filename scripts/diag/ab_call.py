@@ -65,7 +65,9 @@ for i in range(2 * rounds + 4):
         al.align_multi_ops(amps, pr, None, pw.array, out=(stats.array, ops.array, ops_off.array))
     elif c3:
         al.set_reference(amplicon)
+        al.set_known(hdr)
         al.align_ops_packed(pr, out=(stats.array, ops.array, ops_off.array))
+        al.set_known(None)
         al.set_reference(hdr)
         al.align_ops(None, po.array, out=(stats2.array, None, ops_off2.array), resident=True, records_only=True)
     else:

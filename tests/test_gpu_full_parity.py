@@ -88,14 +88,18 @@ def test_c3_both_passes_every_read(al):
     outs2, out2 = _pinned_out(n)
     outs3, out3 = _pinned_out(n)
     al.set_reference(amp)
+    al.set_known(hdr)   # the bench's and align_reads' form: the HDR amplicon's copies from one alignment
     ob1 = al.align_ops_packed(pr, out=out1)
-    _assert_clean(every_read(amp, buf, off, ob1, THREADS), "C3 amplicon pass")
-    al.set_reference(hdr)
+    al.set_known(None)
+    _assert_clean(every_read(amp, buf, off, ob1, THREADS), "C3 amplicon pass (HDR copies known)")
+    s1, oo1 = ob1.stats.copy(), ob1.ops_off.copy()
+    al.set_reference(hdr)   # the reference amplicon's copies from one alignment (known copies)
     ob2 = al.align_ops(None, pr.offsets, out=out2, resident=True)
     _assert_clean(every_read(hdr, buf, off, ob2, THREADS), "C3 HDR pass (resident, runs)")
     # the bench's form of the HDR pass: records only, resident (right after the packed call)
     al.set_reference(amp)
-    al.align_ops_packed(pr, out=out1)
+    ob1b = al.align_ops_packed(pr, out=out1)   # no known sequence: the same records and runs
+    assert every_read_records(ob1b.stats, s1) == 0 and np.array_equal(ob1b.ops_off, oo1)
     al.set_reference(hdr)
     ob3 = al.align_ops(None, pr.offsets, out=(out3[0], None, out3[2]), resident=True, records_only=True)
     assert every_read_records(ob3.stats, ob2.stats) == 0

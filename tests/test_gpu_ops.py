@@ -588,3 +588,46 @@ def test_lane_walk_resident_pass_matches_call_and_oracle(gpu_aligner_factory, or
 
     chk = every_read(amp, buf, off, res, threads=16)
     assert chk["mismatches"] == 0, chk
+
+
+@pytest.mark.parametrize("hdr_kind", ["block", "one_sub", "two_sub", "longer"])
+def test_known_copies_resident_pass(gpu_aligner_factory, hdr_kind):
+    """The HDR pass's copies of the reference amplicon (known copies): a resident pass
+    against a new amplicon takes the reads equal to the batch's previous amplicon (upper or lower
+    case) from one exact-kernel alignment of it.  Every read against the oracle, for an HDR amplicon
+    10 bases apart (the C3 shape), 1 and 2 substitutions apart (the classify certificates take those
+    reads first) and of another length (no known copies)."""
+    from crispresso_amd.aligner import pack_2bit
+    from tests.every_read import every_read
+
+    amp = synth.random_amplicon(250, 21)
+    if hdr_kind == "block":
+        hdr = synth.hdr_amplicon(amp, 4)
+    elif hdr_kind == "one_sub":
+        hdr = amp[:100] + ("A" if amp[100] != "A" else "C") + amp[101:]
+    elif hdr_kind == "two_sub":
+        hdr = amp[:60] + ("G" if amp[60] != "G" else "T") + amp[61:180] + ("A" if amp[180] != "A" else "C") + amp[181:]
+    else:
+        hdr = amp[:120] + "ACGTA" + amp[120:]
+    rng = np.random.Generator(np.random.PCG64(22))
+    b1, o1 = synth.reads_from(amp, 30000, 23, synth.PARITY_MIX)
+    seqs = synth.unpack(b1, o1)
+    for k in rng.choice(len(seqs), 3000, replace=False):   # lower-case copies of the amplicon
+        seqs[k] = amp.lower() if k % 2 else amp[:50] + amp[50:].lower()
+    b2, o2 = synth.reads_from(hdr, 5000, 24)
+    seqs += synth.unpack(b2, o2)
+    buf, off = pack_reads(seqs)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    pr = pack_2bit(buf, off)
+    ob1 = a.align_ops_packed(pr)
+    chk1 = every_read(amp, buf, off, ob1, threads=16)
+    assert chk1["mismatches"] == 0, chk1
+    a.set_reference(hdr)
+    ob2 = a.align_ops(None, off, resident=True)
+    chk2 = every_read(hdr, buf, off, ob2, threads=16)
+    assert chk2["mismatches"] == 0, chk2
+    # the records-only pass (the HDR pass CRISPResso runs, CORE:1740-1741) gives the same records
+    ob3 = a.align_ops(None, off, resident=True, records_only=True)
+    for f in FIELDS:
+        np.testing.assert_array_equal(ob3.stats[f], ob2.stats[f], err_msg=f)
