@@ -196,7 +196,6 @@ struct nw_ctx {
     bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
     bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
-    bool l2_skip = false;             // this chunk: no second-level launches, the wide level takes the redo list
     bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
@@ -1118,7 +1117,6 @@ int launch_range(nw_ctx* c, int64_t base) {
                          ? (int)std::max<int64_t>(1024, std::min<int64_t>(c->n / 16, 2 * c->wide_pairs))
                          : 1024;
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
-        if (c->l2_skip && two && c->wide_fill.grid > 0) direct = 1 << 30;   // every redo read to the wide level
         if (!two) direct = 0;
         c->redo_direct = direct;
         // (the diagonal pass and the traceback fill as one launch measured slower: kernel-resident
@@ -1138,7 +1136,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
             const nw::LaunchCfg& wc = lvl == 0 ? c->diag16_walk : c->diag_walk;
             const bool first = lvl == (two ? 0 : 1);
-            if (!first && c->l2_skip && direct == (1 << 30)) break;   // no second-level launches at all
             if (!first) {   // the second level aligns the redo list only
                 al.order_a = nullptr;
                 al.tile_list = nullptr;
@@ -1849,31 +1846,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         for (auto it = tail.rbegin(); it != tail.rend(); ++it) v.push_back(*it);
         return v;
     };
-    std::vector<int64_t> ramp;   // CRISPR_NW_RAMP=a,b,c (diagnostics): explicit chunk sizes of a one-group call
-    if (const char* e = std::getenv("CRISPR_NW_RAMP")) {
-        for (const char* p = e; *p;) {
-            char* q = nullptr;
-            const long long v = std::strtoll(p, &q, 10);
-            if (q == p) break;
-            if (v > 0) ramp.push_back(v);
-            p = *q ? q + 1 : q;
-        }
-    }
     for (int g = 0; g < ngroups; ++g) {
         const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
         int64_t lo = g0;
-        std::vector<int64_t> sz = sizes(g1 - g0);
-        if (!groups && !ramp.empty()) {
-            sz.clear();
-            int64_t left = g1 - g0;
-            for (size_t i = 0; left > 0; ++i) {
-                const int64_t v = i < ramp.size() ? std::min(ramp[i], left) : std::min(chunk, left);
-                sz.push_back(v);
-                left -= v;
-            }
-            chunk = std::max(chunk, *std::max_element(sz.begin(), sz.end()));
-        }
-        for (int64_t len : sz) {
+        for (int64_t len : sizes(g1 - g0)) {
             if (len <= 0) continue;
             chunks.push_back({lo, lo + len, g});
             lo += len;
@@ -1892,7 +1868,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->diag_off = false;
         c->diag_tail = false;
         c->exact_small = false;
-        c->l2_skip = false;
         c->trace_on = false;
         c->known_on = false;
         c->pkc = nw::KernelArgs{};
@@ -2113,6 +2088,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     };
     // configure every group once up front: the buffers reach their largest size before
     // anything is queued (no allocation inside the pipeline)
+    // (A resident pass -- the C3 HDR pass -- in 524288- / 1048576-read chunks measured 8.95 / 10.77
+    // vs 5.85 ms per C3 step: the wide level's region per chunk overflows to the exact kernel and the
+    // last chunk's records go over PCIe unoverlapped; without the tail stream 5.78 vs 5.70.)
     // two sets overlap a chunk's tail with the next chunk's bulk; a third measured slower
     // (328M vs 306M reads/s at 262144-read chunks, scripts/gpu_sets_sweep.sh)
     const bool several = (n + chunk - 1) / std::max<int64_t>(chunk, 1) > 1 || ngroups > 1;
@@ -2194,22 +2172,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // after the call's last kernel (2.31 -> 2.27 ms per 1M-read call)
     const bool direct_out = nchunks >= 1 && host_mapped(stats) && host_mapped(ops_off) &&
                             (!ops_out || host_mapped(ops_out));
-    // diagnostics / A-B knobs of the call (CRISPR_NW_L2SKIP, CRISPR_NW_SPIN)
-    const char* l2e = std::getenv("CRISPR_NW_L2SKIP");
-    const bool l2_skip_on = l2e && std::strcmp(l2e, "1") == 0;
-    int nosplit_last = 0;
-    if (const char* e = std::getenv("CRISPR_NW_NOSPLIT_LAST")) nosplit_last = std::atoi(e);
-    const char* spe = std::getenv("CRISPR_NW_SPIN");
-    const bool spin = spe && std::strcmp(spe, "1") == 0;
     std::vector<char> direct_done((size_t)std::max<int64_t>(nchunks, 1), 0);
     auto copy_runs = [&](int64_t k) -> int {
         ht.lap(4);
-        if (spin) {
-            hipError_t q;
-            while ((q = hipEventQuery(c->ev_ce[(size_t)k])) == hipErrorNotReady) {
-            }
-            HIP_OR_FAIL(c, q);
-        }
         HIP_OR_FAIL(c, hipEventSynchronize(c->ev_ce[(size_t)k]));
         ht.lap(5);
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
@@ -2251,7 +2216,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             c->cs = c->cstream[k % 2];
             // the last chunks keep their tail on their own compute stream (no later chunk's bulk
             // queues behind it there): their tails overlap instead of queueing on the tail stream
-            c->split_to = k >= nchunks - nosplit_last ? nullptr : c->cstream[2];
+            c->split_to = c->cstream[2];
             c->split_ev = c->ev_bulk[(size_t)k];
             // the set's previous chunk (k - 3) must be through its tail
             if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));
@@ -2319,16 +2284,15 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
-        // no second-level launches while the newest chunk read back needed none (its redo list
-        // went to the wide level: direct hand-off); the wide level then takes the whole redo
-        // list (what its region cannot hold goes on to the exact kernel)
-        c->l2_skip = false;
-        if (l2_skip_on && k >= lag + 1) {
-            const int64_t j = k - lag - 1;
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
-            const int64_t l2 = h[5] - (j > 0 ? c->h_ctl[nw::kOpsCtl * (j - 1) + 5] : 0);
-            c->l2_skip = !one_level[(size_t)j] && !c->skip16 && l2 == 0;
-        }
+        // (No second-level launches while the newest chunk read back needed none -- the wide level
+        // taking the whole redo list -- measured 1.926 vs 1.939 ms per C2 call but is not safe to
+        // choose from earlier chunks: the C3 amplicon pass, whose HDR reads come last, sent ~30k of
+        // them past the wide level's region to the exact kernel, 5.96 -> 14.5 ms per C3 step.  Lost
+        // on C2 and not kept either: spinning on the chunk events, the last chunks' tails on their
+        // own compute streams, explicit chunk ramps ending in small chunks, the last chunk's DP
+        // reads straight to the wide level, the lane walk in the chunks (1.975 vs 1.959 ms; C3 14.50
+        // vs 14.56), the 32-diagonal level's lane walk, the last chunk alone
+        // on a high-priority stream, each chunk's upload split over two streams: +0.01 to +0.58 ms.)
         // the exact kernel's grid: small while the newest chunk read back sent it few reads
         // (after the wide level it gets the rare read no band certifies)
         c->exact_small = true;
@@ -2395,12 +2359,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     for (int64_t k = std::max<int64_t>(runs_queued, nchunks - lag); k < nchunks; ++k)
         if ((rc = copy_runs(k))) return restore(rc);
     ht.lap(4);
-    if (spin) {
-        hipError_t q;
-        while ((q = hipEventQuery(c->ev_out[(size_t)(nchunks - 1)])) == hipErrorNotReady) {
-        }
-        HIP_OR_FAIL(c, q);
-    }
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);
     ops_off[n] = total;

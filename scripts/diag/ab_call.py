@@ -2,7 +2,7 @@
 of env knobs the library reads per call: calls alternate A, B, A, B ... so that box-level
 drift (PCIe, host load) hits both alike.
 Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds] [pooled]   (an empty string = defaults;
-pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads; c3: the dual
+c1: the C1-shape call (151 bp windows x 280 bp amplicon); pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads; c3: the dual
 alignment step, packed amplicon pass + resident HDR pass records-only)"""
 import os
 import sys
@@ -25,7 +25,11 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
 c3 = len(sys.argv) > 4 and sys.argv[4] == "c3"
 c4 = len(sys.argv) > 4 and sys.argv[4] == "c4"
-if c4:   # the C4 shard: 12.5M reads of the native generator in one call
+c1 = len(sys.argv) > 4 and sys.argv[4] == "c1"
+if c1:   # the C1 shape: 151 bp windows of a 280 bp amplicon
+    amplicon, buf, off = synth.c1_shape_workload(bench.READS_PER_GPU)
+    nr = len(off) - 1
+elif c4:   # the C4 shard: 12.5M reads of the native generator in one call
     amplicon = synth.random_amplicon(bench.AMPLICON_LEN, 1)
     buf, off = synth.native_reads(amplicon, bench.C4_CALL_READS, 10)
     nr = len(off) - 1
@@ -82,6 +86,8 @@ for i in range(2 * rounds + 4):
     elif out != ref:
         print("OUTPUT DIFFERS at call", i, which)
         sys.exit(1)
+if os.environ.get("AB_COUNTS"):
+    print("path_counts", al.path_counts(), "ops_times", al.ops_times())
 for w, spec in (("A", sys.argv[1]), ("B", sys.argv[2])):
     t = np.array(times[w])
     print(f"{w} [{spec}]: median {np.median(t):.3f} ms  min {t.min():.3f}  p90 {np.percentile(t, 90):.3f}  "
