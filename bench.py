@@ -344,7 +344,9 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
         q.run_device_ops(amplicon, dev, d_pre.ptr, n_reads, d_out.ptr)
         kms.append(q.last_kernel_ms)
     elapsed = time.perf_counter() - t0
-    algo = int(n_reads * (1 + 4 + 16) + 3 * lens[~um].sum())
+    nruns = np.diff(np.asarray(ob.ops_off, dtype=np.int64))
+    rlen = np.diff(np.asarray(offsets[: n_reads + 1], dtype=np.int64))
+    algo = int(n_reads * (1 + 4 + 8 + 16) + (4 * nruns[~um] + rlen[~um]).sum())
     kavg = float(np.mean(kms))
     qp = pmc_per_call(QUANT_PMC, lambda k: "nwq::" in k)
     out = {
@@ -353,8 +355,10 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
         "unit": "reads/s",
         "ms_per_step": elapsed / steps * 1e3,
         "input": "the aligner's resident ops output (records + runs + reads in HBM; no rows-mode re-run)",
-        "kernel": "nwq::expand_rows (the rows of the non-UNMODIFIED reads, from their runs) + nwq::quant_kernel "
-                  "+ nwq::quant_reduce",
+        "kernel": "nwq::quant_lanes (process_df_chunk's substitution / insertion / deletion positions straight "
+                  "from each read's runs and bytes, one lane per read; the few reads it does not take -- non-ACGT "
+                  "bytes, more runs than a lane holds -- through nwq::expand_rows + nwq::quant_kernel) + "
+                  "nwq::quant_reduce",
         "kernel_ms_avg": kavg,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -364,8 +368,8 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
                                         f"{qp['lib_matches_loaded']})") if qp else None,
                      "traffic_kernels": qp["kernels"] if qp else None,
                      "algo_bytes_per_launch": algo,
-                     "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 16 (result); + 3*aln_len for rows not "
-                                       "UNMODIFIED on input (the three alignment rows)"},
+                     "algo_bytes_def": "per read 1 (flags) + 4 (aln_len) + 8 (run offset) + 16 (result); + 4 per "
+                                       "run + the read's bytes for reads not UNMODIFIED on input"},
         "settings": "guide mid-amplicon, window_around_sgrna 1, exclude 15/15",
     }
     if rank == 0 and world == 1 and not no_cpu:
