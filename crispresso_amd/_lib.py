@@ -44,7 +44,7 @@ EXPORTS = (
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
     "nw_host_register", "nw_host_unregister", "nw_host_threads", "nw_batch_set_lane_walk", "nw_set_known", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts", "nw_batch_exact_reads",
-    "nw_align_ops_packed_lens", "nw_align_multi_ops_packed_lens", "nw_read_lengths16", "nw_fastq_lens",
+    "nw_align_ops_packed_lens", "nw_align_multi_ops_packed_lens", "nw_align_dual_ops_packed_lens", "nw_read_lengths16", "nw_fastq_lens",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
     "nw_expand_ops_subset", "nw_reads_equal_ref", "nw_reads_first_copy", "nw_names_to_ids", "nw_gunzip_parallel", "nw_ops_rows_concat", "nw_fastq_pack", "nw_batch_device_ops",
@@ -168,6 +168,9 @@ def load() -> ctypes.CDLL:
         "nw_align_multi_ops_packed_lens": (c_int, [ctx_p, c_char_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                                    c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
                                                    c_void_p, c_void_p]),
+        "nw_align_dual_ops_packed_lens": (c_int, [ctx_p, c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_int64,
+                                                  c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                                  c_void_p, c_int64, c_void_p, c_void_p]),
         "nw_read_lengths16": (c_int, [c_void_p, c_int64, c_void_p, c_int32]),
         "nw_fastq_lens": (c_int, [c_void_p, POINTER(c_void_p)]),
         "nw_ops_times": (c_int, [ctx_p, POINTER(c_float), POINTER(c_float), POINTER(c_int64), POINTER(c_int64)]),

@@ -462,6 +462,51 @@ class GpuAligner:
         self._check(rc, "nw_align_ops_packed")
         return OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
 
+    def align_dual_packed(self, pr: "PackedReads", ref2: str, out: Optional[tuple] = None,
+                          out2: Optional[tuple] = None, records_only2: bool = False) -> tuple:
+        """nw_align_dual_ops_packed_lens: every read of the packed batch (with lengths) against
+        the current amplicon and against ``ref2`` (the expected HDR amplicon, CORE:1808-1828) in
+        one call -- one upload, the second pass interleaved with the first.  ``out`` / ``out2``:
+        (stats, ops, ops_off) per pass (``out2``'s ops may be None with ``records_only2``: the
+        second pass's runs stay on the device).  Returns the two OpsBatch (the second without runs
+        when records_only2)."""
+        if self.reference is None:
+            raise NeedleError("no amplicon set")
+        if pr.lens is None:
+            raise NeedleError("the dual call takes a packed batch with its lengths")
+        offsets = pr.offsets
+        n = len(offsets) - 1
+        stats, ops, ops_off = out if out is not None else _outputs(n)
+        if out2 is not None:
+            stats2, ops2, ops_off2 = out2
+        else:
+            stats2, ops2, ops_off2 = _outputs(n)
+        if records_only2:
+            ops2 = None
+        exc = (_lib.ptr(pr.exc_pos) if len(pr.exc_pos) else None, _lib.ptr(pr.exc_byte) if len(pr.exc_byte) else None,
+               len(pr.exc_pos))
+        r2 = ref2.encode()
+
+        def call(o, o2):
+            return self.lib.nw_align_dual_ops_packed_lens(
+                self._h, r2, len(r2), _lib.ptr(pr.packed), _lib.ptr(offsets), _lib.ptr(pr.lens), n, *exc,
+                _lib.ptr(o), len(o), _lib.ptr(ops_off), _lib.ptr(stats),
+                _lib.ptr(o2) if o2 is not None else None, len(o2) if o2 is not None else 0, _lib.ptr(ops_off2),
+                _lib.ptr(stats2))
+
+        rc = call(ops, ops2)
+        if rc == _lib.NW_E_CAPACITY:
+            if int(ops_off[n]) > len(ops):
+                ops = _lib.pinned_pool().array(int(ops_off[n]), np.uint32)
+            if ops2 is not None and int(ops_off2[n]) > len(ops2):
+                ops2 = _lib.pinned_pool().array(int(ops_off2[n]), np.uint32)
+            rc = call(ops, ops2)
+        self._check(rc, "nw_align_dual_ops_packed_lens")
+        ob = OpsBatch(stats, ops[: int(ops_off[n])], ops_off, None, self.scale, self.options.awidth, offsets=offsets)
+        ob2 = OpsBatch(stats2, ops2[: int(ops_off2[n])] if ops2 is not None else np.empty(0, np.uint32), ops_off2,
+                       None, self.scale, self.options.awidth, offsets=offsets, has_runs=ops2 is not None)
+        return ob, ob2
+
     def ops_times(self) -> dict:
         """Last align_ops: upload span (ms), summed kernel spans (ms), bytes each way."""
         h2d, comp = ctypes.c_float(), ctypes.c_float()

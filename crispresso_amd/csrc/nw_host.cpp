@@ -97,7 +97,8 @@ struct Scratch {
         d_opsctl.release();
     }
 };
-constexpr int kScratchSets = 3;
+constexpr int kScratchSets = 6;   // 3 per pass of a dual call, 3 otherwise
+constexpr int kComputeStreams = 3;
 constexpr int64_t kDiagMinChunks = 12;
 constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level (region capacity)
 
@@ -127,7 +128,7 @@ struct nw_ctx {
     Scratch sc[kScratchSets];
     Scratch* s = &sc[0];                               // the set launch_range / configure use
     hipStream_t cs = nullptr;                          // the stream launch_range queues on
-    hipStream_t cstream[kScratchSets] = {};            // compute stream of each set ([0] = stream)
+    hipStream_t cstream[kComputeStreams] = {};            // compute stream of each set ([0] = stream)
     // tail split (ops_call): launch_range queues a chunk's first band level on
     // c->cs, then records split_ev there and moves to split_to for the rest (second level,
     // exact kernel, compaction)
@@ -244,13 +245,27 @@ struct nw_ctx {
     // scratch); KernelArgs::known2 / nw::OpsKnown
     std::string resident_ref;
     std::string known_seq;     // nw_set_known: a sequence whose copies take one alignment in every call
-    bool known_on = false;
-    DevBuf<uint8_t> d_kbytes, d_ktb;
-    DevBuf<int64_t> d_koff, d_kfb;
-    DevBuf<uint32_t> d_k2, d_kslots;
-    DevBuf<nw::Stat> d_kstat;
-    DevBuf<int32_t> d_kmisc;   // [0] nops, [1..2] ops_ctl, [8..16) fallback counts
-    hipEvent_t ev_known = nullptr;
+    bool known_on = false;     // the current chunk's known set (kset[kcur]) is prepared
+    struct KnownSet {          // one known sequence's alignment (a dual call has one per pass)
+        DevBuf<uint8_t> d_kbytes, d_ktb;
+        DevBuf<int64_t> d_koff, d_kfb;
+        DevBuf<uint32_t> d_k2, d_kslots;
+        DevBuf<nw::Stat> d_kstat;
+        DevBuf<int32_t> d_kmisc;   // [0] nops, [1..2] ops_ctl, [8..16) fallback counts
+        hipEvent_t ev_known = nullptr;
+        bool on = false;
+        void release() {
+            d_kbytes.release(); d_ktb.release(); d_koff.release(); d_kfb.release(); d_k2.release();
+            d_kslots.release(); d_kstat.release(); d_kmisc.release();
+            if (ev_known) (void)hipEventDestroy(ev_known);
+            ev_known = nullptr;
+        }
+    } kset[2];
+    int kcur = 0;
+    // a dual call (nw_align_dual_ops_packed_lens): the current chunk's pass writes its records and
+    // run offsets at d_stats / d_opsoff + out_off and keeps its running base in ctl block ctl_pass
+    int64_t out_off = 0;
+    int ctl_pass = 0;
     std::vector<std::pair<std::string, hipEvent_t>> trace_ev;
     size_t trace_used = 0;
 };
@@ -761,12 +776,10 @@ void nw_destroy(nw_ctx* c) {
     for (Scratch& S : c->sc) S.release();
     c->d_ctl64.release(); c->d_opsoff.release();
     if (c->s_in) (void)hipStreamSynchronize(c->s_in);
-    c->d_kbytes.release(); c->d_ktb.release(); c->d_koff.release(); c->d_kfb.release(); c->d_k2.release();
-    c->d_kslots.release(); c->d_kstat.release(); c->d_kmisc.release();
-    if (c->ev_known) (void)hipEventDestroy(c->ev_known);
+    for (auto& ks : c->kset) ks.release();
     for (auto& t : c->trace_ev) (void)hipEventDestroy(t.second);
     for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
-    for (int k = 1; k < kScratchSets; ++k)
+    for (int k = 1; k < kComputeStreams; ++k)
         if (c->cstream[k]) (void)hipStreamSynchronize(c->cstream[k]);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out);
     for (auto* v : {&c->ev_in, &c->ev_cs, &c->ev_ce, &c->ev_out})
@@ -776,7 +789,7 @@ void nw_destroy(nw_ctx* c) {
     if (c->ev_h0) (void)hipEventDestroy(c->ev_h0);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->s_in) (void)hipStreamDestroy(c->s_in);
-    for (int k = 1; k < kScratchSets; ++k)
+    for (int k = 1; k < kComputeStreams; ++k)
         if (c->cstream[k]) (void)hipStreamDestroy(c->cstream[k]);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
@@ -1014,7 +1027,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.Lb_max = c->lb_max;
     a.out = c->d_out.p + base * 3 * c->stride;
     a.stride = c->stride;
-    a.stats = c->d_stats.p + base;
+    a.stats = c->d_stats.p + c->out_off + base;
     a.tb_global = c->s->d_tb.p;
     a.sub16 = c->d_sub16.p;
     a.rowpos = c->cur.rowpos;
@@ -1085,7 +1098,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.pk_len = c->pkc.pk_len;
         a.pk_gbase = c->pkc.pk_gbase;
         a.pk_call_lo = c->pkc.pk_call_lo;
-        a.known2 = c->known_on ? c->d_k2.p : nullptr;
+        a.known2 = c->known_on ? c->kset[c->kcur].d_k2.p : nullptr;
         // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
         // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
         const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
@@ -1219,7 +1232,7 @@ int ops_reserve(nw_ctx* c, int64_t chunk, int64_t n) {
     HIP_OR_FAIL(c, c->s->d_nops.reserve((size_t)chunk));
     HIP_OR_FAIL(c, c->s->d_spill.reserve((size_t)c->spill_cap));
     HIP_OR_FAIL(c, c->s->d_opsctl.reserve(2));
-    HIP_OR_FAIL(c, c->d_ctl64.reserve(nw::kOpsCtlAll));
+    HIP_OR_FAIL(c, c->d_ctl64.reserve(2 * nw::kOpsCtlAll));   // a dual call: one block per pass
     HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(chunk)));
     HIP_OR_FAIL(c, c->d_opsoff.reserve((size_t)std::max<int64_t>(n, 1) + 1));
     HIP_OR_FAIL(c, c->s->d_staging.reserve((size_t)c->staging_cap));
@@ -1259,13 +1272,15 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     if (c->n <= 0) cnt.fallback = nullptr;
     nw::OpsKnown kn{};
     if (c->known_on) {   // the known alignment (computed on the upload stream) before any copy takes it
-        HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_known, 0));
-        kn = nw::OpsKnown{c->d_kstat.p, c->d_kmisc.p, c->d_kslots.p, c->d_kslots.p + 2 * nw::kOpsSlot, nw::kOpsSlot};
+        auto& K = c->kset[c->kcur];
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, K.ev_known, 0));
+        kn = nw::OpsKnown{K.d_kstat.p, K.d_kmisc.p, K.d_kslots.p, K.d_kslots.p + 2 * nw::kOpsSlot, nw::kOpsSlot};
     }
     HIP_OR_FAIL(c, nw::launch_ops_compact(c->s->d_nops.p, c->s->d_slots.p, c->ops_slot, c->ops_stride, c->s->d_spill.p, c->n,
-                                          c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p, c->d_opsoff.p + base,
+                                          c->s->d_lb.p, next_epoch(c), parity, c->d_ctl64.p + c->ctl_pass * nw::kOpsCtlAll,
+                                          c->d_opsoff.p + c->out_off + base,
                                           c->s->d_staging.p, c->staging_cap, c->s->d_opsctl.p, cnt, c->cs, hctl, host,
-                                          c->d_stats.p + base, c->known_on ? &kn : nullptr));
+                                          c->d_stats.p + c->out_off + base, c->known_on ? &kn : nullptr));
     tmark(c, "compact");
     return NW_OK;
 }
@@ -1732,6 +1747,17 @@ struct Groups {
     const std::vector<int64_t>* first;
 };
 
+// A dual call (nw_align_dual_ops_packed_lens, CORE:1808-1828): every read against refs[0] (pass 0:
+// the caller's stats / ops_off / ops_out) and refs[1] (pass 1: these outputs; null ops_out2: records
+// only), the two passes' chunks interleaved -- pass 1's chunk of a read range runs as soon as that
+// range is uploaded, on the time the upload-bound pass 0 leaves the GPU idle.
+struct Dual {
+    uint32_t* ops_out2;
+    int64_t ops_cap2;
+    int64_t* ops_off2;
+    nw_stat* stats2;
+};
+
 // Known copies (nw_ctx::resident_ref): the resident batch was aligned against amplicon A and is
 // now aligned against H (the HDR pass, CORE:1808-1828): reads equal to A all have A's alignment
 // against H.  A goes through the exact kernel once, as a one-read batch with its own buffers, on
@@ -1739,8 +1765,9 @@ struct Groups {
 // (KernelArgs::known2) and every chunk's compaction waits for the alignment and gives it to them.
 // Off unless both sequences are A C G T, of one length <= 256 (classify's lane-per-read compare)
 // and at most the batch's longest read (the exact kernel's LDS sizing).
-int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks) {
-    c->known_on = false;
+int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks, int set = 0) {
+    auto& K = c->kset[set];
+    K.on = false;
     const int La = (int)c->ref.size();
     if ((int)A.size() != La || La > 256 || La > c->lb_max || A == c->ref || !c->cur.amp_acgt || !c->cur.amp2 ||
         c->cfg.R <= 0 || c->end_weight)
@@ -1752,23 +1779,23 @@ int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks) {
     std::vector<uint32_t> w2((size_t)(La + 15) / 16 + 2, 0u);
     for (int p = 0; p < La; ++p) w2[(size_t)p / 16] |= (uint32_t)(((unsigned char)A[p] >> 1) & 3u) << (2 * (p % 16));
     const int64_t tbw = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cfg.R, c->lb_max) : 0;
-    HIP_OR_FAIL(c, c->d_kbytes.reserve((size_t)La + 64));
-    HIP_OR_FAIL(c, c->d_koff.reserve(2));
-    HIP_OR_FAIL(c, c->d_k2.reserve(w2.size()));
-    HIP_OR_FAIL(c, c->d_kslots.reserve(2 * nw::kOpsSlot + 4096));   // column-major + row-major slot, spill
-    HIP_OR_FAIL(c, c->d_kstat.reserve(1));
-    HIP_OR_FAIL(c, c->d_kmisc.reserve(16));
-    HIP_OR_FAIL(c, c->d_kfb.reserve(1));
-    HIP_OR_FAIL(c, c->d_ktb.reserve((size_t)std::max<int64_t>(tbw * c->cfg.wpb, 16)));
-    if (!c->ev_known) HIP_OR_FAIL(c, hipEventCreateWithFlags(&c->ev_known, hipEventDisableTiming));
+    HIP_OR_FAIL(c, K.d_kbytes.reserve((size_t)La + 64));
+    HIP_OR_FAIL(c, K.d_koff.reserve(2));
+    HIP_OR_FAIL(c, K.d_k2.reserve(w2.size()));
+    HIP_OR_FAIL(c, K.d_kslots.reserve(2 * nw::kOpsSlot + 4096));   // column-major + row-major slot, spill
+    HIP_OR_FAIL(c, K.d_kstat.reserve(1));
+    HIP_OR_FAIL(c, K.d_kmisc.reserve(16));
+    HIP_OR_FAIL(c, K.d_kfb.reserve(1));
+    HIP_OR_FAIL(c, K.d_ktb.reserve((size_t)std::max<int64_t>(tbw * c->cfg.wpb, 16)));
+    if (!K.ev_known) HIP_OR_FAIL(c, hipEventCreateWithFlags(&K.ev_known, hipEventDisableTiming));
     const int64_t off[2] = {0, La};
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_kbytes.p, A.data(), (size_t)La, hipMemcpyHostToDevice, ks));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_koff.p, off, sizeof off, hipMemcpyHostToDevice, ks));
-    HIP_OR_FAIL(c, hipMemcpyAsync(c->d_k2.p, w2.data(), 4 * w2.size(), hipMemcpyHostToDevice, ks));
-    HIP_OR_FAIL(c, hipMemsetAsync(c->d_kmisc.p, 0, 16 * sizeof(int32_t), ks));
+    HIP_OR_FAIL(c, hipMemcpyAsync(K.d_kbytes.p, A.data(), (size_t)La, hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemcpyAsync(K.d_koff.p, off, sizeof off, hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemcpyAsync(K.d_k2.p, w2.data(), 4 * w2.size(), hipMemcpyHostToDevice, ks));
+    HIP_OR_FAIL(c, hipMemsetAsync(K.d_kmisc.p, 0, 16 * sizeof(int32_t), ks));
     nw::KernelArgs ka{};
-    ka.reads = c->d_kbytes.p;
-    ka.offsets = c->d_koff.p;
+    ka.reads = K.d_kbytes.p;
+    ka.offsets = K.d_koff.p;
     ka.n = 1;
     ka.prof = c->cur.prof;
     ka.lut = c->d_lut.p;
@@ -1777,23 +1804,23 @@ int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks) {
     ka.gap_open = c->gap_open;
     ka.gap_extend = c->gap_extend;
     ka.Lb_max = c->lb_max;
-    ka.stats = c->d_kstat.p;
-    ka.tb_global = c->d_ktb.p;
+    ka.stats = K.d_kstat.p;
+    ka.tb_global = K.d_ktb.p;
     ka.tb_wave_bytes = tbw;
-    ka.fallback_list = c->d_kfb.p;
-    ka.fallback_count = c->d_kmisc.p + 8;
-    ka.ops = c->d_kslots.p;
+    ka.fallback_list = K.d_kfb.p;
+    ka.fallback_count = K.d_kmisc.p + 8;
+    ka.ops = K.d_kslots.p;
     ka.ops_slot = nw::kOpsSlot;
     ka.ops_stride = 1;
-    ka.nops = c->d_kmisc.p;
-    ka.spill = c->d_kslots.p + 2 * nw::kOpsSlot;
+    ka.nops = K.d_kmisc.p;
+    ka.spill = K.d_kslots.p + 2 * nw::kOpsSlot;
     ka.spill_cap = 4096;
-    ka.ops_ctl = c->d_kmisc.p + 1;
+    ka.ops_ctl = K.d_kmisc.p + 1;
     nw::LaunchCfg one = c->cfg;
     one.grid = 1;
     HIP_OR_FAIL(c, nw::launch(ka, one, ks));
-    HIP_OR_FAIL(c, hipEventRecord(c->ev_known, ks));
-    c->known_on = true;
+    HIP_OR_FAIL(c, hipEventRecord(K.ev_known, ks));
+    K.on = true;
     return NW_OK;
 }
 
@@ -1802,8 +1829,10 @@ int known_prepare(nw_ctx* c, const std::string& A, hipStream_t ks) {
 // straddle two amplicons; each chunk's kernels use its amplicon's tables).
 int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
              int64_t* ops_off, nw_stat* stats, bool upload, const Groups* groups = nullptr,
-             const PackedInput* pk = nullptr) {
+             const PackedInput* pk = nullptr, const Dual* dual = nullptr) {
     if (!c) return NW_E_INVALID;
+    if (dual && (!groups || groups->refs->size() != 2 || !upload || !pk || !dual->stats2 || !dual->ops_off2))
+        return fail(c, NW_E_INVALID, "bad dual call");
     HostTimer ht("scan configure setup uploads launch wait sync");
     if (!groups && c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
     if (n < 0 || (n > 0 && (!offsets || (upload && !reads && !(pk && pk->packed)) || !stats)) || !ops_off)
@@ -1817,8 +1846,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     int64_t chunk = 262144;
     if (const char* e = std::getenv("CRISPR_NW_CHUNK")) chunk = std::max(1ll, std::atoll(e));
     chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, n));
-    // chunks [lo, hi) of one amplicon group each
-    struct Chunk { int64_t lo, hi; int g; };
+    // chunks [lo, hi) of one amplicon group each; a dual call's pass-1 chunk reads the bytes its
+    // pass-0 twin (chunk `up`) uploaded
+    struct Chunk { int64_t lo, hi; int g; int pass; int64_t up; };
     std::vector<Chunk> chunks;
     const int ngroups = groups ? (int)groups->refs->size() : 1;
     // sizes ramp up and down at both ends of the call (chunk / 4, chunk / 2, ...): the
@@ -1846,15 +1876,35 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         for (auto it = tail.rbegin(); it != tail.rend(); ++it) v.push_back(*it);
         return v;
     };
-    for (int g = 0; g < ngroups; ++g) {
-        const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
-        int64_t lo = g0;
-        for (int64_t len : sizes(g1 - g0)) {
+    if (dual) {
+        int64_t lo = 0;
+        for (int64_t len : sizes(n)) {
             if (len <= 0) continue;
-            chunks.push_back({lo, lo + len, g});
+            const int64_t k0 = (int64_t)chunks.size();
+            chunks.push_back({lo, lo + len, 0, 0, k0});
+            chunks.push_back({lo, lo + len, 1, 1, k0});
             lo += len;
         }
+    } else {
+        for (int g = 0; g < ngroups; ++g) {
+            const int64_t g0 = groups ? (*groups->first)[(size_t)g] : 0, g1 = groups ? (*groups->first)[(size_t)g + 1] : n;
+            int64_t lo = g0;
+            for (int64_t len : sizes(g1 - g0)) {
+                if (len <= 0) continue;
+                chunks.push_back({lo, lo + len, g, 0, (int64_t)chunks.size()});
+                lo += len;
+            }
+        }
     }
+    // chunk k's predecessor of its own pass, the newest chunk of its pass the host has read back
+    // lag chunks behind it, and its index within its pass (a dual call's passes alternate)
+    auto prev_same = [&](int64_t j) { return dual ? j - 2 : j - 1; };
+    auto newest_same = [&](int64_t k, int64_t back) {
+        int64_t j = k - back;
+        if (dual && j >= 0 && chunks[(size_t)j].pass != chunks[(size_t)k].pass) --j;
+        return j;
+    };
+    auto in_pass = [&](int64_t k) { return dual ? k >> 1 : k; };
     const int mode_before = c->out_mode;
     const int64_t base0 = n ? offsets[0] : 0;
     const int64_t nbytes = n ? offsets[n] - base0 : 0;
@@ -1870,6 +1920,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->exact_small = false;
         c->trace_on = false;
         c->known_on = false;
+        c->kcur = 0;
+        c->out_off = 0;
+        c->ctl_pass = 0;
         c->pkc = nw::KernelArgs{};
         c->out_mode = mode_before;
         c->n = 0;
@@ -1893,7 +1946,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
          c->d_exc_byte.reserve((size_t)std::max<int64_t>(pk->n_exc, 1)) != hipSuccess))
         return restore(fail(c, NW_E_NOMEM, "device allocation failed for the packed batch"));
     if (c->d_reads.reserve((size_t)nbytes + 512 + 16) != hipSuccess || c->d_offsets.reserve((size_t)n + 1) != hipSuccess ||
-        c->d_stats.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess)
+        c->d_stats.reserve((size_t)std::max<int64_t>(dual ? 2 * n + 2 : n, 1)) != hipSuccess)
         return restore(fail(c, NW_E_NOMEM, "device allocation failed for %lld reads", (long long)n));
     if ((rc = ops_events(c, (size_t)std::max<int64_t>(nchunks, 1)))) return restore(rc);
     ht.lap(2);
@@ -1939,12 +1992,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     }
     nw_host::Pool& pool = nw_host::Pool::get();
     for (int64_t k = 0; upload && k < nchunks; ++k) {
+        if (chunks[(size_t)k].pass) continue;   // its twin's upload holds its reads
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         const int64_t b0 = offsets[lo], b1 = offsets[hi];
         // chunk 0's lengths went with the group bases; every later chunk's in one copy queued
         // ahead of chunk 1's bases: fewer copies, fewer gaps on the engine (C4 16.9 -> 16.4 ms,
         // C5 17.2 -> 17.0 ms against one lengths copy per chunk)
-        if (lens_on && k == 1) {
+        if (lens_on && k == (dual ? 2 : 1)) {
             HIP_OR_FAIL(c, hipMemcpyAsync(c->d_lens.p + 8 * ngroups_len + 2 * lo, pk->lens + lo, 2 * (size_t)(n - lo),
                                           hipMemcpyHostToDevice, c->s_in));
             h2d_bytes += 2 * (n - lo);
@@ -2100,9 +2154,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // longer queues behind chunk k's tail (C5 pooled call 24.7 -> 21.6 ms, C2 unchanged).
     // (Chunk k's compaction waits for the copy of the runs a set back, ev_out[k - nsets],
     // recorded once the host has read that chunk's total: one set cannot pipeline chunks.)
-    static_assert(kScratchSets >= 3, "the tail split needs three scratch sets");
+    static_assert(kScratchSets >= 6 && kComputeStreams == 3, "the tail split needs three scratch sets (a dual call six)");
     const bool tail_split = several;
-    const int nsets = several ? 3 : 1;
+    // a dual call: three sets per pass (set k % 6 keeps a pass's chunks on its own sets), so a slow
+    // pass-1 chunk never holds back the set a pass-0 chunk needs
+    const int nsets = dual ? 6 : several ? 3 : 1;
     for (int si = 0; si < nsets && !rc; ++si) {
         c->s = &c->sc[si];
         configured = -1;
@@ -2114,7 +2170,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                 have_cfg[(size_t)g] = 1;
             }
         }
-        if (!rc) rc = ops_reserve(c, chunk, n);
+        if (!rc) rc = ops_reserve(c, chunk, dual ? 2 * n + 1 : n);
         // the fallback lists are indexed by the call's read (d_fallback + chunk base)
         if (!rc && (c->s->d_fallback.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess ||
                     c->s->d_fallback2.reserve((size_t)std::max<int64_t>(n, 1)) != hipSuccess))
@@ -2147,13 +2203,20 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         (void)hipStreamSynchronize(c->s_in);
         return restore(rc);
     }
-    HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, 2 * nw::kOpsCtlAll * sizeof(int64_t), c->stream));
     // copies of a known sequence from one alignment (packed classify): the caller's (nw_set_known),
     // or in a resident pass against a new amplicon the one the batch was last aligned against.  The
     // alignment runs on the upload stream of a resident pass (idle), else on the tail stream (its
     // first tail packet comes a chunk's chain later); every compaction waits for it
     c->known_on = false;
-    {
+    c->kset[0].on = c->kset[1].on = false;
+    if (dual) {   // each pass's copies of the other pass's amplicon
+        for (int q = 0; q < 2 && n > 0; ++q) {
+            if ((rc = use_group(q, std::min(chunk, n)))) return restore(rc);
+            if (c->use_diag && (rc = known_prepare(c, (*groups->refs)[(size_t)(1 - q)], c->cstream[2], q)))
+                return restore(rc);
+        }
+    } else {
         const std::string& K = (!c->known_seq.empty() && c->known_seq != c->ref) ? c->known_seq
                                : (!upload && c->resident_ref != c->ref) ? c->resident_ref : c->known_seq;
         const bool packed_classify = (pk != nullptr && upload) || (!upload && c->resident_packed);
@@ -2162,7 +2225,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                 return restore(rc);
         }
     }
-    int64_t total = 0, err = 0;
+    // per pass: the caller's outputs, the runs' running total
+    nw_stat* st_p[2] = {stats, dual ? dual->stats2 : nullptr};
+    int64_t* oo_p[2] = {ops_off, dual ? dual->ops_off2 : nullptr};
+    uint32_t* ops_p[2] = {ops_out, dual ? dual->ops_out2 : nullptr};
+    const int64_t cap_p[2] = {ops_cap, dual ? dual->ops_cap2 : 0};
+    int64_t total_p[2] = {0, 0};
+    int64_t err = 0;
     bool cap_short = false;
     // Chunk k's runs go back once the host has read its total (copy_runs).  (Copying an
     // estimate of them as soon as the chunk is done measured no gain on the 1M-read call and a
@@ -2170,8 +2239,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // The last chunk's records, offsets and runs are written by its compaction kernel straight
     // into the caller's buffers when they are page-locked: no copies and no host round trip
     // after the call's last kernel (2.31 -> 2.27 ms per 1M-read call)
-    const bool direct_out = nchunks >= 1 && host_mapped(stats) && host_mapped(ops_off) &&
-                            (!ops_out || host_mapped(ops_out));
+    const int last_pass = nchunks >= 1 ? chunks[(size_t)nchunks - 1].pass : 0;
+    const bool direct_out = nchunks >= 1 && host_mapped(st_p[last_pass]) && host_mapped(oo_p[last_pass]) &&
+                            (!ops_p[last_pass] || host_mapped(ops_p[last_pass]));
     std::vector<char> direct_done((size_t)std::max<int64_t>(nchunks, 1), 0);
     auto copy_runs = [&](int64_t k) -> int {
         ht.lap(4);
@@ -2180,21 +2250,24 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         const int64_t* h = c->h_ctl + nw::kOpsCtl * k;
         err |= h[3];
         const int64_t cb = h[1], tot = h[2];
-        if (!ops_out) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
-        } else if (cb + tot > ops_cap) cap_short = true;
+        const int pass = chunks[(size_t)k].pass;
+        uint32_t* po = ops_p[pass];
+        if (!po) {   // records only (a scores-only pass, CORE:1740-1741): the runs stay on the device
+        } else if (cb + tot > cap_p[pass]) cap_short = true;
         else if (tot > 0 && !direct_done[(size_t)k])
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_out + cb, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)tot,
+            HIP_OR_FAIL(c, hipMemcpyAsync(po + cb, c->sc[k % nsets].d_staging.p, sizeof(uint32_t) * (size_t)tot,
                                           hipMemcpyDeviceToHost, c->s_out));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_out[(size_t)k], c->s_out));
-        total = cb + tot;
-        if (ops_out) c->ops_d2h_bytes += 4 * tot;
+        total_p[pass] = cb + tot;
+        if (po) c->ops_d2h_bytes += 4 * tot;
         return NW_OK;
     };
     c->ops_d2h_bytes = 0;
     int trace_chunks = 0;
     if (const char* e = std::getenv("CRISPR_NW_TRACE")) trace_chunks = std::atoi(e);
     c->trace_used = 0;
-    const int64_t lag = std::max(1, nsets - 1);
+    // (a dual call: its pass's chunk two back -- the host never waits for the other pass's chunks)
+    const int64_t lag = dual ? 4 : std::max(1, nsets - 1);
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
     // a resident packed batch (nw_align_ops_resident after nw_align_ops_packed): the band path's
@@ -2207,11 +2280,12 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     // the ctl reset and the exceptions' upload are on the first compute stream and s_in:
     // both compute streams start after them
     HIP_OR_FAIL(c, hipEventRecord(c->ev_start, c->stream));
-    for (int k = 1; k < nsets; ++k) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cstream[k], c->ev_start, 0));
+    for (int k = 1; k < std::min(nsets, kComputeStreams); ++k)
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->cstream[k], c->ev_start, 0));
     for (int64_t k = 0; k < nchunks; ++k) {
         const int64_t lo = chunks[(size_t)k].lo, hi = chunks[(size_t)k].hi;
         c->s = &c->sc[k % nsets];
-        c->cs = c->cstream[k % nsets];
+        c->cs = c->cstream[k % std::min(nsets, kComputeStreams)];
         if (tail_split) {
             c->cs = c->cstream[k % 2];
             // the last chunks keep their tail on their own compute stream (no later chunk's bulk
@@ -2221,9 +2295,14 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             // the set's previous chunk (k - 3) must be through its tail
             if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));
         }
-        if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)k], 0));
+        if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)chunks[(size_t)k].up], 0));
         HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
+        const int pass = chunks[(size_t)k].pass;
+        c->out_off = pass ? n + 1 : 0;   // a dual call's pass 1: its records and run offsets after pass 0's
+        c->ctl_pass = pass;
+        c->kcur = dual ? pass : 0;
+        c->known_on = c->kset[c->kcur].on;
         c->pkc = nw::KernelArgs{};
         if (pk && upload && !c->use_diag) {   // the exact kernels read bytes: the chunk's bases -> bytes + exceptions
             const int64_t b0 = offsets[lo], b1 = offsets[hi];
@@ -2271,16 +2350,18 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // The newest chunk the host has read back (k - lag - 1, synchronised in copy_runs)
         // decides from its own counts when it ran both levels; while the level is skipped
         // every 4th chunk runs both again, so input that changes back is noticed.
-        if (adaptive && k >= lag + 1) {   // pooled calls too: one library's amplicons, one read source
-            const int64_t j = k - lag - 1;
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
-            static const int64_t zero[nw::kOpsCtl] = {};
-            const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
-            if (!one_level[(size_t)j]) {
-                const int64_t dp = (h[6] - h[7]) - (hp[6] - hp[7]), l2 = h[5] - hp[5];
+        // (a dual call: its pass's own chunks; the passes' counts accumulate apart)
+        static const int64_t zero[nw::kOpsCtl] = {};
+        const int64_t jn = newest_same(k, lag + 1);
+        const int64_t* hn = jn >= 0 ? c->h_ctl + nw::kOpsCtl * jn : zero;
+        const int64_t* hpn = jn >= 0 && prev_same(jn) >= 0 ? c->h_ctl + nw::kOpsCtl * prev_same(jn) : zero;
+        if (dual) c->skip16 = false;   // (each chunk decides for its own pass)
+        if (adaptive && jn >= 0) {   // pooled calls too: one library's amplicons, one read source
+            if (!one_level[(size_t)jn]) {
+                const int64_t dp = (hn[6] - hn[7]) - (hpn[6] - hpn[7]), l2 = hn[5] - hpn[5];
                 c->skip16 = dp >= 2048 && 2 * l2 > dp;
             } else {
-                c->skip16 = (k & 3) != 0;
+                c->skip16 = (in_pass(k) & 3) != 0;
             }
         }
         one_level[(size_t)k] = c->skip16 && c->diag16_fill.grid > 0;
@@ -2295,12 +2376,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // on a high-priority stream, each chunk's upload split over two streams: +0.01 to +0.58 ms.)
         // the exact kernel's grid: small while the newest chunk read back sent it few reads
         // (after the wide level it gets the rare read no band certifies)
-        c->exact_small = true;
-        if (k >= lag + 1) {
-            const int64_t j = k - lag - 1;
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
-            c->exact_small = h[10] - (j > 0 ? c->h_ctl[nw::kOpsCtl * (j - 1) + 10] : 0) < 256;
-        }
+        c->exact_small = jn < 0 || hn[10] - hpn[10] < 256;
         // the last chunks of a call run without the diagonal pass: their chains' latency (not
         // the GPU's throughput) is what the call waits for at its end, and the pass adds a
         // launch to the chain
@@ -2309,16 +2385,13 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
         // two gaps, not down one diagonal), the next chunks skip it; while skipped, every 4th
         // chunk runs it again
-        if (adaptive && k >= lag + 1) {
-            const int64_t j = k - lag - 1;
-            const int64_t* h = c->h_ctl + nw::kOpsCtl * j;
-            static const int64_t zero[nw::kOpsCtl] = {};
-            const int64_t* hp = j > 0 ? c->h_ctl + nw::kOpsCtl * (j - 1) : zero;
-            if (!no_diag[(size_t)j]) {
-                const int64_t la = h[8] - hp[8], ho = h[9] - hp[9];
+        if (dual) c->diag_off = false;
+        if (adaptive && jn >= 0) {
+            if (!no_diag[(size_t)jn]) {
+                const int64_t la = hn[8] - hpn[8], ho = hn[9] - hpn[9];
                 c->diag_off = la >= 2048 && 2 * ho > la;
             } else {
-                c->diag_off = (k & 3) != 0;
+                c->diag_off = (in_pass(k) & 3) != 0;
             }
         }
         // diagnostics: the last chunks' launches
@@ -2327,11 +2400,12 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // the compaction writes the chunk's ctl into h_ctl[k] itself
         nw::OpsHostOut ho{};
         const bool direct_k = direct_out && k == nchunks - 1;
-        if (direct_k) ho = nw::OpsHostOut{(const int4*)(c->d_stats.p + lo), (int4*)(stats + lo), ops_off + lo, ops_out,
-                                          ops_out ? ops_cap : 0};
+        if (direct_k) ho = nw::OpsHostOut{(const int4*)(c->d_stats.p + c->out_off + lo), (int4*)(st_p[pass] + lo),
+                                          oo_p[pass] + lo, ops_p[pass], ops_p[pass] ? cap_p[pass] : 0};
+        // the compaction after its pass's previous one (the running base of the pass's ctl block)
         if ((rc = launch_range_ops(c, lo, k >= nsets ? c->ev_out[(size_t)(k - nsets)] : nullptr,
-                                   k >= 1 ? c->ev_ce[(size_t)(k - 1)] : nullptr, c->h_ctl + nw::kOpsCtl * k,
-                                   (int)(k & 1), direct_k ? &ho : nullptr)))
+                                   prev_same(k) >= 0 ? c->ev_ce[(size_t)prev_same(k)] : nullptr,
+                                   c->h_ctl + nw::kOpsCtl * k, (int)(in_pass(k) & 1), direct_k ? &ho : nullptr)))
             return restore(rc);
         direct_done[(size_t)k] = direct_k;
         no_diag[(size_t)k] = !c->diag_ran;
@@ -2349,10 +2423,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             }
         if (!direct_k) {
             HIP_OR_FAIL(c, hipStreamWaitEvent(c->s_out, c->ev_ce[(size_t)k], 0));
-            HIP_OR_FAIL(c, hipMemcpyAsync(stats + lo, c->d_stats.p + lo, sizeof(nw::Stat) * (size_t)(hi - lo),
-                                          hipMemcpyDeviceToHost, c->s_out));
-            HIP_OR_FAIL(c, hipMemcpyAsync(ops_off + lo, c->d_opsoff.p + lo, sizeof(int64_t) * (size_t)(hi - lo),
-                                          hipMemcpyDeviceToHost, c->s_out));
+            HIP_OR_FAIL(c, hipMemcpyAsync(st_p[pass] + lo, c->d_stats.p + c->out_off + lo,
+                                          sizeof(nw::Stat) * (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_out));
+            HIP_OR_FAIL(c, hipMemcpyAsync(oo_p[pass] + lo, c->d_opsoff.p + c->out_off + lo,
+                                          sizeof(int64_t) * (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_out));
         }
         c->ops_d2h_bytes += (int64_t)(sizeof(nw::Stat) + sizeof(int64_t)) * (hi - lo);
     }
@@ -2361,9 +2435,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     ht.lap(4);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->s_out));
     ht.lap(6);
-    ops_off[n] = total;
-    if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks)
-        const int64_t* h = c->h_ctl + nw::kOpsCtl * (nchunks - 1);
+    ops_off[n] = total_p[0];
+    if (dual) dual->ops_off2[n] = total_p[1];
+    if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks; a dual call: pass 0's)
+        const int64_t* h = c->h_ctl + nw::kOpsCtl * (dual ? nchunks - 2 : nchunks - 1);
         const bool two = any_diag && c->diag16_fill.grid > 0;
         c->call_counts[0] = any_diag ? n - h[6] : 0;
         c->call_counts[1] = two ? h[6] - h[7] : 0;                // first level: two-level chunks' DP reads
@@ -2377,7 +2452,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->ops_compute_ms = 0.0f;
     c->ops_h2d_bytes = upload ? h2d_bytes : 0;
     if (nchunks > 0) {
-        if (upload) HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)(nchunks - 1)]));
+        if (upload)
+            HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)chunks[(size_t)nchunks - 1].up]));
         for (int64_t k = 0; k < nchunks; ++k) {
             float ms = 0.0f;
             HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
@@ -2393,7 +2469,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (ht.on)   // per chunk (ms from the first upload): upload done, compute start, compute end
             for (int64_t k = 0; k < nchunks; ++k) {
                 float a = 0, b = 0, e = 0;
-                if (upload) (void)hipEventElapsedTime(&a, c->ev_h0, c->ev_in[(size_t)k]);
+                if (upload) (void)hipEventElapsedTime(&a, c->ev_h0, c->ev_in[(size_t)chunks[(size_t)k].up]);
                 (void)hipEventElapsedTime(&b, c->ev_h0, c->ev_cs[(size_t)k]);
                 (void)hipEventElapsedTime(&e, c->ev_h0, c->ev_ce[(size_t)k]);
                 std::fprintf(stderr, "  chunk %lld [%lld reads]: in %.3f start %.3f end %.3f\n", (long long)k,
@@ -2411,8 +2487,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->resident_ref = groups ? std::string() : c->ref;   // a later resident pass's known sequence
     if ((rc = ops_error(c, err))) return restore(rc);
     if (cap_short)
-        return restore(fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs (ops_off holds the offsets)", (long long)ops_cap,
-                            (long long)total));
+        return restore(fail(c, NW_E_CAPACITY, "ops_cap %lld < %lld runs (ops_off holds the offsets)",
+                            (long long)(total_p[0] > ops_cap ? ops_cap : cap_p[1]),
+                            (long long)(total_p[0] > ops_cap ? total_p[0] : total_p[1])));
     return restore(NW_OK);
 }
 
@@ -2594,6 +2671,34 @@ int nw_align_multi_ops_packed_lens(nw_ctx* c, const char* refs, const int64_t* r
     pk.lens = lens;
     return multi_ops(c, refs, ref_offsets, n_refs, nullptr, offsets, ref_of_read, n, ops_out, ops_cap, ops_off, stats,
                      &pk);
+}
+
+int nw_align_dual_ops_packed_lens(nw_ctx* c, const char* ref2, int32_t ref2_len, const uint8_t* packed,
+                                  const int64_t* offsets, const uint16_t* lens, int64_t n, const int64_t* exc_pos,
+                                  const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap,
+                                  int64_t* ops_off, nw_stat* stats, uint32_t* ops_out2, int64_t ops_cap2,
+                                  int64_t* ops_off2, nw_stat* stats2) {
+    if (!c) return NW_E_INVALID;
+    if (c->ref.empty()) return fail(c, NW_E_STATE, "nw_set_reference must come first");
+    if (!ref2 || ref2_len <= 0) return fail(c, NW_E_INVALID, "empty second amplicon");
+    if (ref2_len > kMaxRef) return fail(c, NW_E_UNSUPPORTED, "amplicon length %d exceeds %d", ref2_len, kMaxRef);
+    if (n_exc < 0 || (n > 0 && (!packed || !lens || !stats2 || !ops_off2))) return fail(c, NW_E_INVALID, "bad packed batch");
+    (void)hipSetDevice(c->device);
+    PackedInput pk{packed, exc_pos, exc_byte, n_exc};
+    pk.lens = lens;
+    const std::string ref0 = c->ref;
+    std::vector<std::string> amps{ref0, std::string(ref2, ref2 + ref2_len)};
+    std::vector<Profile> profs;
+    int rc = upload_shared(c);
+    if (!rc) rc = upload_profiles(c, amps, &profs);
+    if (rc) return rc;
+    const std::vector<int64_t> first{0, n, 2 * n};
+    Groups grp{&amps, &profs, &first};
+    const Dual d{ops_out2, ops_cap2, ops_off2, stats2};
+    rc = ops_call(c, nullptr, offsets, n, ops_out, ops_cap, ops_off, stats, true, &grp, &pk, &d);
+    c->ref = ref0;   // the context keeps its amplicon (the arena holds both tables)
+    c->cur = profs[0];
+    return rc;
 }
 
 int nw_ops_times(const nw_ctx* c, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes) {

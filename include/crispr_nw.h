@@ -271,6 +271,18 @@ int nw_pack_reads(const char* reads, const int64_t* offsets, int64_t n, uint8_t*
  * (HDR amplicon, CRISPRessoCORE.py:1808-1828).  offsets / n must be that batch's. */
 int nw_align_ops_resident(nw_ctx* ctx, const int64_t* offsets, int64_t n, uint32_t* ops_out, int64_t ops_cap,
                           int64_t* ops_off, nw_stat* stats);
+/* CRISPResso's dual alignment in one call (CRISPRessoCORE.py:1808-1828: every read against the
+ * amplicon, then against the expected HDR amplicon): the packed batch (nw_align_ops_packed_lens'
+ * layout) crosses PCIe once; each read is aligned against the current reference (records, runs,
+ * run offsets into stats / ops_out / ops_off as nw_align_ops_packed_lens) and against ref2 (into
+ * stats2 / ops_out2 / ops_off2; ops_out2 may be null: records and run offsets only).  The second
+ * pass's chunk of a read range runs as soon as that range is uploaded.  Results equal the two
+ * separate calls'.  The context keeps its reference; the batch stays resident. */
+int nw_align_dual_ops_packed_lens(nw_ctx* ctx, const char* ref2, int32_t ref2_len, const uint8_t* packed,
+                                  const int64_t* offsets, const uint16_t* lens, int64_t n, const int64_t* exc_pos,
+                                  const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap,
+                                  int64_t* ops_off, nw_stat* stats, uint32_t* ops_out2, int64_t ops_cap2,
+                                  int64_t* ops_off2, nw_stat* stats2);
 /* Last nw_align_ops: span of the uploads on the copy stream, sum of the chunks'
  * kernel spans, bytes each way. */
 int nw_ops_times(const nw_ctx* ctx, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes);

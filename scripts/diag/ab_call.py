@@ -3,7 +3,8 @@ of env knobs the library reads per call: calls alternate A, B, A, B ... so that 
 drift (PCIe, host load) hits both alike.
 Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds] [pooled]   (an empty string = defaults;
 c1: the C1-shape call (151 bp windows x 280 bp amplicon); pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads; c3: the dual
-alignment step, packed amplicon pass + resident HDR pass records-only)"""
+alignment step, packed amplicon pass + resident HDR pass records-only; dual: A = that step, B = the
+one-call dual alignment, nw_align_dual_ops_packed_lens; dualonly: the dual call alone)"""
 import os
 import sys
 import time
@@ -26,6 +27,10 @@ pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
 c3 = len(sys.argv) > 4 and sys.argv[4] == "c3"
 c4 = len(sys.argv) > 4 and sys.argv[4] == "c4"
 c1 = len(sys.argv) > 4 and sys.argv[4] == "c1"
+# dual: A = the two-call C3 step, B = the dual call (the env specs still apply); dualonly: the dual call
+dual = len(sys.argv) > 4 and sys.argv[4] in ("dual", "dualonly")
+dualonly = len(sys.argv) > 4 and sys.argv[4] == "dualonly"
+c3 = c3 or dual
 if c1:   # the C1 shape: 151 bp windows of a 280 bp amplicon
     amplicon, buf, off = synth.c1_shape_workload(bench.READS_PER_GPU)
     nr = len(off) - 1
@@ -67,6 +72,10 @@ for i in range(2 * rounds + 4):
     t0 = time.perf_counter()
     if pooled:
         al.align_multi_ops(amps, pr, None, pw.array, out=(stats.array, ops.array, ops_off.array))
+    elif dual and (which == "B" or dualonly):
+        al.set_reference(amplicon)
+        al.align_dual_packed(pr, hdr, out=(stats.array, ops.array, ops_off.array),
+                             out2=(stats2.array, None, ops_off2.array), records_only2=True)
     elif c3:
         al.set_reference(amplicon)
         al.set_known(hdr)

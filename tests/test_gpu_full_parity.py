@@ -5,7 +5,8 @@ pass) and 1812-1828 (HDR pass).
 * C2: the headline's 1M-read batch (seed 2) through nw_align_ops_packed_lens (2-bit
   reads + lengths in, records + runs out);
 * C3: the C3 reads against the amplicon (the same packed call) and, still resident in
-  HBM, against the HDR amplicon (nw_align_ops_resident, with runs and records-only);
+  HBM, against the HDR amplicon (nw_align_ops_resident, with runs and records-only); and
+  both passes of the dual call (nw_align_dual_ops_packed_lens, the bench's C3 step);
 * C5: 96 amplicons x 10k reads in one nw_align_multi_ops_packed_lens call;
 * C4: a 1M-read slice of the C4 generator (native, seed 10: rank 0's shard).
 
@@ -104,6 +105,53 @@ def test_c3_both_passes_every_read(al):
     ob3 = al.align_ops(None, pr.offsets, out=(out3[0], None, out3[2]), resident=True, records_only=True)
     assert every_read_records(ob3.stats, ob2.stats) == 0
     _close(keep, outs1, outs2, outs3)
+
+
+def test_c3_dual_call_every_read(al):
+    """The dual call (nw_align_dual_ops_packed_lens: one upload, the HDR pass's chunks interleaved
+    with the amplicon pass's) against the oracle on every read of both passes, and its records-only
+    form (the bench's C3 step) against the runs form."""
+    amp, hdr, buf, off = synth.c3_workload(READS)
+    pr, keep = _packed(buf, off)
+    n = len(off) - 1
+    outs1, out1 = _pinned_out(n)
+    outs2, out2 = _pinned_out(n)
+    outs3, out3 = _pinned_out(n)
+    outs4, out4 = _pinned_out(n)
+    al.set_reference(amp)
+    ob1, ob2 = al.align_dual_packed(pr, hdr, out=out1, out2=out2)
+    assert al.reference == amp
+    _assert_clean(every_read(amp, buf, off, ob1, THREADS), "C3 dual call, amplicon pass")
+    _assert_clean(every_read(hdr, buf, off, ob2, THREADS), "C3 dual call, HDR pass")
+    ob3, ob4 = al.align_dual_packed(pr, hdr, out=out3, out2=(out4[0], None, out4[2]), records_only2=True)
+    assert every_read_records(ob3.stats, ob1.stats) == 0 and np.array_equal(ob3.ops_off, ob1.ops_off)
+    assert np.array_equal(ob3.ops, ob1.ops)
+    assert every_read_records(ob4.stats, ob2.stats) == 0 and np.array_equal(ob4.ops_off, ob2.ops_off)
+    assert not ob4.has_runs
+    _close(keep, outs1, outs2, outs3, outs4)
+
+
+def test_dual_call_small_and_odd_reads(al):
+    """A one-chunk dual call with N bytes (exceptions of the packed stream) and reads that equal
+    either amplicon: every read of both passes against the oracle."""
+    amp, hdr, buf, off = synth.c3_workload(3000, seed=7)
+    reads = [bytes(buf[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+    reads[17] = reads[17][:40] + b"N" + reads[17][41:]
+    reads[23] = reads[23][:100] + b"NN" + reads[23][102:]
+    reads[31] = amp.encode()
+    reads[37] = hdr.encode()
+    lens = np.array([len(r) for r in reads], np.int64)
+    off2 = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum(lens, out=off2[1:])
+    buf2 = np.frombuffer(b"".join(reads), np.uint8).copy()
+    pr, keep = _packed(buf2, off2)
+    outs1, out1 = _pinned_out(len(reads))
+    outs2, out2 = _pinned_out(len(reads))
+    al.set_reference(amp)
+    ob1, ob2 = al.align_dual_packed(pr, hdr, out=out1, out2=out2)
+    _assert_clean(every_read(amp, buf2, off2, ob1, THREADS), "dual call (small), amplicon pass")
+    _assert_clean(every_read(hdr, buf2, off2, ob2, THREADS), "dual call (small), HDR pass")
+    _close(keep, outs1, outs2)
 
 
 def test_c5_pooled_every_read(al):
