@@ -42,7 +42,8 @@ import numpy as np
 import pandas as pd
 
 from . import _lib, fastq
-from .aligner import AlignmentBatch, GpuAligner, NeedleError, OpsBatch, format_srspair, printed_percent
+from .aligner import (AlignmentBatch, GpuAligner, NeedleError, OpsBatch, default_output_mode, format_srspair,
+                      printed_percent)
 from .needle_options import DEFAULT_NEEDLE_OPTIONS, NeedleOptions, UnsupportedNeedleOption
 
 
@@ -501,21 +502,39 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
         t0 = clock()
         # the HDR amplicon's copies among the reads take one alignment of it in the forward pass
         # (nw_set_known), the reference amplicon's copies in the resident HDR pass (automatic)
-        known = args.expected_hdr_amplicon_seq if native and hasattr(aligner, "set_known") else None
-        if known:
-            aligner.set_known(known)
-        try:
-            fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
-                              _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None, packed=packed)
-        finally:
+        # both passes in one call (nw_align_dual_ops_packed_lens: one upload, the HDR pass's chunks
+        # interleaved with the forward pass's) when no needle file is kept
+        dual = (native and bool(args.expected_hdr_amplicon_seq) and not keep_files and packed is not None
+                and getattr(packed, "lens", None) is not None and hasattr(aligner, "align_dual_packed")
+                and default_output_mode() == "ops")
+        known = args.expected_hdr_amplicon_seq if native and not dual and hasattr(aligner, "set_known") else None
+        rep = None
+        if dual:
+            if aligner.reference != args.amplicon_seq:
+                aligner.set_reference(args.amplicon_seq)
+            try:
+                ob1, ob2 = aligner.align_dual_packed(packed, args.expected_hdr_amplicon_seq, records_only2=True)
+            except NeedleError as exc:
+                raise NeedleException("Needle failed to run, please check the log file.") from exc
+            nl = names if isinstance(names, (list, fastq.NameList)) else list(names)
+            fwd = PassResult(nl, None, ob1, args.amplicon_seq, buf, offsets)
+            rep = PassResult(nl, None, ob2, args.expected_hdr_amplicon_seq, buf, offsets)
+        else:
             if known:
-                aligner.set_known(None)
+                aligner.set_known(known)
+            try:
+                fwd = needle_pass(aligner, args.amplicon_seq, names, buf, offsets, database_id,
+                                  _jp(f"needle_output_{database_id}.txt.gz") if keep_files else None, packed=packed)
+            finally:
+                if known:
+                    aligner.set_known(None)
         tm["align_s"] = clock() - t0
         if args.expected_hdr_amplicon_seq:
             t0 = clock()
-            rep = needle_pass(aligner, args.expected_hdr_amplicon_seq, names, buf, offsets, database_id,
-                              _jp(f"needle_output_repair_{database_id}.txt.gz") if keep_files else None,
-                              just_score=True, resident=native)
+            if rep is None:
+                rep = needle_pass(aligner, args.expected_hdr_amplicon_seq, names, buf, offsets, database_id,
+                                  _jp(f"needle_output_repair_{database_id}.txt.gz") if keep_files else None,
+                                  just_score=True, resident=native)
             tm["align_hdr_s"] = clock() - t0
             t0 = clock()
             df_database = fwd.dataframe("ref")
