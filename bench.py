@@ -902,7 +902,7 @@ def main():
         from crispresso_amd.aligner import pack_2bit
 
         pr = pack_2bit(pb.array, po.array, nthreads=threads, packed=p_packed.array, lens=p_lens.array)
-        kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup)
+        kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
         if rank == 0:
             print(json.dumps({"metric": "kernel-resident aligned reads/s (profiling run, not the bench metric)",
                               "value": n / (kms * 1e-3), "kernel_ms": kms, "phases_ms": phases,
@@ -950,8 +950,10 @@ def main():
     ob.expand(amplicon, pb.array, po.array, nthreads=threads)
     expand_s = time.perf_counter() - t1
 
-    kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup)
-    kms_lw, phases_lw, _, _, _ = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
+    # the call's kernels on the resident batch: its 1M-read call runs the first level's lane walk + stop
+    # summary on every chunk (>= 65536 reads); the wave-per-read walk for reference
+    kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
+    kms_ww, phases_ww, _, _, _ = kernel_pass(al, pr, args.steps, args.warmup)
     geo["fallback_reads"] = counts["band_fallback"]
     geo["exact_kernel_reads"] = counts["exact_kernel"]
 
@@ -1055,14 +1057,13 @@ def main():
             "kernel_rate": {
                 "value": n / (kms * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms, "phases_ms": phases,
                 "path_counts": counts,
-                "note": "the call's own kernels (the wave-per-read walk) + ops compaction on the batch resident in "
-                        "HBM, one launch of each over the batch, outputs left in HBM (HIP events on the aligner's "
-                        "stream)",
+                "note": "the call's own kernels (the first level's lane walk + stop summary, as the call's chunks of "
+                        ">= 65536 reads run them) + ops compaction on the batch resident in HBM, one launch of each "
+                        "over the batch, outputs left in HBM (HIP events on the aligner's stream)",
             },
-            "kernel_rate_lane_walk": {
-                "value": n / (kms_lw * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms_lw, "phases_ms": phases_lw,
-                "note": "the same resident pass with the first level's lane walk + stop summary "
-                        "(nw_batch_set_lane_walk): faster on one long list, no pipelined call runs it (DESIGN.md 4a)",
+            "kernel_rate_wave_walk": {
+                "value": n / (kms_ww * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms_ww, "phases_ms": phases_ww,
+                "note": "the same resident pass with the wave-per-read walk (what the pooled call's small chunks run)",
             },
             "expand": {"ms": expand_s * 1e3, "reads_per_s": n / expand_s, "threads": threads,
                        "note": "nw_expand_ops: the three rows of every read rebuilt from its runs on the host "
@@ -1083,8 +1084,9 @@ def main():
                                    f"{cp['lib_matches_loaded']})") if cp else None,
                 "traffic_kernels": cp["kernels"] if cp else None,
                 "kernel": "the call's kernels over the 1M reads: nw_band_classify<true> + nw_band_segsort + "
-                          "nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1> + nw_band_walk<16> (wave per "
-                          "read) + redo compaction + nw_band_fill/walk<128> (wide level) + nw_align_kernel + "
+                          "nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1, true> + nw_band_walk<16, true> "
+                          "(lane walk + stop summary) + redo compaction + nw_band_fill/walk<128> (wide level) + "
+                          "nw_align_kernel + "
                           "nw_ops_compact; achieved = their resident pass (one launch each), the call itself: "
                           "call_achieved",
                 "kernel_ms_avg": kms,

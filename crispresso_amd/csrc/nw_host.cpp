@@ -198,6 +198,7 @@ struct nw_ctx {
     bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
     bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
+    bool lane_call = false;           // this chunk of ops_call: the lane walk + stop summary (chunks of >= 65536 reads)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -1033,7 +1034,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     a.rowpos = c->cur.rowpos;
     a.end_weight = c->end_weight;
     a.tail_prio = c->tail_prio;
-    a.band_summ = c->lane_walk && c->phases ? 1 : 0;   // resident passes only (nw_batch_run_async)
+    a.band_summ = (c->lane_walk && c->phases) || c->lane_call ? 1 : 0;   // resident passes, the call's large chunks
     a.end_open = c->end_open;
     a.end_extend = c->end_extend;
     a.tb_wave_bytes = c->cfg.tb_mode == nw::TB_GLOBAL_FULL ? nw::tb_bytes_per_wave(c->cur.R, c->lb_max) : 0;
@@ -1920,6 +1921,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->exact_small = false;
         c->trace_on = false;
         c->known_on = false;
+        c->lane_call = false;
         c->kcur = 0;
         c->out_off = 0;
         c->ctl_pass = 0;
@@ -2303,6 +2305,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->ctl_pass = pass;
         c->kcur = dual ? pass : 0;
         c->known_on = c->kset[c->kcur].on;
+        // the first level's lane walk + stop summary on chunks of >= 65536 reads of one
+        // amplicon (in-process A/Bs, wave walk vs lane walk on every such chunk: C2 1.954 vs 1.961 ms,
+        // C3 5.578 vs 5.570, C1 7.082 vs 7.070 -- the same -- while the kernel-resident pass of the
+        // same kernels runs 0.81 -> 0.69 ms; the pooled call's 96 small chunks lost: 16.61 vs 17.15 ms)
+        c->lane_call = (!groups || dual) && hi - lo >= 65536;
         c->pkc = nw::KernelArgs{};
         if (pk && upload && !c->use_diag) {   // the exact kernels read bytes: the chunk's bases -> bytes + exceptions
             const int64_t b0 = offsets[lo], b1 = offsets[hi];
