@@ -665,13 +665,20 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // diagonals of every exact hit of its disjoint 16-base blocks among the amplicon's 16-mers.
         // The wide level then centres its band on them and certifies it (nw_band_walk).  A block
         // with more than 8 hits (a repeat) leaves the read to the exact kernel.
-        int32_t sinfo = 0;
+        int32_t sinfo = 0, sinfo2 = 0;
         if constexpr (PK) {
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
                 !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull)) {
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
+                // the refined certificate's facts (nw_band_walk), for reads whose blocks have at most one
+                // hit each: blocks without a hit, the blocks on each hit diagonal (at most 4), the
+                // cheapest move between two blocks' diagonals in read order -- an increase of d = j - i
+                // by D leaves D read bases unpaired: O + (D - 1) E + m D; a decrease: O + (|D| - 1) E
+                int n0 = 0, nd = 0, shift = 0xffff;
+                bool uniq = true;
+                int dd0 = 0, dd1 = 0, dd2 = 0, dd3 = 0, dc0 = 0, dc1 = 0, dc2 = 0, dc3 = 0;
                 for (int b0 = 0; b0 < nb && ok; b0 += 8) {   // eight blocks' words in flight together
                     unsigned keys[8];
 #pragma unroll
@@ -688,12 +695,43 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                             dmin = min(dmin, d);
                             dmax = max(dmax, d);
                         }
+                        n0 += l == f;
+                        uniq = uniq && l - f <= 1;
+                        if (uniq && l - f == 1) {
+                            const int d = 16 * b - (int)spos[f];
+                            auto mv = [&](int d1) {
+                                const int D = d - d1;
+                                return D > 0 ? a.gap_open + (D - 1) * a.gap_extend + a.band_maxsub * D
+                                             : a.gap_open + (-D - 1) * a.gap_extend;
+                            };
+                            const bool h0 = nd > 0 && dd0 == d, h1 = nd > 1 && dd1 == d, h2 = nd > 2 && dd2 == d,
+                                       h3 = nd > 3 && dd3 == d;
+                            if (nd > 0 && !h0) shift = min(shift, mv(dd0));
+                            if (nd > 1 && !h1) shift = min(shift, mv(dd1));
+                            if (nd > 2 && !h2) shift = min(shift, mv(dd2));
+                            if (nd > 3 && !h3) shift = min(shift, mv(dd3));
+                            dc0 += h0;
+                            dc1 += h1;
+                            dc2 += h2;
+                            dc3 += h3;
+                            if (!(h0 || h1 || h2 || h3)) {
+                                if (nd == 0) { dd0 = d; dc0 = 1; }
+                                else if (nd == 1) { dd1 = d; dc1 = 1; }
+                                else if (nd == 2) { dd2 = d; dc2 = 1; }
+                                else if (nd == 3) { dd3 = d; dc3 = 1; }
+                                uniq = uniq && nd < 4;
+                                ++nd;
+                            }
+                        }
                     }
                 }
-                if (ok && dmax >= dmin && dmax - dmin <= kWideDiags / 2 && nb < 128)
+                if (ok && dmax >= dmin && dmax - dmin <= kWideDiags / 2 && nb < 128) {
                     sinfo = seed_pack(dmin, dmax, nb);
+                    if (uniq) sinfo2 = seed2_pack(n0, max(max(dc0, dc1), max(dc2, dc3)), shift);
+                }
             }
             if (a.seed_info && r < r_end) a.seed_info[r] = sinfo;
+            if (a.seed_info2 && r < r_end) a.seed_info2[r] = sinfo2;
         }
         if (r < r_end)
             a.sort_key[r] = (((exact | sub1 | sub2 | win | known) >> lane) & 1ull)
@@ -2502,9 +2540,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
             const int dexit = min(smin - dlo + 1, dhi - smax + 1);
             const int m = a.band_maxsub;
             const bool plainr = amp_acgt && !(hdr.z & (h ? (REGION_BAD_B | REGION_NP_B) : (REGION_BAD_A | REGION_NP_A)));
-            certified = plainr && seed_valid(si) && dexit >= 1 && a.gap_open >= m && a.gap_open >= a.gap_extend &&
-                        a.gap_extend >= 0 && score > m * (Lb - nb) &&
+            const bool pen_ok = a.gap_open >= m && a.gap_open >= a.gap_extend && a.gap_extend >= 0;
+            certified = plainr && seed_valid(si) && dexit >= 1 && pen_ok && score > m * (Lb - nb) &&
                         score > m * Lb - a.gap_open - (dexit - 1) * a.gap_extend;
+            const int32_t si2 = a.seed_info2 ? a.seed_info2[rd] : 0;
+            if (!certified && plainr && seed_valid(si) && seed2_valid(si2) && dexit >= 1 && pen_ok) {
+                // Refined (round 5): a block not paired as an exact match loses >= m when it can sit
+                // in a free end gap (the first and the last block), else >= w = min(m + x, O, m + O / 2)
+                // -- a mismatch, a deletion opened inside it, or unpaired bases in an insertion whose
+                // open it shares with at most one neighbouring block.  An alignment with a cell outside
+                // the band pairs (a) no block exactly: every block loses; (b) blocks on one diagonal only:
+                // the others lose and it moves >= d_exit diagonals; (c) blocks on two diagonals: it also
+                // pays the cheapest move between them (seed_info2).  S above all three bounds.
+                const int x = 4 * (m / 5), O = a.gap_open;
+                const int w = min(min(m + x, O), m + O / 2);
+                auto lose = [&](int k) { return w * max(0, k - 2) + m * min(k, 2); };
+                const int ex = O + (dexit - 1) * a.gap_extend;
+                const int ba = lose(nb);
+                const int bb = ex + lose(max(0, nb - seed2_cmax(si2)));
+                const int bc = seed2_shift(si2) >= 0xffff ? (1 << 30) : ex + seed2_shift(si2) + lose(seed2_n0(si2));
+                const int loss = m * Lb - score;
+                certified = loss < ba && loss < bb && loss < bc;
+            }
         }
         if (!certified && !bad_code && score > a.band_maxsub * pmax - a.gap_open) {
             // Refined bound: an alignment leaving the band with an internal gap pays at

@@ -83,6 +83,7 @@ struct KernelArgs {
     // than the second level's fill + walk ahead of it.  Decided on the device per chunk.
     int32_t redo_direct;
     int32_t band_from_work;    // the wide level: the band list is the exact kernel's work list (exact_work_read)
+    int32_t* seed_info2;       // [n] the seeded reads' block facts for the refined certificate (seed2_pack; null: off)
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
     // every read's traceback runs (RUN_* << 28 | length, start -> end) go to its slot
     // ops[r * ops_slot ..]; a read with more runs than a slot holds writes them to the
@@ -194,6 +195,16 @@ __host__ __device__ inline bool seed_valid(int32_t s) { return ((unsigned)s >> 3
 __host__ __device__ inline int seed_dmin(int32_t s) { return (int)((unsigned)s & 0x7ffu) - 1024; }
 __host__ __device__ inline int seed_dmax(int32_t s) { return (int)(((unsigned)s >> 11) & 0x7ffu) - 1024; }
 __host__ __device__ inline int seed_blocks(int32_t s) { return (int)(((unsigned)s >> 22) & 0x7fu); }
+// seed_info2 word (reads whose blocks have at most one hit each, on at most 4 diagonals): bit 31
+// valid; the blocks without a hit (7 bits), the most blocks on one diagonal (7 bits), the cheapest
+// move between two blocks' diagonals in read order (16 bits, scaled score; 0xffff: one diagonal)
+__host__ __device__ inline int32_t seed2_pack(int n0, int cmax, int shift) {
+    return (int32_t)(0x80000000u | (unsigned)n0 | ((unsigned)cmax << 7) | ((unsigned)(shift < 0xffff ? shift : 0xffff) << 14));
+}
+__host__ __device__ inline bool seed2_valid(int32_t s) { return ((unsigned)s >> 31) != 0u; }
+__host__ __device__ inline int seed2_n0(int32_t s) { return (int)((unsigned)s & 0x7fu); }
+__host__ __device__ inline int seed2_cmax(int32_t s) { return (int)(((unsigned)s >> 7) & 0x7fu); }
+__host__ __device__ inline int seed2_shift(int32_t s) { return (int)(((unsigned)s >> 14) & 0xffffu); }
 
 // certified diagonal-band fill + walk (nw_band.hip): kBandDiags diagonals per read,
 // two equal-length reads per 16-lane row, reads sorted by length on the device.

@@ -78,6 +78,7 @@ struct Scratch {
     DevBuf<uint8_t> d_tb;              // exact kernel: traceback slabs when they do not fit LDS
     DevBuf<int64_t> d_fallback;        // reads the 16 / 32-diagonal levels gave up on (the wide level's input)
     DevBuf<int32_t> d_seed;            // seeded band: per read of the chunk, its hits' diagonals (seed_pack)
+    DevBuf<int32_t> d_seed2;           // ... and its blocks' facts for the refined certificate (seed2_pack)
     DevBuf<int32_t> d_seed_list;       // seeded band: the chunk's seeded reads (the segment sort's third list)
     DevBuf<int64_t> d_fallback2;       // reads the wide level gave up on (the exact kernel's list)
     DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
@@ -92,7 +93,7 @@ struct Scratch {
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
-        d_tile.release(); d_seed.release(); d_seed_list.release();
+        d_tile.release(); d_seed.release(); d_seed2.release(); d_seed_list.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
@@ -713,6 +714,7 @@ int configure(nw_ctx* c) {
             HIP_OR_FAIL(c, c->s->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
             if (c->seed_on) {
                 HIP_OR_FAIL(c, c->s->d_seed.reserve((size_t)std::max<int64_t>(c->n, 1)));
+                HIP_OR_FAIL(c, c->s->d_seed2.reserve((size_t)std::max<int64_t>(c->n, 1)));
                 HIP_OR_FAIL(c, c->s->d_seed_list.reserve((size_t)std::max<int64_t>(c->n, 1)));
             }
             c->use_diag = true;
@@ -1084,6 +1086,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         c->seed_chunk = c->seed_on && c->pkc.pk_words && c->wide_fill.grid > 0 && c->cur.n_seed > 0;
         if (c->seed_chunk) {
             a.seed_info = c->s->d_seed.p;
+            a.seed_info2 = c->s->d_seed2.p;
             a.seed_keys = c->seed_keys;
             a.seed_list = c->s->d_seed_list.p;
             a.seed_count = c->s->d_fallback_count.p + 7;   // zeroed by nw_band_classify
@@ -2292,7 +2295,10 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             c->cs = c->cstream[k % 2];
             // the last chunks keep their tail on their own compute stream (no later chunk's bulk
             // queues behind it there): their tails overlap instead of queueing on the tail stream
-            c->split_to = c->cstream[2];
+            // (a one-amplicon call keeps each chunk's tail on its compute stream: in-process A/Bs,
+            // C1 shape 5.05 -> 4.49 ms, C2 1.977 -> 1.958 ms; the pooled call's many small chunks and the
+            // dual call keep the tail stream: 16.35 vs 19.14 ms, 5.34 vs 5.46 ms)
+            c->split_to = groups ? c->cstream[2] : nullptr;
             c->split_ev = c->ev_bulk[(size_t)k];
             // the set's previous chunk (k - 3) must be through its tail
             if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));

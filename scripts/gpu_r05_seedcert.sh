@@ -1,0 +1,14 @@
+#!/bin/bash
+# The refined seeded certificate: window / C1-shape parity tests, the C1 call's path counts and time;
+# then the no-tail-stream A/B.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-r05_seedcert}
+mkdir -p $O
+cd $R
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_windows.py \
+  "tests/test_gpu_full_parity.py::test_c1_shape_every_read" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+AB_COUNTS=1 timeout -k 10 200 python3 scripts/diag/ab_call.py "" "" 6 c1 > $O/c1.log 2>&1 || { tail -20 $O/c1.log; exit 1; }
+cat $O/c1.log
+bash scripts/gpu_r05_nosplit.sh r05_nosplit

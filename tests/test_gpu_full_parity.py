@@ -191,7 +191,7 @@ def test_c1_shape_every_read(al):
     counts = al.path_counts()
     _assert_clean(every_read(amp, buf, off, ob, THREADS), "C1 shape")
     # the seeded band takes most reads no window certificate took: the wide level
-    # certifies them, few reach the exact kernel
+    # certifies them (the refined certificate: insertions too), very few reach the exact kernel
     dp = len(off) - 1 - counts["exact_copies"]
-    assert counts["wide128"] > 0.8 * dp and counts["exact_kernel"] < 0.15 * dp, counts
+    assert counts["wide128"] > 0.8 * dp and counts["exact_kernel"] < 0.01 * dp, counts
     _close(keep, outs)
