@@ -101,6 +101,24 @@ __device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned c) {
 }
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) { return ~wave_max_u32(~v); }
 
+// The range [lb, ub) of each of K keys among n sorted keys (LDS): branch-free binary searches in
+// lockstep, one step per power of two from top (the largest <= n; wave-uniform), so every key's two
+// probes of a step are in flight together (K = 8: 16 LDS loads per round trip, not one)
+template <int K>
+__device__ __forceinline__ void sorted_ranges(const unsigned* skey, int n, const unsigned* key, int* lb, int* ub) {
+#pragma unroll
+    for (int t = 0; t < K; ++t) lb[t] = ub[t] = 0;
+    for (int step = n > 0 ? 1 << (31 - __builtin_clz((unsigned)n)) : 0; step > 0; step >>= 1) {
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+            const int pl = lb[t] + step, pu = ub[t] + step;
+            const unsigned kl = skey[min(pl, n) - 1], ku = skey[min(pu, n) - 1];
+            lb[t] = pl <= n && kl < key[t] ? pl : lb[t];
+            ub[t] = pu <= n && ku <= key[t] ? pu : ub[t];
+        }
+    }
+}
+
 }  // namespace
 
 // ---- geometry shared by fill, walk and host --------------------------------------
@@ -341,19 +359,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         return cnt;
     };
     auto ham16 = [&](unsigned x, unsigned y) { const unsigned z = x ^ y; return __builtin_popcount((z | (z >> 1)) & 0x55555555u); };
-    // positions of a 16-mer key among the amplicon's (sorted): [lo, hi)
-    auto seed_range = [&](unsigned key, int* first) -> int {
-        int lo = 0, hi = nseed;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (skey[mid] <= key) lo = mid + 1;
-            else hi = mid;
-        }
-        int f = lo;
-        while (f > 0 && skey[f - 1] == key && lo - f < 8) --f;   // at most 8 offsets (repeats: the DP)
-        *first = f;
-        return lo;
-    };
     // a wavefront batch of the 64 reads r0 .. r0 + 63 (below r_end): lane u holds read r0 + u's
     // offset and length; exc: the reads holding an exception byte (packed input)
     auto batch = [&](long long r0, long long r_end, long long my_off, int my_len, bool exc) {
@@ -595,8 +600,12 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     // substitution cannot hit both); the other end word must then be within one mismatch
                     // -- one word compare rejects most offsets (reads with an indel) before the middle
                     const unsigned key0 = rword(my_off), key1 = rword(my_off + my_len - 16);
-                    int f0, f1;
-                    const int l0 = seed_range(key0, &f0), l1 = seed_range(key1, &f1);
+                    // their offsets among the amplicon's sorted 16-mers: [f, l), the last 8 at most
+                    // (repeats: the DP)
+                    const unsigned kk[2] = {key0, key1};
+                    int lb[2], ub[2];
+                    sorted_ranges<2>(skey, nseed, kk, lb, ub);
+                    const int l0 = ub[0], f0 = max(lb[0], ub[0] - 8), l1 = ub[1], f1 = max(lb[1], ub[1] - 8);
                     for (int i = l0 - 1; i >= f0; --i) {   // offsets descending: the largest exact window first
                         const int s = spos[i];
                         if (s + my_len > La) continue;
@@ -683,13 +692,14 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     unsigned keys[8];
 #pragma unroll
                     for (int t = 0; t < 8; ++t) keys[t] = b0 + t < nb ? rword(my_off + 16 * (b0 + t)) : 0u;
+                    int lbs[8], ubs[8];   // each block's hits among the amplicon's sorted 16-mers: [lb, ub)
+                    sorted_ranges<8>(skey, nseed, keys, lbs, ubs);
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
                         const int b = b0 + t;
                         if (b >= nb || !ok) continue;
-                        int f;
-                        const int l = seed_range(keys[t], &f);
-                        if (f > 0 && skey[f - 1] == keys[t]) ok = false;   // more occurrences than seed_range returns
+                        const int l = ubs[t], f = lbs[t];
+                        if (l - f > 8) ok = false;   // a repeat: more than 8 hits
                         for (int i = f; ok && i < l; ++i) {
                             const int d = 16 * b - (int)spos[i];
                             dmin = min(dmin, d);
