@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const int La = a.La, nd = (La + 3) / 4;
     // the chunk's counters (fallback / redo counts, spill bump and error flag): zeroed
     // here, the first kernel of the chain, instead of by memset launches
-    if (blockIdx.x == 0 && threadIdx.x < 8) a.fallback_count[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 16) a.fallback_count[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 2 && a.ops) a.ops_ctl[threadIdx.x] = 0;
     // packed input, block b: the chunk's reads of call block B = call_lo / kPkBlock + b, [bl, bh)
     // (kPkBlock reads, one per thread; four blocks per group of kLenGroup lengths).  Its lengths'
@@ -1255,15 +1255,40 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
 // a.band_count = a.work_count.
 // The wide level's list ends with the seeded reads (the segment sort's seeded list, sorted by
 // their hits' diagonals, so a pair's two reads share a band).
+// The 32-diagonal level with the seeded list (KernelArgs::seed_l2 == 1): its own list (the redo
+// list, none when the direct hand-off gave it to the wide level; as the only level, the sorted DP
+// list and the diagonal pass's hand-ons), then, from the next even position, the seeded list -- an
+// odd count before it leaves one hole (read by no walk), so no pair mixes a seeded read with another.
+__device__ __forceinline__ long long l2_redo_n(const KernelArgs& a) {
+    return redo_direct_taken(a) ? 0ll : (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
+}
+__device__ __forceinline__ long long l2_seed0(const KernelArgs& a) { return (l2_redo_n(a) + 1) & ~1ll; }
+// The wide level after the 32-diagonal level took the seeded list (seed_l2 == 2): the few seeded reads
+// that level left come first, each as a pair of itself (positions 2q, 2q + 1: the walk takes 2q), so no
+// pair holds reads of distant hits (the seeded list is sorted per sort segment, not across them).
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
+    if (a.band_from_work && a.seed_l2 == 2) return 2 * (long long)*a.seed_count + exact_work_count(a);
     if (a.band_from_work) return exact_work_count(a) + (a.seed_list ? (long long)*a.seed_count : 0ll);
+    if (a.seed_l2 == 1) return l2_seed0(a) + (long long)*a.seed_count;
     return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
+    if (a.band_from_work && a.seed_l2 == 2) {
+        const long long n2 = 2 * (long long)*a.seed_count;
+        if (k < n2) return a.seed_list[k >> 1];
+        k -= n2;
+        if (k < nb) return a.work_list[k];
+        return a.redo_list[k - nb];   // (direct hand-off)
+    }
     if (a.band_from_work) {
         if (k < nb) return a.work_list[k];
         const long long nr = redo_direct_taken(a) ? (long long)*a.redo_count : 0ll;
         return k < nb + nr ? (long long)a.redo_list[k - nb] : (long long)a.seed_list[k - nb - nr];
+    }
+    if (a.seed_l2 == 1) {
+        const long long nr = l2_redo_n(a), s0 = (nr + 1) & ~1ll;
+        if (k >= s0) return (long long)a.seed_list[k - s0];
+        if (k >= nr) --k;   // the hole: its pair's read A again (the pair holds one read)
     }
     return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
 }
@@ -1281,7 +1306,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     using G = BandGeo<W>;
     constexpr int kBL = G::L, kBPW = G::PW, kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if (W == kBandDiags && redo_direct_taken(a)) return;   // second level skipped: its reads go to the wide level
+    // second level skipped: its reads go to the wide level (with the seeded list: that list alone)
+    if (W == kBandDiags && redo_direct_taken(a) && a.seed_l2 != 1) return;
     if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
@@ -1358,14 +1384,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
             act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo, W);
-            if constexpr (TB && W > kBandDiags) {
+            if constexpr (TB && W >= kBandDiags) {
                 // seeded reads (both of the pair): the band centred on their hits' diagonals
                 if (a.seed_info) {
                     const int32_t sa = a.seed_info[ra], sb = a.seed_info[rb];
                     const int lo = min(seed_dmin(sa), seed_dmin(sb)), hi = max(seed_dmax(sa), seed_dmax(sb));
                     const int sdlo = lo - (W - (hi - lo + 1)) / 2;
+                    // the second level's LDS code pads hold columns j >= -(kJPad - 1) and rows i < La + 112
+                    // (the sweep's first and last steps): narrower than the wide level's
+                    const bool pads_ok = W > kBandDiags || (sdlo >= -2 * (kJPad - 3) && max(LbA, LbB) - sdlo < La + 200);
                     if (seed_valid(sa) && seed_valid(sb) && hi - lo + 1 <= W - 2 && LbA <= a.band_lb_cap &&
-                        LbB <= a.band_lb_cap && sdlo <= kBK && sdlo + W - 1 >= 1 - La) {
+                        LbB <= a.band_lb_cap && sdlo <= kBK && sdlo + W - 1 >= 1 - La && pads_ok) {
                         dlo = sdlo;   // (tau = t - dlo + kBK stays >= 0)
                         act = true;
                         seeded = true;
@@ -2377,7 +2406,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
     using G = BandGeo<W>;
     constexpr int kCapBytes = G::CapBytes;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if (W == kBandDiags && redo_direct_taken(a)) return;   // second level skipped: its reads go to the wide level
+    // second level skipped: its reads go to the wide level (with the seeded list: that list alone)
+    if (W == kBandDiags && redo_direct_taken(a) && a.seed_l2 != 1) return;
     if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     constexpr int CW = W > 64 ? W / 64 : 1;   // captures (band diagonals) per lane
     const int La = a.La, E = a.gap_extend;
@@ -2403,7 +2433,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
         if (lane < fb_n) a.fallback_list[base + lane] = fb_v;
         fb_n = 0;
     };
+    // the second level over the seeded list (seed_l2 == 1): positions from l2_s0 on are seeded reads
+    const bool l2s = W == kBandDiags && a.seed_l2 == 1;
+    const long long l2_nr = l2s ? l2_redo_n(a) : 0ll;
+    const long long l2_s0 = l2s ? (l2_nr + 1) & ~1ll : (1ll << 62), l2_hole = (l2_nr & 1) ? l2_nr : -1ll;
+    const long long w2_twins = W > kBandDiags && a.seed_l2 == 2 ? 2 * (long long)*a.seed_count : 0ll;
+    auto seed_done = [&](long long k) {   // a seeded read's record and runs are out
+        if (k >= l2_s0 && lane == 0) a.seed_flags[k - l2_s0] = 0;
+    };
     auto give_up = [&](long long k, long long rd, bool retry) {
+        if (k >= l2_s0) {   // a seeded read: to the wide level, in the seeded list's order (compaction)
+            if (lane == 0) a.seed_flags[k - l2_s0] = 1;
+            return;
+        }
         if (W < kBandDiags && retry && a.redo_flags) {
             // the next level's list keeps the sorted order (nw_band_redo_* compaction):
             // its pairs are reads of similar length, as on this level
@@ -2489,6 +2531,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
     auto process = [&](long long k, const int4 hdr, const int4 hr, const unsigned* cw, int h, long long rd, int Lb,
                        long long off, unsigned char* rbuf) {
         if (W < kBandDiags && a.redo_flags && lane == 0) a.redo_flags[k] = 0;   // give_up may set it
+        if (k == l2_hole || (k < w2_twins && (k & 1))) return;   // the second level's hole, the wide level's twins
         if (Lb <= 0) {
             if (lane == 0) {
                 Stat z = {};
@@ -2538,7 +2581,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
         if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
         bool certified = pmax < 0 || score > a.band_maxsub * pmax;
         const bool bad_code = (hdr.z & (h ? REGION_BAD_B : REGION_BAD_A)) != 0;
-        if (W > kBandDiags && (hdr.z & REGION_SEEDED) && !certified) {
+        if (W >= kBandDiags && (hdr.z & REGION_SEEDED) && !certified) {
             // Seeded band: every exact hit of the read's nb disjoint 16-base blocks
             // lies on diagonals [smin, smax] inside the band.  An alignment with a cell outside the
             // band either has a block paired as an exact match -- on one of those diagonals, so its
@@ -2641,6 +2684,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
                     a.stats[rd] = r;
                 }
                 lds_fence();
+                seed_done(k);
                 return;
             }
         } else {
@@ -2668,6 +2712,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
                     a.stats[rd] = r;
                 }
                 lds_fence();
+                seed_done(k);
                 return;
             }
         }
@@ -2686,6 +2731,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
                             score, ei, ej, a.stats + rd, lane);
         }
         lds_fence();
+        seed_done(k);
     };
     if constexpr (LN && W < kBandDiags) {
         if (a.ops) {
@@ -2753,7 +2799,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
         // the wide level's list entries past its region's capacity: straight to the exact kernel
         const long long nb = (long long)*a.band_count;
         for (long long k2 = khi + (long long)blockIdx.x * wpb + wave; k2 < count; k2 += kstep)
-            give_up(k2, band_list_read(a, k2, nb), false);
+            if (!(k2 < w2_twins && (k2 & 1))) give_up(k2, band_list_read(a, k2, nb), false);
     }
     if (redo_n) flush_redo();
     if (fb_n) flush_fb();

@@ -133,6 +133,11 @@ struct KernelArgs {
     int32_t seed_keys;
     int32_t* seed_list;            // the segment sort's seeded reads (sorted), the wide level's list tail
     int32_t* seed_count;
+    // the seeded list through the 32-diagonal level first: 1 on that level's launches
+    // (its list, then the seeded list); it sets seed_flags[q] for the seeded list's entry q it leaves
+    // to the wide level (clears it for a read it certified), and a compaction keeps those; 0: off
+    int32_t seed_l2;
+    uint8_t* seed_flags;
     const uint32_t* cls_img;       // classify's LDS image of the amplicon (nw_host.cpp cls_image)
     int32_t cls_words;
     int32_t amp_acgt;              // every amplicon byte A C G T (either case)
@@ -282,7 +287,8 @@ struct OpsCounts {
     const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
     const int32_t* handed;     // ... and the reads it handed on
     const int32_t* exact;      // the wide level's give-ups: the exact kernel's reads (null: no wide level)
-    const int32_t* seeded;     // the seeded reads (straight to the wide level; null: none)
+    const int32_t* seeded;     // the seeded reads (to the wide level, or the second level first; null: none)
+    const int32_t* seeded_l2;  // of those, the ones the 32-diagonal level left to the wide level (null: it took none)
 };
 // The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
 // straight into the caller's page-locked buffers (no copies and no host round trip after it).

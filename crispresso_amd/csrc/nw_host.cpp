@@ -80,6 +80,8 @@ struct Scratch {
     DevBuf<int32_t> d_seed;            // seeded band: per read of the chunk, its hits' diagonals (seed_pack)
     DevBuf<int32_t> d_seed2;           // ... and its blocks' facts for the refined certificate (seed2_pack)
     DevBuf<int32_t> d_seed_list;       // seeded band: the chunk's seeded reads (the segment sort's third list)
+    DevBuf<uint8_t> d_seed_flags;      // ... per entry: left to the wide level by the 32-diagonal level
+    DevBuf<int32_t> d_seed_list2;      // ... those entries, in order (the wide level's seeded list)
     DevBuf<int64_t> d_fallback2;       // reads the wide level gave up on (the exact kernel's list)
     DevBuf<int32_t> d_fallback_count;  // [0] fallback count, [1] -, [2] redo count
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
@@ -93,7 +95,7 @@ struct Scratch {
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
-        d_tile.release(); d_seed.release(); d_seed2.release(); d_seed_list.release();
+        d_tile.release(); d_seed.release(); d_seed2.release(); d_seed_list.release(); d_seed_flags.release(); d_seed_list2.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
@@ -184,6 +186,9 @@ struct nw_ctx {
     // (La - Lb >= 16) go to the wide level centred on their 16-mer hits; seed_pairs widens the
     // wide level's region for them, seed_keys their sort keys
     bool seed_on = false, seed_chunk = false;
+    // the seeded list through the second level (32 diagonals, 4 pairs per wavefront) before the wide
+    // level, which takes what it leaves (KernelArgs::seed_l2)
+    bool seed_l2 = true;
     int64_t seed_pairs = 0;
     int32_t seed_keys = 0;
     int64_t diag16_pass_pairs = 0, diag16_stride = 0;
@@ -567,7 +572,7 @@ int configure_long(nw_ctx* c) {
     c->exact_grid = (int)grid;
     c->exact_full = true;
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(16));
     return NW_OK;
 }
 
@@ -636,7 +641,7 @@ int configure(nw_ctx* c) {
         c->use_diag = false;
         c->diag16_fill.grid = 0;
         HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-        HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
+        HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(16));
         return NW_OK;
     }
     const char* kern = std::getenv("CRISPR_NW_KERNEL");   // "diag" (default) | "diag32" | "full" (tests)
@@ -647,7 +652,7 @@ int configure(nw_ctx* c) {
     const int64_t diag_hi = 5ll * c->scale * La + (int64_t)c->gap_extend * (2 * La + 300) + c->gap_open;
     if (want_diag && La <= 1024 && diag_hi < 15000 && c->gap_extend >= 0 &&
         c->gap_open >= c->gap_extend) {
-        const int64_t pairs = (c->n + 1) / 2;
+        const int64_t pairs = (c->n + 2) / 2;   // (the second level's list may hold one hole)
         int64_t cap_bytes = 16ll << 30;
         if (const char* rb = std::getenv("CRISPR_NW_REGION_MB")) cap_bytes = std::max(1ll, std::atoll(rb)) << 20;
         c->diag_lb_cap = La + nw::kBandDiags - 1;
@@ -716,12 +721,14 @@ int configure(nw_ctx* c) {
                 HIP_OR_FAIL(c, c->s->d_seed.reserve((size_t)std::max<int64_t>(c->n, 1)));
                 HIP_OR_FAIL(c, c->s->d_seed2.reserve((size_t)std::max<int64_t>(c->n, 1)));
                 HIP_OR_FAIL(c, c->s->d_seed_list.reserve((size_t)std::max<int64_t>(c->n, 1)));
+                HIP_OR_FAIL(c, c->s->d_seed_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
+                HIP_OR_FAIL(c, c->s->d_seed_list2.reserve((size_t)std::max<int64_t>(c->n, 1)));
             }
             c->use_diag = true;
         }
     }
     HIP_OR_FAIL(c, c->s->d_fallback.reserve((size_t)std::max<int64_t>(c->n, 1)));
-    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(8));
+    HIP_OR_FAIL(c, c->s->d_fallback_count.reserve(16));
     return NW_OK;
 }
 
@@ -1061,7 +1068,7 @@ int launch_range(nw_ctx* c, int64_t base) {
     }
     if (c->use_diag) {
         // length sort, certified band fill + walk per pass, exact int32 kernel on the rest
-        if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs) == hipSuccess
+        if (c->n <= 0) return hipMemsetAsync(c->s->d_fallback_count.p, 0, 16 * sizeof(int32_t), c->cs) == hipSuccess
                                   ? NW_OK : fail(c, NW_E_HIP, "hipMemsetAsync failed");
         a.lut6 = c->d_lut6.p;
         a.band_order = c->s->d_order.p;
@@ -1117,7 +1124,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         tmark(c, "classify+sort");
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
-        const int64_t pairs = (c->n + 1) / 2;
+        const int64_t pairs = (c->n + 2) / 2;   // (the second level's list may hold one hole)
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
         // ranges to the device-side counts.
@@ -1148,6 +1155,10 @@ int launch_range(nw_ctx* c, int64_t base) {
                 al.band_order = c->s->d_redo.p;
                 al.band_count = a.redo_count;
             }
+            if (lvl == 1 && c->seed_chunk && c->seed_l2) {   // then the seeded list
+                al.seed_l2 = 1;
+                al.seed_flags = c->s->d_seed_flags.p;
+            }
             al.band_stride = lvl == 0 ? c->diag16_stride : c->diag_stride;
             const int64_t pp = lvl == 0 ? c->diag16_pass_pairs : c->diag_pass_pairs;
             const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
@@ -1175,6 +1186,21 @@ int launch_range(nw_ctx* c, int64_t base) {
                 c->cs = c->split_to;
             }
         }
+        if (c->seed_chunk && c->seed_l2) {
+            // the seeded reads the 32-diagonal level left, compacted in the seeded list's order (so the
+            // wide level's pairs keep reads of nearby hits): they replace that list
+            nw::KernelArgs ac = a;
+            ac.band_order = c->s->d_seed_list.p;
+            ac.band_count = a.seed_count;
+            ac.tile_count = nullptr;
+            ac.redo_flags = c->s->d_seed_flags.p;
+            ac.redo_list = c->s->d_seed_list2.p;
+            ac.redo_count = c->s->d_fallback_count.p + 8;   // zeroed by nw_band_classify
+            HIP_OR_FAIL(c, nw::launch_redo_compact(ac, c->n, next_epoch(c), c->cs));
+            tmark(c, "seed compact");
+            a.seed_list = ac.redo_list;
+            a.seed_count = ac.redo_count;
+        }
         if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // what the 16 / 32 levels could not certify
         a.work_count = c->s->d_fallback_count.p;
@@ -1197,6 +1223,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             aw.band_pair_hi = c->wide_pairs;
             aw.fallback_list = c->s->d_fallback2.p + base;
             aw.fallback_count = c->s->d_fallback_count.p + 6;   // zeroed by nw_band_classify
+            if (c->seed_chunk && c->seed_l2) aw.seed_l2 = 2;   // the 32-diagonal level's seeded leftovers, one per pair
             HIP_OR_FAIL(c, nw::launch_band(nw::kWideDiags, aw, c->wide_fill, c->wide_walk, c->cs, nullptr));
             tmark(c, "wide");
             a.work_list = aw.fallback_list;
@@ -1207,7 +1234,7 @@ int launch_range(nw_ctx* c, int64_t base) {
         tmark(c, "exact");
         return NW_OK;
     }
-    HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 8 * sizeof(int32_t), c->cs));
+    HIP_OR_FAIL(c, hipMemsetAsync(c->s->d_fallback_count.p, 0, 16 * sizeof(int32_t), c->cs));
     if (c->exact_full) {   // long amplicon: every read through the multi-wave kernel
         if (c->n > 0)
             HIP_OR_FAIL(c, nw::launch_exact(a, c->exact_grid, c->exact_lds, c->exact_tb_lds, c->exact_slab, false,
@@ -1272,6 +1299,7 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
         }
         if (c->wide_fill.grid > 0) cnt.exact = c->s->d_fallback_count.p + 6;
         if (c->seed_chunk) cnt.seeded = c->s->d_fallback_count.p + 7;
+        if (c->seed_chunk && c->seed_l2) cnt.seeded_l2 = c->s->d_fallback_count.p + 8;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
     nw::OpsKnown kn{};
@@ -2109,6 +2137,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                      !c->end_weight && La <= 1024 && cap + 3 + keys <= 2048 &&
                      4 * 17 * (cap + keys + 3) + 128 <= 64 * 1024;   // segsort_lds_bytes (default LDS limit)
         c->seed_keys = c->seed_on ? keys : 0;
+        const char* e2 = std::getenv("CRISPR_NW_SEED32");   // TEMP A/B
+        c->seed_l2 = !(e2 && std::atoi(e2) == 0);
         c->seed_pairs = c->seed_on ? std::min<int64_t>(chunk, n_short) / 2 + 1 : 0;
     }
     ht.lap(0);

@@ -163,9 +163,11 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
         if (direct) fb += *cnt.redo;
         const long long ns = cnt.seeded ? (long long)*cnt.seeded : 0ll;   // seeded: DP reads the wide level takes first
-        ctl[4] += fb + ns;
+        const long long n2 = cnt.seeded_l2 ? ns - (long long)*cnt.seeded_l2 : 0ll;   // ... but the 32-diagonal level's
+        ctl[4] += fb + ns - n2;
         ctl[10] += cnt.exact ? (long long)*cnt.exact : fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
+        ctl[5] += n2;
         const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0) + ns;
         ctl[6] += dp;
         if (cnt.one_level) ctl[7] += dp;

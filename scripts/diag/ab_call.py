@@ -63,6 +63,7 @@ if not pooled:
     al.set_reference(amplicon)
 keys = set(A) | set(B)
 times = {"A": [], "B": []}
+counts = {}
 ref = None
 for i in range(2 * rounds + 4):
     which = "A" if i % 2 == 0 else "B"
@@ -88,6 +89,8 @@ for i in range(2 * rounds + 4):
     dt = time.perf_counter() - t0
     if i >= 4:
         times[which].append(dt * 1e3)
+    if os.environ.get("AB_COUNTS"):
+        counts[which] = al.path_counts()
     out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes(),
            stats2.array.tobytes() if c3 else b"")
     if ref is None:
@@ -96,7 +99,7 @@ for i in range(2 * rounds + 4):
         print("OUTPUT DIFFERS at call", i, which)
         sys.exit(1)
 if os.environ.get("AB_COUNTS"):
-    print("path_counts", al.path_counts(), "ops_times", al.ops_times())
+    print("path_counts A", counts.get("A"), "B", counts.get("B"), "ops_times", al.ops_times())
 for w, spec in (("A", sys.argv[1]), ("B", sys.argv[2])):
     t = np.array(times[w])
     print(f"{w} [{spec}]: median {np.median(t):.3f} ms  min {t.min():.3f}  p90 {np.percentile(t, 90):.3f}  "
