@@ -1033,7 +1033,9 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
     __syncthreads();
     // the seeded keys are the tail of the key range: their prefix past the band list's total is
     // their place in the seeded list
-    const int dpB = KS < NB ? kbase[KS] : dp, dpS = dp - dpB;
+    // the seeded list: an odd segment count gets its last entry twice (a pair of one read: the walks take
+    // its first position), so every pair of that list lies within one segment's sorted run
+    const int dpB = KS < NB ? kbase[KS] : dp, dpS0 = dp - dpB, dpS = dpS0 + (dpS0 & 1);
     const int dpA = misc[3];
     if (wave == 0) {
         const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dpB, &misc[2]);
@@ -1052,7 +1054,11 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
     for (int i = 0; i < 4; ++i) {
         const int k = key[i];
         if (k == KA) a.order_a[baseA + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
-        else if (k >= KS) a.seed_list[baseS + (kbase[k] - dpB) + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
+        else if (k >= KS) {
+            const int q = (kbase[k] - dpB) + cnt[wave * NB + k] + rank[i];
+            a.seed_list[baseS + q] = (int32_t)(r0 + i);
+            if (q == dpS0 - 1 && dpS != dpS0) a.seed_list[baseS + q + 1] = (int32_t)(r0 + i);
+        }
         else if (k != EX) order[base + kbase[k] + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
     }
     if (tid == 0) {
@@ -1263,23 +1269,12 @@ __device__ __forceinline__ long long l2_redo_n(const KernelArgs& a) {
     return redo_direct_taken(a) ? 0ll : (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long l2_seed0(const KernelArgs& a) { return (l2_redo_n(a) + 1) & ~1ll; }
-// The wide level after the 32-diagonal level took the seeded list (seed_l2 == 2): the few seeded reads
-// that level left come first, each as a pair of itself (positions 2q, 2q + 1: the walk takes 2q), so no
-// pair holds reads of distant hits (the seeded list is sorted per sort segment, not across them).
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
-    if (a.band_from_work && a.seed_l2 == 2) return 2 * (long long)*a.seed_count + exact_work_count(a);
     if (a.band_from_work) return exact_work_count(a) + (a.seed_list ? (long long)*a.seed_count : 0ll);
     if (a.seed_l2 == 1) return l2_seed0(a) + (long long)*a.seed_count;
     return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
-    if (a.band_from_work && a.seed_l2 == 2) {
-        const long long n2 = 2 * (long long)*a.seed_count;
-        if (k < n2) return a.seed_list[k >> 1];
-        k -= n2;
-        if (k < nb) return a.work_list[k];
-        return a.redo_list[k - nb];   // (direct hand-off)
-    }
     if (a.band_from_work) {
         if (k < nb) return a.work_list[k];
         const long long nr = redo_direct_taken(a) ? (long long)*a.redo_count : 0ll;
@@ -2436,8 +2431,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
     // the second level over the seeded list (seed_l2 == 1): positions from l2_s0 on are seeded reads
     const bool l2s = W == kBandDiags && a.seed_l2 == 1;
     const long long l2_nr = l2s ? l2_redo_n(a) : 0ll;
-    const long long l2_s0 = l2s ? (l2_nr + 1) & ~1ll : (1ll << 62), l2_hole = (l2_nr & 1) ? l2_nr : -1ll;
-    const long long w2_twins = W > kBandDiags && a.seed_l2 == 2 ? 2 * (long long)*a.seed_count : 0ll;
+    const long long l2_s0 = l2s ? (l2_nr + 1) & ~1ll : (1ll << 62);
     auto seed_done = [&](long long k) {   // a seeded read's record and runs are out
         if (k >= l2_s0 && lane == 0) a.seed_flags[k - l2_s0] = 0;
     };
@@ -2531,7 +2525,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
     auto process = [&](long long k, const int4 hdr, const int4 hr, const unsigned* cw, int h, long long rd, int Lb,
                        long long off, unsigned char* rbuf) {
         if (W < kBandDiags && a.redo_flags && lane == 0) a.redo_flags[k] = 0;   // give_up may set it
-        if (k == l2_hole || (k < w2_twins && (k & 1))) return;   // the second level's hole, the wide level's twins
+        // a pair of one read (the seeded list's padding, the 32-diagonal level's hole): its first position
+        if (W >= kBandDiags && (k & 1) && hr.x == hr.y) {
+            seed_done(k);   // (its flag: the pair's first position decides)
+            return;
+        }
         if (Lb <= 0) {
             if (lane == 0) {
                 Stat z = {};
@@ -2799,7 +2797,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
         // the wide level's list entries past its region's capacity: straight to the exact kernel
         const long long nb = (long long)*a.band_count;
         for (long long k2 = khi + (long long)blockIdx.x * wpb + wave; k2 < count; k2 += kstep)
-            if (!(k2 < w2_twins && (k2 & 1))) give_up(k2, band_list_read(a, k2, nb), false);
+            if (!((k2 & 1) && band_list_read(a, k2 - 1, nb) == band_list_read(a, k2, nb))) give_up(k2, band_list_read(a, k2, nb), false);
     }
     if (redo_n) flush_redo();
     if (fb_n) flush_fb();
@@ -2836,8 +2834,9 @@ __device__ int block_excl_scan_i32(int v, int* total) {
 }
 
 // One launch: flags of block b's 1024 positions, its exclusive prefix by look-back,
-// scatter; the last block writes the count (*redo_count).
-__global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, unsigned epoch) {
+// scatter; the last block writes the count (*redo_count).  pairs: positions 2q, 2q + 1 are kept
+// together when either is flagged (the seeded list's pairs stay pairs).
+__global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, unsigned epoch, int pairs) {
     __shared__ int sh[2];
     if (a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const long long nb = *a.band_count;
@@ -2847,6 +2846,14 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         f[t] = k0 + t < n ? a.redo_flags[k0 + t] : 0;
+    }
+    if (pairs) {   // (k0 is even: positions k0 .. k0 + 3 are two whole pairs)
+        f[0] = f[1] = f[0] | f[1];
+        f[2] = f[3] = f[2] | f[3];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        f[t] = f[t] && k0 + t < n;
         s += f[t];
     }
     if (threadIdx.x == 0) sh[1] = 0;
@@ -2867,9 +2874,9 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
     }
 }
 
-hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s) {
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s, bool pairs) {
     const int nblk = (int)std::max<int64_t>(1, (nmax + kRedoBlock - 1) / kRedoBlock);
-    hipLaunchKernelGGL(nw_band_redo_compact, dim3(nblk), dim3(256), 0, s, a, epoch);
+    hipLaunchKernelGGL(nw_band_redo_compact, dim3(nblk), dim3(256), 0, s, a, epoch, pairs ? 1 : 0);
     return hipGetLastError();
 }
 

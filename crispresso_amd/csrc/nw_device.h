@@ -248,7 +248,7 @@ hipError_t launch_unpack(const uint32_t* packed, int64_t pbyte0, int64_t b0, int
                          const LenSeg* lens = nullptr);
 // the first level's flagged positions -> a.redo_list (sorted order) and *a.redo_count;
 // nmax >= the number of sorted positions (grid size)
-hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s);
+hipError_t launch_redo_compact(const KernelArgs& a, int64_t nmax, unsigned epoch, hipStream_t s, bool pairs = false);
 
 // exact int32 kernel for work lists (nw_exact.hip): one workgroup of exact_waves(La)
 // wavefronts per read; traceback slots in LDS (tb_lds) or a per-block HBM slab of

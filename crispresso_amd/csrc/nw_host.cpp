@@ -1187,8 +1187,9 @@ int launch_range(nw_ctx* c, int64_t base) {
             }
         }
         if (c->seed_chunk && c->seed_l2) {
-            // the seeded reads the 32-diagonal level left, compacted in the seeded list's order (so the
-            // wide level's pairs keep reads of nearby hits): they replace that list
+            // the pairs of seeded reads the 32-diagonal level did not certify both of, compacted in the
+            // seeded list's order (the wide level's pairs are that level's pairs: reads of nearby hits,
+            // one sort segment): they replace that list (a certified partner is aligned again, the same)
             nw::KernelArgs ac = a;
             ac.band_order = c->s->d_seed_list.p;
             ac.band_count = a.seed_count;
@@ -1196,7 +1197,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             ac.redo_flags = c->s->d_seed_flags.p;
             ac.redo_list = c->s->d_seed_list2.p;
             ac.redo_count = c->s->d_fallback_count.p + 8;   // zeroed by nw_band_classify
-            HIP_OR_FAIL(c, nw::launch_redo_compact(ac, c->n, next_epoch(c), c->cs));
+            HIP_OR_FAIL(c, nw::launch_redo_compact(ac, c->n + c->n / 4096 + 2, next_epoch(c), c->cs, true));
             tmark(c, "seed compact");
             a.seed_list = ac.redo_list;
             a.seed_count = ac.redo_count;
@@ -1223,7 +1224,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             aw.band_pair_hi = c->wide_pairs;
             aw.fallback_list = c->s->d_fallback2.p + base;
             aw.fallback_count = c->s->d_fallback_count.p + 6;   // zeroed by nw_band_classify
-            if (c->seed_chunk && c->seed_l2) aw.seed_l2 = 2;   // the 32-diagonal level's seeded leftovers, one per pair
             HIP_OR_FAIL(c, nw::launch_band(nw::kWideDiags, aw, c->wide_fill, c->wide_walk, c->cs, nullptr));
             tmark(c, "wide");
             a.work_list = aw.fallback_list;
