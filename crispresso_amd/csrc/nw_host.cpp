@@ -2137,7 +2137,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                      !c->end_weight && La <= 1024 && cap + 3 + keys <= 2048 &&
                      4 * 17 * (cap + keys + 3) + 128 <= 64 * 1024;   // segsort_lds_bytes (default LDS limit)
         c->seed_keys = c->seed_on ? keys : 0;
-        const char* e2 = std::getenv("CRISPR_NW_SEED32");   // TEMP A/B
+        const char* e2 = std::getenv("CRISPR_NW_SEED32");   // "0": the seeded list straight to the wide level (tests, A/Bs)
         c->seed_l2 = !(e2 && std::atoi(e2) == 0);
         c->seed_pairs = c->seed_on ? std::min<int64_t>(chunk, n_short) / 2 + 1 : 0;
     }

@@ -113,3 +113,54 @@ def test_window_c1_shape_resident_hdr(gpu_aligner_factory):
     a.set_reference(hdr)
     ob2 = a.align_ops(None, pr.offsets, resident=True)
     assert every_read(hdr, buf, off, ob2, threads=8)["mismatches"] == 0
+
+
+def _seeded_mix(amp, seed):
+    """Full-length reads with the parity mix (the 16-diagonal level and its redo list) and window
+    reads (the seeded list): edits the 32-diagonal seeded band certifies, and ones it leaves to the
+    wide level (deletions of 20-40 bases: hits too far apart; insertions of 12-15: the certificate)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    La = len(amp)
+    b1, o1 = synth.reads_from(amp, 5000, seed, synth.PARITY_MIX)
+    reads = [bytes(b1[o1[i]:o1[i + 1]]).decode() for i in range(len(o1) - 1)]
+    b2, o2 = synth.window_reads(amp, 6000, seed + 1)
+    reads += [bytes(b2[o2[i]:o2[i + 1]]).decode() for i in range(len(o2) - 1)]
+    for _ in range(1500):
+        Lb = int(rng.integers(100, La - 60))
+        s = int(rng.integers(0, La - Lb - 40))
+        r = amp[s:s + Lb + 40]
+        kind = int(rng.integers(0, 4))
+        p = int(rng.integers(30, Lb - 30))
+        if kind == 0:
+            r = r[:p] + r[p + int(rng.integers(20, 41)):]
+        elif kind == 1:
+            r = r[:p] + "".join(rng.choice(list("ACGT"), int(rng.integers(12, 16)))) + r[p:Lb]
+        elif kind == 2:   # two indels far apart
+            q = min(p + 50, len(r) - 10)
+            r = r[:p] + r[p + 4:q] + "GATTACA" + r[q:Lb]
+        else:
+            r = _sub(_sub(_sub(r[:Lb], 10), Lb // 2), Lb - 20)
+        reads.append(r)
+    order = rng.permutation(len(reads))
+    return [reads[i] for i in order]
+
+
+@pytest.mark.parametrize("env", [{}, {"CRISPR_NW_DIRECT": "0"}, {"CRISPR_NW_CHUNK": "3001"},
+                                 {"CRISPR_NW_ADAPT": "0", "CRISPR_NW_CHUNK": "4097"}, {"CRISPR_NW_SEED32": "0"}])
+def test_seeded_levels_mixed_lists(gpu_aligner_factory, monkeypatch, env):
+    """The seeded list through the 32-diagonal level: after that level's own list (the
+    redo list, or as the only level the sorted DP list) from an even position -- an odd count leaves a
+    hole --, padded to even per sort segment, its leftovers compacted as whole pairs for the wide level;
+    chunks of odd sizes, both levels forced, the direct hand-off: every read against the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    amp = synth.random_amplicon(280, 31)
+    reads = _seeded_mix(amp, 32)
+    buf, off, pr = _run(amp, reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops_packed(pr)
+    counts = a.path_counts()
+    res = every_read(amp, buf, off, ob, threads=8)
+    assert res["mismatches"] == 0, (res, counts)
+    assert counts["wide128"] > 0, counts
