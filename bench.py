@@ -2,17 +2,26 @@
 """Benchmark: aligned reads/sec, 250 bp amplicon x 1M synthetic reads per GPU.
 
 BASELINE.json metric: "aligned reads/sec (250 bp amplicon x 1M reads) at
-1/2/4/8 MI355X".  SURVEY.md 8d defines it at the boundary of the process it
-replaces (CRISPRessoCORE.py:1791-1806: reads in, alignments out): the read count
-over the wall time of the aligner call, host batch in -> per-read records in
-host memory.  One step = one nw_align_ops_packed call (include/crispr_nw.h) on
-the rank's 1M C2 reads held in pinned host memory as 2 bits per base (+ an
-exception list for non-ACGT bytes; nw_pack_reads makes it from the text, timed
-separately as "ingest_pack"): chunks of reads pipelined over PCIe and through
-the kernels, every read's record (nw_stat) and traceback runs copied back to
-pinned host memory (an exact copy is one run; the host rebuilds the rows from
-the text with nw_expand_ops, timed separately as "expand").  The same call on
-the text (one byte per base, nw_align_ops) is reported as "text_input".
+1/2/4/8 MI355X".  value (round 5 on): whole-job throughput with the rank's batch
+already resident in HBM when the timed region starts, as the build contract asks
+("the PCIe-inclusive rate is never value").  One step = one pass of the hot path
+over the rank's 1M C2 reads held in HBM as 2 bits per base (+ exceptions +
+uint16 lengths, nw_batch_upload_packed, include/crispr_nw.h): classify (exact
+copies, certificates, the DP reads' bytes), length sort, the certified band
+levels with traceback, the wide and exact levels, and the ops compaction --
+every read's record (nw_stat) and traceback runs written to HBM
+(nw_batch_run_async + nw_batch_sync, one launch of each kernel over the batch,
+the kernels the pipelined call runs on its chunks of >= 65536 reads).  K steps
+between barriers, wall clock, max over ranks.
+
+The boundary of SURVEY.md 8d (CRISPRessoCORE.py:1791-1806: host batch in ->
+per-read records in host memory) is reported beside it as "call_pcie": one
+nw_align_ops_packed call on the same batch in pinned host memory, chunks
+pipelined over PCIe (2 bits per base in; records, run offsets and runs back to
+pinned host memory) -- the rate a caller with host buffers sees; it was value
+up to round 4.  The same call on the text (one byte per base, nw_align_ops) is
+"text_input"; nw_pack_reads making the 2-bit batch is "ingest_pack"; the host
+rebuilding the rows from the runs is "expand".
 
 N GPUs: one process per GPU (torch.distributed.run), each aligning its own 1M
 read shard (reads are independent, no collective on the data
@@ -27,11 +36,12 @@ seed 10 + rank, in calls of at most 12.5M reads; at N = 1 one 12.5M-read call,
 ranks by DP cells, crispresso_amd.distributed.cell_partition, one
 nw_align_multi_ops_packed call per rank).
 
-Extra keys: "kernel_rate" (the same kernels + compaction on the batch resident in
-HBM, HIP events), "pcie" (upload span and bytes each way of the timed call),
-"sample_check" (every 100th read of the timed batch re-aligned by the CPU oracle,
-outside the timed region), "roofline" (HBM: algorithmic bytes per pass over the
-kernel-resident pass time; VALU: issue fraction of nw_band_fill<16>),
+Extra keys: "kernel_rate" (the same resident pass timed by HIP events on the
+aligner's stream, per phase and per path), "resident_check" (the timed pass's
+records and runs against the pipelined call's, every read), "sample_check"
+(every 100th read of the call's output re-aligned by the CPU oracle, outside the
+timed region), "roofline" (HBM: algorithmic bytes per pass over the resident
+pass's HIP-event time; VALU: issue fraction of nw_band_fill<16>),
 "cpu_baseline" (the CPU oracle -- a port, EMBOSS is absent -- on bounded samples,
 1 thread and the process's CPU share, rank 0 at N = 1 only); legs either side of the
 path at N = 1: "e2e" (a 1M-read C2 FASTQ.gz through needle.align_reads to the
@@ -62,8 +72,10 @@ READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries (scripts/gpu_pmc_call.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the guide's
 # gfx950 correction) of the TIMED CALL's kernels (every launch of warmup + steps calls, per call) and of the
 # quantification leg's kernels; each records the sha1 of the library it profiled (checked against the one loaded)
-CALL_PMC = os.path.join(ROOT, "profiles", "r05_pmc", "summary_call.json")
-QUANT_PMC = os.path.join(ROOT, "profiles", "r05_pmc", "summary_quant.json")
+PMC_DIR = os.path.join(ROOT, "profiles", "r05_pmc2")
+RESIDENT_PMC = os.path.join(PMC_DIR, "summary_resident.json")   # bench.py --kernel-only: the value's pass
+CALL_PMC = os.path.join(PMC_DIR, "summary_call.json")           # bench.py --skip-kernel-pass: call_pcie's calls
+QUANT_PMC = os.path.join(PMC_DIR, "summary_quant.json")
 LIB_SO = os.path.join(ROOT, "crispresso_amd", "lib", "libcrispr_nw.so")
 AMPLICON_LEN = 250
 
@@ -490,6 +502,7 @@ def c1_shape_leg(al, n_reads, steps, warmup, threads, sample_every):
     return res
 
 
+RESIDENT_WARM_S = 0.2   # untimed seconds of resident passes before the headline's timed steps (steady clocks)
 LEG_WARM_S = 0.5   # untimed seconds of calls before a leg's timed steps (steady GPU clocks)
 
 
@@ -919,7 +932,7 @@ def main():
     def headline_call():
         state["ob"] = al.align_ops_packed(pr, out=out)   # synchronous: records + runs are in host memory
 
-    elapsed = timed_calls(dist, headline_call, args.steps, args.warmup)
+    elapsed_call = timed_calls(dist, headline_call, args.steps, args.warmup)
     ob = state["ob"]
     pcie = al.ops_times()
     n_runs = int(ob.ops_off[n])
@@ -928,7 +941,8 @@ def main():
     if args.skip_kernel_pass:   # tracing / call A/B: the timed calls only
         if rank == 0:
             print(json.dumps({"metric": "aligned reads/s (timed calls only, --skip-kernel-pass)",
-                              "value": n * world * args.steps / elapsed, "ms_per_step": elapsed / args.steps * 1e3,
+                              "value": n * world * args.steps / elapsed_call,
+                              "ms_per_step": elapsed_call / args.steps * 1e3,
                               "n_gpus": world, "pcie": pcie, "path_counts": call_counts}), flush=True)
         al.close()
         return
@@ -950,8 +964,29 @@ def main():
     ob.expand(amplicon, pb.array, po.array, nthreads=threads)
     expand_s = time.perf_counter() - t1
 
-    # the call's kernels on the resident batch: its 1M-read call runs the first level's lane walk + stop
-    # summary on every chunk (>= 65536 reads); the wave-per-read walk for reference
+    # value: the hot path over the batch resident in HBM (wall clock, barriers, max over ranks); the
+    # 1M-read call runs the first level's lane walk + stop summary on every chunk (>= 65536 reads,
+    # DESIGN.md 4a), so the resident pass does too
+    al.upload_packed(pr)
+    al.set_lane_walk(True)
+
+    def resident_step():
+        al.run_async()
+        al.sync()   # records + runs of every read in HBM
+
+    elapsed = timed_calls(dist, resident_step, args.steps, args.warmup, warm_s=RESIDENT_WARM_S)
+    res = al.download_ops(n)
+    n_res = int(res.ops_off[n])
+    resident_check = {
+        "reads": n, "runs": n_res,
+        "same_as_call": bool(n_res == n_runs and np.array_equal(res.ops_off, ob.ops_off[:n + 1])
+                             and np.array_equal(res.stats, ob.stats) and np.array_equal(res.ops[:n_res], ob.ops[:n_runs])),
+        "what": "every record, run offset and run of the timed resident pass (downloaded after it) against the "
+                "pipelined call's output on the same reads (which sample_check holds against the oracle)",
+    }
+    del res
+    al.set_lane_walk(False)
+    # the same pass by HIP events (per phase), and with the wave-per-read walk for reference
     kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
     kms_ww, phases_ww, _, _, _ = kernel_pass(al, pr, args.steps, args.warmup)
     geo["fallback_reads"] = counts["band_fallback"]
@@ -1001,15 +1036,19 @@ def main():
             except Exception as exc:
                 legs[name] = {"error": f"{type(exc).__name__}: {exc}"}
 
-    # the call's own kernels: HBM traffic and the fill<16> VALU count per call (PMC of the timed call)
-    cp = pmc_per_call(CALL_PMC, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
+    # HBM traffic and the fill<16> VALU count per pass of the timed resident pass (PMC of bench.py
+    # --kernel-only: the same kernels, one launch each per pass); the call's per-call traffic beside it
+    aligner_kernel = lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k  # noqa: E731
+    cp = pmc_per_call(RESIDENT_PMC, aligner_kernel)
+    ccp = pmc_per_call(CALL_PMC, aligner_kernel)
     traffic = cp["traffic"] if cp else None
     fill_valu = cp["valu_fill16"] if cp else None
     lens = np.diff(offsets)
     cells = band_cells(counts, AMPLICON_LEN, float(lens.mean()) if n else 0.0)
     pass_gbs = algo_bytes / (kms * 1e-3) / 1e9
     ms_step = elapsed / args.steps * 1e3
-    call_gbs = algo_bytes / (ms_step * 1e-3) / 1e9
+    ms_call = elapsed_call / args.steps * 1e3
+    call_gbs = algo_bytes / (ms_call * 1e-3) / 1e9
     fill_ms = phases["fill16_ms"]
     value = n * world * args.steps / elapsed
     if rank == 0:
@@ -1029,15 +1068,23 @@ def main():
             "data": "synthetic (SURVEY 8d C2 mix: 60% exact, 20% 1-3 subs, 10% del, 5% ins, 5% 1% noise)",
             "config": {
                 "workload": f"C2: {n} synthetic ~250 bp reads x 250 bp amplicon per GPU, EMBOSS needle semantics "
-                            "(EDNAFULL, gapopen 10, gapextend 0.5, free end gaps); step = one nw_align_ops_packed "
-                            "call, pinned host reads (2 bits per base) in -> records + traceback runs in pinned host "
-                            "memory",
+                            "(EDNAFULL, gapopen 10, gapextend 0.5, free end gaps); step = one pass of the hot path over "
+                            "the batch resident in HBM (2 bits per base + lengths): every read's record + traceback "
+                            "runs written to HBM (nw_batch_run_async + nw_batch_sync); the PCIe-inclusive call "
+                            "(pinned host batch in -> pinned host records out) is call_pcie",
                 "reads_per_gpu": n,
                 "amplicon_len": AMPLICON_LEN,
                 "parallelism": f"read shards x{world} (no collective on the data path; gloo host barrier)",
                 "kernel_geometry": geo,
             },
-            "path_counts": call_counts,
+            "resident_check": resident_check,
+            "call_pcie": {
+                "value": n * world * args.steps / elapsed_call, "unit": "aligned reads/s", "ms_per_step": ms_call,
+                "path_counts": call_counts,
+                "note": "SURVEY 8d's boundary: one nw_align_ops_packed call per step, the pinned host batch (2 bits "
+                        "per base) in -> records + runs in pinned host memory, chunks pipelined over PCIe (value up "
+                        "to round 4); same barriers and max over ranks",
+            },
             "host_placement": place,
             "ingest_pack": {"ms": pack_s * 1e3, "bases_per_s": (int(offsets[-1]) - int(offsets[0])) / pack_s,
                             "threads": threads, "exceptions": int(len(pr.exc_pos)),
@@ -1051,7 +1098,7 @@ def main():
                 "h2d_gbs": pcie["h2d_bytes"] / max(pcie["h2d_ms"], 1e-9) / 1e6,
                 "d2h_bytes": pcie["d2h_bytes"], "compute_ms_in_call": pcie["compute_ms"],
                 "runs_per_read": n_runs / max(n, 1),
-                "note": "last timed call: upload span on the copy stream; d2h = records (32 B) + run offsets (8 B) "
+                "note": "last timed call_pcie call: upload span on the copy stream; d2h = records (32 B) + run offsets (8 B) "
                         "per read + 4 B per run; compute = the chunks' kernel spans summed (overlapped with the copies)",
             },
             "kernel_rate": {
@@ -1075,24 +1122,29 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": pass_gbs / HBM_PEAK_GBS,
-                "call_achieved": call_gbs,
+                "call_achieved": call_gbs,   # the same bytes over call_pcie's ms_per_step
                 "call_frac": call_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": (f"{cp['source']} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py "
-                                   f"--skip-kernel-pass: every launch of {cp['calls_profiled']} timed calls, summed "
-                                   f"per call; library sha1 {cp['lib_sha1']}, matches the loaded one: "
+                                   f"--kernel-only: every launch of {cp['calls_profiled']} resident passes, summed "
+                                   f"per pass; library sha1 {cp['lib_sha1']}, matches the loaded one: "
                                    f"{cp['lib_matches_loaded']})") if cp else None,
                 "traffic_kernels": cp["kernels"] if cp else None,
-                "kernel": "the call's kernels over the 1M reads: nw_band_classify<true> + nw_band_segsort + "
-                          "nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1, true> + nw_band_walk<16, true> "
-                          "(lane walk + stop summary) + redo compaction + nw_band_fill/walk<128> (wide level) + "
-                          "nw_align_kernel + "
-                          "nw_ops_compact; achieved = their resident pass (one launch each), the call itself: "
-                          "call_achieved",
+                "call_traffic": ccp["traffic"] if ccp else None,
+                "call_traffic_source": (f"{ccp['source']} (bench.py --skip-kernel-pass: every launch of "
+                                        f"{ccp['calls_profiled']} call_pcie calls, summed per call; library sha1 "
+                                        f"{ccp['lib_sha1']}, matches the loaded one: {ccp['lib_matches_loaded']})")
+                                       if ccp else None,
+                "kernel": "the timed pass's kernels over the 1M resident reads: nw_band_classify<true> + "
+                          "nw_band_segsort + nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1, true> + "
+                          "nw_band_walk<16, true> (lane walk + stop summary) + redo compaction + nw_band_fill/walk<32> "
+                          "+ nw_band_fill/walk<128> (wide level) + nw_align_kernel + nw_ops_compact, one launch each "
+                          "(the kernels call_pcie runs per chunk of >= 65536 reads); call_achieved: the same bytes over "
+                          "call_pcie's time",
                 "kernel_ms_avg": kms,
                 "achieved_def": "algorithmic bytes of the pass / its device time (HIP events on the aligner's "
-                                "stream, batch resident in HBM); call_achieved: the same bytes / ms_per_step (the "
-                                "whole call: PCIe both ways, host scan, every kernel)",
+                                "stream, batch resident in HBM); call_achieved: the same bytes / call_pcie.ms_per_step "
+                                "(the whole call: PCIe both ways, host scan, every kernel)",
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",
                 "valu": {

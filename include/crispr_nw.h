@@ -124,9 +124,10 @@ int nw_batch_upload(nw_ctx* ctx, const char* reads, const int64_t* offsets, int6
 /* nw_batch_upload for a batch in nw_align_ops_packed_lens' layout (2 bits per base by batch
  * position + exceptions + uint16 lengths; NW_OUT_OPS only): runs then execute the kernels of
  * the packed call on the resident batch (classify decodes the reads, rebuilds their offsets
- * from the lengths and writes the bytes of the reads that need the DP only), so
- * nw_batch_run_async times exactly the pipelined call's kernels.  nw_batch_device_ops unpacks
- * every read's bytes first. */
+ * from the lengths and writes the bytes of the reads that need the DP only): one launch of each
+ * of the pipelined call's kernels over the whole batch (with nw_batch_set_lane_walk on, the lane
+ * walk + stop summary the call's chunks of >= 65536 reads run; off, the wave walk its smaller
+ * chunks run).  nw_batch_device_ops unpacks every read's bytes first. */
 int nw_batch_upload_packed(nw_ctx* ctx, const uint8_t* packed, const int64_t* offsets, const uint16_t* lens, int64_t n,
                            const int64_t* exc_pos, const uint8_t* exc_byte, int64_t n_exc);
 int nw_batch_run_async(nw_ctx* ctx);
@@ -305,9 +306,9 @@ int nw_host_threads(void);
  * none is set.  Results are those of aligning every read; used when both sequences are A C G T,
  * of one length <= 256, and the input is packed. */
 int nw_set_known(nw_ctx* ctx, const char* seq, int32_t len);
-/* Resident passes (nw_batch_run_async) only: the first band level's lane walk and the stop
- * summary its fill writes (on != 0), instead of the wave-per-read walk every pipelined call
- * runs.  The bench times both; off by default. */
+/* Resident passes (nw_batch_run_async): the first band level's lane walk and the stop summary
+ * its fill writes (on != 0) -- what a pipelined call runs on its chunks of >= 65536 reads of one
+ * amplicon -- instead of the wave-per-read walk (smaller chunks, pooled calls).  Off by default. */
 int nw_batch_set_lane_walk(nw_ctx* ctx, int on);
 
 /* The three alignment rows of n reads from their runs (host, nthreads threads;

@@ -13,7 +13,8 @@ timeout -k 10 700 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail 
 python3 - "$OUT/bench.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print("value", d["value"], "ms", d["ms_per_step"])
+print("value", d["value"], "ms", d["ms_per_step"], "resident_check", (d.get("resident_check") or {}).get("same_as_call"))
+print("call_pcie", {x: (d.get("call_pcie") or {}).get(x) for x in ("value", "ms_per_step")})
 for k in ("c4_shard", "pooled", "dual_alignment", "c1_shape", "e2e", "downstream_quantification", "upstream_merge"):
     v = d.get(k) or {}
     print(k, {x: v.get(x) for x in ("value", "ms_per_step", "error") if x in v},

@@ -1,6 +1,6 @@
 """bench.py's host-side pieces (no GPU): the PMC traffic it reports comes from the committed
-rocprofv3 summaries of the TIMED CALL's kernels and of the quantification leg (per call), and
-records which library build they profiled."""
+rocprofv3 summaries of the TIMED resident pass's kernels (per pass), of call_pcie's calls and of
+the quantification leg (per call), and records which library build they profiled."""
 import importlib.util
 import json
 import os
@@ -15,14 +15,20 @@ def load_bench():
     return mod
 
 
-def test_call_pmc_summary_covers_the_calls_kernels():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("which", ["RESIDENT_PMC", "CALL_PMC"])
+def test_pmc_summary_covers_the_timed_kernels(which):
     b = load_bench()
-    with open(b.CALL_PMC) as f:
+    path = getattr(b, which)
+    with open(path) as f:
         summ = json.load(f)
     assert summ["_meta"]["calls"] and summ["_meta"]["lib_sha1"]
-    for k in ("nw_band_classify", "nw_band_segsort", "nw_band_fill<16, 1", "nw_band_walk<16", "nw_ops_compact"):
+    for k in ("nw_band_classify", "nw_band_segsort", "nw_band_fill<16, 1, true>", "nw_band_walk<16, true>",
+              "nw_ops_compact"):
         assert any(k in name for name in summ), k
-    cp = b.pmc_per_call(b.CALL_PMC, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
+    cp = b.pmc_per_call(path, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
     assert cp["traffic"] > 5e7 and cp["valu_fill16"] > 0   # ~0.1-1.5 GB per 1M C2 reads
 
 

@@ -631,3 +631,55 @@ def test_known_copies_resident_pass(gpu_aligner_factory, hdr_kind):
     ob3 = a.align_ops(None, off, resident=True, records_only=True)
     for f in FIELDS:
         np.testing.assert_array_equal(ob3.stats[f], ob2.stats[f], err_msg=f)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["hdr", "parity", "long_indels"])
+def test_certificate_split_resident_pass(gpu_aligner_factory, oracle, kind, monkeypatch):
+    """The certificate split of a resident lane-walk pass (the first level's certificates alone,
+    then its walk while the second and wide levels run on a side stream) gives the
+    records and runs of the same pass without it (CRISPR_NW_CERTSPLIT=0), every read, and every
+    read against the oracle.  "hdr": reads against the HDR amplicon (most DP reads leave the first
+    level: the second level runs, no direct hand-off); "parity": N codes and IUPAC bytes (reads
+    the split hands on without the wave path's refined certificate, the wave path in the walk);
+    "long_indels": deletions and insertions the wide level takes."""
+    from crispresso_amd.aligner import pack_2bit
+    from tests.every_read import every_read
+
+    n = 200_000
+    if kind == "hdr":
+        amp, hdr, buf, off = synth.c3_workload(n)
+        ref = hdr
+    elif kind == "parity":
+        ref = synth.random_amplicon(250, 11)
+        buf, off = synth.reads_from(ref, n, 12, synth.PARITY_MIX)
+    else:
+        ref = synth.random_amplicon(250, 13)
+        buf, off = synth.reads_from(ref, n, 14)
+        # every read with a length change of >= 10 bases (the wide level's share of C2) four times over
+        lens = np.diff(off)
+        idx = np.flatnonzero(np.abs(lens - 250) >= 10)
+        keep = np.concatenate([np.arange(len(lens))[: n // 2], np.tile(idx, 4)])
+        parts = [buf[off[i]:off[i + 1]] for i in keep]
+        buf = np.concatenate(parts)
+        off = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64)
+    n = len(off) - 1
+    pr = pack_2bit(buf, off)
+    res = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("CRISPR_NW_CERTSPLIT", split)
+        a = gpu_aligner_factory()
+        a.set_reference(ref)
+        a.upload_packed(pr)
+        a.set_lane_walk(True)
+        a.run_async()
+        a.sync()
+        res[split] = a.download_ops(n)
+        a.set_lane_walk(False)
+    on, off_ = res["1"], res["0"]
+    np.testing.assert_array_equal(on.ops_off, off_.ops_off)
+    for f in FIELDS:
+        np.testing.assert_array_equal(on.stats[f], off_.stats[f], err_msg=f)
+    np.testing.assert_array_equal(on.ops[:int(on.ops_off[n])], off_.ops[:int(off_.ops_off[n])])
+    chk = every_read(ref, buf, off, on, threads=16)
+    assert chk["mismatches"] == 0, chk
