@@ -2019,6 +2019,9 @@ constexpr int kMRows = 2;   // tile rows per M round of the lane walk (<= 4: 32 
 // its chunks of >= 65536 reads of one amplicon (the call's time the same, C2 1.961 vs 1.954 ms; its
 // kernels faster); the pooled call's small chunks keep the wave walk (C5 17.15 vs 16.61 ms with the
 // lane walk on every chunk, in-process A/Bs).  KernelArgs::band_summ selects it per launch.
+// (Running it twice -- the certificates alone, then, while the next levels ran on a side stream, the
+// walk of what they kept -- measured no gain: resident pass 0.700-0.703 vs 0.690-0.700 ms, C2 call
+// 1.951 vs 1.956 ms; the walk and the wide level slowed each other to the serial sum)
 template <int W, class Defer>
 __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, unsigned char* wb,
                            const unsigned char* amp_lds, bool amp_acgt, int sc5, const Defer& defer) {
@@ -2034,11 +2037,6 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
         // 0: done, 1: the wave path, 2: redo list (retry), 3: fallback list
         int fate = 0;
         long long rd = 0;
-        // cert_mode 1 / 2: a fate the certificates decide (2, 3) is routed by the first launch alone;
-        // the first launch walks nothing, the second walks what they kept
-        const int cm = a.cert_mode;
-        const bool walk_it = cm != 1;
-        bool routed = false;   // the fate came from the certificates (or the pair / the read's codes), not the walk
         if (live) {
             const unsigned char* region = a.band_region + ((k >> 1) - a.band_pair_lo) * a.band_stride;
             const int4 hdr = *(const int4*)region, hr = *(const int4*)(region + 16), ho = *(const int4*)(region + 32);
@@ -2047,18 +2045,14 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
             const int Lb = h ? hr.w : hr.z;
             if (a.redo_flags) a.redo_flags[k] = 0;
             if (Lb <= 0) {
-                if (cm != 1) {   // (the second launch writes it)
                 Stat z = {};
                 z.flags = FLAG_EMPTY;
                 a.stats[rd] = z;
                 a.nops[rd] = 0;
-                }
             } else if (hdr.z & kPairInactive) {
                 fate = 2;
-                routed = true;
             } else if (Lb > rcap) {
                 fate = 3;
-                routed = true;
             } else {
                 const int dlo = hdr.y, tau0 = hdr.x;
                 // start cell: the largest end key over the band's diagonals (their last cells)
@@ -2121,8 +2115,7 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                     // band whose overlap could reach the score sums below it -- a plain read's diagonal d
                     // sums to m P - 9 sc5 mis_d; other reads: the wave path
                     if (!plain) {
-                        fate = cm ? 2 : 1;   // split: the wave path's refined certificate is not run; handed on
-                        routed = cm != 0;
+                        fate = 1;
                     } else {
                         cert = true;
                         for (int side = 0; side < 2 && cert; ++side) {
@@ -2142,8 +2135,6 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                 if (fate != 0) {
                 } else if (bad_code || !cert) {
                     fate = bad_code ? 3 : 2;
-                    routed = true;
-                } else if (!walk_it) {
                 } else if (!plain || nd >= 1024) {
                     fate = 1;
                 } else {
@@ -2379,9 +2370,6 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                 }
             }
         }
-        // the split's second launch: what the certificates routed (the first launch's) is not its own; a
-        // read it gives up while walking goes to the exact kernel's list (the next levels run meanwhile)
-        if (cm == 2 && fate >= 2) fate = routed ? 0 : 3;
         // the lists: one atomic per list and wavefront (redo flags instead when the level keeps them)
         const unsigned long long to_redo = __ballot(fate == 2 && !a.redo_flags), to_fb = __ballot(fate == 3);
         if (fate == 2 && a.redo_flags) a.redo_flags[k] = 1;
@@ -2461,7 +2449,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
             // the next level's list keeps the sorted order (nw_band_redo_* compaction):
             // its pairs are reads of similar length, as on this level
             if (lane == 0) a.redo_flags[k] = 1;
-        } else if (W < kBandDiags && retry && a.cert_mode != 2) {   // (the split's walk: the exact kernel's list)
+        } else if (W < kBandDiags && retry) {
             if (lane == redo_n) redo_v = (int)rd;
             if (++redo_n == 64) flush_redo();
         } else {
@@ -2950,12 +2938,11 @@ int64_t band_lookback_words(int64_t n) {
 }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill, int parts) {
+                       hipEvent_t after_fill) {
     // the lane walk (and the stop summary its fill writes for it) when the context asked for it
     KernelArgs al = a;
     al.band_summ = W == 16 && a.ops && a.band_summ;
-    if (!(parts & 1)) {   // the walk alone (the certificate split's launches)
-    } else if (al.band_summ)
+    if (al.band_summ)
         hipLaunchKernelGGL((nw_band_fill<16, 1, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, al);
     else if (W == 16)
         hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
@@ -2966,7 +2953,6 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
-    if (!(parts & 2)) return hipSuccess;
     if (al.band_summ)
         hipLaunchKernelGGL((nw_band_walk<16, true>), dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, al);
     else if (W == 16)

@@ -56,10 +56,6 @@ struct KernelArgs {
     int64_t band_stride;
     int32_t band_words;            // traceback words per lane and pair
     int32_t band_summ;             // the first level's fill writes the stop summary the lane walk reads (nw_batch_set_lane_walk)
-    // the first level's lane walk split around the next levels (certificate split):
-    // 1 = certificates only (redo flags / fallback list, nothing else written); 2 = the walk of the
-    // reads the certificates kept, give-ups found while walking to the fallback list (the exact kernel's)
-    int32_t cert_mode;
     int32_t band_lb_cap;           // longest read the band kernels take; longer ones sort last
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
     const uint32_t* band_tab;      // [17 amplicon codes (EDNAFULL, pad)][6][6 read codes] packed int16x2 score + 2 E
@@ -230,9 +226,8 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
 // not used by the previous look-back launch on a.lb_status
 hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
 int64_t band_lookback_words(int64_t n);
-// parts: 1 = the fill, 2 = the walk, 3 = both (the fill's end recorded in after_fill)
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
-                       hipEvent_t after_fill, int parts = 3);
+                       hipEvent_t after_fill);
 // the diagonal pass (nw_band_fill<W, false>) over list A; `pairs`: an upper bound of its pairs
 hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte

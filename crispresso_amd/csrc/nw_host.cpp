@@ -90,14 +90,13 @@ struct Scratch {
     DevBuf<int32_t> d_order_a, d_tile;  // the diagonal pass: list A, the reads it hands on
     DevBuf<unsigned long long> d_lb;   // look-back words of the single-pass scans (sort, redo list, ops)
     DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
-    DevBuf<uint8_t> d_bregion2;        // the certificate split's second and wide levels (beside the first level's tiles)
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
     DevBuf<int32_t> d_nops, d_opsctl;
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
         d_tile.release(); d_seed.release(); d_seed2.release(); d_seed_list.release(); d_seed_flags.release(); d_seed_list2.release();
-        d_bregion.release(); d_bregion2.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
+        d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
 };
@@ -206,8 +205,6 @@ struct nw_ctx {
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
     bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
     bool lane_call = false;           // this chunk of ops_call: the lane walk + stop summary (chunks of >= 65536 reads)
-    bool cert_split = true;           // resident lane-walk passes: the certificate split (CRISPR_NW_CERTSPLIT=0: off)
-    hipEvent_t ev_split_a = nullptr, ev_split_b = nullptr;   // the split: side stream start / end
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -762,15 +759,12 @@ int nw_create(int device, nw_ctx** out) {
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess ||
-        hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_split_a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_split_b, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess) {
         delete c;
         return NW_E_HIP;
     }
     c->cs = c->stream;
     c->cstream[0] = c->stream;
-    if (const char* e = std::getenv("CRISPR_NW_CERTSPLIT")) c->cert_split = std::atoi(e) != 0;   // A/Bs
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
@@ -809,8 +803,6 @@ void nw_destroy(nw_ctx* c) {
         if (c->cstream[k]) (void)hipStreamDestroy(c->cstream[k]);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
-    if (c->ev_split_a) (void)hipEventDestroy(c->ev_split_a);
-    if (c->ev_split_b) (void)hipEventDestroy(c->ev_split_b);
     if (c->ev_sort) (void)hipEventDestroy(c->ev_sort);
     if (c->ev_l2) (void)hipEventDestroy(c->ev_l2);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
@@ -1153,86 +1145,6 @@ int launch_range(nw_ctx* c, int64_t base) {
         c->redo_direct = direct;
         // (the diagonal pass and the traceback fill as one launch measured slower: kernel-resident
         // fill 0.578 vs 0.477 ms per 1M reads)
-        // Certificate split (resident passes with the lane walk, one region pass): the first
-        // level's lane walk runs twice -- its certificates alone first (redo flags, fallback list), then,
-        // while the second and wide levels align what they handed on (side stream, own region), the walk
-        // of the reads they kept: the next levels leave the pass's serial chain.
-        const bool split = two && c->cert_split && c->phases && a.band_summ && c->out_mode == NW_OUT_OPS &&
-                           !c->seed_chunk && c->wide_fill.grid > 0 && c->diag_fill.grid > 0 &&
-                           pairs <= c->diag16_pass_pairs && c->cstream[1] != nullptr;
-        if (split) {
-            const int64_t pp2 = std::min(pairs, c->diag_pass_pairs);
-            const int64_t rb2 = std::max(pp2 * c->diag_stride, c->wide_pairs * c->wide_stride);
-            HIP_OR_FAIL(c, c->s->d_bregion2.reserve((size_t)std::max<int64_t>(rb2, 1)));
-            nw::KernelArgs al = a;
-            al.redo_direct = 0;
-            al.redo_flags = c->s->d_redo_flags.p;
-            al.band_stride = c->diag16_stride;
-            al.band_pair_lo = 0;
-            al.band_pair_hi = pairs;
-            if (al.order_a) {
-                HIP_OR_FAIL(c, nw::launch_band_diag(16, al, c->diag16_fill, pairs, c->cs));
-                tmark(c, "diag");
-            }
-            HIP_OR_FAIL(c, nw::launch_band(16, al, c->diag16_fill, c->diag16_walk, c->cs, c->ev_fill, 1));
-            nw::KernelArgs ac = al;
-            ac.cert_mode = 1;
-            HIP_OR_FAIL(c, nw::launch_band(16, ac, c->diag16_fill, c->diag16_walk, c->cs, nullptr, 2));
-            HIP_OR_FAIL(c, nw::launch_redo_compact(a, c->n, next_epoch(c), c->cs));
-            tmark(c, "cert+redo");
-            // the side stream: the second level over the redo list (or, direct hand-off, nothing), the
-            // wide level over the fallback list (+ the redo list); their give-ups -> the exact kernel's list
-            hipStream_t main_cs = c->cs, side = c->cstream[1];
-            HIP_OR_FAIL(c, hipEventRecord(c->ev_split_a, main_cs));
-            HIP_OR_FAIL(c, hipStreamWaitEvent(side, c->ev_split_a, 0));
-            nw::KernelArgs a2 = a;
-            a2.band_region = c->s->d_bregion2.p;
-            a2.redo_direct = direct;
-            a2.band_order = c->s->d_redo.p;
-            a2.band_count = a.redo_count;
-            a2.order_a = nullptr;
-            a2.tile_list = nullptr;
-            a2.tile_count = nullptr;
-            a2.band_stride = c->diag_stride;
-            for (int64_t lo = 0; lo < pairs; lo += c->diag_pass_pairs) {
-                nw::KernelArgs ap = a2;
-                ap.band_pair_lo = lo;
-                ap.band_pair_hi = std::min(pairs, lo + c->diag_pass_pairs);
-                HIP_OR_FAIL(c, nw::launch_band(32, ap, c->diag_fill, c->diag_walk, side, nullptr));
-            }
-            nw::KernelArgs aw = a2;
-            aw.work_list = a.fallback_list;
-            aw.work_count = c->s->d_fallback_count.p;
-            aw.band_from_work = 1;
-            aw.band_count = aw.work_count;
-            aw.redo_flags = nullptr;
-            aw.band_stride = c->wide_stride;
-            aw.band_words = c->wide_words;
-            aw.band_lb_cap = c->wide_lb_cap;
-            aw.band_pair_lo = 0;
-            aw.band_pair_hi = c->wide_pairs;
-            aw.fallback_list = c->s->d_fallback2.p + base;
-            aw.fallback_count = c->s->d_fallback_count.p + 6;   // zeroed by nw_band_classify
-            HIP_OR_FAIL(c, nw::launch_band(nw::kWideDiags, aw, c->wide_fill, c->wide_walk, side, nullptr));
-            HIP_OR_FAIL(c, hipEventRecord(c->ev_split_b, side));
-            // the first level's walk of the reads its certificates kept (give-ups found walking: exact kernel)
-            nw::KernelArgs ak = al;
-            ak.cert_mode = 2;
-            ak.redo_flags = nullptr;
-            ak.fallback_list = aw.fallback_list;
-            ak.fallback_count = aw.fallback_count;
-            HIP_OR_FAIL(c, nw::launch_band(16, ak, c->diag16_fill, c->diag16_walk, main_cs, nullptr, 2));
-            tmark(c, "walk16 (split)");
-            if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, main_cs));
-            HIP_OR_FAIL(c, hipStreamWaitEvent(main_cs, c->ev_split_b, 0));
-            if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, main_cs));
-            a.work_list = aw.fallback_list;
-            a.work_count = aw.fallback_count;
-            a.redo_direct = 0;
-            HIP_OR_FAIL(c, launch_work(c, a));
-            tmark(c, "exact");
-            return NW_OK;
-        }
         for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
             al.redo_direct = lvl == 1 ? direct : 0;

@@ -635,14 +635,12 @@ def test_known_copies_resident_pass(gpu_aligner_factory, hdr_kind):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["hdr", "parity", "long_indels"])
-def test_certificate_split_resident_pass(gpu_aligner_factory, oracle, kind, monkeypatch):
-    """The certificate split of a resident lane-walk pass (the first level's certificates alone,
-    then its walk while the second and wide levels run on a side stream) gives the
-    records and runs of the same pass without it (CRISPR_NW_CERTSPLIT=0), every read, and every
-    read against the oracle.  "hdr": reads against the HDR amplicon (most DP reads leave the first
-    level: the second level runs, no direct hand-off); "parity": N codes and IUPAC bytes (reads
-    the split hands on without the wave path's refined certificate, the wave path in the walk);
-    "long_indels": deletions and insertions the wide level takes."""
+def test_lane_walk_resident_pass_hard_inputs(gpu_aligner_factory, oracle, kind):
+    """A resident pass with the first level's lane walk (the kernels bench.py times) against the same
+    pass with the wave walk, every read, and every read against the oracle, on inputs that load the
+    levels after the first: "hdr" (reads against the HDR amplicon: most DP reads need the second
+    level, no direct hand-off), "parity" (N codes, IUPAC bytes: the wave path inside the lane walk),
+    "long_indels" (length changes of >= 10 bases, four times over: the wide level)."""
     from crispresso_amd.aligner import pack_2bit
     from tests.every_read import every_read
 
@@ -656,7 +654,6 @@ def test_certificate_split_resident_pass(gpu_aligner_factory, oracle, kind, monk
     else:
         ref = synth.random_amplicon(250, 13)
         buf, off = synth.reads_from(ref, n, 14)
-        # every read with a length change of >= 10 bases (the wide level's share of C2) four times over
         lens = np.diff(off)
         idx = np.flatnonzero(np.abs(lens - 250) >= 10)
         keep = np.concatenate([np.arange(len(lens))[: n // 2], np.tile(idx, 4)])
@@ -665,18 +662,17 @@ def test_certificate_split_resident_pass(gpu_aligner_factory, oracle, kind, monk
         off = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64)
     n = len(off) - 1
     pr = pack_2bit(buf, off)
+    a = gpu_aligner_factory()
+    a.set_reference(ref)
+    a.upload_packed(pr)
     res = {}
-    for split in ("1", "0"):
-        monkeypatch.setenv("CRISPR_NW_CERTSPLIT", split)
-        a = gpu_aligner_factory()
-        a.set_reference(ref)
-        a.upload_packed(pr)
-        a.set_lane_walk(True)
+    for lane_walk in (True, False):
+        a.set_lane_walk(lane_walk)
         a.run_async()
         a.sync()
-        res[split] = a.download_ops(n)
-        a.set_lane_walk(False)
-    on, off_ = res["1"], res["0"]
+        res[lane_walk] = a.download_ops(n)
+    a.set_lane_walk(False)
+    on, off_ = res[True], res[False]
     np.testing.assert_array_equal(on.ops_off, off_.ops_off)
     for f in FIELDS:
         np.testing.assert_array_equal(on.stats[f], off_.stats[f], err_msg=f)
