@@ -847,6 +847,8 @@ def main():
                     help="profiling: only the downstream quantification leg (its kernels on the resident batch)")
     ap.add_argument("--skip-kernel-pass", action="store_true",
                     help="tracing: stop after the timed packed calls (no text call, kernel-resident pass or legs)")
+    ap.add_argument("--phase-events", action="store_true",
+                    help="A/B: keep the resident pass's per-phase timing events in the timed steps")
     ap.add_argument("--pooled-amplicons", type=int, default=96)
     ap.add_argument("--pooled-reads", type=int, default=100_000, help="C5 reads per amplicon")
     ap.add_argument("--dry-run", action="store_true",
@@ -969,6 +971,7 @@ def main():
     # DESIGN.md 4a), so the resident pass does too
     al.upload_packed(pr)
     al.set_lane_walk(True)
+    al.set_phase_events(args.phase_events)   # off: kernel_rate below times the phases, with their events
 
     def resident_step():
         al.run_async()
@@ -986,6 +989,7 @@ def main():
     }
     del res
     al.set_lane_walk(False)
+    al.set_phase_events(True)
     # the same pass by HIP events (per phase), and with the wave-per-read walk for reference
     kms, phases, counts, algo_bytes, geo = kernel_pass(al, pr, args.steps, args.warmup, lane_walk=True)
     kms_ww, phases_ww, _, _, _ = kernel_pass(al, pr, args.steps, args.warmup)
@@ -1099,7 +1103,7 @@ def main():
                 "d2h_bytes": pcie["d2h_bytes"], "compute_ms_in_call": pcie["compute_ms"],
                 "runs_per_read": n_runs / max(n, 1),
                 "note": "last timed call_pcie call: upload span on the copy stream; d2h = records (32 B) + run offsets (8 B) "
-                        "per read + 4 B per run; compute = the chunks' kernel spans summed (overlapped with the copies)",
+                        "per read + 4 B per run; compute = the call's device span, first upload to the last chunk's end",
             },
             "kernel_rate": {
                 "value": n / (kms * 1e-3), "unit": "aligned reads/s", "kernel_ms": kms, "phases_ms": phases,

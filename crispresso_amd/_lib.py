@@ -43,7 +43,7 @@ EXPORTS = (
     "nw_batch_cells", "nw_batch_geometry", "nw_batch_fallbacks", "nw_batch_kernel_times",
     "nw_align_multi", "nw_required_stride_multi", "nw_format_srspair", "nw_batch_device_output",
     "nw_batch_set_output", "nw_batch_download_ops", "nw_align_ops", "nw_ops_times", "nw_host_alloc", "nw_host_free",
-    "nw_host_register", "nw_host_unregister", "nw_host_threads", "nw_batch_set_lane_walk", "nw_set_known", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts", "nw_batch_exact_reads",
+    "nw_host_register", "nw_host_unregister", "nw_host_threads", "nw_batch_set_lane_walk", "nw_batch_set_phase_events", "nw_set_known", "nw_expand_ops", "nw_batch_phase_times", "nw_batch_path_counts", "nw_batch_exact_reads",
     "nw_align_ops_packed_lens", "nw_align_multi_ops_packed_lens", "nw_align_dual_ops_packed_lens", "nw_read_lengths16", "nw_fastq_lens",
     "nw_align_ops_resident", "nw_align_multi_ops", "nw_align_multi_ops_packed", "nw_align_ops_packed", "nw_pack_reads",
     "nw_fastq_read", "nw_fastq_read_filtered", "nw_fastq_dropped", "nw_fastq_pass", "nw_fastq_count", "nw_fastq_seqs", "nw_fastq_offsets", "nw_fastq_names", "nw_fastq_free",
@@ -178,6 +178,7 @@ def load() -> ctypes.CDLL:
         "nw_host_free": (None, [c_void_p]),
         "nw_host_threads": (c_int, []),
         "nw_batch_set_lane_walk": (c_int, [ctx_p, c_int]),
+        "nw_batch_set_phase_events": (c_int, [ctx_p, c_int]),
         "nw_set_known": (c_int, [ctx_p, c_char_p, c_int32]),
         "nw_host_register": (c_int, [c_void_p, c_int64]),
         "nw_host_unregister": (c_int, [c_void_p]),
@@ -208,7 +209,9 @@ def load() -> ctypes.CDLL:
         ),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:   # an older build (variant A/Bs): build() checks that every symbol is exported
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

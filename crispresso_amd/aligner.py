@@ -291,9 +291,14 @@ class GpuAligner:
         self._check(self.lib.nw_set_known(self._h, b, len(b)), "nw_set_known")
 
     def set_lane_walk(self, on: bool) -> None:
-        """Resident passes only: the first band level's lane walk + stop summary
-        (nw_batch_set_lane_walk; no pipelined call runs it)."""
+        """Resident passes: the first band level's lane walk + stop summary (nw_batch_set_lane_walk;
+        what a pipelined call runs on its chunks of >= 65536 reads of one amplicon)."""
         self._check(self.lib.nw_batch_set_lane_walk(self._h, 1 if on else 0), "nw_batch_set_lane_walk")
+
+    def set_phase_events(self, on: bool) -> None:
+        """Resident passes: record the per-phase events phase_times() reads (default on; a timed
+        pass turns them off: each writes back the L2 between two kernels)."""
+        self._check(self.lib.nw_batch_set_phase_events(self._h, 1 if on else 0), "nw_batch_set_phase_events")
 
     def run_async(self) -> None:
         self._check(self.lib.nw_batch_run_async(self._h), "nw_batch_run_async")

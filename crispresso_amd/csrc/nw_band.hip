@@ -277,6 +277,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // here, the first kernel of the chain, instead of by memset launches
     if (blockIdx.x == 0 && threadIdx.x < 16) a.fallback_count[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x < 2 && a.ops) a.ops_ctl[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && a.zero_ctl64 && (int)threadIdx.x < a.zero_ctl64_n) a.zero_ctl64[threadIdx.x] = 0;
     // packed input, block b: the chunk's reads of call block B = call_lo / kPkBlock + b, [bl, bh)
     // (kPkBlock reads, one per thread; four blocks per group of kLenGroup lengths).  Its lengths'
     // loads go out before the image copy's barrier.

@@ -56,6 +56,8 @@ struct KernelArgs {
     int64_t band_stride;
     int32_t band_words;            // traceback words per lane and pair
     int32_t band_summ;             // the first level's fill writes the stop summary the lane walk reads (nw_batch_set_lane_walk)
+    int64_t* zero_ctl64;           // a resident pass: the ops compaction's control block, zeroed by classify (no memset launch)
+    int32_t zero_ctl64_n;
     int32_t band_lb_cap;           // longest read the band kernels take; longer ones sort last
     int32_t band_maxsub;           // largest substitution score (scaled): the certificate's bound
     const uint32_t* band_tab;      // [17 amplicon codes (EDNAFULL, pad)][6][6 read codes] packed int16x2 score + 2 E

@@ -205,6 +205,11 @@ struct nw_ctx {
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
     bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
     bool lane_call = false;           // this chunk of ops_call: the lane walk + stop summary (chunks of >= 65536 reads)
+    int64_t* zero_ctl = nullptr;      // nw_batch_run_async: classify zeroes the compaction's control block
+    // resident passes: the phase events between the kernels (nw_batch_set_phase_events; each timing event
+    // recorded between two kernels held the stream ~5-7 us: it writes back the L2's dirty lines)
+    bool phase_events = true, phases_recorded = false;
+    hipEvent_t ev_h1 = nullptr;       // ops_call: after the last upload (the upload span; ev_in[] do not time)
     int redo_direct = 0;              // this chunk's KernelArgs::redo_direct (launch_range)
     int64_t exact_slab = 0;
     int64_t diag_pass_pairs = 0, diag_stride = 0;
@@ -759,7 +764,8 @@ int nw_create(int device, nw_ctx** out) {
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_fill) != hipSuccess || hipEventCreate(&c->ev_walk) != hipSuccess ||
-        hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess) {
+        hipEventCreate(&c->ev_sort) != hipSuccess || hipEventCreate(&c->ev_l2) != hipSuccess ||
+        hipEventCreate(&c->ev_h1) != hipSuccess) {
         delete c;
         return NW_E_HIP;
     }
@@ -803,6 +809,7 @@ void nw_destroy(nw_ctx* c) {
         if (c->cstream[k]) (void)hipStreamDestroy(c->cstream[k]);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
+    if (c->ev_h1) (void)hipEventDestroy(c->ev_h1);
     if (c->ev_sort) (void)hipEventDestroy(c->ev_sort);
     if (c->ev_l2) (void)hipEventDestroy(c->ev_l2);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
@@ -1121,9 +1128,12 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.tile_list = c->s->d_tile.p;
             a.tile_count = c->s->d_fallback_count.p + 5;
         }
+        a.zero_ctl64 = c->zero_ctl;
+        a.zero_ctl64_n = nw::kOpsCtlAll;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
         tmark(c, "classify+sort");
-        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
+        const bool pev = c->phases && c->phase_events;   // phase events (resident passes that ask for them)
+        if (pev) HIP_OR_FAIL(c, hipEventRecord(c->ev_sort, c->cs));
         const int64_t pairs = (c->n + 2) / 2;   // (the second level's list may hold one hole)
         // level 1 (16 diagonals) over the sorted reads; what it cannot certify -> redo list
         // -> level 2 (32 diagonals) -> the exact int32 kernel.  Kernels clamp the pair
@@ -1176,9 +1186,9 @@ int launch_range(nw_ctx* c, int64_t base) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
                 ap.band_pair_hi = std::min(pairs, lo + pp);
-                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, first && lo == 0 ? c->ev_fill : nullptr));
+                HIP_OR_FAIL(c, nw::launch_band(W, ap, fc, wc, c->cs, pev && first && lo == 0 ? c->ev_fill : nullptr));
                 tmark(c, W == 16 ? "fill16+walk16" : "fill32+walk32");
-                if (first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
+                if (pev && first && lo == 0) HIP_OR_FAIL(c, hipEventRecord(c->ev_walk, c->cs));
             }
             if (first && c->split_to) {   // the latency-bound rest of the chunk on the tail stream
                 HIP_OR_FAIL(c, hipEventRecord(c->split_ev, c->cs));
@@ -1202,7 +1212,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             a.seed_list = ac.redo_list;
             a.seed_count = ac.redo_count;
         }
-        if (c->phases) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
+        if (pev) HIP_OR_FAIL(c, hipEventRecord(c->ev_l2, c->cs));
         a.work_list = a.fallback_list;   // what the 16 / 32 levels could not certify
         a.work_count = c->s->d_fallback_count.p;
         a.redo_direct = direct;
@@ -1347,7 +1357,7 @@ int ops_events(nw_ctx* c, size_t chunks) {
         }
         return hipSuccess;
     };
-    HIP_OR_FAIL(c, grow(c->ev_in, hipEventDefault));
+    HIP_OR_FAIL(c, grow(c->ev_in, hipEventDisableTiming));
     HIP_OR_FAIL(c, grow(c->ev_cs, hipEventDefault));
     HIP_OR_FAIL(c, grow(c->ev_ce, hipEventDefault));
     HIP_OR_FAIL(c, grow(c->ev_out, hipEventDisableTiming));
@@ -1382,6 +1392,7 @@ int nw_batch_run_async(nw_ctx* c) {
     int rc;
     c->call_done = false;
     c->phases = true;
+    c->phases_recorded = c->phase_events;
     struct PhasesOff {
         nw_ctx* c;
         ~PhasesOff() { c->phases = false; }
@@ -1389,8 +1400,15 @@ int nw_batch_run_async(nw_ctx* c) {
     if (c->out_mode == NW_OUT_OPS) {
         if (!c->s->d_slots.p || c->s->d_nops.cap < (size_t)std::max<int64_t>(c->n, 1))
             return fail(c, NW_E_STATE, "batch uploaded before nw_batch_set_output(NW_OUT_OPS)");
-        HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
+        // the compaction's control block: zeroed by the band path's classify (the pass's first kernel;
+        // a memset launch here cost two fill kernels, ~9 us, per pass), else by a memset
+        if (c->use_diag && c->n > 0) {
+            c->zero_ctl = c->d_ctl64.p;
+        } else {
+            HIP_OR_FAIL(c, hipMemsetAsync(c->d_ctl64.p, 0, nw::kOpsCtlAll * sizeof(int64_t), c->stream));
+        }
         rc = launch_range_ops(c, 0);
+        c->zero_ctl = nullptr;
     } else {
         rc = launch_range(c, 0);
     }
@@ -1456,6 +1474,8 @@ int nw_batch_kernel_times(nw_ctx* c, float* fill_ms, float* walk_ms, float* rest
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     float total = 0.0f, f = 0.0f, w = 0.0f;
     HIP_OR_FAIL(c, hipEventElapsedTime(&total, c->ev0, c->ev1));
+    if (c->use_diag && c->n > 0 && !c->phases_recorded)
+        return fail(c, NW_E_STATE, "the last run recorded no phase events (nw_batch_set_phase_events)");
     if (c->use_diag && c->n > 0) {
         HIP_OR_FAIL(c, hipEventElapsedTime(&f, c->ev0, c->ev_fill));
         HIP_OR_FAIL(c, hipEventElapsedTime(&w, c->ev_fill, c->ev_walk));
@@ -2056,6 +2076,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         }
         HIP_OR_FAIL(c, hipEventRecord(c->ev_in[(size_t)k], c->s_in));
     }
+    if (upload) HIP_OR_FAIL(c, hipEventRecord(c->ev_h1, c->s_in));
     ht.lap(3);
     // lengths given: the longest read, and every length must equal its offsets' difference
     // (the device rebuilds the offsets from the lengths and the group bases, the host expands
@@ -2334,7 +2355,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
             if (k >= nsets) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_ce[(size_t)(k - nsets)], 0));
         }
         if (upload) HIP_OR_FAIL(c, hipStreamWaitEvent(c->cs, c->ev_in[(size_t)chunks[(size_t)k].up], 0));
-        HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
+        // (a timing event here sat in every chunk's chain: only with the host timing on)
+        if (ht.on) HIP_OR_FAIL(c, hipEventRecord(c->ev_cs[(size_t)k], c->cs));
         if ((rc = use_group(chunks[(size_t)k].g, hi - lo))) return restore(rc);
         const int pass = chunks[(size_t)k].pass;
         c->out_off = pass ? n + 1 : 0;   // a dual call's pass 1: its records and run offsets after pass 0's
@@ -2496,12 +2518,15 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->ops_h2d_bytes = upload ? h2d_bytes : 0;
     if (nchunks > 0) {
         if (upload)
-            HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_in[(size_t)chunks[(size_t)nchunks - 1].up]));
+            HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_h2d_ms, c->ev_h0, c->ev_h1));
+        // the chunks' compute spans summed (host timing on: their start events), else the call's device
+        // span, first upload to the last chunk's end
         for (int64_t k = 0; k < nchunks; ++k) {
             float ms = 0.0f;
-            HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
+            if (ht.on) HIP_OR_FAIL(c, hipEventElapsedTime(&ms, c->ev_cs[(size_t)k], c->ev_ce[(size_t)k]));
             c->ops_compute_ms += ms;
         }
+        if (!ht.on) HIP_OR_FAIL(c, hipEventElapsedTime(&c->ops_compute_ms, c->ev_h0, c->ev_ce[(size_t)nchunks - 1]));
         for (size_t i = 0; i < c->trace_used; ++i) {
             float t = 0;
             (void)hipEventElapsedTime(&t, c->ev_h0, c->trace_ev[i].second);
@@ -2512,7 +2537,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         if (ht.on)   // per chunk (ms from the first upload): upload done, compute start, compute end
             for (int64_t k = 0; k < nchunks; ++k) {
                 float a = 0, b = 0, e = 0;
-                if (upload) (void)hipEventElapsedTime(&a, c->ev_h0, c->ev_in[(size_t)chunks[(size_t)k].up]);
+                (void)a;   // (the uploads' events do not time: ev_h1 is the last one's end)
                 (void)hipEventElapsedTime(&b, c->ev_h0, c->ev_cs[(size_t)k]);
                 (void)hipEventElapsedTime(&e, c->ev_h0, c->ev_ce[(size_t)k]);
                 std::fprintf(stderr, "  chunk %lld [%lld reads]: in %.3f start %.3f end %.3f\n", (long long)k,
@@ -2761,6 +2786,12 @@ int nw_set_known(nw_ctx* c, const char* seq, int32_t len) {
     return NW_OK;
 }
 
+int nw_batch_set_phase_events(nw_ctx* c, int on) {
+    if (!c) return NW_E_INVALID;
+    c->phase_events = on != 0;
+    return NW_OK;
+}
+
 int nw_batch_set_lane_walk(nw_ctx* c, int on) {
     if (!c) return NW_E_INVALID;
     c->lane_walk = on != 0;
@@ -2794,6 +2825,7 @@ int nw_batch_phase_times(nw_ctx* c, float* ms5) {
     (void)hipSetDevice(c->device);
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < 5; ++k) ms5[k] = 0.0f;
+    if (!c->phases_recorded) return fail(c, NW_E_STATE, "the last run recorded no phase events (nw_batch_set_phase_events)");
     if (!c->use_diag || c->n <= 0) {
         HIP_OR_FAIL(c, hipEventElapsedTime(&ms5[4], c->ev0, c->ev1));
         return NW_OK;

@@ -204,6 +204,11 @@ int nw_align_multi_ops_packed(nw_ctx* ctx, const char* refs, const int64_t* ref_
  * [0] classify + length sort, [1] nw_band_fill<16>, [2] nw_band_walk<16>, [3] the
  * 32-diagonal level, [4] the exact kernel + ops compaction.  Other paths: all in [4]. */
 int nw_batch_phase_times(nw_ctx* ctx, float* ms5);
+/* Whether nw_batch_run_async records the phase events nw_batch_phase_times and nw_batch_kernel_times
+ * read (on != 0, the default).  Each is a timing event between two kernels, which writes back the L2's
+ * dirty lines (~5-7 us per event on the pass's critical path): a timed resident pass turns them off;
+ * both calls then return NW_E_STATE for that run. */
+int nw_batch_set_phase_events(nw_ctx* ctx, int on);
 /* Reads of the last run by path: [0] exact copies (no DP), [1] first band level,
  * [2] second band level, [3] the 128-diagonal wide level and the exact int32 kernel after
  * it (synchronises).  A chunk whose first level gave up on at most 1024 reads skips the
