@@ -1,4 +1,5 @@
 #!/bin/bash
+# (libcrispr_nw_r5base.so: the parent commit's build, copied aside before rebuilding)
 # A/B of the timing events: the resident pass with / without its phase events (bench value, wall clock),
 # and the C2 / C1 calls with the previous library (every chunk's ev_cs, ev_fill, ev_walk, timing uploads'
 # events) against this one; then the GPU tests of the phase / ops-times paths.
