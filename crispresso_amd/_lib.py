@@ -210,12 +210,30 @@ def load() -> ctypes.CDLL:
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
-        if fn is None:   # an older build (variant A/Bs): build() checks that every symbol is exported
+        if fn is None:   # a stale build: a use of the entry point says so (build() checks every symbol)
+            _MISSING.add(name)
+            setattr(lib, name, _stale(name))
             continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+_MISSING: set = set()
+
+
+def _stale(name: str):
+    def call(*_a, **_k):
+        raise RuntimeError(f"libcrispr_nw.so is out of date: it does not export {name} "
+                           "(rebuild it: make -C crispresso_amd/csrc)")
+    return call
+
+
+def has_symbol(name: str) -> bool:
+    """Whether the loaded library exports ``name`` (False for an out-of-date build)."""
+    lib = load()
+    return name not in _MISSING and getattr(lib, name, None) is not None
 
 
 def exported_symbols() -> dict:
@@ -225,7 +243,7 @@ def exported_symbols() -> dict:
     for name in EXPORTS + QUANT_EXPORTS + FLASH_EXPORTS + SYNTH_EXPORTS:
         try:
             getattr(lib, name)
-            out[name] = True
+            out[name] = name not in _MISSING
         except AttributeError:
             out[name] = False
     return out

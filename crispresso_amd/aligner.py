@@ -513,7 +513,9 @@ class GpuAligner:
         return ob, ob2
 
     def ops_times(self) -> dict:
-        """Last align_ops: upload span (ms), summed kernel spans (ms), bytes each way."""
+        """Last align_ops: upload span (ms); ``compute_ms`` = the device span from the first upload to
+        the last chunk's end (uploads included; with CRISPR_NW_HOST_TIMING=1 the chunks' kernel spans
+        summed); bytes each way (nw_ops_times)."""
         h2d, comp = ctypes.c_float(), ctypes.c_float()
         hb, db = ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.nw_ops_times(self._h, ctypes.byref(h2d), ctypes.byref(comp), ctypes.byref(hb),

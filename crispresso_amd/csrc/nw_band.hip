@@ -1060,7 +1060,10 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
         else if (k >= KS) {
             const int q = (kbase[k] - dpB) + cnt[wave * NB + k] + rank[i];
             a.seed_list[baseS + q] = (int32_t)(r0 + i);
-            if (q == dpS0 - 1 && dpS != dpS0) a.seed_list[baseS + q + 1] = (int32_t)(r0 + i);
+            if (q == dpS0 - 1 && dpS != dpS0) {   // the segment's odd count padded to a pair
+                a.seed_list[baseS + q + 1] = (int32_t)(r0 + i);
+                atomicAdd(a.fallback_count + 9, 1);   // the path counters leave the padding out
+            }
         }
         else if (k != EX) order[base + kbase[k] + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
     }
@@ -1623,7 +1626,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                 }
             }
             if constexpr (TB) {
-                const unsigned d3 = sub2(Y, X);     // sign: X > Y
+                const unsigned d3 = sub2(X, Y);     // sign: Y > X (X wins an X == Y tie)
                 const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
                 const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
                 const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
@@ -1733,7 +1736,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
 // lane tests CPL cells; the round's first stop is found with one ballot.  `word(tau,
 // kd)` returns the band dword of anti-diagonal step tau (relative to the stored
 // range) and band diagonal kd; bit positions of read h at sub-step s: Y opens hb,
-// X > Y hb + 4, X opens 16 + hb, M < max(X, Y) 20 + hb, with hb = 8 h + s.
+// Y > X hb + 4, X opens 16 + hb, M < max(X, Y) 20 + hb, with hb = 8 h + s.
 // tot (optional): [0] M columns, [1] gap columns, [2] the paid gaps' cost (runs opened inside the
 // matrix: O + (k - 1) E; the end overhangs are free) -- a plain read's record without band_emit.
 template <int CPL, int W>
@@ -1815,7 +1818,7 @@ __device__ int band_walk_runs2(const unsigned* bits, int NW, int La, int Lb, int
             const int q = u0 >> 1;
             const unsigned wq = (unsigned)__builtin_amdgcn_readlane(
                 (int)(q == 0 ? v.w : (q == 1 ? v.z : (q == 2 ? v.y : v.x))), L);
-            nb = ((wq >> (4 + hb + ((u0 & 1) ? p : 2 + p))) & 1u) ? RUN_X : RUN_Y;
+            nb = ((wq >> (4 + hb + ((u0 & 1) ? p : 2 + p))) & 1u) ? RUN_Y : RUN_X;
             push(RUN_M, k0 + 1);
             i -= k0 + 1;
             j -= k0 + 1;
@@ -2276,13 +2279,13 @@ __device__ void walk_lanes(const KernelArgs& a, long long klo, long long khi, un
                                     push(RUN_M, run, false);
                                     i -= run;
                                     j -= run;
-                                    const int ts = tc - 2 * u0;   // the stop cell: "X > Y" picks the gap it continues in
+                                    const int ts = tc - 2 * u0;   // the stop cell: "Y > X" picks the gap it continues in
                                     uint4 vs = v[0];
 #pragma unroll
                                     for (int q = 1; q < kMRows; ++q) vs = (ts >> 4) == r0 - q ? v[q] : vs;
                                     const int qs = (ts >> 2) & 3;
                                     const unsigned ws = qs == 0 ? vs.x : (qs == 1 ? vs.y : (qs == 2 ? vs.z : vs.w));
-                                    state = ((ws >> (4 + hb + (ts & 3))) & 1u) ? RUN_X : RUN_Y;
+                                    state = ((ws >> (4 + hb + (ts & 3))) & 1u) ? RUN_Y : RUN_X;
                                     kc = 0;
                                 } else {
                                     kc += ncell;

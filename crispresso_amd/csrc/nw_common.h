@@ -150,7 +150,7 @@ __device__ __forceinline__ void decode_end(long long key, int La, int Lb, int* s
 enum { RUN_M = 0, RUN_X = 1, RUN_Y = 2 };
 
 // Traceback walk in runs.  `nib(ai, bj, &oob)` returns the 4-bit cell code
-// (bit0: M < max(X,Y), bit1: X > Y, bit2: X opens, bit3: Y opens) of the
+// (bit0: M < max(X,Y), bit1: Y > X, bit2: X opens, bit3: Y opens) of the
 // 0-based cell, setting oob when the cell is not stored.  Writes runs in
 // end->start order to `runs` (lane 0, at most `cap`), returns the count, or -1
 // when the walk needs a cell outside the stored band or more than `cap` runs.
@@ -183,8 +183,8 @@ __device__ int walk_runs(const Nib& nib, int La, int Lb, int ei, int ej, unsigne
             const unsigned c = valid ? nib(ci - 1, cj - 1, &oob) : 0u;
             oob = valid && oob;
             // EMBOSS tie rules (pinned by the reference's e2e values):
-            // M when M >= max(X, Y); a gap run ends only where open > extend
-            const int best = (c & 1u) ? ((c & 2u) ? RUN_X : RUN_Y) : RUN_M;
+            // M when M >= max(X, Y), else X when X >= Y; a gap run ends only where open > extend
+            const int best = (c & 1u) ? ((c & 2u) ? RUN_Y : RUN_X) : RUN_M;
             m = __ballot(!valid || oob || best != RUN_M);
             if (m == 0) { push(RUN_M, 64); i -= 64; j -= 64; continue; }
             nb = __builtin_amdgcn_readlane(best, (int)__builtin_ctzll(m));
@@ -264,7 +264,7 @@ __device__ int walk_runs_wide(const Nib& nib, int La, int Lb, int ei, int ej, un
         }
 #pragma unroll
         for (int u = CPL - 1; u >= 0; --u) {
-            const int best = (c[u] & 1u) ? ((c[u] & 2u) ? RUN_X : RUN_Y) : RUN_M;
+            const int best = (c[u] & 1u) ? ((c[u] & 2u) ? RUN_Y : RUN_X) : RUN_M;
             const bool go = state == RUN_M ? best == RUN_M : (c[u] & (state == RUN_X ? 4u : 8u)) == 0;
             if (!valid[u] || oob[u] || !go) {
                 first = u;

@@ -291,6 +291,7 @@ struct OpsCounts {
     const int32_t* exact;      // the wide level's give-ups: the exact kernel's reads (null: no wide level)
     const int32_t* seeded;     // the seeded reads (to the wide level, or the second level first; null: none)
     const int32_t* seeded_l2;  // of those, the ones the 32-diagonal level left to the wide level (null: it took none)
+    const int32_t* seed_pad;   // entries the segment sort added to pair up odd segments (counted in seeded)
 };
 // The call's last chunk: the compaction also writes the chunk's records, run offsets and runs
 // straight into the caller's page-locked buffers (no copies and no host round trip after it).

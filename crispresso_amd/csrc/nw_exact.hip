@@ -200,7 +200,7 @@ __global__ __launch_bounds__(1024) void nw_exact_kernel(const KernelArgs a, int6
                         const int H = max(M, mxy);
                         unsigned nib = (unsigned)(Ye - Mou) >> 31;             // bit 3: Y opens
                         nib = __builtin_amdgcn_alignbit(nib, (unsigned)(Xe - Mol[k]), 31);   // bit 2: X opens
-                        nib = __builtin_amdgcn_alignbit(nib, (unsigned)(Y - X), 31);         // bit 1: X > Y
+                        nib = __builtin_amdgcn_alignbit(nib, (unsigned)(X - Y), 31);         // bit 1: Y > X
                         nib = __builtin_amdgcn_alignbit(nib, (unsigned)(M - mxy), 31);       // bit 0: M < max
                         acc |= nib << (4 * k);
                         mlast = k == klast ? M : mlast;

@@ -725,9 +725,12 @@ int configure(nw_ctx* c) {
             if (c->seed_on) {
                 HIP_OR_FAIL(c, c->s->d_seed.reserve((size_t)std::max<int64_t>(c->n, 1)));
                 HIP_OR_FAIL(c, c->s->d_seed2.reserve((size_t)std::max<int64_t>(c->n, 1)));
-                HIP_OR_FAIL(c, c->s->d_seed_list.reserve((size_t)std::max<int64_t>(c->n, 1)));
-                HIP_OR_FAIL(c, c->s->d_seed_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
-                HIP_OR_FAIL(c, c->s->d_seed_list2.reserve((size_t)std::max<int64_t>(c->n, 1)));
+                // the segment sort pads each 4096-read segment's seeded list to an even length (one
+                // entry per segment at most): the list, its flags and its compaction hold n + n/4096 + 2
+                const size_t nseed = (size_t)(c->n + c->n / 4096 + 2);
+                HIP_OR_FAIL(c, c->s->d_seed_list.reserve(nseed));
+                HIP_OR_FAIL(c, c->s->d_seed_flags.reserve(nseed));
+                HIP_OR_FAIL(c, c->s->d_seed_list2.reserve(nseed));
             }
             c->use_diag = true;
         }
@@ -1308,7 +1311,10 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
             cnt.handed = c->s->d_fallback_count.p + 5;
         }
         if (c->wide_fill.grid > 0) cnt.exact = c->s->d_fallback_count.p + 6;
-        if (c->seed_chunk) cnt.seeded = c->s->d_fallback_count.p + 7;
+        if (c->seed_chunk) {
+            cnt.seeded = c->s->d_fallback_count.p + 7;
+            cnt.seed_pad = c->s->d_fallback_count.p + 9;   // the sort's padding entries (zeroed by classify)
+        }
         if (c->seed_chunk && c->seed_l2) cnt.seeded_l2 = c->s->d_fallback_count.p + 8;
     }
     if (c->n <= 0) cnt.fallback = nullptr;
@@ -2324,6 +2330,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     c->trace_used = 0;
     // (a dual call: its pass's chunk two back -- the host never waits for the other pass's chunks)
     const int64_t lag = dual ? 4 : std::max(1, nsets - 1);
+    // chunk k waits on ev_out[k - nsets], recorded by copy_runs(k - nsets) once k - nsets <= k' - lag for
+    // an earlier k': every wait needs lag < nsets
+    if (lag >= nsets) return restore(fail(c, NW_E_INVALID, "ops call: run-copy lag must be below the scratch sets"));
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
     // a resident packed batch (nw_align_ops_resident after nw_align_ops_packed): the band path's
@@ -2503,7 +2512,9 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     ops_off[n] = total_p[0];
     if (dual) dual->ops_off2[n] = total_p[1];
     if (nchunks > 0) {   // the call's reads by path (nw_batch_path_counts / nw_batch_fallbacks; a dual call: pass 0's)
-        const int64_t* h = c->h_ctl + nw::kOpsCtl * (dual ? nchunks - 2 : nchunks - 1);
+        int64_t kl = nchunks - 1;   // the last chunk of pass 0 (a dual call interleaves the passes)
+        while (kl > 0 && chunks[(size_t)kl].pass != 0) --kl;
+        const int64_t* h = c->h_ctl + nw::kOpsCtl * kl;
         const bool two = any_diag && c->diag16_fill.grid > 0;
         c->call_counts[0] = any_diag ? n - h[6] : 0;
         c->call_counts[1] = two ? h[6] - h[7] : 0;                // first level: two-level chunks' DP reads

@@ -13,7 +13,7 @@
 //     lane l+1 with one DPP wave_shr:1 per value per step -- no LDS round trip.
 //   * substitution scores come from a per-amplicon profile in LDS laid out
 //     [code][lane][RP] int8, so one ds_read_b32/b64 yields a lane's R scores.
-//   * traceback: 4 bits per cell (best-state >M, X>Y, X-extend, Y-extend), every
+//   * traceback: 4 bits per cell (best-state >M, Y>X, X-extend, Y-extend), every
 //     cell stored: in LDS (TB_LDS_FULL) or a per-wave HBM slab (TB_GLOBAL_FULL).
 //     This is the exact fallback of the certified band path (nw_band.hip): the
 //     reads no band level certifies, rare codes, -endweight, and every read when
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void nw_align_kernel(const KernelArgs args) {
                     const int H = max(M, mxy);
                     unsigned a = (unsigned)(Ye - Mou) >> 31;   // Y opens (open > extend)
                     a = push_sign(a, Xe - Mol[k]);            // X opens
-                    a = push_sign(a, Y - X);                  // X > Y
+                    a = push_sign(a, X - Y);                  // Y > X (X wins an X == Y tie)
                     a = push_sign(a, M - mxy);                // M < max(X, Y)
                     nib[k] = a;
                     mlast = (k == klast) ? M : mlast;

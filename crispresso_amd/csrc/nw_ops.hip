@@ -162,13 +162,20 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         // list to the exact kernel
         const bool direct = cnt.direct > 0 && cnt.redo && *cnt.redo <= cnt.direct;
         if (direct) fb += *cnt.redo;
-        const long long ns = cnt.seeded ? (long long)*cnt.seeded : 0ll;   // seeded: DP reads the wide level takes first
-        const long long n2 = cnt.seeded_l2 ? ns - (long long)*cnt.seeded_l2 : 0ll;   // ... but the 32-diagonal level's
-        ctl[4] += fb + ns - n2;
+        // seeded: DP reads the wide level takes first, but the 32-diagonal level's; a padding entry
+        // repeats its segment's last read, so it sits in whichever share that read's pair went to
+        const long long ns = cnt.seeded ? (long long)*cnt.seeded : 0ll;
+        const long long pad = cnt.seed_pad ? (long long)*cnt.seed_pad : 0ll;
+        long long n2 = cnt.seeded_l2 ? ns - (long long)*cnt.seeded_l2 : 0ll;
+        long long nw = ns - n2;
+        const long long pw = nw < pad ? nw : pad;
+        nw -= pw;
+        n2 -= pad - pw;
+        ctl[4] += fb + nw;
         ctl[10] += cnt.exact ? (long long)*cnt.exact : fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
         ctl[5] += n2;
-        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0) + ns;
+        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0) + ns - pad;
         ctl[6] += dp;
         if (cnt.one_level) ctl[7] += dp;
         if (cnt.list_a) ctl[8] += *cnt.list_a;

@@ -506,7 +506,7 @@ def align_reads(args: AlignArgs, processed_output_filename: str, aligner: Option
         # interleaved with the forward pass's) when no needle file is kept
         dual = (native and bool(args.expected_hdr_amplicon_seq) and not keep_files and packed is not None
                 and getattr(packed, "lens", None) is not None and hasattr(aligner, "align_dual_packed")
-                and default_output_mode() == "ops")
+                and default_output_mode() == "ops" and _lib.has_symbol("nw_align_dual_ops_packed_lens"))
         known = args.expected_hdr_amplicon_seq if native and not dual and hasattr(aligner, "set_known") else None
         rep = None
         if dual:

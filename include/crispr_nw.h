@@ -289,8 +289,9 @@ int nw_align_dual_ops_packed_lens(nw_ctx* ctx, const char* ref2, int32_t ref2_le
                                   const uint8_t* exc_byte, int64_t n_exc, uint32_t* ops_out, int64_t ops_cap,
                                   int64_t* ops_off, nw_stat* stats, uint32_t* ops_out2, int64_t ops_cap2,
                                   int64_t* ops_off2, nw_stat* stats2);
-/* Last nw_align_ops: span of the uploads on the copy stream, sum of the chunks'
- * kernel spans, bytes each way. */
+/* Last nw_align_ops: span of the uploads on the copy stream (h2d_ms); compute_ms = the device span
+ * from the first upload to the last chunk's end (uploads included), or, with host timing on
+ * (CRISPR_NW_HOST_TIMING=1), the sum of the chunks' kernel spans; bytes each way. */
 int nw_ops_times(const nw_ctx* ctx, float* h2d_ms, float* compute_ms, int64_t* h2d_bytes, int64_t* d2h_bytes);
 
 /* Page-locked host memory for the batch buffers (hipHostMalloc / hipHostRegister). */

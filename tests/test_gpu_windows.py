@@ -164,3 +164,32 @@ def test_seeded_levels_mixed_lists(gpu_aligner_factory, monkeypatch, env):
     res = every_read(amp, buf, off, ob, threads=8)
     assert res["mismatches"] == 0, (res, counts)
     assert counts["wide128"] > 0, counts
+
+
+@pytest.mark.parametrize("n", [8193, 4097 * 3])
+def test_all_seeded_odd_batch(gpu_aligner_factory, n):
+    """Every read of an odd-sized batch on the seeded list (151-base windows of a 280-base amplicon with
+    a deletion and a substitution: no window certificate, and the 16-diagonal band cannot hold them), so
+    every sort segment with an odd count pads its last pair past n entries: the seeded list, its flags
+    and their compaction are reserved for that (n + n/4096 + 2 entries).  One-chunk call and a resident
+    pass of the same batch: every read against the oracle, and the path counters leave the padding out
+    (no read is a certified copy: n minus the DP reads is 0, not minus the padding entries)."""
+    amp = synth.random_amplicon(280, 77)
+    rng = np.random.Generator(np.random.PCG64(n))
+    reads = []
+    for _ in range(n):
+        s = int(rng.integers(0, 280 - 155))
+        r = amp[s:s + 154]
+        p = int(rng.integers(40, 110))
+        r = r[:p] + r[p + 3:]
+        reads.append(_sub(r, int(rng.integers(120, 150))))
+    buf, off, pr = _run(amp, reads)
+    a = gpu_aligner_factory()
+    a.set_reference(amp)
+    ob = a.align_ops_packed(pr)
+    counts = a.path_counts()
+    assert every_read(amp, buf, off, ob, threads=8)["mismatches"] == 0
+    assert counts["exact_copies"] == 0, counts
+    assert all(0 <= v <= n for v in counts.values()), counts
+    ob2 = a.align_ops(None, pr.offsets, resident=True)
+    assert every_read(amp, buf, off, ob2, threads=8)["mismatches"] == 0
