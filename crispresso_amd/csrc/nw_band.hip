@@ -203,6 +203,7 @@ __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W)
 // (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
 __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
 
+constexpr int kIndelMax = 10;   // classify's one-indel certificate: gaps of at most this many residues
 constexpr int kCand = NW_CAND; // exact-copy candidates compared together (2 dword loads each in flight)
 
 // Reads of the amplicon's length with ONE substitution (A C G T against A C G T; ops output,
@@ -312,6 +313,16 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     const bool sub2_ok = sub1_ok && 2 * a.gap_open > 2 * xl - mt2 && a.gap_open > 2 * xl - 2 * mt2 &&
                          a.gap_open > xl - mt2 && xl < 2 * mt2 && (2 * xl - mt2) / xl + 1 == 2 &&
                          (2 * xl - 2 * mt2) / xl + 1 == 1 && (2 * xl - 3 * mt2) / xl + 1 == 1;
+    // one indel of k residues (below): certified for k <= indel_kmax, the largest k with m > (k - 1) E (no
+    // alternative leaves a read or amplicon residue unpaired or mismatched), O > (k - 1) E (no alternative
+    // with two internal gaps) and O + (k - 1) E < 4 m (no single diagonal pairing four residues fewer)
+    int indel_kmax = 0;
+    if (PK && sub1_ok && a.amp2)
+        for (int k = 1; k <= kIndelMax; ++k) {
+            const int p = (k - 1) * a.gap_extend;
+            if (!(a.band_maxsub > p && a.gap_open > p && a.gap_open + p < 4 * a.band_maxsub)) break;
+            indel_kmax = k;
+        }
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
@@ -591,12 +602,112 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 }
             }
         }
+        // One indel (round 6; packed input, ops output, an A C G T amplicon of at most 256 bp, no exception
+        // bytes): a read of La -+ k bases, 1 <= k <= indel_kmax.  Call the shorter of read and amplicon s
+        // (Ls bases), the longer l; the candidate alignment pairs every residue of s, identically, with
+        // one internal gap of k residues of l: S = m Ls - O - (k - 1) E.  Any alignment pairs <= Ls
+        // residues; with u of s's residues unpaired, w mismatches and g the gap residues of one internal
+        // gap it scores m (Ls - u - w) - x w - O - (g - 1) E, >= S only if m u + (m + x) w <= (k - g) E:
+        // u = w = 0 (m > (k - 1) E), so the gap is in l (an l-gap of g <= k: an s-gap leaves s residues
+        // unpaired); two or more internal gaps score <= m Ls - 2 O < S (O > (k - 1) E).  A one-gap
+        // alignment with u = w = 0 pairs a prefix of s on diagonal shift s1 (l's residue i + s1 against
+        // s's i) and the rest on s2 = s1 + g, 0 <= s1 < s2 <= k: it exists iff the last mismatch of
+        // shift s2 precedes the first of s1 (G[s2] <= F[s1]); every such pair but (0, k) would score
+        // >= S with a different alignment: none may exist.  No internal gap: a single shift pairs
+        // P = min(Ls, Ll - s) residues (shifts of s, 1..3, pair Ls - s): each score m (P - c) - x c with
+        // c mismatches must stay below S (shifts pairing 4 or more residues fewer do: O + (k - 1) E <
+        // 4 m).  Then the optimal alignments are exactly (0, k) with the gap at any q in [G[k], F[0]]
+        // (ties), all paired residues identical; the traceback from the corner (score S, first in the
+        // scan) stays on the shift-k diagonal while M ties the gap state (M wins ties) and leaves it where
+        // a mismatch precedes (q = G[k]): the gap is placed left-most, X when it is in the read, else Y.
+        // Runs M q, gap k, M Ls - q; identities Ls, gaps k, length Ll.  Reads of C2's deletion and
+        // insertion classes (~15 % of the reads) need no DP: the traceback fill and the wide level lose
+        // their bulk (tests/test_gpu_indel.py: homopolymer and tandem-repeat indels against the oracle).
+        unsigned long long indel1 = 0ull;
+        int ind_q = 0, ind_k = 0;
+        if constexpr (PK) {
+            const int dl = my_len - La, kab = dl < 0 ? -dl : dl;
+            const bool ci = indel_kmax > 0 && a.ops && one_chunk && amp_acgt_all && r < r_end && !exc && kab >= 1 &&
+                            kab <= indel_kmax;
+            if (__ballot(ci)) {
+                const bool del = dl < 0;
+                const int Ls = del ? my_len : La, Ll = del ? La : my_len;
+                unsigned rw[18];
+                {
+                    const long long q0 = my_off - a.pk_pos0;
+                    const unsigned* src = a.pk_words + (q0 >> 4);
+                    const unsigned s2 = (unsigned)(2 * (q0 & 15));
+                    const int nrw = (my_len + 15) >> 4;
+                    unsigned wd[18];
+#pragma unroll
+                    for (int t = 0; t < 18; ++t) wd[t] = ci && t <= nrw ? src[t] : 0u;
+#pragma unroll
+                    for (int t = 0; t < 17; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
+                    rw[17] = 0u;
+                }
+                auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
+                    const int b = len - 16 * t;
+                    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
+                };
+                const int mm = a.band_maxsub, xx = 4 * sc5;
+                const int S = mm * Ls - a.gap_open - (kab - 1) * a.gap_extend;
+                bool ok = false;
+                int gk = 0;
+                // the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
+                // registers (one branch per case: a wave holding both runs both, masked)
+                auto test = [&](auto del_tag) {
+                    constexpr bool DEL = decltype(del_tag)::value;
+                    auto wl = [&](int t) -> unsigned { return DEL ? (t < n2 ? amp2s[t] : 0u) : rw[t]; };
+                    auto ws = [&](int t) -> unsigned { return DEL ? rw[t] : (t < n2 ? amp2s[t] : 0u); };
+                    bool o = true;
+                    // shifts sh = 0 .. kab + 3 of l (a runtime loop); for sh <= kab the pair test G[s2] > F[s1]
+                    // (s1 < s2) as a running maximum of F: every earlier shift's for s2 < kab, shifts
+                    // 1 .. kab - 1 for s2 = kab (the pair (0, kab) is the candidate)
+                    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
+                    for (int sh = 0; sh <= kab + 3; ++sh) {
+                        const int P = min(Ls, Ll - sh);
+                        int c = 0, f = Ls, g = 0;
+#pragma unroll
+                        for (int t = 0; t < 17; ++t) {
+                            const unsigned z = __builtin_amdgcn_alignbit(wl(t + 1), wl(t), (unsigned)(2 * sh)) ^ ws(t);
+                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+                            c += __builtin_popcount(mk);
+                            f = (mk != 0u && f == Ls) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : f;
+                            g = mk != 0u ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : g;
+                        }
+                        o = o && mm * (P - c) - xx * c < S;
+                        if (sh <= kab) {
+                            if (sh == 0) f0 = f;
+                            if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
+                            if (sh == kab) gk = g;
+                            fmax_all = max(fmax_all, f);
+                            if (sh > 0) fmax_1 = max(fmax_1, f);
+                        }
+                    }
+                    for (int sh = 1; sh <= 3; ++sh) {   // s shifted by sh against l: Ls - sh pairs
+                        int c = 0;
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) {
+                            const unsigned z = __builtin_amdgcn_alignbit(ws(t + 1), ws(t), (unsigned)(2 * sh)) ^ wl(t);
+                            c += __builtin_popcount((z | (z >> 1)) & vmask(t, Ls - sh));
+                        }
+                        o = o && mm * (Ls - sh - c) - xx * c < S;
+                    }
+                    ok = o && gk >= 1 && gk <= f0;
+                };
+                if (ci && del) test(std::true_type{});
+                if (ci && !del) test(std::false_type{});
+                indel1 = __ballot(ok);
+                ind_q = gk;
+                ind_k = kab;
+            }
+        }
         // window reads (above): an exact window at the largest offset, else one substitution
         unsigned long long win = 0ull;
         int win_s = 0, win_k = 0;
         if constexpr (PK) {
             if (win_ok) {
-                bool cand_w = r < r_end && !exc && my_len >= 32 && my_len < La;
+                bool cand_w = r < r_end && !exc && my_len >= 32 && my_len < La && !((indel1 >> lane) & 1ull);
                 int best1 = -1;   // -2: an exact window at win_s; >= 0: an offset with one mismatch
                 if (cand_w) {
                     // a window at s has the read's first 16 bases at s or its last 16 at s + Lb - 16 (one
@@ -680,7 +791,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         int32_t sinfo = 0, sinfo2 = 0;
         if constexpr (PK) {
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
-                !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull)) {
+                !(((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull)) {
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
@@ -747,7 +858,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             if (a.seed_info2 && r < r_end) a.seed_info2[r] = sinfo2;
         }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2 | win | known) >> lane) & 1ull)
+            a.sort_key[r] = (((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull)
                                 ? a.band_lb_cap + 2
                                 : (sinfo ? a.band_lb_cap + 3 +
                                                min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
@@ -763,6 +874,19 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             int4* st = (int4*)(a.stats + r);
             st[0] = make_int4(La, my_len - win_k, my_len - win_k, La - my_len);   // aln_len, n_ident, n_sim, n_gaps
             st[1] = make_int4(a.band_maxsub * (my_len - win_k) - win_k * 4 * sc5, win_s + my_len, my_len, 0);
+        }
+        if (a.ops && r < r_end && ((indel1 >> lane) & 1ull)) {
+            // runs: M q, the gap (X: residues of the read, Y: of the amplicon), M the rest of the shorter
+            const bool del = my_len < La;
+            const int Ls = del ? my_len : La;
+            const long long sst = a.ops_stride;
+            a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)ind_q;
+            a.ops[sst + r] = ((unsigned)(del ? RUN_Y : RUN_X) << 28) | (unsigned)ind_k;
+            a.ops[2 * sst + r] = ((unsigned)RUN_M << 28) | (unsigned)(Ls - ind_q);
+            a.nops[r] = 3;
+            int4* st = (int4*)(a.stats + r);
+            st[0] = make_int4(Ls + ind_k, Ls, Ls, ind_k);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * Ls - a.gap_open - (ind_k - 1) * a.gap_extend, La, my_len, 0);
         }
         // a known copy: record and runs from the known alignment, by the compaction
         if (a.ops && r < r_end && ((known >> lane) & 1ull)) a.nops[r] = kNopsKnown;
@@ -809,7 +933,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
             // before any store (one read per round trip measured 2.7x the byte-input classify)
             constexpr int kWr = 8;
-            unsigned long long dp = __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull));
+            unsigned long long dp =
+                __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull));
             uint8_t* dst = const_cast<uint8_t*>(a.reads);
             while (dp) {
                 long long o[kWr], e[kWr];

@@ -2332,7 +2332,8 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const int64_t lag = dual ? 4 : std::max(1, nsets - 1);
     // chunk k waits on ev_out[k - nsets], recorded by copy_runs(k - nsets) once k - nsets <= k' - lag for
     // an earlier k': every wait needs lag < nsets
-    if (lag >= nsets) return restore(fail(c, NW_E_INVALID, "ops call: run-copy lag must be below the scratch sets"));
+    if (nchunks > nsets && lag >= nsets)
+        return restore(fail(c, NW_E_INVALID, "ops call: run-copy lag must be below the scratch sets"));
     int64_t runs_queued = 0;   // chunks [0, runs_queued) had their runs copies queued early (the last iteration)
     bool any_diag = false;
     // a resident packed batch (nw_align_ops_resident after nw_align_ops_packed): the band path's

@@ -194,14 +194,131 @@ class MultiGpuAligner:
         self._pool.shutdown()
 
 
-def _gather_ops(mine: OpsBatch, dist, rank: int, world: int) -> Optional[OpsBatch]:
-    """Rank 0 receives every rank's records + runs (compact payload) in rank order."""
-    payload = (mine.stats, mine.ops, mine.ops_off, mine.read_lens)
-    got: List = [None] * world if rank == 0 else None
-    dist.gather_object(payload, got, dst=0)
+def _populate(mm, lo: int, hi: int) -> None:
+    """Fault in bytes [lo, hi) of a shared mapping in one call (MADV_POPULATE_WRITE, Linux 5.14+;
+    without it the first writes fault page by page)."""
+    if hi <= lo:
+        return
+    page = 4096
+    a, b = lo - lo % page, min(len(mm), hi + (-hi) % page)
+    try:
+        mm.madvise(23, a, b - a)
+    except (OSError, ValueError, AttributeError):
+        pass
+
+
+def _gather_ops(mine: OpsBatch, dist, rank: int, world: int, method: str = "auto") -> Optional[OpsBatch]:
+    """Rank 0 receives every rank's records + runs in rank order (others get None) -- no pickling
+    (round 5 sent them through ``gather_object``: pickled objects over gloo TCP, ~4.5 GB into rank 0
+    for C4).  The part sizes go first (one ``all_gather`` of four int64 per rank), then ``method``:
+
+    * ``"shm"`` -- ranks on one host (torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE: the 8-GPU node of
+      SURVEY 8e): rank 0 creates one shared-memory segment laid out as the joined arrays (records 32 B
+      per read, runs uint32, run offsets int64, read lengths int64); every rank faults in and writes
+      its own slices in parallel (its run offsets already rebased); rank 0's result is views of the
+      segment (unlinked at once: it lives as long as the returned batch) -- no copy on rank 0;
+    * ``"p2p"`` -- otherwise: each rank sends its arrays as tensors (``isend``; records as bytes, runs
+      as int32) and rank 0 receives them into the joined arrays' slices (every ``irecv`` in flight);
+    * ``"auto"`` -- shm when the ranks share the host, else p2p.
+    """
+    import mmap
+    import os
+
+    import torch
+
+    if method == "auto":
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", "0") or 0)
+        method = "shm" if local == world else "p2p"
+    n = len(mine)
+    off0 = int(mine.ops_off[0]) if len(mine.ops_off) else 0
+    has = bool(mine.has_runs)
+    nr = int(mine.ops_off[-1]) - off0 if (len(mine.ops_off) and has) else 0
+    ops = np.ascontiguousarray(mine.ops[off0:off0 + nr]) if has else np.zeros(0, np.uint32)
+    stats = np.ascontiguousarray(mine.stats)
+    lens = np.ascontiguousarray(mine.read_lens, dtype=np.int64)
+    offs = np.ascontiguousarray(mine.ops_off, dtype=np.int64)
+    mine_sz = torch.tensor([n, nr, int(has), os.getpid()], dtype=torch.int64)
+    allsz = [torch.zeros(4, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allsz, mine_sz)
+    szs = [tuple(int(v) for v in t.tolist()) for t in allsz]
+    N = sum(z[0] for z in szs)
+    all_runs = all(z[2] for z in szs)
+    R = sum(z[1] for z in szs) if all_runs else 0
+    lo = sum(z[0] for z in szs[:rank])
+    rbase = sum(z[1] for z in szs[:rank])
+    sb = stats.dtype.itemsize
+    if method == "shm":
+        # layout: records | runs | run offsets | read lengths (8-byte aligned sections)
+        o_stats = 0
+        o_ops = N * sb
+        o_off = o_ops + 4 * R + (-(4 * R)) % 8
+        o_lens = o_off + 8 * (N + 1)
+        total = max(o_lens + 8 * N, 1)
+        path = f"/dev/shm/crispr_gather_{os.environ.get('MASTER_PORT', '0')}_{szs[0][3]}"
+        if rank == 0:
+            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+            os.ftruncate(fd, total)
+        dist.barrier()
+        if rank != 0:
+            fd = os.open(path, os.O_RDWR)
+        mm = mmap.mmap(fd, total)
+        os.close(fd)
+        view = np.ndarray(total, np.uint8, buffer=mm)
+        out_stats = view[o_stats:o_stats + N * sb].view(stats.dtype)
+        out_ops = view[o_ops:o_ops + 4 * R].view(np.uint32)
+        out_off = view[o_off:o_off + 8 * (N + 1)].view(np.int64)
+        out_lens = view[o_lens:o_lens + 8 * N].view(np.int64)
+        for a_, b_ in ((o_stats + lo * sb, o_stats + (lo + n) * sb), (o_ops + 4 * rbase, o_ops + 4 * (rbase + nr)),
+                       (o_off + 8 * lo, o_off + 8 * (lo + n + 1)), (o_lens + 8 * lo, o_lens + 8 * (lo + n))):
+            _populate(mm, a_, b_)
+        out_stats[lo:lo + n].view(np.uint8)[...] = stats.view(np.uint8)   # bytes: a structured copy is 10x slower
+        if all_runs:
+            out_ops[rbase:rbase + nr] = ops
+        if n:
+            np.subtract(offs[1:], offs[0] - rbase, out=out_off[lo + 1:lo + n + 1])
+        if rank == 0:
+            out_off[0] = 0
+        out_lens[lo:lo + n] = lens
+        dist.barrier()   # every part written
+        if rank != 0:
+            del view, out_stats, out_ops, out_off, out_lens
+            mm.close()
+            return None
+        os.unlink(path)   # the mapping stays until the batch is freed
+        res = OpsBatch(out_stats, out_ops, out_off, out_lens, mine.scale, mine.awidth, has_runs=all_runs)
+        res._shm = mm
+        return res
+    parts = [(stats.view(np.uint8), 0), (ops.view(np.int32), 1), (offs, 2), (lens, 3)]
     if rank != 0:
+        reqs = [dist.isend(torch.from_numpy(x.reshape(-1)), dst=0, tag=k) for x, k in parts if x.size]
+        for q in reqs:
+            q.wait()
         return None
-    return concat_ops([OpsBatch(s, o, f, l, mine.scale, mine.awidth) for s, o, f, l in got])
+    out_stats = np.empty(N, dtype=stats.dtype)
+    out_ops = np.empty(R, dtype=np.uint32)
+    out_off = np.zeros(N + 1, dtype=np.int64)
+    out_lens = np.empty(N, dtype=np.int64)
+    reqs, part_offs = [], []
+    plo = pr = 0
+    for r, (pn, pnr, _, _) in enumerate(szs):
+        dst = [out_stats[plo:plo + pn].view(np.uint8), out_ops[pr:pr + pnr].view(np.int32) if all_runs else None,
+               np.empty(pn + 1, np.int64), out_lens[plo:plo + pn]]
+        if r == 0:
+            for d, (x, _) in zip(dst, parts):
+                if d is not None and x.size:
+                    d[...] = x
+        else:
+            for k, d in enumerate(dst):
+                if d is not None and d.size:
+                    reqs.append(dist.irecv(torch.from_numpy(d.reshape(-1)), src=r, tag=k))
+        part_offs.append((dst[2], plo, pn, pr))
+        plo, pr = plo + pn, pr + pnr
+    for q in reqs:
+        q.wait()
+    for po, plo, pn, pr in part_offs:
+        if pn:
+            np.subtract(po[1:], po[0] - pr, out=out_off[plo + 1:plo + pn + 1])
+    return OpsBatch(out_stats, out_ops, out_off, out_lens, mine.scale, mine.awidth, has_runs=all_runs)
 
 
 def align_sharded(amplicon: str, buf: np.ndarray, offsets: np.ndarray, aligner, dist=None,

@@ -193,3 +193,76 @@ def test_multi_device_resident_second_pass():
     with pytest.raises(Exception):
         multi.align_ops(None, off[:100], resident=True)
     multi.close()
+
+
+def _gather_worker(rank, world, port, out_dir, n, method):
+    import time
+
+    from crispresso_amd import _lib
+    from crispresso_amd.aligner import OpsBatch
+    from crispresso_amd.distributed import _gather_ops
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.Generator(np.random.PCG64(rank))
+    lo, hi = shard_range(n, world, rank)
+    m = hi - lo
+    stats = np.zeros(m, _lib.STAT_DTYPE)
+    stats["aln_len"] = rng.integers(200, 300, m)
+    stats["score"] = np.arange(lo, hi)
+    cnt = rng.integers(1, 4, m)
+    off = np.zeros(m + 1, np.int64)
+    np.cumsum(cnt, out=off[1:])
+    ops = (np.arange(int(off[-1]), dtype=np.uint32) + np.uint32(7 * rank)) & np.uint32(0x3fffffff)
+    mine = OpsBatch(stats, ops, off, rng.integers(220, 260, m).astype(np.int64), 2)
+    dist.barrier()
+    t0 = time.perf_counter()
+    res = _gather_ops(mine, dist, rank, world, method)
+    dt = time.perf_counter() - t0
+    if rank == 0:
+        np.save(os.path.join(out_dir, "g_stats.npy"), res.stats)
+        np.save(os.path.join(out_dir, "g_ops.npy"), res.ops)
+        np.save(os.path.join(out_dir, "g_off.npy"), res.ops_off)
+        np.save(os.path.join(out_dir, "g_lens.npy"), res.read_lens)
+        nbytes = res.stats.nbytes + res.ops.nbytes + res.ops_off.nbytes + res.read_lens.nbytes
+        with open(os.path.join(out_dir, "g_rate.txt"), "w") as f:
+            f.write(f"{nbytes / dt / 1e9:.3f} {dt:.3f}")
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("method,n", [("shm", 10_000_000), ("p2p", 1_000_000)])
+def test_gather_records_and_runs_scales(tmp_path, method, n):
+    """Rank 0 gathers 10M reads' records + runs (about 45 B per read, ~0.5 GB) of a world-2 job
+    without pickling: shared memory between the ranks of one host (>= 2 GB/s here), tensors
+    point-to-point otherwise; the joined arrays equal the parts concatenated in read order."""
+    from crispresso_amd import _lib
+    from crispresso_amd.aligner import OpsBatch
+    from crispresso_amd.distributed import concat_ops
+
+    mp.start_processes(_gather_worker, args=(2, _free_port(), str(tmp_path), n, method), nprocs=2, join=True,
+                       start_method="fork")
+    parts = []
+    for rank in range(2):
+        rng = np.random.Generator(np.random.PCG64(rank))
+        lo, hi = shard_range(n, 2, rank)
+        m = hi - lo
+        stats = np.zeros(m, _lib.STAT_DTYPE)
+        stats["aln_len"] = rng.integers(200, 300, m)
+        stats["score"] = np.arange(lo, hi)
+        cnt = rng.integers(1, 4, m)
+        off = np.zeros(m + 1, np.int64)
+        np.cumsum(cnt, out=off[1:])
+        ops = (np.arange(int(off[-1]), dtype=np.uint32) + np.uint32(7 * rank)) & np.uint32(0x3fffffff)
+        parts.append(OpsBatch(stats, ops, off, rng.integers(220, 260, m).astype(np.int64), 2))
+    want = concat_ops(parts)
+    assert np.array_equal(np.load(tmp_path / "g_stats.npy"), want.stats)
+    assert np.array_equal(np.load(tmp_path / "g_ops.npy"), want.ops)
+    assert np.array_equal(np.load(tmp_path / "g_off.npy"), want.ops_off)
+    assert np.array_equal(np.load(tmp_path / "g_lens.npy"), want.read_lens)
+    rate, secs = map(float, open(tmp_path / "g_rate.txt").read().split())
+    print(f"gather {method}: {rate:.2f} GB/s ({secs:.3f} s)")
+    if method == "shm":
+        assert rate >= 2.0, rate
