@@ -1187,6 +1187,21 @@ def main():
             "downstream_quantification": quant,
             "upstream_merge": legs["merge"],
         }
+
+        def pick(d, *ks):
+            return {k: d.get(k) for k in ks} if isinstance(d, dict) else None
+        # the line's last key (a driver record keeps the line's tail): the figures the long keys above hold
+        line["summary"] = {
+            "value_resident": value, "ms_per_step": ms_step,
+            "call_pcie": pick(line["call_pcie"], "value", "ms_per_step"),
+            "roofline": pick(line["roofline"], "frac", "achieved", "traffic", "call_frac"),
+            "cpu_baseline": pick(cpu, "value", "cores", "kind"),
+            "sample_mismatches": (check or {}).get("sample_mismatches") if isinstance(check, dict) else None,
+            "resident_same_as_call": (resident_check or {}).get("same_as_call") if isinstance(resident_check, dict) else None,
+            "legs_ms_per_step": {k: (line.get(k) or {}).get("ms_per_step") if isinstance(line.get(k), dict) else None
+                                 for k in ("c4" if world > 1 else "c4_shard", "pooled", "dual_alignment", "c1_shape",
+                                           "downstream_quantification", "upstream_merge")},
+        }
         print(json.dumps(line), flush=True)
     for b in (pb, po, p_packed, p_stats, p_off, p_ops):
         b.close()

@@ -654,27 +654,46 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 bool ok = false;
                 int gk = 0;
                 // the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
-                // registers (one branch per case: a wave holding both runs both, masked)
-                auto test = [&](auto del_tag) {
-                    constexpr bool DEL = decltype(del_tag)::value;
-                    auto wl = [&](int t) -> unsigned { return DEL ? (t < n2 ? amp2s[t] : 0u) : rw[t]; };
-                    auto ws = [&](int t) -> unsigned { return DEL ? rw[t] : (t < n2 ? amp2s[t] : 0u); };
+                // registers, picked per lane (deletion and insertion reads in one pass over the shifts)
+                if (ci) {
+                    auto am = [&](int t) -> unsigned { return t < n2 ? amp2s[t] : 0u; };
+                    auto wl = [&](int t) -> unsigned { return del ? am(t) : rw[t]; };
+                    auto ws = [&](int t) -> unsigned { return del ? rw[t] : am(t); };
                     bool o = true;
-                    // shifts sh = 0 .. kab + 3 of l (a runtime loop); for sh <= kab the pair test G[s2] > F[s1]
-                    // (s1 < s2) as a running maximum of F: every earlier shift's for s2 < kab, shifts
-                    // 1 .. kab - 1 for s2 = kab (the pair (0, kab) is the candidate)
+                    // first and last mismatch of a shift (one side's sequence shifted by sh against the
+                    // other's, P positions): scans from either end that stop as soon as every lane has found
+                    // one (random sequence mismatches within a word; only the two diagonals of the
+                    // candidate run to the gap).  Mismatches: 0 (f == P), 1 (f == g - 1) or >= 2 -- all the
+                    // score test needs (its bound falls with the count)
+                    auto ends = [&](auto lw, auto rw2, int sh, int P, int* f, int* g) {
+                        int ff = P, gg = 0;
+#pragma unroll
+                        for (int t = 0; t < 17; ++t) {
+                            if (__ballot(ff == P && 16 * t < P) == 0ull) break;
+                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+                            ff = (ff == P && mk != 0u) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : ff;
+                        }
+#pragma unroll
+                        for (int t = 16; t >= 0; --t) {
+                            if (__ballot(gg == 0 && ff < P) == 0ull) break;   // (words past P: mk == 0)
+                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+                            gg = (gg == 0 && mk != 0u) ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : gg;
+                        }
+                        *f = ff;
+                        *g = gg;
+                    };
+                    auto cnt = [](int f, int g, int P) { return f == P ? 0 : (f == g - 1 ? 1 : 2); };
+                    // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
+                    // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
+                    // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
                     int f0 = Ls, fmax_all = -1, fmax_1 = -1;
                     for (int sh = 0; sh <= kab + 3; ++sh) {
                         const int P = min(Ls, Ll - sh);
-                        int c = 0, f = Ls, g = 0;
-#pragma unroll
-                        for (int t = 0; t < 17; ++t) {
-                            const unsigned z = __builtin_amdgcn_alignbit(wl(t + 1), wl(t), (unsigned)(2 * sh)) ^ ws(t);
-                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
-                            c += __builtin_popcount(mk);
-                            f = (mk != 0u && f == Ls) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : f;
-                            g = mk != 0u ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : g;
-                        }
+                        int f, g;
+                        ends(wl, ws, sh, P, &f, &g);
+                        const int c = cnt(f, g, P);
                         o = o && mm * (P - c) - xx * c < S;
                         if (sh <= kab) {
                             if (sh == 0) f0 = f;
@@ -685,18 +704,13 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         }
                     }
                     for (int sh = 1; sh <= 3; ++sh) {   // s shifted by sh against l: Ls - sh pairs
-                        int c = 0;
-#pragma unroll
-                        for (int t = 0; t < 16; ++t) {
-                            const unsigned z = __builtin_amdgcn_alignbit(ws(t + 1), ws(t), (unsigned)(2 * sh)) ^ wl(t);
-                            c += __builtin_popcount((z | (z >> 1)) & vmask(t, Ls - sh));
-                        }
+                        int f, g;
+                        ends(ws, wl, sh, Ls - sh, &f, &g);
+                        const int c = cnt(f, g, Ls - sh);
                         o = o && mm * (Ls - sh - c) - xx * c < S;
                     }
-                    ok = o && gk >= 1 && gk <= f0;
-                };
-                if (ci && del) test(std::true_type{});
-                if (ci && !del) test(std::false_type{});
+                    ok = ci && o && gk >= 1 && gk <= f0;
+                }
                 indel1 = __ballot(ok);
                 ind_q = gk;
                 ind_k = kab;
