@@ -372,6 +372,7 @@ def quant_leg(al, amplicon, buf, offsets, n_reads, steps, warmup, rank, world, c
                   "bytes, more runs than a lane holds -- through nwq::expand_rows + nwq::quant_kernel) + "
                   "nwq::quant_reduce",
         "kernel_ms_avg": kavg,
+        "lane_fallbacks": q.last_lane_fallbacks,
         "roofline": {"bound": "hbm", "achieved": algo / (kavg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": qp["traffic"] if qp else None,

@@ -53,7 +53,7 @@ EXPORTS = (
 # Every symbol include/crispr_quant.h declares.
 QUANT_EXPORTS = (
     "nwq_create", "nwq_destroy", "nwq_last_error", "nwq_set_params", "nwq_totals_words", "nwq_run",
-    "nwq_run_device", "nwq_run_device_ops",
+    "nwq_run_device", "nwq_run_device_ops", "nwq_lane_fallbacks",
 )
 
 
@@ -196,6 +196,7 @@ def load() -> ctypes.CDLL:
                             POINTER(c_float)]),
         "nwq_run_device": (c_int, [ctx_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                    c_void_p, POINTER(c_float)]),
+        "nwq_lane_fallbacks": (c_int64, [ctx_p]),
         "nwq_run_device_ops": (c_int, [ctx_p, c_char_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, POINTER(c_float)]),
         "nw_synth_offsets": (c_int64, [c_char_p, c_int32, c_int64, c_int64, ctypes.c_uint64, c_void_p, c_void_p,

@@ -131,12 +131,15 @@ __global__ __launch_bounds__(512) void quant_kernel(QArgs a) {
     // Reads go to waves in groups of 64: one coalesced load of the flags and
     // lengths, one coalesced store of the results; rows of the next read to
     // process are loaded while the current one is worked on.
+    // A work list (quant_lanes' fallback reads: a few dozen per 1M) goes one read per wave, not 64:
+    // a wave works through its group's reads one after another.
     const int64_t n_eff = a.list ? (int64_t)*a.list_count : a.n;
-    const int64_t ngroups = (n_eff + 63) >> 6;
+    const int gsz = a.list ? 1 : 64;
+    const int64_t ngroups = (n_eff + gsz - 1) / gsz;
     const int64_t tw = (int64_t)gridDim.x * wpb;
     for (int64_t grp = (int64_t)blockIdx.x * wpb + wave; grp < ngroups; grp += tw) {
-        const int64_t pos = (grp << 6) + lane;
-        const bool valid = pos < n_eff;
+        const int64_t pos = grp * gsz + lane;
+        const bool valid = lane < gsz && pos < n_eff;
         const int32_t ridx = valid ? (a.list ? a.list[pos] : (int32_t)pos) : 0;
         const int64_t idx = ridx;
         const unsigned mypre = valid ? (unsigned)a.pre[idx] : (unsigned)NWQ_PRE_UNMODIFIED;
@@ -515,8 +518,13 @@ __global__ __launch_bounds__(256) void expand_rows(const uint32_t* __restrict__ 
 // of align_seq inside an M or X run) and more than kQS / kQD / kQI substitutions / deletions /
 // insertions: such a read goes to the fallback list, which expand_rows + quant_kernel process
 // after this kernel (the same results, by the row path).
-constexpr int kQS = 16, kQD = 4, kQI = 4;   // per-lane list capacities (LDS, [cap][64] per wave)
-constexpr int kQWaveWords = kQS * 64 / 2 + (kQD + kQI) * 64 * 2;
+//
+// Occupancy (round 6): the lists are small (a C2 read has at most one indel and a few substitutions;
+// more go to the row path) and each wave first queues the reads of its 256 that need work (60 % of a
+// C2 batch are UNMODIFIED on input), so every lane of the main loop holds a read; blocks of 8 waves.
+constexpr int kQS = 8, kQD = 2, kQI = 2;    // per-lane list capacities (LDS, [cap][64] per wave)
+constexpr int kQSuper = 256;                // reads a wave queues at a time (uint16 queue in LDS)
+constexpr int kQWaveWords = kQS * 64 / 2 + (kQD + kQI) * 64 * 2 + kQSuper / 2;
 
 struct LArgs {
     const uint32_t* ops;
@@ -540,7 +548,7 @@ struct LArgs {
     uint32_t flags;
 };
 
-__global__ __launch_bounds__(256) void quant_lanes(const LArgs a) {
+__global__ __launch_bounds__(512) void quant_lanes(const LArgs a) {
     extern __shared__ uint32_t smem[];
     const int LEN = a.LEN;
     uint32_t* blk = smem;
@@ -555,6 +563,7 @@ __global__ __launch_bounds__(256) void quant_lanes(const LArgs a) {
     uint16_t* subl = (uint16_t*)(amp32 + a.amp_words + wave * kQWaveWords);   // [kQS][64]
     uint2* dell = (uint2*)(subl + kQS * 64);                                    // [kQD][64]
     uint2* insl = dell + kQD * 64;                                              // [kQI][64]
+    uint16_t* queue = (uint16_t*)(insl + kQI * 64);                             // [kQSuper]
 
     for (int i = threadIdx.x; i < a.nwords; i += blockDim.x) blk[i] = 0;
     const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
@@ -574,277 +583,297 @@ __global__ __launch_bounds__(256) void quant_lanes(const LArgs a) {
     uint32_t* hin = ctr + 4;
     uint32_t* hfs = hin + a.H;
 
-    const int64_t ngroups = (a.n + 63) >> 6;
+    const int64_t nsuper = (a.n + kQSuper - 1) / kQSuper;
     const int64_t tw = (int64_t)gridDim.x * wpb;
-    for (int64_t grp = (int64_t)blockIdx.x * wpb + wave; grp < ngroups; grp += tw) {
-        const int64_t r = (grp << 6) + lane;
-        const bool valid = r < a.n;
-        const unsigned pre = valid ? (unsigned)a.pre[r] : (unsigned)NWQ_PRE_UNMODIFIED;
-        const int L = valid ? a.stats[r * 8] : 1;
-        const bool skip = pre & NWQ_PRE_UNMODIFIED;
-        const bool badlen = L <= 0 || L > a.stride;
-        int4 res = make_int4((!skip && badlen) ? -1 : 0, 0, 0, 0);
-        const bool act = valid && !skip && !badlen;
-        bool fb = false, bad = false;
-        int nsub = 0, nsubi = 0, nd = 0, ni = 0;
-        unsigned subbits = 0;   // 1 exon, 2 splice, 4 exon & include, 8 splice & include
-        if (act) {
-            const int nid = a.stats[r * 8 + 1];
-            const int64_t k0 = a.ops_off[r], k1 = a.ops_off[r + 1];
-            const int64_t o0 = a.offsets[r];
-            const int Lb = (int)(a.offsets[r + 1] - o0);
-            const uint8_t* R = a.reads + (o0 - a.bias);
-            int left = LEN + Lb - L - nid;   // non-identical M columns
-            fb = left < 0;
-            int col = 0, ia = 0, jb = 0, ctype = -1, clen = 0;
-            for (int64_t k = k0; k <= k1 && !fb && !bad; ++k) {
-                int t = -2, l = 0;
-                if (k < k1) {
-                    const uint32_t op = a.ops[k];
-                    t = (int)(op >> 28);
-                    l = (int)(op & 0x0fffffffu);
-                }
-                if (t == ctype) {   // consecutive runs of one type: one column run
-                    clen += l;
-                    continue;
-                }
-                if (ctype == 0) {   // M: the '.' columns among the non-identical ones
-                    if (ia + clen > LEN) {
-                        bad = true;
-                    } else if (left > 0) {
-                        const uintptr_t ra = (uintptr_t)(R + jb);
-                        const uint32_t* rw = (const uint32_t*)(ra & ~(uintptr_t)3);
-                        const int rsh = (int)(ra & 3), ash = ia & 3;
-                        const uint32_t* aw = amp32 + (ia >> 2);
-                        uint32_t rlo = rw[0], alo = aw[0];
-                        for (int p = 0, q = 0; p < clen && left > 0; p += 4, ++q) {
-                            const uint32_t rhi = rw[q + 1], ahi = aw[q + 1];
-                            const uint32_t rv = __builtin_amdgcn_alignbyte(rhi, rlo, rsh);
-                            const uint32_t av = __builtin_amdgcn_alignbyte(ahi, alo, ash);
-                            rlo = rhi;
-                            alo = ahi;
-                            uint32_t x = rv ^ av;
-                            if (clen - p < 4) x &= (1u << (8 * (clen - p))) - 1u;
-                            while (x) {
-                                const int b = __builtin_ctz(x) >> 3;
-                                x &= ~(255u << (8 * b));
-                                const unsigned cb = (rv >> (8 * b)) & 255u, ca = (av >> (8 * b)) & 255u;
-                                if (cb == '-') {   // a '-' byte of the read: a deletion column of align_seq
-                                    fb = true;
-                                    break;
+    for (int64_t sg = (int64_t)blockIdx.x * wpb + wave; sg < nsuper; sg += tw) {
+        // queue the reads that need work (not UNMODIFIED, a valid length); the others' results now
+        const int64_t r_base = sg * kQSuper;
+        int qn = 0;
+        for (int h = 0; h < kQSuper / 64; ++h) {
+            const int64_t r = r_base + 64 * h + lane;
+            const bool valid = r < a.n;
+            const unsigned pre = valid ? (unsigned)a.pre[r] : (unsigned)NWQ_PRE_UNMODIFIED;
+            const int L = valid ? a.stats[r * 8] : 1;
+            const bool skip = pre & NWQ_PRE_UNMODIFIED;
+            const bool badlen = L <= 0 || L > a.stride;
+            const bool act = valid && !skip && !badlen;
+            if (valid && !act) a.out[r] = make_int4((!skip && badlen) ? -1 : 0, 0, 0, 0);
+            const unsigned long long m = ballot(act);
+            if (act)
+                queue[qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+                    (uint16_t)(64 * h + lane);
+            qn += __popcll(m);
+        }
+        nw::lds_fence();
+        for (int q0 = 0; q0 < qn; q0 += 64) {
+            const bool act = q0 + lane < qn;
+            const int64_t r = act ? r_base + queue[q0 + lane] : a.n;
+            const bool valid = act;
+            const unsigned pre = act ? (unsigned)a.pre[r] : (unsigned)NWQ_PRE_UNMODIFIED;
+            const int L = act ? a.stats[r * 8] : 1;
+            int4 res = make_int4(0, 0, 0, 0);
+            bool fb = false, bad = false;
+            int nsub = 0, nsubi = 0, nd = 0, ni = 0;
+            unsigned subbits = 0;   // 1 exon, 2 splice, 4 exon & include, 8 splice & include
+            if (act) {
+                const int nid = a.stats[r * 8 + 1];
+                const int64_t k0 = a.ops_off[r], k1 = a.ops_off[r + 1];
+                const int64_t o0 = a.offsets[r];
+                const int Lb = (int)(a.offsets[r + 1] - o0);
+                const uint8_t* R = a.reads + (o0 - a.bias);
+                int left = LEN + Lb - L - nid;   // non-identical M columns
+                fb = left < 0;
+                int col = 0, ia = 0, jb = 0, ctype = -1, clen = 0;
+                for (int64_t k = k0; k <= k1 && !fb && !bad; ++k) {
+                    int t = -2, l = 0;
+                    if (k < k1) {
+                        const uint32_t op = a.ops[k];
+                        t = (int)(op >> 28);
+                        l = (int)(op & 0x0fffffffu);
+                    }
+                    if (t == ctype) {   // consecutive runs of one type: one column run
+                        clen += l;
+                        continue;
+                    }
+                    if (ctype == 0) {   // M: the '.' columns among the non-identical ones
+                        if (ia + clen > LEN) {
+                            bad = true;
+                        } else if (left > 0) {
+                            const uintptr_t ra = (uintptr_t)(R + jb);
+                            const uint32_t* rw = (const uint32_t*)(ra & ~(uintptr_t)3);
+                            const int rsh = (int)(ra & 3), ash = ia & 3;
+                            const uint32_t* aw = amp32 + (ia >> 2);
+                            uint32_t rlo = rw[0], alo = aw[0];
+                            for (int p = 0, q = 0; p < clen && left > 0; p += 4, ++q) {
+                                const uint32_t rhi = rw[q + 1], ahi = aw[q + 1];
+                                const uint32_t rv = __builtin_amdgcn_alignbyte(rhi, rlo, rsh);
+                                const uint32_t av = __builtin_amdgcn_alignbyte(ahi, alo, ash);
+                                rlo = rhi;
+                                alo = ahi;
+                                uint32_t x = rv ^ av;
+                                if (clen - p < 4) x &= (1u << (8 * (clen - p))) - 1u;
+                                while (x) {
+                                    const int b = __builtin_ctz(x) >> 3;
+                                    x &= ~(255u << (8 * b));
+                                    const unsigned cb = (rv >> (8 * b)) & 255u, ca = (av >> (8 * b)) & 255u;
+                                    if (cb == '-') {   // a '-' byte of the read: a deletion column of align_seq
+                                        fb = true;
+                                        break;
+                                    }
+                                    if ((cb ^ ca) == 0x20u && cb >= 'a' && cb <= 'z') continue;   // '|' (case)
+                                    --left;
+                                    const int qp = ia + p + b;
+                                    if ((a.rowpos[qp] >> a.lut[cb]) & 1u) continue;   // ':'
+                                    if (ign_sub) continue;
+                                    if (nsub >= kQS) {
+                                        fb = true;
+                                        break;
+                                    }
+                                    subl[nsub * 64 + lane] = (uint16_t)qp;
+                                    ++nsub;
+                                    const unsigned tb = tbl[qp];
+                                    nsubi += tb & T_INC;
+                                    subbits |= ((tb & T_EXON) ? 1u : 0u) | ((tb & T_SPL) ? 2u : 0u);
+                                    if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
                                 }
-                                if ((cb ^ ca) == 0x20u && cb >= 'a' && cb <= 'z') continue;   // '|' (case)
-                                --left;
-                                const int qp = ia + p + b;
-                                if ((a.rowpos[qp] >> a.lut[cb]) & 1u) continue;   // ':'
-                                if (ign_sub) continue;
-                                if (nsub >= kQS) {
-                                    fb = true;
-                                    break;
-                                }
-                                subl[nsub * 64 + lane] = (uint16_t)qp;
-                                ++nsub;
-                                const unsigned tb = tbl[qp];
-                                nsubi += tb & T_INC;
-                                subbits |= ((tb & T_EXON) ? 1u : 0u) | ((tb & T_SPL) ? 2u : 0u);
-                                if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
+                                if (fb) break;
                             }
-                            if (fb) break;
                         }
-                    }
-                    col += clen;
-                    ia += clen;
-                    jb += clen;
-                } else if (ctype == 2) {   // Y: a deletion (its amplicon positions)
-                    if (ia + clen > LEN) {
-                        bad = true;
-                    } else if (!ign_del) {
-                        if (nd >= kQD) {
-                            fb = true;
-                        } else {
-                            const int e = ia + clen;
-                            const unsigned f = (incp[e] - incp[ia] > 0 ? R_INC : 0) | (splp[e] - splp[ia] > 0 ? R_SPL : 0);
-                            dell[nd * 64 + lane] = make_uint2((unsigned)ia | ((unsigned)clen << 16),
-                                                              f | ((unsigned)(exop[e] - exop[ia]) << 16));
-                            ++nd;
+                        col += clen;
+                        ia += clen;
+                        jb += clen;
+                    } else if (ctype == 2) {   // Y: a deletion (its amplicon positions)
+                        if (ia + clen > LEN) {
+                            bad = true;
+                        } else if (!ign_del) {
+                            if (nd >= kQD) {
+                                fb = true;
+                            } else {
+                                const int e = ia + clen;
+                                const unsigned f = (incp[e] - incp[ia] > 0 ? R_INC : 0) | (splp[e] - splp[ia] > 0 ? R_SPL : 0);
+                                dell[nd * 64 + lane] = make_uint2((unsigned)ia | ((unsigned)clen << 16),
+                                                                  f | ((unsigned)(exop[e] - exop[ia]) << 16));
+                                ++nd;
+                            }
                         }
-                    }
-                    col += clen;
-                    ia += clen;
-                } else if (ctype == 1) {   // X: an insertion (its flanking reference positions)
-                    for (int p = 0; p < clen && !fb; ++p) fb = R[jb + p] == '-';
-                    if (!ign_ins && !fb) {
-                        if (ni >= kQI) {
-                            fb = true;
-                        } else {
-                            const int fa = col > 0 ? ia - 1 : -1;
-                            const int fbk = col + clen < L ? ia : (ia > 0 ? -ia : -1);
-                            unsigned f = 0;   // T_* and R_INC / R_EXON / R_SPL share bit positions
-                            if (fa >= 0 && fa < LEN) f |= tbl[fa];
-                            if (fbk >= 0 && fbk < LEN) f |= tbl[fbk];
-                            insl[ni * 64 + lane] = make_uint2(((unsigned)fa & 0xffffu) | ((unsigned)fbk << 16),
-                                                              (unsigned)clen | (f << 24));
-                            ++ni;
+                        col += clen;
+                        ia += clen;
+                    } else if (ctype == 1) {   // X: an insertion (its flanking reference positions)
+                        for (int p = 0; p < clen && !fb; ++p) fb = R[jb + p] == '-';
+                        if (!ign_ins && !fb) {
+                            if (ni >= kQI) {
+                                fb = true;
+                            } else {
+                                const int fa = col > 0 ? ia - 1 : -1;
+                                const int fbk = col + clen < L ? ia : (ia > 0 ? -ia : -1);
+                                unsigned f = 0;   // T_* and R_INC / R_EXON / R_SPL share bit positions
+                                if (fa >= 0 && fa < LEN) f |= tbl[fa];
+                                if (fbk >= 0 && fbk < LEN) f |= tbl[fbk];
+                                insl[ni * 64 + lane] = make_uint2(((unsigned)fa & 0xffffu) | ((unsigned)fbk << 16),
+                                                                  (unsigned)clen | (f << 24));
+                                ++ni;
+                            }
                         }
+                        col += clen;
+                        jb += clen;
+                    } else if (ctype >= 3) {
+                        fb = true;
                     }
-                    col += clen;
-                    jb += clen;
-                } else if (ctype >= 3) {
-                    fb = true;
+                    ctype = t;
+                    clen = l;
                 }
-                ctype = t;
-                clen = l;
+                if (!fb && !bad && (col != L || jb != Lb)) fb = true;
+                if (!fb && !bad && ia != LEN) bad = true;
+                if (bad) res = make_int4(-1, 0, 0, 0);
             }
-            if (!fb && !bad && (col != L || jb != Lb)) fb = true;
-            if (!fb && !bad && ia != LEN) bad = true;
-            if (bad) res = make_int4(-1, 0, 0, 0);
-        }
-        // the reads left to the row path: one atomic per wave
-        {
-            const unsigned long long fbm = ballot(fb);
-            if (fbm) {
-                int base = 0;
-                if (lane == 0) base = atomicAdd(a.fb_count, __popcll(fbm));
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (fb) a.fb_list[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fbm >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)fbm, 0u))] = (int32_t)r;
-            }
-        }
-        if (act && !fb && !bad) {
-            // classification (CORE:530-575)
-            bool hit = nsubi > 0;
-            for (int j = 0; j < nd; ++j) hit |= (dell[j * 64 + lane].y & R_INC) != 0;
-            for (int j = 0; j < ni; ++j) hit |= ((insl[j * 64 + lane].y >> 24) & R_INC) != 0;
-            const int cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
-            const bool windowed = cls == 1 && a.window != 0;
-            // NHEJ window filter (CORE:611-641): deletion_positions_flat is recomputed only when
-            // a deletion survives the filter
-            bool anykept = false;
-            for (int j = 0; j < nd; ++j) anykept |= !windowed || (dell[j * 64 + lane].y & R_INC);
-            const bool post_sel = windowed && anykept;
-            int ndel = 0, exdel = 0;
-            bool spldel = false;
-            for (int j = 0; j < nd; ++j) {
-                uint2 d = dell[j * 64 + lane];
-                const bool kept = !windowed || (d.y & R_INC);
-                const bool post = post_sel ? kept : true;
-                d.y |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
-                dell[j * 64 + lane] = d;
-                ndel += kept ? (int)(d.x >> 16) : 0;
-                exdel += post ? (int)(d.y >> 16) : 0;
-                spldel |= post && (d.y & R_SPL);
-            }
-            int nins = 0, insex_len = 0;
-            bool insex = false, insspl = false;
-            for (int j = 0; j < ni; ++j) {
-                const uint2 e = insl[j * 64 + lane];
-                const int fa = (int)(short)(e.x & 0xffffu), fbk = (int)(short)(e.x >> 16);
-                const int sz = (int)(e.y & 0xffffffu);
-                const unsigned f = e.y >> 24;
-                const bool kept = !windowed || (f & R_INC);
-                insspl |= (f & R_SPL) != 0;
-                if (kept) {
-                    nins += sz;
-                    if (f & R_EXON) {
-                        insex = true;
-                        insex_len += sz;
-                    }
-                    if (cls != 0) {
-                        const int wa = fa < 0 ? fa + LEN : fa, wb = fbk < 0 ? fbk + LEN : fbk;
-                        atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)sz);
-                        if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)sz);
-                    }
+            // the reads left to the row path: one atomic per wave
+            {
+                const unsigned long long fbm = ballot(fb);
+                if (fbm) {
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(a.fb_count, __popcll(fbm));
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    if (fb) a.fb_list[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fbm >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)fbm, 0u))] = (int32_t)r;
                 }
             }
-            const int n_mut = windowed ? nsubi : nsub;
-            bool noncoding = false;
-            if ((flags & F_FRAMESHIFT) && cls != 0) {   // CORE:653-725
-                const bool sub_exon = windowed ? (subbits & 4u) : (subbits & 1u);
-                const bool sub_spl = windowed ? (subbits & 8u) : (subbits & 2u);
-                const int eff = insex_len - exdel;
-                const bool exon_mod = insex || exdel > 0 || sub_exon;
-                const bool has_lens = insex || exdel > 0;
-                if (sub_spl || spldel || insspl) atomicAdd(ctr + C_SPLICE, 1u);
-                if (exon_mod) {
-                    if (!has_lens) {
-                        atomicAdd(ctr + C_NONFS, 1u);
-                        atomicAdd(hin + LEN, 1u);
-                    } else if (eff % 3 == 0) {
-                        atomicAdd(ctr + C_NONFS, 1u);
-                        atomicAdd(hin + LEN + eff, 1u);
+            if (act && !fb && !bad) {
+                // classification (CORE:530-575)
+                bool hit = nsubi > 0;
+                for (int j = 0; j < nd; ++j) hit |= (dell[j * 64 + lane].y & R_INC) != 0;
+                for (int j = 0; j < ni; ++j) hit |= ((insl[j * 64 + lane].y >> 24) & R_INC) != 0;
+                const int cls = (pre & NWQ_PRE_HDR) ? 2 : (pre & NWQ_PRE_MIXED) ? 3 : hit ? 1 : 0;
+                const bool windowed = cls == 1 && a.window != 0;
+                // NHEJ window filter (CORE:611-641): deletion_positions_flat is recomputed only when
+                // a deletion survives the filter
+                bool anykept = false;
+                for (int j = 0; j < nd; ++j) anykept |= !windowed || (dell[j * 64 + lane].y & R_INC);
+                const bool post_sel = windowed && anykept;
+                int ndel = 0, exdel = 0;
+                bool spldel = false;
+                for (int j = 0; j < nd; ++j) {
+                    uint2 d = dell[j * 64 + lane];
+                    const bool kept = !windowed || (d.y & R_INC);
+                    const bool post = post_sel ? kept : true;
+                    d.y |= (kept ? R_KEPT : 0) | (post ? R_POST : 0);
+                    dell[j * 64 + lane] = d;
+                    ndel += kept ? (int)(d.x >> 16) : 0;
+                    exdel += post ? (int)(d.y >> 16) : 0;
+                    spldel |= post && (d.y & R_SPL);
+                }
+                int nins = 0, insex_len = 0;
+                bool insex = false, insspl = false;
+                for (int j = 0; j < ni; ++j) {
+                    const uint2 e = insl[j * 64 + lane];
+                    const int fa = (int)(short)(e.x & 0xffffu), fbk = (int)(short)(e.x >> 16);
+                    const int sz = (int)(e.y & 0xffffffu);
+                    const unsigned f = e.y >> 24;
+                    const bool kept = !windowed || (f & R_INC);
+                    insspl |= (f & R_SPL) != 0;
+                    if (kept) {
+                        nins += sz;
+                        if (f & R_EXON) {
+                            insex = true;
+                            insex_len += sz;
+                        }
+                        if (cls != 0) {
+                            const int wa = fa < 0 ? fa + LEN : fa, wb = fbk < 0 ? fbk + LEN : fbk;
+                            atomicAdd(blk + V_AVG_INS * LEN + wa, (unsigned)sz);
+                            if (wb != wa) atomicAdd(blk + V_AVG_INS * LEN + wb, (unsigned)sz);
+                        }
+                    }
+                }
+                const int n_mut = windowed ? nsubi : nsub;
+                bool noncoding = false;
+                if ((flags & F_FRAMESHIFT) && cls != 0) {   // CORE:653-725
+                    const bool sub_exon = windowed ? (subbits & 4u) : (subbits & 1u);
+                    const bool sub_spl = windowed ? (subbits & 8u) : (subbits & 2u);
+                    const int eff = insex_len - exdel;
+                    const bool exon_mod = insex || exdel > 0 || sub_exon;
+                    const bool has_lens = insex || exdel > 0;
+                    if (sub_spl || spldel || insspl) atomicAdd(ctr + C_SPLICE, 1u);
+                    if (exon_mod) {
+                        if (!has_lens) {
+                            atomicAdd(ctr + C_NONFS, 1u);
+                            atomicAdd(hin + LEN, 1u);
+                        } else if (eff % 3 == 0) {
+                            atomicAdd(ctr + C_NONFS, 1u);
+                            atomicAdd(hin + LEN + eff, 1u);
+                        } else {
+                            atomicAdd(ctr + C_FS, 1u);
+                            atomicAdd(hfs + LEN + eff, 1u);
+                        }
                     } else {
-                        atomicAdd(ctr + C_FS, 1u);
-                        atomicAdd(hfs + LEN + eff, 1u);
+                        atomicAdd(ctr + C_NONMOD, 1u);
                     }
-                } else {
-                    atomicAdd(ctr + C_NONMOD, 1u);
+                    noncoding = !exon_mod;
                 }
-                noncoding = !exon_mod;
-            }
-            res = cls ? make_int4(cls, n_mut, nins, ndel) : make_int4(0, 0, 0, 0);
+                res = cls ? make_int4(cls, n_mut, nins, ndel) : make_int4(0, 0, 0, 0);
 
-            // the read's vector increments, once per distinct position
-            auto is_flank = [&](int p) {
+                // the read's vector increments, once per distinct position
+                auto is_flank = [&](int p) {
+                    for (int j = 0; j < ni; ++j) {
+                        const unsigned x = insl[j * 64 + lane].x;
+                        const int fa = (int)(short)(x & 0xffffu), fbk = (int)(short)(x >> 16);
+                        if ((fa < 0 ? fa + LEN : fa) == p || (fbk < 0 ? fbk + LEN : fbk) == p) return true;
+                    }
+                    return false;
+                };
+                auto incr = [&](int p, unsigned sub, unsigned del, unsigned ins, unsigned sub_post, unsigned del_post,
+                                unsigned dsz, bool kept) {
+                    uint32_t* h = blk + p;
+                    if (cls == 3) {
+                        vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
+                    } else if (cls == 2) {
+                        vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
+                    } else if (cls == 1) {
+                        vadd(h, V_MUT, LEN, hide ? sub_post : sub);
+                        vadd(h, V_DEL, LEN, hide ? del_post : del);
+                        vadd(h, V_INS, LEN, ins);
+                    }
+                    vadd(h, V_ANY, LEN, 1u);
+                    if (noncoding) {
+                        vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
+                    }
+                    if (cls != 0 && del && kept) vadd(h, V_AVG_DEL, LEN, dsz);
+                };
+                for (int j = 0; j < nsub; ++j) {
+                    const int p = subl[j * 64 + lane];
+                    const unsigned sp = (!windowed || (tbl[p] & T_INC)) ? 1u : 0u;
+                    incr(p, 1u, 0u, is_flank(p) ? 1u : 0u, sp, 0u, 0u, false);
+                }
+                for (int j = 0; j < nd; ++j) {
+                    const uint2 d = dell[j * 64 + lane];
+                    const int s = (int)(d.x & 0xffffu), sz = (int)(d.x >> 16);
+                    const unsigned dp = (d.y & R_POST) ? 1u : 0u;
+                    const bool kept = d.y & R_KEPT;
+                    for (int p = s; p < s + sz; ++p) incr(p, 0u, 1u, (ni && is_flank(p)) ? 1u : 0u, 0u, dp, (unsigned)sz, kept);
+                }
                 for (int j = 0; j < ni; ++j) {
                     const unsigned x = insl[j * 64 + lane].x;
                     const int fa = (int)(short)(x & 0xffffu), fbk = (int)(short)(x >> 16);
-                    if ((fa < 0 ? fa + LEN : fa) == p || (fbk < 0 ? fbk + LEN : fbk) == p) return true;
-                }
-                return false;
-            };
-            auto incr = [&](int p, unsigned sub, unsigned del, unsigned ins, unsigned sub_post, unsigned del_post,
-                            unsigned dsz, bool kept) {
-                uint32_t* h = blk + p;
-                if (cls == 3) {
-                    vadd(h, V_MUT_MIX, LEN, sub); vadd(h, V_DEL_MIX, LEN, del); vadd(h, V_INS_MIX, LEN, ins);
-                } else if (cls == 2) {
-                    vadd(h, V_MUT_HDR, LEN, sub); vadd(h, V_DEL_HDR, LEN, del); vadd(h, V_INS_HDR, LEN, ins);
-                } else if (cls == 1) {
-                    vadd(h, V_MUT, LEN, hide ? sub_post : sub);
-                    vadd(h, V_DEL, LEN, hide ? del_post : del);
-                    vadd(h, V_INS, LEN, ins);
-                }
-                vadd(h, V_ANY, LEN, 1u);
-                if (noncoding) {
-                    vadd(h, V_MUT_NC, LEN, sub_post); vadd(h, V_DEL_NC, LEN, del_post); vadd(h, V_INS_NC, LEN, ins);
-                }
-                if (cls != 0 && del && kept) vadd(h, V_AVG_DEL, LEN, dsz);
-            };
-            for (int j = 0; j < nsub; ++j) {
-                const int p = subl[j * 64 + lane];
-                const unsigned sp = (!windowed || (tbl[p] & T_INC)) ? 1u : 0u;
-                incr(p, 1u, 0u, is_flank(p) ? 1u : 0u, sp, 0u, 0u, false);
-            }
-            for (int j = 0; j < nd; ++j) {
-                const uint2 d = dell[j * 64 + lane];
-                const int s = (int)(d.x & 0xffffu), sz = (int)(d.x >> 16);
-                const unsigned dp = (d.y & R_POST) ? 1u : 0u;
-                const bool kept = d.y & R_KEPT;
-                for (int p = s; p < s + sz; ++p) incr(p, 0u, 1u, (ni && is_flank(p)) ? 1u : 0u, 0u, dp, (unsigned)sz, kept);
-            }
-            for (int j = 0; j < ni; ++j) {
-                const unsigned x = insl[j * 64 + lane].x;
-                const int fa = (int)(short)(x & 0xffffu), fbk = (int)(short)(x >> 16);
-                const int w2[2] = {fa < 0 ? fa + LEN : fa, fbk < 0 ? fbk + LEN : fbk};
-                for (int h = 0; h < 2; ++h) {
-                    const int w = w2[h];
-                    if (h == 1 && w == w2[0]) continue;
-                    bool seen = false;
-                    for (int jj = 0; jj < j && !seen; ++jj) {
-                        const unsigned xx = insl[jj * 64 + lane].x;
-                        const int ga = (int)(short)(xx & 0xffffu), gb = (int)(short)(xx >> 16);
-                        seen = (ga < 0 ? ga + LEN : ga) == w || (gb < 0 ? gb + LEN : gb) == w;
+                    const int w2[2] = {fa < 0 ? fa + LEN : fa, fbk < 0 ? fbk + LEN : fbk};
+                    for (int h = 0; h < 2; ++h) {
+                        const int w = w2[h];
+                        if (h == 1 && w == w2[0]) continue;
+                        bool seen = false;
+                        for (int jj = 0; jj < j && !seen; ++jj) {
+                            const unsigned xx = insl[jj * 64 + lane].x;
+                            const int ga = (int)(short)(xx & 0xffffu), gb = (int)(short)(xx >> 16);
+                            seen = (ga < 0 ? ga + LEN : ga) == w || (gb < 0 ? gb + LEN : gb) == w;
+                        }
+                        for (int q = 0; q < nsub && !seen; ++q) seen = subl[q * 64 + lane] == w;
+                        for (int q = 0; q < nd && !seen; ++q) {
+                            const unsigned dx = dell[q * 64 + lane].x;
+                            seen = w >= (int)(dx & 0xffffu) && w < (int)(dx & 0xffffu) + (int)(dx >> 16);
+                        }
+                        if (!seen) incr(w, 0u, 0u, 1u, 0u, 0u, 0u, false);
                     }
-                    for (int q = 0; q < nsub && !seen; ++q) seen = subl[q * 64 + lane] == w;
-                    for (int q = 0; q < nd && !seen; ++q) {
-                        const unsigned dx = dell[q * 64 + lane].x;
-                        seen = w >= (int)(dx & 0xffffu) && w < (int)(dx & 0xffffu) + (int)(dx >> 16);
-                    }
-                    if (!seen) incr(w, 0u, 0u, 1u, 0u, 0u, 0u, false);
                 }
             }
+            if (valid && !fb) a.out[r] = res;
         }
-        if (valid && !fb) a.out[r] = res;
+        nw::lds_fence();   // every lane's queue reads before the next super-group's writes
     }
 
     __syncthreads();
@@ -903,6 +932,7 @@ struct nwq_ctx {
     int32_t LEN = 0;
     uint32_t flags = 0;
     int32_t window = 0;
+    int64_t lane_fallbacks = -1;     // the last nwq_run_device_ops' quant_lanes fallback count
     std::vector<int32_t> prefix;     // host copy of QArgs::prefix
     QBuf<int32_t> d_prefix;
     QBuf<uint32_t> d_partial;
@@ -1028,6 +1058,8 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
 }  // namespace
 
 extern "C" {
+
+int64_t nwq_lane_fallbacks(const nwq_ctx* c) { return c ? c->lane_fallbacks : -1; }
 
 int nwq_create(int device, nwq_ctx** out) {
     if (!out) return NW_E_INVALID;
@@ -1190,16 +1222,17 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
     const int pref_words = 3 * (LEN + 1) + (LEN + 3) / 4;
     const int base_words = nwords + pref_words;
     const int amp_words = (LEN + 3) / 4 + 2;
-    int lane_wpb = 4;
+    int lane_wpb = 8;
     while (lane_wpb > 1 && 4 * (base_words + amp_words + lane_wpb * nwq::kQWaveWords) > kMaxLds / 2) lane_wpb >>= 1;
     const int lane_lds = 4 * (base_words + amp_words + lane_wpb * nwq::kQWaveWords);
     const bool lanes = acgt && !(c->flags & nwq::F_NFIX) && lane_lds <= kMaxLds && n > 0 && !c->rows_only;
     QHIP(c, hipEventRecord(c->ev0, c->stream));   // kernel_ms covers the expansion too
+    c->lane_fallbacks = -1;
     if (lanes) {
         int per_cu = 0;
         QHIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwq::quant_lanes, 64 * lane_wpb, lane_lds));
         per_cu = std::max(per_cu, 1);
-        const int64_t groups = (n + 63) / 64;
+        const int64_t groups = (n + nwq::kQSuper - 1) / nwq::kQSuper;   // a wave's super-groups
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((groups + lane_wpb - 1) / lane_wpb,
                                                                      (int64_t)c->num_cus * per_cu));
         QHIP(c, c->d_fb.reserve(nn + 1));
@@ -1243,8 +1276,12 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
                            (const int32_t*)d_stats, d_reads, d_offsets, reads_bias, c->d_amp.p, c->d_rowpos.p,
                            c->d_lut.p, amplicon_len, d_pre, 0, n, c->d_aln.p, stride, c->d_fb.p, c->d_fb.p + nn);
         QHIP(c, hipGetLastError());
-        return run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms, true,
-                        c->d_fb.p, c->d_fb.p + nn, grid);
+        const int rc = run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms,
+                                true, c->d_fb.p, c->d_fb.p + nn, grid);
+        int32_t nfb = -1;
+        if (rc == NW_OK) QHIP(c, hipMemcpy(&nfb, c->d_fb.p + nn, sizeof nfb, hipMemcpyDeviceToHost));
+        c->lane_fallbacks = nfb;
+        return rc;
     }
     if (n > 0) {
         int wpb = 4;

@@ -233,6 +233,7 @@ class GpuQuantifier:
                                                  dev["reads"], dev["offsets"], dev["reads_bias"], stride, d_pre, n,
                                                  d_out, totals.ctypes.data, ctypes.byref(ms)), "nwq_run_device_ops")
         self.last_kernel_ms = ms.value
+        self.last_lane_fallbacks = int(self._lib.nwq_lane_fallbacks(self._ctx))
         return totals
 
     def unpack_totals(self, totals: np.ndarray, stride: int) -> Dict:

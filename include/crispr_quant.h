@@ -96,6 +96,11 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
                        int64_t reads_bias, int64_t stride, const uint8_t* d_pre, int64_t n, nwq_read* d_out,
                        int64_t* totals, float* kernel_ms);
 
+/* Reads the lane path of the last nwq_run_device_ops left to the row path (nwq::quant_lanes'
+ * fallback list: a '-' byte in the read, more substitutions / deletions / insertions than a lane
+ * holds); -1 when that run did not take the lane path.  A diagnostic (bench.py reports it). */
+int64_t nwq_lane_fallbacks(const nwq_ctx* c);
+
 #ifdef __cplusplus
 }
 #endif
