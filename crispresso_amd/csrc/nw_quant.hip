@@ -639,44 +639,55 @@ __global__ __launch_bounds__(512) void quant_lanes(const LArgs a) {
                         if (ia + clen > LEN) {
                             bad = true;
                         } else if (left > 0) {
+                            // 16 columns per step: the read's next four dwords loaded together (one
+                            // round trip per 16 columns instead of per 4), the amplicon's from LDS
                             const uintptr_t ra = (uintptr_t)(R + jb);
                             const uint32_t* rw = (const uint32_t*)(ra & ~(uintptr_t)3);
                             const int rsh = (int)(ra & 3), ash = ia & 3;
+                            const int wlast = (rsh + clen) >> 2;   // the last dword a step may read
                             const uint32_t* aw = amp32 + (ia >> 2);
                             uint32_t rlo = rw[0], alo = aw[0];
-                            for (int p = 0, q = 0; p < clen && left > 0; p += 4, ++q) {
-                                const uint32_t rhi = rw[q + 1], ahi = aw[q + 1];
-                                const uint32_t rv = __builtin_amdgcn_alignbyte(rhi, rlo, rsh);
-                                const uint32_t av = __builtin_amdgcn_alignbyte(ahi, alo, ash);
-                                rlo = rhi;
-                                alo = ahi;
-                                uint32_t x = rv ^ av;
-                                if (clen - p < 4) x &= (1u << (8 * (clen - p))) - 1u;
-                                while (x) {
-                                    const int b = __builtin_ctz(x) >> 3;
-                                    x &= ~(255u << (8 * b));
-                                    const unsigned cb = (rv >> (8 * b)) & 255u, ca = (av >> (8 * b)) & 255u;
-                                    if (cb == '-') {   // a '-' byte of the read: a deletion column of align_seq
-                                        fb = true;
-                                        break;
-                                    }
-                                    if ((cb ^ ca) == 0x20u && cb >= 'a' && cb <= 'z') continue;   // '|' (case)
-                                    --left;
-                                    const int qp = ia + p + b;
-                                    if ((a.rowpos[qp] >> a.lut[cb]) & 1u) continue;   // ':'
-                                    if (ign_sub) continue;
-                                    if (nsub >= kQS) {
-                                        fb = true;
-                                        break;
-                                    }
-                                    subl[nsub * 64 + lane] = (uint16_t)qp;
-                                    ++nsub;
-                                    const unsigned tb = tbl[qp];
-                                    nsubi += tb & T_INC;
-                                    subbits |= ((tb & T_EXON) ? 1u : 0u) | ((tb & T_SPL) ? 2u : 0u);
-                                    if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
+                            for (int p = 0, q = 0; p < clen && left > 0 && !fb; p += 16, q += 4) {
+                                uint32_t rn[4], an[4];
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) {
+                                    rn[i] = q + 1 + i <= wlast ? rw[q + 1 + i] : 0u;
+                                    an[i] = aw[q + 1 + i];
                                 }
-                                if (fb) break;
+#pragma unroll
+                                for (int i = 0; i < 4 && !fb; ++i) {
+                                    const int pi = p + 4 * i;
+                                    const uint32_t rv = __builtin_amdgcn_alignbyte(rn[i], i ? rn[i - 1] : rlo, rsh);
+                                    const uint32_t av = __builtin_amdgcn_alignbyte(an[i], i ? an[i - 1] : alo, ash);
+                                    uint32_t x = pi < clen ? rv ^ av : 0u;
+                                    if (clen - pi < 4) x &= (1u << (8 * (clen - pi))) - 1u;
+                                    while (x) {
+                                        const int b = __builtin_ctz(x) >> 3;
+                                        x &= ~(255u << (8 * b));
+                                        const unsigned cb = (rv >> (8 * b)) & 255u, ca = (av >> (8 * b)) & 255u;
+                                        if (cb == '-') {   // a '-' byte of the read: a deletion column of align_seq
+                                            fb = true;
+                                            break;
+                                        }
+                                        if ((cb ^ ca) == 0x20u && cb >= 'a' && cb <= 'z') continue;   // '|' (case)
+                                        --left;
+                                        const int qp = ia + pi + b;
+                                        if ((a.rowpos[qp] >> a.lut[cb]) & 1u) continue;   // ':'
+                                        if (ign_sub) continue;
+                                        if (nsub >= kQS) {
+                                            fb = true;
+                                            break;
+                                        }
+                                        subl[nsub * 64 + lane] = (uint16_t)qp;
+                                        ++nsub;
+                                        const unsigned tb = tbl[qp];
+                                        nsubi += tb & T_INC;
+                                        subbits |= ((tb & T_EXON) ? 1u : 0u) | ((tb & T_SPL) ? 2u : 0u);
+                                        if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
+                                    }
+                                }
+                                rlo = rn[3];
+                                alo = an[3];
                             }
                         }
                         col += clen;
