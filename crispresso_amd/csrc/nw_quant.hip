@@ -523,7 +523,8 @@ __global__ __launch_bounds__(256) void expand_rows(const uint32_t* __restrict__ 
 // more go to the row path) and each wave first queues the reads of its 256 that need work (60 % of a
 // C2 batch are UNMODIFIED on input), so every lane of the main loop holds a read; blocks of 8 waves.
 constexpr int kQS = 8, kQD = 2, kQI = 2;    // per-lane list capacities (LDS, [cap][64] per wave)
-constexpr int kQSuper = 256;                // reads a wave queues at a time (uint16 queue in LDS)
+constexpr int kQSuper = 128;                // reads a wave queues at a time (uint16 queue in LDS)
+constexpr int kQStep = 32;                  // M-run columns compared per step (their loads in flight together)
 constexpr int kQWaveWords = kQS * 64 / 2 + (kQD + kQI) * 64 * 2 + kQSuper / 2;
 
 struct LArgs {
@@ -639,27 +640,27 @@ __global__ __launch_bounds__(512) void quant_lanes(const LArgs a) {
                         if (ia + clen > LEN) {
                             bad = true;
                         } else if (left > 0) {
-                            // 16 columns per step: the read's next four dwords loaded together (one
-                            // round trip per 16 columns instead of per 4), the amplicon's from LDS
+                            // kQStep columns per step: the read's next kQStep / 4 dwords loaded together
+                            // (one round trip per kQStep columns instead of per 4), the amplicon's from LDS
                             const uintptr_t ra = (uintptr_t)(R + jb);
                             const uint32_t* rw = (const uint32_t*)(ra & ~(uintptr_t)3);
                             const int rsh = (int)(ra & 3), ash = ia & 3;
                             const int wlast = (rsh + clen) >> 2;   // the last dword a step may read
                             const uint32_t* aw = amp32 + (ia >> 2);
                             uint32_t rlo = rw[0], alo = aw[0];
-                            for (int p = 0, q = 0; p < clen && left > 0 && !fb; p += 16, q += 4) {
-                                uint32_t rn[4], an[4];
+                            for (int p = 0, q = 0; p < clen && left > 0 && !fb; p += kQStep, q += kQStep / 4) {
+                                uint32_t rn[kQStep / 4], an[kQStep / 4];
 #pragma unroll
-                                for (int i = 0; i < 4; ++i) {
+                                for (int i = 0; i < kQStep / 4; ++i) {
                                     rn[i] = q + 1 + i <= wlast ? rw[q + 1 + i] : 0u;
                                     an[i] = aw[q + 1 + i];
                                 }
 #pragma unroll
-                                for (int i = 0; i < 4 && !fb; ++i) {
+                                for (int i = 0; i < kQStep / 4; ++i) {
                                     const int pi = p + 4 * i;
                                     const uint32_t rv = __builtin_amdgcn_alignbyte(rn[i], i ? rn[i - 1] : rlo, rsh);
                                     const uint32_t av = __builtin_amdgcn_alignbyte(an[i], i ? an[i - 1] : alo, ash);
-                                    uint32_t x = pi < clen ? rv ^ av : 0u;
+                                    uint32_t x = (pi < clen && !fb) ? rv ^ av : 0u;
                                     if (clen - pi < 4) x &= (1u << (8 * (clen - pi))) - 1u;
                                     while (x) {
                                         const int b = __builtin_ctz(x) >> 3;
@@ -686,8 +687,8 @@ __global__ __launch_bounds__(512) void quant_lanes(const LArgs a) {
                                         if (tb & T_INC) subbits |= ((tb & T_EXON) ? 4u : 0u) | ((tb & T_SPL) ? 8u : 0u);
                                     }
                                 }
-                                rlo = rn[3];
-                                alo = an[3];
+                                rlo = rn[kQStep / 4 - 1];
+                                alo = an[kQStep / 4 - 1];
                             }
                         }
                         col += clen;
