@@ -323,6 +323,13 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             if (!(a.band_maxsub > p && a.gap_open > p && a.gap_open + p < 4 * a.band_maxsub)) break;
             indel_kmax = k;
         }
+    // three substitutions (below): with D = m La - 3 (m + x), every alignment but the diagonal scores below
+    // D when, beyond the per-read checks, x < m (|d| >= 6), 4 m + O, 2 m + 2 O and 3 O exceed 3 (m + x)
+    // (one gap leaving 4 or more residues unpaired, two gaps leaving 2, three gaps) and a jog through a
+    // neighbouring diagonal (two gaps, one residue of each sequence unpaired) with one mismatch scores below D
+    const int m3 = a.band_maxsub, x3 = 4 * sc5, O3 = a.gap_open, D3 = 3 * (m3 + x3);
+    const bool sub3_ok = sub2_ok && x3 < m3 && 4 * m3 + O3 > D3 && 2 * m3 + 2 * O3 > D3 && 3 * O3 > D3 &&
+                         m3 + 2 * O3 + (m3 + x3) > D3;
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
     const int sd = (int)(a.stride / 4);
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     auto batch = [&](long long r0, long long r_end, long long my_off, int my_len, bool exc) {
         const long long r = r0 + lane;
         unsigned long long cand = __ballot(my_len == La && !exc);   // reads of the amplicon's length
-        unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull;
+        unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull, sub3 = 0ull;
         unsigned long long known = 0ull;   // copies of the known sequence (KernelArgs::known2)
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
@@ -411,14 +418,19 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     for (int t = 0; t < 16; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
                     rw[16] = 0u;   // bases past the read: masked below
                 }
-                int k = 0, f = -1, l = -1;   // mismatches of the main diagonal, first and last base
+                int k = 0, f = -1, f2 = -1, l = -1;   // mismatches of the main diagonal, first, second and last base
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     if (t >= nw) continue;
                     const unsigned x = rw[t] ^ amp2s[t];
                     const unsigned m = (x | (x >> 1)) & vmask(t, La);
                     k += __builtin_popcount(m);
-                    if (m != 0u && f < 0) f = 16 * t + (__builtin_ctz(m) >> 1);
+                    if (m != 0u && f >= 0 && f2 < 0) f2 = 16 * t + (__builtin_ctz(m) >> 1);
+                    if (m != 0u && f < 0) {
+                        f = 16 * t + (__builtin_ctz(m) >> 1);
+                        const unsigned m2 = m & (m - 1u);
+                        if (m2 != 0u) f2 = 16 * t + (__builtin_ctz(m2) >> 1);
+                    }
                     if (m != 0u) l = 16 * t + ((31 - __builtin_clz(m)) >> 1);
                 }
                 exact = __ballot(c && k == 0);
@@ -464,6 +476,118 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     }
                     sub2 = __ballot(ok2);
                 }
+                // Three substitutions (round 6; bases f < f2 < l of the main diagonal, D = m La - 3 (m + x)).
+                // An alignment scores m (La - U) - (m + x) w - (its gaps' cost), U residues of each sequence
+                // unpaired and w mismatches; below D when m U + (m + x) w + gaps > 3 (m + x).  Left open by
+                // the gate above: (i) single diagonals 1 <= |d| <= 5 with too few mismatches (each must have
+                // more than (3 (m + x) - m |d|) / (m + x)); (ii) one gap between diagonals d1 (prefix) and d2
+                // (suffix), |d1|, |d2| <= 3, with at most w_max mismatches in all -- it exists iff, in read
+                // coordinates, the prefix's mismatches on d1 end before the suffix's on d2 begin (the suffix
+                // starts max(0, d2 - d1) read bases later: those are the gap's); (iii) a jog 0 -> +-1 -> 0
+                // with no mismatch: its middle covers the read bases (f, l] (d = +1) / [f, l) (d = -1), so a
+                // mismatch of that diagonal in [f + 1, l - 1] excludes both.  Then the diagonal is the unique
+                // optimum and M beats X and Y along it (a tie would be a second alignment scoring D).
+                const bool s3 = c && sub3_ok && k == 3;
+                if (__ballot(s3)) {
+                    // per diagonal d = -5 .. 5: mismatches (capped at 3), the first two and the last two
+                    // (read index; last ones + 1), over the diagonal's pairs
+                    int dc[11], df1[11], df2[11], dg1[11], dg2[11];
+                    // jogs (iii): diagonals +-1 against the 16 read bases from f + 1 (up to l - 1), one
+                    // word each from the packed stream (random sequence mismatches there; a read whose
+                    // diagonals +-1 match all 16 is left to the DP)
+                    bool jog_in[2] = {false, false};
+                    if (s3) {
+                        const int len = min(16, l - f - 1);
+                        const unsigned lm = len <= 0 ? 0u : (len >= 16 ? 0x55555555u : (0x55555555u >> (32 - 2 * len)));
+                        const unsigned rd = rword(my_off + f + 1);
+                        const unsigned zp = rd ^ aword(f), zm = rd ^ aword(f + 2);   // d = +1 / -1
+                        jog_in[1] = ((zp | (zp >> 1)) & lm) != 0u;
+                        jog_in[0] = ((zm | (zm >> 1)) & lm) != 0u;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 11; ++e) {
+                        const int d = e - 5;
+                        if (d == 0) {
+                            dc[e] = 3; df1[e] = f; df2[e] = f2; dg1[e] = l + 1; dg2[e] = f2 + 1;   // (k == 3)
+                            continue;
+                        }
+                        const int sh = d > 0 ? d : -d;
+                        // the first two and the last two mismatches (read index; the last ones + 1) by scans
+                        // from either end that stop once every lane has found two (random sequence: within a
+                        // word); the count up to 3 follows (3 when the second-last lies past the second)
+                        int a1 = La, a2 = La, b1 = 0, b2 = 0;
+                        auto word = [&](int t) -> unsigned {
+                            // d > 0: read base j = i + d against amplicon base i (words of i); d < 0: read
+                            // base j against amplicon base j - d (words of j)
+                            const unsigned am = d > 0 ? amp2s[t]
+                                                      : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
+                            const unsigned rd = d > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
+                            const unsigned z = rd ^ am;
+                            return (z | (z >> 1)) & vmask(t, La - sh);
+                        };
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) {
+                            if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
+                            const unsigned mk = word(t);
+                            const int off = 16 * t + (d > 0 ? d : 0);   // read index of the word's base 0
+                            if (mk != 0u && a1 == La) {
+                                a1 = off + (__builtin_ctz(mk) >> 1);
+                                const unsigned m2 = mk & (mk - 1u);
+                                if (m2 != 0u) a2 = off + (__builtin_ctz(m2) >> 1);
+                            } else if (mk != 0u && a2 == La) {
+                                a2 = off + (__builtin_ctz(mk) >> 1);
+                            }
+                        }
+#pragma unroll
+                        for (int t = 15; t >= 0; --t) {
+                            if (__ballot(s3 && b2 == 0 && a1 < La) == 0ull) break;
+                            if (t >= nw) continue;
+                            const unsigned mk = word(t);
+                            const int off = 16 * t + (d > 0 ? d : 0);
+                            if (mk != 0u && b1 == 0) {
+                                const int hb = 31 - __builtin_clz(mk);
+                                b1 = off + (hb >> 1) + 1;
+                                const unsigned mh = mk & ~(1u << hb);
+                                if (mh != 0u) b2 = off + ((31 - __builtin_clz(mh)) >> 1) + 1;
+                            } else if (mk != 0u && b2 == 0) {
+                                b2 = off + ((31 - __builtin_clz(mk)) >> 1) + 1;
+                            }
+                        }
+                        const int cc = a1 == La ? 0 : (a2 == La ? 1 : (b2 > a2 ? 3 : 2));
+                        dc[e] = min(cc, 3); df1[e] = a1; df2[e] = a2; dg1[e] = b1; dg2[e] = b2;
+                    }
+                    bool ok3 = s3;
+                    // (i) single diagonals
+#pragma unroll
+                    for (int e = 0; e < 11; ++e) {
+                        const int sh = e > 5 ? e - 5 : 5 - e;
+                        if (sh == 0) continue;
+                        ok3 = ok3 && m3 * sh + (m3 + x3) * dc[e] > D3;
+                    }
+                    // (ii) one gap, prefix on d1, suffix on d2 (|d| <= 3)
+#pragma unroll
+                    for (int e1 = 2; e1 <= 8; ++e1) {
+#pragma unroll
+                        for (int e2 = 2; e2 <= 8; ++e2) {
+                            if (e1 == e2) continue;
+                            const int d1 = e1 - 5, d2 = e2 - 5, g = d2 > d1 ? d2 - d1 : d1 - d2;
+                            // unpaired residues of the amplicon (= of the read): its leading / trailing overhang
+                            // and the gap's residues when the gap is in the read (the diagonal falls)
+                            const int U = (d1 < 0 ? -d1 : 0) + (d2 > 0 ? d2 : 0) + (d1 > d2 ? d1 - d2 : 0);
+                            const int slack = D3 - m3 * U - O3 - (g - 1) * a.gap_extend;   // (m + x) w must not exceed it
+                            if (slack < 0) continue;
+                            const int wmax = slack / (m3 + x3);
+                            const int gb = d2 > d1 ? d2 - d1 : 0;   // read bases in the gap
+                            bool exists = dg1[e2] - gb <= df1[e1];
+                            if (wmax >= 1) exists = exists || dg2[e2] - gb <= df1[e1] || dg1[e2] - gb <= df2[e1];
+                            if (wmax >= 2) exists = true;   // (not reached with the gate's parameters: reject)
+                            ok3 = ok3 && !exists;
+                        }
+                    }
+                    // (iii) jogs through d = +-1: a mismatch of that diagonal in [f + 1, l - 1] (read index)
+                    ok3 = ok3 && l - f >= 2 && jog_in[0] && jog_in[1];
+                    sub3 = __ballot(ok3);
+                }
                 if (a.known2) {   // a copy of the known sequence that no certificate above took
                     int k2 = 0;
 #pragma unroll
@@ -472,7 +596,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         const unsigned x = rw[t] ^ s_known[t];
                         k2 += __builtin_popcount((x | (x >> 1)) & vmask(t, La));
                     }
-                    known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2);
+                    known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2 | sub3);
                 }
             }
         }
@@ -805,7 +929,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         int32_t sinfo = 0, sinfo2 = 0;
         if constexpr (PK) {
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
-                !(((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull)) {
+                !(((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull)) {
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
@@ -872,7 +996,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             if (a.seed_info2 && r < r_end) a.seed_info2[r] = sinfo2;
         }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull)
+            a.sort_key[r] = (((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull)
                                 ? a.band_lb_cap + 2
                                 : (sinfo ? a.band_lb_cap + 3 +
                                                min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
@@ -907,9 +1031,9 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
-        if (a.ops && r < r_end && (((exact | sub1 | sub2) >> lane) & 1ull)) {
-            // substitutions (0, 1 or 2; a mismatch scores -4 / 5 maxsub)
-            const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull);
+        if (a.ops && r < r_end && (((exact | sub1 | sub2 | sub3) >> lane) & 1ull)) {
+            // substitutions (0 .. 3; a mismatch scores -4 / 5 maxsub)
+            const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull) + 3 * (int)((sub3 >> lane) & 1ull);
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
             a.nops[r] = 1;
             int4* st = (int4*)(a.stats + r);
@@ -948,7 +1072,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             // before any store (one read per round trip measured 2.7x the byte-input classify)
             constexpr int kWr = 8;
             unsigned long long dp =
-                __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | win | known | indel1) >> lane) & 1ull));
+                __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull));
             uint8_t* dst = const_cast<uint8_t*>(a.reads);
             while (dp) {
                 long long o[kWr], e[kWr];

@@ -129,3 +129,43 @@ def test_indel_reads_c2_mix_resident(gpu_aligner_factory):
     assert every_read(amp, buf, off, ob, threads=8)["mismatches"] == 0
     ob2 = a.align_ops(None, pr.offsets, resident=True)
     assert every_read(amp, buf, off, ob2, threads=8)["mismatches"] == 0
+
+
+def sub_reads(amp: str, n: int, seed: int, k: int = 3) -> list:
+    """Reads of the amplicon's length with k substitutions: uniform, clustered (adjacent or two apart),
+    near the ends, and one copying the neighbouring base (a shifted diagonal then matches locally)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    La = len(amp)
+    reads = []
+    for _ in range(n):
+        kind = int(rng.integers(0, 5))
+        if kind == 0:
+            pos = sorted(rng.choice(La, k, replace=False).tolist())
+        elif kind == 1:
+            p = int(rng.integers(0, La - 2 * k))
+            pos = [p + i * int(rng.integers(1, 3)) for i in range(k)]
+        elif kind == 2:
+            pos = sorted(rng.choice(list(range(4)) + list(range(La - 4, La)), k, replace=False).tolist())
+        else:
+            pos = sorted(rng.choice(La, k, replace=False).tolist())
+        r = list(amp)
+        for p in pos:
+            if kind == 4 and 0 < p < La - 1 and amp[p - 1] != amp[p]:
+                r[p] = amp[p - 1]   # copies its left neighbour
+            else:
+                r[p] = SUB[amp[p]] if rng.integers(0, 2) else {"A": "G", "C": "T", "G": "A", "T": "C"}[amp[p]]
+        reads.append("".join(r))
+    return reads
+
+
+@pytest.mark.parametrize("maker,seed", [("random", 21), ("repeat", 22), ("repeat", 23), ("reference", 24)])
+def test_three_substitution_reads(gpu_aligner_factory, maker, seed):
+    """Classify's three-substitution certificate: every read against the oracle, on random,
+    repeat-laced and the reference's own amplicon (jogs through a neighbouring diagonal and one-gap
+    alternatives are possible there), with 2- and 4-substitution reads mixed in."""
+    amp = {"random": synth.random_amplicon(250, seed), "repeat": repeat_amplicon(250, seed),
+           "reference": REF_AMPLICON}[maker]
+    reads = sub_reads(amp, 3000, seed) + sub_reads(amp, 500, seed + 1, 2) + sub_reads(amp, 500, seed + 2, 4)
+    _, _, _, _, counts = run_every_read(gpu_aligner_factory, amp, reads)
+    if maker == "random":   # most 3-substitution reads leave the DP
+        assert counts["exact_copies"] > 2500, counts
