@@ -203,6 +203,12 @@ __host__ __device__ inline int64_t band_region_stride(int La, int Lb_max, int W)
 // (byte | 0x20) folds case, the amplicon's folded dwords are 0 at non-ACGT bases.
 __device__ __forceinline__ unsigned ld_dw(const uint8_t* p) { return *(const unsigned*)p; }
 
+#ifndef NW_NO_SUB3
+#define NW_NO_SUB3 0   // A/B builds only (scripts/diag/build_variant.sh): classify without the 3-substitution certificate
+#endif
+#ifndef NW_NO_INDEL1
+#define NW_NO_INDEL1 0   // ... without the one-indel certificate
+#endif
 constexpr int kIndelMax = 10;   // classify's one-indel certificate: gaps of at most this many residues
 constexpr int kCand = NW_CAND; // exact-copy candidates compared together (2 dword loads each in flight)
 
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // alternative leaves a read or amplicon residue unpaired or mismatched), O > (k - 1) E (no alternative
     // with two internal gaps) and O + (k - 1) E < 4 m (no single diagonal pairing four residues fewer)
     int indel_kmax = 0;
-    if (PK && sub1_ok && a.amp2)
+    if (PK && !NW_NO_INDEL1 && sub1_ok && a.amp2)
         for (int k = 1; k <= kIndelMax; ++k) {
             const int p = (k - 1) * a.gap_extend;
             if (!(a.band_maxsub > p && a.gap_open > p && a.gap_open + p < 4 * a.band_maxsub)) break;
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     // (one gap leaving 4 or more residues unpaired, two gaps leaving 2, three gaps) and a jog through a
     // neighbouring diagonal (two gaps, one residue of each sequence unpaired) with one mismatch scores below D
     const int m3 = a.band_maxsub, x3 = 4 * sc5, O3 = a.gap_open, D3 = 3 * (m3 + x3);
-    const bool sub3_ok = sub2_ok && x3 < m3 && 4 * m3 + O3 > D3 && 2 * m3 + 2 * O3 > D3 && 3 * O3 > D3 &&
+    const bool sub3_ok = !NW_NO_SUB3 && sub2_ok && x3 < m3 && 4 * m3 + O3 > D3 && 2 * m3 + 2 * O3 > D3 && 3 * O3 > D3 &&
                          m3 + 2 * O3 + (m3 + x3) > D3;
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const unsigned tail_mask = (La & 3) ? (0xffffffffu >> (8 * (4 - (La & 3)))) : 0xffffffffu;
@@ -527,6 +533,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         };
 #pragma unroll
                         for (int t = 0; t < 16; ++t) {
+                            // (|d| >= 4: the score test needs one mismatch, no pair test reads the diagonal)
                             if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
                             const unsigned mk = word(t);
                             const int off = 16 * t + (d > 0 ? d : 0);   // read index of the word's base 0
@@ -812,27 +819,35 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
                     // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
                     // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
-                    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
-                    for (int sh = 0; sh <= kab + 3; ++sh) {
-                        const int P = min(Ls, Ll - sh);
-                        int f, g;
-                        ends(wl, ws, sh, P, &f, &g);
-                        const int c = cnt(f, g, P);
-                        o = o && mm * (P - c) - xx * c < S;
-                        if (sh <= kab) {
-                            if (sh == 0) f0 = f;
-                            if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
-                            if (sh == kab) gk = g;
-                            fmax_all = max(fmax_all, f);
-                            if (sh > 0) fmax_1 = max(fmax_1, f);
+                    // the shifts past kab and the other side's need only enough mismatches for the score test
+                    // (the smallest c with m (P - c) - x c < S, 0 .. 2; more: the DP): forward scans that stop
+                    // once that many are found
+                    auto enough = [&](auto lw, auto rw2, int sh, int P) -> bool {
+                        int need = 0;
+                        while (need <= 2 && !(mm * (P - need) - xx * need < S)) ++need;
+                        int c = 0;
+#pragma unroll
+                        for (int t = 0; t < 17; ++t) {
+                            if (__ballot(c < need && need <= 2 && 16 * t < P) == 0ull) break;
+                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                            c += c < need ? __builtin_popcount((z | (z >> 1)) & vmask(t, P)) : 0;
                         }
-                    }
-                    for (int sh = 1; sh <= 3; ++sh) {   // s shifted by sh against l: Ls - sh pairs
+                        return need <= 2 && c >= need;
+                    };
+                    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
+                    for (int sh = 0; sh <= kab; ++sh) {
                         int f, g;
-                        ends(ws, wl, sh, Ls - sh, &f, &g);
-                        const int c = cnt(f, g, Ls - sh);
-                        o = o && mm * (Ls - sh - c) - xx * c < S;
+                        ends(wl, ws, sh, Ls, &f, &g);
+                        const int c = cnt(f, g, Ls);
+                        o = o && mm * (Ls - c) - xx * c < S;
+                        if (sh == 0) f0 = f;
+                        if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
+                        if (sh == kab) gk = g;
+                        fmax_all = max(fmax_all, f);
+                        if (sh > 0) fmax_1 = max(fmax_1, f);
                     }
+                    for (int sh = kab + 1; sh <= kab + 3; ++sh) o = o && enough(wl, ws, sh, Ll - sh);
+                    for (int sh = 1; sh <= 3; ++sh) o = o && enough(ws, wl, sh, Ls - sh);   // s shifted against l
                     ok = ci && o && gk >= 1 && gk <= f0;
                 }
                 indel1 = __ballot(ok);
