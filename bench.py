@@ -72,7 +72,7 @@ READS_PER_GPU = 1_000_000
 # rocprofv3 --pmc summaries (scripts/gpu_pmc_call.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the guide's
 # gfx950 correction) of the TIMED CALL's kernels (every launch of warmup + steps calls, per call) and of the
 # quantification leg's kernels; each records the sha1 of the library it profiled (checked against the one loaded)
-PMC_DIR = os.path.join(ROOT, "profiles", "r05_pmc2")
+PMC_DIR = os.path.join(ROOT, "profiles", "r06_pmc")
 RESIDENT_PMC = os.path.join(PMC_DIR, "summary_resident.json")   # bench.py --kernel-only: the value's pass
 CALL_PMC = os.path.join(PMC_DIR, "summary_call.json")           # bench.py --skip-kernel-pass: call_pcie's calls
 QUANT_PMC = os.path.join(PMC_DIR, "summary_quant.json")
