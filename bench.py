@@ -1144,7 +1144,7 @@ def main():
                                         f"{ccp['lib_sha1']}, matches the loaded one: {ccp['lib_matches_loaded']})")
                                        if ccp else None,
                 "kernel": "the timed pass's kernels over the 1M resident reads: nw_band_classify<true> + "
-                          "nw_band_segsort + nw_band_fill<16, 0> (diagonal pass) + nw_band_fill<16, 1, true> + "
+                          "nw_band_segsort + nw_band_fill<16, true> + "
                           "nw_band_walk<16, true> (lane walk + stop summary) + redo compaction + nw_band_fill/walk<32> "
                           "+ nw_band_fill/walk<128> (wide level) + nw_align_kernel + nw_ops_compact, one launch each "
                           "(the kernels call_pcie runs per chunk of >= 65536 reads); call_achieved: the same bytes over "
@@ -1158,7 +1158,7 @@ def main():
                 "algo_bytes_per_launch": algo_bytes,
                 "algo_bytes_def": "sum over reads of read_len + 3*aln_len + 16 (SURVEY 8d)",
                 "valu": {
-                    "kernel": "nw_band_fill<16, *> (the largest phase: the diagonal pass and the traceback fill)",
+                    "kernel": "nw_band_fill<16, true> (the first level's traceback fill)",
                     "fill16_ms": fill_ms,
                     "valu_instructions_per_launch": fill_valu,
                     "valu_source": cp["source"] if cp else None,

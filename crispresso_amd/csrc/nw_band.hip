@@ -47,9 +47,6 @@
 //     [words / 4][lanes][4 words]: the fill writes 16 steps of a pair's lanes as one
 //     contiguous dwordx4 row, an M run of the walk reads 16 steps of its diagonal
 //     pair with one dwordx4 per lane;
-//   * ops output: a diagonal pass (nw_band_fill<W, 0>) first aligns the reads of
-//     the amplicon's length without traceback bits and finishes the single-diagonal
-//     ones in its epilogue; the rest join the traceback pass (nw_band_fill<W, 1>);
 //   * nw_band_walk: one wavefront per read: start cell from the W captures,
 //     certificate, the run-based walk of nw_common.h over the band, strings.
 #include <hip/hip_runtime.h>
@@ -1230,9 +1227,6 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
 // CRISPResso segment shares the amplicon's length), so a pair's band holds both reads.
 // Replaces a global counting sort (per-block histograms, two scans, scatter: four
 // launches of ~8 us each per chunk).  The last segment writes the DP count (*band_count).
-// With a.order_a (the diagonal pass, ops output): reads of the amplicon's length go to
-// their own list instead (order_a, *count_a; a second look-back): the reads of a
-// substitution-only variant, which nw_band_fill<W, 0> aligns without traceback bits.
 // ============================================================================
 constexpr int kSegReads = 4096, kSegThreads = 1024, kSegWaves = kSegThreads / 64;
 
@@ -1245,8 +1239,7 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
     const int NB = a.band_lb_cap + 3 + a.seed_keys, EX = a.band_lb_cap + 2;
     int* cnt = seg_sm;                  // [kSegWaves][NB]: per-wave counts, then prefix over waves
     int* kbase = seg_sm + kSegWaves * NB;   // [NB]: bucket totals, then their exclusive prefix
-    int* misc = kbase + NB;             // [0], [1] look-back results (lists B, A), [2] error, [16..31] wave sums
-    const int KA = a.order_a ? a.La : -1;   // the key of list A (none without the diagonal pass)
+    int* misc = kbase + NB;             // [0], [4] look-back results (band list, seeded list), [2] error, [16..31] wave sums
     const int KS = a.seed_list ? a.band_lb_cap + 3 : NB;   // keys >= KS: seeded reads (their own list)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int k = tid; k < kSegWaves * NB + NB; k += kSegThreads) seg_sm[k] = 0;
@@ -1282,8 +1275,7 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
             cnt[w * NB + k] = run;
             run += v;
         }
-        kbase[k] = (k == EX || k == KA) ? 0 : run;
-        if (k == KA) misc[3] = run;   // list A's reads in this segment
+        kbase[k] = k == EX ? 0 : run;
     }
     __syncthreads();
     // exclusive prefix of the key totals (thread t: keys [t * per, (t + 1) * per))
@@ -1317,25 +1309,20 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
     // the seeded list: an odd segment count gets its last entry twice (a pair of one read: the walks take
     // its first position), so every pair of that list lies within one segment's sorted run
     const int dpB = KS < NB ? kbase[KS] : dp, dpS0 = dp - dpB, dpS = dpS0 + (dpS0 & 1);
-    const int dpA = misc[3];
     if (wave == 0) {
         const unsigned base = lookback_excl(a.lb_status, blockIdx.x, epoch, (unsigned)dpB, &misc[2]);
         if (lane == 0) misc[0] = (int)base;
-    } else if (wave == 1 && KA >= 0) {   // list A: the look-back words after list B's
-        const unsigned base = lookback_excl(a.lb_status + gridDim.x + 1, blockIdx.x, epoch, (unsigned)dpA, &misc[2]);
-        if (lane == 0) misc[1] = (int)base;
-    } else if (wave == 2 && a.seed_list) {   // the seeded list: after list A's words
-        const unsigned base = lookback_excl(a.lb_status + 2 * (gridDim.x + 1), blockIdx.x, epoch, (unsigned)dpS, &misc[2]);
+    } else if (wave == 1 && a.seed_list) {   // the seeded list: the look-back words after the band list's
+        const unsigned base = lookback_excl(a.lb_status + gridDim.x + 1, blockIdx.x, epoch, (unsigned)dpS, &misc[2]);
         if (lane == 0) misc[4] = (int)base;
     }
     __syncthreads();
-    const long long base = misc[0], baseA = misc[1], baseS = misc[4];
+    const long long base = misc[0], baseS = misc[4];
     int32_t* order = const_cast<int32_t*>(a.band_order);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = key[i];
-        if (k == KA) a.order_a[baseA + cnt[wave * NB + k] + rank[i]] = (int32_t)(r0 + i);
-        else if (k >= KS) {
+        if (k >= KS) {
             const int q = (kbase[k] - dpB) + cnt[wave * NB + k] + rank[i];
             a.seed_list[baseS + q] = (int32_t)(r0 + i);
             if (q == dpS0 - 1 && dpS != dpS0) {   // the segment's odd count padded to a pair
@@ -1349,7 +1336,6 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
         if (misc[2]) a.fallback_count[3] = 1;   // look-back cut off: the call reports an error
         if (blockIdx.x == gridDim.x - 1) {
             *const_cast<int32_t*>(a.band_count) = (int32_t)(base + dpB);
-            if (KA >= 0) *a.count_a = (int32_t)(baseA + dpA);
             if (a.seed_list) *a.seed_count = (int32_t)(baseS + dpS);
         }
     }
@@ -1358,188 +1344,10 @@ __global__ __launch_bounds__(kSegThreads) void nw_band_segsort(const KernelArgs 
 // ============================================================================
 // Fill
 // ============================================================================
-// Epilogue of the diagonal pass (nw_band_fill<W, 0 / 2>): every lane of the wavefront
-// calls it (ballots).  Per read of the lane's pair: the start cell from the captures (the
-// last cell of each band diagonal lies on the last row or column; same keys and scan
-// order as nw_band_walk), the plain certificate (every alignment leaving the band scores
-// <= UB < S), and the single-diagonal test: the start cell's M equals the plain sum of
-// scores down its diagonal (captured beside M), so the traceback is that diagonal plus
-// the end gaps (nw_band_walk's fast path).  A read that passes gets its
-// record and runs here (identical / similar counts along the diagonal from the LDS
-// codes); any other read -- not certified, not diagonal, a code outside A C G T N, a byte
-// EDNAFULL does not score, more runs than a slot -- goes to tile_list, where the
-// traceback pass and the walk take it (and the refined certificate / the next level).
 // Overlap of diagonal d = j - i (pairs of the alignment that stays on it).
 __device__ __forceinline__ int diag_pairs(int La, int Lb, int d) { return d >= 0 ? min(La, Lb - d) : min(Lb, La + d); }
 
-template <int W>
-__device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const uint16_t* acd, const uint32_t* tab,
-                                   const unsigned char* pcd, int La, int dlo, int q, int grp, bool valid, bool act,
-                                   long long ra, long long rb, int LbA, int LbB, unsigned badA, unsigned badB,
-                                   unsigned padA, unsigned padB, unsigned nA, unsigned nB, bool amp_n,
-                                   unsigned cap0, unsigned cap1, unsigned capB0,
-                                   unsigned capB1, unsigned dc0, unsigned dc1, unsigned dcB0, unsigned dcB1,
-                                   unsigned bv0, unsigned bv1, int lane) {
-    using G = BandGeo<W>;
-    constexpr int L = G::L, PR = G::PR;
-    using LdsU = const __attribute__((address_space(3))) unsigned;
-    const int E = a.gap_extend;
-    const unsigned tabbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)tab;
-    bool fail[2] = {false, false};
-    bool use[2] = {valid, valid && rb != ra};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int Lb = h ? LbB : LbA;
-        const long long rd = h ? rb : ra;
-        // start cell: best key over the pair's W diagonals
-        unsigned key = 0u, eqbits = 0u;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int d = dlo + 2 * q + p;
-            const unsigned cm = p ? (h ? capB1 : cap1) : (h ? capB0 : cap0);
-            const unsigned cd = p ? (h ? dcB1 : dc1) : (h ? dcB0 : dc0);
-            const unsigned bv = p ? bv1 : bv0;
-            const int iend = La < Lb - d ? La : Lb - d;
-            const int ilo = 1 - d > 1 ? 1 - d : 1;
-            if (Lb > 0 && iend >= ilo) {
-                const int v = half(cm, h) - kBias16 - E * (2 * iend + d);
-                const int jend = iend + d;
-                const unsigned k = (iend == La && jend == Lb) ? end_key32(v, 3, 0)
-                                   : (jend == Lb ? end_key32(v, 2, iend - 1) : end_key32(v, 1, jend - 1));
-                key = k > key ? k : key;
-            }
-            // M of the diagonal's last cell == the diagonal's plain sum (both biased alike)
-            eqbits |= (unsigned)(((cm ^ add2(bv, cd)) >> (16 * h) & 0xffffu) == 0u) << p;
-        }
-#pragma unroll
-        for (int o = PR; o < 16; o <<= 1) {
-            const unsigned u = (unsigned)__shfl_xor((int)key, o, 64);
-            key = u > key ? u : key;
-        }
-        int score = 0, ei = 0, ej = 0;
-        decode_end(end_key_widen(key), La, Lb, &score, &ei, &ej);
-        const int dhi = dlo + W - 1;
-        int pmax = -1;
-        if (dhi < Lb - 1) pmax = max(pmax, min(Lb - dhi - 1, La));
-        if (dlo > 1 - La) pmax = max(pmax, min(Lb, La + dlo - 1));
-        bool certified = pmax < 0 || score > a.band_maxsub * pmax;
-        // the start diagonal's test bit, from the lane that owns it
-        const int ds = ej - ei - dlo;
-        const int src = (lane & ~15) | (((ds >> 1) & (L - 1)) * PR + (lane & 15) % PR);
-        const unsigned eqs = (unsigned)__shfl((int)eqbits, src, 64);
-        const bool diag = ((eqs >> (ds & 1)) & 1u) != 0u && ds >= 0 && ds < W;
-        const bool codes_ok = !(h ? (badB | padB) : (badA | padA));
-        // Refined certificate (nw_band_walk's band_single_diagonals_below): when
-        // S <= UB but S > UB - O, an alignment leaving the band with an internal gap scores
-        // below S; one without is a single diagonal beyond the band, summed here down its
-        // whole overlap from the LDS codes (the pair's lanes stride over it) for the diagonals
-        // with maxsub * P(d) >= S.  (The HDR pass: 10 clustered mismatches against the HDR
-        // amplicon leave S below the plain bound of 16 diagonals.)  Control flow stays
-        // uniform over the wavefront: the diagonal counts are wave maxima, the sums reduced
-        // over every lane.
-        {
-            const bool need = use[h] && act && Lb > 0 && !certified && diag && codes_ok &&
-                              score > a.band_maxsub * pmax - a.gap_open;
-            int kn[2] = {0, 0};
-            if (need)
-                for (int side = 0; side < 2; ++side)
-                    for (int k = 1;; ++k) {
-                        const int P = diag_pairs(La, Lb, side == 0 ? dhi + k : dlo - k);
-                        if (P <= 0 || a.band_maxsub * P < score) break;
-                        kn[side] = k;
-                    }
-            bool beaten = false;
-#pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const int km = (int)wave_max_u32((unsigned)kn[side]);
-                for (int k = 1; k <= km; ++k) {
-                    const int d = side == 0 ? dhi + k : dlo - k;
-                    const bool on = k <= kn[side];
-                    const int P = on ? diag_pairs(La, Lb, d) : 0;
-                    const int i0 = d >= 0 ? 1 : 1 - d, j0 = d >= 0 ? 1 + d : 1;   // first cell, 1-based
-                    int sum = 0;
-                    for (int t = q; t < P; t += L)
-                        sum += half(*(LdsU*)(uintptr_t)(acd[kAPad + i0 + t] + pcd[kJPad + j0 + t]), h) - 2 * E;
-#pragma unroll
-                    for (int o = PR; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
-                    beaten = beaten || (on && sum >= score);
-                }
-            }
-            if (need && !beaten) certified = true;
-        }
-        const int nd = ei < ej ? ei : ej;
-        const bool endg = (ei == La && ej < Lb) || (ej == Lb && ei < La);
-        const int lead = (ei > ej ? ei : ej) - nd;
-        const int nruns = 1 + (int)endg + (lead > 0);
-        const bool ok = use[h] && act && Lb > 0 && certified && diag && codes_ok && nruns <= a.ops_slot;
-        fail[h] = use[h] && !ok;
-        // identical / similar columns down the diagonal.  Without N in the amplicon or the read
-        // every pair is A C G T against A C G T: identical scores maxsub, any other -4/5 of it,
-        // so the diagonal's plain sum (captured beside M by the lane owning the start diagonal)
-        // gives the identities, and the similar pairs are the identical ones.  Otherwise the
-        // pair's L lanes stride down the diagonal.
-        const unsigned dsel0 = __shfl((int)(h ? dcB0 : dc0), src, 64), dsel1 = __shfl((int)(h ? dcB1 : dc1), src, 64);
-        int fast_id = -1;
-        if (ok && !amp_n && !(h ? nB : nA)) {
-            const int sc5 = a.band_maxsub / 5;
-            const int sum = half((ds & 1) ? dsel1 : dsel0, h) - 2 * E * nd;   // plain scores down the diagonal
-            const int num = sum + 4 * sc5 * nd;
-            if (a.band_maxsub == 5 * sc5 && num >= 0 && num % (9 * sc5) == 0 && num / (9 * sc5) <= nd)
-                fast_id = num / (9 * sc5);
-        }
-        unsigned cnt = 0u;
-        if (ok && fast_id < 0) {
-            for (int t = q; t < nd; t += L) {
-                const int i = ei - t, j = ej - t;   // 1-based cell
-                const unsigned ab = acd[kAPad + i];
-                const unsigned pc = pcd[kJPad + j];
-                const int x = (int)((ab - tabbase) / 144u);   // amplicon EDNAFULL code (row of the table)
-                const int y = (int)(h ? (pc >> 2) % 6u : (pc >> 2) / 6u);   // read: A T G C N pad
-                const int s = half(*(LdsU*)(uintptr_t)(ab + pc), h) - 2 * E;
-                const int ycode = y == 0 ? 0 : y == 1 ? 1 : y == 2 ? 2 : y == 3 ? 3 : 14;
-                const bool id = y < 5 && x == ycode;
-                cnt += (unsigned)id | ((unsigned)(id || s > 0) << 16);
-            }
-        }
-#pragma unroll
-        for (int o = PR; o < 16; o <<= 1) cnt += (unsigned)__shfl_xor((int)cnt, o, 64);
-        if (ok && q == 0) {
-            const int endlen = endg ? (ei == La ? Lb - ej : La - ei) : 0;
-            uint32_t* slot = a.ops + rd;
-            const long long sst = a.ops_stride;
-            int w = 0;
-            if (lead > 0) slot[sst * w++] = ((unsigned)(ei > nd ? RUN_Y : RUN_X) << 28) | (unsigned)lead;
-            slot[sst * w++] = ((unsigned)RUN_M << 28) | (unsigned)nd;
-            if (endg) slot[sst * w++] = ((unsigned)(ei == La ? RUN_X : RUN_Y) << 28) | (unsigned)endlen;
-            a.nops[rd] = w;
-            Stat r;
-            r.aln_len = nd + endlen + lead;
-            r.n_ident = fast_id >= 0 ? fast_id : (int)(cnt & 0xffffu);
-            r.n_sim = fast_id >= 0 ? fast_id : (int)(cnt >> 16);
-            r.n_gaps = endlen + lead;
-            r.score = score;
-            r.end_i = ei;
-            r.end_j = ej;
-            r.flags = 0;
-            a.stats[rd] = r;
-        }
-    }
-    // the reads handed on: one atomic per wavefront
-    const unsigned long long m0 = __ballot(q == 0 && fail[0]), m1 = __ballot(q == 0 && fail[1]);
-    const int n0 = (int)__builtin_popcountll(m0), tot = n0 + (int)__builtin_popcountll(m1);
-    if (tot) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(a.tile_count, tot);
-        base = __builtin_amdgcn_readfirstlane(base);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        if (q == 0 && fail[0]) a.tile_list[base + __builtin_popcountll(m0 & below)] = (int32_t)ra;
-        if (q == 0 && fail[1]) a.tile_list[base + n0 + __builtin_popcountll(m1 & below)] = (int32_t)rb;
-    }
-}
-
-// Virtual DP list of the traceback pass: band_order[0, *band_count) then (diagonal pass
-// on, separate launches) tile_list[0, *tile_count) -- the list-A reads the diagonal pass
-// handed on.
+// DP list of the traceback pass: band_order[0, *band_count).
 // The wide level (a.band_from_work) reads the exact kernel's work list instead: the reads the
 // narrower levels gave up on, then (direct hand-off) the first level's redo list; there
 // a.band_count = a.work_count.
@@ -1547,16 +1355,16 @@ __device__ __forceinline__ void band_diag_epilogue(const KernelArgs& a, const ui
 // their hits' diagonals, so a pair's two reads share a band).
 // The 32-diagonal level with the seeded list (KernelArgs::seed_l2 == 1): its own list (the redo
 // list, none when the direct hand-off gave it to the wide level; as the only level, the sorted DP
-// list and the diagonal pass's hand-ons), then, from the next even position, the seeded list -- an
+// list), then, from the next even position, the seeded list -- an
 // odd count before it leaves one hole (read by no walk), so no pair mixes a seeded read with another.
 __device__ __forceinline__ long long l2_redo_n(const KernelArgs& a) {
-    return redo_direct_taken(a) ? 0ll : (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
+    return redo_direct_taken(a) ? 0ll : (long long)*a.band_count;
 }
 __device__ __forceinline__ long long l2_seed0(const KernelArgs& a) { return (l2_redo_n(a) + 1) & ~1ll; }
 __device__ __forceinline__ long long band_list_count(const KernelArgs& a) {
     if (a.band_from_work) return exact_work_count(a) + (a.seed_list ? (long long)*a.seed_count : 0ll);
     if (a.seed_l2 == 1) return l2_seed0(a) + (long long)*a.seed_count;
-    return (long long)*a.band_count + (a.tile_count ? (long long)*a.tile_count : 0ll);
+    return (long long)*a.band_count;
 }
 __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long long k, long long nb) {
     if (a.band_from_work) {
@@ -1569,17 +1377,14 @@ __device__ __forceinline__ long long band_list_read(const KernelArgs& a, long lo
         if (k >= s0) return (long long)a.seed_list[k - s0];
         if (k >= nr) --k;   // the hole: its pair's read A again (the pair holds one read)
     }
-    return k < nb ? (long long)a.band_order[k] : (long long)a.tile_list[k - nb];
+    return (long long)a.band_order[k];
 }
 
-// TB = true: the traceback pass (bits into the pair's region, the walk follows).
-// TB = false: the diagonal pass over list A (ops output only): no traceback bits at all
-// (9 VALU per lane-step instead of 17), the pure-diagonal score of every band diagonal
-// accumulated beside M; the epilogue takes the start cell, the certificate and the
-// single-diagonal test (start cell's M == its diagonal's plain sum: the traceback is the
-// diagonal, nw_band_walk's fast path) and writes the record and runs of every read that
-// passes; the others go to tile_list for the traceback pass.
-template <int W, int MODE, bool SUMM = false>   // SUMM: the traceback fill also writes the stop summary (lane walk)
+// The traceback fill: a level's band list, its traceback bits into each pair's region (the walk
+// follows).  (Round 6 removed the diagonal pass, a score-only fill over the reads of the
+// amplicon's length ahead of this one: with the classify certificates taking nearly all of them,
+// its sweep only lengthened the chain -- resident pass 0.536 -> 0.484 ms without it)
+template <int W, bool SUMM = false>   // SUMM: the traceback fill also writes the stop summary (lane walk)
 #define NW_FILL_WPE 6   // 5: no spills in the traceback fill but slower
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE))) void nw_band_fill(const KernelArgs a) {
     using G = BandGeo<W>;
@@ -1605,16 +1410,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     unsigned* stage = (unsigned*)(lut6 + 256) + wave * 256 + 4 * lane;
     for (int k = tid; k < kTabRows * 36; k += blockDim.x) tab[k] = a.band_tab[k];
     for (int k = tid; k < 256; k += blockDim.x) lut6[k] = a.lut6[k];
-    int has_n = 0;
     for (int k = tid; k < band_acd_elems(La); k += blockDim.x) {
         const int i = k - kAPad;   // row i = amplicon residue i - 1
         // the amplicon's EDNAFULL code (IUPAC codes included: their row of the table), pad outside
         const int c = (i >= 1 && i <= La) ? a.lut[a.amp[i - 1]] : NCODE_PAD;
         // the score table's LDS address is folded in: a0 + j0 is the entry's LDS address
         acd[k] = (uint16_t)(c * 36 * 4 + (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)tab);
-        has_n = has_n || c == 14;
     }
-    const bool amp_n = __syncthreads_or(has_n) != 0;   // the amplicon has N (the identity count's shortcut is off)
+    __syncthreads();
 
     // byte-plane masks of the sign bits (SGPRs: v_and_or_b32 takes no literal)
     unsigned mT[4], mU[4];
@@ -1627,23 +1430,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     asm volatile("s_mov_b32 %0, 0x40404040" : "=s"(mU[2]));
     asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(mU[3]));
 
-    // list A (the diagonal pass, MODE 0) or the band list (the traceback fill, MODE 1): wave
-    // work items of kBPW pairs each
+    // the band list: wave work items of kBPW pairs each
     const int NW = a.band_words;
-    const long long cntA = MODE != 1 ? (long long)*a.count_a : 0ll;
-    const long long pA = (cntA + 1) / 2;
-    const long long nA = (pA + kBPW - 1) / kBPW;
-    const long long nbB = MODE != 0 ? (long long)*a.band_count : 0ll;
-    const long long cntB = MODE != 0 ? band_list_count(a) : 0ll;
-    const long long pB = MODE != 0 ? min(a.band_pair_hi, (cntB + 1) / 2) : 0ll;
-    const long long npB = pB - (MODE != 0 ? a.band_pair_lo : 0ll);
+    const long long nb = (long long)*a.band_count;
+    const long long count = band_list_count(a);
+    const long long pair_lo = a.band_pair_lo;
+    const long long pair_hi = min(a.band_pair_hi, (count + 1) / 2);
+    const long long npB = pair_hi - pair_lo;
     const long long nB = npB > 0 ? (npB + kBPW - 1) / kBPW : 0ll;
-    auto body = [&](auto TBc, long long wv) __attribute__((always_inline)) {
-        constexpr bool TB = decltype(TBc)::value;
-        const long long pair_lo = TB ? a.band_pair_lo : 0ll;
-        const long long pair_hi = TB ? pB : pA;
-        const long long count = TB ? cntB : cntA;
-        const long long nb = nbB;
+    auto body = [&](long long wv) __attribute__((always_inline)) {
         const long long g = pair_lo + wv * kBPW + grp;
         int dlo = 0;
         bool act = false;
@@ -1651,19 +1446,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         int LbA = 0, LbB = 0;
         bool seeded = false;
         if (g < pair_hi) {
-            if constexpr (TB) {
-                ra = band_list_read(a, 2 * g, nb);
-                rb = (2 * g + 1 < count) ? band_list_read(a, 2 * g + 1, nb) : ra;
-            } else {
-                ra = a.order_a[2 * g];
-                rb = (2 * g + 1 < count) ? a.order_a[2 * g + 1] : ra;
-            }
+            ra = band_list_read(a, 2 * g, nb);
+            rb = (2 * g + 1 < count) ? band_list_read(a, 2 * g + 1, nb) : ra;
             offA = a.offsets[ra];
             offB = a.offsets[rb];
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
             act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo, W);
-            if constexpr (TB && W >= kBandDiags) {
+            if constexpr (W >= kBandDiags) {
                 // seeded reads (both of the pair): the band centred on their hits' diagonals
                 if (a.seed_info) {
                     const int32_t sa = a.seed_info[ra], sb = a.seed_info[rb];
@@ -1694,7 +1484,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         const int Lw = (int)wave_max_u32((unsigned)Lmax);
         unsigned bad_mask = 0u;   // bit p: pair p has a read A / B code outside A C G T N (bits 0-15 / 16-31)
         unsigned pad_mask = 0u;   // the same for bytes EDNAFULL does not score ('-', '*', ...: the walk's gap columns)
-        unsigned n_mask = 0u;     // the same for N (the diagonal pass's identity count)
+        unsigned n_mask = 0u;     // the same for N
         constexpr int kSub = kBPW < 4 ? kBPW : 4;   // pairs staged together (loads in flight)
         for (int c0 = 0; c0 < Lw; c0 += 256)
         for (int p0 = 0; p0 < kBPW; p0 += kSub) {
@@ -1771,15 +1561,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         const int tau_end = (int)wave_max_u32(thi);
         const int tau_pro = (int)wave_max_u32(tpro);
         lds_fence();
-        unsigned char* region = TB ? a.band_region + (g - pair_lo) * a.band_stride : nullptr;
-        if (TB && q == 0 && g < pair_hi) {
+        unsigned char* region = a.band_region + (g - pair_lo) * a.band_stride;
+        if (q == 0 && g < pair_hi) {
             // everything the walk needs to find the pair's reads: one 48-byte load
             int4* hp = (int4*)region;
             hp[0] = make_int4(tau0, dlo, flags | (act ? 0 : kPairInactive) | (seeded ? REGION_SEEDED : 0), 0);
             hp[1] = make_int4((int)ra, (int)rb, (int)(a.offsets[ra + 1] - offA), (int)(a.offsets[rb + 1] - offB));
             hp[2] = make_int4((int)(unsigned)offA, (int)(offA >> 32), (int)(unsigned)offB, (int)(offB >> 32));
         }
-        if (tau_end == 0 && TB) return;   // no active group in this wavefront
+        if (tau_end == 0) return;   // no active group in this wavefront
 
         const int d0 = dlo + 2 * q;
         int tb[2], te[2], teB[2];
@@ -1800,12 +1590,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         // or column; blocks before it skip the capture selects
         const int te_lo = (int)wave_min_u32(min(min((unsigned)te[0], (unsigned)te[1]),
                                                 min((unsigned)teB[0], (unsigned)teB[1])));
-        unsigned* bits = TB ? (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q : nullptr;   // this lane's slot of each tile
+        unsigned* bits = (unsigned*)(region + kHdrBytes + kCapBytes) + 4 * q;   // this lane's slot of each tile
         // the stop summary (band_summ): the OR of a 16-word block's words (accumulated in LDS at each
         // row's store, next to the row's stage), one byte per block, gathered in LDS 16 blocks at a
         // time and stored as one 16-byte line piece per lane (byte stores spread over the pass had
         // cost +0.12 GB of partial-line writes)
-        constexpr bool summ_on = TB && SUMM;
+        constexpr bool summ_on = SUMM;
         unsigned* sum_lds = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 320 + lane;   // the block's OR
         unsigned* sum_chunk = (unsigned*)(lut6 + 256) + wpb * 256 + wave * 320 + 64 + 4 * lane;   // 16 blocks' bytes
         if (summ_on) {
@@ -1824,8 +1614,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
 
         unsigned Hp0 = pk(kBias16, kBias16), Hp1 = Hp0, MoP = NEG2, XP = NEG2, YP = NEG2;
         unsigned cap0 = NEG2, cap1 = NEG2, capB0 = NEG2, capB1 = NEG2;   // read A's (low) / B's (high half)
-        // diagonal pass: plain sums of the scores (+2E each) down each diagonal, and their captures
-        unsigned ds0 = 0u, ds1 = 0u, dc0 = 0u, dc1 = 0u, dcB0 = 0u, dcB1 = 0u;
         // LDS code cursors of the block starting at tau4: rows i0, i0 + 1; columns j0 .. j0 + 2
         auto ibase = [&](int tau4) { return (tau4 - kBK) / 2 - q; };
         const uint16_t* ap = acd + kAPad + ibase(tau0);
@@ -1854,32 +1642,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                 // up = own diagonal d0 + 1 one step back; left = lane q-1's d0 - 1
                 const unsigned Ml = G::shr(MoP), Xl = G::shr(XP);
                 X = max2(Ml, Xl);
-                if constexpr (TB) d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
+                d2 = sub2(Xl, Ml);     // sign: X opens (open > extend)
                 Y = max2(MoP, YP);
-                if constexpr (TB) d1 = sub2(YP, MoP);    // sign: Y opens
+                d1 = sub2(YP, MoP);    // sign: Y opens
             } else {
                 // up = lane q+1's d0 one step back; left = own diagonal d0
                 const unsigned Mu = G::shl(MoP), Yu = G::shl(YP);
                 Y = max2(Mu, Yu);
-                if constexpr (TB) d1 = sub2(Yu, Mu);
+                d1 = sub2(Yu, Mu);
                 X = max2(MoP, XP);
-                if constexpr (TB) d2 = sub2(XP, MoP);
+                d2 = sub2(XP, MoP);
             }
             unsigned M = add2(P ? Hp1 : Hp0, scr[U]);
             const unsigned mxy = max2(X, Y);
             unsigned H = max2(M, mxy);
-            if constexpr (!TB) {
-                if constexpr (P == 0) ds0 = add2(ds0, scr[U]); else ds1 = add2(ds1, scr[U]);
-            }
             if constexpr (PRO) {
                 if (tau == tb[P]) {   // DP boundary cell (row 0 / column 0): M = 0, X = Y = -inf
                     M = bval[P];
                     H = M;
                     X = NEG2;
                     Y = NEG2;
-                    if constexpr (!TB) {
-                        if constexpr (P == 0) ds0 = 0u; else ds1 = 0u;
-                    }
                 }
             }
             if constexpr (P == 0) Hp0 = H; else Hp1 = H;
@@ -1890,27 +1672,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                 if constexpr (P == 0) {
                     cap0 = tau == te[0] ? M : cap0;
                     capB0 = tau == teB[0] ? M : capB0;
-                    if constexpr (!TB) {
-                        dc0 = tau == te[0] ? ds0 : dc0;
-                        dcB0 = tau == teB[0] ? ds0 : dcB0;
-                    }
                 } else {
                     cap1 = tau == te[1] ? M : cap1;
                     capB1 = tau == teB[1] ? M : capB1;
-                    if constexpr (!TB) {
-                        dc1 = tau == te[1] ? ds1 : dc1;
-                        dcB1 = tau == teB[1] ? ds1 : dcB1;
-                    }
                 }
             }
-            if constexpr (TB) {
-                const unsigned d3 = sub2(X, Y);     // sign: Y > X (X wins an X == Y tie)
-                const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
-                const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
-                const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
-                acc = and_or(tt, mT[U], acc);
-                acc = and_or(uu, mU[U], acc);
-            }
+            const unsigned d3 = sub2(X, Y);     // sign: Y > X (X wins an X == Y tie)
+            const unsigned d4 = sub2(M, mxy);   // sign: M < max(X, Y)
+            const unsigned tt = __builtin_amdgcn_perm(d2, d1, 0x0B0A0908u);
+            const unsigned uu = __builtin_amdgcn_perm(d4, d3, 0x0B0A0908u);
+            acc = and_or(tt, mT[U], acc);
+            acc = and_or(uu, mU[U], acc);
         };
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
@@ -1931,29 +1703,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
         // a block pair (8 steps) is half a tile row; its words wait in LDS and the
         // second half stores the row (the phases may split a row: the stage carries it)
         auto flush = [&](int tau4) {
-            if constexpr (TB) {
-                asm volatile("" ::: "memory");
-                const int w = ((tau4 - tau0) >> 2) & ~3;
-                const uint4 row = *(const uint4*)stage;
-                if (act && w < NW) *(uint4*)(bits + w * kBL) = row;
-                if (summ_on) {
-                    const unsigned x = *sum_lds | row.x | row.y | row.z | row.w;
-                    const bool last = ((w >> 2) & 3) == 3;   // the block's fourth row: its summary byte
-                    if (last && act && (w >> 4) <= ((NW - 1) >> 4)) summ_put(w >> 4, x);   // a block with stored words
-                    *sum_lds = last ? 0u : x;
-                }
+            asm volatile("" ::: "memory");
+            const int w = ((tau4 - tau0) >> 2) & ~3;
+            const uint4 row = *(const uint4*)stage;
+            if (act && w < NW) *(uint4*)(bits + w * kBL) = row;
+            if (summ_on) {
+                const unsigned x = *sum_lds | row.x | row.y | row.z | row.w;
+                const bool last = ((w >> 2) & 3) == 3;   // the block's fourth row: its summary byte
+                if (last && act && (w >> 4) <= ((NW - 1) >> 4)) summ_put(w >> 4, x);   // a block with stored words
+                *sum_lds = last ? 0u : x;
             }
         };
         auto pair8 = [&](int tau4, auto PROc, auto CAPc) {
-            if constexpr (TB) {
-                const int h2 = ((tau4 - tau0) >> 2) & 2;
-                stage[h2] = block(tau4, PROc, CAPc, sc, sn);
-                stage[h2 + 1] = block(tau4 + 4, PROc, CAPc, sn, sc);
-                if (h2) flush(tau4);
-            } else {
-                (void)block(tau4, PROc, CAPc, sc, sn);
-                (void)block(tau4 + 4, PROc, CAPc, sn, sc);
-            }
+            const int h2 = ((tau4 - tau0) >> 2) & 2;
+            stage[h2] = block(tau4, PROc, CAPc, sc, sn);
+            stage[h2 + 1] = block(tau4 + 4, PROc, CAPc, sn, sc);
+            if (h2) flush(tau4);
         };
         // phases in whole block pairs (8 steps) from tau0: prologue (boundary cells,
         // captures of short reads), bulk, capture window to tau_end (may run up to 7
@@ -1983,25 +1748,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
                 if (open || (bl & 15) != 15) summ_flush(bl);
             }
         }
-
-        if constexpr (!TB) {
-            band_diag_epilogue<W>(a, acd, tab, pcd, La, dlo, q, grp, g < pair_hi, act, ra, rb, LbA, LbB,
-                                  (bad_mask >> grp) & 1u, (bad_mask >> (16 + grp)) & 1u, (pad_mask >> grp) & 1u,
-                                  (pad_mask >> (16 + grp)) & 1u, (n_mask >> grp) & 1u, (n_mask >> (16 + grp)) & 1u,
-                                  amp_n, cap0, cap1, capB0, capB1, dc0, dc1, dcB0, dcB1,
-                                  bval[0], bval[1], lane);
-            return;
-        }
         if (act) {
             unsigned* caps = (unsigned*)(region + kHdrBytes);
             caps[2 * q] = (cap0 & 0xffffu) | (capB0 & 0xffff0000u);
             caps[2 * q + 1] = (cap1 & 0xffffu) | (capB1 & 0xffff0000u);
         }
     };
-    for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nA + nB; wv += (long long)gridDim.x * wpb) {
-        if constexpr (MODE == 0) body(std::false_type{}, wv);
-        else body(std::true_type{}, wv);
-    }
+    for (long long wv = (long long)blockIdx.x * wpb + wave; wv < nB; wv += (long long)gridDim.x * wpb) body(wv);
 }
 
 // ============================================================================
@@ -3184,8 +2937,8 @@ hipError_t band_occupancy(int W, int fill_wpb, int walk_wpb, int fill_lds, int w
                           int* walk_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
         fill_blocks,
-        W == 16 ? (const void*)nw_band_fill<16, 1>
-                : (W == 32 ? (const void*)nw_band_fill<32, 1> : (const void*)nw_band_fill<kWideDiags, 1>),
+        W == 16 ? (const void*)nw_band_fill<16>
+                : (W == 32 ? (const void*)nw_band_fill<32> : (const void*)nw_band_fill<kWideDiags>),
         64 * fill_wpb, fill_lds);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -3212,11 +2965,11 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) 
     return hipGetLastError();
 }
 // words of the single-pass scans over n reads: the largest of the segment sort's two lists
-// (list A after list B's ceil(n / kSegReads) + 1 words), the redo and ops compactions
-// (1024-read blocks)
+// (the seeded list after the band list's ceil(n / kSegReads) + 1 words), the redo and ops
+// compactions (1024-read blocks)
 int64_t band_lookback_words(int64_t n) {
     const int64_t seg = std::max<int64_t>(1, (n + kSegReads - 1) / kSegReads);
-    return std::max<int64_t>(std::max<int64_t>(1, (n + 1023) / 1024) + 1, 3 * seg + 3);   // lists B, A, seeded
+    return std::max<int64_t>(std::max<int64_t>(1, (n + 1023) / 1024) + 1, 2 * seg + 2);   // band list, seeded list
 }
 
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
@@ -3225,13 +2978,13 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
     KernelArgs al = a;
     al.band_summ = W == 16 && a.ops && a.band_summ;
     if (al.band_summ)
-        hipLaunchKernelGGL((nw_band_fill<16, 1, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, al);
+        hipLaunchKernelGGL((nw_band_fill<16, true>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, al);
     else if (W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<16>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else if (W == 32)
-        hipLaunchKernelGGL((nw_band_fill<32, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<32>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     else
-        hipLaunchKernelGGL((nw_band_fill<kWideDiags, 1>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
+        hipLaunchKernelGGL((nw_band_fill<kWideDiags>), dim3(fill.grid), dim3(64 * fill.wpb), fill.lds_bytes, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (after_fill && (e = hipEventRecord(after_fill, s)) != hipSuccess) return e;
@@ -3243,22 +2996,6 @@ hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const 
         hipLaunchKernelGGL(nw_band_walk<32>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
     else
         hipLaunchKernelGGL(nw_band_walk<kWideDiags>, dim3(walk.grid), dim3(64 * walk.wpb), walk.lds_bytes, s, a);
-    return hipGetLastError();
-}
-
-// the diagonal pass over list A (KernelArgs::order_a): one launch, as many blocks as the
-// traceback fill of the same level would use for its pairs
-hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s) {
-    const int ppw = W == 16 ? BandGeo<16>::PW : BandGeo<32>::PW;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(((pairs + ppw - 1) / ppw + fill.wpb - 1) / fill.wpb,
-                                                                  (int64_t)fill.grid));
-    KernelArgs d = a;   // every pair of list A in one launch (no traceback region to bound the pass)
-    d.band_pair_lo = 0;
-    d.band_pair_hi = pairs;
-    if (W == 16)
-        hipLaunchKernelGGL((nw_band_fill<16, 0>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
-    else
-        hipLaunchKernelGGL((nw_band_fill<32, 0>), dim3(grid), dim3(64 * fill.wpb), fill.lds_bytes, s, d);
     return hipGetLastError();
 }
 

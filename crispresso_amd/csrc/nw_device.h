@@ -69,16 +69,6 @@ struct KernelArgs {
     int32_t* redo_list;            // reads a narrow first band could not certify (next level's band_order)
     int32_t* redo_count;
     uint8_t* redo_flags;           // [n] per sorted position: handed to the next level (compacted in order)
-    // the diagonal pass (nw_band_fill<W, false>, ops output): the sort puts the reads of the
-    // amplicon's length in order_a[0, *count_a); the pass hands the reads it does not finish
-    // to tile_list[0, *tile_count), which the traceback pass takes after band_order's
-    int32_t* order_a;              // null: no diagonal pass (every DP read in band_order)
-    int32_t* count_a;
-    int32_t* tile_list;
-    int32_t* tile_count;           // null outside the first level's traceback pass
-    // 1: the merged first-level fill (nw_band_fill<W, 2>: diagonal pass over list A and the
-    // traceback fill over band_order in one launch): the reads the diagonal pass hands on go
-    // to the next level's redo list (first), not to this level's traceback pass
     // > 0: when the first level hands on at most this many reads (*redo_count), the second
     // level's kernels return at once and the exact kernel takes them too (its fallback list,
     // then the redo list): a few hundred reads cost the exact kernel's latency once, less
@@ -230,8 +220,6 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s);
 int64_t band_lookback_words(int64_t n);
 hipError_t launch_band(int W, const KernelArgs& a, const LaunchCfg& fill, const LaunchCfg& walk, hipStream_t s,
                        hipEvent_t after_fill);
-// the diagonal pass (nw_band_fill<W, false>) over list A; `pairs`: an upper bound of its pairs
-hipError_t launch_band_diag(int W, const KernelArgs& a, const LaunchCfg& fill, int64_t pairs, hipStream_t s);
 // 2-bit packed bases [b0, b1) (batch positions; device copy of the stream from byte
 // pbyte0, 4-aligned) -> dst[pos - bias] bytes (A C T G), then exceptions [e0, e1)
 // With `lens`: the same launch also rebuilds the chunk's offsets d_off[r_lo .. r_hi]
@@ -269,25 +257,22 @@ hipError_t launch_exact(const KernelArgs& a, int grid, int lds_bytes, bool tb_ld
 // this chunk's total, [3] errors (1: staging full, 2: spill area full, from opsctl[1], 4: a
 // look-back cut off); running over the call: [4] exact-kernel reads, [5] second band level
 // reads of two-level chunks, [6] reads that needed the DP, [7] DP reads of chunks run on the
-// second level alone, [8] reads of the diagonal passes' lists A, [9] the reads those passes
-// handed to the traceback pass, [10] reads that reached the exact kernel (after the wide level) (OpsCounts: the device counters of the chunk's kernels);
+// second level alone, [8] reads that reached the exact kernel (after the wide level) (OpsCounts:
+// the device counters of the chunk's kernels);
 // [kOpsCtl], [kOpsCtl + 1]: the running base, read from [kOpsCtl + parity] and written to
 // the other (chunk k: parity k & 1).
 // status: band_lookback_words(n) look-back words; epoch: new per launch.  opsctl: the
 // kernels' flags.  hctl: pinned host copy of ctl[0 .. kOpsCtl) written by the launch (or null).
 constexpr int kOpsBlockReads = 1024;
-constexpr int kOpsCtl = 11;
+constexpr int kOpsCtl = 9;
 constexpr int kOpsCtlAll = kOpsCtl + 2;
 struct OpsCounts {
     const int32_t* fallback;   // [0]: exact-kernel reads of the chunk, [3]: look-back error flag
     const int32_t* redo;       // second band level reads (null: one level)
     const int32_t* band;       // reads that needed the DP (null: not the band path)
-    const int32_t* band_a;     // + the diagonal pass's list A (null: none)
     int32_t direct;            // KernelArgs::redo_direct of the chunk (0: off)
     int32_t one_level;         // the chunk ran the 32-diagonal level alone: its DP reads go to ctl[7]
     int32_t prio;              // raise the compaction's issue priority (KernelArgs::tail_prio)
-    const int32_t* list_a;     // the diagonal pass's list A (null: no diagonal pass)
-    const int32_t* handed;     // ... and the reads it handed on
     const int32_t* exact;      // the wide level's give-ups: the exact kernel's reads (null: no wide level)
     const int32_t* seeded;     // the seeded reads (to the wide level, or the second level first; null: none)
     const int32_t* seeded_l2;  // of those, the ones the 32-diagonal level left to the wide level (null: it took none)

@@ -58,7 +58,6 @@ struct Profile {
     const uint32_t* rowpos = nullptr;  // band walk: codes each row scores > 0 against
     const uint8_t* amp = nullptr;      // amplicon bytes (+16 pad)
     int R = 0;
-    bool amp_plain = false;            // every amplicon byte is an EDNAFULL letter (the diagonal pass's codes)
     // window seeds (classify, packed input): the amplicon 2 bits per base (the reads' packing) and
     // its A C G T 16-mers sorted by (key, position); null for amplicons over 1024 bp
     const uint32_t* amp2 = nullptr;
@@ -87,22 +86,20 @@ struct Scratch {
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
     DevBuf<int32_t> d_order, d_sort_key;
-    DevBuf<int32_t> d_order_a, d_tile;  // the diagonal pass: list A, the reads it hands on
     DevBuf<unsigned long long> d_lb;   // look-back words of the single-pass scans (sort, redo list, ops)
     DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
     DevBuf<int32_t> d_nops, d_opsctl;
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
-        d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release(); d_order_a.release();
-        d_tile.release(); d_seed.release(); d_seed2.release(); d_seed_list.release(); d_seed_flags.release(); d_seed_list2.release();
+        d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release();
+        d_seed.release(); d_seed2.release(); d_seed_list.release(); d_seed_flags.release(); d_seed_list2.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
     }
 };
 constexpr int kScratchSets = 6;   // 3 per pass of a dual call, 3 otherwise
 constexpr int kComputeStreams = 3;
-constexpr int64_t kDiagMinChunks = 12;
 constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level (region capacity)
 
 // Test switches (environment, read per call).  Each forces a path the defaults reach only on
@@ -112,17 +109,12 @@ constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level
 //   CRISPR_NW_EXACT      "multi[:grid]": the exact work lists through the multi-wave kernel (the
 //                        first `grid` entries, the rest through the one-wave kernel); "lds": the
 //                        one-wave kernel keeps its traceback in LDS however few waves fit
-//   CRISPR_NW_DIAGPASS   "0" / "1": the diagonal pass off / on in every chunk
 //   CRISPR_NW_WIDE       "0": no 128-diagonal level
 //   CRISPR_NW_DIRECT     reads up to which a chunk's first level hands straight to the wide level
 //   CRISPR_NW_ADAPT      "0": no adaptive level choice across chunks
 //   CRISPR_NW_CHUNK, CRISPR_NW_OPS_SLOT, CRISPR_NW_SPILL_WORDS, CRISPR_NW_REGION_MB: sizes
 //                        (chunk reads, runs per slot, spill words, band region MB)
 // and CRISPR_NW_HOST_TIMING=1 (diagnostics: the host's phase split of a call on stderr).
-int diag_pass_env() {   // -1: default, 0 / 1: forced off / on
-    const char* e = std::getenv("CRISPR_NW_DIAGPASS");
-    return e ? (std::atoi(e) != 0) : -1;
-}
 
 struct nw_ctx {
     int device = 0;
@@ -199,9 +191,6 @@ struct nw_ctx {
     bool exact_tb_lds = true;
     bool exact_full = false;          // long amplicon: every read through the multi-wave kernel
     bool skip16 = false;              // this chunk: the 32-diagonal level only (ops_call's adaptive choice)
-    bool diag_off = false;            // this chunk: no diagonal pass (ops_call's adaptive choice)
-    bool diag_ran = false;            // launch_range ran the diagonal pass for this chunk
-    bool diag_tail = false;           // this chunk is one of the call's last (no diagonal pass)
     bool exact_small = false;         // this chunk: the exact kernel's work list on a small grid (ops_call)
     bool lane_walk = false;           // resident passes: the first level's lane walk + stop summary (nw_batch_set_lane_walk)
     bool lane_call = false;           // this chunk of ops_call: the lane walk + stop summary (chunks of >= 65536 reads)
@@ -326,7 +315,6 @@ unsigned next_epoch(nw_ctx* c) {
 // the markup bits of the band walk (codes each row scores > 0 against).
 struct AmpTables {
     int R = 0;
-    bool amp_plain = true;
     std::vector<int8_t> prof;
     std::vector<uint32_t> rowpos;
     std::vector<uint32_t> amp2, seed_key;   // window seeds (Profile::amp2 / seed_key / seed_pos)
@@ -399,7 +387,6 @@ bool amp_tables(const std::string& ref, int scale, AmpTables* t) {
         for (int code = 0; code < nw::NCODE; ++code)
             if (ca < 16 && code < 16 && nw::kEdna[ca][code] > 0) m |= 1u << code;
         t->rowpos[(size_t)ai] = m;
-        t->amp_plain = t->amp_plain && ca < 16;
     }
     const int R = La <= kMaxRefWave ? nw::rows_per_lane_for(La) : 0;
     t->R = R;
@@ -518,7 +505,6 @@ int upload_profiles(nw_ctx* c, const std::vector<std::string>& refs, std::vector
         p.rowpos = (const uint32_t*)(b + o.rowpos);
         p.amp = b + o.amp;
         p.R = tabs[g].R;
-        p.amp_plain = tabs[g].amp_plain;
         p.cls_img = (const uint32_t*)(b + o.cls);
         p.cls_words = (int32_t)tabs[g].cls.size();
         p.amp_acgt = tabs[g].amp_acgt;
@@ -716,8 +702,6 @@ int configure(nw_ctx* c) {
             }
             HIP_OR_FAIL(c, c->s->d_bregion.reserve((size_t)rbytes));
             HIP_OR_FAIL(c, c->s->d_order.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->s->d_order_a.reserve((size_t)std::max<int64_t>(c->n, 1)));
-            HIP_OR_FAIL(c, c->s->d_tile.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(c->n)));
@@ -1031,7 +1015,6 @@ hipError_t launch_work(nw_ctx* c, const nw::KernelArgs& a) {
 // uploaded arrays (outputs, records and fallback queue at the same index).
 // Everything is queued on c->stream; nothing synchronises.
 int launch_range(nw_ctx* c, int64_t base) {
-    c->diag_ran = false;
     c->tail_prio = true;   // the latency-bound kernels of a chunk's chain at raised issue priority (-1.1 %)
     nw::KernelArgs a{};
     a.reads = c->d_reads.p - c->reads_bias;
@@ -1120,17 +1103,6 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.pk_gbase = c->pkc.pk_gbase;
         a.pk_call_lo = c->pkc.pk_call_lo;
         a.known2 = c->known_on ? c->kset[c->kcur].d_k2.p : nullptr;
-        // the diagonal pass (ops output, an amplicon of EDNAFULL letters): the sort puts the
-        // reads of the amplicon's length in their own list (CRISPR_NW_DIAGPASS=0: off)
-        const bool diag_pass = c->out_mode == NW_OUT_OPS && c->cur.amp_plain && !c->diag_off && !c->diag_tail &&
-                               diag_pass_env() != 0;
-        c->diag_ran = diag_pass;
-        if (diag_pass) {
-            a.order_a = c->s->d_order_a.p;
-            a.count_a = c->s->d_fallback_count.p + 4;
-            a.tile_list = c->s->d_tile.p;
-            a.tile_count = c->s->d_fallback_count.p + 5;
-        }
         a.zero_ctl64 = c->zero_ctl;
         a.zero_ctl64_n = nw::kOpsCtlAll;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
@@ -1156,8 +1128,6 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
         if (!two) direct = 0;
         c->redo_direct = direct;
-        // (the diagonal pass and the traceback fill as one launch measured slower: kernel-resident
-        // fill 0.578 vs 0.477 ms per 1M reads)
         for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
             al.redo_direct = lvl == 1 ? direct : 0;
@@ -1177,14 +1147,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             const nw::LaunchCfg& fc = lvl == 0 ? c->diag16_fill : c->diag_fill;
             const nw::LaunchCfg& wc = lvl == 0 ? c->diag16_walk : c->diag_walk;
             const bool first = lvl == (two ? 0 : 1);
-            if (!first) {   // the second level aligns the redo list only
-                al.order_a = nullptr;
-                al.tile_list = nullptr;
-                al.tile_count = nullptr;
-            } else if (al.order_a) {
-                HIP_OR_FAIL(c, nw::launch_band_diag(W, al, fc, pairs, c->cs));
-                tmark(c, "diag");
-            }
             for (int64_t lo = 0; lo < pairs; lo += pp) {
                 nw::KernelArgs ap = al;
                 ap.band_pair_lo = lo;
@@ -1206,7 +1168,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             nw::KernelArgs ac = a;
             ac.band_order = c->s->d_seed_list.p;
             ac.band_count = a.seed_count;
-            ac.tile_count = nullptr;
             ac.redo_flags = c->s->d_seed_flags.p;
             ac.redo_list = c->s->d_seed_list2.p;
             ac.redo_count = c->s->d_fallback_count.p + 8;   // zeroed by nw_band_classify
@@ -1227,9 +1188,6 @@ int launch_range(nw_ctx* c, int64_t base) {
             aw.band_from_work = 1;
             aw.band_count = a.work_count;
             aw.redo_flags = nullptr;
-            aw.order_a = nullptr;
-            aw.tile_list = nullptr;
-            aw.tile_count = nullptr;
             aw.band_stride = c->wide_stride;
             aw.band_words = c->wide_words;
             aw.band_lb_cap = c->wide_lb_cap;
@@ -1300,16 +1258,11 @@ int launch_range_ops(nw_ctx* c, int64_t base, hipEvent_t staging_free = nullptr,
     cnt.prio = c->tail_prio;
     if (c->use_diag && c->n > 0) {
         cnt.band = c->s->d_fallback_count.p + 1;
-        cnt.band_a = c->s->d_fallback_count.p + 4;   // list A (0 without the diagonal pass: zeroed by classify)
         // second-level reads of a two-level chunk; a chunk run on the 32-diagonal level alone
         // counts its DP reads apart (ctl[7]: the adaptive choice reads two-level chunks only)
         if (c->diag16_fill.grid > 0 && !c->skip16) cnt.redo = c->s->d_fallback_count.p + 2;
         cnt.one_level = c->diag16_fill.grid > 0 && c->skip16;
         cnt.direct = c->skip16 ? 0 : c->redo_direct;
-        if (c->diag_ran) {
-            cnt.list_a = c->s->d_fallback_count.p + 4;
-            cnt.handed = c->s->d_fallback_count.p + 5;
-        }
         if (c->wide_fill.grid > 0) cnt.exact = c->s->d_fallback_count.p + 6;
         if (c->seed_chunk) {
             cnt.seeded = c->s->d_fallback_count.p + 7;
@@ -1973,8 +1926,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->seed_pairs = 0;
         c->split_to = nullptr;
         c->skip16 = false;
-        c->diag_off = false;
-        c->diag_tail = false;
         c->exact_small = false;
         c->trace_on = false;
         c->known_on = false;
@@ -2245,22 +2196,11 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
     const char* adapt = std::getenv("CRISPR_NW_ADAPT");   // "0": every chunk runs both band levels
     const bool adaptive = !(adapt && std::strcmp(adapt, "0") == 0);
     std::vector<char> one_level((size_t)std::max<int64_t>(nchunks, 1), 0);   // chunk ran the 32-diagonal level alone
-    std::vector<char> no_diag((size_t)std::max<int64_t>(nchunks, 1), 0);     // chunk ran without the diagonal pass
-    c->diag_off = false;
-    // The diagonal pass saves GPU time but adds a launch to every chunk's chain.  The call's
-    // last chunk, whose latency the call waits for at its end, runs without it; every other
-    // chunk of an uploading call with it (with the wide level taking the exact kernel's ~80 us
-    // off each chain, the 1M-read C2 call measured 2.17 ms vs 2.26 without the pass in its 7
-    // chunks).  A resident pass (the C3 HDR pass, whose list-A reads the pass mostly hands on)
-    // keeps round 3's rule: calls of fewer than kDiagMinChunks chunks run without it.
-    // CRISPR_NW_DIAGPASS=1 / 0: on / off for every chunk (tests).
-    int64_t diag_tail = nchunks < 2 ? 0 : 1;
-    {
-        const int forced = diag_pass_env();
-        if (forced == 1) diag_tail = 0;
-        const int64_t min_chunks = upload ? 2 : kDiagMinChunks;
-        if (forced != 1 && nchunks > 1 && nchunks < min_chunks) diag_tail = nchunks;   // short pipeline: no diagonal pass
-    }
+    // (Rounds 3-5 ran a score-only diagonal pass over the reads of the amplicon's length ahead of
+    // the first level's traceback fill in all but a call's last chunk, switched off per chunk when it
+    // handed most reads on.  With round 6's classify certificates taking nearly all of those reads its
+    // sweep only lengthened each chain: removed, in-process A/Bs C2 call 1.894 -> 1.833 ms, resident
+    // pass 0.536 -> 0.484 ms, dual call 5.28 -> 5.12 ms, C1 shape 3.03 -> 2.98 ms)
     if (rc) {
         (void)hipStreamSynchronize(c->s_in);
         return restore(rc);
@@ -2453,24 +2393,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         // on a high-priority stream, each chunk's upload split over two streams: +0.01 to +0.58 ms.)
         // the exact kernel's grid: small while the newest chunk read back sent it few reads
         // (after the wide level it gets the rare read no band certifies)
-        c->exact_small = jn < 0 || hn[10] - hpn[10] < 256;
-        // the last chunks of a call run without the diagonal pass: their chains' latency (not
-        // the GPU's throughput) is what the call waits for at its end, and the pass adds a
-        // launch to the chain
-        c->diag_tail = k >= nchunks - diag_tail;
-        // adaptive diagonal pass: when it handed most of a chunk's list A on to the traceback
-        // pass (the HDR pass: 10 clustered mismatches against the HDR amplicon are aligned as
-        // two gaps, not down one diagonal), the next chunks skip it; while skipped, every 4th
-        // chunk runs it again
-        if (dual) c->diag_off = false;
-        if (adaptive && jn >= 0) {
-            if (!no_diag[(size_t)jn]) {
-                const int64_t la = hn[8] - hpn[8], ho = hn[9] - hpn[9];
-                c->diag_off = la >= 2048 && 2 * ho > la;
-            } else {
-                c->diag_off = (in_pass(k) & 3) != 0;
-            }
-        }
+        c->exact_small = jn < 0 || hn[8] - hpn[8] < 256;
         // diagnostics: the last chunks' launches
         c->trace_on = trace_chunks > 0 && k >= nchunks - trace_chunks;
         c->trace_chunk = (int)k;
@@ -2485,7 +2408,6 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
                                    c->h_ctl + nw::kOpsCtl * k, (int)(in_pass(k) & 1), direct_k ? &ho : nullptr)))
             return restore(rc);
         direct_done[(size_t)k] = direct_k;
-        no_diag[(size_t)k] = !c->diag_ran;
         HIP_OR_FAIL(c, hipEventRecord(c->ev_ce[(size_t)k], c->cs));
         // s_out order: chunk k - lag's runs (their size is known once that chunk is done:
         // the host waits for it, so lag = nsets - 1 chunks stay queued ahead), then chunk
@@ -2523,7 +2445,7 @@ int ops_call(nw_ctx* c, const char* reads, const int64_t* offsets, int64_t n, ui
         c->call_counts[1] = two ? h[6] - h[7] : 0;                // first level: two-level chunks' DP reads
         c->call_counts[2] = any_diag ? (two ? h[5] + h[7] : h[6]) : 0;
         c->call_counts[3] = h[4];
-        c->call_exact = h[10];
+        c->call_exact = h[8];
     }
     c->call_done = true;
     // device times: the upload span on s_in, the chunks' compute spans summed
@@ -2872,7 +2794,7 @@ int nw_batch_path_counts(nw_ctx* c, int64_t* counts4) {
     }
     int32_t fb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, need = 0;
     HIP_OR_FAIL(c, hipMemcpy(fb, c->s->d_fallback_count.p, sizeof fb, hipMemcpyDeviceToHost));
-    need = fb[1] + fb[4];   // the sort's DP count: list B + list A (the diagonal pass)
+    need = fb[1];   // the sort's DP count
     const bool two = c->diag16_fill.grid > 0;
     counts4[0] = c->n - need;             // exact copies (no DP)
     counts4[1] = two ? need : 0;          // first level (16 diagonals)

@@ -172,14 +172,12 @@ __global__ __launch_bounds__(kOpsThreads) void nw_ops_compact(const int32_t* nop
         nw -= pw;
         n2 -= pad - pw;
         ctl[4] += fb + nw;
-        ctl[10] += cnt.exact ? (long long)*cnt.exact : fb;
+        ctl[8] += cnt.exact ? (long long)*cnt.exact : fb;
         if (cnt.redo && !direct) ctl[5] += *cnt.redo;
         ctl[5] += n2;
-        const long long dp = (cnt.band ? *cnt.band : 0) + (cnt.band_a ? *cnt.band_a : 0) + ns - pad;
+        const long long dp = (cnt.band ? *cnt.band : 0) + ns - pad;
         ctl[6] += dp;
         if (cnt.one_level) ctl[7] += dp;
-        if (cnt.list_a) ctl[8] += *cnt.list_a;
-        if (cnt.handed) ctl[9] += *cnt.handed;
         if (hctl)
             for (int q = 0; q < kOpsCtl; ++q) hctl[q] = ctl[q];
     }

@@ -4,7 +4,8 @@ drift (PCIe, host load) hits both alike.
 Usage: ab_call.py "VAR=v,VAR2=w" "VAR=u" [rounds] [pooled]   (an empty string = defaults;
 c1: the C1-shape call (151 bp windows x 280 bp amplicon); pooled: the C5 call, nw_align_multi_ops_packed over 96 amplicons x 100k reads; c3: the dual
 alignment step, packed amplicon pass + resident HDR pass records-only; dual: A = that step, B = the
-one-call dual alignment, nw_align_dual_ops_packed_lens; dualonly: the dual call alone)"""
+one-call dual alignment, nw_align_dual_ops_packed_lens; dualonly: the dual call alone; resident: the bench value's pass over the C2 batch held in HBM,
+nw_batch_run_async + nw_batch_sync with the lane walk, as bench.py times it)"""
 import os
 import sys
 import time
@@ -27,6 +28,7 @@ pooled = len(sys.argv) > 4 and sys.argv[4] == "pooled"
 c3 = len(sys.argv) > 4 and sys.argv[4] == "c3"
 c4 = len(sys.argv) > 4 and sys.argv[4] == "c4"
 c1 = len(sys.argv) > 4 and sys.argv[4] == "c1"
+resident = len(sys.argv) > 4 and sys.argv[4] == "resident"
 # dual: A = the two-call C3 step, B = the dual call (the env specs still apply); dualonly: the dual call
 dual = len(sys.argv) > 4 and sys.argv[4] in ("dual", "dualonly")
 dualonly = len(sys.argv) > 4 and sys.argv[4] == "dualonly"
@@ -61,6 +63,10 @@ stats2 = _lib.PinnedBuffer(nr, _lib.STAT_DTYPE)
 ops_off2 = _lib.PinnedBuffer(nr + 1, np.int64)
 if not pooled:
     al.set_reference(amplicon)
+if resident:
+    al.upload_packed(pr)
+    al.set_lane_walk(True)
+    al.set_phase_events(False)
 keys = set(A) | set(B)
 times = {"A": [], "B": []}
 counts = {}
@@ -71,7 +77,10 @@ for i in range(2 * rounds + 4):
         os.environ.pop(k, None)
     os.environ.update(A if which == "A" else B)
     t0 = time.perf_counter()
-    if pooled:
+    if resident:
+        al.run_async()
+        al.sync()
+    elif pooled:
         al.align_multi_ops(amps, pr, None, pw.array, out=(stats.array, ops.array, ops_off.array))
     elif dual and (which == "B" or dualonly):
         al.set_reference(amplicon)
@@ -91,8 +100,12 @@ for i in range(2 * rounds + 4):
         times[which].append(dt * 1e3)
     if os.environ.get("AB_COUNTS"):
         counts[which] = al.path_counts()
-    out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes(),
-           stats2.array.tobytes() if c3 else b"")
+    if resident:
+        r = al.download_ops(nr)
+        out = (r.stats.tobytes(), r.ops_off.tobytes(), r.ops[:int(r.ops_off[nr])].tobytes())
+    else:
+        out = (stats.array.tobytes(), ops_off.array.tobytes(), ops.array[:int(ops_off.array[-1])].tobytes(),
+               stats2.array.tobytes() if c3 else b"")
     if ref is None:
         ref = out
     elif out != ref:

@@ -14,7 +14,7 @@ Every read's record (length, identity, similarity, gaps, score, start cell, flag
 the three rows expanded from its runs equal the oracle's (tests/every_read.py: the
 oracle runs once per distinct read; duplicates must carry the same GPU output).  These
 cover round 3's certificate paths (one- and two-substitution reads finished in
-classify, the diagonal pass's single-diagonal reads, the walk's plain-read records, the
+classify, the walk's single-diagonal and plain-read records, the
 128-diagonal wide level) on the workloads that exercise them.
 """
 import os

@@ -19,19 +19,13 @@ pytestmark = pytest.mark.gpu
 KERNELS = ["diag", "full"]
 
 
-# the band path's ops-mode variant without the diagonal pass (what every call's last chunk runs)
-VARIANTS = {"diag-nodiagpass": {"CRISPR_NW_DIAGPASS": "0"}}
-
-
-@pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")] + [f"{v}/ops" for v in VARIANTS])
+@pytest.fixture(params=[f"{k}/{m}" for k in KERNELS for m in ("ops", "rows")])
 def kernel(request, monkeypatch):
     """Run a test once per kernel family (CRISPR_NW_KERNEL selects it) and output
     mode (ops: runs over PCIe + host expansion, the default; rows: the kernels write
     the three strings)."""
     fam, mode = request.param.split("/")
-    for k, v in VARIANTS.get(fam, {}).items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("CRISPR_NW_KERNEL", fam.split("-")[0])
+    monkeypatch.setenv("CRISPR_NW_KERNEL", fam)
     monkeypatch.setenv("CRISPR_NW_OUTPUT", mode)
     return request.param
 
