@@ -108,7 +108,7 @@ for i in range(2 * rounds + 4):
                stats2.array.tobytes() if c3 else b"")
     if ref is None:
         ref = out
-    elif out != ref:
+    elif out != ref and not os.environ.get("AB_NOCHECK"):
         print("OUTPUT DIFFERS at call", i, which)
         sys.exit(1)
 if os.environ.get("AB_COUNTS"):
