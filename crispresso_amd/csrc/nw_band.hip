@@ -390,6 +390,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         unsigned long long cand = __ballot(my_len == La && !exc);   // reads of the amplicon's length
         unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull, sub3 = 0ull;
         unsigned long long known = 0ull;   // copies of the known sequence (KernelArgs::known2)
+        unsigned long long jog = 0ull;     // reads closer to the known sequence than to the amplicon (below)
         // compare kCand candidates at a time (their loads in flight together); when the read
         // fits one 256-byte chunk (La <= 256) its exact copy's rows are written right
         // away from the words already in registers
@@ -601,6 +602,12 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         k2 += __builtin_popcount((x | (x >> 1)) & vmask(t, La));
                     }
                     known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2 | sub3);
+                    // A read of the amplicon's length closer to the known sequence (the other pass's amplicon)
+                    // than to this one: a variant of it carries the amplicons' difference -- C3's 10-base HDR
+                    // block, two 10-base gaps against this amplicon, more than 16 diagonals hold.  It skips
+                    // the first band level (its sort key marks it; nw_band_fill<16> leaves its pair inactive,
+                    // the walk hands it to the 32-diagonal level) instead of failing there first.
+                    jog = __ballot(c && k2 < k && k > 3) & ~(sub1 | sub2 | sub3 | known);
                 }
             }
         }
@@ -1012,7 +1019,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                                 ? a.band_lb_cap + 2
                                 : (sinfo ? a.band_lb_cap + 3 +
                                                min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
-                                         : (my_len <= a.band_lb_cap ? my_len : a.band_lb_cap + 1));
+                                         : (my_len <= a.band_lb_cap && !((jog >> lane) & 1ull) ? my_len : a.band_lb_cap + 1));
         if (a.ops && r < r_end && ((win >> lane) & 1ull)) {
             // runs: s amplicon residues (Y), the window (M), the rest of the amplicon (Y)
             int q = 0;
@@ -1453,6 +1460,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
             LbA = (int)(a.offsets[ra + 1] - offA);
             LbB = (int)(a.offsets[rb + 1] - offB);
             act = LbA <= a.band_lb_cap && LbB <= a.band_lb_cap && band_geometry2(La, LbA, LbB, &dlo, W);
+            // the first level (16 diagonals) leaves a pair with a read classify keyed past the band's lengths
+            // -- one that needs more diagonals (a known sequence's variant: nw_band_classify) -- to the next
+            if constexpr (W < kBandDiags) act = act && a.sort_key[ra] <= a.band_lb_cap && a.sort_key[rb] <= a.band_lb_cap;
             if constexpr (W >= kBandDiags) {
                 // seeded reads (both of the pair): the band centred on their hits' diagonals
                 if (a.seed_info) {

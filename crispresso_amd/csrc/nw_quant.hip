@@ -958,9 +958,30 @@ struct nwq_ctx {
     std::string amp_key;
     QBuf<int32_t> d_fb;      // quant_lanes' fallback list [n] + its count
     bool rows_only = false;  // CRISPR_NWQ_ROWS=1: every read through the rows (A/B, tests)
+    // page-locked landing space of the call's results (the totals, the fallback count): copied back on
+    // the stream before its one synchronisation, no pageable staging or second round trip
+    int64_t* h_totals = nullptr;
+    int64_t h_totals_cap = 0;
+    int32_t* h_nfb = nullptr;
+    // blocks per CU of (kernel, block size, LDS) -- the occupancy query once per shape, not per call
+    struct Occ { const void* f; int threads, lds, per_cu; };
+    Occ occ[8] = {};
+    int n_occ = 0;
 };
 
 namespace {
+
+int occupancy(nwq_ctx* c, const void* f, int threads, int lds, int* per_cu) {
+    for (int i = 0; i < c->n_occ; ++i)
+        if (c->occ[i].f == f && c->occ[i].threads == threads && c->occ[i].lds == lds) {
+            *per_cu = c->occ[i].per_cu;
+            return 0;
+        }
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, threads, lds);
+    if (e != hipSuccess) return (int)e;
+    if (c->n_occ < 8) c->occ[c->n_occ++] = nwq_ctx::Occ{f, threads, lds, *per_cu};
+    return 0;
+}
 
 int qfail(nwq_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
@@ -1006,7 +1027,7 @@ int geometry(nwq_ctx* c, int64_t stride, int64_t n, QGeom* g) {
         return qfail(c, NW_E_UNSUPPORTED, "quantification state for amplicon length %d / stride %lld exceeds LDS",
                      LEN, (long long)stride);
     int per_cu = 0;
-    QHIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwq::quant_kernel, 64 * g->wpb, g->lds));
+    QHIP(c, (hipError_t)occupancy(c, (const void*)nwq::quant_kernel, 64 * g->wpb, g->lds, &per_cu));
     per_cu = std::max(per_cu, 1);
     const int64_t need = (n + g->wpb - 1) / g->wpb;
     g->grid = (int)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)c->num_cus * per_cu));
@@ -1019,7 +1040,7 @@ int geometry(nwq_ctx* c, int64_t stride, int64_t n, QGeom* g) {
 int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, int64_t len_stride,
              const uint8_t* d_pre, int64_t n, nwq_read* d_out, int64_t* totals, float* kernel_ms,
              bool started = false, const int32_t* list = nullptr, const int32_t* list_count = nullptr,
-             int slabs0 = 0) {
+             int slabs0 = 0, int32_t* nfb = nullptr) {
     if (!c->have_params) return qfail(c, NW_E_STATE, "nwq_set_params not called");
     if (stride <= 0 || (stride & 3) || stride >= 32768)
         return qfail(c, NW_E_INVALID, "stride %lld must be a positive multiple of 4 below 32768", (long long)stride);
@@ -1060,9 +1081,19 @@ int run_impl(nwq_ctx* c, uint8_t* d_aln, int64_t stride, const int32_t* d_len, i
                        c->d_partial.p, nslabs, g.nwords, slice, reinterpret_cast<unsigned long long*>(c->d_totals.p));
     QHIP(c, hipGetLastError());
     QHIP(c, hipEventRecord(c->ev1, c->stream));
-    QHIP(c, hipMemcpyAsync(totals, c->d_totals.p, sizeof(int64_t) * (size_t)g.nwords, hipMemcpyDeviceToHost,
+    if (c->h_totals_cap < g.nwords) {
+        if (c->h_totals) (void)hipHostFree(c->h_totals);
+        c->h_totals = nullptr;
+        c->h_totals_cap = 0;
+        QHIP(c, hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * (size_t)g.nwords, hipHostMallocDefault));
+        c->h_totals_cap = g.nwords;
+    }
+    QHIP(c, hipMemcpyAsync(c->h_totals, c->d_totals.p, sizeof(int64_t) * (size_t)g.nwords, hipMemcpyDeviceToHost,
                            c->stream));
+    if (nfb && list_count) QHIP(c, hipMemcpyAsync(c->h_nfb, list_count, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     QHIP(c, hipStreamSynchronize(c->stream));
+    std::memcpy(totals, c->h_totals, sizeof(int64_t) * (size_t)g.nwords);
+    if (nfb && list_count) *nfb = *c->h_nfb;
     if (kernel_ms) QHIP(c, hipEventElapsedTime(kernel_ms, c->ev0, c->ev1));
     return NW_OK;
 }
@@ -1081,7 +1112,8 @@ int nwq_create(int device, nwq_ctx** out) {
     nwq_ctx* c = new nwq_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_nfb, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         nwq_destroy(c);
         return NW_E_HIP;
     }
@@ -1106,6 +1138,8 @@ void nwq_destroy(nwq_ctx* c) {
     c->d_lut.release();
     c->d_rowpos.release();
     c->d_fb.release();
+    if (c->h_totals) (void)hipHostFree(c->h_totals);
+    if (c->h_nfb) (void)hipHostFree(c->h_nfb);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1242,7 +1276,7 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
     c->lane_fallbacks = -1;
     if (lanes) {
         int per_cu = 0;
-        QHIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nwq::quant_lanes, 64 * lane_wpb, lane_lds));
+        QHIP(c, (hipError_t)occupancy(c, (const void*)nwq::quant_lanes, 64 * lane_wpb, lane_lds, &per_cu));
         per_cu = std::max(per_cu, 1);
         const int64_t groups = (n + nwq::kQSuper - 1) / nwq::kQSuper;   // a wave's super-groups
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((groups + lane_wpb - 1) / lane_wpb,
@@ -1288,11 +1322,10 @@ int nwq_run_device_ops(nwq_ctx* c, const char* amplicon, int32_t amplicon_len, c
                            (const int32_t*)d_stats, d_reads, d_offsets, reads_bias, c->d_amp.p, c->d_rowpos.p,
                            c->d_lut.p, amplicon_len, d_pre, 0, n, c->d_aln.p, stride, c->d_fb.p, c->d_fb.p + nn);
         QHIP(c, hipGetLastError());
-        const int rc = run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms,
-                                true, c->d_fb.p, c->d_fb.p + nn, grid);
         int32_t nfb = -1;
-        if (rc == NW_OK) QHIP(c, hipMemcpy(&nfb, c->d_fb.p + nn, sizeof nfb, hipMemcpyDeviceToHost));
-        c->lane_fallbacks = nfb;
+        const int rc = run_impl(c, c->d_aln.p, stride, (const int32_t*)d_stats, 8, d_pre, n, d_out, totals, kernel_ms,
+                                true, c->d_fb.p, c->d_fb.p + nn, grid, &nfb);
+        c->lane_fallbacks = rc == NW_OK ? nfb : -1;
         return rc;
     }
     if (n > 0) {
