@@ -1399,6 +1399,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NW_FILL_WPE
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // second level skipped: its reads go to the wide level (with the seeded list: that list alone)
     if (W == kBandDiags && redo_direct_taken(a) && a.seed_l2 != 1) return;
+    if (W < kBandDiags && l1_skipped(a)) return;   // first level skipped (KernelArgs::l1_skip)
     if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     const int La = a.La;
     const int O = a.gap_open, E = a.gap_extend;
@@ -2453,6 +2454,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(LN ? NW_WAL
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // second level skipped: its reads go to the wide level (with the seeded list: that list alone)
     if (W == kBandDiags && redo_direct_taken(a) && a.seed_l2 != 1) return;
+    if (W < kBandDiags && l1_skipped(a)) return;   // first level skipped (KernelArgs::l1_skip)
     if (W >= kBandDiags && a.tail_prio) __builtin_amdgcn_s_setprio(3);
     constexpr int CW = W > 64 ? W / 64 : 1;   // captures (band diagonals) per lane
     const int La = a.La, E = a.gap_extend;
@@ -2893,9 +2895,10 @@ __global__ __launch_bounds__(256) void nw_band_redo_compact(const KernelArgs a, 
     const long long n = band_list_count(a);
     const long long k0 = (long long)blockIdx.x * kRedoBlock + threadIdx.x * 4;
     int f[4], s = 0;
+    const bool all = l1_skipped(a);   // the first level was skipped: every position goes on
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        f[t] = k0 + t < n ? a.redo_flags[k0 + t] : 0;
+        f[t] = k0 + t < n ? (all ? 1 : a.redo_flags[k0 + t]) : 0;
     }
     if (pairs) {   // (k0 is even: positions k0 .. k0 + 3 are two whole pairs)
         f[0] = f[1] = f[0] | f[1];

@@ -74,6 +74,11 @@ struct KernelArgs {
     // then the redo list): a few hundred reads cost the exact kernel's latency once, less
     // than the second level's fill + walk ahead of it.  Decided on the device per chunk.
     int32_t redo_direct;
+    // > 0: a chunk whose sort found at most this many reads that need the DP (*band_count of the first
+    // level's launches) sends them all past the 16-diagonal level: its fill and walk return at once, the
+    // redo compaction takes every position, and (l1_skip <= redo_direct) the wide level aligns them -- a
+    // chunk with few DP reads waits for one level's latency instead of three.  Decided on the device.
+    int32_t l1_skip;
     int32_t band_from_work;    // the wide level: the band list is the exact kernel's work list (exact_work_read)
     int32_t* seed_info2;       // [n] the seeded reads' block facts for the refined certificate (seed2_pack; null: off)
     // ops output (include/crispr_nw.h nw_align_ops): instead of the three string rows,
@@ -151,6 +156,9 @@ __host__ __device__ inline int end_trail(const KernelArgs& a, int k) { return -e
 // by the second level's kernels, the exact kernel and the ops counts alike).
 __host__ __device__ inline bool redo_direct_taken(const KernelArgs& a) {
     return a.redo_direct > 0 && a.redo_count && *a.redo_count <= a.redo_direct;
+}
+__host__ __device__ inline bool l1_skipped(const KernelArgs& a) {
+    return a.l1_skip > 0 && a.band_count && *a.band_count <= a.l1_skip;
 }
 // The exact kernel's work: entries [0, fallbacks) of the work list, then (direct) the redo list.
 __host__ __device__ inline long long exact_work_count(const KernelArgs& a) {

@@ -111,6 +111,7 @@ constexpr int64_t kWidePairs = 2048;     // read pairs of one chunk's wide level
 //                        one-wave kernel keeps its traceback in LDS however few waves fit
 //   CRISPR_NW_WIDE       "0": no 128-diagonal level
 //   CRISPR_NW_DIRECT     reads up to which a chunk's first level hands straight to the wide level
+//   CRISPR_NW_L1SKIP     "0": chunks of >= 65536 reads with few DP reads keep the first level
 //   CRISPR_NW_ADAPT      "0": no adaptive level choice across chunks
 //   CRISPR_NW_CHUNK, CRISPR_NW_OPS_SLOT, CRISPR_NW_SPILL_WORDS, CRISPR_NW_REGION_MB: sizes
 //                        (chunk reads, runs per slot, spill words, band region MB)
@@ -1128,6 +1129,14 @@ int launch_range(nw_ctx* c, int64_t base) {
         if (const char* e = std::getenv("CRISPR_NW_DIRECT")) direct = std::max(0, std::atoi(e));
         if (!two) direct = 0;
         c->redo_direct = direct;
+        // a chunk of >= 65536 reads with at most `direct` DP reads (device count) skips the first level too,
+        // when the wide level can take them: one level's latency in its chain instead of three (in-process
+        // A/B, C2 call 1.849 -> 1.771 ms, outputs identical; C1, C3, C5 unchanged).  Smaller launches (the
+        // tests' batches) keep the first level.  CRISPR_NW_L1SKIP=0: off
+        {
+            const char* e = std::getenv("CRISPR_NW_L1SKIP");
+            a.l1_skip = two && c->wide_fill.grid > 0 && c->n >= 65536 && !(e && std::atoi(e) == 0) ? direct : 0;
+        }
         for (int lvl = two ? 0 : 1; lvl < 2; ++lvl) {
             nw::KernelArgs al = a;
             al.redo_direct = lvl == 1 ? direct : 0;
@@ -1169,6 +1178,7 @@ int launch_range(nw_ctx* c, int64_t base) {
             ac.band_order = c->s->d_seed_list.p;
             ac.band_count = a.seed_count;
             ac.redo_flags = c->s->d_seed_flags.p;
+            ac.l1_skip = 0;
             ac.redo_list = c->s->d_seed_list2.p;
             ac.redo_count = c->s->d_fallback_count.p + 8;   // zeroed by nw_band_classify
             HIP_OR_FAIL(c, nw::launch_redo_compact(ac, c->n + c->n / 4096 + 2, next_epoch(c), c->cs, true));

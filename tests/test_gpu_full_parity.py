@@ -81,6 +81,34 @@ def test_c2_every_read(al):
     _close(keep, outs)
 
 
+def test_first_level_skip_every_read(al, monkeypatch):
+    """KernelArgs::l1_skip (round 6): a launch of >= 65536 reads whose sort finds few DP reads sends
+    them all to the wide level, past the 16-diagonal level.  A 200k-read C2-shaped batch as one resident
+    pass (one launch: the skip) and as the pipelined call (its chunks take the skip too), every read
+    against the oracle, and against the same reads with the skip off (CRISPR_NW_L1SKIP=0)."""
+    amp = synth.random_amplicon(AMPLICON_LEN, 1)
+    buf, off = synth.reads_from(amp, 200_000, 21)
+    pr, keep = _packed(buf, off)
+    n = len(off) - 1
+    outs1, out1 = _pinned_out(n)
+    outs2, out2 = _pinned_out(n)
+    al.set_reference(amp)
+    ob = al.align_ops_packed(pr, out=out1)
+    _assert_clean(every_read(amp, buf, off, ob, THREADS), "call, first level skipped")
+    res = al.align_ops(None, pr.offsets, out=out2, resident=True)
+    c = al.path_counts()
+    assert every_read_records(res.stats, ob.stats) == 0 and np.array_equal(res.ops_off, ob.ops_off)
+    assert np.array_equal(res.ops[:int(res.ops_off[n])], ob.ops[:int(ob.ops_off[n])])
+    monkeypatch.setenv("CRISPR_NW_L1SKIP", "0")
+    res0 = al.align_ops(None, pr.offsets, out=out2, resident=True)
+    c0 = al.path_counts()
+    # with the skip the chunks' DP reads went to the wide level; without it the first level certified most
+    assert c["band16"] == c0["band16"] > 0 and c["band_fallback"] > 2 * c0["band_fallback"]
+    assert every_read_records(res0.stats, ob.stats) == 0 and np.array_equal(res0.ops_off, ob.ops_off)
+    assert np.array_equal(res0.ops[:int(res0.ops_off[n])], ob.ops[:int(ob.ops_off[n])])
+    _close(keep, outs1, outs2)
+
+
 def test_c3_both_passes_every_read(al):
     amp, hdr, buf, off = synth.c3_workload(READS)
     pr, keep = _packed(buf, off)
