@@ -25,7 +25,7 @@ def test_pmc_summary_covers_the_timed_kernels(which):
     with open(path) as f:
         summ = json.load(f)
     assert summ["_meta"]["calls"] and summ["_meta"]["lib_sha1"]
-    for k in ("nw_band_classify", "nw_band_segsort", "nw_band_fill<16, 1, true>", "nw_band_walk<16, true>",
+    for k in ("nw_band_classify", "nw_band_segsort", "nw_band_fill<16, true>", "nw_band_walk<16, true>",
               "nw_ops_compact"):
         assert any(k in name for name in summ), k
     cp = b.pmc_per_call(path, lambda k: ("nw::" in k and "nwq::" not in k) or "nw_align_kernel" in k)
