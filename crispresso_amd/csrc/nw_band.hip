@@ -268,10 +268,328 @@ __device__ inline long long exc_lower_bound(const KernelArgs& a, long long pos, 
     return lo + (long long)__builtin_popcountll(__ballot(below));
 }
 
-// (at 95 VGPRs, 5 wavefronts per SIMD; forced to 6 / 8 with 31 / 60 VGPRs spilled it ran 0.188 / 0.223 vs 0.150 ms
-// per resident pass)
+// (classify and nw_band_cert) the bases 16 t + i < len of a 2-bit word (one bit per base)
+__device__ __forceinline__ unsigned vmask16(int t, int len) {
+    const int b = len - 16 * t;
+    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
+}
+// 16 bases of the packed stream from batch position p
+__device__ __forceinline__ unsigned pk_word16(const KernelArgs& a, long long p) {
+    const long long q = p - a.pk_pos0;
+    const unsigned* w = a.pk_words + (q >> 4);
+    return __builtin_amdgcn_alignbit(w[1], w[0], (unsigned)(2 * (q & 15)));
+}
+// 16 bases of the amplicon from position p (its 2-bit words in LDS)
+__device__ __forceinline__ unsigned amp_word16(const unsigned* amp2s, int p) {
+    return __builtin_amdgcn_alignbit(amp2s[(p >> 4) + 1], amp2s[p >> 4], (unsigned)(2 * (p & 15)));
+}
+// A lane's read of the amplicon's length at batch position my_off: its 2-bit words shifted to base 0
+// (rw[16] = 0; bases past the read are masked by the users); c: the lane holds such a read
+__device__ __forceinline__ void load_read_words(const KernelArgs& a, bool c, long long my_off, unsigned (&rw)[17]) {
+    const int nw = (a.La + 15) >> 4;   // <= 16
+    const long long q0 = my_off - a.pk_pos0;
+    const unsigned* src = a.pk_words + (q0 >> 4);
+    const unsigned s2 = (unsigned)(2 * (q0 & 15));
+    unsigned wd[17];
+#pragma unroll
+    for (int t = 0; t < 17; ++t) wd[t] = c && t <= nw ? src[t] : 0u;   // <= the read's last dword + 1
+#pragma unroll
+    for (int t = 0; t < 16; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
+    rw[16] = 0u;
+}
+// Its main diagonal against the amplicon's words (LDS): mismatches k, the first, second and last
+// mismatching base (-1: none)
+__device__ __forceinline__ void main_diag_mism(const unsigned (&rw)[17], const unsigned* amp2s, int La, int* k_, int* f_,
+                                               int* f2_, int* l_) {
+    const int nw = (La + 15) >> 4;
+    int k = 0, f = -1, f2 = -1, l = -1;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        if (t >= nw) continue;
+        const unsigned x = rw[t] ^ amp2s[t];
+        const unsigned m = (x | (x >> 1)) & vmask16(t, La);
+        k += __builtin_popcount(m);
+        if (m != 0u && f >= 0 && f2 < 0) f2 = 16 * t + (__builtin_ctz(m) >> 1);
+        if (m != 0u && f < 0) {
+            f = 16 * t + (__builtin_ctz(m) >> 1);
+            const unsigned m2 = m & (m - 1u);
+            if (m2 != 0u) f2 = 16 * t + (__builtin_ctz(m2) >> 1);
+        }
+        if (m != 0u) l = 16 * t + ((31 - __builtin_clz(m)) >> 1);
+    }
+    *k_ = k;
+    *f_ = f;
+    *f2_ = f2;
+    *l_ = l;
+}
+
+// The three-substitution certificate's per-read checks (i)-(iii) (classify, below; lanes s3: reads of the
+// amplicon's length with three mismatches on the main diagonal, at bases f < f2 < l; the caller checked
+// sub3_ok).  Called by the whole wavefront.
+__device__ __forceinline__ bool cert_sub3(const KernelArgs& a, const unsigned* amp2s, const unsigned (&rw)[17], bool s3,
+                                          int f, int f2, int l, long long my_off) {
+    const int La = a.La, nw = (La + 15) >> 4, sc5 = a.band_maxsub / 5;
+    const int m3 = a.band_maxsub, x3 = 4 * sc5, O3 = a.gap_open, D3 = 3 * (m3 + x3);
+    auto vmask = [](int t, int len) { return vmask16(t, len); };
+    auto rword = [&](long long p) { return pk_word16(a, p); };
+    auto aword = [&](int p) { return amp_word16(amp2s, p); };
+    // per diagonal d = -5 .. 5: mismatches (capped at 3), the first two and the last two
+    // (read index; last ones + 1), over the diagonal's pairs
+    int dc[11], df1[11], df2[11], dg1[11], dg2[11];
+    // jogs (iii): diagonals +-1 against the 16 read bases from f + 1 (up to l - 1), one
+    // word each from the packed stream (random sequence mismatches there; a read whose
+    // diagonals +-1 match all 16 is left to the DP)
+    bool jog_in[2] = {false, false};
+    if (s3) {
+        const int len = min(16, l - f - 1);
+        const unsigned lm = len <= 0 ? 0u : (len >= 16 ? 0x55555555u : (0x55555555u >> (32 - 2 * len)));
+        const unsigned rd = rword(my_off + f + 1);
+        const unsigned zp = rd ^ aword(f), zm = rd ^ aword(f + 2);   // d = +1 / -1
+        jog_in[1] = ((zp | (zp >> 1)) & lm) != 0u;
+        jog_in[0] = ((zm | (zm >> 1)) & lm) != 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+        const int d = e - 5;
+        if (d == 0) {
+            dc[e] = 3; df1[e] = f; df2[e] = f2; dg1[e] = l + 1; dg2[e] = f2 + 1;   // (k == 3)
+            continue;
+        }
+        const int sh = d > 0 ? d : -d;
+        // the first two and the last two mismatches (read index; the last ones + 1) by scans
+        // from either end that stop once every lane has found two (random sequence: within a
+        // word); the count up to 3 follows (3 when the second-last lies past the second)
+        int a1 = La, a2 = La, b1 = 0, b2 = 0;
+        auto word = [&](int t) -> unsigned {
+            // d > 0: read base j = i + d against amplicon base i (words of i); d < 0: read
+            // base j against amplicon base j - d (words of j)
+            const unsigned am = d > 0 ? amp2s[t]
+                                      : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
+            const unsigned rd = d > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
+            const unsigned z = rd ^ am;
+            return (z | (z >> 1)) & vmask(t, La - sh);
+        };
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            // (|d| >= 4: the score test needs one mismatch, no pair test reads the diagonal)
+            if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
+            const unsigned mk = word(t);
+            const int off = 16 * t + (d > 0 ? d : 0);   // read index of the word's base 0
+            if (mk != 0u && a1 == La) {
+                a1 = off + (__builtin_ctz(mk) >> 1);
+                const unsigned m2 = mk & (mk - 1u);
+                if (m2 != 0u) a2 = off + (__builtin_ctz(m2) >> 1);
+            } else if (mk != 0u && a2 == La) {
+                a2 = off + (__builtin_ctz(mk) >> 1);
+            }
+        }
+#pragma unroll
+        for (int t = 15; t >= 0; --t) {
+            if (__ballot(s3 && b2 == 0 && a1 < La) == 0ull) break;
+            if (t >= nw) continue;
+            const unsigned mk = word(t);
+            const int off = 16 * t + (d > 0 ? d : 0);
+            if (mk != 0u && b1 == 0) {
+                const int hb = 31 - __builtin_clz(mk);
+                b1 = off + (hb >> 1) + 1;
+                const unsigned mh = mk & ~(1u << hb);
+                if (mh != 0u) b2 = off + ((31 - __builtin_clz(mh)) >> 1) + 1;
+            } else if (mk != 0u && b2 == 0) {
+                b2 = off + ((31 - __builtin_clz(mk)) >> 1) + 1;
+            }
+        }
+        const int cc = a1 == La ? 0 : (a2 == La ? 1 : (b2 > a2 ? 3 : 2));
+        dc[e] = min(cc, 3); df1[e] = a1; df2[e] = a2; dg1[e] = b1; dg2[e] = b2;
+    }
+    bool ok3 = s3;
+    // (i) single diagonals
+#pragma unroll
+    for (int e = 0; e < 11; ++e) {
+        const int sh = e > 5 ? e - 5 : 5 - e;
+        if (sh == 0) continue;
+        ok3 = ok3 && m3 * sh + (m3 + x3) * dc[e] > D3;
+    }
+    // (ii) one gap, prefix on d1, suffix on d2 (|d| <= 3)
+#pragma unroll
+    for (int e1 = 2; e1 <= 8; ++e1) {
+#pragma unroll
+        for (int e2 = 2; e2 <= 8; ++e2) {
+            if (e1 == e2) continue;
+            const int d1 = e1 - 5, d2 = e2 - 5, g = d2 > d1 ? d2 - d1 : d1 - d2;
+            // unpaired residues of the amplicon (= of the read): its leading / trailing overhang
+            // and the gap's residues when the gap is in the read (the diagonal falls)
+            const int U = (d1 < 0 ? -d1 : 0) + (d2 > 0 ? d2 : 0) + (d1 > d2 ? d1 - d2 : 0);
+            const int slack = D3 - m3 * U - O3 - (g - 1) * a.gap_extend;   // (m + x) w must not exceed it
+            if (slack < 0) continue;
+            const int wmax = slack / (m3 + x3);
+            const int gb = d2 > d1 ? d2 - d1 : 0;   // read bases in the gap
+            bool exists = dg1[e2] - gb <= df1[e1];
+            if (wmax >= 1) exists = exists || dg2[e2] - gb <= df1[e1] || dg1[e2] - gb <= df2[e1];
+            if (wmax >= 2) exists = true;   // (not reached with the gate's parameters: reject)
+            ok3 = ok3 && !exists;
+        }
+    }
+    // (iii) jogs through d = +-1: a mismatch of that diagonal in [f + 1, l - 1] (read index)
+    ok3 = ok3 && l - f >= 2 && jog_in[0] && jog_in[1];
+    return ok3;
+}
+
+// The one-indel certificate (classify, below; lanes ci: reads of La -+ kab bases, 1 <= kab <= the
+// certificate's largest gap, at batch position my_off).  True: certified, *gk_ the gap's read index q
+// (runs M q, the gap, M the rest).  Called by the whole wavefront.
+__device__ __forceinline__ bool cert_indel(const KernelArgs& a, const unsigned* amp2s, bool ci, long long my_off, int my_len,
+                                           int* gk_) {
+    const int La = a.La, n2 = (La + 15) / 16 + 2, sc5 = a.band_maxsub / 5;
+    const int dl = my_len - La, kab = dl < 0 ? -dl : dl;
+const bool del = dl < 0;
+const int Ls = del ? my_len : La, Ll = del ? La : my_len;
+unsigned rw[18];
+{
+    const long long q0 = my_off - a.pk_pos0;
+    const unsigned* src = a.pk_words + (q0 >> 4);
+    const unsigned s2 = (unsigned)(2 * (q0 & 15));
+    const int nrw = (my_len + 15) >> 4;
+    unsigned wd[18];
+#pragma unroll
+    for (int t = 0; t < 18; ++t) wd[t] = ci && t <= nrw ? src[t] : 0u;
+#pragma unroll
+    for (int t = 0; t < 17; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
+    rw[17] = 0u;
+}
+auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
+    const int b = len - 16 * t;
+    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
+};
+const int mm = a.band_maxsub, xx = 4 * sc5;
+const int S = mm * Ls - a.gap_open - (kab - 1) * a.gap_extend;
+bool ok = false;
+int gk = 0;
+// the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
+// registers, picked per lane (deletion and insertion reads in one pass over the shifts)
+if (ci) {
+    auto am = [&](int t) -> unsigned { return t < n2 ? amp2s[t] : 0u; };
+    auto wl = [&](int t) -> unsigned { return del ? am(t) : rw[t]; };
+    auto ws = [&](int t) -> unsigned { return del ? rw[t] : am(t); };
+    bool o = true;
+    // first and last mismatch of a shift (one side's sequence shifted by sh against the
+    // other's, P positions): scans from either end that stop as soon as every lane has found
+    // one (random sequence mismatches within a word; only the two diagonals of the
+    // candidate run to the gap).  Mismatches: 0 (f == P), 1 (f == g - 1) or >= 2 -- all the
+    // score test needs (its bound falls with the count)
+    auto ends = [&](auto lw, auto rw2, int sh, int P, int* f, int* g) {
+        int ff = P, gg = 0;
+#pragma unroll
+        for (int t = 0; t < 17; ++t) {
+            if (__ballot(ff == P && 16 * t < P) == 0ull) break;
+            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+            ff = (ff == P && mk != 0u) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : ff;
+        }
+#pragma unroll
+        for (int t = 16; t >= 0; --t) {
+            if (__ballot(gg == 0 && ff < P) == 0ull) break;   // (words past P: mk == 0)
+            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+            gg = (gg == 0 && mk != 0u) ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : gg;
+        }
+        *f = ff;
+        *g = gg;
+    };
+    auto cnt = [](int f, int g, int P) { return f == P ? 0 : (f == g - 1 ? 1 : 2); };
+    // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
+    // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
+    // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
+    // the shifts past kab and the other side's need only enough mismatches for the score test
+    // (the smallest c with m (P - c) - x c < S, 0 .. 2; more: the DP): forward scans that stop
+    // once that many are found
+    auto enough = [&](auto lw, auto rw2, int sh, int P) -> bool {
+        int need = 0;
+        while (need <= 2 && !(mm * (P - need) - xx * need < S)) ++need;
+        int c = 0;
+#pragma unroll
+        for (int t = 0; t < 17; ++t) {
+            if (__ballot(c < need && need <= 2 && 16 * t < P) == 0ull) break;
+            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+            c += c < need ? __builtin_popcount((z | (z >> 1)) & vmask(t, P)) : 0;
+        }
+        return need <= 2 && c >= need;
+    };
+    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
+    for (int sh = 0; sh <= kab; ++sh) {
+        int f, g;
+        ends(wl, ws, sh, Ls, &f, &g);
+        const int c = cnt(f, g, Ls);
+        o = o && mm * (Ls - c) - xx * c < S;
+        if (sh == 0) f0 = f;
+        if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
+        if (sh == kab) gk = g;
+        fmax_all = max(fmax_all, f);
+        if (sh > 0) fmax_1 = max(fmax_1, f);
+    }
+    for (int sh = kab + 1; sh <= kab + 3; ++sh) o = o && enough(wl, ws, sh, Ll - sh);
+    for (int sh = 1; sh <= 3; ++sh) o = o && enough(ws, wl, sh, Ls - sh);   // s shifted against l
+    ok = ci && o && gk >= 1 && gk <= f0;
+}
+    *gk_ = gk;
+    return ok;
+}
+
+// Packed input: the bytes of the reads in dp (the lanes' reads at my_off, my_len; the whole wavefront)
+// decoded into a.reads -- each read's own bytes exactly (neighbouring reads' bytes are never written by
+// another read's wavefront: no races between blocks)
+__device__ __forceinline__ void write_read_bytes(const KernelArgs& a, unsigned long long dp, long long my_off, int my_len) {
+    const int lane = threadIdx.x & 63;
+    // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
+    // before any store (one read per round trip measured 2.7x the byte-input classify)
+    constexpr int kWr = 8;
+    uint8_t* dst = const_cast<uint8_t*>(a.reads);
+    while (dp) {
+        long long o[kWr], e[kWr];
+        int rounds = 0;
+#pragma unroll
+        for (int t = 0; t < kWr; ++t) {
+            o[t] = e[t] = 0;
+            if (dp) {
+                const int u = (int)__builtin_ctzll(dp);
+                dp &= dp - 1;
+                const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
+                const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
+                o[t] = (long long)(((unsigned long long)hi << 32) | lo);
+                e[t] = o[t] + __builtin_amdgcn_readlane(my_len, u);
+                const int span = (int)(e[t] - (o[t] & ~3ll));
+                rounds = max(rounds, (span + 255) >> 8);
+            }
+        }
+        for (int rd2 = 0; rd2 < rounds; ++rd2) {
+            unsigned v[kWr];
+#pragma unroll
+            for (int t = 0; t < kWr; ++t) {
+                const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
+                v[t] = p < e[t] ? pk_decode4_al(a, p) : 0u;
+            }
+#pragma unroll
+            for (int t = 0; t < kWr; ++t) {
+                const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
+                if (p >= e[t]) continue;
+                if (p >= o[t] && p + 4 <= e[t]) {
+                    *(unsigned*)(dst + p) = v[t];
+                } else {
+                    for (int b = 0; b < 4; ++b)
+                        if (p + b >= o[t] && p + b < e[t]) dst[p + b] = (uint8_t)(v[t] >> (8 * b));
+                }
+            }
+        }
+    }
+}
+
+
+// (5 wavefronts per SIMD; forced to 6 / 8 with 31 / 60 VGPRs spilled it ran 0.188 / 0.223 vs 0.150 ms per resident
+// pass in round 5)
+#ifndef NW_CLASSIFY_WPE
+#define NW_CLASSIFY_WPE 5
+#endif
 template <bool PK>
-__global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW_CLASSIFY_WPE))) void nw_band_classify(const KernelArgs a) {
     extern __shared__ unsigned amp_sh[];   // [nd] folded amplicon dwords (0 at non-ACGT), [nd] raw dwords
     constexpr int kRbw = 66;               // a window read's 16-base words (Lb < La <= 1024) + a zero word
     __shared__ unsigned s_rbw[4][kRbw];
@@ -388,7 +706,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
     auto batch = [&](long long r0, long long r_end, long long my_off, int my_len, bool exc) {
         const long long r = r0 + lane;
         unsigned long long cand = __ballot(my_len == La && !exc);   // reads of the amplicon's length
-        unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull, sub3 = 0ull;
+        unsigned long long exact = 0ull, sub1 = 0ull, sub2 = 0ull;
+        unsigned long long pend3 = 0ull, pend_i = 0ull;   // queued for nw_band_cert (KernelArgs::cert_q)
         unsigned long long known = 0ull;   // copies of the known sequence (KernelArgs::known2)
         unsigned long long jog = 0ull;     // reads closer to the known sequence than to the amplicon (below)
         // compare kCand candidates at a time (their loads in flight together); when the read
@@ -411,32 +730,9 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                     return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
                 };
                 unsigned rw[17];
-                {
-                    const long long q0 = my_off - a.pk_pos0;
-                    const unsigned* src = a.pk_words + (q0 >> 4);
-                    const unsigned s2 = (unsigned)(2 * (q0 & 15));
-                    unsigned wd[17];
-#pragma unroll
-                    for (int t = 0; t < 17; ++t) wd[t] = c && t <= nw ? src[t] : 0u;   // <= the read's last dword + 1
-#pragma unroll
-                    for (int t = 0; t < 16; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
-                    rw[16] = 0u;   // bases past the read: masked below
-                }
-                int k = 0, f = -1, f2 = -1, l = -1;   // mismatches of the main diagonal, first, second and last base
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    if (t >= nw) continue;
-                    const unsigned x = rw[t] ^ amp2s[t];
-                    const unsigned m = (x | (x >> 1)) & vmask(t, La);
-                    k += __builtin_popcount(m);
-                    if (m != 0u && f >= 0 && f2 < 0) f2 = 16 * t + (__builtin_ctz(m) >> 1);
-                    if (m != 0u && f < 0) {
-                        f = 16 * t + (__builtin_ctz(m) >> 1);
-                        const unsigned m2 = m & (m - 1u);
-                        if (m2 != 0u) f2 = 16 * t + (__builtin_ctz(m2) >> 1);
-                    }
-                    if (m != 0u) l = 16 * t + ((31 - __builtin_clz(m)) >> 1);
-                }
+                load_read_words(a, c, my_off, rw);
+                int k, f, f2, l;   // mismatches of the main diagonal, first, second and last base
+                main_diag_mism(rw, amp2s, La, &k, &f, &f2, &l);
                 exact = __ballot(c && k == 0);
                 const bool s1 = c && sub1_ok && k == 1, s2 = c && sub2_ok && k == 2;
                 // diagonal d = sgn * sh (q <= La - 1 - sh): mismatches (counted up to 2), any at q >= qa, any at q <= qb
@@ -490,109 +786,10 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                 // starts max(0, d2 - d1) read bases later: those are the gap's); (iii) a jog 0 -> +-1 -> 0
                 // with no mismatch: its middle covers the read bases (f, l] (d = +1) / [f, l) (d = -1), so a
                 // mismatch of that diagonal in [f + 1, l - 1] excludes both.  Then the diagonal is the unique
-                // optimum and M beats X and Y along it (a tie would be a second alignment scoring D).
+                // optimum and M beats X and Y along it (a tie would be a second alignment scoring D).  The checks
+                // (cert_sub3) run in nw_band_cert, on the queued candidates.
                 const bool s3 = c && sub3_ok && k == 3;
-                if (__ballot(s3)) {
-                    // per diagonal d = -5 .. 5: mismatches (capped at 3), the first two and the last two
-                    // (read index; last ones + 1), over the diagonal's pairs
-                    int dc[11], df1[11], df2[11], dg1[11], dg2[11];
-                    // jogs (iii): diagonals +-1 against the 16 read bases from f + 1 (up to l - 1), one
-                    // word each from the packed stream (random sequence mismatches there; a read whose
-                    // diagonals +-1 match all 16 is left to the DP)
-                    bool jog_in[2] = {false, false};
-                    if (s3) {
-                        const int len = min(16, l - f - 1);
-                        const unsigned lm = len <= 0 ? 0u : (len >= 16 ? 0x55555555u : (0x55555555u >> (32 - 2 * len)));
-                        const unsigned rd = rword(my_off + f + 1);
-                        const unsigned zp = rd ^ aword(f), zm = rd ^ aword(f + 2);   // d = +1 / -1
-                        jog_in[1] = ((zp | (zp >> 1)) & lm) != 0u;
-                        jog_in[0] = ((zm | (zm >> 1)) & lm) != 0u;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 11; ++e) {
-                        const int d = e - 5;
-                        if (d == 0) {
-                            dc[e] = 3; df1[e] = f; df2[e] = f2; dg1[e] = l + 1; dg2[e] = f2 + 1;   // (k == 3)
-                            continue;
-                        }
-                        const int sh = d > 0 ? d : -d;
-                        // the first two and the last two mismatches (read index; the last ones + 1) by scans
-                        // from either end that stop once every lane has found two (random sequence: within a
-                        // word); the count up to 3 follows (3 when the second-last lies past the second)
-                        int a1 = La, a2 = La, b1 = 0, b2 = 0;
-                        auto word = [&](int t) -> unsigned {
-                            // d > 0: read base j = i + d against amplicon base i (words of i); d < 0: read
-                            // base j against amplicon base j - d (words of j)
-                            const unsigned am = d > 0 ? amp2s[t]
-                                                      : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
-                            const unsigned rd = d > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
-                            const unsigned z = rd ^ am;
-                            return (z | (z >> 1)) & vmask(t, La - sh);
-                        };
-#pragma unroll
-                        for (int t = 0; t < 16; ++t) {
-                            // (|d| >= 4: the score test needs one mismatch, no pair test reads the diagonal)
-                            if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
-                            const unsigned mk = word(t);
-                            const int off = 16 * t + (d > 0 ? d : 0);   // read index of the word's base 0
-                            if (mk != 0u && a1 == La) {
-                                a1 = off + (__builtin_ctz(mk) >> 1);
-                                const unsigned m2 = mk & (mk - 1u);
-                                if (m2 != 0u) a2 = off + (__builtin_ctz(m2) >> 1);
-                            } else if (mk != 0u && a2 == La) {
-                                a2 = off + (__builtin_ctz(mk) >> 1);
-                            }
-                        }
-#pragma unroll
-                        for (int t = 15; t >= 0; --t) {
-                            if (__ballot(s3 && b2 == 0 && a1 < La) == 0ull) break;
-                            if (t >= nw) continue;
-                            const unsigned mk = word(t);
-                            const int off = 16 * t + (d > 0 ? d : 0);
-                            if (mk != 0u && b1 == 0) {
-                                const int hb = 31 - __builtin_clz(mk);
-                                b1 = off + (hb >> 1) + 1;
-                                const unsigned mh = mk & ~(1u << hb);
-                                if (mh != 0u) b2 = off + ((31 - __builtin_clz(mh)) >> 1) + 1;
-                            } else if (mk != 0u && b2 == 0) {
-                                b2 = off + ((31 - __builtin_clz(mk)) >> 1) + 1;
-                            }
-                        }
-                        const int cc = a1 == La ? 0 : (a2 == La ? 1 : (b2 > a2 ? 3 : 2));
-                        dc[e] = min(cc, 3); df1[e] = a1; df2[e] = a2; dg1[e] = b1; dg2[e] = b2;
-                    }
-                    bool ok3 = s3;
-                    // (i) single diagonals
-#pragma unroll
-                    for (int e = 0; e < 11; ++e) {
-                        const int sh = e > 5 ? e - 5 : 5 - e;
-                        if (sh == 0) continue;
-                        ok3 = ok3 && m3 * sh + (m3 + x3) * dc[e] > D3;
-                    }
-                    // (ii) one gap, prefix on d1, suffix on d2 (|d| <= 3)
-#pragma unroll
-                    for (int e1 = 2; e1 <= 8; ++e1) {
-#pragma unroll
-                        for (int e2 = 2; e2 <= 8; ++e2) {
-                            if (e1 == e2) continue;
-                            const int d1 = e1 - 5, d2 = e2 - 5, g = d2 > d1 ? d2 - d1 : d1 - d2;
-                            // unpaired residues of the amplicon (= of the read): its leading / trailing overhang
-                            // and the gap's residues when the gap is in the read (the diagonal falls)
-                            const int U = (d1 < 0 ? -d1 : 0) + (d2 > 0 ? d2 : 0) + (d1 > d2 ? d1 - d2 : 0);
-                            const int slack = D3 - m3 * U - O3 - (g - 1) * a.gap_extend;   // (m + x) w must not exceed it
-                            if (slack < 0) continue;
-                            const int wmax = slack / (m3 + x3);
-                            const int gb = d2 > d1 ? d2 - d1 : 0;   // read bases in the gap
-                            bool exists = dg1[e2] - gb <= df1[e1];
-                            if (wmax >= 1) exists = exists || dg2[e2] - gb <= df1[e1] || dg1[e2] - gb <= df2[e1];
-                            if (wmax >= 2) exists = true;   // (not reached with the gate's parameters: reject)
-                            ok3 = ok3 && !exists;
-                        }
-                    }
-                    // (iii) jogs through d = +-1: a mismatch of that diagonal in [f + 1, l - 1] (read index)
-                    ok3 = ok3 && l - f >= 2 && jog_in[0] && jog_in[1];
-                    sub3 = __ballot(ok3);
-                }
+                pend3 = __ballot(s3);   // checked by nw_band_cert
                 if (a.known2) {   // a copy of the known sequence that no certificate above took
                     int k2 = 0;
 #pragma unroll
@@ -601,13 +798,14 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
                         const unsigned x = rw[t] ^ s_known[t];
                         k2 += __builtin_popcount((x | (x >> 1)) & vmask(t, La));
                     }
-                    known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2 | sub3);
+                    known = __ballot(c && k != 0 && k2 == 0) & ~(sub1 | sub2);
+                    pend3 &= ~known;   // (a known copy takes its record from the known alignment)
                     // A read of the amplicon's length closer to the known sequence (the other pass's amplicon)
                     // than to this one: a variant of it carries the amplicons' difference -- C3's 10-base HDR
                     // block, two 10-base gaps against this amplicon, more than 16 diagonals hold.  It skips
                     // the first band level (its sort key marks it; nw_band_fill<16> leaves its pair inactive,
                     // the walk hands it to the 32-diagonal level) instead of failing there first.
-                    jog = __ballot(c && k2 < k && k > 3) & ~(sub1 | sub2 | sub3 | known);
+                    jog = __ballot(c && k2 < k && k > 3) & ~(sub1 | sub2 | known);
                 }
             }
         }
@@ -758,113 +956,19 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // Runs M q, gap k, M Ls - q; identities Ls, gaps k, length Ll.  Reads of C2's deletion and
         // insertion classes (~15 % of the reads) need no DP: the traceback fill and the wide level lose
         // their bulk (tests/test_gpu_indel.py: homopolymer and tandem-repeat indels against the oracle).
-        unsigned long long indel1 = 0ull;
-        int ind_q = 0, ind_k = 0;
+        // The checks (cert_indel) run in nw_band_cert, on the queued candidates.
         if constexpr (PK) {
             const int dl = my_len - La, kab = dl < 0 ? -dl : dl;
             const bool ci = indel_kmax > 0 && a.ops && one_chunk && amp_acgt_all && r < r_end && !exc && kab >= 1 &&
                             kab <= indel_kmax;
-            if (__ballot(ci)) {
-                const bool del = dl < 0;
-                const int Ls = del ? my_len : La, Ll = del ? La : my_len;
-                unsigned rw[18];
-                {
-                    const long long q0 = my_off - a.pk_pos0;
-                    const unsigned* src = a.pk_words + (q0 >> 4);
-                    const unsigned s2 = (unsigned)(2 * (q0 & 15));
-                    const int nrw = (my_len + 15) >> 4;
-                    unsigned wd[18];
-#pragma unroll
-                    for (int t = 0; t < 18; ++t) wd[t] = ci && t <= nrw ? src[t] : 0u;
-#pragma unroll
-                    for (int t = 0; t < 17; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
-                    rw[17] = 0u;
-                }
-                auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
-                    const int b = len - 16 * t;
-                    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
-                };
-                const int mm = a.band_maxsub, xx = 4 * sc5;
-                const int S = mm * Ls - a.gap_open - (kab - 1) * a.gap_extend;
-                bool ok = false;
-                int gk = 0;
-                // the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
-                // registers, picked per lane (deletion and insertion reads in one pass over the shifts)
-                if (ci) {
-                    auto am = [&](int t) -> unsigned { return t < n2 ? amp2s[t] : 0u; };
-                    auto wl = [&](int t) -> unsigned { return del ? am(t) : rw[t]; };
-                    auto ws = [&](int t) -> unsigned { return del ? rw[t] : am(t); };
-                    bool o = true;
-                    // first and last mismatch of a shift (one side's sequence shifted by sh against the
-                    // other's, P positions): scans from either end that stop as soon as every lane has found
-                    // one (random sequence mismatches within a word; only the two diagonals of the
-                    // candidate run to the gap).  Mismatches: 0 (f == P), 1 (f == g - 1) or >= 2 -- all the
-                    // score test needs (its bound falls with the count)
-                    auto ends = [&](auto lw, auto rw2, int sh, int P, int* f, int* g) {
-                        int ff = P, gg = 0;
-#pragma unroll
-                        for (int t = 0; t < 17; ++t) {
-                            if (__ballot(ff == P && 16 * t < P) == 0ull) break;
-                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
-                            ff = (ff == P && mk != 0u) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : ff;
-                        }
-#pragma unroll
-                        for (int t = 16; t >= 0; --t) {
-                            if (__ballot(gg == 0 && ff < P) == 0ull) break;   // (words past P: mk == 0)
-                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-                            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
-                            gg = (gg == 0 && mk != 0u) ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : gg;
-                        }
-                        *f = ff;
-                        *g = gg;
-                    };
-                    auto cnt = [](int f, int g, int P) { return f == P ? 0 : (f == g - 1 ? 1 : 2); };
-                    // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
-                    // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
-                    // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
-                    // the shifts past kab and the other side's need only enough mismatches for the score test
-                    // (the smallest c with m (P - c) - x c < S, 0 .. 2; more: the DP): forward scans that stop
-                    // once that many are found
-                    auto enough = [&](auto lw, auto rw2, int sh, int P) -> bool {
-                        int need = 0;
-                        while (need <= 2 && !(mm * (P - need) - xx * need < S)) ++need;
-                        int c = 0;
-#pragma unroll
-                        for (int t = 0; t < 17; ++t) {
-                            if (__ballot(c < need && need <= 2 && 16 * t < P) == 0ull) break;
-                            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-                            c += c < need ? __builtin_popcount((z | (z >> 1)) & vmask(t, P)) : 0;
-                        }
-                        return need <= 2 && c >= need;
-                    };
-                    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
-                    for (int sh = 0; sh <= kab; ++sh) {
-                        int f, g;
-                        ends(wl, ws, sh, Ls, &f, &g);
-                        const int c = cnt(f, g, Ls);
-                        o = o && mm * (Ls - c) - xx * c < S;
-                        if (sh == 0) f0 = f;
-                        if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
-                        if (sh == kab) gk = g;
-                        fmax_all = max(fmax_all, f);
-                        if (sh > 0) fmax_1 = max(fmax_1, f);
-                    }
-                    for (int sh = kab + 1; sh <= kab + 3; ++sh) o = o && enough(wl, ws, sh, Ll - sh);
-                    for (int sh = 1; sh <= 3; ++sh) o = o && enough(ws, wl, sh, Ls - sh);   // s shifted against l
-                    ok = ci && o && gk >= 1 && gk <= f0;
-                }
-                indel1 = __ballot(ok);
-                ind_q = gk;
-                ind_k = kab;
-            }
+            pend_i = __ballot(ci);   // checked by nw_band_cert
         }
         // window reads (above): an exact window at the largest offset, else one substitution
         unsigned long long win = 0ull;
         int win_s = 0, win_k = 0;
         if constexpr (PK) {
             if (win_ok) {
-                bool cand_w = r < r_end && !exc && my_len >= 32 && my_len < La && !((indel1 >> lane) & 1ull);
+                bool cand_w = r < r_end && !exc && my_len >= 32 && my_len < La && !((pend_i >> lane) & 1ull);
                 int best1 = -1;   // -2: an exact window at win_s; >= 0: an offset with one mismatch
                 if (cand_w) {
                     // a window at s has the read's first 16 bases at s or its last 16 at s + Lb - 16 (one
@@ -948,7 +1052,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         int32_t sinfo = 0, sinfo2 = 0;
         if constexpr (PK) {
             if (win_ok && a.seed_info && r < r_end && !exc && my_len >= 32 && La - my_len >= 16 &&
-                !(((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull)) {
+                !(((exact | sub1 | sub2 | win | known) >> lane) & 1ull)) {
                 int dmin = 1 << 20, dmax = -(1 << 20);
                 bool ok = true;
                 const int nb = my_len >> 4;
@@ -1015,7 +1119,7 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             if (a.seed_info2 && r < r_end) a.seed_info2[r] = sinfo2;
         }
         if (r < r_end)
-            a.sort_key[r] = (((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull)
+            a.sort_key[r] = (((exact | sub1 | sub2 | win | known) >> lane) & 1ull)
                                 ? a.band_lb_cap + 2
                                 : (sinfo ? a.band_lb_cap + 3 +
                                                min(a.seed_keys - 1, max(0, ((seed_dmin(sinfo) + seed_dmax(sinfo)) / 2 + La) >> 2))
@@ -1032,27 +1136,14 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             st[0] = make_int4(La, my_len - win_k, my_len - win_k, La - my_len);   // aln_len, n_ident, n_sim, n_gaps
             st[1] = make_int4(a.band_maxsub * (my_len - win_k) - win_k * 4 * sc5, win_s + my_len, my_len, 0);
         }
-        if (a.ops && r < r_end && ((indel1 >> lane) & 1ull)) {
-            // runs: M q, the gap (X: residues of the read, Y: of the amplicon), M the rest of the shorter
-            const bool del = my_len < La;
-            const int Ls = del ? my_len : La;
-            const long long sst = a.ops_stride;
-            a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)ind_q;
-            a.ops[sst + r] = ((unsigned)(del ? RUN_Y : RUN_X) << 28) | (unsigned)ind_k;
-            a.ops[2 * sst + r] = ((unsigned)RUN_M << 28) | (unsigned)(Ls - ind_q);
-            a.nops[r] = 3;
-            int4* st = (int4*)(a.stats + r);
-            st[0] = make_int4(Ls + ind_k, Ls, Ls, ind_k);   // aln_len, n_ident, n_sim, n_gaps
-            st[1] = make_int4(a.band_maxsub * Ls - a.gap_open - (ind_k - 1) * a.gap_extend, La, my_len, 0);
-        }
         // a known copy: record and runs from the known alignment, by the compaction
         if (a.ops && r < r_end && ((known >> lane) & 1ull)) a.nops[r] = kNopsKnown;
         // ops output: every exact copy of the wave's 64 reads at once, lane u its own read's
         // record (2 x 16 B), its one M run of La columns (run 0 of its slot) and run count --
         // coalesced stores instead of three partial-line stores per copy
-        if (a.ops && r < r_end && (((exact | sub1 | sub2 | sub3) >> lane) & 1ull)) {
-            // substitutions (0 .. 3; a mismatch scores -4 / 5 maxsub)
-            const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull) + 3 * (int)((sub3 >> lane) & 1ull);
+        if (a.ops && r < r_end && (((exact | sub1 | sub2) >> lane) & 1ull)) {
+            // substitutions (0 .. 2; three: nw_band_cert; a mismatch scores -4 / 5 maxsub)
+            const int k = (int)((sub1 >> lane) & 1ull) + 2 * (int)((sub2 >> lane) & 1ull);
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
             a.nops[r] = 1;
             int4* st = (int4*)(a.stats + r);
@@ -1086,49 +1177,19 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
         // packed input: the bytes of every read that needs the DP (the only reads a later kernel
         // reads), exactly its own bytes (neighbouring reads' bytes are never written by another
         // read's wave: no races between blocks); exception bytes follow (below)
+        if constexpr (PK)
+            write_read_bytes(a, __ballot(r < r_end && my_len > 0 &&
+                                         !(((exact | sub1 | sub2 | win | known | pend3 | pend_i) >> lane) & 1ull)),
+                             my_off, my_len);
+        // deferred certificates (KernelArgs::cert_q): the wavefront's queued reads for nw_band_cert, the
+        // three-substitution candidates from the front of its 64 entries, the one-indel ones from the back
         if constexpr (PK) {
-            // kWr reads at a time, lane l their dwords l, l + 64, ...: all their loads in flight
-            // before any store (one read per round trip measured 2.7x the byte-input classify)
-            constexpr int kWr = 8;
-            unsigned long long dp =
-                __ballot(r < r_end && my_len > 0 && !(((exact | sub1 | sub2 | sub3 | win | known | indel1) >> lane) & 1ull));
-            uint8_t* dst = const_cast<uint8_t*>(a.reads);
-            while (dp) {
-                long long o[kWr], e[kWr];
-                int rounds = 0;
-#pragma unroll
-                for (int t = 0; t < kWr; ++t) {
-                    o[t] = e[t] = 0;
-                    if (dp) {
-                        const int u = (int)__builtin_ctzll(dp);
-                        dp &= dp - 1;
-                        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)my_off, u);
-                        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(my_off >> 32), u);
-                        o[t] = (long long)(((unsigned long long)hi << 32) | lo);
-                        e[t] = o[t] + __builtin_amdgcn_readlane(my_len, u);
-                        const int span = (int)(e[t] - (o[t] & ~3ll));
-                        rounds = max(rounds, (span + 255) >> 8);
-                    }
-                }
-                for (int rd2 = 0; rd2 < rounds; ++rd2) {
-                    unsigned v[kWr];
-#pragma unroll
-                    for (int t = 0; t < kWr; ++t) {
-                        const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
-                        v[t] = p < e[t] ? pk_decode4_al(a, p) : 0u;
-                    }
-#pragma unroll
-                    for (int t = 0; t < kWr; ++t) {
-                        const long long p = (o[t] & ~3ll) + 256 * rd2 + 4 * lane;
-                        if (p >= e[t]) continue;
-                        if (p >= o[t] && p + 4 <= e[t]) {
-                            *(unsigned*)(dst + p) = v[t];
-                        } else {
-                            for (int b = 0; b < 4; ++b)
-                                if (p + b >= o[t] && p + b < e[t]) dst[p + b] = (uint8_t)(v[t] >> (8 * b));
-                        }
-                    }
-                }
+            if (a.cert_q) {
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                const long long slot = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+                if ((pend3 >> lane) & 1ull) a.cert_q[slot * 64 + __builtin_popcountll(pend3 & lt)] = (int32_t)r;
+                if ((pend_i >> lane) & 1ull) a.cert_q[slot * 64 + 63 - __builtin_popcountll(pend_i & lt)] = (int32_t)r;
+                if (lane == 0) a.cert_cnt[slot] = (int32_t)(__builtin_popcountll(pend3) | (__builtin_popcountll(pend_i) << 8));
             }
         }
     };
@@ -1214,6 +1275,8 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             const long long my_off = r < bh ? s_off[r - bl] : 0;
             const int my_len = r < bh ? (int)(s_off[r - bl + 1] - my_off) : -1;
             batch(r0, bh, my_off, my_len, r < bh && s_exc[r - bl] != 0);
+        } else if (a.cert_q && lane == 0) {
+            a.cert_cnt[(long long)blockIdx.x * 4 + wave] = 0;   // (every wavefront's queue count is written)
         }
         if (any_exc && x1 > x0) {
             // after every wave's byte stores (completed: workgroup-scope release), the exception bytes
@@ -1222,6 +1285,99 @@ __global__ __launch_bounds__(256) void nw_band_classify(const KernelArgs a) {
             uint8_t* dst = const_cast<uint8_t*>(a.reads);
             for (long long t = x0 + tid; t < x1; t += blockDim.x) dst[a.pk_exc_pos[t]] = a.pk_exc_byte[t];
         }
+    }
+}
+
+// ============================================================================
+// Deferred certificates (KernelArgs::cert_q), between classify and the sort.  In classify each
+// wavefront runs a check for all its 64 lanes when any lane needs it: the three-substitution and
+// one-indel checks cost ~70 us of a 1M-read C2 pass there, for the ~20 % of reads that take them.
+// Classify queues those reads instead (per wavefront: three-substitution candidates from the front of
+// its 64 entries, one-indel candidates from the back, the two counts in cert_cnt) with the DP's sort
+// key and no bytes; here one block gathers the queues of kCertSlots classify wavefronts into two dense
+// lists in LDS and its wavefronts run the same checks (cert_sub3, cert_indel) 64 reads at a time.  A
+// certified read gets its record, runs and the finished key; the others get their bytes for the DP.
+// ============================================================================
+constexpr int kCertSlots = 16;   // classify wavefronts per block (4 classify blocks)
+
+__global__ __launch_bounds__(256) void nw_band_cert(const KernelArgs a, int nslots) {
+    extern __shared__ unsigned c_amp2[];   // the amplicon's 2-bit words (classify's image from 2 nd)
+    __shared__ int s_n3[kCertSlots], s_ni[kCertSlots], s_o3[kCertSlots + 1], s_oi[kCertSlots + 1];
+    __shared__ int s_l3[kCertSlots * 64], s_li[kCertSlots * 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long slot0 = (long long)blockIdx.x * kCertSlots;
+    const int ns = (int)min<long long>(kCertSlots, nslots - slot0);
+    if (tid < kCertSlots) {
+        const int v = tid < ns ? a.cert_cnt[slot0 + tid] : 0;
+        s_n3[tid] = v & 0xff;
+        s_ni[tid] = v >> 8;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int x = 0, y = 0;
+        for (int i = 0; i < kCertSlots; ++i) {
+            s_o3[i] = x;
+            s_oi[i] = y;
+            x += s_n3[i];
+            y += s_ni[i];
+        }
+        s_o3[kCertSlots] = x;
+        s_oi[kCertSlots] = y;
+    }
+    __syncthreads();
+    const int n3 = s_o3[kCertSlots], ni = s_oi[kCertSlots];
+    if (n3 + ni == 0) return;   // (block-uniform)
+    const int La = a.La, nd = (La + 3) / 4, n2 = (La + 15) / 16 + 2;
+    for (int k = tid; k < n2; k += 256) c_amp2[k] = a.cls_img[2 * nd + k];
+    for (int p = tid; p < ns * 64; p += 256) {
+        const int sl = p >> 6, j = p & 63;
+        if (j < s_n3[sl]) s_l3[s_o3[sl] + j] = a.cert_q[(slot0 + sl) * 64 + j];
+        else if (j >= 64 - s_ni[sl]) s_li[s_oi[sl] + 63 - j] = a.cert_q[(slot0 + sl) * 64 + j];
+    }
+    __syncthreads();
+    const int sc5 = a.band_maxsub / 5;
+    const long long sst = a.ops_stride;
+    // three substitutions: reads of the amplicon's length, three mismatches on the main diagonal
+    for (int b = 64 * wave; b < n3; b += 256) {
+        const bool v = b + lane < n3;
+        const long long r = v ? s_l3[b + lane] : 0;
+        const long long my_off = v ? a.offsets[r] : a.pk_pos0;
+        unsigned rw[17];
+        load_read_words(a, v, my_off, rw);
+        int k, f, f2, l;
+        main_diag_mism(rw, c_amp2, La, &k, &f, &f2, &l);
+        const bool ok = cert_sub3(a, c_amp2, rw, v && k == 3, f, f2, l, my_off);
+        if (ok) {   // the diagonal with three substitutions (classify's record for them)
+            a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
+            a.nops[r] = 1;
+            int4* st = (int4*)(a.stats + r);
+            st[0] = make_int4(La, La - 3, La - 3, 0);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * (La - 3) - 3 * 4 * sc5, La, La, 0);   // score, end_i, end_j, flags
+            a.sort_key[r] = a.band_lb_cap + 2;
+        }
+        write_read_bytes(a, __ballot(v && !ok), my_off, La);
+    }
+    // one indel: reads of La -+ k bases
+    for (int b = 64 * wave; b < ni; b += 256) {
+        const bool v = b + lane < ni;
+        const long long r = v ? s_li[b + lane] : 0;
+        const long long my_off = v ? a.offsets[r] : a.pk_pos0;
+        const int my_len = v ? (int)(a.offsets[r + 1] - my_off) : La;
+        int gk = 0;
+        const bool ok = cert_indel(a, c_amp2, v, my_off, my_len, &gk);
+        if (ok) {   // runs M q, the gap (X: residues of the read, Y: of the amplicon), M the rest of the shorter
+            const bool del = my_len < La;
+            const int Ls = del ? my_len : La, kab = del ? La - my_len : my_len - La;
+            a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)gk;
+            a.ops[sst + r] = ((unsigned)(del ? RUN_Y : RUN_X) << 28) | (unsigned)kab;
+            a.ops[2 * sst + r] = ((unsigned)RUN_M << 28) | (unsigned)(Ls - gk);
+            a.nops[r] = 3;
+            int4* st = (int4*)(a.stats + r);
+            st[0] = make_int4(Ls + kab, Ls, Ls, kab);   // aln_len, n_ident, n_sim, n_gaps
+            st[1] = make_int4(a.band_maxsub * Ls - a.gap_open - (kab - 1) * a.gap_extend, La, my_len, 0);
+            a.sort_key[r] = a.band_lb_cap + 2;
+        }
+        write_read_bytes(a, __ballot(v && !ok), my_off, my_len);
     }
 }
 
@@ -2968,6 +3124,11 @@ hipError_t launch_band_sort(const KernelArgs& a, unsigned epoch, hipStream_t s) 
         const size_t lds = (size_t)(8 * ((a.La + 3) / 4)) +
                            (a.amp2 ? (size_t)(4 * ((a.La + 15) / 16 + 2) + 6 * a.n_seed + 16) : 0);
         hipLaunchKernelGGL(nw_band_classify<true>, dim3((unsigned)(g1 - g0 + 1)), dim3(256), lds, s, a);
+        if (a.cert_q) {   // its four wavefronts' queues per block
+            const int nslots = (int)(4 * (g1 - g0 + 1));
+            hipLaunchKernelGGL(nw_band_cert, dim3((unsigned)((nslots + kCertSlots - 1) / kCertSlots)), dim3(256),
+                               (size_t)(4 * ((a.La + 15) / 16 + 2)), s, a, nslots);
+        }
     } else {
         hipLaunchKernelGGL(nw_band_classify<false>, dim3(std::max(1, std::min(2048, (int)((a.n + 255) / 256)))),
                            dim3(256), (size_t)(8 * ((a.La + 3) / 4)), s, a);

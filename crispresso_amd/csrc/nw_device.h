@@ -135,6 +135,11 @@ struct KernelArgs {
     // to the wide level (clears it for a read it certified), and a compaction keeps those; 0: off
     int32_t seed_l2;
     uint8_t* seed_flags;
+    // deferred certificates (packed classify, ops output): each classify wavefront queues its reads
+    // that take the three-substitution or one-indel checks (64 entries per wavefront, its count in
+    // cert_cnt) and nw_band_cert runs those checks on dense lists; null: classify runs them itself
+    int32_t* cert_q;
+    int32_t* cert_cnt;
     const uint32_t* cls_img;       // classify's LDS image of the amplicon (nw_host.cpp cls_image)
     int32_t cls_words;
     int32_t amp_acgt;              // every amplicon byte A C G T (either case)

@@ -86,6 +86,7 @@ struct Scratch {
     DevBuf<int32_t> d_redo;            // reads the first band level could not certify
     DevBuf<uint8_t> d_redo_flags;      // per sorted position: handed to the second level
     DevBuf<int32_t> d_order, d_sort_key;
+    DevBuf<int32_t> d_cert_q, d_cert_cnt;   // classify's queues for nw_band_cert (KernelArgs::cert_q)
     DevBuf<unsigned long long> d_lb;   // look-back words of the single-pass scans (sort, redo list, ops)
     DevBuf<uint8_t> d_bregion;         // band regions (per read pair)
     DevBuf<uint32_t> d_slots, d_spill, d_staging;   // ops output: run slots, spill area, compaction output
@@ -93,6 +94,7 @@ struct Scratch {
     void release() {
         d_tb.release(); d_fallback.release(); d_fallback2.release(); d_fallback_count.release(); d_redo.release();
         d_redo_flags.release(); d_order.release(); d_sort_key.release(); d_lb.release();
+        d_cert_q.release(); d_cert_cnt.release();
         d_seed.release(); d_seed2.release(); d_seed_list.release(); d_seed_flags.release(); d_seed_list2.release();
         d_bregion.release(); d_slots.release(); d_spill.release(); d_staging.release(); d_nops.release();
         d_opsctl.release();
@@ -707,6 +709,9 @@ int configure(nw_ctx* c) {
             HIP_OR_FAIL(c, c->s->d_redo_flags.reserve((size_t)std::max<int64_t>(c->n, 1)));
             HIP_OR_FAIL(c, c->s->d_lb.reserve((size_t)nw::band_lookback_words(c->n)));
             HIP_OR_FAIL(c, c->s->d_sort_key.reserve((size_t)std::max<int64_t>(c->n, 1)));
+            // 64 entries per classify wavefront: 4 per block of 256 reads, ceil(n / 256) + 1 blocks
+            HIP_OR_FAIL(c, c->s->d_cert_q.reserve((size_t)std::max<int64_t>(c->n, 1) + 1024));
+            HIP_OR_FAIL(c, c->s->d_cert_cnt.reserve((size_t)std::max<int64_t>(c->n, 1) / 64 + 16));
             if (c->seed_on) {
                 HIP_OR_FAIL(c, c->s->d_seed.reserve((size_t)std::max<int64_t>(c->n, 1)));
                 HIP_OR_FAIL(c, c->s->d_seed2.reserve((size_t)std::max<int64_t>(c->n, 1)));
@@ -1104,6 +1109,12 @@ int launch_range(nw_ctx* c, int64_t base) {
         a.pk_gbase = c->pkc.pk_gbase;
         a.pk_call_lo = c->pkc.pk_call_lo;
         a.known2 = c->known_on ? c->kset[c->kcur].d_k2.p : nullptr;
+        // the three-substitution and one-indel checks on classify's queues (nw_band_cert; packed input,
+        // ops output: the only classify that has those certificates)
+        if (a.pk_words && a.ops) {
+            a.cert_q = c->s->d_cert_q.p;
+            a.cert_cnt = c->s->d_cert_cnt.p;
+        }
         a.zero_ctl64 = c->zero_ctl;
         a.zero_ctl64_n = nw::kOpsCtlAll;
         HIP_OR_FAIL(c, nw::launch_band_sort(a, next_epoch(c), c->cs));
