@@ -325,17 +325,14 @@ __device__ __forceinline__ void main_diag_mism(const unsigned (&rw)[17], const u
 
 // The three-substitution certificate's per-read checks (i)-(iii) (classify, below; lanes s3: reads of the
 // amplicon's length with three mismatches on the main diagonal, at bases f < f2 < l; the caller checked
-// sub3_ok).  Called by the whole wavefront.
+// sub3_ok).  Called by the whole wavefront; fact: the wavefront's LDS for the diagonals' mismatch places
+// (kSub3FactWords).  The diagonal loop stays rolled (its scans unrolled once: the kernel's code fits the
+// instruction cache), the facts the pair test (ii) needs go through LDS.
+constexpr int kSub3FactWords = 14 * 64;   // diagonals -3 .. 3: first two | last two mismatches, per lane
 __device__ __forceinline__ bool cert_sub3(const KernelArgs& a, const unsigned* amp2s, const unsigned (&rw)[17], bool s3,
-                                          int f, int f2, int l, long long my_off) {
-    const int La = a.La, nw = (La + 15) >> 4, sc5 = a.band_maxsub / 5;
+                                          int f, int f2, int l, long long my_off, unsigned* fact) {
+    const int La = a.La, nw = (La + 15) >> 4, sc5 = a.band_maxsub / 5, lane = threadIdx.x & 63;
     const int m3 = a.band_maxsub, x3 = 4 * sc5, O3 = a.gap_open, D3 = 3 * (m3 + x3);
-    auto vmask = [](int t, int len) { return vmask16(t, len); };
-    auto rword = [&](long long p) { return pk_word16(a, p); };
-    auto aword = [&](int p) { return amp_word16(amp2s, p); };
-    // per diagonal d = -5 .. 5: mismatches (capped at 3), the first two and the last two
-    // (read index; last ones + 1), over the diagonal's pairs
-    int dc[11], df1[11], df2[11], dg1[11], dg2[11];
     // jogs (iii): diagonals +-1 against the 16 read bases from f + 1 (up to l - 1), one
     // word each from the packed stream (random sequence mismatches there; a read whose
     // diagonals +-1 match all 16 is left to the DP)
@@ -343,79 +340,86 @@ __device__ __forceinline__ bool cert_sub3(const KernelArgs& a, const unsigned* a
     if (s3) {
         const int len = min(16, l - f - 1);
         const unsigned lm = len <= 0 ? 0u : (len >= 16 ? 0x55555555u : (0x55555555u >> (32 - 2 * len)));
-        const unsigned rd = rword(my_off + f + 1);
-        const unsigned zp = rd ^ aword(f), zm = rd ^ aword(f + 2);   // d = +1 / -1
+        const unsigned rd = pk_word16(a, my_off + f + 1);
+        const unsigned zp = rd ^ amp_word16(amp2s, f), zm = rd ^ amp_word16(amp2s, f + 2);   // d = +1 / -1
         jog_in[1] = ((zp | (zp >> 1)) & lm) != 0u;
         jog_in[0] = ((zm | (zm >> 1)) & lm) != 0u;
     }
-#pragma unroll
-    for (int e = 0; e < 11; ++e) {
-        const int d = e - 5;
-        if (d == 0) {
-            dc[e] = 3; df1[e] = f; df2[e] = f2; dg1[e] = l + 1; dg2[e] = f2 + 1;   // (k == 3)
-            continue;
-        }
-        const int sh = d > 0 ? d : -d;
-        // the first two and the last two mismatches (read index; the last ones + 1) by scans
-        // from either end that stop once every lane has found two (random sequence: within a
-        // word); the count up to 3 follows (3 when the second-last lies past the second)
-        int a1 = La, a2 = La, b1 = 0, b2 = 0;
-        auto word = [&](int t) -> unsigned {
-            // d > 0: read base j = i + d against amplicon base i (words of i); d < 0: read
-            // base j against amplicon base j - d (words of j)
-            const unsigned am = d > 0 ? amp2s[t]
-                                      : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
-            const unsigned rd = d > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
-            const unsigned z = rd ^ am;
-            return (z | (z >> 1)) & vmask(t, La - sh);
-        };
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            // (|d| >= 4: the score test needs one mismatch, no pair test reads the diagonal)
-            if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
-            const unsigned mk = word(t);
-            const int off = 16 * t + (d > 0 ? d : 0);   // read index of the word's base 0
-            if (mk != 0u && a1 == La) {
-                a1 = off + (__builtin_ctz(mk) >> 1);
-                const unsigned m2 = mk & (mk - 1u);
-                if (m2 != 0u) a2 = off + (__builtin_ctz(m2) >> 1);
-            } else if (mk != 0u && a2 == La) {
-                a2 = off + (__builtin_ctz(mk) >> 1);
-            }
-        }
-#pragma unroll
-        for (int t = 15; t >= 0; --t) {
-            if (__ballot(s3 && b2 == 0 && a1 < La) == 0ull) break;
-            if (t >= nw) continue;
-            const unsigned mk = word(t);
-            const int off = 16 * t + (d > 0 ? d : 0);
-            if (mk != 0u && b1 == 0) {
-                const int hb = 31 - __builtin_clz(mk);
-                b1 = off + (hb >> 1) + 1;
-                const unsigned mh = mk & ~(1u << hb);
-                if (mh != 0u) b2 = off + ((31 - __builtin_clz(mh)) >> 1) + 1;
-            } else if (mk != 0u && b2 == 0) {
-                b2 = off + ((31 - __builtin_clz(mk)) >> 1) + 1;
-            }
-        }
-        const int cc = a1 == La ? 0 : (a2 == La ? 1 : (b2 > a2 ? 3 : 2));
-        dc[e] = min(cc, 3); df1[e] = a1; df2[e] = a2; dg1[e] = b1; dg2[e] = b2;
-    }
     bool ok3 = s3;
-    // (i) single diagonals
+    // per diagonal d = -5 .. 5: mismatches (capped at 3), the first two and the last two (read index;
+    // last ones + 1) over the diagonal's pairs; (i) single diagonals 1 <= |d| <= 5 need more than
+    // (3 (m + x) - m |d|) / (m + x) mismatches each
+#pragma unroll 1
+    for (int d = -5; d <= 5; ++d) {
+        int a1 = f, a2 = f2, b1 = l + 1, b2 = f2 + 1;   // d = 0: the main diagonal's three (k == 3)
+        if (d != 0) {
+            const int sh = d > 0 ? d : -d;
+            a1 = La; a2 = La; b1 = 0; b2 = 0;
+            // the first two and the last two by scans from either end that stop once every lane has
+            // found two (random sequence: within a word); the count up to 3 follows (3 when the
+            // second-last lies past the second)
+            auto word = [&](int t) -> unsigned {
+                // d > 0: read base j = i + d against amplicon base i (words of i); d < 0: read
+                // base j against amplicon base j - d (words of j)
+                const unsigned am = d > 0 ? amp2s[t]
+                                          : __builtin_amdgcn_alignbit(amp2s[t + 1], amp2s[t], (unsigned)(2 * sh));
+                const unsigned rd = d > 0 ? __builtin_amdgcn_alignbit(rw[t + 1], rw[t], (unsigned)(2 * sh)) : rw[t];
+                const unsigned z = rd ^ am;
+                return (z | (z >> 1)) & vmask16(t, La - sh);
+            };
+            const int o0 = d > 0 ? d : 0;   // read index of a word's base 0, past 16 t
 #pragma unroll
-    for (int e = 0; e < 11; ++e) {
-        const int sh = e > 5 ? e - 5 : 5 - e;
-        if (sh == 0) continue;
-        ok3 = ok3 && m3 * sh + (m3 + x3) * dc[e] > D3;
+            for (int t = 0; t < 16; ++t) {
+                if (__ballot(s3 && a2 == La && t < nw) == 0ull) break;
+                const unsigned mk = word(t);
+                const int off = 16 * t + o0;
+                if (mk != 0u && a1 == La) {
+                    a1 = off + (__builtin_ctz(mk) >> 1);
+                    const unsigned m2 = mk & (mk - 1u);
+                    if (m2 != 0u) a2 = off + (__builtin_ctz(m2) >> 1);
+                } else if (mk != 0u && a2 == La) {
+                    a2 = off + (__builtin_ctz(mk) >> 1);
+                }
+            }
+#pragma unroll
+            for (int t = 15; t >= 0; --t) {
+                if (__ballot(s3 && b2 == 0 && a1 < La) == 0ull) break;
+                if (t >= nw) continue;
+                const unsigned mk = word(t);
+                const int off = 16 * t + o0;
+                if (mk != 0u && b1 == 0) {
+                    const int hb = 31 - __builtin_clz(mk);
+                    b1 = off + (hb >> 1) + 1;
+                    const unsigned mh = mk & ~(1u << hb);
+                    if (mh != 0u) b2 = off + ((31 - __builtin_clz(mh)) >> 1) + 1;
+                } else if (mk != 0u && b2 == 0) {
+                    b2 = off + ((31 - __builtin_clz(mk)) >> 1) + 1;
+                }
+            }
+            // (|d| >= 4: the score test needs one mismatch, no pair test reads the diagonal)
+            const int cc = a1 == La ? 0 : (a2 == La ? 1 : (b2 > a2 ? 3 : 2));
+            ok3 = ok3 && m3 * sh + (m3 + x3) * cc > D3;
+        }
+        if (d >= -3 && d <= 3) {
+            fact[(d + 3) * 128 + lane] = (unsigned)a1 | ((unsigned)a2 << 16);
+            fact[(d + 3) * 128 + 64 + lane] = (unsigned)b1 | ((unsigned)b2 << 16);
+        }
     }
-    // (ii) one gap, prefix on d1, suffix on d2 (|d| <= 3)
+    // (ii) one gap, prefix on d1, suffix on d2 (|d| <= 3), with at most w_max mismatches in all: it exists
+    // iff, in read coordinates, the prefix's mismatches on d1 end before the suffix's on d2 begin (the
+    // suffix starts max(0, d2 - d1) read bases later: those are the gap's)
+    unsigned fa[7], fb[7];
 #pragma unroll
-    for (int e1 = 2; e1 <= 8; ++e1) {
+    for (int e = 0; e < 7; ++e) {
+        fa[e] = fact[e * 128 + lane];
+        fb[e] = fact[e * 128 + 64 + lane];
+    }
 #pragma unroll
-        for (int e2 = 2; e2 <= 8; ++e2) {
+    for (int e1 = 0; e1 < 7; ++e1) {
+#pragma unroll
+        for (int e2 = 0; e2 < 7; ++e2) {
             if (e1 == e2) continue;
-            const int d1 = e1 - 5, d2 = e2 - 5, g = d2 > d1 ? d2 - d1 : d1 - d2;
+            const int d1 = e1 - 3, d2 = e2 - 3, g = d2 > d1 ? d2 - d1 : d1 - d2;
             // unpaired residues of the amplicon (= of the read): its leading / trailing overhang
             // and the gap's residues when the gap is in the read (the diagonal falls)
             const int U = (d1 < 0 ? -d1 : 0) + (d2 > 0 ? d2 : 0) + (d1 > d2 ? d1 - d2 : 0);
@@ -423,15 +427,16 @@ __device__ __forceinline__ bool cert_sub3(const KernelArgs& a, const unsigned* a
             if (slack < 0) continue;
             const int wmax = slack / (m3 + x3);
             const int gb = d2 > d1 ? d2 - d1 : 0;   // read bases in the gap
-            bool exists = dg1[e2] - gb <= df1[e1];
-            if (wmax >= 1) exists = exists || dg2[e2] - gb <= df1[e1] || dg1[e2] - gb <= df2[e1];
+            const int df1 = (int)(fa[e1] & 0xffffu), df2 = (int)(fa[e1] >> 16);
+            const int dg1 = (int)(fb[e2] & 0xffffu), dg2 = (int)(fb[e2] >> 16);
+            bool exists = dg1 - gb <= df1;
+            if (wmax >= 1) exists = exists || dg2 - gb <= df1 || dg1 - gb <= df2;
             if (wmax >= 2) exists = true;   // (not reached with the gate's parameters: reject)
             ok3 = ok3 && !exists;
         }
     }
     // (iii) jogs through d = +-1: a mismatch of that diagonal in [f + 1, l - 1] (read index)
-    ok3 = ok3 && l - f >= 2 && jog_in[0] && jog_in[1];
-    return ok3;
+    return ok3 && l - f >= 2 && jog_in[0] && jog_in[1];
 }
 
 // The one-indel certificate (classify, below; lanes ci: reads of La -+ kab bases, 1 <= kab <= the
@@ -1304,6 +1309,7 @@ __global__ __launch_bounds__(256) void nw_band_cert(const KernelArgs a, int nslo
     extern __shared__ unsigned c_amp2[];   // the amplicon's 2-bit words (classify's image from 2 nd)
     __shared__ int s_n3[kCertSlots], s_ni[kCertSlots], s_o3[kCertSlots + 1], s_oi[kCertSlots + 1];
     __shared__ int s_l3[kCertSlots * 64], s_li[kCertSlots * 64];
+    __shared__ unsigned s_fact[4][kSub3FactWords];   // cert_sub3's per-wavefront facts
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long slot0 = (long long)blockIdx.x * kCertSlots;
     const int ns = (int)min<long long>(kCertSlots, nslots - slot0);
@@ -1346,7 +1352,7 @@ __global__ __launch_bounds__(256) void nw_band_cert(const KernelArgs a, int nslo
         load_read_words(a, v, my_off, rw);
         int k, f, f2, l;
         main_diag_mism(rw, c_amp2, La, &k, &f, &f2, &l);
-        const bool ok = cert_sub3(a, c_amp2, rw, v && k == 3, f, f2, l, my_off);
+        const bool ok = cert_sub3(a, c_amp2, rw, v && k == 3, f, f2, l, my_off, s_fact[wave]);
         if (ok) {   // the diagonal with three substitutions (classify's record for them)
             a.ops[r] = ((unsigned)RUN_M << 28) | (unsigned)La;
             a.nops[r] = 1;
