@@ -961,12 +961,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW_CLASSIFY
         // Runs M q, gap k, M Ls - q; identities Ls, gaps k, length Ll.  Reads of C2's deletion and
         // insertion classes (~15 % of the reads) need no DP: the traceback fill and the wide level lose
         // their bulk (tests/test_gpu_indel.py: homopolymer and tandem-repeat indels against the oracle).
-        // The checks (cert_indel) run in nw_band_cert, on the queued candidates.
+        // The checks (cert_indel) run in nw_band_cert, on the queued candidates.  A shorter read may instead be
+        // a window of the amplicon (below; a read one certificate takes fails the other: a window scores m Lb,
+        // an alignment with an internal gap less): one whose first and last 16 bases are the amplicon's ends
+        // is queued at once, the others after the window check found none.
+        bool ci_win = false;   // (a candidate the window check sees first)
         if constexpr (PK) {
             const int dl = my_len - La, kab = dl < 0 ? -dl : dl;
             const bool ci = indel_kmax > 0 && a.ops && one_chunk && amp_acgt_all && r < r_end && !exc && kab >= 1 &&
                             kab <= indel_kmax;
-            pend_i = __ballot(ci);   // checked by nw_band_cert
+            if (ci && dl < 0 && my_len >= 16 && La >= 16)
+                ci_win = pk_word16(a, my_off) != amp2s[0] ||
+                         pk_word16(a, my_off + my_len - 16) != amp_word16(amp2s, La - 16);
+            pend_i = __ballot(ci && !ci_win);   // checked by nw_band_cert
         }
         // window reads (above): an exact window at the largest offset, else one substitution
         unsigned long long win = 0ull;
@@ -1048,6 +1055,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NW_CLASSIFY
                     lds_fence();   // every lane's reads of rbw before the next candidate's writes
                 }
             }
+            pend_i |= __ballot(ci_win && !((win >> lane) & 1ull));   // no window: the one-indel check
         }
         // Seeded band: a read the 16-diagonal band cannot hold (La - Lb >= 16, the
         // reference's own 151 bp reads on a 280 bp amplicon) and no window certificate took: the
