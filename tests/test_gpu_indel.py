@@ -169,3 +169,41 @@ def test_three_substitution_reads(gpu_aligner_factory, maker, seed):
     _, _, _, _, counts = run_every_read(gpu_aligner_factory, amp, reads)
     if maker == "random":   # most 3-substitution reads leave the DP
         assert counts["exact_copies"] > 2500, counts
+
+
+def clean_indel_reads(amp: str, n: int, seed: int) -> list:
+    """One deletion or one insertion of random bases, 1..10 residues, away from the ends."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    La = len(amp)
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(1, 11))
+        p = int(rng.integers(20, La - 30))
+        if rng.integers(0, 2):
+            out.append(amp[:p] + amp[p + k:])
+        else:
+            out.append(amp[:p] + "".join(rng.choice(list("ACGT"), k)) + amp[p:])
+    return out
+
+
+def test_cert_queue_layouts(gpu_aligner_factory):
+    """nw_band_cert's queues ("Where the two checks run"): classify wavefronts whose 64 reads are
+    all three-substitution candidates (the front of the wavefront's 64 entries full), all one-indel candidates
+    (the back full), both kinds alternating, none (exact copies), a run of 1024 mixed candidates (one cert
+    block's 16 wavefronts, both lists long) and a partial last wavefront -- every read against the oracle, in
+    the call and in a resident pass of the same batch."""
+    amp = synth.random_amplicon(250, 31)
+    s3 = sub_reads(amp, 64 * 3 + 512 + 37, 32)
+    ind = clean_indel_reads(amp, 64 * 3 + 512, 33)
+    reads = s3[:64] + ind[:64]
+    reads += [x for pair in zip(s3[64:96], ind[64:96]) for x in pair]   # alternating
+    reads += [amp] * 64
+    mixed = s3[192:704] + ind[192:704]
+    rng = np.random.Generator(np.random.PCG64(34))
+    reads += [mixed[i] for i in rng.permutation(len(mixed))]
+    reads += s3[704:]   # a partial last wavefront (37 reads)
+    a, pr, buf, off, counts = run_every_read(gpu_aligner_factory, amp, reads)
+    # most candidates leave the DP (sub_reads' clustered and neighbour-copying reads may not)
+    assert counts["exact_copies"] > 64 + 0.6 * (len(reads) - 64), counts
+    res = a.align_ops(None, pr.offsets, resident=True)
+    assert every_read(amp, buf, off, res, threads=8)["mismatches"] == 0
