@@ -446,95 +446,95 @@ __device__ __forceinline__ bool cert_indel(const KernelArgs& a, const unsigned* 
                                            int* gk_) {
     const int La = a.La, n2 = (La + 15) / 16 + 2, sc5 = a.band_maxsub / 5;
     const int dl = my_len - La, kab = dl < 0 ? -dl : dl;
-const bool del = dl < 0;
-const int Ls = del ? my_len : La, Ll = del ? La : my_len;
-unsigned rw[18];
-{
-    const long long q0 = my_off - a.pk_pos0;
-    const unsigned* src = a.pk_words + (q0 >> 4);
-    const unsigned s2 = (unsigned)(2 * (q0 & 15));
-    const int nrw = (my_len + 15) >> 4;
-    unsigned wd[18];
+    const bool del = dl < 0;
+    const int Ls = del ? my_len : La, Ll = del ? La : my_len;
+    unsigned rw[18];
+    {
+        const long long q0 = my_off - a.pk_pos0;
+        const unsigned* src = a.pk_words + (q0 >> 4);
+        const unsigned s2 = (unsigned)(2 * (q0 & 15));
+        const int nrw = (my_len + 15) >> 4;
+        unsigned wd[18];
 #pragma unroll
-    for (int t = 0; t < 18; ++t) wd[t] = ci && t <= nrw ? src[t] : 0u;
+        for (int t = 0; t < 18; ++t) wd[t] = ci && t <= nrw ? src[t] : 0u;
 #pragma unroll
-    for (int t = 0; t < 17; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
-    rw[17] = 0u;
-}
-auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
-    const int b = len - 16 * t;
-    return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
-};
-const int mm = a.band_maxsub, xx = 4 * sc5;
-const int S = mm * Ls - a.gap_open - (kab - 1) * a.gap_extend;
-bool ok = false;
-int gk = 0;
-// the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
-// registers, picked per lane (deletion and insertion reads in one pass over the shifts)
-if (ci) {
-    auto am = [&](int t) -> unsigned { return t < n2 ? amp2s[t] : 0u; };
-    auto wl = [&](int t) -> unsigned { return del ? am(t) : rw[t]; };
-    auto ws = [&](int t) -> unsigned { return del ? rw[t] : am(t); };
-    bool o = true;
-    // first and last mismatch of a shift (one side's sequence shifted by sh against the
-    // other's, P positions): scans from either end that stop as soon as every lane has found
-    // one (random sequence mismatches within a word; only the two diagonals of the
-    // candidate run to the gap).  Mismatches: 0 (f == P), 1 (f == g - 1) or >= 2 -- all the
-    // score test needs (its bound falls with the count)
-    auto ends = [&](auto lw, auto rw2, int sh, int P, int* f, int* g) {
-        int ff = P, gg = 0;
-#pragma unroll
-        for (int t = 0; t < 17; ++t) {
-            if (__ballot(ff == P && 16 * t < P) == 0ull) break;
-            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
-            ff = (ff == P && mk != 0u) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : ff;
-        }
-#pragma unroll
-        for (int t = 16; t >= 0; --t) {
-            if (__ballot(gg == 0 && ff < P) == 0ull) break;   // (words past P: mk == 0)
-            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-            const unsigned mk = (z | (z >> 1)) & vmask(t, P);
-            gg = (gg == 0 && mk != 0u) ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : gg;
-        }
-        *f = ff;
-        *g = gg;
-    };
-    auto cnt = [](int f, int g, int P) { return f == P ? 0 : (f == g - 1 ? 1 : 2); };
-    // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
-    // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
-    // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
-    // the shifts past kab and the other side's need only enough mismatches for the score test
-    // (the smallest c with m (P - c) - x c < S, 0 .. 2; more: the DP): forward scans that stop
-    // once that many are found
-    auto enough = [&](auto lw, auto rw2, int sh, int P) -> bool {
-        int need = 0;
-        while (need <= 2 && !(mm * (P - need) - xx * need < S)) ++need;
-        int c = 0;
-#pragma unroll
-        for (int t = 0; t < 17; ++t) {
-            if (__ballot(c < need && need <= 2 && 16 * t < P) == 0ull) break;
-            const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
-            c += c < need ? __builtin_popcount((z | (z >> 1)) & vmask(t, P)) : 0;
-        }
-        return need <= 2 && c >= need;
-    };
-    int f0 = Ls, fmax_all = -1, fmax_1 = -1;
-    for (int sh = 0; sh <= kab; ++sh) {
-        int f, g;
-        ends(wl, ws, sh, Ls, &f, &g);
-        const int c = cnt(f, g, Ls);
-        o = o && mm * (Ls - c) - xx * c < S;
-        if (sh == 0) f0 = f;
-        if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
-        if (sh == kab) gk = g;
-        fmax_all = max(fmax_all, f);
-        if (sh > 0) fmax_1 = max(fmax_1, f);
+        for (int t = 0; t < 17; ++t) rw[t] = __builtin_amdgcn_alignbit(wd[t + 1], wd[t], s2);
+        rw[17] = 0u;
     }
-    for (int sh = kab + 1; sh <= kab + 3; ++sh) o = o && enough(wl, ws, sh, Ll - sh);
-    for (int sh = 1; sh <= 3; ++sh) o = o && enough(ws, wl, sh, Ls - sh);   // s shifted against l
-    ok = ci && o && gk >= 1 && gk <= f0;
-}
+    auto vmask = [](int t, int len) -> unsigned {   // bases 16 t + i < len
+        const int b = len - 16 * t;
+        return b >= 16 ? 0x55555555u : (b <= 0 ? 0u : 0x55555555u >> (32 - 2 * b));
+    };
+    const int mm = a.band_maxsub, xx = 4 * sc5;
+    const int S = mm * Ls - a.gap_open - (kab - 1) * a.gap_extend;
+    bool ok = false;
+    int gk = 0;
+    // the longer sequence l and the shorter s: the amplicon's words from LDS, the read's from
+    // registers, picked per lane (deletion and insertion reads in one pass over the shifts)
+    if (ci) {
+        auto am = [&](int t) -> unsigned { return t < n2 ? amp2s[t] : 0u; };
+        auto wl = [&](int t) -> unsigned { return del ? am(t) : rw[t]; };
+        auto ws = [&](int t) -> unsigned { return del ? rw[t] : am(t); };
+        bool o = true;
+        // first and last mismatch of a shift (one side's sequence shifted by sh against the
+        // other's, P positions): scans from either end that stop as soon as every lane has found
+        // one (random sequence mismatches within a word; only the two diagonals of the
+        // candidate run to the gap).  Mismatches: 0 (f == P), 1 (f == g - 1) or >= 2 -- all the
+        // score test needs (its bound falls with the count)
+        auto ends = [&](auto lw, auto rw2, int sh, int P, int* f, int* g) {
+            int ff = P, gg = 0;
+#pragma unroll
+            for (int t = 0; t < 17; ++t) {
+                if (__ballot(ff == P && 16 * t < P) == 0ull) break;
+                const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+                ff = (ff == P && mk != 0u) ? 16 * t + (int)(__builtin_ctz(mk) >> 1) : ff;
+            }
+#pragma unroll
+            for (int t = 16; t >= 0; --t) {
+                if (__ballot(gg == 0 && ff < P) == 0ull) break;   // (words past P: mk == 0)
+                const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                const unsigned mk = (z | (z >> 1)) & vmask(t, P);
+                gg = (gg == 0 && mk != 0u) ? 16 * t + (int)((31 - __builtin_clz(mk)) >> 1) + 1 : gg;
+            }
+            *f = ff;
+            *g = gg;
+        };
+        auto cnt = [](int f, int g, int P) { return f == P ? 0 : (f == g - 1 ? 1 : 2); };
+        // shifts sh = 0 .. kab + 3 of l; for sh <= kab the pair test G[s2] > F[s1] (s1 < s2) as a
+        // running maximum of F: every earlier shift's for s2 < kab, shifts 1 .. kab - 1 for s2 =
+        // kab (the pair (0, kab) is the candidate).  F / G are indices of s, P = Ls there.
+        // the shifts past kab and the other side's need only enough mismatches for the score test
+        // (the smallest c with m (P - c) - x c < S, 0 .. 2; more: the DP): forward scans that stop
+        // once that many are found
+        auto enough = [&](auto lw, auto rw2, int sh, int P) -> bool {
+            int need = 0;
+            while (need <= 2 && !(mm * (P - need) - xx * need < S)) ++need;
+            int c = 0;
+#pragma unroll
+            for (int t = 0; t < 17; ++t) {
+                if (__ballot(c < need && need <= 2 && 16 * t < P) == 0ull) break;
+                const unsigned z = __builtin_amdgcn_alignbit(lw(t + 1), lw(t), (unsigned)(2 * sh)) ^ rw2(t);
+                c += c < need ? __builtin_popcount((z | (z >> 1)) & vmask(t, P)) : 0;
+            }
+            return need <= 2 && c >= need;
+        };
+        int f0 = Ls, fmax_all = -1, fmax_1 = -1;
+        for (int sh = 0; sh <= kab; ++sh) {
+            int f, g;
+            ends(wl, ws, sh, Ls, &f, &g);
+            const int c = cnt(f, g, Ls);
+            o = o && mm * (Ls - c) - xx * c < S;
+            if (sh == 0) f0 = f;
+            if (sh > 0) o = o && g > (sh == kab ? fmax_1 : fmax_all);
+            if (sh == kab) gk = g;
+            fmax_all = max(fmax_all, f);
+            if (sh > 0) fmax_1 = max(fmax_1, f);
+        }
+        for (int sh = kab + 1; sh <= kab + 3; ++sh) o = o && enough(wl, ws, sh, Ll - sh);
+        for (int sh = 1; sh <= 3; ++sh) o = o && enough(ws, wl, sh, Ls - sh);   // s shifted against l
+        ok = ci && o && gk >= 1 && gk <= f0;
+    }
     *gk_ = gk;
     return ok;
 }
