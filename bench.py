@@ -1144,6 +1144,7 @@ def main():
                                         f"{ccp['lib_sha1']}, matches the loaded one: {ccp['lib_matches_loaded']})")
                                        if ccp else None,
                 "kernel": "the timed pass's kernels over the 1M resident reads: nw_band_classify<true> + "
+                          "nw_band_cert (the three-substitution and one-indel checks on classify's queues) + "
                           "nw_band_segsort + nw_band_fill<16, true> + "
                           "nw_band_walk<16, true> (lane walk + stop summary) + redo compaction + nw_band_fill/walk<32> "
                           "+ nw_band_fill/walk<128> (wide level) + nw_align_kernel + nw_ops_compact, one launch each "
